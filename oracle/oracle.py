@@ -1,0 +1,225 @@
+"""ctypes binding of the CPU parity oracle (oracle/quadswarm_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg.  The product package never imports this module.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "liboracle.so")
+
+D = ctypes.c_double
+I = ctypes.c_int
+
+
+class OrParams(ctypes.Structure):
+    _fields_ = [
+        ("mass", D), ("inertia", D * 3),
+        ("thrust_max", D * 4), ("torque_max", D * 4), ("prop_cross", (D * 3) * 4), ("prop_ccw", D * 4),
+        ("motor_tau_up", D), ("motor_tau_down", D), ("motor_linearity", D),
+        ("arm", D), ("gravity", D), ("omega_max", D), ("vel_damp", D), ("damp_omega_quadratic", D),
+        ("dt", D), ("sim_steps", I), ("since_last_svd_limit", D),
+        ("room_lo", D * 3), ("room_hi", D * 3),
+        ("ou_mu", D), ("ou_theta", D), ("ou_sigma", D),
+        ("sense_noise", I),
+        ("pos_norm_std", D), ("pos_unif_range", D), ("vel_norm_std", D), ("vel_unif_range", D),
+        ("gyro_noise_density", D), ("quat_norm_std", D), ("quat_unif_range", D),
+        ("acc_static_std", D), ("acc_dyn_ratio", D),
+        ("num_agents", I), ("num_envs", I), ("ep_len", I), ("obs_repr", I), ("k_neighbors", I),
+        ("collision_threshold", D), ("collision_falloff_threshold", D), ("control_dt", D),
+        ("rew_pos", D), ("rew_effort", D), ("rew_crash", D), ("rew_orient", D), ("rew_spin", D),
+        ("rew_quadcol_bin", D), ("rew_quadcol_smooth_max", D),
+        ("use_downwash", I), ("apply_collision_force", I),
+        ("spawn_box", D), ("goal", D * 3),
+    ]
+
+
+class OrDrone(ctypes.Structure):
+    _fields_ = [
+        ("pos", D * 3), ("vel", D * 3), ("rot", D * 9), ("omega", D * 3), ("acc", D * 3),
+        ("thrust_rot_damp", D * 4), ("thrust_cmds_damp", D * 4), ("ou", D * 4),
+        ("since_last_svd", D),
+        ("on_floor", I), ("crashed_floor", I), ("crashed_wall", I), ("crashed_ceiling", I),
+        ("prev_wall", I), ("prev_ceiling", I),
+        ("goal", D * 3),
+    ]
+
+
+class OrEnv(ctypes.Structure):
+    _fields_ = [("tick", I), ("prev_pair_bits", ctypes.c_ubyte * (64 * 64)),
+                ("obs_pos", (D * 3) * 64), ("obs_vel", (D * 3) * 64)]
+
+
+class OrRng(ctypes.Structure):
+    _fields_ = [("mode", I), ("seed", ctypes.c_uint32), ("step", ctypes.c_uint64),
+                ("tape", ctypes.POINTER(D)), ("tape_n", ctypes.c_long), ("tape_pos", ctypes.c_long),
+                ("spawn", ctypes.POINTER(D)), ("spawn_n", ctypes.c_long), ("spawn_pos", ctypes.c_long),
+                ("overrun", I)]
+
+
+RNG_PHILOX, RNG_TAPE = 0, 1
+S_SENSOR, S_RESET_SENSOR = 3, 11
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        P = ctypes.POINTER
+        L.or_params_default.argtypes = [P(OrParams)]
+        L.or_dyn_substep.argtypes = [P(OrParams), P(OrDrone), P(D), P(D), P(OrRng), ctypes.c_uint32, I]
+        L.or_ou_noise.argtypes = [P(OrParams), P(D), P(OrRng), ctypes.c_uint32]
+        L.or_sensor_noise.argtypes = [P(OrParams), P(D), P(D), P(D), P(D), P(OrRng), ctypes.c_uint32,
+                                      ctypes.c_uint32, P(D), P(D), P(D), P(D)]
+        L.or_polar.argtypes = [P(D)]
+        L.or_collide_drones.argtypes = [P(D)] * 6 + [P(OrRng), ctypes.c_uint32, ctypes.c_uint32]
+        L.or_collide_wall.argtypes = [P(OrParams), P(OrDrone), P(OrRng), ctypes.c_uint32]
+        L.or_collide_ceiling.argtypes = [P(OrDrone), P(OrRng), ctypes.c_uint32]
+        L.or_obs_dim.argtypes = [P(OrParams)]
+        L.or_env_reset.argtypes = [P(OrParams), P(OrDrone), P(OrEnv), I, P(OrRng), P(D)]
+        L.or_env_step.argtypes = [P(OrParams), P(OrDrone), P(OrEnv), I, P(D), P(OrRng), P(D), P(D),
+                                  P(ctypes.c_ubyte), P(D)]
+        L.or_reset_all.argtypes = [P(OrParams), P(OrDrone), P(OrEnv), ctypes.c_uint32, ctypes.c_uint64, P(D)]
+        L.or_step_all.argtypes = [P(OrParams), P(OrDrone), P(OrEnv), P(D), ctypes.c_uint32, ctypes.c_uint64,
+                                  P(D), P(D), P(ctypes.c_ubyte), P(D), I]
+        L.or_neighbor_obs.argtypes = [P(OrParams), P(OrEnv), P(D), I]
+        L.or_philox4x32_10.argtypes = [P(ctypes.c_uint32), P(ctypes.c_uint32), P(ctypes.c_uint32)]
+        L.or_philox_normal.argtypes = [ctypes.c_uint32] * 3 + [ctypes.c_uint64, ctypes.c_uint32]
+        L.or_philox_normal.restype = D
+        L.or_philox_uniform.argtypes = [ctypes.c_uint32] * 3 + [ctypes.c_uint64, ctypes.c_uint32]
+        L.or_philox_uniform.restype = D
+        for nm, st in [("or_sizeof_params", OrParams), ("or_sizeof_drone", OrDrone),
+                       ("or_sizeof_env", OrEnv), ("or_sizeof_rng", OrRng)]:
+            got = getattr(L, nm)()
+            if got != ctypes.sizeof(st):
+                raise RuntimeError(f"oracle ABI mismatch {nm}: C {got} vs ctypes {ctypes.sizeof(st)}")
+        _lib = L
+    return _lib
+
+
+def dptr(a):
+    return a.ctypes.data_as(ctypes.POINTER(D))
+
+
+def default_params(**over):
+    p = OrParams()
+    lib().or_params_default(ctypes.byref(p))
+    for k, v in over.items():
+        setattr(p, k, v)
+    return p
+
+
+def params_from_golden(g, **over):
+    """Physical constants exactly as the reference derived them (tests/golden/params.npz)."""
+    p = default_params()
+    p.mass = float(g["mass"])
+    for i in range(3):
+        p.inertia[i] = float(g["inertia"][i])
+    for k in range(4):
+        p.thrust_max[k] = float(g["thrust_max"][k])
+        p.torque_max[k] = float(g["torque_max"][k])
+        p.prop_ccw[k] = float(g["prop_ccw"][k])
+        for c in range(3):
+            p.prop_cross[k][c] = float(g["prop_cross"][k][c])
+    p.arm = float(g["arm"])
+    p.motor_tau_up = float(g["motor_tau_up"])
+    p.motor_tau_down = float(g["motor_tau_down"])
+    p.collision_threshold = 2.0 * p.arm
+    p.collision_falloff_threshold = 4.0 * p.arm
+    for k, v in over.items():
+        setattr(p, k, v)
+    return p
+
+
+class TapeRng:
+    """Holds the numpy arrays alive for an OrRng in tape mode."""
+
+    def __init__(self, tape, spawn=None):
+        self.tape = np.ascontiguousarray(tape, dtype=np.float64)
+        self.spawn = np.ascontiguousarray(spawn if spawn is not None else np.zeros(1), dtype=np.float64)
+        self.r = OrRng()
+        self.r.mode = RNG_TAPE
+        self.r.tape = dptr(self.tape)
+        self.r.tape_n = len(tape)
+        self.r.spawn = dptr(self.spawn)
+        self.r.spawn_n = 0 if spawn is None else len(spawn)
+
+    @property
+    def ref(self):
+        return ctypes.byref(self.r)
+
+
+def philox_rng(seed, step):
+    r = OrRng()
+    r.mode = RNG_PHILOX
+    r.seed = seed
+    r.step = step
+    return r
+
+
+def drones_array(n):
+    return (OrDrone * n)()
+
+
+def envs_array(n):
+    return (OrEnv * n)()
+
+
+def set_drone(d, **kw):
+    for k, v in kw.items():
+        f = getattr(d, k)
+        if isinstance(f, ctypes.Array):
+            flat = np.ravel(np.asarray(v, dtype=np.float64))
+            for i, x in enumerate(flat):
+                f[i] = x
+        else:
+            setattr(d, k, type(f)(v) if not isinstance(f, (int, float)) else (int(v) if isinstance(f, int) else float(v)))
+
+
+def get_arr(field, shape=None):
+    a = np.ctypeslib.as_array(field).astype(np.float64).copy()
+    return a.reshape(shape) if shape else a
+
+
+class OracleEnv:
+    """Batched flavor-B env in Philox mode: the CPU baseline and the GPU parity checker."""
+
+    def __init__(self, params, seed=0):
+        self.p = params
+        self.E, self.N = params.num_envs, params.num_agents
+        self.obs_dim = lib().or_obs_dim(ctypes.byref(params))
+        self.drones = drones_array(self.E * self.N)
+        self.envs = envs_array(self.E)
+        self.seed = seed
+        self.ctr = 0
+
+    def reset(self):
+        obs = np.zeros((self.E * self.N, self.obs_dim))
+        lib().or_reset_all(ctypes.byref(self.p), self.drones, self.envs, self.seed, self.ctr, dptr(obs))
+        self.ctr += 1
+        return obs
+
+    def step(self, actions, nthreads=0):
+        a = np.ascontiguousarray(actions, dtype=np.float64).reshape(self.E * self.N, 4)
+        obs = np.zeros((self.E * self.N, self.obs_dim))
+        term = np.zeros_like(obs)
+        rew = np.zeros(self.E * self.N)
+        done = np.zeros(self.E * self.N, dtype=np.uint8)
+        lib().or_step_all(ctypes.byref(self.p), self.drones, self.envs, dptr(a), self.seed, self.ctr,
+                          dptr(obs), dptr(rew), done.ctypes.data_as(ctypes.POINTER(ctypes.c_ubyte)),
+                          dptr(term), nthreads)
+        self.ctr += 1
+        return obs, rew, done.astype(bool), term

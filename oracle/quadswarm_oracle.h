@@ -1,0 +1,144 @@
+/* quadswarm_oracle.h -- CPU restatement of the reference's flavor-B swarm env step.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This is the parity oracle (and the bench's cpu_baseline "port"
+ * leg).  The product path (HIP kernels behind include/quadswarm.h) never links or calls it.
+ *
+ * Every function cites the reference file:line it restates (paths relative to the reference
+ * root, priban42/quad-swarm-rl-stable-baselines3).  Arithmetic is float64, like the reference.
+ *
+ * Random draws come from an or_rng:
+ *   OR_RNG_PHILOX : counter-based Philox4x32-10, keyed exactly like the GPU kernel
+ *                   (key = {drone global id, seed}, counter = {block, stream, step_lo, step_hi}),
+ *                   so GPU fp32 and oracle fp64 consume identical underlying draws.
+ *   OR_RNG_TAPE   : replays values recorded from the reference's own np.random calls, in the
+ *                   reference's call order (tools/gen_golden.py), so the oracle can be pinned
+ *                   bit-for-bit against the reference on full noisy trajectories.
+ */
+#ifndef QUADSWARM_ORACLE_H
+#define QUADSWARM_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- Philox stream ids (shared numbering with the HIP kernel, csrc/qs_rng.h) ---- */
+enum {
+    OR_S_OU = 1,          /* OU thrust noise: 4 normals                      */
+    OR_S_FLOOR = 2,       /* floor flip yaw: 1 uniform; | substep << 8        */
+    OR_S_SENSOR = 3,      /* sensor noise: normals pos 0-2, vel 3-5, omega 6-8 */
+    OR_S_PAIR = 4,        /* drone-drone impulse, key = lower id; | j << 8    */
+    OR_S_WALL = 5,
+    OR_S_CEIL = 6,
+    OR_S_DW = 7,          /* downwash per-source scalars                     */
+    OR_S_DWPAIR = 8,      /* downwash per applied pair; | j << 8              */
+    OR_S_RESET = 9,       /* spawn uniforms 0-2                               */
+    OR_S_RESET_YAW = 10,  /* yaw rejection uniforms                           */
+    OR_S_RESET_SENSOR = 11,
+    OR_S_OBST = 12,
+    OR_UNIF_BIT = 0x80    /* uniform draws use stream | OR_UNIF_BIT           */
+};
+
+enum { OR_RNG_PHILOX = 0, OR_RNG_TAPE = 1 };
+
+typedef struct {
+    int mode;
+    uint32_t seed;
+    uint64_t step;          /* Philox counter words 2,3                       */
+    /* tape mode */
+    const double* tape;      /* np.random legacy draws (global stream)          */
+    long tape_n, tape_pos;
+    const double* spawn;     /* Generator draws used for spawn positions        */
+    long spawn_n, spawn_pos;
+    int overrun;             /* set when a tape ran dry                         */
+} or_rng;
+
+/* Physical + env parameters (host-derived, mirrors QuadrotorDynamics.update_model
+ * quadrotor_dynamics.py:106-168 and QuadrotorEnvMulti.__init__ quadrotor_multi.py:26-227). */
+typedef struct {
+    double mass, inertia[3];
+    double thrust_max[4], torque_max[4], prop_cross[4][3], prop_ccw[4];
+    double motor_tau_up, motor_tau_down, motor_linearity;
+    double arm, gravity, omega_max, vel_damp, damp_omega_quadratic;
+    double dt;                 /* 1/sim_freq = 0.005                                 */
+    int sim_steps;             /* physics substeps per control tick (2)              */
+    double since_last_svd_limit;
+    double room_lo[3], room_hi[3];
+    double ou_mu, ou_theta, ou_sigma;
+    int sense_noise;           /* 0 = bypass                                          */
+    double pos_norm_std, pos_unif_range, vel_norm_std, vel_unif_range;
+    double gyro_noise_density, quat_norm_std, quat_unif_range, acc_static_std, acc_dyn_ratio;
+    /* env */
+    int num_agents, num_envs, ep_len;
+    int obs_repr;              /* 0 xyz_vxyz_R_omega(18) 1 +floor(19) 2 +wall(24)     */
+    int k_neighbors;           /* visible neighbours (0 = none)                       */
+    double collision_threshold, collision_falloff_threshold, control_dt;
+    double rew_pos, rew_effort, rew_crash, rew_orient, rew_spin;
+    double rew_quadcol_bin, rew_quadcol_smooth_max;
+    int use_downwash, apply_collision_force;
+    double spawn_box;          /* QuadrotorSingle.box = 2.0                           */
+    double goal[3];            /* static_same_goal formation centre (0,0,2)            */
+} or_params;
+
+/* Per-drone state (QuadrotorDynamics attributes + QuadrotorSingle bookkeeping). */
+typedef struct {
+    double pos[3], vel[3], rot[9], omega[3], acc[3];
+    double thrust_rot_damp[4], thrust_cmds_damp[4];
+    double ou[4];
+    double since_last_svd;
+    int on_floor, crashed_floor, crashed_wall, crashed_ceiling;
+    int prev_wall, prev_ceiling;   /* quadrotor_multi.py:604-605 (stores the NEW lists)   */
+    double goal[3];
+} or_drone;
+
+typedef struct {
+    int tick;
+    unsigned char prev_pair_bits[64 * 64];  /* [i*64+j], i<j: pair collided at the previous step */
+    double obs_pos[64][3], obs_vel[64][3];  /* QuadrotorEnvMulti.pos / .vel (neighbour obs) */
+} or_env;
+
+/* ---- low level pieces (exported for per-function golden tests) ---- */
+void or_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+double or_philox_normal(uint32_t seed, uint32_t id, uint32_t stream, uint64_t step, uint32_t idx);
+double or_philox_uniform(uint32_t seed, uint32_t id, uint32_t stream, uint64_t step, uint32_t idx);
+
+void or_params_default(or_params* p);
+void or_dyn_substep(const or_params* p, or_drone* d, const double cmds[4], const double thr_noise[4],
+                    or_rng* r, uint32_t gid, int substep);
+void or_ou_noise(const or_params* p, double ou[4], or_rng* r, uint32_t gid);
+void or_sensor_noise(const or_params* p, const double pos[3], const double vel[3], const double rot[9],
+                     const double omega[3], or_rng* r, uint32_t gid, uint32_t stream,
+                     double npos[3], double nvel[3], double nrot[9], double nomega[3]);
+void or_polar(double rot[9]);
+void or_collide_drones(double pos1[3], double vel1[3], double omega1[3],
+                       double pos2[3], double vel2[3], double omega2[3],
+                       or_rng* r, uint32_t gid, uint32_t j);
+void or_collide_wall(const or_params* p, or_drone* d, or_rng* r, uint32_t gid);
+void or_collide_ceiling(or_drone* d, or_rng* r, uint32_t gid);
+
+/* ---- whole env (flavor B, QuadrotorEnvMulti quadrotor_multi.py) ---- */
+/* state arrays are num_envs*num_agents drones and num_envs envs. obs is [E*N, obs_dim]. */
+int or_obs_dim(const or_params* p);
+void or_env_reset(const or_params* p, or_drone* drones, or_env* envs, int env_idx, or_rng* r,
+                  double* obs /* rows of this env */);
+void or_env_step(const or_params* p, or_drone* drones, or_env* envs, int env_idx, const double* actions,
+                 or_rng* r, double* obs, double* rew, unsigned char* done, double* term_obs);
+/* batched helpers (Philox mode, OpenMP over envs) */
+void or_reset_all(const or_params* p, or_drone* drones, or_env* envs, uint32_t seed, uint64_t step,
+                  double* obs);
+void or_step_all(const or_params* p, or_drone* drones, or_env* envs, const double* actions,
+                 uint32_t seed, uint64_t step, double* obs, double* rew, unsigned char* done,
+                 double* term_obs, int nthreads);
+
+void or_neighbor_obs(const or_params* p, const or_env* ev, double* obs, int obs_dim);
+
+/* sizes for ctypes */
+int or_sizeof_params(void);
+int or_sizeof_drone(void);
+int or_sizeof_env(void);
+int or_sizeof_rng(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
