@@ -1,0 +1,224 @@
+#!/usr/bin/env python
+"""Benchmark: agent-steps/s of the fused HIP swarm step (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
+
+A "step" = one QuadrotorEnvMulti.step of every env on the GPU (qs_step: physics x2 substeps,
+collisions, proximity, impulses, neighbour top-k, sensor noise, obs, rewards, fused auto-reset),
+actions read from a fixed device buffer of U(-1,1) draws (seed 1234), state resident in HBM.
+Weak scaling: every rank owns its own 4096 envs x 8 drones (disjoint Philox key ranges), no
+collective on the data path; value = all ranks' agent-steps / max-over-ranks wall time.
+
+Besides the required fields the JSON line carries:
+  roofline      algorithmic bytes per launch / HIP-event kernel time vs 8 TB/s
+  cpu_baseline  the C oracle (oracle/, OpenMP over envs) on this host, bounded ~10 s sample
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "quad-swarm-rl-stable-baselines3_amd"))
+
+# BASELINE.json configs -> (envs per GPU, agents, visible neighbours, downwash)
+CONFIGS = {
+    "c2": dict(num_envs=16384, num_agents=1, neighbor_visible_num=0, neighbor_obs_type="none"),
+    "c3": dict(num_envs=4096, num_agents=8, neighbor_visible_num=6, neighbor_obs_type="pos_vel"),
+    "c5": dict(num_envs=1024, num_agents=32, neighbor_visible_num=6, neighbor_obs_type="pos_vel"),
+}
+WORKLOAD = {"c2": "single_quad x 16384 envs", "c3": "8-drone swarm static_same_goal x 4096 envs (pos_vel k=6)",
+            "c5": "32-drone swarm x 1024 envs per GPU (pos_vel k=6)"}
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
+
+
+def algorithmic_bytes_per_agent_step(obs_dim, n_agents):
+    """B = 4 (S_r + S_w + A + O + 1) + 1 with S_r = 33 persistent fp32 state
+    (pos3 vel3 rot9 omega3 cmd_damp4 rot_damp4 OU4 goal3), S_w = 30, A = 4, O = obs_dim, +1 reward,
+    +1 byte done.  C3: 489 B, C2: 345 B."""
+    return 4 * (33 + 30 + 4 + obs_dim + 1) + 1
+
+
+def cpu_baseline(cfg_kw, seconds=10.0):
+    """The C oracle (fp64, OpenMP over envs) on the same workload shape, time-bounded sample."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle as O
+    from parity_utils import oracle_params
+    from quadswarm_amd import QuadSwarmConfig
+
+    cores = len(os.sched_getaffinity(0))
+    cores = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
+    cfg = QuadSwarmConfig(**cfg_kw)
+    env = O.OracleEnv(oracle_params(cfg), seed=0)
+    env.reset()
+    a = np.random.default_rng(1234).uniform(-1.0, 1.0, (cfg.num_envs * cfg.num_agents, 4))
+    env.step(a, nthreads=cores)
+    steps, t0 = 0, time.perf_counter()
+    while True:
+        env.step(a, nthreads=cores)
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or steps >= 4000:
+            break
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": round(steps * cfg.num_envs * cfg.num_agents / el, 1), "unit": "agent-steps/s", "cores": cores,
+            "kind": "port",
+            "sample": f"{steps} steps x {cfg.num_envs} envs x {cfg.num_agents} drones, fp64 C oracle, "
+                      f"{cores} OpenMP threads, {el:.1f} s on '{model}'"}
+
+
+def pmc_traffic(config):
+    """HBM bytes per launch measured by rocprofv3 --pmc (profiles/pmc_<config>.json, written by
+    tools/profile_pmc.py from separate FETCH_SIZE / WRITE_SIZE passes with the gfx950 correction)."""
+    p = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        return json.load(open(p)).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--graph", type=int, default=100, help="steps per captured hipGraph (0 = eager launches)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from quadswarm_amd import QuadSwarmConfig
+    from quadswarm_amd.env import QuadSwarmEnv
+
+    kw = CONFIGS[args.config]
+    cfg = QuadSwarmConfig(**kw, seed=0)
+    I = cfg.num_envs * cfg.num_agents
+    cfg.drone_id_offset = rank * I
+    env = QuadSwarmEnv(cfg, device=dev)
+    gen = torch.Generator(device=dev).manual_seed(1234)
+    actions = (torch.rand(I, 4, device=dev, generator=gen) * 2.0 - 1.0).contiguous()
+    env.reset()
+
+    stream = torch.cuda.current_stream(dev)
+    graph = None
+    chunk = args.graph if args.graph > 0 else 0
+    if chunk:
+        # capture `chunk` steps into one hipGraph on a side stream (the RNG counter lives on the device)
+        for _ in range(3):
+            env.step(actions)
+        torch.cuda.synchronize(dev)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            for _ in range(chunk):
+                env.step(actions)
+        torch.cuda.synchronize(dev)
+
+    def run(n):
+        if graph is None:
+            for _ in range(n):
+                env.step(actions)
+            return n
+        done = 0
+        while done + chunk <= n:
+            graph.replay()
+            done += chunk
+        for _ in range(n - done):
+            env.step(actions)
+        return n
+
+    run(args.warmup)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    run(args.steps)
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+
+    # kernel duration with HIP events on the stream the kernel is launched on (eager launches,
+    # events around each launch, averaged)
+    nk = min(200, max(20, args.steps // 10))
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(nk)]
+    for s_ev, e_ev in evs:
+        s_ev.record(stream)
+        env.step(actions)
+        e_ev.record(stream)
+    torch.cuda.synchronize(dev)
+    k_ms = sum(s.elapsed_time(e) for s, e in evs) / nk
+
+    if rank == 0:
+        value = world * I * args.steps / el
+        bpa = algorithmic_bytes_per_agent_step(cfg.obs_dim, cfg.num_agents)
+        achieved = bpa * I / (k_ms * 1e-3) / 1e9
+        traffic = pmc_traffic(args.config)
+        out = {
+            "metric": "agent-steps/sec, 8-drone swarm x 4096 envs, at 1/2/4/8 MI355X" if args.config == "c3"
+            else f"agent-steps/sec, {WORKLOAD[args.config]}",
+            "value": round(value, 1),
+            "unit": "agent-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(el * 1e3 / args.steps, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: U(-1,1) actions (seed 1234) from a fixed device buffer; Crazyflie constants; "
+                    "static_same_goal spawns (Philox seed 0)",
+            "config": {"workload": WORKLOAD[args.config], "envs_per_gpu": cfg.num_envs,
+                       "agents_per_env": cfg.num_agents, "visible_neighbors": cfg.k_neighbors,
+                       "obs_dim": cfg.obs_dim, "global_batch": world * I, "parallelism": f"env-shard x{world}",
+                       "launch": f"hipGraph of {chunk} steps" if chunk else "eager"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic, "kernel": "qs::step_kernel<8>" if cfg.num_agents == 8 else "qs::step_kernel",
+                         "kernel_us": round(k_ms * 1e3, 3), "bytes_per_agent_step": bpa,
+                         "bytes_per_launch": bpa * I},
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                out["cpu_baseline"] = cpu_baseline(kw, seconds=args.cpu_seconds)
+            except Exception as e:  # never let the baseline leg kill the GPU number
+                out["cpu_baseline"] = {"error": repr(e)}
+        print(json.dumps(out), flush=True)
+    env.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,166 @@
+/* quadswarm.h -- C ABI of the MI355X-native quadrotor-swarm environment step (libquadswarm.so).
+ *
+ * Drop-in boundary for the reference's env-stepping path
+ * (priban42/quad-swarm-rl-stable-baselines3):
+ *   - qs_step   replaces QuadrotorEnvMulti.step        gym_art/quadrotor_multi/quadrotor_multi.py:521-841
+ *               as driven per env by SubprocVecEnvCustom  swarm_rl/env_wrappers/subproc_vec_env_custom.py:141-153
+ *               (worker loop :33-52: step, terminal_observation, auto-reset)
+ *   - qs_reset  replaces QuadrotorEnvMulti.reset       quadrotor_multi.py:440-517
+ *               (SubprocVecEnvCustom.reset :155-164)
+ *   - qs_set_param replaces rew_coeff updates          swarm_rl/env_wrappers/reward_shaping.py:70-76,110-118
+ *   - qs_get_state/qs_set_state: env snapshot/restore (no reference equivalent; checkpoint + parity)
+ * The Python mirror of the reference's VecEnv surface (quadswarm_amd.vec_env.GpuQuadVecEnv) calls
+ * these through ctypes; INTEGRATION.md shows the binding.
+ *
+ * Conventions: plain C types only; every call returns 0 on success or a negative QS_E* code and sets a
+ * thread-local message readable with qs_last_error().  HIP errors are surfaced, never aborted on.
+ * One handle = one HIP device; calls are asynchronous on the caller's stream (hipStream_t passed as
+ * void*; NULL = the default stream) and a handle is not re-entrant.
+ */
+#ifndef QUADSWARM_H
+#define QUADSWARM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QS_ABI_VERSION 1
+#define QS_MAX_AGENTS 32            /* drones per env: one env lives inside one 64-lane wavefront */
+
+enum qs_status {
+    QS_OK = 0,
+    QS_E_INVALID = -1,              /* bad argument / config                          */
+    QS_E_UNSUPPORTED = -2,          /* config outside what the kernels implement      */
+    QS_E_HIP = -3,                  /* HIP runtime error (message has the HIP string) */
+    QS_E_NOMEM = -4,
+};
+
+enum qs_obs_repr {                  /* quad_utils.py:30-38 (QUADS_OBS_REPR) */
+    QS_OBS_XYZ_VXYZ_R_OMEGA = 0,       /* 18 */
+    QS_OBS_XYZ_VXYZ_R_OMEGA_FLOOR = 1, /* 19 */
+    QS_OBS_XYZ_VXYZ_R_OMEGA_WALL = 2,  /* 24 */
+};
+
+enum qs_neighbor_obs {              /* quad_utils.py:40-58 (QUADS_NEIGHBOR_OBS_TYPE) */
+    QS_NEIGHBOR_NONE = 0,
+    QS_NEIGHBOR_POS_VEL = 1,           /* 6 per visible neighbour */
+};
+
+/* Environment + physical configuration.  Physical constants are derived on the host exactly like
+ * QuadrotorDynamics.update_model (quadrotor_dynamics.py:106-168); quadswarm_amd.params does it for
+ * Python callers, qs_config_default() fills the Crazyflie values for C callers. */
+typedef struct qs_config {
+    int32_t abi_version;            /* must be QS_ABI_VERSION */
+    int32_t num_envs;               /* E */
+    int32_t num_agents;             /* N, 1..QS_MAX_AGENTS */
+    int32_t obs_repr;               /* enum qs_obs_repr */
+    int32_t neighbor_obs;           /* enum qs_neighbor_obs */
+    int32_t k_neighbors;            /* visible neighbours (0..N-1); N-1 = all, no sorting */
+    int32_t ep_len;                 /* int(ep_time / (dt * sim_steps)); done when tick > ep_len */
+    int32_t sim_steps;              /* physics substeps per control tick (2) */
+    int32_t svd_every;              /* substeps between polar re-orthonormalisations (100) */
+    int32_t sense_noise;            /* 0: SensorNoise(bypass=True); 1: default noise */
+    int32_t use_downwash;
+    int32_t apply_collision_force;
+    uint32_t seed;
+    uint32_t drone_id_offset;       /* global id of drone 0 (RNG key): env shards on several GPUs draw
+                                       exactly what one big env would (DESIGN.md multi-GPU) */
+    float dt;                       /* 1 / sim_freq (0.005) */
+    float control_dt;               /* dt * sim_steps (0.01) */
+    /* rigid body */
+    float mass, inertia[3];
+    float thrust_max[4], torque_max[4], prop_cross[4][3], prop_ccw[4];
+    float motor_tau_up, motor_tau_down, motor_linearity;
+    float arm, gravity, omega_max, vel_damp, damp_omega_quadratic, vxyz_max;
+    float room_lo[3], room_hi[3];
+    /* noise */
+    float ou_mu, ou_theta, ou_sigma;
+    float pos_norm_std, pos_unif_range, vel_norm_std, vel_unif_range;
+    float gyro_noise_density, quat_norm_std, quat_unif_range;
+    /* rewards / collisions */
+    float collision_threshold, collision_falloff_threshold;
+    float rew_pos, rew_effort, rew_crash, rew_orient, rew_spin;
+    float rew_quadcol_bin, rew_quadcol_smooth_max;
+    /* static_same_goal scenario */
+    float spawn_box, goal[3];
+} qs_config;
+
+/* Device buffers of a handle.  State is structure-of-arrays: field f of drone g lives at
+ * state[f * I + g] with I = E * N (fp32), istate[f * I + g] (int32).  Observations are row-major
+ * [I, obs_dim] fp32 so a torch tensor can consume them zero-copy. */
+enum qs_state_field {
+    QS_F_POS = 0, QS_F_VEL = 3, QS_F_ROT = 6, QS_F_OMEGA = 15, QS_F_ROT_DAMP = 18, QS_F_CMD_DAMP = 22,
+    QS_F_OU = 26, QS_F_GOAL = 30, QS_NF = 33
+};
+enum qs_istate_field { QS_I_SVD = 0, QS_I_FLAGS = 1, QS_I_PREV_LO = 2, QS_I_PREV_HI = 3, QS_NI = 4 };
+enum qs_drone_flags {
+    QS_FL_ON_FLOOR = 1, QS_FL_PREV_WALL = 2, QS_FL_PREV_CEIL = 4,
+    QS_FL_CRASH_FLOOR = 8, QS_FL_CRASH_WALL = 16, QS_FL_CRASH_CEIL = 32
+};
+enum qs_env_field { QS_E_TICK = 0, QS_E_FLAGS = 1, QS_NE = 2 };
+
+typedef struct qs_layout {          /* byte offsets inside one workspace allocation */
+    size_t counter;                 /* uint64 RNG counter + uint32 block-arrival word (device-advanced) */
+    size_t state, istate, env, stale_vel, obs, term_obs, rew, done, total_bytes;
+    int32_t obs_dim, num_drones;
+} qs_layout;
+
+typedef struct qs_buffers {         /* device pointers (valid for the handle's lifetime) */
+    float* state;                   /* [QS_NF, I] */
+    int32_t* istate;                /* [QS_NI, I] */
+    int32_t* env;                   /* [QS_NE, E] */
+    float* stale_vel;               /* [3, I]  QuadrotorEnvMulti.vel as last seen by a reset */
+    float* obs;                     /* [I, obs_dim] */
+    float* term_obs;                /* [I, obs_dim] rows of envs that finished this step */
+    float* rew;                     /* [I] */
+    uint8_t* done;                  /* [I] */
+} qs_buffers;
+
+typedef struct qs_handle qs_handle;
+
+int qs_abi_version(void);
+const char* qs_last_error(void);
+/* sizeof(qs_config), sizeof(qs_layout), sizeof(qs_buffers): lets FFI callers check struct mirrors. */
+int qs_struct_sizes(size_t* config, size_t* layout, size_t* buffers);
+
+/* Crazyflie + flavor-B defaults (values of quad_models.py:1-42 via QuadLink, SF quad_utils.py). */
+int qs_config_default(qs_config* cfg, int32_t num_envs, int32_t num_agents);
+int qs_layout_query(const qs_config* cfg, qs_layout* out);
+
+/* d_workspace: NULL -> the library allocates (and frees) layout.total_bytes on hip_device;
+ * otherwise caller-owned device memory of at least layout.total_bytes, 256-byte aligned. */
+int qs_create(const qs_config* cfg, int hip_device, void* d_workspace, qs_handle** out);
+int qs_destroy(qs_handle* h);
+int qs_buffers_get(qs_handle* h, qs_buffers* out);
+
+/* Reset the envs whose byte in d_env_mask[E] is non-zero (NULL = all); writes obs rows of those envs. */
+int qs_reset(qs_handle* h, const uint8_t* d_env_mask, void* stream);
+/* One control step for every env: d_actions is [I, 4] fp32 raw policy output (clipped inside).
+ * Writes obs, rew, done; envs with tick > ep_len are auto-reset in the same launch, their final
+ * observation goes to term_obs and obs holds the reset observation (SubprocVecEnvCustom semantics). */
+int qs_step(qs_handle* h, const float* d_actions, void* stream);
+
+/* RNG counter (Philox counter words 2-3), kept in device memory and bumped on the device by every
+ * qs_step / qs_reset launch, so a captured hipGraph of K steps draws K distinct random streams.
+ * get/set synchronise the device. */
+int qs_counter_get(qs_handle* h, uint64_t* ctr);
+int qs_counter_set(qs_handle* h, uint64_t ctr);
+
+/* Runtime-tunable scalars: "rew_pos", "rew_effort", "rew_crash", "rew_orient", "rew_spin",
+ * "quadcol_bin", "quadcol_bin_smooth_max", "ep_len", "seed". */
+int qs_set_param(qs_handle* h, const char* key, double value);
+int qs_get_param(qs_handle* h, const char* key, double* value);
+
+/* Host snapshot of the whole env state (state, istate, env, stale_vel + counter): bytes =
+ * qs_state_bytes(); round-trips exactly through qs_set_state. Synchronises the stream. */
+size_t qs_state_bytes(qs_handle* h);
+int qs_get_state(qs_handle* h, void* host_dst, size_t bytes, void* stream);
+int qs_set_state(qs_handle* h, const void* host_src, size_t bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* QUADSWARM_H */

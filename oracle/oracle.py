@@ -206,9 +206,15 @@ class OracleEnv:
         self.seed = seed
         self.ctr = 0
 
-    def reset(self):
+    def reset(self, mask=None):
         obs = np.zeros((self.E * self.N, self.obs_dim))
-        lib().or_reset_all(ctypes.byref(self.p), self.drones, self.envs, self.seed, self.ctr, dptr(obs))
+        if mask is None:
+            lib().or_reset_all(ctypes.byref(self.p), self.drones, self.envs, self.seed, self.ctr, dptr(obs))
+        else:
+            r = philox_rng(self.seed, self.ctr)
+            for e in np.flatnonzero(mask):
+                rows = obs[e * self.N:(e + 1) * self.N]
+                lib().or_env_reset(ctypes.byref(self.p), self.drones, self.envs, int(e), ctypes.byref(r), dptr(rows))
         self.ctr += 1
         return obs
 

@@ -1,0 +1,84 @@
+// qs_rng.h -- counter-based RNG for the swarm step (Philox4x32-10, Salmon et al. SC'11).
+//
+// Every random draw of the reference (numba_utils.py:101-105 OU, sensor_noise.py:234-261,
+// collisions/*.py impulses, quadrotor_dynamics.py:624 floor flip, quadrotor_single.py:409,454 reset)
+// becomes a pure function of (seed, drone id, stream, step counter, index): results do not depend
+// on the launch geometry or on how many GPUs the envs are sharded over.
+//   key     = {drone global id, seed}
+//   counter = {block = index / 4, stream id, step_lo, step_hi}
+// Normals: Box-Muller on word pairs (0,1) and (2,3) of a block -> 4 normals per block.
+// Uniforms: stream | QS_UNIF_BIT, one word per draw.  The CPU oracle uses the same numbering.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace qs {
+
+enum : uint32_t {
+    S_OU = 1, S_FLOOR = 2, S_SENSOR = 3, S_PAIR = 4, S_WALL = 5, S_CEIL = 6, S_DW = 7, S_DWPAIR = 8,
+    S_RESET = 9, S_RESET_YAW = 10, S_RESET_SENSOR = 11, S_OBST = 12, UNIF_BIT = 0x80
+};
+
+struct Rng {
+    uint32_t seed, ctr_lo, ctr_hi;
+};
+
+struct W4 {
+    uint32_t w[4];
+};
+
+__device__ __forceinline__ W4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+    W4 o;
+    o.w[0] = c0; o.w[1] = c1; o.w[2] = c2; o.w[3] = c3;
+    return o;
+}
+
+__device__ __forceinline__ W4 block(const Rng& r, uint32_t id, uint32_t stream, uint32_t blk) {
+    return philox(blk, stream, r.ctr_lo, r.ctr_hi, id, r.seed);
+}
+
+// (0,1), exact in fp32: 24 high bits + half ulp
+__device__ __forceinline__ float u01(uint32_t x) { return ((float)(x >> 8) + 0.5f) * (1.0f / 16777216.0f); }
+
+__device__ __forceinline__ void box_muller(uint32_t a, uint32_t b, float& z0, float& z1) {
+    const float rr = sqrtf(-2.0f * logf(u01(a)));
+    float s, c;
+    sincospif(2.0f * u01(b), &s, &c);
+    z0 = rr * c;
+    z1 = rr * s;
+}
+
+// 4 normals of block blk
+__device__ __forceinline__ void normals4(const Rng& r, uint32_t id, uint32_t stream, uint32_t blk, float* z) {
+    const W4 q = block(r, id, stream, blk);
+    box_muller(q.w[0], q.w[1], z[0], z[1]);
+    box_muller(q.w[2], q.w[3], z[2], z[3]);
+}
+
+__device__ __forceinline__ float normal1(const Rng& r, uint32_t id, uint32_t stream, uint32_t idx) {
+    float z[4];
+    normals4(r, id, stream, idx >> 2, z);
+    return z[idx & 3];
+}
+
+// 4 uniforms of block blk of stream | UNIF_BIT
+__device__ __forceinline__ void uniforms4(const Rng& r, uint32_t id, uint32_t stream, uint32_t blk, float* u) {
+    const W4 q = block(r, id, stream | UNIF_BIT, blk);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) u[i] = u01(q.w[i]);
+}
+
+__device__ __forceinline__ float uniform1(const Rng& r, uint32_t id, uint32_t stream, uint32_t idx) {
+    const W4 q = block(r, id, stream | UNIF_BIT, idx >> 2);
+    return u01(q.w[idx & 3]);
+}
+
+}  // namespace qs

@@ -1,0 +1,105 @@
+"""ctypes binding of libquadswarm.so (include/quadswarm.h).
+
+The HIP library is the only implementation of the step: if it is missing or cannot be loaded this
+module raises instead of falling back to anything else.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("QUADSWARM_LIB", os.path.join(HERE, "lib", "libquadswarm.so"))
+
+ABI_VERSION = 1
+MAX_AGENTS = 32
+F, I32, U32, U64, SZ = ctypes.c_float, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_size_t
+
+# enum values (quadswarm.h)
+OBS_REPR = {"xyz_vxyz_R_omega": 0, "xyz_vxyz_R_omega_floor": 1, "xyz_vxyz_R_omega_wall": 2}
+SELF_OBS_DIM = {0: 18, 1: 19, 2: 24}
+NEIGHBOR_NONE, NEIGHBOR_POS_VEL = 0, 1
+F_POS, F_VEL, F_ROT, F_OMEGA, F_ROT_DAMP, F_CMD_DAMP, F_OU, F_GOAL, NF = 0, 3, 6, 15, 18, 22, 26, 30, 33
+I_SVD, I_FLAGS, I_PREV_LO, I_PREV_HI, NI = 0, 1, 2, 3, 4
+FL_ON_FLOOR, FL_PREV_WALL, FL_PREV_CEIL, FL_CRASH_FLOOR, FL_CRASH_WALL, FL_CRASH_CEIL = 1, 2, 4, 8, 16, 32
+E_TICK, E_FLAGS, NE = 0, 1, 2
+
+
+class QsConfig(ctypes.Structure):
+    _fields_ = [
+        ("abi_version", I32), ("num_envs", I32), ("num_agents", I32), ("obs_repr", I32), ("neighbor_obs", I32),
+        ("k_neighbors", I32), ("ep_len", I32), ("sim_steps", I32), ("svd_every", I32), ("sense_noise", I32),
+        ("use_downwash", I32), ("apply_collision_force", I32), ("seed", U32), ("drone_id_offset", U32),
+        ("dt", F), ("control_dt", F),
+        ("mass", F), ("inertia", F * 3),
+        ("thrust_max", F * 4), ("torque_max", F * 4), ("prop_cross", (F * 3) * 4), ("prop_ccw", F * 4),
+        ("motor_tau_up", F), ("motor_tau_down", F), ("motor_linearity", F),
+        ("arm", F), ("gravity", F), ("omega_max", F), ("vel_damp", F), ("damp_omega_quadratic", F), ("vxyz_max", F),
+        ("room_lo", F * 3), ("room_hi", F * 3),
+        ("ou_mu", F), ("ou_theta", F), ("ou_sigma", F),
+        ("pos_norm_std", F), ("pos_unif_range", F), ("vel_norm_std", F), ("vel_unif_range", F),
+        ("gyro_noise_density", F), ("quat_norm_std", F), ("quat_unif_range", F),
+        ("collision_threshold", F), ("collision_falloff_threshold", F),
+        ("rew_pos", F), ("rew_effort", F), ("rew_crash", F), ("rew_orient", F), ("rew_spin", F),
+        ("rew_quadcol_bin", F), ("rew_quadcol_smooth_max", F),
+        ("spawn_box", F), ("goal", F * 3),
+    ]
+
+
+class QsLayout(ctypes.Structure):
+    _fields_ = [("counter", SZ), ("state", SZ), ("istate", SZ), ("env", SZ), ("stale_vel", SZ), ("obs", SZ), ("term_obs", SZ),
+                ("rew", SZ), ("done", SZ), ("total_bytes", SZ), ("obs_dim", I32), ("num_drones", I32)]
+
+
+class QsBuffers(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("state", "istate", "env", "stale_vel", "obs", "term_obs", "rew", "done")]
+
+
+class QuadSwarmError(RuntimeError):
+    pass
+
+
+# every symbol include/quadswarm.h declares (tests check the library exports all of them)
+EXPORTS = ["qs_abi_version", "qs_last_error", "qs_struct_sizes", "qs_config_default", "qs_layout_query", "qs_create", "qs_destroy",
+           "qs_buffers_get", "qs_reset", "qs_step", "qs_counter_get", "qs_counter_set", "qs_set_param",
+           "qs_get_param", "qs_state_bytes", "qs_get_state", "qs_set_state"]
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise QuadSwarmError(f"libquadswarm.so not found at {LIB_PATH}; build it with __graft_entry__.build() "
+                             "or `make -C quad-swarm-rl-stable-baselines3_amd`")
+    L = ctypes.CDLL(LIB_PATH)
+    P, V = ctypes.POINTER, ctypes.c_void_p
+    sig = {
+        "qs_abi_version": ([], I32), "qs_last_error": ([], ctypes.c_char_p),
+        "qs_struct_sizes": ([P(SZ), P(SZ), P(SZ)], I32),
+        "qs_config_default": ([P(QsConfig), I32, I32], I32), "qs_layout_query": ([P(QsConfig), P(QsLayout)], I32),
+        "qs_create": ([P(QsConfig), ctypes.c_int, V, P(V)], I32), "qs_destroy": ([V], I32),
+        "qs_buffers_get": ([V, P(QsBuffers)], I32), "qs_reset": ([V, V, V], I32), "qs_step": ([V, V, V], I32),
+        "qs_counter_get": ([V, P(U64)], I32), "qs_counter_set": ([V, U64], I32),
+        "qs_set_param": ([V, ctypes.c_char_p, ctypes.c_double], I32),
+        "qs_get_param": ([V, ctypes.c_char_p, P(ctypes.c_double)], I32),
+        "qs_state_bytes": ([V], SZ), "qs_get_state": ([V, V, SZ, V], I32), "qs_set_state": ([V, V, SZ, V], I32),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes, fn.restype = args, res
+    if L.qs_abi_version() != ABI_VERSION:
+        raise QuadSwarmError("libquadswarm ABI version mismatch")
+    c, lay, b = SZ(), SZ(), SZ()
+    L.qs_struct_sizes(ctypes.byref(c), ctypes.byref(lay), ctypes.byref(b))
+    want = (ctypes.sizeof(QsConfig), ctypes.sizeof(QsLayout), ctypes.sizeof(QsBuffers))
+    if (c.value, lay.value, b.value) != want:
+        raise QuadSwarmError(f"struct mirror mismatch: C {(c.value, lay.value, b.value)} vs ctypes {want}")
+    _lib = L
+    return L
+
+
+def check(rc, what=""):
+    if rc != 0:
+        msg = lib().qs_last_error().decode(errors="replace")
+        raise QuadSwarmError(f"{what}: {msg} (code {rc})")

@@ -1,0 +1,152 @@
+"""Batched, HBM-resident QuadrotorEnvMulti (flavor B): E envs x N drones stepped by one HIP launch.
+
+Semantics per env follow QuadrotorEnvMulti.step / reset (gym_art/quadrotor_multi/quadrotor_multi.py:440-841)
+with the in-env auto-reset of :739-838 and the SubprocVecEnvCustom terminal_observation contract
+(swarm_rl/env_wrappers/subproc_vec_env_custom.py:33-52).  All buffers are torch tensors viewing one
+device workspace that libquadswarm.so reads and writes in place (zero-copy).
+"""
+import ctypes
+
+import numpy as np
+
+from . import _native as N
+from .config import QuadSwarmConfig
+
+
+class QuadSwarmEnv:
+    def __init__(self, cfg: QuadSwarmConfig, device=None):
+        import torch
+
+        self.cfg = cfg
+        self.device = torch.device(device if device is not None else cfg.device)
+        if self.device.type != "cuda" or not torch.cuda.is_available():
+            raise N.QuadSwarmError("QuadSwarmEnv needs a HIP device (torch.cuda on ROCm)")
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        self.qcfg = cfg.to_qs_config()
+        L = N.lib()
+        lay = N.QsLayout()
+        N.check(L.qs_layout_query(self.qcfg, lay), "qs_layout_query")
+        self.layout = lay
+        self.E, self.N = cfg.num_envs, cfg.num_agents
+        self.I = self.E * self.N
+        self.obs_dim = lay.obs_dim
+        self._raw = torch.zeros(lay.total_bytes + 256, dtype=torch.uint8, device=self.device)
+        off = (-self._raw.data_ptr()) % 256
+        ws = self._raw[off:off + lay.total_bytes]
+        self._ws = ws
+        h = ctypes.c_void_p()
+        N.check(L.qs_create(self.qcfg, self.device.index, ctypes.c_void_p(ws.data_ptr()), ctypes.byref(h)), "qs_create")
+        self._h = h
+
+        def view(o, nbytes, dtype, shape):
+            return ws[o:o + nbytes].view(dtype).view(*shape)
+        E, I, od = self.E, self.I, self.obs_dim
+        self.state = view(lay.state, 4 * N.NF * I, torch.float32, (N.NF, I))
+        self.istate = view(lay.istate, 4 * N.NI * I, torch.int32, (N.NI, I))
+        self.env_state = view(lay.env, 4 * N.NE * E, torch.int32, (N.NE, E))
+        self.stale_vel = view(lay.stale_vel, 4 * 3 * I, torch.float32, (3, I))
+        self.obs = view(lay.obs, 4 * I * od, torch.float32, (I, od))
+        self.term_obs = view(lay.term_obs, 4 * I * od, torch.float32, (I, od))
+        self.rew = view(lay.rew, 4 * I, torch.float32, (I,))
+        self.done = view(lay.done, I, torch.uint8, (I,))
+        self._torch = torch
+
+    # ------------------------------------------------------------------------------------------
+    def _stream(self):
+        return ctypes.c_void_p(self._torch.cuda.current_stream(self.device).cuda_stream)
+
+    def reset(self, env_mask=None):
+        """QuadrotorEnvMulti.reset for all envs (or those with env_mask[e] != 0); returns obs [I, obs_dim]."""
+        m = None
+        if env_mask is not None:
+            m = self._torch.as_tensor(env_mask, device=self.device).to(self._torch.uint8).contiguous()
+            if m.numel() != self.E:
+                raise ValueError("env_mask must have num_envs entries")
+        N.check(N.lib().qs_reset(self._h, ctypes.c_void_p(m.data_ptr()) if m is not None else None, self._stream()),
+                "qs_reset")
+        self._mask_keepalive = m
+        return self.obs
+
+    def step(self, actions):
+        """One control step of every env.  actions: [E*N, 4] (or [E, N, 4]) raw policy output.
+
+        Returns device views (obs, rew, done, term_obs); they are overwritten by the next call."""
+        a = actions
+        if not (self._torch.is_tensor(a) and a.device == self.device and a.dtype == self._torch.float32
+                and a.is_contiguous() and a.data_ptr() % 16 == 0):
+            a = self._torch.as_tensor(a, device=self.device, dtype=self._torch.float32).contiguous()
+        if a.numel() != self.I * 4:
+            raise ValueError(f"actions must have {self.I * 4} elements, got {a.numel()}")
+        self._act_keepalive = a
+        N.check(N.lib().qs_step(self._h, ctypes.c_void_p(a.data_ptr()), self._stream()), "qs_step")
+        return self.obs, self.rew, self.done, self.term_obs
+
+    # ------------------------------------------------------------------------------------------
+    def set_param(self, key, value):
+        N.check(N.lib().qs_set_param(self._h, key.encode(), float(value)), "qs_set_param")
+
+    def get_param(self, key):
+        v = ctypes.c_double()
+        N.check(N.lib().qs_get_param(self._h, key.encode(), ctypes.byref(v)), "qs_get_param")
+        return v.value
+
+    @property
+    def counter(self):
+        c = ctypes.c_uint64()
+        N.check(N.lib().qs_counter_get(self._h, ctypes.byref(c)), "qs_counter_get")
+        return c.value
+
+    @counter.setter
+    def counter(self, v):
+        N.check(N.lib().qs_counter_set(self._h, int(v)), "qs_counter_set")
+
+    def get_state(self):
+        """Host snapshot (bytes) of the full env state + RNG counter (checkpoint / replay)."""
+        n = N.lib().qs_state_bytes(self._h)
+        buf = (ctypes.c_uint8 * n)()
+        N.check(N.lib().qs_get_state(self._h, buf, n, self._stream()), "qs_get_state")
+        return bytes(buf)
+
+    def set_state(self, blob):
+        n = N.lib().qs_state_bytes(self._h)
+        if len(blob) < n:
+            raise ValueError("state blob too small")
+        buf = (ctypes.c_uint8 * n).from_buffer_copy(blob[:n])
+        N.check(N.lib().qs_set_state(self._h, buf, n, self._stream()), "qs_set_state")
+
+    # structured views (float32 SoA) for tests / debugging
+    def drone_fields(self):
+        s = self.state
+        return dict(pos=s[N.F_POS:N.F_POS + 3].T, vel=s[N.F_VEL:N.F_VEL + 3].T, rot=s[N.F_ROT:N.F_ROT + 9].T.reshape(-1, 3, 3),
+                    omega=s[N.F_OMEGA:N.F_OMEGA + 3].T, rot_damp=s[N.F_ROT_DAMP:N.F_ROT_DAMP + 4].T,
+                    cmd_damp=s[N.F_CMD_DAMP:N.F_CMD_DAMP + 4].T, ou=s[N.F_OU:N.F_OU + 4].T, goal=s[N.F_GOAL:N.F_GOAL + 3].T)
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._torch.cuda.synchronize(self.device)
+            N.check(N.lib().qs_destroy(self._h), "qs_destroy")
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def observation_bounds(cfg: QuadSwarmConfig):
+    """Observation-space box (QuadrotorSingle.make_observation_space, quadrotor_single.py:278-349)."""
+    rd = np.array(cfg.room_dims, dtype=np.float64)
+    room_range = np.array([rd[0], rd[1], rd[2]])
+    vmax, omax = 3.0, 40.0
+    lo = [-room_range, -vmax * np.ones(3), -np.ones(9), -omax * np.ones(3)]
+    hi = [room_range, vmax * np.ones(3), np.ones(9), omax * np.ones(3)]
+    if cfg.obs_repr.endswith("floor"):
+        lo.append(np.zeros(1)); hi.append(rd[2] * np.ones(1))
+    elif cfg.obs_repr.endswith("wall"):
+        lo.append(np.zeros(6)); hi.append(5.0 * np.ones(6))
+    for _ in range(cfg.k_neighbors):
+        lo += [-room_range, -2 * vmax * np.ones(3)]
+        hi += [room_range, 2 * vmax * np.ones(3)]
+    return np.concatenate(lo).astype(np.float32), np.concatenate(hi).astype(np.float32)

@@ -1,0 +1,159 @@
+"""Helpers shared by the parity tests: build the oracle twin of a GPU env and move state between them.
+
+Test infrastructure: the oracle (oracle/) is the checker, the GPU env (quadswarm_amd) is the product.
+"""
+import ctypes
+
+import numpy as np
+
+import oracle as O
+from quadswarm_amd import _native as NAT
+from quadswarm_amd.config import QuadSwarmConfig
+from quadswarm_amd.params import dynamics_constants, crazyflie_params
+
+
+def oracle_params(cfg: QuadSwarmConfig):
+    """OrParams with the constants the GPU handle was built from (float64 of the same derivation)."""
+    k = dynamics_constants(crazyflie_params(), dt=cfg.dt, thrust_noise_ratio=cfg.thrust_noise_ratio)
+    p = O.default_params()
+    p.mass = k["mass"]
+    for i in range(3):
+        p.inertia[i] = k["inertia"][i]
+    for j in range(4):
+        p.thrust_max[j] = k["thrust_max"][j]
+        p.torque_max[j] = k["torque_max"][j]
+        p.prop_ccw[j] = k["prop_ccw"][j]
+        for a in range(3):
+            p.prop_cross[j][a] = k["prop_cross"][j][a]
+    p.motor_tau_up, p.motor_tau_down = k["motor_tau_up"], k["motor_tau_down"]
+    p.arm = k["arm"]
+    # the GPU (like numba's jitclass spec, numba_utils.py:67-74) stores theta/sigma as float32
+    p.ou_theta = float(np.float32(0.15))
+    p.ou_sigma = float(np.float32(k["ou_sigma"]))
+    p.sense_noise = 0 if cfg.sense_noise is None else 1
+    p.num_agents, p.num_envs = cfg.num_agents, cfg.num_envs
+    p.ep_len = cfg.ep_len
+    p.obs_repr = NAT.OBS_REPR[cfg.obs_repr]
+    p.k_neighbors = cfg.k_neighbors
+    p.collision_threshold = cfg.collision_hitbox_radius * k["arm"]
+    p.collision_falloff_threshold = cfg.collision_falloff_radius * k["arm"]
+    p.control_dt = cfg.dt * cfg.sim_steps
+    p.rew_quadcol_bin = cfg.collision_reward
+    p.rew_quadcol_smooth_max = cfg.collision_smooth_max_penalty
+    p.use_downwash = int(cfg.use_downwash)
+    p.apply_collision_force = int(cfg.apply_collision_force)
+    rd = cfg.room_dims
+    for i, (lo, hi) in enumerate([(-rd[0] / 2, rd[0] / 2), (-rd[1] / 2, rd[1] / 2), (0.0, rd[2])]):
+        p.room_lo[i], p.room_hi[i] = lo, hi
+    return p
+
+
+def gpu_to_oracle(env, oenv):
+    """Copy the GPU env state (fp32 SoA) into the oracle's drones/envs (fp64)."""
+    st = env.state.double().cpu().numpy()
+    ist = env.istate.cpu().numpy()
+    es = env.env_state.cpu().numpy()
+    stale = env.stale_vel.double().cpu().numpy()
+    N, E = env.N, env.E
+    dt = env.cfg.dt
+    for g in range(env.I):
+        d = oenv.drones[g]
+        O.set_drone(d, pos=st[0:3, g], vel=st[3:6, g], rot=st[6:15, g], omega=st[15:18, g],
+                    thrust_rot_damp=st[18:22, g], thrust_cmds_damp=st[22:26, g], ou=st[26:30, g], goal=st[30:33, g])
+        fl = int(ist[NAT.I_FLAGS, g])
+        d.since_last_svd = float(ist[NAT.I_SVD, g]) * dt
+        d.on_floor = int(bool(fl & NAT.FL_ON_FLOOR))
+        d.prev_wall = int(bool(fl & NAT.FL_PREV_WALL))
+        d.prev_ceiling = int(bool(fl & NAT.FL_PREV_CEIL))
+    for e in range(E):
+        ev = oenv.envs[e]
+        ev.tick = int(es[NAT.E_TICK, e])
+        stale_valid = bool(es[NAT.E_FLAGS, e] & 1)
+        for i in range(N):
+            g = e * N + i
+            prev = int(np.uint32(ist[NAT.I_PREV_LO, g])) | (int(np.uint32(ist[NAT.I_PREV_HI, g])) << 32)
+            for j in range(N):
+                if j > i:
+                    ev.prev_pair_bits[i * 64 + j] = (prev >> j) & 1
+            for c in range(3):
+                ev.obs_vel[i][c] = stale[c, g] if stale_valid else st[3 + c, g]
+                ev.obs_pos[i][c] = st[c, g]
+
+
+def oracle_to_gpu(oenv, env):
+    """Copy oracle state (fp64) into the GPU env (rounded to fp32)."""
+    import torch
+    N, E, I = env.N, env.E, env.I
+    st = np.zeros((NAT.NF, I), np.float32)
+    ist = np.zeros((NAT.NI, I), np.int64)
+    es = np.zeros((NAT.NE, E), np.int32)
+    stale = np.zeros((3, I), np.float32)
+    dt = env.cfg.dt
+    for g in range(I):
+        d = oenv.drones[g]
+        st[0:3, g] = d.pos[:]
+        st[3:6, g] = d.vel[:]
+        st[6:15, g] = d.rot[:]
+        st[15:18, g] = d.omega[:]
+        st[18:22, g] = d.thrust_rot_damp[:]
+        st[22:26, g] = d.thrust_cmds_damp[:]
+        st[26:30, g] = d.ou[:]
+        st[30:33, g] = d.goal[:]
+        ist[NAT.I_SVD, g] = int(round(d.since_last_svd / dt))
+        ist[NAT.I_FLAGS, g] = (NAT.FL_ON_FLOOR if d.on_floor else 0) | (NAT.FL_PREV_WALL if d.prev_wall else 0) | \
+            (NAT.FL_PREV_CEIL if d.prev_ceiling else 0)
+    for e in range(E):
+        ev = oenv.envs[e]
+        es[NAT.E_TICK, e] = ev.tick
+        es[NAT.E_FLAGS, e] = 1      # neighbour reset obs read stale_vel (== oracle obs_vel)
+        for i in range(N):
+            g = e * N + i
+            prev = 0
+            for j in range(N):
+                a, b = min(i, j), max(i, j)
+                if i != j and ev.prev_pair_bits[a * 64 + b]:
+                    prev |= 1 << j
+            ist[NAT.I_PREV_LO, g] = np.int64(prev & 0xFFFFFFFF).astype(np.uint32).view(np.int32)
+            ist[NAT.I_PREV_HI, g] = np.int64(prev >> 32).astype(np.uint32).view(np.int32)
+            stale[:, g] = ev.obs_vel[i][:]
+    env.state.copy_(torch.from_numpy(st))
+    env.istate.copy_(torch.from_numpy(ist.astype(np.uint32).view(np.int32)))
+    env.env_state.copy_(torch.from_numpy(es))
+    env.stale_vel.copy_(torch.from_numpy(stale))
+
+
+def oracle_state_arrays(oenv):
+    n = oenv.E * oenv.N
+    pos = np.array([oenv.drones[g].pos[:] for g in range(n)])
+    vel = np.array([oenv.drones[g].vel[:] for g in range(n)])
+    rot = np.array([oenv.drones[g].rot[:] for g in range(n)])
+    omega = np.array([oenv.drones[g].omega[:] for g in range(n)])
+    return pos, vel, rot, omega
+
+
+def crowd(oenv, rng, frac_pairs=0.5, walls=True):
+    """Perturb a reset oracle env so the next steps hit every branch: close pairs (collisions and
+    proximity), wall/ceiling crossings, upside-down floor hits and near-terminal ticks."""
+    N = oenv.N
+    for e in range(oenv.E):
+        base = e * N
+        for i in range(0, N - 1, 2):
+            if rng.uniform() < frac_pairs:
+                a, b = oenv.drones[base + i], oenv.drones[base + i + 1]
+                off = rng.normal(scale=0.04, size=3)
+                for c in range(3):
+                    b.pos[c] = a.pos[c] + off[c]
+                    a.vel[c] = rng.uniform(-1, 1)
+        if walls and N >= 3:
+            k = oenv.drones[base + N - 1]
+            kind = e % 4
+            if kind == 0:
+                k.pos[0] = 4.995; k.vel[0] = 3.0
+            elif kind == 1:
+                k.pos[2] = 9.995; k.vel[2] = 3.0
+            elif kind == 2:
+                k.pos[2] = 0.06; k.vel[2] = -2.0
+                for c, v in enumerate([1.0, 0, 0, 0, -1.0, 0, 0, 0, -1.0]):
+                    k.rot[c] = v
+        if e % 5 == 0:
+            oenv.envs[e].tick = oenv.p.ep_len   # finishes on the next step

@@ -1,0 +1,126 @@
+"""CPU-side checks of the C ABI: libquadswarm.so loads, exports every symbol include/quadswarm.h
+declares, and its host-side logic (defaults, layout, validation, error reporting) behaves.  No
+compute calls: this runs without a GPU."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from quadswarm_amd import QuadSwarmConfig, _native as N
+from quadswarm_amd.params import dynamics_constants, svd_every
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    src = open(os.path.join(ROOT, "include", "quadswarm.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(qs_\w+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    L = N.lib()
+    syms = header_symbols()
+    assert len(syms) >= 15
+    for s in syms:
+        assert hasattr(L, s), f"libquadswarm.so does not export {s}"
+    assert sorted(N.EXPORTS) == syms
+
+
+def test_struct_mirrors_and_abi():
+    L = N.lib()
+    assert L.qs_abi_version() == N.ABI_VERSION
+    c, lay, b = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
+    assert L.qs_struct_sizes(ctypes.byref(c), ctypes.byref(lay), ctypes.byref(b)) == 0
+    assert (c.value, lay.value, b.value) == (ctypes.sizeof(N.QsConfig), ctypes.sizeof(N.QsLayout),
+                                             ctypes.sizeof(N.QsBuffers))
+
+
+def test_config_default_matches_host_derivation():
+    c = N.QsConfig()
+    assert N.lib().qs_config_default(c, 4096, 8) == 0
+    k = dynamics_constants()
+    assert c.num_envs == 4096 and c.num_agents == 8 and c.k_neighbors == 6 and c.ep_len == 1500
+    assert c.svd_every == svd_every() == 100
+    np.testing.assert_allclose(c.mass, k["mass"], rtol=1e-7)
+    np.testing.assert_allclose(list(c.inertia), k["inertia"], rtol=1e-7)
+    np.testing.assert_allclose(list(c.thrust_max), k["thrust_max"], rtol=1e-7)
+    np.testing.assert_allclose(c.arm, k["arm"], rtol=1e-7)
+    cfg = QuadSwarmConfig(num_envs=4096).to_qs_config()
+    for f in ("mass", "arm", "motor_tau_up", "ou_sigma", "collision_threshold", "ep_len", "k_neighbors"):
+        assert getattr(cfg, f) == pytest.approx(getattr(c, f), rel=1e-6), f
+
+
+@pytest.mark.parametrize("N_,K,repr_,od", [(8, 6, "xyz_vxyz_R_omega", 54), (1, 0, "xyz_vxyz_R_omega", 18),
+                                          (8, 2, "xyz_vxyz_R_omega_floor", 31), (32, 6, "xyz_vxyz_R_omega", 54),
+                                          (8, -1, "xyz_vxyz_R_omega_wall", 66)])
+def test_layout(N_, K, repr_, od):
+    cfg = QuadSwarmConfig(num_envs=100, num_agents=N_, neighbor_visible_num=K, obs_repr=repr_,
+                          neighbor_obs_type="pos_vel" if N_ > 1 else "none")
+    assert cfg.obs_dim == od
+    lay = N.QsLayout()
+    assert N.lib().qs_layout_query(cfg.to_qs_config(), lay) == 0
+    assert lay.obs_dim == od and lay.num_drones == 100 * N_
+    offs = [lay.counter, lay.state, lay.istate, lay.env, lay.stale_vel, lay.obs, lay.term_obs, lay.rew, lay.done]
+    assert all(o % 256 == 0 for o in offs) and offs == sorted(offs)
+    assert lay.obs - lay.state >= 4 * (N.NF + N.NI + 3) * 100 * N_
+    assert lay.total_bytes >= lay.done + 100 * N_
+
+
+def test_validation_errors_are_reported():
+    L = N.lib()
+    c = QuadSwarmConfig(num_envs=4, num_agents=8).to_qs_config()
+    lay = N.QsLayout()
+    bad = N.QsConfig.from_buffer_copy(c)
+    bad.k_neighbors = 9
+    assert L.qs_layout_query(bad, lay) == -1
+    assert b"k_neighbors" in L.qs_last_error()
+    bad = N.QsConfig.from_buffer_copy(c)
+    bad.num_agents = 33
+    assert L.qs_layout_query(bad, lay) == -2
+    bad = N.QsConfig.from_buffer_copy(c)
+    bad.abi_version = 99
+    assert L.qs_layout_query(bad, lay) == -1
+    with pytest.raises(N.QuadSwarmError):
+        N.check(L.qs_layout_query(bad, lay), "qs_layout_query")
+
+
+def test_config_rejects_unbuilt_flavors():
+    with pytest.raises(NotImplementedError):
+        QuadSwarmConfig(obs_repr="cdist_cdistdot_dist_distdot_sangle_angledot").to_qs_config()
+    with pytest.raises(NotImplementedError):
+        QuadSwarmConfig(quads_mode="mix").to_qs_config()
+
+
+def test_from_reference_cfg_names():
+    class Cfg:  # swarm_rl/global_cfg.py field names
+        num_agents = 8
+        episode_duration = 15.0
+        neighbor_visible_num = 6
+        neighbor_obs_type = "pos_vel"
+        obs_repr = "xyz_vxyz_R_omega"
+        quads_mode = "static_same_goal"
+        room_dims = [10, 10, 10]
+        seed = None
+    c = QuadSwarmConfig.from_reference_cfg(Cfg, num_envs=4096)
+    assert c.num_envs == 4096 and c.ep_len == 1500 and c.obs_dim == 54 and c.seed == 0
+
+
+def test_params_restatement_matches_reference(golden):
+    g = golden("params")
+    k = dynamics_constants()
+    for f in ("mass", "inertia", "thrust_max", "torque_max", "prop_cross", "arm", "motor_tau_up", "motor_tau_down"):
+        np.testing.assert_array_equal(np.asarray(k[f]), g[f])
+
+
+def test_create_without_device_fails_loudly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    L = N.lib()
+    h = ctypes.c_void_p()
+    rc = L.qs_create(QuadSwarmConfig(num_envs=4, num_agents=8).to_qs_config(), 0, None, ctypes.byref(h))
+    assert rc == -3 and not h.value
+    assert L.qs_last_error()

@@ -1,0 +1,228 @@
+"""GPU parity: the HIP step (libquadswarm.so through the C ABI) against the CPU oracle and the
+reference's golden fixtures.  Needs an MI355X: every test is marked gpu.
+
+Tolerances (fp32 GPU vs fp64 oracle, identical Philox draws):
+  * one step from an identical state:  obs / rewards / state within 2e-4 abs (2e-5 typical),
+    discrete outputs (done, collisions -> rewards) identical;
+  * free-running 10 steps from the same reset: 2e-3 abs on obs;
+  * reference noise-free golden trajectory (n8quiet, 300 steps): positions within 2e-3 m.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("no HIP device", allow_module_level=True)
+
+import oracle as O  # noqa: E402
+from parity_utils import crowd, gpu_to_oracle, oracle_params, oracle_to_gpu  # noqa: E402
+from quadswarm_amd import QuadSwarmConfig  # noqa: E402
+from quadswarm_amd.env import QuadSwarmEnv  # noqa: E402
+from quadswarm_amd.vec_env import GpuQuadVecEnv  # noqa: E402
+
+
+def make_pair(E=64, N=8, K=6, seed=7, **kw):
+    cfg = QuadSwarmConfig(num_envs=E, num_agents=N, neighbor_visible_num=K,
+                          neighbor_obs_type="pos_vel" if N > 1 else "none", seed=seed, **kw)
+    env = QuadSwarmEnv(cfg)
+    oenv = O.OracleEnv(oracle_params(cfg), seed=seed)
+    return cfg, env, oenv
+
+
+def np_(t):
+    return t.double().cpu().numpy()
+
+
+@pytest.mark.parametrize("N,K", [(8, 6), (8, 7), (1, 0), (4, 2), (32, 6)])
+def test_reset_matches_oracle(N, K):
+    E = 2048 // N
+    cfg, env, oenv = make_pair(E=E, N=N, K=K if N > 1 else -1)
+    obs = np_(env.reset())
+    want = oenv.reset()
+    np.testing.assert_allclose(obs, want, atol=2e-5, rtol=1e-5)
+    fields = env.drone_fields()
+    pos = np.array([oenv.drones[g].pos[:] for g in range(env.I)])
+    np.testing.assert_allclose(np_(fields["pos"]), pos, atol=2e-6)
+
+
+@pytest.mark.parametrize("N,K,dw", [(8, 6, False), (8, 7, False), (1, 0, False), (8, 2, True), (32, 6, False)])
+def test_one_step_from_identical_state(N, K, dw):
+    """Re-sync the GPU to the oracle's fp64 state every step: tight per-step parity incl. every branch."""
+    E = 2048 // N
+    cfg, env, oenv = make_pair(E=E, N=N, K=K if N > 1 else -1, use_downwash=dw, episode_duration=0.5)
+    env.reset()
+    oenv.reset()
+    rng = np.random.default_rng(3)
+    crowd(oenv, rng)
+    stats = dict(done=0, wall=0, coll=0)
+    for t in range(12):
+        oracle_to_gpu(oenv, env)
+        env.counter = oenv.ctr
+        a = rng.uniform(-1, 1, (env.I, 4)).astype(np.float32)
+        obs, rew, done, term = env.step(torch.from_numpy(a).cuda())
+        w_obs, w_rew, w_done, w_term = oenv.step(a.astype(np.float64))
+        np.testing.assert_array_equal(done.cpu().numpy().astype(bool), w_done)
+        np.testing.assert_allclose(np_(rew), w_rew, atol=2e-4, rtol=1e-4)
+        np.testing.assert_allclose(np_(obs), w_obs, atol=2e-4, rtol=1e-4)
+        if w_done.any():
+            np.testing.assert_allclose(np_(term)[w_done], w_term[w_done], atol=2e-4, rtol=1e-4)
+        stats["done"] += int(w_done.sum())
+        stats["coll"] += int((w_rew < -0.5).sum())
+        # states agree after the step too
+        f = env.drone_fields()
+        pos = np.array([oenv.drones[g].pos[:] for g in range(env.I)])
+        vel = np.array([oenv.drones[g].vel[:] for g in range(env.I)])
+        np.testing.assert_allclose(np_(f["pos"]), pos, atol=2e-5)
+        np.testing.assert_allclose(np_(f["vel"]), vel, atol=5e-4, rtol=1e-4)
+    assert stats["done"] > 0
+    if N > 1:
+        assert stats["coll"] > 0
+
+
+def test_free_run_matches_oracle():
+    cfg, env, oenv = make_pair(E=256, N=8, K=6)
+    np.testing.assert_allclose(np_(env.reset()), oenv.reset(), atol=2e-5)
+    rng = np.random.default_rng(5)
+    for t in range(10):
+        a = rng.uniform(-1, 1, (env.I, 4)).astype(np.float32)
+        obs, rew, done, _ = env.step(torch.from_numpy(a).cuda())
+        w_obs, w_rew, w_done, _ = oenv.step(a.astype(np.float64))
+        np.testing.assert_allclose(np_(obs), w_obs, atol=2e-3, rtol=1e-3)
+        np.testing.assert_allclose(np_(rew), w_rew, atol=1e-3)
+
+
+def test_reference_quiet_trajectory(golden):
+    """Noise-free reference trajectory (tests/golden/traj_n8quiet.npz, 300 steps) replayed on the GPU."""
+    g = golden("traj_n8quiet")
+    n = int(g["n"])
+    cfg = QuadSwarmConfig(num_envs=1, num_agents=n, neighbor_visible_num=int(g["k"]), sense_noise=None,
+                          thrust_noise_ratio=0.0, episode_duration=15.0)
+    env = QuadSwarmEnv(cfg)
+    env.reset()
+    st = env.state.cpu().numpy()
+    for i in range(n):
+        st[0:3, i], st[3:6, i] = g["init_pos"][i], g["init_vel"][i]
+        st[6:15, i], st[15:18, i] = g["init_rot"][i].ravel(), g["init_omega"][i]
+        st[18:22, i], st[22:26, i], st[26:30, i] = g["init_rd"][i], g["init_cd"][i], g["init_ou"][i]
+        st[30:33, i] = g["init_goal"][i]
+    env.state.copy_(torch.from_numpy(st))
+    ist = env.istate.cpu().numpy()
+    ist[0, :n] = np.round(g["init_since"] / 0.005).astype(np.int32)
+    ist[1:, :n] = 0
+    env.istate.copy_(torch.from_numpy(ist))
+    env.env_state.zero_()
+    for t in range(len(g["actions"])):
+        obs, rew, done, _ = env.step(torch.from_numpy(g["actions"][t].astype(np.float32)).cuda())
+        o = np_(obs)
+        assert not done.any()
+        np.testing.assert_allclose(o[:, 0:3], g["obs"][t][:, 0:3], atol=2e-3)
+        np.testing.assert_allclose(o, g["obs"][t], atol=2e-2)
+        np.testing.assert_allclose(np_(rew), g["rew"][t], atol=2e-4)
+
+
+def test_full_size_properties():
+    """Headline config (4096 envs x 8 drones): episode boundary, finiteness, clip boxes."""
+    cfg = QuadSwarmConfig(num_envs=4096, num_agents=8)
+    env = QuadSwarmEnv(cfg)
+    obs = env.reset()
+    assert obs.shape == (32768, 54)
+    a = torch.empty(32768, 4, device="cuda")
+    g = torch.Generator(device="cuda").manual_seed(0)
+    n_done_steps = 0
+    for t in range(cfg.ep_len + 3):
+        a.uniform_(-1, 1, generator=g)
+        obs, rew, done, term = env.step(a)
+        if done.any():
+            assert bool(done.all())          # synchronised episodes end together
+            assert t == cfg.ep_len           # tick > ep_len: 1501st step
+            assert torch.isfinite(term).all()
+            n_done_steps += 1
+        if t % 100 == 0 or done.any():
+            assert torch.isfinite(obs).all() and torch.isfinite(rew).all()
+            nb = obs[:, 18:].view(-1, 6, 6)
+            assert (nb[:, :, 0:3].abs() <= 10.0).all() and (nb[:, :, 3:6].abs() <= 6.0).all()
+            assert (obs[:, 6:15].abs() <= 1.0 + 1e-3).all()
+    assert n_done_steps == 1
+    # after the reset every drone spawned inside the static_same_goal box
+    pos = env.drone_fields()["pos"]
+    assert (pos[:, 0:2].abs() <= 2.0 + 1e-5).all() and (pos[:, 2] >= 0.75 - 1e-6).all() and (pos[:, 2] <= 4.0).all()
+
+
+def test_deterministic_and_shard_invariant():
+    """Same seed -> bitwise identical; two half-size shards with drone_id_offset == one big env."""
+    cfg = QuadSwarmConfig(num_envs=128, num_agents=8, seed=11, episode_duration=0.3)
+    a_env, b_env = QuadSwarmEnv(cfg), QuadSwarmEnv(cfg)
+    s0 = QuadSwarmEnv(QuadSwarmConfig(num_envs=64, num_agents=8, seed=11, episode_duration=0.3))
+    s1 = QuadSwarmEnv(QuadSwarmConfig(num_envs=64, num_agents=8, seed=11, episode_duration=0.3, drone_id_offset=512))
+    outs = [e.reset().clone() for e in (a_env, b_env)]
+    assert torch.equal(outs[0], outs[1])
+    assert torch.equal(torch.cat([s0.reset(), s1.reset()]), outs[0])
+    g = torch.Generator(device="cuda").manual_seed(1)
+    for t in range(40):
+        act = torch.rand(1024, 4, device="cuda", generator=g) * 2 - 1
+        ra = [x.clone() for x in a_env.step(act)[:3]]
+        rb = [x.clone() for x in b_env.step(act)[:3]]
+        r0 = [x.clone() for x in s0.step(act[:512].contiguous())[:3]]
+        r1 = [x.clone() for x in s1.step(act[512:].contiguous())[:3]]
+        for x, y, p, q in zip(ra, rb, r0, r1):
+            assert torch.equal(x, y)
+            assert torch.equal(torch.cat([p, q]), x)
+
+
+def test_state_snapshot_roundtrip():
+    env = QuadSwarmEnv(QuadSwarmConfig(num_envs=32, num_agents=8, seed=2))
+    env.reset()
+    act = torch.rand(256, 4, device="cuda") * 2 - 1
+    for _ in range(5):
+        env.step(act)
+    blob = env.get_state()
+    first = [x.clone() for x in env.step(act)[:3]]
+    env.set_state(blob)
+    again = [x.clone() for x in env.step(act)[:3]]
+    for x, y in zip(first, again):
+        assert torch.equal(x, y)
+
+
+def test_partial_reset_mask_matches_oracle():
+    cfg, env, oenv = make_pair(E=64, N=8, K=6)
+    env.reset()
+    oenv.reset()
+    a = np.random.default_rng(0).uniform(-1, 1, (env.I, 4)).astype(np.float32)
+    env.step(torch.from_numpy(a).cuda())
+    oenv.step(a.astype(np.float64))
+    mask = np.zeros(64, np.uint8)
+    mask[::3] = 1
+    before = np_(env.obs).copy()
+    gpu_to_oracle(env, oenv)   # oracle twin of the post-step state
+    oenv.ctr = env.counter
+    obs = np_(env.reset(mask))
+    want = oenv.reset(mask)
+    rows = np.repeat(mask.astype(bool), 8)
+    np.testing.assert_array_equal(obs[~rows], before[~rows])
+    np.testing.assert_allclose(obs[rows], want[rows], atol=2e-5, rtol=1e-5)
+    f = env.drone_fields()
+    assert (np_(f["vel"])[rows] == 0).all()
+    assert (env.env_state[0].cpu().numpy()[mask.astype(bool)] == 0).all()
+
+
+def test_vec_env_surface():
+    venv = GpuQuadVecEnv(QuadSwarmConfig(num_envs=16, num_agents=8, episode_duration=0.05))
+    assert venv.num_envs == 128
+    obs = venv.reset()
+    assert obs.shape == (128, 54) and obs.dtype == np.float32
+    assert venv.observation_space.shape == (54,) and venv.action_space.shape == (4,)
+    got_done = False
+    for t in range(10):
+        obs, rew, dones, infos = venv.step(np.random.uniform(-1, 1, (128, 4)).astype(np.float32))
+        assert obs.shape == (128, 54) and rew.shape == (128,) and dones.dtype == bool and len(infos) == 128
+        if dones.any():
+            got_done = True
+            i = int(np.flatnonzero(dones)[0])
+            assert infos[i]["terminal_observation"].shape == (54,)
+            assert venv.reset_infos[i // 8] == {}
+        else:
+            assert all(r is None for r in venv.reset_infos)
+    assert got_done
+    venv.close()
