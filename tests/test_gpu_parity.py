@@ -113,13 +113,39 @@ def test_reference_quiet_trajectory(golden):
     ist[1:, :n] = 0
     env.istate.copy_(torch.from_numpy(ist))
     env.env_state.zero_()
+    # Compare each drone while it is airborne.  All eight eventually drop to the floor (open-loop
+    # near-hover actions); floor sliding switches friction direction on |v| < 1e-6 (quadrotor_dynamics
+    # .py:593-611), which is ill-conditioned between fp32 and fp64, so contact phases are checked
+    # only for sanity.
+    airborne = np.ones(n, bool)
+    compared = 0
     for t in range(len(g["actions"])):
         obs, rew, done, _ = env.step(torch.from_numpy(g["actions"][t].astype(np.float32)).cuda())
         o = np_(obs)
-        assert not done.any()
-        np.testing.assert_allclose(o[:, 0:3], g["obs"][t][:, 0:3], atol=2e-3)
-        np.testing.assert_allclose(o, g["obs"][t], atol=2e-2)
-        np.testing.assert_allclose(np_(rew), g["rew"][t], atol=2e-4)
+        assert not done.any() and np.isfinite(o).all()
+        want = g["obs"][t]
+        airborne &= (want[:, 2] + 2.0) > 0.3
+        m = airborne
+        np.testing.assert_allclose(o[m, 0:3], want[m, 0:3], atol=2e-3, err_msg=f"step {t}")
+        np.testing.assert_allclose(o[m, :18], want[m, :18], atol=2e-2, err_msg=f"step {t}")
+        np.testing.assert_allclose(np_(rew)[m], g["rew"][t][m], atol=2e-4, err_msg=f"step {t}")
+        if m.all():
+            assert_neighbors_close(o[:, 18:], want[:, 18:], atol=2e-2)
+        compared += int(m.sum())
+        assert (o[:, 2] + 2.0 >= 0.0459).all()      # nobody sinks through the floor
+    assert compared >= 8 * 60
+
+
+def assert_neighbors_close(got, want, atol):
+    """Neighbour slots compared up to a permutation: after hundreds of fp32 steps two neighbours whose
+    sort keys are within rounding of each other may trade slots (the reference sorts in fp64)."""
+    got = got.reshape(len(got), -1, 6)
+    want = want.reshape(len(want), -1, 6)
+    for i in range(len(got)):
+        d = np.abs(got[i][:, None, :] - want[i][None, :, :]).max(-1)   # [slot_got, slot_want]
+        match = d.argmin(1)
+        assert len(set(match.tolist())) == len(match), f"drone {i}: neighbour sets differ"
+        assert d[np.arange(len(match)), match].max() <= atol, f"drone {i}: {d.min(1).max()}" 
 
 
 def test_full_size_properties():
@@ -139,15 +165,18 @@ def test_full_size_properties():
             assert t == cfg.ep_len           # tick > ep_len: 1501st step
             assert torch.isfinite(term).all()
             n_done_steps += 1
+            # the reset put every drone inside the static_same_goal spawn box, at rest
+            f = env.drone_fields()
+            pos = f["pos"]
+            assert (pos[:, 0:2].abs() <= 2.0 + 1e-5).all() and (pos[:, 2] >= 0.75 - 1e-6).all()
+            assert (pos[:, 2] <= 4.0 + 1e-5).all() and (f["vel"] == 0).all() and (f["omega"] == 0).all()
+            assert (env.env_state[0] == 0).all()
         if t % 100 == 0 or done.any():
             assert torch.isfinite(obs).all() and torch.isfinite(rew).all()
             nb = obs[:, 18:].view(-1, 6, 6)
             assert (nb[:, :, 0:3].abs() <= 10.0).all() and (nb[:, :, 3:6].abs() <= 6.0).all()
             assert (obs[:, 6:15].abs() <= 1.0 + 1e-3).all()
     assert n_done_steps == 1
-    # after the reset every drone spawned inside the static_same_goal box
-    pos = env.drone_fields()["pos"]
-    assert (pos[:, 0:2].abs() <= 2.0 + 1e-5).all() and (pos[:, 2] >= 0.75 - 1e-6).all() and (pos[:, 2] <= 4.0).all()
 
 
 def test_deterministic_and_shard_invariant():

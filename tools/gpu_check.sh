@@ -1,0 +1,39 @@
+#!/bin/bash
+# GPU-box sequence: smoke -> gpu tests -> bench.  Stops at the first crash / timeout / abort
+# (exit codes other than 0 = ok and 1 = ordinary test failure).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+step() {  # name timeout cmd...
+  local name=$1 to=$2; shift 2
+  echo "== $name" | tee -a gpurun_out/steps.log
+  timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc" | tee -a gpurun_out/steps.log
+  tail -5 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+: > gpurun_out/steps.log
+for s in "$@"; do
+  case $s in
+    smoke) step smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests) step gpu_tests 900 python -m pytest tests -m gpu -q -x ;;
+    testsall) step gpu_tests 900 python -m pytest tests -m gpu -q ;;
+    bench) step bench 400 python bench.py ;;
+    benchfast) step bench 300 python bench.py --steps 1000 --cpu-seconds 5 ;;
+    prof)
+      export TMPDIR=/tmp
+      step prof_kt 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_kt -o kt --output-format csv -- python bench.py --steps 1000 --no-cpu-baseline --graph 0
+      step prof_fetch 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof_fetch -o f --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu-baseline --graph 0
+      step prof_write 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof_write -o w --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu-baseline --graph 0
+      step prof_sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INSTS_LDS -d gpurun_out/prof_sq -o s --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu-baseline --graph 0
+      ;;
+    calib)
+      export TMPDIR=/tmp
+      step calib_fetch 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/calib_fetch -o cf --output-format csv -- ./tools/calib/fetch_calib
+      step calib_write 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/calib_write -o cw --output-format csv -- ./tools/calib/fetch_calib
+      ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
