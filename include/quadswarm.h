@@ -104,6 +104,7 @@ enum qs_env_field { QS_E_TICK = 0, QS_E_FLAGS = 1, QS_NE = 2 };
 
 typedef struct qs_layout {          /* byte offsets inside one workspace allocation */
     size_t counter;                 /* uint64 RNG counter + uint32 block-arrival word (device-advanced) */
+    size_t params;                  /* kernel parameter block (device copy of the config + runtime params) */
     size_t state, istate, env, stale_vel, obs, term_obs, rew, done, total_bytes;
     int32_t obs_dim, num_drones;
 } qs_layout;

@@ -48,12 +48,13 @@ __device__ __forceinline__ W4 block(const Rng& r, uint32_t id, uint32_t stream, 
 // (0,1), exact in fp32: 24 high bits + half ulp
 __device__ __forceinline__ float u01(uint32_t x) { return ((float)(x >> 8) + 0.5f) * (1.0f / 16777216.0f); }
 
+// Box-Muller on the hardware transcendentals: v_log_f32 (log2), v_sqrt_f32, and v_sin/v_cos_f32,
+// which take their argument in revolutions (sin(2 pi x)), exactly the Box-Muller angle.
 __device__ __forceinline__ void box_muller(uint32_t a, uint32_t b, float& z0, float& z1) {
-    const float rr = sqrtf(-2.0f * logf(u01(a)));
-    float s, c;
-    sincospif(2.0f * u01(b), &s, &c);
-    z0 = rr * c;
-    z1 = rr * s;
+    const float rr = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u01(a)));  // -2 ln u
+    const float ub = u01(b);
+    z0 = rr * __builtin_amdgcn_cosf(ub);
+    z1 = rr * __builtin_amdgcn_sinf(ub);
 }
 
 // 4 normals of block blk

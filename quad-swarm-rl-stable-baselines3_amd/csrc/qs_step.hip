@@ -64,6 +64,10 @@ struct Drone {
 };
 
 __device__ __forceinline__ float clampf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
+// single-instruction sqrt / reciprocal (v_sqrt_f32 / v_rcp_f32, ~1 ulp): the step is compared with the
+// fp64 oracle at 1e-5..1e-4, far above these errors
+__device__ __forceinline__ float fsqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+__device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
 
 // ---------------------------------------------------------------------------------------------
 // state I/O (SoA, coalesced per field)
@@ -129,7 +133,7 @@ __device__ __forceinline__ void polar3(float* x) {
     for (int it = 0; it < 3; ++it) {
         const float a = x[0], b = x[1], c = x[2], d = x[3], e = x[4], f = x[5], g = x[6], h = x[7], i = x[8];
         const float A = e * i - f * h, B = f * g - d * i, C = d * h - e * g;
-        const float inv = 1.0f / (a * A + b * B + c * C);
+        const float inv = frcp(a * A + b * B + c * C);
         const float cof[9] = {A, B, C, c * h - b * i, a * i - c * g, b * g - a * h, b * f - c * e, c * d - a * f,
                               a * e - b * d};
 #pragma unroll
@@ -146,7 +150,7 @@ __device__ void substep(const KP& kp, Drone& d, const float* cmds, const float* 
         const float cmd = cmds[k];
         float tau = cmd < d.cd[k] ? kp.tau_down : kp.tau_up;
         tau = fminf(tau, 1.0f);
-        d.rd[k] = tau * (sqrtf(cmd) - d.rd[k]) + d.rd[k];
+        d.rd[k] = tau * (fsqrt(cmd) - d.rd[k]) + d.rd[k];
         const float c = clampf(d.rd[k] * d.rd[k] + cmd * noise[k], 0.f, 1.f);
         d.cd[k] = c;
         thrusts[k] = kp.thrust_max[k] * ((1.f - kp.lin) * c * c + kp.lin * c);
@@ -159,30 +163,39 @@ __device__ void substep(const KP& kp, Drone& d, const float* cmds, const float* 
         tsum += thrusts[k];
     }
     float* R = d.rot;
-    {  // Rodrigues with world-frame omega (:544-551)
-        const float w0 = R[0] * d.om[0] + R[1] * d.om[1] + R[2] * d.om[2];
-        const float w1 = R[3] * d.om[0] + R[4] * d.om[1] + R[5] * d.om[2];
-        const float w2 = R[6] * d.om[0] + R[7] * d.om[1] + R[8] * d.om[2];
-        const float wn = sqrtf(w0 * w0 + w1 * w1 + w2 * w2);
-        if (wn != 0.f) {
-            const float inv = 1.0f / wn;
-            const float x = w0 * inv, y = w1 * inv, z = w2 * inv;
+    {  // Rodrigues with world-frame omega (:544-551):  dR = I + sin(a) K + (1 - cos a) K^2,
+       // K = skew(w)/|w|, a = |w| dt.  Written as I + dt S(a^2) skew(w) + dt^2 C(a^2) (w w^T - |w|^2 I)
+       // with S = sin(a)/a and C = (1 - cos a)/a^2: no sqrt, no division, no branch at w = 0 (where
+       // the reference skips the update: dR = I exactly as the series gives).
+        const float wx = R[0] * d.om[0] + R[1] * d.om[1] + R[2] * d.om[2];
+        const float wy = R[3] * d.om[0] + R[4] * d.om[1] + R[5] * d.om[2];
+        const float wz = R[6] * d.om[0] + R[7] * d.om[1] + R[8] * d.om[2];
+        const float w2 = wx * wx + wy * wy + wz * wz;
+        const float x = w2 * (dt * dt);
+        float sf, cf;
+        if (x < 0.36f) {  // a < 0.6: Taylor to a^8, truncation < 2e-10 (|omega| <= 40 per axis gives a <= 0.35)
+            sf = dt * (1.f + x * (-1.f / 6.f + x * (1.f / 120.f + x * (-1.f / 5040.f + x * (1.f / 362880.f)))));
+            cf = dt * dt * (0.5f + x * (-1.f / 24.f + x * (1.f / 720.f + x * (-1.f / 40320.f + x * (1.f / 3628800.f)))));
+        } else {          // after collision kicks (|omega| up to ~100 rad/s before the clip)
+            const float wn = fsqrt(w2), a = wn * dt;
             float sa, ca;
-            sincosf(wn * dt, &sa, &ca);
-            ca = 1.0f - ca;
-            // dR = I + sa K + ca K^2, K^2 = n n^T - I
-            const float dR[9] = {1.f + ca * (x * x - 1.f), -sa * z + ca * x * y, sa * y + ca * x * z,
-                                 sa * z + ca * x * y, 1.f + ca * (y * y - 1.f), -sa * x + ca * y * z,
-                                 -sa * y + ca * x * z, sa * x + ca * y * z, 1.f + ca * (z * z - 1.f)};
-            float Rn[9];
-#pragma unroll
-            for (int i = 0; i < 3; ++i)
-#pragma unroll
-                for (int j = 0; j < 3; ++j)
-                    Rn[i * 3 + j] = dR[i * 3] * R[j] + dR[i * 3 + 1] * R[3 + j] + dR[i * 3 + 2] * R[6 + j];
-#pragma unroll
-            for (int i = 0; i < 9; ++i) R[i] = Rn[i];
+            sincosf(0.5f * a, &sa, &ca);
+            sf = 2.f * sa * ca / wn;
+            cf = 2.f * sa * sa / w2;
         }
+        const float sx = sf * wx, sy = sf * wy, sz = sf * wz;
+        const float d0 = 1.f - cf * w2;
+        const float dR[9] = {d0 + cf * wx * wx, -sz + cf * wx * wy, sy + cf * wx * wz,
+                             sz + cf * wx * wy, d0 + cf * wy * wy, -sx + cf * wy * wz,
+                             -sy + cf * wx * wz, sx + cf * wy * wz, d0 + cf * wz * wz};
+        float Rn[9];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+                Rn[i * 3 + j] = dR[i * 3] * R[j] + dR[i * 3 + 1] * R[3 + j] + dR[i * 3 + 2] * R[6 + j];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) R[i] = Rn[i];
     }
     if (++d.svd >= kp.svd_every) {  // since_last_svd > 0.5 s (:553-558)
         polar3(R);
@@ -219,9 +232,9 @@ __device__ void substep(const KP& kp, Drone& d, const float* cmds, const float* 
         if (fl & QS_FL_ON_FLOOR) {
             yaw_rot(atan2f(R[3], R[0] + 1e-6f), R);
             const float fric = 0.6f * (kp.mass * kp.grav - fz);
-            const float vn = sqrtf(d.vel[0] * d.vel[0] + d.vel[1] * d.vel[1] + d.vel[2] * d.vel[2]);
+            const float vn = fsqrt(d.vel[0] * d.vel[0] + d.vel[1] * d.vel[1] + d.vel[2] * d.vel[2]);
             if (vn < 1e-6f) {
-                float fxy = sqrtf(fx * fx + fy * fy);
+                float fxy = fsqrt(fx * fx + fy * fy);
                 fxy = fmaxf(fxy - fric, 0.f);
                 if (fxy == 0.f) {
                     fx = 0.f; fy = 0.f;
@@ -302,12 +315,12 @@ __device__ void self_obs(const KP& kp, const Drone& d, const Rng& rng, uint32_t 
         const float q2 = (th[0] * th[0] + th[1] * th[1] + th[2] * th[2]) * 0.25f;
         float qt[4];
         if (q2 < 1.f) {
-            qt[0] = sqrtf(1.f - q2); qt[1] = th[0] * 0.5f; qt[2] = th[1] * 0.5f; qt[3] = th[2] * 0.5f;
+            qt[0] = fsqrt(1.f - q2); qt[1] = th[0] * 0.5f; qt[2] = th[1] * 0.5f; qt[3] = th[2] * 0.5f;
         } else {
             const float w = rsqrtf(1.f + q2), f = 0.5f * w;
             qt[0] = w; qt[1] = th[0] * f; qt[2] = th[1] * f; qt[3] = th[2] * f;
         }
-        const float qn = 1.0f / sqrtf(qt[0] * qt[0] + qt[1] * qt[1] + qt[2] * qt[2] + qt[3] * qt[3]);
+        const float qn = frcp(fsqrt(qt[0] * qt[0] + qt[1] * qt[1] + qt[2] * qt[2] + qt[3] * qt[3]));
 #pragma unroll
         for (int i = 0; i < 4; ++i) qt[i] *= qn;
         // rot2quat (sensor_noise.py:34-63)
@@ -315,16 +328,16 @@ __device__ void self_obs(const KP& kp, const Drone& d, const Rng& rng, uint32_t 
         float q[4];
         const float tr = R[0] + R[4] + R[8];
         if (tr > 0.f) {
-            const float S = sqrtf(tr + 1.f) * 2.f, iS = 1.f / S;
+            const float S = fsqrt(tr + 1.f) * 2.f, iS = frcp(S);
             q[0] = 0.25f * S; q[1] = (R[7] - R[5]) * iS; q[2] = (R[2] - R[6]) * iS; q[3] = (R[3] - R[1]) * iS;
         } else if (R[0] > R[4] && R[0] > R[8]) {
-            const float S = sqrtf(1.f + R[0] - R[4] - R[8]) * 2.f, iS = 1.f / S;
+            const float S = fsqrt(1.f + R[0] - R[4] - R[8]) * 2.f, iS = frcp(S);
             q[0] = (R[7] - R[5]) * iS; q[1] = 0.25f * S; q[2] = (R[1] + R[3]) * iS; q[3] = (R[2] + R[6]) * iS;
         } else if (R[4] > R[8]) {
-            const float S = sqrtf(1.f + R[4] - R[0] - R[8]) * 2.f, iS = 1.f / S;
+            const float S = fsqrt(1.f + R[4] - R[0] - R[8]) * 2.f, iS = frcp(S);
             q[0] = (R[2] - R[6]) * iS; q[1] = (R[1] + R[3]) * iS; q[2] = 0.25f * S; q[3] = (R[5] + R[7]) * iS;
         } else {
-            const float S = sqrtf(1.f + R[8] - R[0] - R[4]) * 2.f, iS = 1.f / S;
+            const float S = fsqrt(1.f + R[8] - R[0] - R[4]) * 2.f, iS = frcp(S);
             q[0] = (R[3] - R[1]) * iS; q[1] = (R[2] + R[6]) * iS; q[2] = (R[5] + R[7]) * iS; q[3] = 0.25f * S;
         }
         // quatXquat + quat2R (quad_utils.py:146-174)
@@ -359,44 +372,52 @@ __device__ void self_obs(const KP& kp, const Drone& d, const Rng& rng, uint32_t 
     }
 }
 
+// Neighbour exchange tile in LDS: lane l stores {pos, 0} at xch[2l] and {vel, 0} at xch[2l+1]; the
+// drones of one env read each other's rows with broadcast ds_read_b128 (one wave per workgroup, so a
+// workgroup barrier costs nothing but orders the LDS traffic).
+// LDS-only workgroup barrier: workgroups are one wave, so this just orders LDS traffic.  Unlike
+// __syncthreads() it does not wait for outstanding global stores (vmcnt) or fence global memory.
+__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+__device__ __forceinline__ void xch_put(float4* xch, int lane, const float* P, const float* V) {
+    xch[2 * lane] = make_float4(P[0], P[1], P[2], 0.f);
+    xch[2 * lane + 1] = make_float4(V[0], V[1], V[2], 0.f);
+}
+
 // pos_vel neighbour obs: neighborhood_indices (quadrotor_multi.py:344-375) + extend_obs_space
 // clip (:328-342).  Key = |[rel_pos, rel_vel]| clamped at 0.01 (compared squared, clamp 1e-4);
 // stable (index) tie-break like numpy's insertion sort; k == N-1 keeps index order (all keys 0).
-// Every lane of the wave executes the shuffles; only lanes with write == true store.
+// Reads the exchange tile (caller has synchronised); only lanes with write == true store.
 template <int NPAD>
-__device__ void neighbor_obs(const KP& kp, int base, int di, const float* P, const float* V, bool write, float* out) {
+__device__ void neighbor_obs(const KP& kp, const float4* xch, int base, int di, const float* P, const float* V,
+                             bool write, float* out) {
     float key[NPAD];
     const bool sorted = kp.K < kp.N - 1;
 #pragma unroll
     for (int j = 0; j < NPAD; ++j) {
-        float s = 0.f;
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            const float rp = __shfl(P[c], base + j) - P[c];
-            const float rv = __shfl(V[c], base + j) - V[c];
-            s += rp * rp + rv * rv;
-        }
+        const float4 pj = xch[2 * (base + j)], vj = xch[2 * (base + j) + 1];
+        const float a0 = pj.x - P[0], a1 = pj.y - P[1], a2 = pj.z - P[2];
+        const float b0 = vj.x - V[0], b1 = vj.y - V[1], b2 = vj.z - V[2];
+        const float s = a0 * a0 + a1 * a1 + a2 * a2 + b0 * b0 + b1 * b1 + b2 * b2;
         const bool valid = (j != di) && (j < kp.N);
         key[j] = valid ? (sorted ? fmaxf(s, 1e-4f) : 0.f) : __builtin_inff();
     }
+    if (!write) return;
 #pragma unroll
     for (int j = 0; j < NPAD; ++j) {
         int rank = 0;
 #pragma unroll
         for (int m = 0; m < NPAD; ++m) rank += (key[m] < key[j]) || (m < j && key[m] == key[j]);
-        float rp[3], rv[3];
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            rp[c] = __shfl(P[c], base + j) - P[c];
-            rv[c] = __shfl(V[c], base + j) - V[c];
-        }
-        if (write && j != di && j < kp.N && rank < kp.K) {
+        if (key[j] != __builtin_inff() && rank < kp.K) {
+            const float4 pj = xch[2 * (base + j)], vj = xch[2 * (base + j) + 1];
             float* o = out + kp.so_dim + rank * 6;
-#pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                o[c] = clampf(rp[c], -kp.room_range[c], kp.room_range[c]);
-                o[3 + c] = clampf(rv[c], -2.f * kp.vxyz_max, 2.f * kp.vxyz_max);
-            }
+            o[0] = clampf(pj.x - P[0], -kp.room_range[0], kp.room_range[0]);
+            o[1] = clampf(pj.y - P[1], -kp.room_range[1], kp.room_range[1]);
+            o[2] = clampf(pj.z - P[2], -kp.room_range[2], kp.room_range[2]);
+            const float vm = 2.f * kp.vxyz_max;
+            o[3] = clampf(vj.x - V[0], -vm, vm);
+            o[4] = clampf(vj.y - V[1], -vm, vm);
+            o[5] = clampf(vj.z - V[2], -vm, vm);
         }
     }
 }
@@ -407,8 +428,8 @@ __device__ void neighbor_obs(const KP& kp, int base, int di, const float* P, con
 // compute_new_vel (collisions/utils.py:7-20)
 __device__ __forceinline__ void new_vel(float maxv, float* v, const float* sh, float ratio) {
     const float n0 = v[0] + sh[0], n1 = v[1] + sh[1], n2 = v[2] + sh[2];
-    const float mag = sqrtf(n0 * n0 + n1 * n1 + n2 * n2);
-    const float inv = 1.0f / (mag == 0.f ? 1e-5f : mag);
+    const float mag = fsqrt(n0 * n0 + n1 * n1 + n2 * n2);
+    const float inv = frcp(mag == 0.f ? 1e-5f : mag);
     const float nm = fminf(mag * ratio, maxv);
     v[0] += n0 * inv * nm - v[0];
     v[1] += n1 * inv * nm - v[1];
@@ -421,8 +442,8 @@ __device__ void collide_pair(const float* p1, float* v1, float* w1, const float*
                              const Rng& rng, uint32_t gid, uint32_t j) {
     const uint32_t st = S_PAIR | (j << 8);
     float n[3] = {p1[0] - p2[0], p1[1] - p2[1], p1[2] - p2[2]};
-    const float m = sqrtf(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
-    const float im = 1.0f / (m == 0.f ? 1e-5f : m);
+    const float m = fsqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+    const float im = frcp(m == 0.f ? 1e-5f : m);
     n[0] *= im; n[1] *= im; n[2] *= im;
     const float v1n = v1[0] * n[0] + v1[1] * n[1] + v1[2] * n[2];
     const float v2n = v2[0] * n[0] + v2[1] * n[1] + v2[2] * n[2];
@@ -446,8 +467,8 @@ __device__ void collide_pair(const float* p1, float* v1, float* w1, const float*
         }
         if (d1 > 0.f && 0.f > d2) break;
     }
-    const float mx = fmaxf(sqrtf(v1[0] * v1[0] + v1[1] * v1[1] + v1[2] * v1[2]),
-                           sqrtf(v2[0] * v2[0] + v2[1] * v2[1] + v2[2] * v2[2]));
+    const float mx = fmaxf(fsqrt(v1[0] * v1[0] + v1[1] * v1[1] + v1[2] * v1[2]),
+                           fsqrt(v2[0] * v2[0] + v2[1] * v2[1] + v2[2] * v2[2]));
     float u[8];
     uniforms4(rng, gid, st, 0, u);
     uniforms4(rng, gid, st, 1, u + 4);
@@ -456,8 +477,8 @@ __device__ void collide_pair(const float* p1, float* v1, float* w1, const float*
     // compute_new_omega (collisions/utils.py:23-33), magn_scale 20
     const float om = 20.f * 3.14159265358979f;
     float w[3] = {-1.f + 2.f * u[2], -1.f + 2.f * u[3], -1.f + 2.f * u[4]};
-    const float wm = sqrtf(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
-    const float iw = 1.0f / (wm == 0.f ? 1e-5f : wm);
+    const float wm = fsqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+    const float iw = frcp(wm == 0.f ? 1e-5f : wm);
     const float mg = om * 0.5f + (om - om * 0.5f) * u[5];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -474,7 +495,7 @@ __device__ void collide_room(const KP& kp, Drone& d, const Rng& rng, uint32_t gi
     uniforms4(rng, gid, st, 0, u);
     uniforms4(rng, gid, st, 1, u + 4);
     uniforms4(rng, gid, st, 2, u + 8);
-    const float sp = sqrtf(d.vel[0] * d.vel[0] + d.vel[1] * d.vel[1] + d.vel[2] * d.vel[2]);
+    const float sp = fsqrt(d.vel[0] * d.vel[0] + d.vel[1] * d.vel[1] + d.vel[2] * d.vel[2]);
     const float real = clampf(0.2f * sp + (0.8f * sp - 0.2f * sp) * u[0], 0.1f, 6.0f);
     float dir[3] = {-1.f + 2.f * u[1], -1.f + 2.f * u[2], -1.f + 2.f * u[3]};
     int ow;
@@ -489,9 +510,9 @@ __device__ void collide_room(const KP& kp, Drone& d, const Rng& rng, uint32_t gi
         dir[2] = -1.f + 0.5f * u[4];
         ow = 5;
     }
-    const float idm = 1.0f / (sqrtf(dir[0] * dir[0] + dir[1] * dir[1] + dir[2] * dir[2]) + 1e-5f);
+    const float idm = frcp(fsqrt(dir[0] * dir[0] + dir[1] * dir[1] + dir[2] * dir[2]) + 1e-5f);
     float w[3] = {-1.f + 2.f * u[ow], -1.f + 2.f * u[ow + 1], -1.f + 2.f * u[ow + 2]};
-    const float iw = 1.0f / (sqrtf(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]) + 1e-5f);
+    const float iw = frcp(fsqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]) + 1e-5f);
     const float om = 20.f * 3.14159265358979f;
     const float mg = om * 0.5f + (om - om * 0.5f) * u[ow + 3];
 #pragma unroll
@@ -517,7 +538,7 @@ __device__ void reset_drone(const KP& kp, Drone& d, const Rng& rng, uint32_t gid
     if (d.pos[2] < 0.75f) d.pos[2] = 0.75f;
     // randyaw rejection until the body x axis points within 60 deg of the origin (:454-456)
     float tx = -d.pos[0], ty = -d.pos[1];
-    const float tn = sqrtf(tx * tx + ty * ty);
+    const float tn = fsqrt(tx * tx + ty * ty);
     const bool degenerate = tn < 1e-5f;
     tx = degenerate ? 0.f : tx / tn;
     ty = degenerate ? 0.f : ty / tn;
@@ -548,19 +569,18 @@ __device__ void reset_drone(const KP& kp, Drone& d, const Rng& rng, uint32_t gid
 // block-level obs staging: LDS tile [rows, obs_dim] -> contiguous global rows
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ void tile_store(const float* lds, float* dst, int nfloat, int lane) {
-    // dst is the start of the block's row range; 16-byte vectors for the aligned body
-    const uintptr_t addr = (uintptr_t)dst;
-    int head = (int)(((16 - (addr & 15)) & 15) >> 2);
-    if (head > nfloat) head = nfloat;
-    if (lane < head) dst[lane] = lds[lane];
-    const int nvec = (nfloat - head) >> 2;
-    float4* dv = reinterpret_cast<float4*>(dst + head);
-    for (int v = lane; v < nvec; v += 64) {
-        const int o = head + 4 * v;
-        dv[v] = make_float4(lds[o], lds[o + 1], lds[o + 2], lds[o + 3]);
+    // dst = first row of the block; rows are contiguous in HBM.  obs is 256-B aligned and a block owns
+    // 64/NPAD*N rows, so the start is 16-B aligned whenever rows*obs_dim*4 is: b128 in, dwordx4 out.
+    if ((((uintptr_t)dst) & 15) == 0) {
+        const int nvec = nfloat >> 2;
+        const float4* lv = reinterpret_cast<const float4*>(lds);
+        float4* dv = reinterpret_cast<float4*>(dst);
+        for (int v = lane; v < nvec; v += 64) dv[v] = lv[v];
+        const int t = (nvec << 2) + lane;
+        if (t < nfloat) dst[t] = lds[t];
+    } else {
+        for (int f = lane; f < nfloat; f += 64) dst[f] = lds[f];
     }
-    const int tail0 = head + 4 * nvec;
-    if (tail0 + lane < nfloat) dst[tail0 + lane] = lds[tail0 + lane];
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -577,9 +597,12 @@ __device__ __forceinline__ Rng load_rng(const Bufs& b, uint32_t seed) {
     return r;
 }
 
+// Relaxed is enough: every block consumed its counter value (data dependency) long before it
+// arrives, and the next launch is ordered by the kernel boundary.  (An acq_rel atomic here would
+// emit an L2 write-back per block on gfx950: several microseconds on every wave's critical path.)
 __device__ __forceinline__ void advance_ctr(const Bufs& b) {
     if (threadIdx.x == 0) {
-        const uint32_t prev = __hip_atomic_fetch_add(b.arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t prev = __hip_atomic_fetch_add(b.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (prev == gridDim.x - 1) {
             __hip_atomic_store(b.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_fetch_add(b.ctr, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -588,8 +611,9 @@ __device__ __forceinline__ void advance_ctr(const Bufs& b) {
 }
 
 template <int NPAD>
-__global__ __launch_bounds__(64) void step_kernel(KP kp, Bufs b, uint32_t seed) {
+__global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bufs b, uint32_t seed) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
+    const KP& kp = *kpp;
     const Rng rng = load_rng(b, seed);
     constexpr int EPB = 64 / NPAD;
     const int lane = threadIdx.x;
@@ -603,6 +627,7 @@ __global__ __launch_bounds__(64) void step_kernel(KP kp, Bufs b, uint32_t seed) 
     const int nenv_blk = min(EPB, kp.E - env0);
     const int rows = nenv_blk * kp.N;
     float* row = lds + (size_t)(el * kp.N + di) * kp.obs_dim;
+    float4* xch = reinterpret_cast<float4*>(lds + 64 * kp.obs_dim);
 
     Drone d;
     load_drone(kp, b, g, d);
@@ -628,23 +653,24 @@ __global__ __launch_bounds__(64) void step_kernel(KP kp, Bufs b, uint32_t seed) 
         // compute_reward_weighted (quadrotor_single.py:34-66)
         const float gx = d.goal[0] - d.pos[0], gy = d.goal[1] - d.pos[1], gz = d.goal[2] - d.pos[2];
         const bool on_floor = d.flags & QS_FL_ON_FLOOR;
-        const float cost = kp.rew_pos * sqrtf(gx * gx + gy * gy + gz * gz) +
-                           kp.rew_effort * sqrtf(a[0] * a[0] + a[1] * a[1] + a[2] * a[2] + a[3] * a[3]) +
+        const float cost = kp.rew_pos * fsqrt(gx * gx + gy * gy + gz * gz) +
+                           kp.rew_effort * fsqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2] + a[3] * a[3]) +
                            kp.rew_crash * (on_floor ? 1.f : 0.f) + kp.rew_orient * (on_floor ? 1.f : -d.rot[8]) +
-                           kp.rew_spin * sqrtf(d.om[0] * d.om[0] + d.om[1] * d.om[1] + d.om[2] * d.om[2]);
+                           kp.rew_spin * fsqrt(d.om[0] * d.om[0] + d.om[1] * d.om[1] + d.om[2] * d.om[2]);
         rw = -kp.dt * cost;
     }
 
     // ---- swarm phase: collisions + proximity (quadrotor_multi.py:537-568, 608-622) ----
     uint64_t cur = 0;
     float pen = 0.f;
+    xch_put(xch, lane, d.pos, d.vel);
+    lds_sync();
     if (kp.N > 1) {
 #pragma unroll
         for (int j = 0; j < NPAD; ++j) {
-            const float dx = d.pos[0] - __shfl(d.pos[0], base + j);
-            const float dy = d.pos[1] - __shfl(d.pos[1], base + j);
-            const float dz = d.pos[2] - __shfl(d.pos[2], base + j);
-            const float dist = sqrtf(dx * dx + dy * dy + dz * dz);
+            const float4 pj = xch[2 * (base + j)];
+            const float dx = d.pos[0] - pj.x, dy = d.pos[1] - pj.y, dz = d.pos[2] - pj.z;
+            const float dist = fsqrt(dx * dx + dy * dy + dz * dz);
             if (j != di && j < kp.N) {
                 if (dist <= kp.col_thr) cur |= 1ull << j;
                 if (dist <= kp.fall_thr) pen += kp.prox_ratio * dist + kp.prox_max;
@@ -666,6 +692,7 @@ __global__ __launch_bounds__(64) void step_kernel(KP kp, Bufs b, uint32_t seed) 
               (ceil_new ? QS_FL_PREV_CEIL : 0u);
 
     // ---- random forces (:659-698) ----
+    bool vchanged = false;
     if (kp.downwash && kp.N > 1) {  // perform_downwash (aerodynamics/downwash.py:4-51)
         float dwu[4];
         uniforms4(rng, gid, S_DW, 0, dwu);
@@ -677,9 +704,9 @@ __global__ __launch_bounds__(64) void step_kernel(KP kp, Bufs b, uint32_t seed) 
             const float ani = __shfl(an, base + i), wni = __shfl(wn, base + i);
             if (!active || i >= kp.N || i == di) continue;
             const float r0 = P0 - pi0, r1 = P1 - pi1, r2 = P2 - pi2;
-            const float dist = sqrtf(r0 * r0 + r1 * r1 + r2 * r2);
+            const float dist = fsqrt(r0 * r0 + r1 * r1 + r2 * r2);
             const float rz = r0 * zi0 + r1 * zi1 + r2 * zi2;
-            const float rxy = sqrtf(dist * dist - rz * rz);
+            const float rxy = fsqrt(dist * dist - rz * rz);
             if (-0.7f < rz && rz < 0.f && rxy < 0.1f) {
                 const float acc = fmaxf((6.f / 17.f) * (-10.f * dist + 7.f) + ani, 1e-6f);
                 const float wd = fmaxf(0.3f * (dist - 1.f) * (dist - 1.f) + wni, 1e-6f);
@@ -688,16 +715,17 @@ __global__ __launch_bounds__(64) void step_kernel(KP kp, Bufs b, uint32_t seed) 
                 uniforms4(rng, gi, S_DWPAIR | ((uint32_t)di << 8), 0, u);
                 uniforms4(rng, gi, S_DWPAIR | ((uint32_t)di << 8), 1, u + 4);
                 float nz[3] = {zi0 - 0.1f + 0.2f * u[0], zi1 - 0.1f + 0.2f * u[1], zi2 - 0.1f + 0.2f * u[2]};
-                const float nm = sqrtf(nz[0] * nz[0] + nz[1] * nz[1] + nz[2] * nz[2]);
-                const float inz = 1.0f / (nm == 0.f ? 1e-6f : nm);
+                const float nm = fsqrt(nz[0] * nz[0] + nz[1] * nz[1] + nz[2] * nz[2]);
+                const float inz = frcp(nm == 0.f ? 1e-6f : nm);
                 float dw[3] = {-1.f + 2.f * u[3], -1.f + 2.f * u[4], -1.f + 2.f * u[5]};
-                const float dm = sqrtf(dw[0] * dw[0] + dw[1] * dw[1] + dw[2] * dw[2]);
-                const float idw = 1.0f / (dm == 0.f ? 1e-6f : dm);
+                const float dm = fsqrt(dw[0] * dw[0] + dw[1] * dw[1] + dw[2] * dw[2]);
+                const float idw = frcp(dm == 0.f ? 1e-6f : dm);
 #pragma unroll
                 for (int c = 0; c < 3; ++c) {
                     d.vel[c] += acc * (-(nz[c] * inz)) * kp.cdt;
                     d.om[c] += wd * (dw[c] * idw) * kp.cdt;
                 }
+                vchanged = true;
             }
         }
     }
@@ -720,6 +748,7 @@ __global__ __launch_bounds__(64) void step_kernel(KP kp, Bufs b, uint32_t seed) 
                 pw[c] = __shfl(d.om[c], base + partner);
             }
             const bool involved = eb != 0 && (di == istar || di == jstar);
+            vchanged |= involved;
             if (involved) {
                 const uint32_t gi = kp.id0 + (uint32_t)(env * kp.N + istar);
                 if (di == istar) collide_pair(d.pos, d.vel, d.om, pp, pv, pw, rng, gi, (uint32_t)jstar);
@@ -729,23 +758,30 @@ __global__ __launch_bounds__(64) void step_kernel(KP kp, Bufs b, uint32_t seed) 
         }
         if (active && wall_new) collide_room(kp, d, rng, gid, true);
         if (active && ceil_new) collide_room(kp, d, rng, gid, false);
+        vchanged |= active && (wall_new || ceil_new);
     }
     d.prev = cur;
 
     // ---- observations (post-impulse state; quadrotor_multi.py:704-720) ----
+    const bool nbr = kp.neighbor == QS_NEIGHBOR_POS_VEL && kp.K > 0;
+    if (nbr && __ballot(vchanged)) {  // impulses changed velocities: refresh the tile
+        lds_sync();
+        xch_put(xch, lane, d.pos, d.vel);
+        lds_sync();
+    }
     if (active) self_obs(kp, d, rng, gid, S_SENSOR, row);
-    if (kp.neighbor == QS_NEIGHBOR_POS_VEL && kp.K > 0) neighbor_obs<NPAD>(kp, base, di, d.pos, d.vel, active, row);
+    if (nbr) neighbor_obs<NPAD>(kp, xch, base, di, d.pos, d.vel, active, row);
 
     const uint64_t dball = __ballot(active && done);
     if (dball) {  // rare: some env of this block finished -> terminal obs + fused auto-reset (:739-838)
-        __syncthreads();
+        lds_sync();
         for (int r = 0; r < rows; ++r) {
             const int e = env0 + r / kp.N;
             if (b.env[QS_E_TICK * kp.E + e] + 1 <= kp.ep_len) continue;
             for (int c = lane; c < kp.obs_dim; c += 64)
                 b.term[(size_t)(env0 * kp.N + r) * kp.obs_dim + c] = lds[(size_t)r * kp.obs_dim + c];
         }
-        __syncthreads();
+        lds_sync();
         float sv[3] = {d.vel[0], d.vel[1], d.vel[2]};  // QuadrotorEnvMulti.vel seen by the reset (:477)
         if (active && done) {
             b.stale[0 * kp.I + g] = sv[0];
@@ -754,9 +790,13 @@ __global__ __launch_bounds__(64) void step_kernel(KP kp, Bufs b, uint32_t seed) 
             reset_drone(kp, d, rng, gid);
             self_obs(kp, d, rng, gid, S_RESET_SENSOR, row);
         }
-        if (kp.neighbor == QS_NEIGHBOR_POS_VEL && kp.K > 0) neighbor_obs<NPAD>(kp, base, di, d.pos, sv, active && done, row);
+        if (nbr) {
+            xch_put(xch, lane, d.pos, sv);
+            lds_sync();
+            neighbor_obs<NPAD>(kp, xch, base, di, d.pos, sv, active && done, row);
+        }
     }
-    __syncthreads();
+    lds_sync();
     tile_store(lds, b.obs + (size_t)env0 * kp.N * kp.obs_dim, rows * kp.obs_dim, lane);
 
     if (active) {
@@ -775,8 +815,9 @@ __global__ __launch_bounds__(64) void step_kernel(KP kp, Bufs b, uint32_t seed) 
 
 // explicit reset of masked envs (QuadrotorEnvMulti.reset quadrotor_multi.py:440-517)
 template <int NPAD>
-__global__ __launch_bounds__(64) void reset_kernel(KP kp, Bufs b, uint32_t seed) {
+__global__ __launch_bounds__(64) void reset_kernel(const KP* __restrict__ kpp, Bufs b, uint32_t seed) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
+    const KP& kp = *kpp;
     const Rng rng = load_rng(b, seed);
     constexpr int EPB = 64 / NPAD;
     const int lane = threadIdx.x;
@@ -799,8 +840,13 @@ __global__ __launch_bounds__(64) void reset_kernel(KP kp, Bufs b, uint32_t seed)
         reset_drone(kp, d, rng, kp.id0 + (uint32_t)g);
         self_obs(kp, d, rng, kp.id0 + (uint32_t)g, S_RESET_SENSOR, row);
     }
-    if (kp.neighbor == QS_NEIGHBOR_POS_VEL && kp.K > 0) neighbor_obs<NPAD>(kp, base, di, d.pos, sv, sel, row);
-    __syncthreads();
+    if (kp.neighbor == QS_NEIGHBOR_POS_VEL && kp.K > 0) {
+        float4* xch = reinterpret_cast<float4*>(lds + 64 * kp.obs_dim);
+        xch_put(xch, lane, d.pos, sv);
+        lds_sync();
+        neighbor_obs<NPAD>(kp, xch, base, di, d.pos, sv, sel, row);
+    }
+    lds_sync();
     const int nenv_blk = min(EPB, kp.E - env0);
     for (int r = 0; r < nenv_blk * kp.N; ++r) {
         const int e = env0 + r / kp.N;
@@ -888,6 +934,7 @@ static qs_layout make_layout(const qs_config* c) {
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     size_t o = 0;
     L.counter = o; o = al(o + 16);
+    L.params = o; o = al(o + sizeof(qs::KP));
     L.state = o; o = al(o + sizeof(float) * QS_NF * I);
     L.istate = o; o = al(o + sizeof(int32_t) * QS_NI * I);
     L.env = o; o = al(o + sizeof(int32_t) * QS_NE * (size_t)c->num_envs);
@@ -1023,10 +1070,11 @@ extern "C" int qs_create(const qs_config* c, int dev, void* ws, qs_handle** out)
         h->owns_ws = true;
     }
     hipError_t e = hipMemset(h->ws, 0, h->lay.total_bytes);
+    if (e == hipSuccess) e = hipMemcpy((char*)h->ws + h->lay.params, &h->kp, sizeof(qs::KP), hipMemcpyHostToDevice);
     if (e != hipSuccess) {
         if (h->owns_ws) (void)hipFree(h->ws);
         delete h;
-        return fail(QS_E_HIP, std::string("hipMemset: ") + hipGetErrorString(e));
+        return fail(QS_E_HIP, std::string("workspace init: ") + hipGetErrorString(e));
     }
     *out = h;
     return QS_OK;
@@ -1075,13 +1123,14 @@ static int launch(qs_handle* h, bool step, const float* act, const uint8_t* mask
     b.act = act;
     b.mask = mask;
     const uint32_t seed = h->cfg.seed;
+    const qs::KP* kpd = (const qs::KP*)((char*)h->ws + h->lay.params);
     const int epb = 64 / h->npad;
     const dim3 grid((unsigned)((h->kp.E + epb - 1) / epb)), block(64);
-    const size_t shm = sizeof(float) * 64 * (size_t)h->kp.obs_dim;
+    const size_t shm = sizeof(float) * 64 * (size_t)h->kp.obs_dim + sizeof(float) * 64 * 8;  // obs tile + exchange
 #define QS_LAUNCH(NP)                                                                                           \
     case NP:                                                                                                   \
-        if (step) hipLaunchKernelGGL(qs::step_kernel<NP>, grid, block, shm, s, h->kp, b, seed);                \
-        else hipLaunchKernelGGL(qs::reset_kernel<NP>, grid, block, shm, s, h->kp, b, seed);                    \
+        if (step) hipLaunchKernelGGL(qs::step_kernel<NP>, grid, block, shm, s, kpd, b, seed);                  \
+        else hipLaunchKernelGGL(qs::reset_kernel<NP>, grid, block, shm, s, kpd, b, seed);                      \
         break;
     switch (h->npad) {
         QS_LAUNCH(1)
@@ -1138,16 +1187,25 @@ static float* param_slot(qs_handle* h, const char* key) {
     return nullptr;
 }
 
+static int upload_params(qs_handle* h) {
+    QS_HIP(hipSetDevice(h->device));
+    QS_HIP(hipDeviceSynchronize());   // launches in flight read the old block
+    QS_HIP(hipMemcpy((char*)h->ws + h->lay.params, &h->kp, sizeof(qs::KP), hipMemcpyHostToDevice));
+    return QS_OK;
+}
+
+// Parameters live in device memory (read by every launch), so a change also reaches launches that
+// are replayed from a captured hipGraph.
 extern "C" int qs_set_param(qs_handle* h, const char* key, double v) {
     if (!h || !key) return fail(QS_E_INVALID, "NULL argument");
-    if (strcmp(key, "ep_len") == 0) { h->kp.ep_len = (int)v; h->cfg.ep_len = (int)v; return QS_OK; }
+    if (strcmp(key, "ep_len") == 0) { h->kp.ep_len = (int)v; h->cfg.ep_len = (int)v; return upload_params(h); }
     if (strcmp(key, "seed") == 0) { h->cfg.seed = (uint32_t)v; return QS_OK; }
     float* p = param_slot(h, key);
     if (!p) return fail(QS_E_INVALID, std::string("unknown param ") + key);
     *p = (float)v;
     if (strcmp(key, "quadcol_bin_smooth_max") == 0)
         h->kp.prox_ratio = h->kp.fall_thr > 0.f ? -h->kp.prox_max / h->kp.fall_thr : 0.f;
-    return QS_OK;
+    return upload_params(h);
 }
 
 extern "C" int qs_get_param(qs_handle* h, const char* key, double* v) {

@@ -45,7 +45,7 @@ class QsConfig(ctypes.Structure):
 
 
 class QsLayout(ctypes.Structure):
-    _fields_ = [("counter", SZ), ("state", SZ), ("istate", SZ), ("env", SZ), ("stale_vel", SZ), ("obs", SZ), ("term_obs", SZ),
+    _fields_ = [("counter", SZ), ("params", SZ), ("state", SZ), ("istate", SZ), ("env", SZ), ("stale_vel", SZ), ("obs", SZ), ("term_obs", SZ),
                 ("rew", SZ), ("done", SZ), ("total_bytes", SZ), ("obs_dim", I32), ("num_drones", I32)]
 
 
