@@ -100,10 +100,11 @@ enum qs_drone_flags {
     QS_FL_ON_FLOOR = 1, QS_FL_PREV_WALL = 2, QS_FL_PREV_CEIL = 4,
     QS_FL_CRASH_FLOOR = 8, QS_FL_CRASH_WALL = 16, QS_FL_CRASH_CEIL = 32
 };
-enum qs_env_field { QS_E_TICK = 0, QS_E_FLAGS = 1, QS_NE = 2 };
+/* per env: tick, flags (bit0: stale_vel holds QuadrotorEnvMulti.vel since the last reset), episode.
+ * {tick, episode} is the env's Philox counter: every step and reset of an env draws a fresh stream. */
+enum qs_env_field { QS_E_TICK = 0, QS_E_FLAGS = 1, QS_E_EPISODE = 2, QS_NE = 3 };
 
 typedef struct qs_layout {          /* byte offsets inside one workspace allocation */
-    size_t counter;                 /* uint64 RNG counter + uint32 block-arrival word (device-advanced) */
     size_t params;                  /* kernel parameter block (device copy of the config + runtime params) */
     size_t state, istate, env, stale_vel, obs, term_obs, rew, done, total_bytes;
     int32_t obs_dim, num_drones;
@@ -144,18 +145,12 @@ int qs_reset(qs_handle* h, const uint8_t* d_env_mask, void* stream);
  * observation goes to term_obs and obs holds the reset observation (SubprocVecEnvCustom semantics). */
 int qs_step(qs_handle* h, const float* d_actions, void* stream);
 
-/* RNG counter (Philox counter words 2-3), kept in device memory and bumped on the device by every
- * qs_step / qs_reset launch, so a captured hipGraph of K steps draws K distinct random streams.
- * get/set synchronise the device. */
-int qs_counter_get(qs_handle* h, uint64_t* ctr);
-int qs_counter_set(qs_handle* h, uint64_t ctr);
-
 /* Runtime-tunable scalars: "rew_pos", "rew_effort", "rew_crash", "rew_orient", "rew_spin",
  * "quadcol_bin", "quadcol_bin_smooth_max", "ep_len", "seed". */
 int qs_set_param(qs_handle* h, const char* key, double value);
 int qs_get_param(qs_handle* h, const char* key, double* value);
 
-/* Host snapshot of the whole env state (state, istate, env, stale_vel + counter): bytes =
+/* Host snapshot of the whole env state (state, istate, env incl. RNG counters, stale_vel): bytes =
  * qs_state_bytes(); round-trips exactly through qs_set_state. Synchronises the stream. */
 size_t qs_state_bytes(qs_handle* h);
 int qs_get_state(qs_handle* h, void* host_dst, size_t bytes, void* stream);

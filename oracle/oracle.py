@@ -50,7 +50,7 @@ class OrDrone(ctypes.Structure):
 
 
 class OrEnv(ctypes.Structure):
-    _fields_ = [("tick", I), ("prev_pair_bits", ctypes.c_ubyte * (64 * 64)),
+    _fields_ = [("tick", I), ("episode", ctypes.c_uint32), ("prev_pair_bits", ctypes.c_ubyte * (64 * 64)),
                 ("obs_pos", (D * 3) * 64), ("obs_vel", (D * 3) * 64)]
 
 
@@ -92,8 +92,8 @@ def lib():
         L.or_env_reset.argtypes = [P(OrParams), P(OrDrone), P(OrEnv), I, P(OrRng), P(D)]
         L.or_env_step.argtypes = [P(OrParams), P(OrDrone), P(OrEnv), I, P(D), P(OrRng), P(D), P(D),
                                   P(ctypes.c_ubyte), P(D)]
-        L.or_reset_all.argtypes = [P(OrParams), P(OrDrone), P(OrEnv), ctypes.c_uint32, ctypes.c_uint64, P(D)]
-        L.or_step_all.argtypes = [P(OrParams), P(OrDrone), P(OrEnv), P(D), ctypes.c_uint32, ctypes.c_uint64,
+        L.or_reset_all.argtypes = [P(OrParams), P(OrDrone), P(OrEnv), ctypes.c_uint32, P(D)]
+        L.or_step_all.argtypes = [P(OrParams), P(OrDrone), P(OrEnv), P(D), ctypes.c_uint32,
                                   P(D), P(D), P(ctypes.c_ubyte), P(D), I]
         L.or_neighbor_obs.argtypes = [P(OrParams), P(OrEnv), P(D), I]
         L.or_philox4x32_10.argtypes = [P(ctypes.c_uint32), P(ctypes.c_uint32), P(ctypes.c_uint32)]
@@ -204,18 +204,16 @@ class OracleEnv:
         self.drones = drones_array(self.E * self.N)
         self.envs = envs_array(self.E)
         self.seed = seed
-        self.ctr = 0
 
     def reset(self, mask=None):
         obs = np.zeros((self.E * self.N, self.obs_dim))
         if mask is None:
-            lib().or_reset_all(ctypes.byref(self.p), self.drones, self.envs, self.seed, self.ctr, dptr(obs))
+            lib().or_reset_all(ctypes.byref(self.p), self.drones, self.envs, self.seed, dptr(obs))
         else:
-            r = philox_rng(self.seed, self.ctr)
+            r = philox_rng(self.seed, 0)
             for e in np.flatnonzero(mask):
                 rows = obs[e * self.N:(e + 1) * self.N]
                 lib().or_env_reset(ctypes.byref(self.p), self.drones, self.envs, int(e), ctypes.byref(r), dptr(rows))
-        self.ctr += 1
         return obs
 
     def step(self, actions, nthreads=0):
@@ -224,8 +222,7 @@ class OracleEnv:
         term = np.zeros_like(obs)
         rew = np.zeros(self.E * self.N)
         done = np.zeros(self.E * self.N, dtype=np.uint8)
-        lib().or_step_all(ctypes.byref(self.p), self.drones, self.envs, dptr(a), self.seed, self.ctr,
+        lib().or_step_all(ctypes.byref(self.p), self.drones, self.envs, dptr(a), self.seed,
                           dptr(obs), dptr(rew), done.ctypes.data_as(ctypes.POINTER(ctypes.c_ubyte)),
                           dptr(term), nthreads)
-        self.ctr += 1
         return obs, rew, done.astype(bool), term

@@ -607,6 +607,7 @@ static int downwash(const or_params* p, or_drone* dr, int N, uint32_t gbase, or_
 void or_env_reset(const or_params* p, or_drone* drones, or_env* envs, int e, or_rng* r, double* obs) {
     const int N = p->num_agents, od = or_obs_dim(p);
     or_env* ev = &envs[e];
+    r->step = ((uint64_t)ev->episode << 32) | (uint32_t)ev->tick;   /* env Philox counter */
     for (int i = 0; i < N; ++i) {
         or_drone* d = &drones[(size_t)e * N + i];
         uint32_t gid = (uint32_t)((size_t)e * N + i);
@@ -637,6 +638,7 @@ void or_env_reset(const or_params* p, or_drone* drones, or_env* envs, int e, or_
         for (int c = 0; c < 3; ++c) ev->obs_pos[i][c] = d->pos[c];
     }
     ev->tick = 0;
+    ev->episode += 1;
     memset(ev->prev_pair_bits, 0, sizeof ev->prev_pair_bits);
     neighbor_obs(p, ev, obs, od);   /* uses fresh obs_pos and the stale obs_vel (:477) */
 }
@@ -653,6 +655,7 @@ void or_env_step(const or_params* p, or_drone* drones, or_env* envs, int e, cons
     const double* act = actions + (size_t)e * N * 4;
     double* o = obs + (size_t)e * N * od;
     double* rw = rew + (size_t)e * N;
+    r->step = ((uint64_t)ev->episode << 32) | (uint32_t)ev->tick;   /* env Philox counter */
 
     for (int i = 0; i < N; ++i) {
         or_drone* d = &dr[i];
@@ -743,22 +746,23 @@ void or_env_step(const or_params* p, or_drone* drones, or_env* envs, int e, cons
     for (int i = 0; i < N; ++i) done[(size_t)e * N + i] = (unsigned char)is_done;
     if (is_done) {
         if (term_obs) memcpy(term_obs + (size_t)e * N * od, o, sizeof(double) * (size_t)N * od);
+        ev->tick -= 1;                              /* the reset draws at the step's counter */
         or_env_reset(p, drones, envs, e, r, o);     /* in-env auto reset (:836) */
     }
 }
 
-void or_reset_all(const or_params* p, or_drone* drones, or_env* envs, uint32_t seed, uint64_t step, double* obs) {
+void or_reset_all(const or_params* p, or_drone* drones, or_env* envs, uint32_t seed, double* obs) {
     const int od = or_obs_dim(p);
     for (int e = 0; e < p->num_envs; ++e) {
         or_rng r;
         memset(&r, 0, sizeof r);
-        r.mode = OR_RNG_PHILOX; r.seed = seed; r.step = step;
+        r.mode = OR_RNG_PHILOX; r.seed = seed;
         or_env_reset(p, drones, envs, e, &r, obs + (size_t)e * p->num_agents * od);
     }
 }
 
 void or_step_all(const or_params* p, or_drone* drones, or_env* envs, const double* actions, uint32_t seed,
-                 uint64_t step, double* obs, double* rew, unsigned char* done, double* term_obs, int nthreads) {
+                 double* obs, double* rew, unsigned char* done, double* term_obs, int nthreads) {
 #ifdef _OPENMP
     if (nthreads > 0) omp_set_num_threads(nthreads);
 #pragma omp parallel for schedule(static)
@@ -766,7 +770,7 @@ void or_step_all(const or_params* p, or_drone* drones, or_env* envs, const doubl
     for (int e = 0; e < p->num_envs; ++e) {
         or_rng r;
         memset(&r, 0, sizeof r);
-        r.mode = OR_RNG_PHILOX; r.seed = seed; r.step = step;
+        r.mode = OR_RNG_PHILOX; r.seed = seed;
         or_env_step(p, drones, envs, e, actions, &r, obs, rew, done, term_obs);
     }
     (void)nthreads;

@@ -8,7 +8,7 @@
  *
  * Random draws come from an or_rng:
  *   OR_RNG_PHILOX : counter-based Philox4x32-10, keyed exactly like the GPU kernel
- *                   (key = {drone global id, seed}, counter = {block, stream, step_lo, step_hi}),
+ *                   (key = {drone global id, seed}, counter = {block, stream, env tick, env episode}),
  *                   so GPU fp32 and oracle fp64 consume identical underlying draws.
  *   OR_RNG_TAPE   : replays values recorded from the reference's own np.random calls, in the
  *                   reference's call order (tools/gen_golden.py), so the oracle can be pinned
@@ -44,7 +44,7 @@ enum { OR_RNG_PHILOX = 0, OR_RNG_TAPE = 1 };
 typedef struct {
     int mode;
     uint32_t seed;
-    uint64_t step;          /* Philox counter words 2,3                       */
+    uint64_t step;          /* Philox counter words 2,3 = {tick, episode}; set per env by the env calls */
     /* tape mode */
     const double* tape;      /* np.random legacy draws (global stream)          */
     long tape_n, tape_pos;
@@ -93,6 +93,7 @@ typedef struct {
 
 typedef struct {
     int tick;
+    uint32_t episode;   /* resets so far; with tick it is the env's Philox counter {tick, episode} */
     unsigned char prev_pair_bits[64 * 64];  /* [i*64+j], i<j: pair collided at the previous step */
     double obs_pos[64][3], obs_vel[64][3];  /* QuadrotorEnvMulti.pos / .vel (neighbour obs) */
 } or_env;
@@ -124,10 +125,9 @@ void or_env_reset(const or_params* p, or_drone* drones, or_env* envs, int env_id
 void or_env_step(const or_params* p, or_drone* drones, or_env* envs, int env_idx, const double* actions,
                  or_rng* r, double* obs, double* rew, unsigned char* done, double* term_obs);
 /* batched helpers (Philox mode, OpenMP over envs) */
-void or_reset_all(const or_params* p, or_drone* drones, or_env* envs, uint32_t seed, uint64_t step,
-                  double* obs);
+void or_reset_all(const or_params* p, or_drone* drones, or_env* envs, uint32_t seed, double* obs);
 void or_step_all(const or_params* p, or_drone* drones, or_env* envs, const double* actions,
-                 uint32_t seed, uint64_t step, double* obs, double* rew, unsigned char* done,
+                 uint32_t seed, double* obs, double* rew, unsigned char* done,
                  double* term_obs, int nthreads);
 
 void or_neighbor_obs(const or_params* p, const or_env* ev, double* obs, int obs_dim);

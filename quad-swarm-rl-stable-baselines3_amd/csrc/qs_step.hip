@@ -42,8 +42,6 @@ struct KP {
 };
 
 struct Bufs {
-    uint64_t* ctr;      // RNG counter (Philox words 2-3), advanced on device by the last block
-    uint32_t* arrive;   // block arrival count of the current launch
     float* st;
     int32_t* ist;
     int32_t* env;
@@ -55,6 +53,30 @@ struct Bufs {
     const float* act;
     const uint8_t* mask;
 };
+
+// Diagnostic phase stamps (build with -DQS_STAMPS=1 only; never in the shipped library): lane 0 of
+// each block records s_memtime at phase boundaries; tools/phase_stamps.py reads them back.
+#ifdef QS_STAMPS
+__device__ uint64_t qs_dbg_stamps[65536 * 16];
+#define QS_STAMP(k)                                                                                   \
+    do {                                                                                              \
+        uint64_t t_;                                                                                  \
+        __builtin_amdgcn_sched_barrier(0);                                                            \
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+        __builtin_amdgcn_sched_barrier(0);                                                            \
+        stamps_[k] = t_;                                                                              \
+    } while (0)
+#define QS_STAMP_FLUSH()                                                                              \
+    do {                                                                                              \
+        if (threadIdx.x == 0 && blockIdx.x < 65536)                                                   \
+            for (int k_ = 0; k_ < 16; ++k_) qs_dbg_stamps[blockIdx.x * 16 + k_] = stamps_[k_];        \
+    } while (0)
+#define QS_STAMP_DECL uint64_t stamps_[16] = {0};
+#else
+#define QS_STAMP(k) do {} while (0)
+#define QS_STAMP_FLUSH() do {} while (0)
+#define QS_STAMP_DECL
+#endif
 
 struct Drone {
     float pos[3], vel[3], rot[9], om[3], rd[4], cd[4], ou[4], goal[3];
@@ -391,33 +413,53 @@ __device__ __forceinline__ void xch_put(float4* xch, int lane, const float* P, c
 template <int NPAD>
 __device__ void neighbor_obs(const KP& kp, const float4* xch, int base, int di, const float* P, const float* V,
                              bool write, float* out) {
+    constexpr bool KEEP = NPAD <= 8;  // small swarms keep the relative vectors in VGPRs between passes
     float key[NPAD];
+    float rel[KEEP ? NPAD : 1][6];
     const bool sorted = kp.K < kp.N - 1;
 #pragma unroll
     for (int j = 0; j < NPAD; ++j) {
         const float4 pj = xch[2 * (base + j)], vj = xch[2 * (base + j) + 1];
-        const float a0 = pj.x - P[0], a1 = pj.y - P[1], a2 = pj.z - P[2];
-        const float b0 = vj.x - V[0], b1 = vj.y - V[1], b2 = vj.z - V[2];
-        const float s = a0 * a0 + a1 * a1 + a2 * a2 + b0 * b0 + b1 * b1 + b2 * b2;
+        const float r[6] = {pj.x - P[0], pj.y - P[1], pj.z - P[2], vj.x - V[0], vj.y - V[1], vj.z - V[2]};
+        const float s = r[0] * r[0] + r[1] * r[1] + r[2] * r[2] + r[3] * r[3] + r[4] * r[4] + r[5] * r[5];
         const bool valid = (j != di) && (j < kp.N);
         key[j] = valid ? (sorted ? fmaxf(s, 1e-4f) : 0.f) : __builtin_inff();
+        if (KEEP) {
+#pragma unroll
+            for (int c = 0; c < 6; ++c) rel[KEEP ? j : 0][c] = r[c];
+        }
     }
     if (!write) return;
+    const float vm = 2.f * kp.vxyz_max;
+    const bool pairs = ((kp.so_dim | kp.obs_dim) & 1) == 0;   // 8-byte aligned slots: ds_write_b64
 #pragma unroll
     for (int j = 0; j < NPAD; ++j) {
         int rank = 0;
 #pragma unroll
         for (int m = 0; m < NPAD; ++m) rank += (key[m] < key[j]) || (m < j && key[m] == key[j]);
         if (key[j] != __builtin_inff() && rank < kp.K) {
-            const float4 pj = xch[2 * (base + j)], vj = xch[2 * (base + j) + 1];
+            float r[6];
+            if (KEEP) {
+#pragma unroll
+                for (int c = 0; c < 6; ++c) r[c] = rel[KEEP ? j : 0][c];
+            } else {
+                const float4 pj = xch[2 * (base + j)], vj = xch[2 * (base + j) + 1];
+                r[0] = pj.x - P[0]; r[1] = pj.y - P[1]; r[2] = pj.z - P[2];
+                r[3] = vj.x - V[0]; r[4] = vj.y - V[1]; r[5] = vj.z - V[2];
+            }
+            const float o0 = clampf(r[0], -kp.room_range[0], kp.room_range[0]);
+            const float o1 = clampf(r[1], -kp.room_range[1], kp.room_range[1]);
+            const float o2 = clampf(r[2], -kp.room_range[2], kp.room_range[2]);
+            const float o3 = clampf(r[3], -vm, vm), o4 = clampf(r[4], -vm, vm), o5 = clampf(r[5], -vm, vm);
             float* o = out + kp.so_dim + rank * 6;
-            o[0] = clampf(pj.x - P[0], -kp.room_range[0], kp.room_range[0]);
-            o[1] = clampf(pj.y - P[1], -kp.room_range[1], kp.room_range[1]);
-            o[2] = clampf(pj.z - P[2], -kp.room_range[2], kp.room_range[2]);
-            const float vm = 2.f * kp.vxyz_max;
-            o[3] = clampf(vj.x - V[0], -vm, vm);
-            o[4] = clampf(vj.y - V[1], -vm, vm);
-            o[5] = clampf(vj.z - V[2], -vm, vm);
+            if (pairs) {
+                float2* o2p = reinterpret_cast<float2*>(o);
+                o2p[0] = make_float2(o0, o1);
+                o2p[1] = make_float2(o2, o3);
+                o2p[2] = make_float2(o4, o5);
+            } else {
+                o[0] = o0; o[1] = o1; o[2] = o2; o[3] = o3; o[4] = o4; o[5] = o5;
+            }
         }
     }
 }
@@ -586,35 +628,23 @@ __device__ __forceinline__ void tile_store(const float* lds, float* dst, int nfl
 // ---------------------------------------------------------------------------------------------
 // the fused step kernel
 // ---------------------------------------------------------------------------------------------
-// Every block reads the counter at its start; the last block to finish bumps it.  The next launch
-// (stream order) sees the new value, so K steps captured in one hipGraph draw K distinct streams.
-__device__ __forceinline__ Rng load_rng(const Bufs& b, uint32_t seed) {
-    const uint64_t c = __hip_atomic_load(b.ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// Philox counter of an env = {tick, episode}: unique for every step and reset of that env, resident
+// with the env state (no global counter, no atomics), so a hipGraph replay of K steps draws K fresh
+// streams and sharding envs over GPUs does not change any draw.
+__device__ __forceinline__ Rng env_rng(uint32_t seed, int32_t tick, int32_t episode) {
     Rng r;
     r.seed = seed;
-    r.ctr_lo = (uint32_t)c;
-    r.ctr_hi = (uint32_t)(c >> 32);
+    r.ctr_lo = (uint32_t)tick;
+    r.ctr_hi = (uint32_t)episode;
     return r;
-}
-
-// Relaxed is enough: every block consumed its counter value (data dependency) long before it
-// arrives, and the next launch is ordered by the kernel boundary.  (An acq_rel atomic here would
-// emit an L2 write-back per block on gfx950: several microseconds on every wave's critical path.)
-__device__ __forceinline__ void advance_ctr(const Bufs& b) {
-    if (threadIdx.x == 0) {
-        const uint32_t prev = __hip_atomic_fetch_add(b.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (prev == gridDim.x - 1) {
-            __hip_atomic_store(b.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_fetch_add(b.ctr, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
 }
 
 template <int NPAD>
 __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bufs b, uint32_t seed) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const KP& kp = *kpp;
-    const Rng rng = load_rng(b, seed);
+    QS_STAMP_DECL
+    QS_STAMP(0);
     constexpr int EPB = 64 / NPAD;
     const int lane = threadIdx.x;
     const int el = lane / NPAD, di = lane % NPAD;
@@ -636,9 +666,14 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
         const float4 av = reinterpret_cast<const float4*>(b.act)[g];
         a[0] = av.x; a[1] = av.y; a[2] = av.z; a[3] = av.w;
     }
-    const int tick = b.env[QS_E_TICK * kp.E + (active ? env : 0)] + 1;
+    const int eidx = active ? env : 0;
+    const int tick0 = b.env[QS_E_TICK * kp.E + eidx];
+    const int episode = b.env[QS_E_EPISODE * kp.E + eidx];
+    const Rng rng = env_rng(seed, tick0, episode);
+    const int tick = tick0 + 1;
     const bool done = tick > kp.ep_len;
 
+    QS_STAMP(1);
     // ---- per-drone control + physics (QuadrotorSingle._step) ----
     float rw = 0.f;
     {
@@ -660,6 +695,7 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
         rw = -kp.dt * cost;
     }
 
+    QS_STAMP(2);
     // ---- swarm phase: collisions + proximity (quadrotor_multi.py:537-568, 608-622) ----
     uint64_t cur = 0;
     float pen = 0.f;
@@ -691,6 +727,7 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     d.flags = (d.flags & ~(uint32_t)(QS_FL_PREV_WALL | QS_FL_PREV_CEIL)) | (wall_new ? QS_FL_PREV_WALL : 0u) |
               (ceil_new ? QS_FL_PREV_CEIL : 0u);
 
+    QS_STAMP(3);
     // ---- random forces (:659-698) ----
     bool vchanged = false;
     if (kp.downwash && kp.N > 1) {  // perform_downwash (aerodynamics/downwash.py:4-51)
@@ -762,6 +799,7 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     }
     d.prev = cur;
 
+    QS_STAMP(4);
     // ---- observations (post-impulse state; quadrotor_multi.py:704-720) ----
     const bool nbr = kp.neighbor == QS_NEIGHBOR_POS_VEL && kp.K > 0;
     if (nbr && __ballot(vchanged)) {  // impulses changed velocities: refresh the tile
@@ -769,8 +807,11 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
         xch_put(xch, lane, d.pos, d.vel);
         lds_sync();
     }
+    QS_STAMP(5);
     if (active) self_obs(kp, d, rng, gid, S_SENSOR, row);
+    QS_STAMP(6);
     if (nbr) neighbor_obs<NPAD>(kp, xch, base, di, d.pos, d.vel, active, row);
+    QS_STAMP(7);
 
     const uint64_t dball = __ballot(active && done);
     if (dball) {  // rare: some env of this block finished -> terminal obs + fused auto-reset (:739-838)
@@ -797,7 +838,9 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
         }
     }
     lds_sync();
+    QS_STAMP(8);
     tile_store(lds, b.obs + (size_t)env0 * kp.N * kp.obs_dim, rows * kp.obs_dim, lane);
+    QS_STAMP(9);
 
     if (active) {
         store_drone(kp, b, g, d);
@@ -805,12 +848,15 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
         b.done[g] = done ? 1 : 0;
         if (di == 0) {
             b.env[QS_E_TICK * kp.E + env] = done ? 0 : tick;
+            if (done) b.env[QS_E_EPISODE * kp.E + env] = episode + 1;
             const int32_t ef = b.env[QS_E_FLAGS * kp.E + env];
             const int32_t nf = done ? (ef | 1) : (ef & ~1);
             if (nf != ef) b.env[QS_E_FLAGS * kp.E + env] = nf;
         }
     }
-    advance_ctr(b);
+    QS_STAMP(10);
+    QS_STAMP(11);
+    QS_STAMP_FLUSH();
 }
 
 // explicit reset of masked envs (QuadrotorEnvMulti.reset quadrotor_multi.py:440-517)
@@ -818,7 +864,6 @@ template <int NPAD>
 __global__ __launch_bounds__(64) void reset_kernel(const KP* __restrict__ kpp, Bufs b, uint32_t seed) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const KP& kp = *kpp;
-    const Rng rng = load_rng(b, seed);
     constexpr int EPB = 64 / NPAD;
     const int lane = threadIdx.x;
     const int el = lane / NPAD, di = lane % NPAD;
@@ -828,6 +873,9 @@ __global__ __launch_bounds__(64) void reset_kernel(const KP* __restrict__ kpp, B
     const bool sel = inr && (b.mask == nullptr || b.mask[env] != 0);
     const int g = inr ? env * kp.N + di : 0;
     const int base = el * NPAD;
+    const int eidx = inr ? env : 0;
+    const int episode = b.env[QS_E_EPISODE * kp.E + eidx];
+    const Rng rng = env_rng(seed, b.env[QS_E_TICK * kp.E + eidx], episode);
     float* row = lds + (size_t)(el * kp.N + di) * kp.obs_dim;
     Drone d;
     load_drone(kp, b, g, d);
@@ -861,10 +909,10 @@ __global__ __launch_bounds__(64) void reset_kernel(const KP* __restrict__ kpp, B
         b.done[g] = 0;
         if (di == 0) {
             b.env[QS_E_TICK * kp.E + env] = 0;
+            b.env[QS_E_EPISODE * kp.E + env] = episode + 1;
             b.env[QS_E_FLAGS * kp.E + env] |= 1;
         }
     }
-    advance_ctr(b);
 }
 
 }  // namespace qs
@@ -896,6 +944,12 @@ static int fail(int code, const std::string& msg) {
     } while (0)
 
 extern "C" int qs_abi_version(void) { return QS_ABI_VERSION; }
+
+#ifdef QS_STAMPS
+extern "C" int qs_debug_stamps(uint64_t* host, size_t n) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(qs::qs_dbg_stamps), n * sizeof(uint64_t)) == hipSuccess ? 0 : -3;
+}
+#endif
 extern "C" const char* qs_last_error(void) { return g_err.c_str(); }
 
 extern "C" int qs_struct_sizes(size_t* c, size_t* l, size_t* b) {
@@ -933,7 +987,6 @@ static qs_layout make_layout(const qs_config* c) {
     const int od = self_obs_dim(c->obs_repr) + (c->neighbor_obs == QS_NEIGHBOR_POS_VEL ? 6 * c->k_neighbors : 0);
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     size_t o = 0;
-    L.counter = o; o = al(o + 16);
     L.params = o; o = al(o + sizeof(qs::KP));
     L.state = o; o = al(o + sizeof(float) * QS_NF * I);
     L.istate = o; o = al(o + sizeof(int32_t) * QS_NI * I);
@@ -1095,8 +1148,6 @@ extern "C" int qs_destroy(qs_handle* h) {
 static qs::Bufs bufs_of(qs_handle* h) {
     char* w = (char*)h->ws;
     qs::Bufs b;
-    b.ctr = (uint64_t*)(w + h->lay.counter);
-    b.arrive = (uint32_t*)(w + h->lay.counter + 8);
     b.st = (float*)(w + h->lay.state);
     b.ist = (int32_t*)(w + h->lay.istate);
     b.env = (int32_t*)(w + h->lay.env);
@@ -1160,22 +1211,6 @@ extern "C" int qs_step(qs_handle* h, const float* d_actions, void* stream) {
     return launch(h, true, d_actions, nullptr, (hipStream_t)stream);
 }
 
-extern "C" int qs_counter_get(qs_handle* h, uint64_t* c) {
-    if (!h || !c) return fail(QS_E_INVALID, "NULL argument");
-    QS_HIP(hipSetDevice(h->device));
-    QS_HIP(hipDeviceSynchronize());
-    QS_HIP(hipMemcpy(c, (char*)h->ws + h->lay.counter, sizeof(uint64_t), hipMemcpyDeviceToHost));
-    return QS_OK;
-}
-
-extern "C" int qs_counter_set(qs_handle* h, uint64_t c) {
-    if (!h) return fail(QS_E_INVALID, "handle is NULL");
-    QS_HIP(hipSetDevice(h->device));
-    QS_HIP(hipDeviceSynchronize());
-    QS_HIP(hipMemcpy((char*)h->ws + h->lay.counter, &c, sizeof(uint64_t), hipMemcpyHostToDevice));
-    return QS_OK;
-}
-
 static float* param_slot(qs_handle* h, const char* key) {
     qs::KP& k = h->kp;
     struct { const char* n; float* p; } t[] = {
@@ -1218,17 +1253,18 @@ extern "C" int qs_get_param(qs_handle* h, const char* key, double* v) {
     return QS_OK;
 }
 
-// snapshot = the workspace from the counter slot up to (not including) the obs buffers
+// snapshot = the workspace from the state buffer up to (not including) the obs buffers; the env
+// block holds tick + episode, i.e. the RNG counters, so a restored env replays the same draws
 extern "C" size_t qs_state_bytes(qs_handle* h) {
     if (!h) return 0;
-    return h->lay.obs - h->lay.counter;
+    return h->lay.obs - h->lay.state;
 }
 
 extern "C" int qs_get_state(qs_handle* h, void* dst, size_t bytes, void* stream) {
     if (!h || !dst) return fail(QS_E_INVALID, "NULL argument");
     if (bytes < qs_state_bytes(h)) return fail(QS_E_INVALID, "buffer too small");
     QS_HIP(hipSetDevice(h->device));
-    QS_HIP(hipMemcpyAsync(dst, (char*)h->ws + h->lay.counter, qs_state_bytes(h), hipMemcpyDeviceToHost,
+    QS_HIP(hipMemcpyAsync(dst, (char*)h->ws + h->lay.state, qs_state_bytes(h), hipMemcpyDeviceToHost,
                           (hipStream_t)stream));
     QS_HIP(hipStreamSynchronize((hipStream_t)stream));
     return QS_OK;
@@ -1238,7 +1274,7 @@ extern "C" int qs_set_state(qs_handle* h, const void* src, size_t bytes, void* s
     if (!h || !src) return fail(QS_E_INVALID, "NULL argument");
     if (bytes < qs_state_bytes(h)) return fail(QS_E_INVALID, "buffer too small");
     QS_HIP(hipSetDevice(h->device));
-    QS_HIP(hipMemcpyAsync((char*)h->ws + h->lay.counter, src, qs_state_bytes(h), hipMemcpyHostToDevice,
+    QS_HIP(hipMemcpyAsync((char*)h->ws + h->lay.state, src, qs_state_bytes(h), hipMemcpyHostToDevice,
                           (hipStream_t)stream));
     QS_HIP(hipStreamSynchronize((hipStream_t)stream));
     return QS_OK;

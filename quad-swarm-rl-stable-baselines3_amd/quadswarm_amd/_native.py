@@ -20,7 +20,7 @@ NEIGHBOR_NONE, NEIGHBOR_POS_VEL = 0, 1
 F_POS, F_VEL, F_ROT, F_OMEGA, F_ROT_DAMP, F_CMD_DAMP, F_OU, F_GOAL, NF = 0, 3, 6, 15, 18, 22, 26, 30, 33
 I_SVD, I_FLAGS, I_PREV_LO, I_PREV_HI, NI = 0, 1, 2, 3, 4
 FL_ON_FLOOR, FL_PREV_WALL, FL_PREV_CEIL, FL_CRASH_FLOOR, FL_CRASH_WALL, FL_CRASH_CEIL = 1, 2, 4, 8, 16, 32
-E_TICK, E_FLAGS, NE = 0, 1, 2
+E_TICK, E_FLAGS, E_EPISODE, NE = 0, 1, 2, 3
 
 
 class QsConfig(ctypes.Structure):
@@ -45,7 +45,7 @@ class QsConfig(ctypes.Structure):
 
 
 class QsLayout(ctypes.Structure):
-    _fields_ = [("counter", SZ), ("params", SZ), ("state", SZ), ("istate", SZ), ("env", SZ), ("stale_vel", SZ), ("obs", SZ), ("term_obs", SZ),
+    _fields_ = [("params", SZ), ("state", SZ), ("istate", SZ), ("env", SZ), ("stale_vel", SZ), ("obs", SZ), ("term_obs", SZ),
                 ("rew", SZ), ("done", SZ), ("total_bytes", SZ), ("obs_dim", I32), ("num_drones", I32)]
 
 
@@ -59,7 +59,7 @@ class QuadSwarmError(RuntimeError):
 
 # every symbol include/quadswarm.h declares (tests check the library exports all of them)
 EXPORTS = ["qs_abi_version", "qs_last_error", "qs_struct_sizes", "qs_config_default", "qs_layout_query", "qs_create", "qs_destroy",
-           "qs_buffers_get", "qs_reset", "qs_step", "qs_counter_get", "qs_counter_set", "qs_set_param",
+           "qs_buffers_get", "qs_reset", "qs_step", "qs_set_param",
            "qs_get_param", "qs_state_bytes", "qs_get_state", "qs_set_state"]
 
 _lib = None
@@ -80,7 +80,6 @@ def lib():
         "qs_config_default": ([P(QsConfig), I32, I32], I32), "qs_layout_query": ([P(QsConfig), P(QsLayout)], I32),
         "qs_create": ([P(QsConfig), ctypes.c_int, V, P(V)], I32), "qs_destroy": ([V], I32),
         "qs_buffers_get": ([V, P(QsBuffers)], I32), "qs_reset": ([V, V, V], I32), "qs_step": ([V, V, V], I32),
-        "qs_counter_get": ([V, P(U64)], I32), "qs_counter_set": ([V, U64], I32),
         "qs_set_param": ([V, ctypes.c_char_p, ctypes.c_double], I32),
         "qs_get_param": ([V, ctypes.c_char_p, P(ctypes.c_double)], I32),
         "qs_state_bytes": ([V], SZ), "qs_get_state": ([V, V, SZ, V], I32), "qs_set_state": ([V, V, SZ, V], I32),

@@ -91,16 +91,6 @@ class QuadSwarmEnv:
         N.check(N.lib().qs_get_param(self._h, key.encode(), ctypes.byref(v)), "qs_get_param")
         return v.value
 
-    @property
-    def counter(self):
-        c = ctypes.c_uint64()
-        N.check(N.lib().qs_counter_get(self._h, ctypes.byref(c)), "qs_counter_get")
-        return c.value
-
-    @counter.setter
-    def counter(self, v):
-        N.check(N.lib().qs_counter_set(self._h, int(v)), "qs_counter_set")
-
     def get_state(self):
         """Host snapshot (bytes) of the full env state + RNG counter (checkpoint / replay)."""
         n = N.lib().qs_state_bytes(self._h)

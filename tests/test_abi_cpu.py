@@ -63,7 +63,7 @@ def test_layout(N_, K, repr_, od):
     lay = N.QsLayout()
     assert N.lib().qs_layout_query(cfg.to_qs_config(), lay) == 0
     assert lay.obs_dim == od and lay.num_drones == 100 * N_
-    offs = [lay.counter, lay.params, lay.state, lay.istate, lay.env, lay.stale_vel, lay.obs, lay.term_obs, lay.rew, lay.done]
+    offs = [lay.params, lay.state, lay.istate, lay.env, lay.stale_vel, lay.obs, lay.term_obs, lay.rew, lay.done]
     assert all(o % 256 == 0 for o in offs) and offs == sorted(offs)
     assert lay.obs - lay.state >= 4 * (N.NF + N.NI + 3) * 100 * N_
     assert lay.total_bytes >= lay.done + 100 * N_

@@ -29,6 +29,7 @@ for s in "$@"; do
       step prof_write 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof_write -o w --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu-baseline --graph 0
       step prof_sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INSTS_LDS -d gpurun_out/prof_sq -o s --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu-baseline --graph 0
       ;;
+    stamps) step stamps 300 python tools/phase_stamps.py ;;
     calib)
       export TMPDIR=/tmp
       step calib_fetch 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/calib_fetch -o cf --output-format csv -- ./tools/calib/fetch_calib
