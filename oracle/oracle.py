@@ -34,7 +34,7 @@ class OrParams(ctypes.Structure):
         ("rew_pos", D), ("rew_effort", D), ("rew_crash", D), ("rew_orient", D), ("rew_spin", D),
         ("rew_quadcol_bin", D), ("rew_quadcol_smooth_max", D),
         ("use_downwash", I), ("apply_collision_force", I),
-        ("spawn_box", D), ("goal", D * 3),
+        ("spawn_box", D), ("goal", D * 3), ("id_offset", ctypes.c_uint32),
     ]
 
 

@@ -610,7 +610,7 @@ void or_env_reset(const or_params* p, or_drone* drones, or_env* envs, int e, or_
     r->step = ((uint64_t)ev->episode << 32) | (uint32_t)ev->tick;   /* env Philox counter */
     for (int i = 0; i < N; ++i) {
         or_drone* d = &drones[(size_t)e * N + i];
-        uint32_t gid = (uint32_t)((size_t)e * N + i);
+        uint32_t gid = p->id_offset + (uint32_t)((size_t)e * N + i);
         for (int c = 0; c < 3; ++c) d->goal[c] = p->goal[c];
         double xyz[3];
         for (int c = 0; c < 3; ++c) {
@@ -651,7 +651,7 @@ void or_env_step(const or_params* p, or_drone* drones, or_env* envs, int e, cons
     const int N = p->num_agents, od = or_obs_dim(p);
     or_env* ev = &envs[e];
     or_drone* dr = &drones[(size_t)e * N];
-    const uint32_t gbase = (uint32_t)((size_t)e * N);
+    const uint32_t gbase = p->id_offset + (uint32_t)((size_t)e * N);
     const double* act = actions + (size_t)e * N * 4;
     double* o = obs + (size_t)e * N * od;
     double* rw = rew + (size_t)e * N;

@@ -78,6 +78,7 @@ typedef struct {
     int use_downwash, apply_collision_force;
     double spawn_box;          /* QuadrotorSingle.box = 2.0                           */
     double goal[3];            /* static_same_goal formation centre (0,0,2)            */
+    uint32_t id_offset;        /* global id of drone 0 (Philox key), for sharded runs    */
 } or_params;
 
 /* Per-drone state (QuadrotorDynamics attributes + QuadrotorSingle bookkeeping). */
