@@ -35,6 +35,16 @@ class OrParams(ctypes.Structure):
         ("rew_quadcol_bin", D), ("rew_quadcol_smooth_max", D),
         ("use_downwash", I), ("apply_collision_force", I),
         ("spawn_box", D), ("goal", D * 3), ("id_offset", ctypes.c_uint32),
+        # flavor A
+        ("flavor", I), ("obs_repr_a", I), ("nfeat", I), ("nfeat_dim", I), ("ticks_per_step", I),
+        ("scenario_a", I), ("nclip_lo", D * 8), ("nclip_hi", D * 8),
+        ("cam_size", D), ("cam_focal", D), ("cam_px_noise", D), ("cam_fov_deg", D), ("cam_res", D),
+        ("n_cameras", I), ("heading_rate", D), ("speed", D),
+        ("pid_kp", D * 10), ("pid_kd", D * 10), ("pid_ki", D * 10), ("pid_sat", D * 10), ("pid_aw", D * 10),
+        ("rate_out_scale", D), ("mixer", D * 16),
+        ("m_mass", D), ("m_g", D), ("m_kf", D), ("m_min_rpm", D), ("m_max_rpm", D), ("m_n_motors", I),
+        ("w_captor", D), ("w_helper", D), ("existence", D),
+        ("target_vmax", D), ("target_dt", D), ("arena_size", D), ("target_z", D),
     ]
 
 
@@ -46,12 +56,14 @@ class OrDrone(ctypes.Structure):
         ("on_floor", I), ("crashed_floor", I), ("crashed_wall", I), ("crashed_ceiling", I),
         ("prev_wall", I), ("prev_ceiling", I),
         ("goal", D * 3),
+        ("pid", D * 20), ("angle", D), ("ang_vel", D),
     ]
 
 
 class OrEnv(ctypes.Structure):
     _fields_ = [("tick", I), ("episode", ctypes.c_uint32), ("prev_pair_bits", ctypes.c_ubyte * (64 * 64)),
-                ("obs_pos", (D * 3) * 64), ("obs_vel", (D * 3) * 64)]
+                ("obs_pos", (D * 3) * 64), ("obs_vel", (D * 3) * 64),
+                ("heading", D * 64), ("target", D * 2), ("capture_radius", D), ("success", I), ("has_pos", I)]
 
 
 class OrRng(ctypes.Structure):
@@ -96,6 +108,23 @@ def lib():
         L.or_step_all.argtypes = [P(OrParams), P(OrDrone), P(OrEnv), P(D), ctypes.c_uint32,
                                   P(D), P(D), P(ctypes.c_ubyte), P(D), I]
         L.or_neighbor_obs.argtypes = [P(OrParams), P(OrEnv), P(D), I]
+        U8 = P(ctypes.c_ubyte)
+        L.or_params_default_a.argtypes = [P(OrParams)]
+        L.or_pid_update.argtypes = [D, P(D), P(D), D, D, D, D, D, D]
+        L.or_pid_update.restype = D
+        L.or_ctrl_a.argtypes = [P(OrParams), P(OrDrone), D, D, P(D)]
+        L.or_motors_to_cmds.argtypes = [P(D), P(D)]
+        L.or_camera.argtypes = [P(OrParams), D, D, D, D, D, P(D), P(D)]
+        L.or_self_obs_a.argtypes = [P(OrParams), P(OrDrone), P(OrRng), ctypes.c_uint32, ctypes.c_uint32,
+                                    ctypes.c_uint32, P(D)]
+        L.or_neighbor_obs_a.argtypes = [P(OrParams), P(OrEnv), P(OrDrone), P(OrRng), ctypes.c_uint32, I, P(D), I]
+        L.or_target_step.argtypes = [P(OrParams), P(OrEnv), P(OrDrone)]
+        L.or_env_reset_a.argtypes = [P(OrParams), P(OrDrone), P(OrEnv), I, P(OrRng), P(D), U8]
+        L.or_env_step_a.argtypes = [P(OrParams), P(OrDrone), P(OrEnv), I, P(D), P(OrRng), P(D), P(D), U8, P(D), U8]
+        L.or_reset_all_a.argtypes = [P(OrParams), P(OrDrone), P(OrEnv), ctypes.c_uint32, P(D), U8]
+        L.or_step_all_a.argtypes = [P(OrParams), P(OrDrone), P(OrEnv), P(D), ctypes.c_uint32, P(D), P(D), U8,
+                                    P(D), U8, I]
+        L.or_obs_dim_a.argtypes = [P(OrParams)]
         L.or_philox4x32_10.argtypes = [P(ctypes.c_uint32), P(ctypes.c_uint32), P(ctypes.c_uint32)]
         L.or_philox_normal.argtypes = [ctypes.c_uint32] * 3 + [ctypes.c_uint64, ctypes.c_uint32]
         L.or_philox_normal.restype = D
@@ -119,6 +148,58 @@ def default_params(**over):
     lib().or_params_default(ctypes.byref(p))
     for k, v in over.items():
         setattr(p, k, v)
+    return p
+
+
+# flavor-A neighbour types: feature mask (OR_NF_*), floats per neighbour, clip-box components
+NF = dict(dist=1, ndist=2, angle=4, sangle=8, nsangle=16, heading=32, sheading=64, npos=128, pos=256, vel=512)
+A_NTYPES = {
+    "dist_angle": ("dist angle", ["dist", "angle"]),
+    "dist_sangle": ("dist sangle", ["dist", "sangle"]),
+    "ndist_nsangle": ("ndist nsangle", ["dist", "sangle"]),
+    "dist_angle_heading": ("dist angle heading", ["dist", "angle", "angle"]),
+    "dist_sangle_sheading": ("dist sangle sheading", ["dist", "sangle", "sangle"]),
+    "pos": ("pos", ["rxyz"]),
+    "npos": ("npos", ["rxyz"]),
+    "pos_vel": ("pos vel", ["rxyz", "rvxyz"]),
+}
+A_REPRS = ["aw_awdot_dist_distdot_angle_angledot", "cdist_cdistdot_dist_distdot_angle_angledot",
+           "cdist_cdistdot_dist_distdot_sangle_angledot", "cdist_cdistdot_ndist_distdot_nsangle_angledot"]
+
+
+def a_neighbor_box(ntype, room):
+    """(mask, dim, lo[], hi[]) of a flavor-A neighbour type: the per-feature clip box is the float32
+    observation-space Box of quadrotor_single_rewards.make_observation_space (:267-319)."""
+    feats, comps = A_NTYPES[ntype]
+    mask = sum(NF[f] for f in feats.split())
+    rr = np.array(room, dtype=np.float64)
+    box = {"dist": ([-rr[0] / 2], [rr[0] / 2]), "angle": ([-np.pi], [np.pi]), "sangle": ([-1.0, -1.0], [1.0, 1.0]),
+           "rxyz": (list(-rr), list(rr)), "rvxyz": ([-6.0] * 3, [6.0] * 3)}
+    lo, hi = [], []
+    for c in comps:
+        lo += box[c][0]
+        hi += box[c][1]
+    lo = np.array(lo, dtype=np.float32).astype(np.float64)
+    hi = np.array(hi, dtype=np.float32).astype(np.float64)
+    return mask, len(lo), lo, hi
+
+
+def params_a(num_agents=4, num_envs=1, k=None, obs_repr="cdist_cdistdot_dist_distdot_sangle_angledot",
+             ntype="ndist_nsangle", room=(15.0, 15.0, 3.0), **over):
+    p = OrParams()
+    lib().or_params_default_a(ctypes.byref(p))
+    p.num_agents, p.num_envs = num_agents, num_envs
+    p.k_neighbors = (num_agents - 1) if k is None or k == -1 else k
+    p.obs_repr_a = A_REPRS.index(obs_repr)
+    mask, dim, lo, hi = a_neighbor_box(ntype, room)
+    p.nfeat, p.nfeat_dim = mask, dim
+    for i in range(dim):
+        p.nclip_lo[i], p.nclip_hi[i] = lo[i], hi[i]
+    for i in range(3):
+        p.room_lo[i] = -room[i] / 2 if i < 2 else 0.0
+        p.room_hi[i] = room[i] / 2 if i < 2 else room[2]
+    for kk, v in over.items():
+        setattr(p, kk, v)
     return p
 
 
@@ -226,3 +307,45 @@ class OracleEnv:
                           dptr(obs), dptr(rew), done.ctypes.data_as(ctypes.POINTER(ctypes.c_ubyte)),
                           dptr(term), nthreads)
         return obs, rew, done.astype(bool), term
+
+
+class OracleEnvA:
+    """Batched flavor-A env (quadrotor_multi_rewards) in Philox mode."""
+
+    def __init__(self, params, seed=0):
+        self.p = params
+        self.E, self.N = params.num_envs, params.num_agents
+        self.obs_dim = lib().or_obs_dim_a(ctypes.byref(params))
+        self.drones = drones_array(self.E * self.N)
+        self.envs = envs_array(self.E)
+        self.seed = seed
+
+    def set_capture_radius(self, r):
+        for e in range(self.E):
+            self.envs[e].capture_radius = float(r)
+
+    def reset(self, mask=None):
+        obs = np.zeros((self.E * self.N, self.obs_dim))
+        ri = np.zeros(self.E, dtype=np.uint8)
+        u8 = ri.ctypes.data_as(ctypes.POINTER(ctypes.c_ubyte))
+        if mask is None:
+            lib().or_reset_all_a(ctypes.byref(self.p), self.drones, self.envs, self.seed, dptr(obs), u8)
+        else:
+            for e in np.flatnonzero(mask):
+                r = philox_rng(self.seed, 0)
+                rows = obs[e * self.N:(e + 1) * self.N]
+                lib().or_env_reset_a(ctypes.byref(self.p), self.drones, self.envs, int(e), ctypes.byref(r),
+                                     dptr(rows), u8)
+        return obs, ri
+
+    def step(self, actions, nthreads=0):
+        a = np.ascontiguousarray(actions, dtype=np.float64).reshape(self.E * self.N, 2)
+        obs = np.zeros((self.E * self.N, self.obs_dim))
+        term = np.zeros_like(obs)
+        rew = np.zeros(self.E * self.N)
+        done = np.zeros(self.E * self.N, dtype=np.uint8)
+        ri = np.zeros(self.E, dtype=np.uint8)
+        lib().or_step_all_a(ctypes.byref(self.p), self.drones, self.envs, dptr(a), self.seed,
+                            dptr(obs), dptr(rew), done.ctypes.data_as(ctypes.POINTER(ctypes.c_ubyte)),
+                            dptr(term), ri.ctypes.data_as(ctypes.POINTER(ctypes.c_ubyte)), nthreads)
+        return obs, rew, done.astype(bool), term, ri

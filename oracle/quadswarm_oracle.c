@@ -86,6 +86,14 @@ static double ru(or_rng* r, uint32_t gid, uint32_t stream, uint32_t idx, double 
     return lo + (hi - lo) * or_philox_uniform(r->seed, gid, stream | OR_UNIF_BIT, r->step, idx);
 }
 
+double or_rn(or_rng* r, uint32_t gid, uint32_t stream, uint32_t idx, double loc, double scale) {
+    return rn(r, gid, stream, idx, loc, scale);
+}
+double or_ru(or_rng* r, uint32_t gid, uint32_t stream, uint32_t idx, double lo, double hi) {
+    return ru(r, gid, stream, idx, lo, hi);
+}
+double or_gnext(or_rng* r) { return spawn_next(r); }
+
 /* ------------------------------------------------------------------------------------------ */
 /* small linear algebra                                                                        */
 /* ------------------------------------------------------------------------------------------ */

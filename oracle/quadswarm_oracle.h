@@ -1,4 +1,4 @@
-/* quadswarm_oracle.h -- CPU restatement of the reference's flavor-B swarm env step.
+/* quadswarm_oracle.h -- CPU restatement of the reference's swarm env step (flavors B and A).
  *
  * TEST INFRASTRUCTURE ONLY.  This is the parity oracle (and the bench's cpu_baseline "port"
  * leg).  The product path (HIP kernels behind include/quadswarm.h) never links or calls it.
@@ -36,8 +36,27 @@ enum {
     OR_S_RESET_YAW = 10,  /* yaw rejection uniforms                           */
     OR_S_RESET_SENSOR = 11,
     OR_S_OBST = 12,
+    /* flavor A */
+    OR_S_CAM = 13,        /* neighbour camera pixel noise (obs pass): normals 0 (u1), 1 (u2); | j << 8 */
+    OR_S_CAM_SEL = 14,    /* same, neighbour-selection pass (k < N-1)          */
+    OR_S_SELF_CAM = 15,   /* ndist self obs: normals 0, 1                       */
+    OR_S_RESET_A = 16,    /* per drone: uniforms 0-1 spawn direction, 2 heading */
+    OR_S_SCEN = 17,       /* per env (key = drone 0): uniforms 0 spawn radius, 1-2 target dir, 3 target radius */
+    OR_S_RESET_CAM = 18,
+    OR_S_RESET_CAM_SEL = 19,
+    OR_S_RESET_SELF_CAM = 20,
     OR_UNIF_BIT = 0x80    /* uniform draws use stream | OR_UNIF_BIT           */
 };
+
+/* flavor-A neighbour features, in get_rel_pos_vel_item order (quadrotor_multi_rewards.py:326-420) */
+enum {
+    OR_NF_DIST = 1, OR_NF_NDIST = 2, OR_NF_ANGLE = 4, OR_NF_SANGLE = 8, OR_NF_NSANGLE = 16,
+    OR_NF_HEADING = 32, OR_NF_SHEADING = 64, OR_NF_NPOS = 128, OR_NF_POS = 256, OR_NF_VEL = 512
+};
+/* flavor-A self obs reprs (get_state.py:7-223) */
+enum { OR_OA_AW = 0, OR_OA_CDIST_ANGLE = 1, OR_OA_CDIST_SANGLE = 2, OR_OA_CDIST_NDIST_NSANGLE = 3 };
+/* flavor-A PIDs, state layout or_drone.pid[2*k] = last_error, [2*k+1] = integral */
+enum { OR_PID_POS_Z = 0, OR_PID_VEL = 1, OR_PID_ATT = 4, OR_PID_RATE = 7, OR_NPID = 10 };
 
 enum { OR_RNG_PHILOX = 0, OR_RNG_TAPE = 1 };
 
@@ -79,6 +98,25 @@ typedef struct {
     double spawn_box;          /* QuadrotorSingle.box = 2.0                           */
     double goal[3];            /* static_same_goal formation centre (0,0,2)            */
     uint32_t id_offset;        /* global id of drone 0 (Philox key), for sharded runs    */
+    /* ---- flavor A: quadrotor_multi_rewards.py / quadrotor_single_rewards.py / Controller/ ---- */
+    int flavor;                /* 0 = B (quadrotor_multi.py), 1 = A                     */
+    int obs_repr_a;            /* OR_OA_*                                                */
+    int nfeat;                 /* OR_NF_* mask of the neighbour obs type                 */
+    int nfeat_dim;             /* floats per visible neighbour                           */
+    int ticks_per_step;        /* 8 single-env ticks per QuadrotorEnvMulti.step (:636)    */
+    int scenario_a;            /* 0 = goals/spawns left as set (tests), 1 = dynamic_repulsive */
+    double nclip_lo[8], nclip_hi[8];   /* neighbour obs clip box per feature (float32 Box) */
+    double cam_size, cam_focal, cam_px_noise, cam_fov_deg, cam_res;
+    int n_cameras;
+    double heading_rate;       /* Controller.MAX_ANGULAR_RATE = pi*80/180                */
+    double speed;              /* fixed 0.2 m/s (Controller.py:88)                       */
+    double pid_kp[OR_NPID], pid_kd[OR_NPID], pid_ki[OR_NPID], pid_sat[OR_NPID], pid_aw[OR_NPID];
+    double rate_out_scale;     /* RateController output x800                             */
+    double mixer[16];          /* Mixer.allocation_matrix_inv, row-major 4x4             */
+    double m_mass, m_g, m_kf, m_min_rpm, m_max_rpm;
+    int m_n_motors;
+    double w_captor, w_helper, existence;
+    double target_vmax, target_dt, arena_size, target_z;
 } or_params;
 
 /* Per-drone state (QuadrotorDynamics attributes + QuadrotorSingle bookkeeping). */
@@ -90,6 +128,9 @@ typedef struct {
     int on_floor, crashed_floor, crashed_wall, crashed_ceiling;
     int prev_wall, prev_ceiling;   /* quadrotor_multi.py:604-605 (stores the NEW lists)   */
     double goal[3];
+    /* flavor A: Controller state (PIDs that reach an output, heading, last command) */
+    double pid[2 * OR_NPID];
+    double angle, ang_vel;
 } or_drone;
 
 typedef struct {
@@ -97,6 +138,12 @@ typedef struct {
     uint32_t episode;   /* resets so far; with tick it is the env's Philox counter {tick, episode} */
     unsigned char prev_pair_bits[64 * 64];  /* [i*64+j], i<j: pair collided at the previous step */
     double obs_pos[64][3], obs_vel[64][3];  /* QuadrotorEnvMulti.pos / .vel (neighbour obs) */
+    /* flavor A */
+    double heading[64];                      /* QuadrotorEnvMulti.heading (stale across resets) */
+    double target[2];                        /* Scenario_dynamic_repulsive.pos                  */
+    double capture_radius;
+    int success;                             /* episode_success                                 */
+    int has_pos;                             /* dynamics.pos exists (hasattr check, :38)        */
 } or_env;
 
 /* ---- low level pieces (exported for per-function golden tests) ---- */
@@ -132,6 +179,36 @@ void or_step_all(const or_params* p, or_drone* drones, or_env* envs, const doubl
                  double* term_obs, int nthreads);
 
 void or_neighbor_obs(const or_params* p, const or_env* ev, double* obs, int obs_dim);
+
+/* ---- flavor A (quadrotor_multi_rewards.QuadrotorEnvMulti) ---- */
+void or_params_default_a(or_params* p);     /* Controller/ModelParams constants, camera, rewards */
+double or_pid_update(double error, double* last_error, double* integral, double dt, double kp, double kd,
+                     double ki, double sat, double aw);
+void or_ctrl_a(const or_params* p, or_drone* d, double cmd0, double height, double motors[4]);
+void or_motors_to_cmds(const double motors[4], double u[4]);
+void or_camera(const or_params* p, double rx, double ry, double global_angle, double n1, double n2,
+               double* dist, double* angle);
+void or_self_obs_a(const or_params* p, const or_drone* d, or_rng* r, uint32_t gid, uint32_t st_sensor,
+                   uint32_t st_cam, double* out);
+void or_neighbor_obs_a(const or_params* p, const or_env* ev, const or_drone* dr, or_rng* r, uint32_t gbase,
+                       int reset, double* obs, int obs_dim);
+void or_target_step(const or_params* p, or_env* ev, or_drone* dr);
+void or_env_reset_a(const or_params* p, or_drone* drones, or_env* envs, int e, or_rng* r, double* obs,
+                    unsigned char* reset_info);
+void or_env_step_a(const or_params* p, or_drone* drones, or_env* envs, int e, const double* actions,
+                   or_rng* r, double* obs, double* rew, unsigned char* done, double* term_obs,
+                   unsigned char* reset_info);
+void or_reset_all_a(const or_params* p, or_drone* drones, or_env* envs, uint32_t seed, double* obs,
+                    unsigned char* reset_info);
+void or_step_all_a(const or_params* p, or_drone* drones, or_env* envs, const double* actions, uint32_t seed,
+                   double* obs, double* rew, unsigned char* done, double* term_obs, unsigned char* reset_info,
+                   int nthreads);
+int or_obs_dim_a(const or_params* p);
+
+/* internal draw helpers shared by the flavor files */
+double or_rn(or_rng* r, uint32_t gid, uint32_t stream, uint32_t idx, double loc, double scale);
+double or_ru(or_rng* r, uint32_t gid, uint32_t stream, uint32_t idx, double lo, double hi);
+double or_gnext(or_rng* r);   /* next Generator draw (tape mode: the "spawn"/gtape stream) */
 
 /* sizes for ctypes */
 int or_sizeof_params(void);
