@@ -1,12 +1,19 @@
 /* quadswarm.h -- C ABI of the MI355X-native quadrotor-swarm environment step (libquadswarm.so).
  *
  * Drop-in boundary for the reference's env-stepping path
- * (priban42/quad-swarm-rl-stable-baselines3):
+ * (priban42/quad-swarm-rl-stable-baselines3), two env flavors:
+ *   flavor B (raw motor control, shaped rewards):
  *   - qs_step   replaces QuadrotorEnvMulti.step        gym_art/quadrotor_multi/quadrotor_multi.py:521-841
  *               as driven per env by SubprocVecEnvCustom  swarm_rl/env_wrappers/subproc_vec_env_custom.py:141-153
  *               (worker loop :33-52: step, terminal_observation, auto-reset)
  *   - qs_reset  replaces QuadrotorEnvMulti.reset       quadrotor_multi.py:440-517
  *               (SubprocVecEnvCustom.reset :155-164)
+ *   flavor A (what swarm_rl/sb_train.py trains: PID pre-controller, pursuit of a repulsive target):
+ *   - qs_step   replaces quadrotor_multi_rewards.QuadrotorEnvMulti.step  quadrotor_multi_rewards.py:630-991
+ *               (8 QuadrotorSingle._step ticks, quadrotor_single_rewards.py:418-452, Controller/Controller.py:76-101)
+ *               plus the worker's reset on done (subproc_vec_env_custom.py:39-46) with reset_infos
+ *   - qs_reset  replaces quadrotor_multi_rewards.QuadrotorEnvMulti.reset   quadrotor_multi_rewards.py:541-627
+ *   - qs_set_param("capture_radius") replaces set_capture_radius         quadrotor_multi_rewards.py:212-213
  *   - qs_set_param replaces rew_coeff updates          swarm_rl/env_wrappers/reward_shaping.py:70-76,110-118
  *   - qs_get_state/qs_set_state: env snapshot/restore (no reference equivalent; checkpoint + parity)
  * The Python mirror of the reference's VecEnv surface (quadswarm_amd.vec_env.GpuQuadVecEnv) calls
@@ -27,7 +34,7 @@
 extern "C" {
 #endif
 
-#define QS_ABI_VERSION 1
+#define QS_ABI_VERSION 2
 #define QS_MAX_AGENTS 32            /* drones per env: one env lives inside one 64-lane wavefront */
 
 enum qs_status {
@@ -38,15 +45,36 @@ enum qs_status {
     QS_E_NOMEM = -4,
 };
 
+enum qs_flavor {
+    QS_FLAVOR_B = 0,                   /* quadrotor_multi.QuadrotorEnvMulti: 4 raw motor commands    */
+    QS_FLAVOR_A = 1,                   /* quadrotor_multi_rewards.QuadrotorEnvMulti: [heading rate, _] */
+};
+
 enum qs_obs_repr {                  /* quad_utils.py:30-38 (QUADS_OBS_REPR) */
-    QS_OBS_XYZ_VXYZ_R_OMEGA = 0,       /* 18 */
-    QS_OBS_XYZ_VXYZ_R_OMEGA_FLOOR = 1, /* 19 */
-    QS_OBS_XYZ_VXYZ_R_OMEGA_WALL = 2,  /* 24 */
+    QS_OBS_XYZ_VXYZ_R_OMEGA = 0,       /* 18, flavor B */
+    QS_OBS_XYZ_VXYZ_R_OMEGA_FLOOR = 1, /* 19, flavor B */
+    QS_OBS_XYZ_VXYZ_R_OMEGA_WALL = 2,  /* 24, flavor B */
+    QS_OBS_AW_AWDOT_DIST_DISTDOT_ANGLE_ANGLEDOT = 3,             /* 6, flavor A */
+    QS_OBS_CDIST_CDISTDOT_DIST_DISTDOT_ANGLE_ANGLEDOT = 4,       /* 6, flavor A */
+    QS_OBS_CDIST_CDISTDOT_DIST_DISTDOT_SANGLE_ANGLEDOT = 5,      /* 7, flavor A */
+    QS_OBS_CDIST_CDISTDOT_NDIST_DISTDOT_NSANGLE_ANGLEDOT = 6,    /* 7, flavor A (camera model) */
 };
 
 enum qs_neighbor_obs {              /* quad_utils.py:40-58 (QUADS_NEIGHBOR_OBS_TYPE) */
     QS_NEIGHBOR_NONE = 0,
-    QS_NEIGHBOR_POS_VEL = 1,           /* 6 per visible neighbour */
+    QS_NEIGHBOR_POS_VEL = 1,           /* 6 per visible neighbour (both flavors) */
+    QS_NEIGHBOR_DIST_ANGLE = 2,        /* 2, flavor A */
+    QS_NEIGHBOR_DIST_SANGLE = 3,       /* 3, flavor A */
+    QS_NEIGHBOR_NDIST_NSANGLE = 4,     /* 3, flavor A, camera model */
+    QS_NEIGHBOR_DIST_ANGLE_HEADING = 5,    /* 3, flavor A */
+    QS_NEIGHBOR_DIST_SANGLE_SHEADING = 6,  /* 5, flavor A */
+    QS_NEIGHBOR_POS = 7,               /* 3, flavor A */
+    QS_NEIGHBOR_NPOS = 8,              /* 3, flavor A (the reference discards its noise) */
+};
+
+enum qs_scenario {
+    QS_SCEN_STATIC_SAME_GOAL = 0,      /* scenarios/static_same_goal.py (flavor A: spawn at the goal)  */
+    QS_SCEN_DYNAMIC_REPULSIVE = 1,     /* scenarios/dynamic_repulsive.py, flavor A only (float-fixed)  */
 };
 
 /* Environment + physical configuration.  Physical constants are derived on the host exactly like
@@ -86,6 +114,13 @@ typedef struct qs_config {
     float rew_quadcol_bin, rew_quadcol_smooth_max;
     /* static_same_goal scenario */
     float spawn_box, goal[3];
+    /* ---- flavor A (ignored for flavor B) ---- */
+    int32_t flavor;                 /* enum qs_flavor */
+    int32_t scenario;               /* enum qs_scenario */
+    int32_t ticks_per_step;         /* QuadrotorSingle._step calls per env step (8, :636) */
+    int32_t n_cameras;              /* camera model (global_cfg.py:14-18) */
+    float capture_radius;           /* initial_capture_radius (global_cfg.py:37); per env at run time */
+    float cam_size, cam_focal, cam_px_noise, cam_fov_deg, cam_res;
 } qs_config;
 
 /* Device buffers of a handle.  State is structure-of-arrays: field f of drone g lives at
@@ -93,20 +128,33 @@ typedef struct qs_config {
  * [I, obs_dim] fp32 so a torch tensor can consume them zero-copy. */
 enum qs_state_field {
     QS_F_POS = 0, QS_F_VEL = 3, QS_F_ROT = 6, QS_F_OMEGA = 15, QS_F_ROT_DAMP = 18, QS_F_CMD_DAMP = 22,
-    QS_F_OU = 26, QS_F_GOAL = 30, QS_NF = 33
+    QS_F_OU = 26, QS_F_GOAL = 30,
+    /* flavor A: Controller PIDs as (last_error, integral) pairs in the order position z, velocity
+     * x y z, attitude x y z, rate x y z; heading angle and last heading-rate command; the
+     * QuadrotorEnvMulti.heading value a reset sees (stale, like stale_vel) */
+    QS_F_PID = 33, QS_F_ANGLE = 53, QS_F_ANGVEL = 54, QS_F_HEADING = 55,
+    QS_NF = 56
 };
 enum qs_istate_field { QS_I_SVD = 0, QS_I_FLAGS = 1, QS_I_PREV_LO = 2, QS_I_PREV_HI = 3, QS_NI = 4 };
 enum qs_drone_flags {
     QS_FL_ON_FLOOR = 1, QS_FL_PREV_WALL = 2, QS_FL_PREV_CEIL = 4,
     QS_FL_CRASH_FLOOR = 8, QS_FL_CRASH_WALL = 16, QS_FL_CRASH_CEIL = 32
 };
-/* per env: tick, flags (bit0: stale_vel holds QuadrotorEnvMulti.vel since the last reset), episode.
- * {tick, episode} is the env's Philox counter: every step and reset of an env draws a fresh stream. */
+/* per env: tick, flags, episode.  {tick, episode} is the env's Philox counter: every step and reset
+ * of an env draws a fresh stream.  Flavor A counts QuadrotorSingle ticks (8 per step). */
 enum qs_env_field { QS_E_TICK = 0, QS_E_FLAGS = 1, QS_E_EPISODE = 2, QS_NE = 3 };
+enum qs_env_flags {
+    QS_EF_STALE = 1,                /* stale_vel / QS_F_HEADING hold QuadrotorEnvMulti.vel / .heading */
+    QS_EF_SUCCESS = 2,              /* flavor A episode_success (a capture happened this episode)     */
+    QS_EF_HAS_POS = 4,              /* drones have been placed once (dynamic_repulsive.py:38 hasattr) */
+};
+/* per env float state [QS_NENVF, E] (flavor A): target position of the dynamic_repulsive scenario and
+ * the env's capture radius (set_capture_radius acts per env, custom_callbacks.py:455-462) */
+enum qs_env_ffield { QS_ENVF_TARGET_X = 0, QS_ENVF_TARGET_Y = 1, QS_ENVF_CAPTURE = 2, QS_NENVF = 3 };
 
 typedef struct qs_layout {          /* byte offsets inside one workspace allocation */
     size_t params;                  /* kernel parameter block (device copy of the config + runtime params) */
-    size_t state, istate, env, stale_vel, obs, term_obs, rew, done, total_bytes;
+    size_t state, istate, env, env_f, stale_vel, obs, term_obs, rew, done, reset_info, total_bytes;
     int32_t obs_dim, num_drones;
 } qs_layout;
 
@@ -114,11 +162,13 @@ typedef struct qs_buffers {         /* device pointers (valid for the handle's l
     float* state;                   /* [QS_NF, I] */
     int32_t* istate;                /* [QS_NI, I] */
     int32_t* env;                   /* [QS_NE, E] */
+    float* env_f;                   /* [QS_NENVF, E] */
     float* stale_vel;               /* [3, I]  QuadrotorEnvMulti.vel as last seen by a reset */
     float* obs;                     /* [I, obs_dim] */
     float* term_obs;                /* [I, obs_dim] rows of envs that finished this step */
     float* rew;                     /* [I] */
     uint8_t* done;                  /* [I] */
+    uint8_t* reset_info;            /* [E] 0: no reset this call; 1: reset, {"success": False}; 2: True */
 } qs_buffers;
 
 typedef struct qs_handle qs_handle;
@@ -130,6 +180,9 @@ int qs_struct_sizes(size_t* config, size_t* layout, size_t* buffers);
 
 /* Crazyflie + flavor-B defaults (values of quad_models.py:1-42 via QuadLink, SF quad_utils.py). */
 int qs_config_default(qs_config* cfg, int32_t num_envs, int32_t num_agents);
+/* Flavor-A defaults as swarm_rl/sb_train.py trains (global_cfg.py, sb_train.py:111-139): dynamic_repulsive,
+ * cdist_cdistdot_dist_distdot_sangle_angledot, ndist_nsangle of all N-1 neighbours, pixel noise 0. */
+int qs_config_default_a(qs_config* cfg, int32_t num_envs, int32_t num_agents);
 int qs_layout_query(const qs_config* cfg, qs_layout* out);
 
 /* d_workspace: NULL -> the library allocates (and frees) layout.total_bytes on hip_device;
@@ -140,17 +193,20 @@ int qs_buffers_get(qs_handle* h, qs_buffers* out);
 
 /* Reset the envs whose byte in d_env_mask[E] is non-zero (NULL = all); writes obs rows of those envs. */
 int qs_reset(qs_handle* h, const uint8_t* d_env_mask, void* stream);
-/* One control step for every env: d_actions is [I, 4] fp32 raw policy output (clipped inside).
- * Writes obs, rew, done; envs with tick > ep_len are auto-reset in the same launch, their final
- * observation goes to term_obs and obs holds the reset observation (SubprocVecEnvCustom semantics). */
+/* One control step for every env.  d_actions: flavor B [I, 4] fp32 raw policy output (clipped
+ * inside, 16-byte aligned); flavor A [I, 2] fp32 (8-byte aligned, a[0] = heading rate, unclipped
+ * like the reference).  Writes obs, rew, done; envs that finished (tick > ep_len, or a capture in
+ * flavor A) are reset in the same launch, their final observation goes to term_obs, obs holds the
+ * reset observation and reset_info[e] says so (SubprocVecEnvCustom semantics). */
 int qs_step(qs_handle* h, const float* d_actions, void* stream);
 
 /* Runtime-tunable scalars: "rew_pos", "rew_effort", "rew_crash", "rew_orient", "rew_spin",
- * "quadcol_bin", "quadcol_bin_smooth_max", "ep_len", "seed". */
+ * "quadcol_bin", "quadcol_bin_smooth_max", "ep_len", "seed", "capture_radius" (flavor A, all envs;
+ * write buffers.env_f[QS_ENVF_CAPTURE * E + e] for one env). */
 int qs_set_param(qs_handle* h, const char* key, double value);
 int qs_get_param(qs_handle* h, const char* key, double* value);
 
-/* Host snapshot of the whole env state (state, istate, env incl. RNG counters, stale_vel): bytes =
+/* Host snapshot of the whole env state (state, istate, env incl. RNG counters, env_f, stale_vel): bytes =
  * qs_state_bytes(); round-trips exactly through qs_set_state. Synchronises the stream. */
 size_t qs_state_bytes(qs_handle* h);
 int qs_get_state(qs_handle* h, void* host_dst, size_t bytes, void* stream);

@@ -523,8 +523,12 @@ void or_env_reset_a(const or_params* p, or_drone* drones, or_env* envs, int e, o
         /* scenario.step() inside reset: the chasers are still at their pre-reset positions */
         or_target_step(p, ev, dr);
         for (int i = 0; i < N; ++i) { dr[i].pos[0] = sp[i][0]; dr[i].pos[1] = sp[i][1]; }
-    } else {
-        for (int i = 0; i < N; ++i) { dr[i].pos[0] = dr[i].goal[0]; dr[i].pos[1] = dr[i].goal[1]; }
+    } else {   /* static_same_goal: goals at the formation centre (size 0), spawn_points None -> spawn at the goal */
+        for (int i = 0; i < N; ++i) {
+            for (int c = 0; c < 3; ++c) dr[i].goal[c] = p->goal[c];
+            dr[i].pos[0] = dr[i].goal[0];
+            dr[i].pos[1] = dr[i].goal[1];
+        }
     }
     for (int i = 0; i < N; ++i) {
         or_drone* d = &dr[i];

@@ -1,0 +1,348 @@
+// qs_common.h -- device-side building blocks shared by the flavor-B and flavor-A step kernels:
+// kernel parameters, SoA state I/O, the QuadrotorDynamics substep (quadrotor_dynamics.py:355-656),
+// LDS staging helpers and the per-env Philox counter.  Included by qs_step.hip only.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "qs_rng.h"
+#include "quadswarm.h"
+
+namespace qs {
+
+// flavor-A neighbour features (get_rel_pos_vel_item, quadrotor_multi_rewards.py:326-420), in the
+// reference's concatenation order
+enum : int {
+    QS_NF_DIST = 1, QS_NF_NDIST = 2, QS_NF_ANGLE = 4, QS_NF_SANGLE = 8, QS_NF_NSANGLE = 16,
+    QS_NF_HEADING = 32, QS_NF_SHEADING = 64, QS_NF_NPOS = 128, QS_NF_POS = 256, QS_NF_VEL = 512
+};
+
+struct KP {
+    int E, N, I, obs_dim, so_dim, K, neighbor, obs_repr, ep_len, sim_steps, svd_every, sense, downwash, collide;
+    uint32_t id0;  // global id of drone 0 (RNG key offset)
+    float dt, cdt, mass, inv_mass, inertia[3], inv_inertia[3];
+    float thrust_max[4], torque_max[4], pc0[4], pc1[4], pc2[4], ccw[4];
+    float tau_up, tau_down, lin, arm, grav, omega_max, vel_damp, dq, vxyz_max;
+    float room_lo[3], room_hi[3], room_range[3];
+    float ou_mu, ou_theta, ou_sigma;
+    float pos_std, pos_unif, vel_std, vel_unif, gyro, quat_std, quat_unif;
+    float col_thr, fall_thr, prox_ratio, prox_max;
+    float rew_pos, rew_effort, rew_crash, rew_orient, rew_spin, quadcol;
+    float spawn_box, goal[3];
+    // ---- flavor A (quadrotor_multi_rewards + Controller/), host-derived in make_kp ----
+    int flavor, scenario, ticks, nfeat, nfd, n_cam;
+    float cam_r, cam_f, cam_px, cam_w, cam_res;      // marker radius, focal, pixel sigma, sensor width, px
+    float hrate;                                      // dt * MAX_ANGULAR_RATE (Controller.py:29,81)
+    float speed, inv_dt;
+    float pkp[10], pkd[10], pki[10], psat[10], paw[10];
+    float rate_scale, mix[16];
+    float m_mass_g, m_mass, m_kf4, m_min_rpm, m_inv_rpm;   // m*g, m, kf*n_motors, min rpm, 1/(max-min)
+    float w_captor, w_helper, existence;
+    float tgt_vmax, tgt_dt, arena, tgt_z;
+    float nclip_lo[8], nclip_hi[8];
+};
+
+struct Bufs {
+    float* st;
+    int32_t* ist;
+    int32_t* env;
+    float* envf;
+    float* stale;
+    float* obs;
+    float* term;
+    float* rew;
+    uint8_t* done;
+    uint8_t* rinfo;
+    const float* act;
+    const uint8_t* mask;
+};
+
+// Diagnostic phase stamps (build with -DQS_STAMPS=1 only; never in the shipped library): lane 0 of
+// each block records s_memtime at phase boundaries; tools/phase_stamps.py reads them back.
+#ifdef QS_STAMPS
+__device__ uint64_t qs_dbg_stamps[65536 * 16];
+#define QS_STAMP(k)                                                                                   \
+    do {                                                                                              \
+        uint64_t t_;                                                                                  \
+        __builtin_amdgcn_sched_barrier(0);                                                            \
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+        __builtin_amdgcn_sched_barrier(0);                                                            \
+        stamps_[k] = t_;                                                                              \
+    } while (0)
+#define QS_STAMP_FLUSH()                                                                              \
+    do {                                                                                              \
+        if (threadIdx.x == 0 && blockIdx.x < 65536)                                                   \
+            for (int k_ = 0; k_ < 16; ++k_) qs_dbg_stamps[blockIdx.x * 16 + k_] = stamps_[k_];        \
+    } while (0)
+#define QS_STAMP_DECL uint64_t stamps_[16] = {0};
+#else
+#define QS_STAMP(k) do {} while (0)
+#define QS_STAMP_FLUSH() do {} while (0)
+#define QS_STAMP_DECL
+#endif
+
+struct Drone {
+    float pos[3], vel[3], rot[9], om[3], rd[4], cd[4], ou[4], goal[3];
+    int32_t svd;
+    uint32_t flags;
+    uint64_t prev;
+};
+
+__device__ __forceinline__ float clampf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
+// single-instruction sqrt / reciprocal (v_sqrt_f32 / v_rcp_f32, ~1 ulp): the step is compared with the
+// fp64 oracle at 1e-5..1e-4, far above these errors
+__device__ __forceinline__ float fsqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+__device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
+
+// sin / cos of a bounded angle on the hardware units (v_sin/v_cos_f32, abs error < 4e-7 on [-pi, pi]):
+// libm sincosf carries a Payne-Hanek path whose private array lands in scratch
+__device__ __forceinline__ void sincos_hw(float x, float* s, float* c) {
+    *s = __sinf(x);
+    *c = __cosf(x);
+}
+// ---------------------------------------------------------------------------------------------
+// state I/O (SoA, coalesced per field)
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void load_drone(const KP& kp, const Bufs& b, int g, Drone& d) {
+    const float* s = b.st + g;
+    const int I = kp.I;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) { d.pos[i] = s[(QS_F_POS + i) * I]; d.vel[i] = s[(QS_F_VEL + i) * I]; }
+#pragma unroll
+    for (int i = 0; i < 9; ++i) d.rot[i] = s[(QS_F_ROT + i) * I];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) { d.om[i] = s[(QS_F_OMEGA + i) * I]; d.goal[i] = s[(QS_F_GOAL + i) * I]; }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        d.rd[i] = s[(QS_F_ROT_DAMP + i) * I];
+        d.cd[i] = s[(QS_F_CMD_DAMP + i) * I];
+        d.ou[i] = s[(QS_F_OU + i) * I];
+    }
+    const int32_t* is = b.ist + g;
+    d.svd = is[QS_I_SVD * I];
+    d.flags = (uint32_t)is[QS_I_FLAGS * I];
+    d.prev = (uint64_t)(uint32_t)is[QS_I_PREV_LO * I] | ((uint64_t)(uint32_t)is[QS_I_PREV_HI * I] << 32);
+}
+
+__device__ __forceinline__ void store_drone(const KP& kp, const Bufs& b, int g, const Drone& d) {
+    float* s = b.st + g;
+    const int I = kp.I;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) { s[(QS_F_POS + i) * I] = d.pos[i]; s[(QS_F_VEL + i) * I] = d.vel[i]; }
+#pragma unroll
+    for (int i = 0; i < 9; ++i) s[(QS_F_ROT + i) * I] = d.rot[i];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) { s[(QS_F_OMEGA + i) * I] = d.om[i]; s[(QS_F_GOAL + i) * I] = d.goal[i]; }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        s[(QS_F_ROT_DAMP + i) * I] = d.rd[i];
+        s[(QS_F_CMD_DAMP + i) * I] = d.cd[i];
+        s[(QS_F_OU + i) * I] = d.ou[i];
+    }
+    int32_t* is = b.ist + g;
+    is[QS_I_SVD * I] = d.svd;
+    is[QS_I_FLAGS * I] = (int32_t)d.flags;
+    is[QS_I_PREV_LO * I] = (int32_t)(uint32_t)d.prev;
+    is[QS_I_PREV_HI * I] = (int32_t)(uint32_t)(d.prev >> 32);
+}
+
+// ---------------------------------------------------------------------------------------------
+// L1 physics: one substep == step1_numba (quadrotor_dynamics.py:355-390)
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void yaw_rot(float theta, float* R) {
+    float s, c;
+    sincos_hw(theta, &s, &c);
+    R[0] = c; R[1] = -s; R[2] = 0.f;
+    R[3] = s; R[4] = c; R[5] = 0.f;
+    R[6] = 0.f; R[7] = 0.f; R[8] = 1.f;
+}
+
+// polar factor (u @ vh of the SVD, :554-558): Newton X <- (X + X^-T)/2; R is within ~1e-5 of
+// orthonormal after 100 fp32 substeps, three iterations converge to fp32 precision.
+__device__ __forceinline__ void polar3(float* x) {
+#pragma unroll
+    for (int it = 0; it < 3; ++it) {
+        const float a = x[0], b = x[1], c = x[2], d = x[3], e = x[4], f = x[5], g = x[6], h = x[7], i = x[8];
+        const float A = e * i - f * h, B = f * g - d * i, C = d * h - e * g;
+        const float inv = frcp(a * A + b * B + c * C);
+        const float cof[9] = {A, B, C, c * h - b * i, a * i - c * g, b * g - a * h, b * f - c * e, c * d - a * f,
+                              a * e - b * d};
+#pragma unroll
+        for (int k = 0; k < 9; ++k) x[k] = 0.5f * (x[k] + cof[k] * inv);
+    }
+}
+
+__device__ __forceinline__ void substep(const KP& kp, Drone& d, const float* cmds, const float* noise, const Rng& rng, uint32_t gid,
+                        int s) {
+    const float dt = kp.dt;
+    float thrusts[4], tq0 = 0.f, tq1 = 0.f, tq2 = 0.f, tsum = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {  // motor filter in sqrt space + multiplicative OU noise (:511-524)
+        const float cmd = cmds[k];
+        float tau = cmd < d.cd[k] ? kp.tau_down : kp.tau_up;
+        tau = fminf(tau, 1.0f);
+        d.rd[k] = tau * (fsqrt(cmd) - d.rd[k]) + d.rd[k];
+        const float c = clampf(d.rd[k] * d.rd[k] + cmd * noise[k], 0.f, 1.f);
+        d.cd[k] = c;
+        thrusts[k] = kp.thrust_max[k] * ((1.f - kp.lin) * c * c + kp.lin * c);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {  // torques (:527-533)
+        tq0 += kp.pc0[k] * thrusts[k];
+        tq1 += kp.pc1[k] * thrusts[k];
+        tq2 += kp.pc2[k] * thrusts[k] + kp.torque_max[k] * kp.ccw[k] * d.cd[k];
+        tsum += thrusts[k];
+    }
+    float* R = d.rot;
+    {  // Rodrigues with world-frame omega (:544-551):  dR = I + sin(a) K + (1 - cos a) K^2,
+       // K = skew(w)/|w|, a = |w| dt.  Written as I + dt S(a^2) skew(w) + dt^2 C(a^2) (w w^T - |w|^2 I)
+       // with S = sin(a)/a and C = (1 - cos a)/a^2: no sqrt, no division, no branch at w = 0 (where
+       // the reference skips the update: dR = I exactly as the series gives).
+        const float wx = R[0] * d.om[0] + R[1] * d.om[1] + R[2] * d.om[2];
+        const float wy = R[3] * d.om[0] + R[4] * d.om[1] + R[5] * d.om[2];
+        const float wz = R[6] * d.om[0] + R[7] * d.om[1] + R[8] * d.om[2];
+        const float w2 = wx * wx + wy * wy + wz * wz;
+        const float x = w2 * (dt * dt);
+        float sf, cf;
+        if (x < 0.36f) {  // a < 0.6: Taylor to a^8, truncation < 2e-10 (|omega| <= 40 per axis gives a <= 0.35)
+            sf = dt * (1.f + x * (-1.f / 6.f + x * (1.f / 120.f + x * (-1.f / 5040.f + x * (1.f / 362880.f)))));
+            cf = dt * dt * (0.5f + x * (-1.f / 24.f + x * (1.f / 720.f + x * (-1.f / 40320.f + x * (1.f / 3628800.f)))));
+        } else {          // after collision kicks (|omega| up to ~100 rad/s before the clip)
+            const float wn = fsqrt(w2), a = wn * dt;
+            float sa, ca;
+            sincos_hw(0.5f * a, &sa, &ca);
+            sf = 2.f * sa * ca / wn;
+            cf = 2.f * sa * sa / w2;
+        }
+        const float sx = sf * wx, sy = sf * wy, sz = sf * wz;
+        const float d0 = 1.f - cf * w2;
+        const float dR[9] = {d0 + cf * wx * wx, -sz + cf * wx * wy, sy + cf * wx * wz,
+                             sz + cf * wx * wy, d0 + cf * wy * wy, -sx + cf * wy * wz,
+                             -sy + cf * wx * wz, sx + cf * wy * wz, d0 + cf * wz * wz};
+        float Rn[9];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+                Rn[i * 3 + j] = dR[i * 3] * R[j] + dR[i * 3 + 1] * R[3 + j] + dR[i * 3 + 2] * R[6 + j];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) R[i] = Rn[i];
+    }
+    if (++d.svd >= kp.svd_every) {  // since_last_svd > 0.5 s (:553-558)
+        polar3(R);
+        d.svd = 0;
+    }
+    {  // omega (:562-567)
+        const float o0 = d.om[0], o1 = d.om[1], o2 = d.om[2];
+        const float I0 = kp.inertia[0] * o0, I1 = kp.inertia[1] * o1, I2 = kp.inertia[2] * o2;
+        const float c0 = -o1 * I2 + o2 * I1, c1 = -o2 * I0 + o0 * I2, c2 = -o0 * I1 + o1 * I0;
+        const float od0 = kp.inv_inertia[0] * (c0 + tq0);
+        const float od1 = kp.inv_inertia[1] * (c1 + tq1);
+        const float od2 = kp.inv_inertia[2] * (c2 + tq2);
+        const float dm0 = clampf(kp.dq * (o0 * o0), 0.f, 1.f), dm1 = clampf(kp.dq * (o1 * o1), 0.f, 1.f),
+                    dm2 = clampf(kp.dq * (o2 * o2), 0.f, 1.f);
+        d.om[0] = clampf(o0 + (1.f - dm0) * dt * od0, -kp.omega_max, kp.omega_max);
+        d.om[1] = clampf(o1 + (1.f - dm1) * dt * od1, -kp.omega_max, kp.omega_max);
+        d.om[2] = clampf(o2 + (1.f - dm2) * dt * od2, -kp.omega_max, kp.omega_max);
+    }
+    // position + room clip (:570, :367-374)
+    float before[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        before[i] = d.pos[i] + dt * d.vel[i];
+        d.pos[i] = clampf(before[i], kp.room_lo[i], kp.room_hi[i]);
+    }
+    uint32_t fl = d.flags & ~(uint32_t)(QS_FL_CRASH_FLOOR | QS_FL_CRASH_WALL | QS_FL_CRASH_CEIL);
+    if (before[0] != d.pos[0] || before[1] != d.pos[1]) fl |= QS_FL_CRASH_WALL;
+    if (before[2] > d.pos[2]) fl |= QS_FL_CRASH_CEIL;
+    // floor (floor_interaction_numba :576-646, threshold = arm)
+    float fx = R[2] * tsum, fy = R[5] * tsum, fz = R[8] * tsum;
+    float ax, ay, az;
+    if (d.pos[2] <= kp.arm) {
+        d.pos[2] = kp.arm;
+        if (fl & QS_FL_ON_FLOOR) {
+            yaw_rot(atan2f(R[3], R[0] + 1e-6f), R);
+            const float fric = 0.6f * (kp.mass * kp.grav - fz);
+            const float vn = fsqrt(d.vel[0] * d.vel[0] + d.vel[1] * d.vel[1] + d.vel[2] * d.vel[2]);
+            if (vn < 1e-6f) {
+                float fxy = fsqrt(fx * fx + fy * fy);
+                fxy = fmaxf(fxy - fric, 0.f);
+                if (fxy == 0.f) {
+                    fx = 0.f; fy = 0.f;
+                } else {
+                    float sa, ca;
+                    sincos_hw(atan2f(fy, fx), &sa, &ca);
+                    fx = fxy * ca; fy = fxy * sa;
+                }
+            } else {
+                float sa, ca;
+                sincos_hw(atan2f(d.vel[1], d.vel[0]), &sa, &ca);
+                fx = fx - ca * fric;
+                fy = fy - sa * fric;
+            }
+        } else {
+            fl |= QS_FL_ON_FLOOR | QS_FL_CRASH_FLOOR;
+#pragma unroll
+            for (int i = 0; i < 3; ++i) { d.vel[i] = 0.f; d.om[i] = 0.f; }
+            float theta = atan2f(R[3], R[0] + 1e-6f);
+            if (R[8] < 0.f) theta = -3.14159265358979f + 6.28318530717959f * uniform1(rng, gid, S_FLOOR | ((uint32_t)s << 8), 0);
+            yaw_rot(theta, R);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) { d.cd[k] = 0.f; d.rd[k] = 0.f; }
+        }
+        ax = kp.inv_mass * fx;
+        ay = kp.inv_mass * fy;
+        az = fmaxf(-kp.grav + kp.inv_mass * fz, 0.f);
+    } else {
+        fl &= ~(uint32_t)QS_FL_ON_FLOOR;
+        ax = kp.inv_mass * fx;
+        ay = kp.inv_mass * fy;
+        az = -kp.grav + kp.inv_mass * fz;
+    }
+    d.flags = fl;
+    d.vel[0] = (1.f - kp.vel_damp) * d.vel[0] + dt * ax;  // (:652)
+    d.vel[1] = (1.f - kp.vel_damp) * d.vel[1] + dt * ay;
+    d.vel[2] = (1.f - kp.vel_damp) * d.vel[2] + dt * az;
+}
+
+
+// Neighbour exchange tile in LDS: lane l stores {pos, 0} at xch[2l] and {vel, 0} at xch[2l+1]; the
+// drones of one env read each other's rows with broadcast ds_read_b128 (one wave per workgroup, so a
+// workgroup barrier costs nothing but orders the LDS traffic).
+// LDS-only workgroup barrier: workgroups are one wave, so this just orders LDS traffic.  Unlike
+// __syncthreads() it does not wait for outstanding global stores (vmcnt) or fence global memory.
+__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// ---------------------------------------------------------------------------------------------
+// block-level obs staging: LDS tile [rows, obs_dim] -> contiguous global rows
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void tile_store(const float* lds, float* dst, int nfloat, int lane) {
+    // dst = first row of the block; rows are contiguous in HBM.  obs is 256-B aligned and a block owns
+    // 64/NPAD*N rows, so the start is 16-B aligned whenever rows*obs_dim*4 is: b128 in, dwordx4 out.
+    if ((((uintptr_t)dst) & 15) == 0) {
+        const int nvec = nfloat >> 2;
+        const float4* lv = reinterpret_cast<const float4*>(lds);
+        float4* dv = reinterpret_cast<float4*>(dst);
+        for (int v = lane; v < nvec; v += 64) dv[v] = lv[v];
+        const int t = (nvec << 2) + lane;
+        if (t < nfloat) dst[t] = lds[t];
+    } else {
+        for (int f = lane; f < nfloat; f += 64) dst[f] = lds[f];
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// the fused step kernel
+// ---------------------------------------------------------------------------------------------
+// Philox counter of an env = {tick, episode}: unique for every step and reset of that env, resident
+// with the env state (no global counter, no atomics), so a hipGraph replay of K steps draws K fresh
+// streams and sharding envs over GPUs does not change any draw.
+__device__ __forceinline__ Rng env_rng(uint32_t seed, int32_t tick, int32_t episode) {
+    Rng r;
+    r.seed = seed;
+    r.ctr_lo = (uint32_t)tick;
+    r.ctr_hi = (uint32_t)episode;
+    return r;
+}
+
+}  // namespace qs

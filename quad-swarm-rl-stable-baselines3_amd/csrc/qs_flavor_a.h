@@ -1,0 +1,603 @@
+// qs_flavor_a.h -- flavor-A kernels: the env swarm_rl/sb_train.py trains on.
+//
+//   quadrotor_multi_rewards.QuadrotorEnvMulti.step   quadrotor_multi_rewards.py:630-991
+//     8 x QuadrotorSingle._step                      quadrotor_single_rewards.py:418-452
+//         Controller.update_vel_height_dir           Controller/Controller.py:76-101 (+ Position/Velocity/
+//                                                    Acceleration/Attitude/Rate controllers, Mixer, Pid.py)
+//         CustomPidControl.step + QuadrotorDynamics  quadrotor_control.py:90-94, quadrotor_dynamics.py:215-221
+//     capture reward / dones                         quadrotor_multi_rewards.py:711-735, 882-988
+//     Scenario_dynamic_repulsive.step / reset        scenarios/dynamic_repulsive.py:37-74 (float-fixed)
+//     neighbour obs + camera model                   quadrotor_multi_rewards.py:238-476
+//   SubprocVecEnvCustom worker reset on done         subproc_vec_env_custom.py:39-46 (reset_infos)
+//
+// Same execution model as flavor B (qs_flavor_b.h): one lane per drone, an env is an NPAD-lane
+// segment of a 64-lane wave, one wave per workgroup.  The 8 controller+physics ticks of a step run in
+// registers; an env that finishes mid-step (capture) idles for the remaining ticks, like the
+// reference's `break`.  Cross-drone work per tick is one segment reduction (target repulsion) and
+// two segment ballots (capture, done); neighbour features read an LDS exchange tile once per step.
+#pragma once
+#include "qs_common.h"
+
+namespace qs {
+
+constexpr float kPi = 3.14159265358979f;
+constexpr float k2Pi = 6.28318530717959f;
+
+struct Ctl {
+    float pid[20];  // (last_error, integral) x {pos z, vel x y z, att x y z, rate x y z}
+    float angle, angvel;
+};
+
+__device__ __forceinline__ void load_ctl(const KP& kp, const Bufs& b, int g, Ctl& c) {
+    const float* s = b.st + g;
+#pragma unroll
+    for (int i = 0; i < 20; ++i) c.pid[i] = s[(QS_F_PID + i) * kp.I];
+    c.angle = s[QS_F_ANGLE * kp.I];
+    c.angvel = s[QS_F_ANGVEL * kp.I];
+}
+
+__device__ __forceinline__ void store_ctl(const KP& kp, const Bufs& b, int g, const Ctl& c) {
+    float* s = b.st + g;
+#pragma unroll
+    for (int i = 0; i < 20; ++i) s[(QS_F_PID + i) * kp.I] = c.pid[i];
+    s[QS_F_ANGLE * kp.I] = c.angle;
+    s[QS_F_ANGVEL * kp.I] = c.angvel;
+}
+
+// sin(x) for 0 <= x < pi/2, odd Taylor series to x^11 (relative error < 1e-7 for small x, where the
+// camera range r / sin(alpha/2) needs it)
+__device__ __forceinline__ float sin_small(float x) {
+    const float x2 = x * x;
+    return x * (1.f + x2 * (-1.f / 6.f + x2 * (1.f / 120.f + x2 * (-1.f / 5040.f + x2 * (1.f / 362880.f + x2 * (-1.f / 39916800.f))))));
+}
+
+// (x + pi) % (2 pi) - pi with Python's modulo sign convention
+__device__ __forceinline__ float wrap_pi(float x) {
+    float r = fmodf(x + kPi, k2Pi);
+    if (r < 0.f) r += k2Pi;
+    return r - kPi;
+}
+
+// _pid_update_numba (Controller/Pid.py:6-26)
+__device__ __forceinline__ float pid_update(const KP& kp, int k, float e, float* st) {
+    const float diff = (e - st[0]) * kp.inv_dt;
+    st[0] = e;
+    float out = kp.pkp[k] * e + kp.pkd[k] * diff + kp.pki[k] * st[1];
+    const float sat = kp.psat[k];
+    if (sat > 0.f) out = out >= sat ? sat : (out <= -sat ? -sat : out);
+    const float aw = kp.paw[k];
+    if (aw > 0.f && -aw < out && out < aw) st[1] += e * kp.dt;
+    return out;
+}
+
+// Controller.update_vel_height_dir (Controller.py:76-101) -> Mixer output -> _step's reorder/arctan
+// (quadrotor_single_rewards.py:436-437) -> CustomPidControl.step (quadrotor_control.py:90-94): the 4
+// normalised thrust commands for QuadrotorDynamics.step.
+__device__ __forceinline__ void controller(const KP& kp, const Drone& d, Ctl& c, float a0, float height, float* u) {
+    c.angvel = a0;
+    c.angle = wrap_pi(c.angle + a0 * kp.hrate);
+    float sa, ca;
+    sincos_hw(c.angle, &sa, &ca);
+    // PositionController z (PositionController.py:62-77); x/y outputs are overwritten by the heading
+    // velocity (:90) and their PID state never reaches an output, so they are not carried.
+    const float vz = pid_update(kp, 0, height - d.pos[2], c.pid);
+    const float vref[3] = {ca * kp.speed, sa * kp.speed, vz};
+    float acc[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) acc[i] = pid_update(kp, 1 + i, vref[i] - d.vel[i], c.pid + 2 * (1 + i));
+    // AccelerationController (AccelerationController.py:18-108), heading 0: the oblique projection of
+    // (1,0,0) along z onto the plane normal to n is (1, 0, -n0/n2), i.e. x_des = (|n2|, 0, -n0 sgn n2)/|(n0,n2)|
+    const float fd0 = acc[0] * kp.m_mass, fd1 = acc[1] * kp.m_mass, fd2 = acc[2] * kp.m_mass + kp.m_mass_g;
+    const float ifn = rsqrtf(fd0 * fd0 + fd1 * fd1 + fd2 * fd2);
+    const float n0 = fd0 * ifn, n1 = fd1 * ifn, n2 = fd2 * ifn;
+    const float ixn = rsqrtf(n0 * n0 + n2 * n2);
+    const float x0 = fabsf(n2) * ixn, x1 = 0.f, x2 = (n2 >= 0.f ? -n0 : n0) * ixn;
+    float y0 = n1 * x2 - n2 * x1, y1 = n2 * x0 - n0 * x2, y2 = n0 * x1 - n1 * x0;
+    const float iyn = rsqrtf(y0 * y0 + y1 * y1 + y2 * y2);
+    y0 *= iyn; y1 *= iyn; y2 *= iyn;
+    const float* R = d.rot;
+    const float tf = fmaxf(fd0 * R[2] + fd1 * R[5] + fd2 * R[8], 0.f);
+    const float thr = clampf((fsqrt(tf / kp.m_kf4) - kp.m_min_rpm) * kp.m_inv_rpm, 0.f, 1.f);
+    // AttitudeController (AttitudeController.py:60-82): e = vee(0.5 (Rd^T R - R^T Rd)); M = Rd^T R
+    const float Rd0[3] = {x0, x1, x2}, Rd1[3] = {y0, y1, y2}, Rd2[3] = {n0, n1, n2};
+    auto M = [&](const float* col, int j) { return col[0] * R[j] + col[1] * R[3 + j] + col[2] * R[6 + j]; };
+    const float e0 = 0.5f * (M(Rd1, 2) - M(Rd2, 1));
+    const float e1 = 0.5f * (M(Rd2, 0) - M(Rd0, 2));
+    const float e2 = 0.5f * (M(Rd0, 1) - M(Rd1, 0));
+    const float rate0 = pid_update(kp, 4, e0, c.pid + 8);
+    const float rate1 = pid_update(kp, 5, e1, c.pid + 10);
+    const float rate2 = pid_update(kp, 6, e2, c.pid + 12);
+    // RateController (RateController.py:71-89)
+    float cg[4];
+    cg[0] = pid_update(kp, 7, rate0 - d.om[0], c.pid + 14) * kp.rate_scale;
+    cg[1] = pid_update(kp, 8, rate1 - d.om[1], c.pid + 16) * kp.rate_scale;
+    cg[2] = pid_update(kp, 9, rate2 - d.om[2], c.pid + 18) * kp.rate_scale;
+    cg[3] = thr;
+    // Mixer with desaturation (Mixer.py:70-111)
+    const float* X = kp.mix;
+    float m[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) m[i] = X[i * 4] * cg[0] + X[i * 4 + 1] * cg[1] + X[i * 4 + 2] * cg[2] + X[i * 4 + 3] * cg[3];
+    const float mn = fminf(fminf(m[0], m[1]), fminf(m[2], m[3]));
+    if (mn < 0.f) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) m[i] += -mn;
+    }
+    const float mx = fmaxf(fmaxf(m[0], m[1]), fmaxf(m[2], m[3]));
+    if (mx > 1.f) {
+        if (thr > 1e-2f) {
+            const float isc = thr / ((m[0] + ((m[1] + m[2]) + m[3])) * 0.25f);
+            cg[0] *= isc; cg[1] *= isc; cg[2] *= isc;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                m[i] = X[i * 4] * cg[0] + X[i * 4 + 1] * cg[1] + X[i * 4 + 2] * cg[2] + X[i * 4 + 3] * cg[3];
+        } else {
+            const float im = 1.f / mx;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) m[i] *= im;
+        }
+    }
+    const float re[4] = {m[0], m[3], m[1], m[2]};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) u[k] = 0.5f * (clampf(atanf(re[k] * 2.f - 1.f), -1.f, 1.f) + 1.f);
+}
+
+// (|p + v dt| - |p|) / dt without the fp32 cancellation: (2 p.v + dt |v|^2) / (|p + v dt| + |p|)
+__device__ __forceinline__ float norm_rate(float p0, float p1, float v0, float v1, float dt, float pn) {
+    const float q0 = p0 + v0 * dt, q1 = p1 + v1 * dt;
+    const float den = fsqrt(q0 * q0 + q1 * q1) + pn;
+    const float num = 2.f * (p0 * v0 + p1 * v1) + dt * (v0 * v0 + v1 * v1);
+    return den > 0.f ? num / den : 0.f;
+}
+
+// simulate_camera_measurement_vect (get_state.py:128-176 == quadrotor_multi_rewards.py:275-324) for one
+// target; n1, n2: pixel noise.  circle_intersection_vect(c, r, c/2, |c|/2) in closed form: the chord
+// distance a = r^2/|c|, midpoint c (1 - r^2/|c|^2), perpendicular (c1, -c0)/|c|.
+__device__ __forceinline__ void camera(const KP& kp, float rx, float ry, float ga, float n1, float n2, float& dist, float& ang) {
+    float s, c;
+    sincos_hw(-ga, &s, &c);
+    const float rp0 = c * rx - s * ry, rp1 = s * rx + c * ry;
+    float m = fmodf(atan2f(rp1, rp0), k2Pi);
+    if (m < 0.f) m += k2Pi;
+    const float seg = k2Pi / (float)kp.n_cam;
+    const int ci = ((int)rintf(m / seg)) % kp.n_cam;
+    const float cam = (float)ci * seg;
+    sincos_hw(-cam, &s, &c);
+    const float c0 = c * rp0 - s * rp1, c1 = s * rp0 + c * rp1;
+    const float cn2 = c0 * c0 + c1 * c1, cn = fsqrt(cn2);
+    const float r = kp.cam_r, r2 = r * r;
+    const float a = r2 / cn;
+    const float h = sqrtf(r2 - a * a);                   // NaN when the target is inside the marker
+    const float mf = 1.f - r2 / cn2;
+    const float mid0 = c0 * mf, mid1 = c1 * mf;
+    const float pe0 = c1 / cn, pe1 = -c0 / cn;
+    const float x10 = mid0 + h * pe0, x11 = mid1 + h * pe1;
+    const float x20 = mid0 - h * pe0, x21 = mid1 - h * pe1;
+    const float pxs = kp.cam_w / (kp.cam_res * kp.cam_f);  // pixel -> tan(angle)
+    const float at1 = atanf(x11 / x10 + n1 * pxs), at2 = atanf(x21 / x20 + n2 * pxs);
+    const float alpha = fabsf(at1 - at2);
+    const float l = r / sin_small(0.5f * alpha);
+    const float ar = wrap_pi(0.5f * (at1 + at2) + cam);
+    dist = (l != l) ? 0.f : l;
+    ang = (ar != ar) ? 0.f : ar;
+}
+
+// pos / vel sensor noise (sensor_noise.py:234-261, draws 0-5 of the 27; the rest do not reach a
+// flavor-A observation)
+__device__ __forceinline__ void noisy_pos_vel(const KP& kp, const Drone& d, const Rng& rng, uint32_t gid,
+                                              uint32_t st, float* np_, float* nv) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) { np_[i] = d.pos[i]; nv[i] = d.vel[i]; }
+    if (!kp.sense) return;
+    float z[8];
+    normals4(rng, gid, st, 0, z);
+    normals4(rng, gid, st, 1, z + 4);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        np_[i] += kp.pos_std * z[i];
+        nv[i] += kp.vel_std * z[3 + i];
+    }
+    if (kp.pos_unif != 0.f || kp.vel_unif != 0.f) {
+        float u[8];
+        uniforms4(rng, gid, st, 0, u);
+        uniforms4(rng, gid, st, 1, u + 4);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            np_[i] += -kp.pos_unif + 2.f * kp.pos_unif * u[i];
+            nv[i] += -kp.vel_unif + 2.f * kp.vel_unif * u[3 + i];
+        }
+    }
+}
+
+// flavor-A self observation (get_state.py:7-223)
+__device__ __forceinline__ void self_obs_a(const KP& kp, const Drone& d, const Ctl& c, float gx, float gy, const Rng& rng,
+                           uint32_t gid, uint32_t st_sensor, uint32_t st_cam, float* out) {
+    float np_[3], nv[3];
+    noisy_pos_vel(kp, d, rng, gid, st_sensor, np_, nv);
+    const float dt = kp.dt;
+    const float rp0 = gx - np_[0], rp1 = gy - np_[1];
+    const float rd = fsqrt(rp0 * rp0 + rp1 * rp1);
+    const float drd = norm_rate(rp0, rp1, nv[0], nv[1], dt, rd);
+    const float ra = wrap_pi(atan2f(rp1, rp0) - c.angle);
+    const float av = c.angvel, pr = av * ra;
+    const float adot = -(pr > 0.f ? 1.f : (pr < 0.f ? -1.f : 0.f)) * fabsf(av);
+    if (kp.obs_repr == QS_OBS_AW_AWDOT_DIST_DISTDOT_ANGLE_ANGLEDOT) {
+        out[0] = c.angle; out[1] = av; out[2] = rd; out[3] = drd; out[4] = ra; out[5] = adot;
+        return;
+    }
+    const float cd = fsqrt(np_[0] * np_[0] + np_[1] * np_[1]);
+    out[0] = cd;
+    out[1] = norm_rate(np_[0], np_[1], nv[0], nv[1], dt, cd);
+    out[3] = drd;
+    if (kp.obs_repr == QS_OBS_CDIST_CDISTDOT_DIST_DISTDOT_ANGLE_ANGLEDOT) {
+        out[2] = rd; out[4] = ra; out[5] = adot;
+    } else if (kp.obs_repr == QS_OBS_CDIST_CDISTDOT_DIST_DISTDOT_SANGLE_ANGLEDOT) {
+        float s, co;
+        sincos_hw(ra, &s, &co);
+        out[2] = rd; out[4] = co; out[5] = s; out[6] = adot;
+    } else {
+        float n1 = 0.f, n2 = 0.f;
+        if (kp.cam_px != 0.f) {
+            float z[4];
+            normals4(rng, gid, st_cam, 0, z);
+            n1 = kp.cam_px * z[0];
+            n2 = kp.cam_px * z[1];
+        }
+        float nd, na, s, co;
+        camera(kp, rp0, rp1, c.angle, n1, n2, nd, na);
+        sincos_hw(na, &s, &co);
+        out[2] = clampf(nd, 0.f, 10.f); out[4] = co; out[5] = s; out[6] = adot;
+    }
+}
+
+// exchange tile: lane l holds {pos, heading} at xch[2l] and {vel, 0} at xch[2l+1]
+__device__ __forceinline__ void xch_put_a(float4* xch, int lane, const float* P, float H, const float* V) {
+    xch[2 * lane] = make_float4(P[0], P[1], P[2], H);
+    xch[2 * lane + 1] = make_float4(V[0], V[1], V[2], 0.f);
+}
+
+// get_rel_pos_vel_item for the pair (i = this lane, j): emits the features in the reference's order
+// to sink(slot, value) (no private array: slots are runtime, the sink accumulates or writes LDS)
+template <class Sink>
+__device__ __forceinline__ void rel_features(const KP& kp, const float4& pj, const float4& vj, const float* P, float H,
+                                             float aw, const float* V, const Rng& rng, uint32_t gid, uint32_t st,
+                                             Sink&& sink) {
+    const int m = kp.nfeat;
+    const float r0 = pj.x - P[0], r1 = pj.y - P[1], r2 = pj.z - P[2];
+    int n = 0;
+    float na = 0.f;
+    if (m & QS_NF_DIST) sink(n++, fsqrt(r0 * r0 + r1 * r1 + r2 * r2));
+    if (m & QS_NF_NDIST) {
+        float n1 = 0.f, n2 = 0.f;
+        if (kp.cam_px != 0.f) {
+            float z[4];
+            normals4(rng, gid, st, 0, z);
+            n1 = kp.cam_px * z[0];
+            n2 = kp.cam_px * z[1];
+        }
+        float nd;
+        camera(kp, r0, r1, aw, n1, n2, nd, na);
+        sink(n++, clampf(nd, 0.f, 10.f));
+    }
+    if (m & (QS_NF_ANGLE | QS_NF_SANGLE)) {
+        // atan2 of the 3-D-normalised vector (:365-367); undefined (NaN) for coincident drones
+        const float pn = fsqrt(r0 * r0 + r1 * r1 + r2 * r2);
+        const float ra = pn > 0.f ? wrap_pi(atan2f(r1, r0) - aw) : __builtin_nanf("");
+        if (m & QS_NF_ANGLE) sink(n++, ra);
+        if (m & QS_NF_SANGLE) { float s, c; sincos_hw(ra, &s, &c); sink(n++, c); sink(n++, s); }
+    }
+    if (m & QS_NF_NSANGLE) { float s, c; sincos_hw(na, &s, &c); sink(n++, c); sink(n++, s); }
+    if (m & (QS_NF_HEADING | QS_NF_SHEADING)) {
+        const float rh = wrap_pi(pj.w - H);
+        if (m & QS_NF_HEADING) sink(n++, rh);
+        if (m & QS_NF_SHEADING) { float s, c; sincos_hw(rh, &s, &c); sink(n++, c); sink(n++, s); }
+    }
+    if (m & (QS_NF_NPOS | QS_NF_POS)) { sink(n++, r0); sink(n++, r1); sink(n++, r2); }
+    if (m & QS_NF_VEL) { sink(n++, vj.x - V[0]); sink(n++, vj.y - V[1]); sink(n++, vj.z - V[2]); }
+}
+
+// neighborhood_indices (:445-476) + extend_obs_space clip (:422-443).  k < N-1: selection by the norm
+// of the feature vector (clamped at 0.01, stable, NaN last) with its own camera noise, then the
+// selected pairs' features again with the obs-pass noise (the reference calls the camera twice).
+template <int NPAD>
+__device__ __forceinline__ void neighbor_obs_a(const KP& kp, const float4* xch, int base, int di, const float* P, float H, float aw,
+                               const float* V, const Rng& rng, uint32_t gid, bool reset, bool write, float* out) {
+    const bool sorted = kp.K < kp.N - 1;
+    const uint32_t st_obs = reset ? S_RESET_CAM : S_CAM, st_sel = reset ? S_RESET_CAM_SEL : S_CAM_SEL;
+    const int F = kp.nfd;
+    float key[NPAD];
+    if (sorted) {
+#pragma unroll
+        for (int j = 0; j < NPAD; ++j) {
+            const bool valid = (j != di) && (j < kp.N);
+            float s = 0.f;
+            rel_features(kp, xch[2 * (base + j)], xch[2 * (base + j) + 1], P, H, aw, V, rng, gid,
+                         st_sel | ((uint32_t)j << 8), [&](int, float v) { s += v * v; });
+            key[j] = valid ? ((s != s) ? 3.0e38f : fmaxf(s, 1e-4f)) : __builtin_inff();
+        }
+    }
+    if (!write) return;
+#pragma unroll
+    for (int j = 0; j < NPAD; ++j) {
+        const bool valid = (j != di) && (j < kp.N);
+        int rank;
+        if (sorted) {
+            rank = 0;
+#pragma unroll
+            for (int m = 0; m < NPAD; ++m) rank += (key[m] < key[j]) || (m < j && key[m] == key[j]);
+        } else {
+            rank = j < di ? j : j - 1;
+        }
+        if (valid && rank < kp.K) {
+            float* o = out + kp.so_dim + rank * F;
+            rel_features(kp, xch[2 * (base + j)], xch[2 * (base + j) + 1], P, H, aw, V, rng, gid,
+                         st_obs | ((uint32_t)j << 8),
+                         [&](int q, float v) { o[q] = clampf(v, kp.nclip_lo[q], kp.nclip_hi[q]); });
+        }
+    }
+}
+
+// segment (= env) helpers over the NPAD lanes of an env
+template <int NPAD>
+__device__ __forceinline__ bool seg_any(bool x, int base) {
+    const uint64_t gm = (NPAD == 64) ? ~0ull : ((1ull << NPAD) - 1ull);
+    return ((__ballot(x) >> base) & gm) != 0ull;
+}
+template <int NPAD>
+__device__ __forceinline__ float seg_sum(float v) {   // butterfly: every lane ends with the same bits
+#pragma unroll
+    for (int m = 1; m < NPAD; m <<= 1) v += __shfl_xor(v, m);
+    return v;
+}
+
+// Scenario_dynamic_repulsive.step (dynamic_repulsive.py:37-62): target flees the chasers (1/d each)
+// and the arena edge, speed <= v_max.  Every lane of the env computes the same update.
+template <int NPAD>
+__device__ __forceinline__ void target_step(const KP& kp, float& tx, float& ty, const float* pos, bool contrib) {
+    const float r0 = tx - pos[0], r1 = ty - pos[1];
+    const float d2 = r0 * r0 + r1 * r1;
+    const float fx = seg_sum<NPAD>(contrib ? r0 / d2 : 0.f);
+    const float fy = seg_sum<NPAD>(contrib ? r1 / d2 : 0.f);
+    const float de = fsqrt(tx * tx + ty * ty);
+    const float den = de * fmaxf(kp.arena - de, 0.1f);
+    const float vx = fx - tx / den, vy = fy - ty / den;
+    const float vs = fsqrt(vx * vx + vy * vy);
+    const float sc = fminf(vs, kp.tgt_vmax) / vs * kp.tgt_dt;
+    tx = tx + vx * sc;
+    ty = ty + vy * sc;
+}
+
+// QuadrotorEnvMulti.reset (quadrotor_multi_rewards.py:541-627) for the lanes of one env, including
+// Scenario_dynamic_repulsive.reset (dynamic_repulsive.py:64-74, its step() sees the pre-reset chaser
+// positions) and QuadrotorSingle._reset (quadrotor_single_rewards.py:480-549).  All lanes of the
+// segment must call it (the target update is a segment reduction); `sel` lanes take the new state.
+template <int NPAD>
+__device__ __forceinline__ void reset_env_a(const KP& kp, Drone& d, Ctl& c, float& tx, float& ty, bool has_pos, bool active,
+                            bool sel, const Rng& rng, uint32_t gid, uint32_t genv) {
+    float ru[4], ue[4];
+    uniforms4(rng, gid, S_RESET_A, 0, ru);
+    if (kp.scenario == QS_SCEN_DYNAMIC_REPULSIVE) {
+        uniforms4(rng, genv, S_SCEN, 0, ue);
+        const float a = ue[1] - 0.5f, b = ue[2] - 0.5f, in = rsqrtf(a * a + b * b), tr = ue[3] * 3.f + 2.f;
+        float ntx = a * in * tr, nty = b * in * tr;
+        target_step<NPAD>(kp, ntx, nty, d.pos, active && has_pos);
+        if (sel) {
+            tx = ntx;
+            ty = nty;
+            const float sa = ru[0] - 0.5f, sb = ru[1] - 0.5f, isn = rsqrtf(sa * sa + sb * sb), rad = ue[0] * 0.5f;
+            d.goal[0] = tx; d.goal[1] = ty; d.goal[2] = fmaxf(kp.tgt_z, 0.25f);
+            d.pos[0] = sa * isn * rad;
+            d.pos[1] = sb * isn * rad;
+        }
+    } else if (sel) {
+        d.goal[0] = kp.goal[0]; d.goal[1] = kp.goal[1]; d.goal[2] = kp.goal[2];
+        d.pos[0] = d.goal[0];
+        d.pos[1] = d.goal[1];
+    }
+    if (!sel) return;
+    d.pos[2] = fmaxf(d.goal[2], 0.75f);
+    c.angle = (ru[2] - 0.5f) * k2Pi;
+    {   // randyaw (quad_utils.py:228-230)
+        float sy, cy;
+        sincos_hw(-kPi + k2Pi * uniform1(rng, gid, S_RESET_YAW, 0), &sy, &cy);
+        d.rot[0] = cy; d.rot[1] = -sy; d.rot[2] = 0.f;
+        d.rot[3] = sy; d.rot[4] = cy; d.rot[5] = 0.f;
+        d.rot[6] = 0.f; d.rot[7] = 0.f; d.rot[8] = 1.f;
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) { d.vel[i] = 0.f; d.om[i] = 0.f; }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { d.rd[k] = 0.f; d.cd[k] = 0.f; }
+    d.flags = 0;
+}
+
+template <int NPAD>
+__global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, Bufs b, uint32_t seed) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const KP& kp = *kpp;
+    constexpr int EPB = 64 / NPAD;
+    const int lane = threadIdx.x;
+    const int el = lane / NPAD, di = lane % NPAD;
+    const int env0 = blockIdx.x * EPB;
+    const int env = env0 + el;
+    const bool active = env < kp.E && di < kp.N;
+    const int g = active ? env * kp.N + di : 0;
+    const uint32_t gid = kp.id0 + (uint32_t)g;
+    const int base = el * NPAD;
+    const int nenv_blk = min(EPB, kp.E - env0);
+    const int rows = nenv_blk * kp.N;
+    float* row = lds + (size_t)(el * kp.N + di) * kp.obs_dim;
+    float4* xch = reinterpret_cast<float4*>(lds + 64 * kp.obs_dim);
+    int* efin = reinterpret_cast<int*>(lds + 64 * kp.obs_dim + 64 * 8);
+
+    Drone d;
+    load_drone(kp, b, g, d);
+    Ctl c;
+    load_ctl(kp, b, g, c);
+    const float a0 = reinterpret_cast<const float2*>(b.act)[g].x;
+    const int eidx = active ? env : 0;
+    int tick = b.env[QS_E_TICK * kp.E + eidx];
+    const int episode = b.env[QS_E_EPISODE * kp.E + eidx];
+    const int eflags = b.env[QS_E_FLAGS * kp.E + eidx];
+    float tx = b.envf[QS_ENVF_TARGET_X * kp.E + eidx], ty = b.envf[QS_ENVF_TARGET_Y * kp.E + eidx];
+    const float capr = b.envf[QS_ENVF_CAPTURE * kp.E + eidx];
+    const bool repulsive = kp.scenario == QS_SCEN_DYNAMIC_REPULSIVE;
+
+    bool fin = false, success = eflags & QS_EF_SUCCESS;
+    float rw = 0.f, gox = d.goal[0], goy = d.goal[1];
+    bool dn = false;
+    for (int sub = 0; sub < kp.ticks; ++sub) {
+        if (fin) continue;   // the reference breaks out of its tick loop (:988); segment-uniform
+        const Rng rng = env_rng(seed, tick, episode);
+        float u[4];
+        controller(kp, d, c, a0, d.goal[2], u);
+        float z[4];
+        normals4(rng, gid, S_OU, 0, z);  // QuadrotorDynamics.step: one OU draw per tick (:216)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) d.ou[k] = d.ou[k] + (kp.ou_theta * (kp.ou_mu - d.ou[k]) + kp.ou_sigma * z[k]);
+        for (int s = 0; s < kp.sim_steps; ++s) substep(kp, d, u, d.ou, rng, gid, s);
+        ++tick;
+        gox = d.goal[0];
+        goy = d.goal[1];
+        // capture reward (:711-735) against env 0's goal; dones (:882-988)
+        const float g0x = repulsive ? tx : __shfl(d.goal[0], base), g0y = repulsive ? ty : __shfl(d.goal[1], base);
+        const float dx = g0x - d.pos[0], dy = g0y - d.pos[1];
+        const float rel = fsqrt(dx * dx + dy * dy);
+        const bool capi = capr > rel;
+        const bool cap = seg_any<NPAD>(active && capi, base);
+        const float captor = cap && capi ? kp.w_captor : 0.f;
+        const float helper = cap && capr < rel ? kp.w_helper : 0.f;
+        rw = ((0.f + captor) + helper) + kp.existence;
+        dn = cap ? capi : (tick > kp.ep_len);
+        fin = seg_any<NPAD>(active && dn, base);
+        success = success || cap;
+        if (repulsive) {   // scenario.step() (:797)
+            target_step<NPAD>(kp, tx, ty, d.pos, active);
+            d.goal[0] = tx;
+            d.goal[1] = ty;
+        }
+    }
+
+    // ---- observations of the final tick (self obs of the last _step, neighbours after the loop) ----
+    const Rng rng_last = env_rng(seed, tick - 1, episode);
+    xch_put_a(xch, lane, d.pos, c.angle, d.vel);
+    if (lane < EPB) efin[lane] = 0;
+    lds_sync();
+    if (fin && di == 0) efin[el] = 1;
+    if (active) self_obs_a(kp, d, c, gox, goy, rng_last, gid, S_SENSOR, S_SELF_CAM, row);
+    if (kp.K > 0) neighbor_obs_a<NPAD>(kp, xch, base, di, d.pos, c.angle, c.angle, d.vel, rng_last, gid, false, active, row);
+
+    const uint64_t fball = __ballot(active && fin);
+    if (fball) {  // some env finished: terminal obs + the worker's reset (subproc_vec_env_custom.py:42-46)
+        lds_sync();
+        for (int r = 0; r < rows; ++r) {
+            if (!efin[r / kp.N]) continue;
+            for (int q = lane; q < kp.obs_dim; q += 64)
+                b.term[(size_t)(env0 * kp.N + r) * kp.obs_dim + q] = lds[(size_t)r * kp.obs_dim + q];
+        }
+        lds_sync();
+        const float sh = c.angle, sv[3] = {d.vel[0], d.vel[1], d.vel[2]};  // QuadrotorEnvMulti.heading / .vel
+        const Rng rr = env_rng(seed, tick, episode);
+        reset_env_a<NPAD>(kp, d, c, tx, ty, true, active, active && fin, rr, gid, kp.id0 + (uint32_t)(env * kp.N));
+        if (active && fin) {
+            self_obs_a(kp, d, c, d.goal[0], d.goal[1], rr, gid, S_RESET_SENSOR, S_RESET_SELF_CAM, row);
+            b.stale[0 * kp.I + g] = sv[0];
+            b.stale[1 * kp.I + g] = sv[1];
+            b.stale[2 * kp.I + g] = sv[2];
+            b.st[QS_F_HEADING * kp.I + g] = sh;
+        }
+        if (kp.K > 0) {
+            xch_put_a(xch, lane, d.pos, sh, sv);
+            lds_sync();
+            neighbor_obs_a<NPAD>(kp, xch, base, di, d.pos, sh, c.angle, sv, rr, gid, true, active && fin, row);
+        }
+    }
+    lds_sync();
+    tile_store(lds, b.obs + (size_t)env0 * kp.N * kp.obs_dim, rows * kp.obs_dim, lane);
+
+    if (active) {
+        store_drone(kp, b, g, d);
+        store_ctl(kp, b, g, c);
+        b.rew[g] = rw;
+        b.done[g] = fin ? 1 : 0;
+        if (di == 0) {
+            b.env[QS_E_TICK * kp.E + env] = fin ? 0 : tick;
+            if (fin) b.env[QS_E_EPISODE * kp.E + env] = episode + 1;
+            const int32_t nf = fin ? (QS_EF_STALE | QS_EF_HAS_POS) : ((eflags & ~QS_EF_STALE) | (success ? QS_EF_SUCCESS : 0));
+            if (nf != eflags) b.env[QS_E_FLAGS * kp.E + env] = nf;
+            if (repulsive) {
+                b.envf[QS_ENVF_TARGET_X * kp.E + env] = tx;
+                b.envf[QS_ENVF_TARGET_Y * kp.E + env] = ty;
+            }
+            b.rinfo[env] = fin ? (success ? 2 : 1) : 0;
+        }
+    }
+}
+
+// explicit reset of masked envs (quadrotor_multi_rewards.QuadrotorEnvMulti.reset)
+template <int NPAD>
+__global__ __launch_bounds__(64) void reset_kernel_a(const KP* __restrict__ kpp, Bufs b, uint32_t seed) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const KP& kp = *kpp;
+    constexpr int EPB = 64 / NPAD;
+    const int lane = threadIdx.x;
+    const int el = lane / NPAD, di = lane % NPAD;
+    const int env0 = blockIdx.x * EPB;
+    const int env = env0 + el;
+    const bool inr = env < kp.E && di < kp.N;
+    const bool envsel = env < kp.E && (b.mask == nullptr || b.mask[env] != 0);
+    const bool sel = inr && envsel;
+    const int g = inr ? env * kp.N + di : 0;
+    const uint32_t gid = kp.id0 + (uint32_t)g;
+    const int base = el * NPAD;
+    const int eidx = env < kp.E ? env : 0;
+    const int episode = b.env[QS_E_EPISODE * kp.E + eidx];
+    const int eflags = b.env[QS_E_FLAGS * kp.E + eidx];
+    const Rng rng = env_rng(seed, b.env[QS_E_TICK * kp.E + eidx], episode);
+    float* row = lds + (size_t)(el * kp.N + di) * kp.obs_dim;
+    Drone d;
+    load_drone(kp, b, g, d);
+    Ctl c;
+    load_ctl(kp, b, g, c);
+    float tx = b.envf[QS_ENVF_TARGET_X * kp.E + eidx], ty = b.envf[QS_ENVF_TARGET_Y * kp.E + eidx];
+    // stale QuadrotorEnvMulti.vel / .heading: last step's values unless a reset happened since
+    const bool stale_valid = eflags & QS_EF_STALE;
+    float sv[3], sh = stale_valid ? b.st[QS_F_HEADING * kp.I + g] : c.angle;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) sv[q] = stale_valid ? b.stale[q * kp.I + g] : d.vel[q];
+    const bool success = eflags & QS_EF_SUCCESS;
+    reset_env_a<NPAD>(kp, d, c, tx, ty, eflags & QS_EF_HAS_POS, inr, sel, rng, gid, kp.id0 + (uint32_t)(env * kp.N));
+    if (sel) self_obs_a(kp, d, c, d.goal[0], d.goal[1], rng, gid, S_RESET_SENSOR, S_RESET_SELF_CAM, row);
+    if (kp.K > 0) {
+        float4* xch = reinterpret_cast<float4*>(lds + 64 * kp.obs_dim);
+        xch_put_a(xch, lane, d.pos, sh, sv);
+        lds_sync();
+        neighbor_obs_a<NPAD>(kp, xch, base, di, d.pos, sh, c.angle, sv, rng, gid, true, sel, row);
+    }
+    lds_sync();
+    const int nenv_blk = min(EPB, kp.E - env0);
+    for (int r = 0; r < nenv_blk * kp.N; ++r) {
+        const int e = env0 + r / kp.N;
+        if (b.mask != nullptr && b.mask[e] == 0) continue;
+        for (int q = lane; q < kp.obs_dim; q += 64)
+            b.obs[(size_t)(env0 * kp.N + r) * kp.obs_dim + q] = lds[(size_t)r * kp.obs_dim + q];
+    }
+    if (env < kp.E && di == 0) b.rinfo[env] = envsel ? (success ? 2 : 1) : 0;
+    if (sel) {
+        store_drone(kp, b, g, d);
+        store_ctl(kp, b, g, c);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) b.stale[q * kp.I + g] = sv[q];
+        b.st[QS_F_HEADING * kp.I + g] = sh;
+        b.done[g] = 0;
+        if (di == 0) {
+            b.env[QS_E_TICK * kp.E + env] = 0;
+            b.env[QS_E_EPISODE * kp.E + env] = episode + 1;
+            b.env[QS_E_FLAGS * kp.E + env] = QS_EF_STALE | QS_EF_HAS_POS;
+            b.envf[QS_ENVF_TARGET_X * kp.E + env] = tx;
+            b.envf[QS_ENVF_TARGET_Y * kp.E + env] = ty;
+        }
+    }
+}
+
+}  // namespace qs

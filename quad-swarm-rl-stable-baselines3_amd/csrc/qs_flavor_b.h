@@ -1,0 +1,588 @@
+// qs_flavor_b.h -- flavor-B kernels (quadrotor_multi.QuadrotorEnvMulti: raw motor commands, shaped
+// rewards, drone/room impulses, pos_vel neighbour obs, in-env auto-reset).  Included by qs_step.hip.
+#pragma once
+#include "qs_common.h"
+
+namespace qs {
+
+// ---------------------------------------------------------------------------------------------
+// observations
+// ---------------------------------------------------------------------------------------------
+// sensor noise (add_noise_numba sensor_noise.py:172-218) + state_xyz_vxyz_R_omega[_floor|_wall]
+// (get_state.py:226-292), written to an LDS row.
+__device__ void self_obs(const KP& kp, const Drone& d, const Rng& rng, uint32_t gid, uint32_t stream, float* out) {
+    float np_[3], nv[3], no[3], nr[9];
+    if (kp.sense) {
+        float z[12];
+        normals4(rng, gid, stream, 0, z);
+        normals4(rng, gid, stream, 1, z + 4);
+        normals4(rng, gid, stream, 2, z + 8);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            np_[i] = d.pos[i] + kp.pos_std * z[i];
+            nv[i] = d.vel[i] + kp.vel_std * z[3 + i];
+            no[i] = d.om[i] + kp.gyro * z[6 + i];
+        }
+        float th[3] = {0.f, 0.f, 0.f};
+        if (kp.pos_unif != 0.f || kp.vel_unif != 0.f || kp.quat_unif != 0.f) {
+            float u[12];
+            uniforms4(rng, gid, stream, 0, u);
+            uniforms4(rng, gid, stream, 1, u + 4);
+            uniforms4(rng, gid, stream, 2, u + 8);
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                np_[i] += -kp.pos_unif + 2.f * kp.pos_unif * u[i];
+                nv[i] += -kp.vel_unif + 2.f * kp.vel_unif * u[3 + i];
+                th[i] = -kp.quat_unif + 2.f * kp.quat_unif * u[6 + i];
+            }
+        }
+        if (kp.quat_std != 0.f) {
+            float zq[4];
+            normals4(rng, gid, stream, 2, zq);  // normals 9..11 live in block 2, words 1..3
+#pragma unroll
+            for (int i = 0; i < 3; ++i) th[i] = kp.quat_std * zq[1 + i] + th[i];
+        }
+        // quat_from_small_angle (sensor_noise.py:11-23)
+        const float q2 = (th[0] * th[0] + th[1] * th[1] + th[2] * th[2]) * 0.25f;
+        float qt[4];
+        if (q2 < 1.f) {
+            qt[0] = fsqrt(1.f - q2); qt[1] = th[0] * 0.5f; qt[2] = th[1] * 0.5f; qt[3] = th[2] * 0.5f;
+        } else {
+            const float w = rsqrtf(1.f + q2), f = 0.5f * w;
+            qt[0] = w; qt[1] = th[0] * f; qt[2] = th[1] * f; qt[3] = th[2] * f;
+        }
+        const float qn = frcp(fsqrt(qt[0] * qt[0] + qt[1] * qt[1] + qt[2] * qt[2] + qt[3] * qt[3]));
+#pragma unroll
+        for (int i = 0; i < 4; ++i) qt[i] *= qn;
+        // rot2quat (sensor_noise.py:34-63)
+        const float* R = d.rot;
+        float q[4];
+        const float tr = R[0] + R[4] + R[8];
+        if (tr > 0.f) {
+            const float S = fsqrt(tr + 1.f) * 2.f, iS = frcp(S);
+            q[0] = 0.25f * S; q[1] = (R[7] - R[5]) * iS; q[2] = (R[2] - R[6]) * iS; q[3] = (R[3] - R[1]) * iS;
+        } else if (R[0] > R[4] && R[0] > R[8]) {
+            const float S = fsqrt(1.f + R[0] - R[4] - R[8]) * 2.f, iS = frcp(S);
+            q[0] = (R[7] - R[5]) * iS; q[1] = 0.25f * S; q[2] = (R[1] + R[3]) * iS; q[3] = (R[2] + R[6]) * iS;
+        } else if (R[4] > R[8]) {
+            const float S = fsqrt(1.f + R[4] - R[0] - R[8]) * 2.f, iS = frcp(S);
+            q[0] = (R[2] - R[6]) * iS; q[1] = (R[1] + R[3]) * iS; q[2] = 0.25f * S; q[3] = (R[5] + R[7]) * iS;
+        } else {
+            const float S = fsqrt(1.f + R[8] - R[0] - R[4]) * 2.f, iS = frcp(S);
+            q[0] = (R[3] - R[1]) * iS; q[1] = (R[2] + R[6]) * iS; q[2] = (R[5] + R[7]) * iS; q[3] = 0.25f * S;
+        }
+        // quatXquat + quat2R (quad_utils.py:146-174)
+        const float w = q[0] * qt[0] - q[1] * qt[1] - q[2] * qt[2] - q[3] * qt[3];
+        const float x = q[0] * qt[1] + q[1] * qt[0] - q[2] * qt[3] + q[3] * qt[2];
+        const float y = q[0] * qt[2] + q[1] * qt[3] + q[2] * qt[0] - q[3] * qt[1];
+        const float zz = q[0] * qt[3] - q[1] * qt[2] + q[2] * qt[1] + q[3] * qt[0];
+        nr[0] = 1.f - 2.f * y * y - 2.f * zz * zz; nr[1] = 2.f * x * y - 2.f * zz * w; nr[2] = 2.f * x * zz + 2.f * y * w;
+        nr[3] = 2.f * x * y + 2.f * zz * w; nr[4] = 1.f - 2.f * x * x - 2.f * zz * zz; nr[5] = 2.f * y * zz - 2.f * x * w;
+        nr[6] = 2.f * x * zz - 2.f * y * w; nr[7] = 2.f * y * zz + 2.f * x * w; nr[8] = 1.f - 2.f * x * x - 2.f * y * y;
+    } else {
+#pragma unroll
+        for (int i = 0; i < 3; ++i) { np_[i] = d.pos[i]; nv[i] = d.vel[i]; no[i] = d.om[i]; }
+#pragma unroll
+        for (int i = 0; i < 9; ++i) nr[i] = d.rot[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        out[i] = np_[i] - d.goal[i];
+        out[3 + i] = nv[i];
+        out[15 + i] = no[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 9; ++i) out[6 + i] = nr[i];
+    if (kp.obs_repr == QS_OBS_XYZ_VXYZ_R_OMEGA_FLOOR) out[18] = np_[2];
+    if (kp.obs_repr == QS_OBS_XYZ_VXYZ_R_OMEGA_WALL) {
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            out[18 + i] = clampf(np_[i] - kp.room_lo[i], 0.f, 5.f);
+            out[21 + i] = clampf(kp.room_hi[i] - np_[i], 0.f, 5.f);
+        }
+    }
+}
+
+__device__ __forceinline__ void xch_put(float4* xch, int lane, const float* P, const float* V) {
+    xch[2 * lane] = make_float4(P[0], P[1], P[2], 0.f);
+    xch[2 * lane + 1] = make_float4(V[0], V[1], V[2], 0.f);
+}
+
+// pos_vel neighbour obs: neighborhood_indices (quadrotor_multi.py:344-375) + extend_obs_space
+// clip (:328-342).  Key = |[rel_pos, rel_vel]| clamped at 0.01 (compared squared, clamp 1e-4);
+// stable (index) tie-break like numpy's insertion sort; k == N-1 keeps index order (all keys 0).
+// Reads the exchange tile (caller has synchronised); only lanes with write == true store.
+template <int NPAD>
+__device__ void neighbor_obs(const KP& kp, const float4* xch, int base, int di, const float* P, const float* V,
+                             bool write, float* out) {
+    constexpr bool KEEP = NPAD <= 8;  // small swarms keep the relative vectors in VGPRs between passes
+    float key[NPAD];
+    float rel[KEEP ? NPAD : 1][6];
+    const bool sorted = kp.K < kp.N - 1;
+#pragma unroll
+    for (int j = 0; j < NPAD; ++j) {
+        const float4 pj = xch[2 * (base + j)], vj = xch[2 * (base + j) + 1];
+        const float r[6] = {pj.x - P[0], pj.y - P[1], pj.z - P[2], vj.x - V[0], vj.y - V[1], vj.z - V[2]};
+        const float s = r[0] * r[0] + r[1] * r[1] + r[2] * r[2] + r[3] * r[3] + r[4] * r[4] + r[5] * r[5];
+        const bool valid = (j != di) && (j < kp.N);
+        key[j] = valid ? (sorted ? fmaxf(s, 1e-4f) : 0.f) : __builtin_inff();
+        if (KEEP) {
+#pragma unroll
+            for (int c = 0; c < 6; ++c) rel[KEEP ? j : 0][c] = r[c];
+        }
+    }
+    if (!write) return;
+    const float vm = 2.f * kp.vxyz_max;
+    const bool pairs = ((kp.so_dim | kp.obs_dim) & 1) == 0;   // 8-byte aligned slots: ds_write_b64
+#pragma unroll
+    for (int j = 0; j < NPAD; ++j) {
+        int rank = 0;
+#pragma unroll
+        for (int m = 0; m < NPAD; ++m) rank += (key[m] < key[j]) || (m < j && key[m] == key[j]);
+        if (key[j] != __builtin_inff() && rank < kp.K) {
+            float r[6];
+            if (KEEP) {
+#pragma unroll
+                for (int c = 0; c < 6; ++c) r[c] = rel[KEEP ? j : 0][c];
+            } else {
+                const float4 pj = xch[2 * (base + j)], vj = xch[2 * (base + j) + 1];
+                r[0] = pj.x - P[0]; r[1] = pj.y - P[1]; r[2] = pj.z - P[2];
+                r[3] = vj.x - V[0]; r[4] = vj.y - V[1]; r[5] = vj.z - V[2];
+            }
+            const float o0 = clampf(r[0], -kp.room_range[0], kp.room_range[0]);
+            const float o1 = clampf(r[1], -kp.room_range[1], kp.room_range[1]);
+            const float o2 = clampf(r[2], -kp.room_range[2], kp.room_range[2]);
+            const float o3 = clampf(r[3], -vm, vm), o4 = clampf(r[4], -vm, vm), o5 = clampf(r[5], -vm, vm);
+            float* o = out + kp.so_dim + rank * 6;
+            if (pairs) {
+                float2* o2p = reinterpret_cast<float2*>(o);
+                o2p[0] = make_float2(o0, o1);
+                o2p[1] = make_float2(o2, o3);
+                o2p[2] = make_float2(o4, o5);
+            } else {
+                o[0] = o0; o[1] = o1; o[2] = o2; o[3] = o3; o[4] = o4; o[5] = o5;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// interactions
+// ---------------------------------------------------------------------------------------------
+// compute_new_vel (collisions/utils.py:7-20)
+__device__ __forceinline__ void new_vel(float maxv, float* v, const float* sh, float ratio) {
+    const float n0 = v[0] + sh[0], n1 = v[1] + sh[1], n2 = v[2] + sh[2];
+    const float mag = fsqrt(n0 * n0 + n1 * n1 + n2 * n2);
+    const float inv = frcp(mag == 0.f ? 1e-5f : mag);
+    const float nm = fminf(mag * ratio, maxv);
+    v[0] += n0 * inv * nm - v[0];
+    v[1] += n1 * inv * nm - v[1];
+    v[2] += n2 * inv * nm - v[2];
+}
+
+// perform_collision_between_drones (collisions/quadrotors.py:23-59) for the pair (1 = lower id).
+// Both lanes of the pair evaluate it with identical inputs and draws (key = lower drone, stream j).
+__device__ void collide_pair(const float* p1, float* v1, float* w1, const float* p2, float* v2, float* w2,
+                             const Rng& rng, uint32_t gid, uint32_t j) {
+    const uint32_t st = S_PAIR | (j << 8);
+    float n[3] = {p1[0] - p2[0], p1[1] - p2[1], p1[2] - p2[2]};
+    const float m = fsqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+    const float im = frcp(m == 0.f ? 1e-5f : m);
+    n[0] *= im; n[1] *= im; n[2] *= im;
+    const float v1n = v1[0] * n[0] + v1[1] * n[1] + v1[2] * n[2];
+    const float v2n = v2[0] * n[0] + v2[1] * n[1] + v2[2] * n[2];
+    float vc[3], s1[3], s2[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) { vc[i] = (v2n - v1n) * n[i]; s1[i] = vc[i]; s2[i] = -vc[i]; }
+    for (int t = 0; t < 3; ++t) {  // "make sure new vel direction would be opposite" rejection, 3 tries
+        float z[12];  // normals t*9 .. t*9+8 lie in blocks (t*9)/4 .. (t*9+8)/4
+        const uint32_t b0 = (uint32_t)(t * 9) >> 2, off = (uint32_t)(t * 9) & 3;
+        normals4(rng, gid, st, b0, z);
+        normals4(rng, gid, st, b0 + 1, z + 4);
+        normals4(rng, gid, st, b0 + 2, z + 8);
+        float d1 = 0.f, d2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const float cons = 0.8f * z[off + i], a = 0.15f * z[off + 3 + i], bb = 0.15f * z[off + 6 + i];
+            s1[i] = vc[i] + (cons + a);
+            s2[i] = -vc[i] + (-cons + bb);
+            d1 += (v1[i] + s1[i]) * n[i];
+            d2 += (v2[i] + s2[i]) * n[i];
+        }
+        if (d1 > 0.f && 0.f > d2) break;
+    }
+    const float mx = fmaxf(fsqrt(v1[0] * v1[0] + v1[1] * v1[1] + v1[2] * v1[2]),
+                           fsqrt(v2[0] * v2[0] + v2[1] * v2[1] + v2[2] * v2[2]));
+    float u[8];
+    uniforms4(rng, gid, st, 0, u);
+    uniforms4(rng, gid, st, 1, u + 4);
+    new_vel(mx, v1, s1, 0.2f + 0.6f * u[0]);
+    new_vel(mx, v2, s2, 0.2f + 0.6f * u[1]);
+    // compute_new_omega (collisions/utils.py:23-33), magn_scale 20
+    const float om = 20.f * 3.14159265358979f;
+    float w[3] = {-1.f + 2.f * u[2], -1.f + 2.f * u[3], -1.f + 2.f * u[4]};
+    const float wm = fsqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+    const float iw = frcp(wm == 0.f ? 1e-5f : wm);
+    const float mg = om * 0.5f + (om - om * 0.5f) * u[5];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const float x = w[i] * iw * mg;
+        w1[i] += x;
+        w2[i] -= x;
+    }
+}
+
+// perform_collision_with_wall (collisions/room.py:6-44) / _with_ceiling (:91-113)
+__device__ void collide_room(const KP& kp, Drone& d, const Rng& rng, uint32_t gid, bool wall) {
+    const uint32_t st = wall ? S_WALL : S_CEIL;
+    float u[12];
+    uniforms4(rng, gid, st, 0, u);
+    uniforms4(rng, gid, st, 1, u + 4);
+    uniforms4(rng, gid, st, 2, u + 8);
+    const float sp = fsqrt(d.vel[0] * d.vel[0] + d.vel[1] * d.vel[1] + d.vel[2] * d.vel[2]);
+    const float real = clampf(0.2f * sp + (0.8f * sp - 0.2f * sp) * u[0], 0.1f, 6.0f);
+    float dir[3] = {-1.f + 2.f * u[1], -1.f + 2.f * u[2], -1.f + 2.f * u[3]};
+    int ow;
+    if (wall) {
+        if (d.pos[0] == kp.room_lo[0]) dir[0] = 0.1f + 0.9f * u[4];
+        else if (d.pos[0] == kp.room_hi[0]) dir[0] = -1.f + 0.9f * u[4];
+        if (d.pos[1] == kp.room_lo[1]) dir[1] = 0.1f + 0.9f * u[5];
+        else if (d.pos[1] == kp.room_hi[1]) dir[1] = -1.f + 0.9f * u[5];
+        dir[2] = -1.f + 0.5f * u[6];
+        ow = 7;
+    } else {
+        dir[2] = -1.f + 0.5f * u[4];
+        ow = 5;
+    }
+    const float idm = frcp(fsqrt(dir[0] * dir[0] + dir[1] * dir[1] + dir[2] * dir[2]) + 1e-5f);
+    float w[3] = {-1.f + 2.f * u[ow], -1.f + 2.f * u[ow + 1], -1.f + 2.f * u[ow + 2]};
+    const float iw = frcp(fsqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]) + 1e-5f);
+    const float om = 20.f * 3.14159265358979f;
+    const float mg = om * 0.5f + (om - om * 0.5f) * u[ow + 3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        d.vel[i] = real * (dir[i] * idm);
+        d.om[i] += w[i] * iw * mg;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// reset (QuadrotorSingle._reset quadrotor_single.py:401-469 with static_same_goal goals)
+// ---------------------------------------------------------------------------------------------
+__device__ void reset_drone(const KP& kp, Drone& d, const Rng& rng, uint32_t gid) {
+    float u[4];
+    uniforms4(rng, gid, S_RESET, 0, u);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        d.goal[i] = kp.goal[i];
+        d.pos[i] = (-kp.spawn_box + 2.f * kp.spawn_box * u[i]) + d.goal[i];
+        d.vel[i] = 0.f;
+        d.om[i] = 0.f;
+    }
+    if (d.pos[2] < 0.75f) d.pos[2] = 0.75f;
+    // randyaw rejection until the body x axis points within 60 deg of the origin (:454-456)
+    float tx = -d.pos[0], ty = -d.pos[1];
+    const float tn = fsqrt(tx * tx + ty * ty);
+    const bool degenerate = tn < 1e-5f;
+    tx = degenerate ? 0.f : tx / tn;
+    ty = degenerate ? 0.f : ty / tn;
+    float yaw = 0.f;
+    for (uint32_t blk = 0; blk < 64; ++blk) {
+        float y[4];
+        uniforms4(rng, gid, S_RESET_YAW, blk, y);
+        bool found = false;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if (found) continue;
+            const float cand = -3.14159265358979f + 6.28318530717959f * y[i];
+            float s, c;
+            sincosf(cand, &s, &c);
+            yaw = cand;
+            if (c * tx + s * ty >= 0.5f || degenerate) found = true;
+        }
+        if (found) break;
+    }
+    yaw_rot(yaw, d.rot);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { d.rd[k] = 0.f; d.cd[k] = 0.f; }
+    d.flags = 0;
+    d.prev = 0;
+}
+
+template <int NPAD>
+__global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bufs b, uint32_t seed) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const KP& kp = *kpp;
+    QS_STAMP_DECL
+    QS_STAMP(0);
+    constexpr int EPB = 64 / NPAD;
+    const int lane = threadIdx.x;
+    const int el = lane / NPAD, di = lane % NPAD;
+    const int env0 = blockIdx.x * EPB;
+    const int env = env0 + el;
+    const bool active = env < kp.E && di < kp.N;
+    const int g = active ? env * kp.N + di : 0;
+    const uint32_t gid = kp.id0 + (uint32_t)g;
+    const int base = el * NPAD;
+    const int nenv_blk = min(EPB, kp.E - env0);
+    const int rows = nenv_blk * kp.N;
+    float* row = lds + (size_t)(el * kp.N + di) * kp.obs_dim;
+    float4* xch = reinterpret_cast<float4*>(lds + 64 * kp.obs_dim);
+
+    Drone d;
+    load_drone(kp, b, g, d);
+    float a[4];
+    {
+        const float4 av = reinterpret_cast<const float4*>(b.act)[g];
+        a[0] = av.x; a[1] = av.y; a[2] = av.z; a[3] = av.w;
+    }
+    const int eidx = active ? env : 0;
+    const int tick0 = b.env[QS_E_TICK * kp.E + eidx];
+    const int episode = b.env[QS_E_EPISODE * kp.E + eidx];
+    const Rng rng = env_rng(seed, tick0, episode);
+    const int tick = tick0 + 1;
+    const bool done = tick > kp.ep_len;
+
+    QS_STAMP(1);
+    // ---- per-drone control + physics (QuadrotorSingle._step) ----
+    float rw = 0.f;
+    {
+        float z[4];
+        normals4(rng, gid, S_OU, 0, z);  // OUNoiseNumba.noise, once per control step (:216)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) d.ou[k] = d.ou[k] + (kp.ou_theta * (kp.ou_mu - d.ou[k]) + kp.ou_sigma * z[k]);
+        float cmds[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) cmds[k] = 0.5f * (clampf(a[k], -1.f, 1.f) + 1.f);
+        for (int s = 0; s < kp.sim_steps; ++s) substep(kp, d, cmds, d.ou, rng, gid, s);
+        // compute_reward_weighted (quadrotor_single.py:34-66)
+        const float gx = d.goal[0] - d.pos[0], gy = d.goal[1] - d.pos[1], gz = d.goal[2] - d.pos[2];
+        const bool on_floor = d.flags & QS_FL_ON_FLOOR;
+        const float cost = kp.rew_pos * fsqrt(gx * gx + gy * gy + gz * gz) +
+                           kp.rew_effort * fsqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2] + a[3] * a[3]) +
+                           kp.rew_crash * (on_floor ? 1.f : 0.f) + kp.rew_orient * (on_floor ? 1.f : -d.rot[8]) +
+                           kp.rew_spin * fsqrt(d.om[0] * d.om[0] + d.om[1] * d.om[1] + d.om[2] * d.om[2]);
+        rw = -kp.dt * cost;
+    }
+
+    QS_STAMP(2);
+    // ---- swarm phase: collisions + proximity (quadrotor_multi.py:537-568, 608-622) ----
+    uint64_t cur = 0;
+    float pen = 0.f;
+    xch_put(xch, lane, d.pos, d.vel);
+    lds_sync();
+    if (kp.N > 1) {
+#pragma unroll
+        for (int j = 0; j < NPAD; ++j) {
+            const float4 pj = xch[2 * (base + j)];
+            const float dx = d.pos[0] - pj.x, dy = d.pos[1] - pj.y, dz = d.pos[2] - pj.z;
+            const float dist = fsqrt(dx * dx + dy * dy + dz * dz);
+            if (j != di && j < kp.N) {
+                if (dist <= kp.col_thr) cur |= 1ull << j;
+                if (dist <= kp.fall_thr) pen += kp.prox_ratio * dist + kp.prox_max;
+            }
+        }
+    }
+    const uint64_t newpairs = cur & ~d.prev;
+    // setdiff1d(flat(cur), flat(prev)) and its ".any()" (drone 0 alone does not count)
+    const bool uniq = active && cur != 0 && d.prev == 0;
+    const uint64_t ub = __ballot(uniq && di != 0);
+    const uint64_t gmask = (NPAD == 64) ? ~0ull : ((1ull << NPAD) - 1ull);
+    const bool any_uniq = ((ub >> base) & gmask) != 0;
+    rw += kp.quadcol * ((any_uniq && uniq) ? -1.f : 0.f);
+    rw += -(kp.cdt * pen);
+    // room: new wall / ceiling crashes vs the previous NEW lists (:390-403, :604-605)
+    const bool wall_new = (d.flags & QS_FL_CRASH_WALL) && !(d.flags & QS_FL_PREV_WALL);
+    const bool ceil_new = (d.flags & QS_FL_CRASH_CEIL) && !(d.flags & QS_FL_PREV_CEIL);
+    d.flags = (d.flags & ~(uint32_t)(QS_FL_PREV_WALL | QS_FL_PREV_CEIL)) | (wall_new ? QS_FL_PREV_WALL : 0u) |
+              (ceil_new ? QS_FL_PREV_CEIL : 0u);
+
+    QS_STAMP(3);
+    // ---- random forces (:659-698) ----
+    bool vchanged = false;
+    if (kp.downwash && kp.N > 1) {  // perform_downwash (aerodynamics/downwash.py:4-51)
+        float dwu[4];
+        uniforms4(rng, gid, S_DW, 0, dwu);
+        const float an = -0.1f + 0.2f * dwu[0], wn = -0.01f + 0.02f * dwu[1];
+        const float P0 = d.pos[0], P1 = d.pos[1], P2 = d.pos[2];
+        for (int i = 0; i < NPAD; ++i) {
+            const float zi0 = __shfl(d.rot[2], base + i), zi1 = __shfl(d.rot[5], base + i), zi2 = __shfl(d.rot[8], base + i);
+            const float pi0 = __shfl(P0, base + i), pi1 = __shfl(P1, base + i), pi2 = __shfl(P2, base + i);
+            const float ani = __shfl(an, base + i), wni = __shfl(wn, base + i);
+            if (!active || i >= kp.N || i == di) continue;
+            const float r0 = P0 - pi0, r1 = P1 - pi1, r2 = P2 - pi2;
+            const float dist = fsqrt(r0 * r0 + r1 * r1 + r2 * r2);
+            const float rz = r0 * zi0 + r1 * zi1 + r2 * zi2;
+            const float rxy = fsqrt(dist * dist - rz * rz);
+            if (-0.7f < rz && rz < 0.f && rxy < 0.1f) {
+                const float acc = fmaxf((6.f / 17.f) * (-10.f * dist + 7.f) + ani, 1e-6f);
+                const float wd = fmaxf(0.3f * (dist - 1.f) * (dist - 1.f) + wni, 1e-6f);
+                float u[8];
+                const uint32_t gi = kp.id0 + (uint32_t)(env * kp.N + i);
+                uniforms4(rng, gi, S_DWPAIR | ((uint32_t)di << 8), 0, u);
+                uniforms4(rng, gi, S_DWPAIR | ((uint32_t)di << 8), 1, u + 4);
+                float nz[3] = {zi0 - 0.1f + 0.2f * u[0], zi1 - 0.1f + 0.2f * u[1], zi2 - 0.1f + 0.2f * u[2]};
+                const float nm = fsqrt(nz[0] * nz[0] + nz[1] * nz[1] + nz[2] * nz[2]);
+                const float inz = frcp(nm == 0.f ? 1e-6f : nm);
+                float dw[3] = {-1.f + 2.f * u[3], -1.f + 2.f * u[4], -1.f + 2.f * u[5]};
+                const float dm = fsqrt(dw[0] * dw[0] + dw[1] * dw[1] + dw[2] * dw[2]);
+                const float idw = frcp(dm == 0.f ? 1e-6f : dm);
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    d.vel[c] += acc * (-(nz[c] * inz)) * kp.cdt;
+                    d.om[c] += wd * (dw[c] * idw) * kp.cdt;
+                }
+                vchanged = true;
+            }
+        }
+    }
+    if (kp.collide) {
+        // drone-drone impulses, pairs in (i, j) order; a wave-uniform loop over pending events
+        uint64_t pend = active ? (newpairs & ~((2ull << di) - 1ull)) : 0ull;
+        for (;;) {
+            const uint64_t bal = __ballot(pend != 0ull);
+            if (bal == 0ull) break;
+            const uint64_t eb = (bal >> base) & gmask;
+            const int istar = eb ? (__ffsll((long long)eb) - 1) : 0;
+            const int myj = pend ? (__ffsll((long long)pend) - 1) : 0;
+            const int jstar = __shfl(myj, base + istar);
+            const int partner = (di == istar) ? jstar : istar;
+            float pp[3], pv[3], pw[3];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                pp[c] = __shfl(d.pos[c], base + partner);
+                pv[c] = __shfl(d.vel[c], base + partner);
+                pw[c] = __shfl(d.om[c], base + partner);
+            }
+            const bool involved = eb != 0 && (di == istar || di == jstar);
+            vchanged |= involved;
+            if (involved) {
+                const uint32_t gi = kp.id0 + (uint32_t)(env * kp.N + istar);
+                if (di == istar) collide_pair(d.pos, d.vel, d.om, pp, pv, pw, rng, gi, (uint32_t)jstar);
+                else collide_pair(pp, pv, pw, d.pos, d.vel, d.om, rng, gi, (uint32_t)jstar);
+            }
+            if (eb != 0 && di == istar) pend &= ~(1ull << jstar);
+        }
+        if (active && wall_new) collide_room(kp, d, rng, gid, true);
+        if (active && ceil_new) collide_room(kp, d, rng, gid, false);
+        vchanged |= active && (wall_new || ceil_new);
+    }
+    d.prev = cur;
+
+    QS_STAMP(4);
+    // ---- observations (post-impulse state; quadrotor_multi.py:704-720) ----
+    const bool nbr = kp.neighbor == QS_NEIGHBOR_POS_VEL && kp.K > 0;
+    if (nbr && __ballot(vchanged)) {  // impulses changed velocities: refresh the tile
+        lds_sync();
+        xch_put(xch, lane, d.pos, d.vel);
+        lds_sync();
+    }
+    QS_STAMP(5);
+    if (active) self_obs(kp, d, rng, gid, S_SENSOR, row);
+    QS_STAMP(6);
+    if (nbr) neighbor_obs<NPAD>(kp, xch, base, di, d.pos, d.vel, active, row);
+    QS_STAMP(7);
+
+    const uint64_t dball = __ballot(active && done);
+    if (dball) {  // rare: some env of this block finished -> terminal obs + fused auto-reset (:739-838)
+        lds_sync();
+        for (int r = 0; r < rows; ++r) {
+            const int e = env0 + r / kp.N;
+            if (b.env[QS_E_TICK * kp.E + e] + 1 <= kp.ep_len) continue;
+            for (int c = lane; c < kp.obs_dim; c += 64)
+                b.term[(size_t)(env0 * kp.N + r) * kp.obs_dim + c] = lds[(size_t)r * kp.obs_dim + c];
+        }
+        lds_sync();
+        float sv[3] = {d.vel[0], d.vel[1], d.vel[2]};  // QuadrotorEnvMulti.vel seen by the reset (:477)
+        if (active && done) {
+            b.stale[0 * kp.I + g] = sv[0];
+            b.stale[1 * kp.I + g] = sv[1];
+            b.stale[2 * kp.I + g] = sv[2];
+            reset_drone(kp, d, rng, gid);
+            self_obs(kp, d, rng, gid, S_RESET_SENSOR, row);
+        }
+        if (nbr) {
+            xch_put(xch, lane, d.pos, sv);
+            lds_sync();
+            neighbor_obs<NPAD>(kp, xch, base, di, d.pos, sv, active && done, row);
+        }
+    }
+    lds_sync();
+    QS_STAMP(8);
+    tile_store(lds, b.obs + (size_t)env0 * kp.N * kp.obs_dim, rows * kp.obs_dim, lane);
+    QS_STAMP(9);
+
+    if (active) {
+        store_drone(kp, b, g, d);
+        b.rew[g] = rw;
+        b.done[g] = done ? 1 : 0;
+        if (di == 0) {
+            b.env[QS_E_TICK * kp.E + env] = done ? 0 : tick;
+            if (done) b.env[QS_E_EPISODE * kp.E + env] = episode + 1;
+            const int32_t ef = b.env[QS_E_FLAGS * kp.E + env];
+            const int32_t nf = done ? (ef | 1) : (ef & ~1);
+            if (nf != ef) b.env[QS_E_FLAGS * kp.E + env] = nf;
+        }
+    }
+    QS_STAMP(10);
+    QS_STAMP(11);
+    QS_STAMP_FLUSH();
+}
+
+// explicit reset of masked envs (QuadrotorEnvMulti.reset quadrotor_multi.py:440-517)
+template <int NPAD>
+__global__ __launch_bounds__(64) void reset_kernel(const KP* __restrict__ kpp, Bufs b, uint32_t seed) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const KP& kp = *kpp;
+    constexpr int EPB = 64 / NPAD;
+    const int lane = threadIdx.x;
+    const int el = lane / NPAD, di = lane % NPAD;
+    const int env0 = blockIdx.x * EPB;
+    const int env = env0 + el;
+    const bool inr = env < kp.E && di < kp.N;
+    const bool sel = inr && (b.mask == nullptr || b.mask[env] != 0);
+    const int g = inr ? env * kp.N + di : 0;
+    const int base = el * NPAD;
+    const int eidx = inr ? env : 0;
+    const int episode = b.env[QS_E_EPISODE * kp.E + eidx];
+    const Rng rng = env_rng(seed, b.env[QS_E_TICK * kp.E + eidx], episode);
+    float* row = lds + (size_t)(el * kp.N + di) * kp.obs_dim;
+    Drone d;
+    load_drone(kp, b, g, d);
+    // stale QuadrotorEnvMulti.vel: the state's vel unless a reset already happened since the last step
+    const bool stale_valid = inr && (b.env[QS_E_FLAGS * kp.E + env] & 1);
+    float sv[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) sv[c] = stale_valid ? b.stale[c * kp.I + g] : d.vel[c];
+    if (sel) {
+        reset_drone(kp, d, rng, kp.id0 + (uint32_t)g);
+        self_obs(kp, d, rng, kp.id0 + (uint32_t)g, S_RESET_SENSOR, row);
+    }
+    if (kp.neighbor == QS_NEIGHBOR_POS_VEL && kp.K > 0) {
+        float4* xch = reinterpret_cast<float4*>(lds + 64 * kp.obs_dim);
+        xch_put(xch, lane, d.pos, sv);
+        lds_sync();
+        neighbor_obs<NPAD>(kp, xch, base, di, d.pos, sv, sel, row);
+    }
+    lds_sync();
+    const int nenv_blk = min(EPB, kp.E - env0);
+    for (int r = 0; r < nenv_blk * kp.N; ++r) {
+        const int e = env0 + r / kp.N;
+        if (b.mask != nullptr && b.mask[e] == 0) continue;
+        for (int c = lane; c < kp.obs_dim; c += 64)
+            b.obs[(size_t)(env0 * kp.N + r) * kp.obs_dim + c] = lds[(size_t)r * kp.obs_dim + c];
+    }
+    if (sel) {
+        store_drone(kp, b, g, d);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) b.stale[c * kp.I + g] = sv[c];
+        b.done[g] = 0;
+        if (di == 0) {
+            b.env[QS_E_TICK * kp.E + env] = 0;
+            b.env[QS_E_EPISODE * kp.E + env] = episode + 1;
+            b.env[QS_E_FLAGS * kp.E + env] |= 1;
+        }
+    }
+}
+
+}  // namespace qs

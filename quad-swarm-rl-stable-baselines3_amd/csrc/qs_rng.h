@@ -16,7 +16,11 @@ namespace qs {
 
 enum : uint32_t {
     S_OU = 1, S_FLOOR = 2, S_SENSOR = 3, S_PAIR = 4, S_WALL = 5, S_CEIL = 6, S_DW = 7, S_DWPAIR = 8,
-    S_RESET = 9, S_RESET_YAW = 10, S_RESET_SENSOR = 11, S_OBST = 12, UNIF_BIT = 0x80
+    S_RESET = 9, S_RESET_YAW = 10, S_RESET_SENSOR = 11, S_OBST = 12,
+    // flavor A: camera pixel noise (normals 0 = u1, 1 = u2; | neighbour j << 8), spawn / heading draws
+    S_CAM = 13, S_CAM_SEL = 14, S_SELF_CAM = 15, S_RESET_A = 16, S_SCEN = 17, S_RESET_CAM = 18,
+    S_RESET_CAM_SEL = 19, S_RESET_SELF_CAM = 20,
+    UNIF_BIT = 0x80
 };
 
 struct Rng {

@@ -9,18 +9,30 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("QUADSWARM_LIB", os.path.join(HERE, "lib", "libquadswarm.so"))
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 MAX_AGENTS = 32
 F, I32, U32, U64, SZ = ctypes.c_float, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_size_t
 
 # enum values (quadswarm.h)
-OBS_REPR = {"xyz_vxyz_R_omega": 0, "xyz_vxyz_R_omega_floor": 1, "xyz_vxyz_R_omega_wall": 2}
-SELF_OBS_DIM = {0: 18, 1: 19, 2: 24}
+FLAVOR_B, FLAVOR_A = 0, 1
+OBS_REPR = {"xyz_vxyz_R_omega": 0, "xyz_vxyz_R_omega_floor": 1, "xyz_vxyz_R_omega_wall": 2,
+            "aw_awdot_dist_distdot_angle_angledot": 3, "cdist_cdistdot_dist_distdot_angle_angledot": 4,
+            "cdist_cdistdot_dist_distdot_sangle_angledot": 5, "cdist_cdistdot_ndist_distdot_nsangle_angledot": 6}
+OBS_REPR_B = (0, 1, 2)
+OBS_REPR_A = (3, 4, 5, 6)
+SELF_OBS_DIM = {0: 18, 1: 19, 2: 24, 3: 6, 4: 6, 5: 7, 6: 7}
 NEIGHBOR_NONE, NEIGHBOR_POS_VEL = 0, 1
-F_POS, F_VEL, F_ROT, F_OMEGA, F_ROT_DAMP, F_CMD_DAMP, F_OU, F_GOAL, NF = 0, 3, 6, 15, 18, 22, 26, 30, 33
+NEIGHBOR = {"none": 0, "pos_vel": 1, "dist_angle": 2, "dist_sangle": 3, "ndist_nsangle": 4, "dist_angle_heading": 5,
+            "dist_sangle_sheading": 6, "pos": 7, "npos": 8}
+NEIGHBOR_DIM = {0: 0, 1: 6, 2: 2, 3: 3, 4: 3, 5: 3, 6: 5, 7: 3, 8: 3}
+SCENARIO = {"static_same_goal": 0, "dynamic_repulsive": 1}
+F_POS, F_VEL, F_ROT, F_OMEGA, F_ROT_DAMP, F_CMD_DAMP, F_OU, F_GOAL = 0, 3, 6, 15, 18, 22, 26, 30
+F_PID, F_ANGLE, F_ANGVEL, F_HEADING, NF = 33, 53, 54, 55, 56
 I_SVD, I_FLAGS, I_PREV_LO, I_PREV_HI, NI = 0, 1, 2, 3, 4
 FL_ON_FLOOR, FL_PREV_WALL, FL_PREV_CEIL, FL_CRASH_FLOOR, FL_CRASH_WALL, FL_CRASH_CEIL = 1, 2, 4, 8, 16, 32
 E_TICK, E_FLAGS, E_EPISODE, NE = 0, 1, 2, 3
+EF_STALE, EF_SUCCESS, EF_HAS_POS = 1, 2, 4
+ENVF_TARGET_X, ENVF_TARGET_Y, ENVF_CAPTURE, NENVF = 0, 1, 2, 3
 
 
 class QsConfig(ctypes.Structure):
@@ -41,16 +53,20 @@ class QsConfig(ctypes.Structure):
         ("rew_pos", F), ("rew_effort", F), ("rew_crash", F), ("rew_orient", F), ("rew_spin", F),
         ("rew_quadcol_bin", F), ("rew_quadcol_smooth_max", F),
         ("spawn_box", F), ("goal", F * 3),
+        ("flavor", I32), ("scenario", I32), ("ticks_per_step", I32), ("n_cameras", I32),
+        ("capture_radius", F), ("cam_size", F), ("cam_focal", F), ("cam_px_noise", F), ("cam_fov_deg", F), ("cam_res", F),
     ]
 
 
 class QsLayout(ctypes.Structure):
-    _fields_ = [("params", SZ), ("state", SZ), ("istate", SZ), ("env", SZ), ("stale_vel", SZ), ("obs", SZ), ("term_obs", SZ),
-                ("rew", SZ), ("done", SZ), ("total_bytes", SZ), ("obs_dim", I32), ("num_drones", I32)]
+    _fields_ = [("params", SZ), ("state", SZ), ("istate", SZ), ("env", SZ), ("env_f", SZ), ("stale_vel", SZ), ("obs", SZ),
+                ("term_obs", SZ), ("rew", SZ), ("done", SZ), ("reset_info", SZ), ("total_bytes", SZ), ("obs_dim", I32),
+                ("num_drones", I32)]
 
 
 class QsBuffers(ctypes.Structure):
-    _fields_ = [(n, ctypes.c_void_p) for n in ("state", "istate", "env", "stale_vel", "obs", "term_obs", "rew", "done")]
+    _fields_ = [(n, ctypes.c_void_p) for n in ("state", "istate", "env", "env_f", "stale_vel", "obs", "term_obs", "rew",
+                                               "done", "reset_info")]
 
 
 class QuadSwarmError(RuntimeError):
@@ -58,7 +74,8 @@ class QuadSwarmError(RuntimeError):
 
 
 # every symbol include/quadswarm.h declares (tests check the library exports all of them)
-EXPORTS = ["qs_abi_version", "qs_last_error", "qs_struct_sizes", "qs_config_default", "qs_layout_query", "qs_create", "qs_destroy",
+EXPORTS = ["qs_abi_version", "qs_last_error", "qs_struct_sizes", "qs_config_default", "qs_config_default_a",
+           "qs_layout_query", "qs_create", "qs_destroy",
            "qs_buffers_get", "qs_reset", "qs_step", "qs_set_param",
            "qs_get_param", "qs_state_bytes", "qs_get_state", "qs_set_state"]
 
@@ -77,7 +94,8 @@ def lib():
     sig = {
         "qs_abi_version": ([], I32), "qs_last_error": ([], ctypes.c_char_p),
         "qs_struct_sizes": ([P(SZ), P(SZ), P(SZ)], I32),
-        "qs_config_default": ([P(QsConfig), I32, I32], I32), "qs_layout_query": ([P(QsConfig), P(QsLayout)], I32),
+        "qs_config_default": ([P(QsConfig), I32, I32], I32), "qs_config_default_a": ([P(QsConfig), I32, I32], I32),
+        "qs_layout_query": ([P(QsConfig), P(QsLayout)], I32),
         "qs_create": ([P(QsConfig), ctypes.c_int, V, P(V)], I32), "qs_destroy": ([V], I32),
         "qs_buffers_get": ([V, P(QsBuffers)], I32), "qs_reset": ([V, V, V], I32), "qs_step": ([V, V, V], I32),
         "qs_set_param": ([V, ctypes.c_char_p, ctypes.c_double], I32),

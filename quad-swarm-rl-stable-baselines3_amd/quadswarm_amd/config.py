@@ -1,4 +1,8 @@
-"""Env configuration: the reference's knobs for the flavor-B swarm step, mapped onto qs_config.
+"""Env configuration: the reference's knobs for the swarm step (flavors B and A), mapped onto qs_config.
+
+flavor "B": gym_art.quadrotor_multi.quadrotor_multi.QuadrotorEnvMulti (raw motor commands, shaped rewards).
+flavor "A": gym_art.quadrotor_multi.quadrotor_multi_rewards.QuadrotorEnvMulti, the env swarm_rl/sb_train.py
+            builds (sb3_quad_env.py:34-41): PID pre-controller, heading-rate action, capture reward.
 
 Field names follow the reference's own configs so existing configs drop in:
   * swarm_rl/global_cfg.py:7-190 (QuadrotorEnvConfig, used by sb_train)
@@ -39,15 +43,39 @@ class QuadSwarmConfig:
     apply_collision_force: bool = True
     rew_coeff: dict = field(default_factory=lambda: dict(DEFAULT_REW))
     device: str = "cuda"
+    # ---- flavor A (swarm_rl/global_cfg.py:14-40) ----
+    flavor: str = "B"
+    initial_capture_radius: float = 3.0
+    focal_length_cam: float = 0.035
+    n_cameras: int = 3
+    neighbour_size_cam: float = 0.2
+    pixel_noise_cam: float = 3.0
+    ticks_per_step: int = 8                   # QuadrotorSingle._step calls per env step (:636)
 
     @classmethod
-    def from_reference_cfg(cls, cfg, num_envs=None, **over):
-        """Adapter for swarm_rl.global_cfg.QuadrotorEnvConfig / SF quads_* namespaces."""
+    def sb_train(cls, num_envs=4096, num_agents=8, **over):
+        """Flavor A exactly as swarm_rl/sb_train.py trains it (global_cfg.py defaults + parameter_sweep
+        sb_train.py:111-139): dynamic_repulsive, 15x15x3 room, 30 s episodes, cdist..sangle self obs,
+        camera neighbours (ndist_nsangle) of all N-1 drones, pixel noise 0."""
+        c = cls(num_envs=num_envs, num_agents=num_agents, flavor="A",
+                obs_repr="cdist_cdistdot_dist_distdot_sangle_angledot", episode_duration=30.0,
+                neighbor_visible_num=-1, neighbor_obs_type="ndist_nsangle", quads_mode="dynamic_repulsive",
+                room_dims=(15.0, 15.0, 3.0), pixel_noise_cam=0.0, apply_collision_force=False)
+        for k, v in over.items():
+            setattr(c, k, v)
+        return c
+
+    @classmethod
+    def from_reference_cfg(cls, cfg, num_envs=None, flavor=None, **over):
+        """Adapter for swarm_rl.global_cfg.QuadrotorEnvConfig / SF quads_* namespaces.  A config with
+        dim_mode '2D_horizontal' (global_cfg.py:41, what sb_train builds) maps to flavor A."""
         def g(*names, default=None):
             for n in names:
                 if hasattr(cfg, n):
                     return getattr(cfg, n)
             return default
+        if flavor is None:
+            flavor = "A" if g("dim_mode", default="3D") == "2D_horizontal" else "B"
         c = cls(
             num_envs=num_envs or g("num_envs", default=1),
             num_agents=g("num_agents", "quads_num_agents", default=8),
@@ -66,7 +94,18 @@ class QuadSwarmConfig:
             sense_noise=g("sense_noise", default="default"),
             thrust_noise_ratio=g("thrust_noise_ratio", default=0.05),
             sim_freq=g("sim_freq", default=200.0), sim_steps=g("sim_steps", default=2),
-            seed=g("seed", default=0) or 0, device=g("device", default="cuda"))
+            seed=g("seed", default=0) or 0, device=g("device", default="cuda"), flavor=flavor)
+        if flavor == "A":
+            # quadrotor_multi_rewards builds its dynamics from cfg.dynamics_change only (the
+            # thrust_noise_ratio it computes at :46-49 is never used), default Crazyflie noise 0.05
+            dc = g("dynamics_change", default=None) or {}
+            c.thrust_noise_ratio = (dc.get("noise") or {}).get("thrust_noise_ratio", 0.05)
+            c.apply_collision_force = False   # quadrotor_multi_rewards.py:203
+            ic = g("initial_capture_radius", default=None)
+            c.initial_capture_radius = 0.2 if ic is None else ic   # :205-208
+            for n in ("focal_length_cam", "n_cameras", "neighbour_size_cam", "pixel_noise_cam"):
+                if hasattr(cfg, n):
+                    setattr(c, n, getattr(cfg, n))
         for k, v in over.items():
             setattr(c, k, v)
         return c
@@ -88,19 +127,37 @@ class QuadSwarmConfig:
 
     @property
     def obs_dim(self):
-        return N.SELF_OBS_DIM[N.OBS_REPR[self.obs_repr]] + 6 * self.k_neighbors
+        return N.SELF_OBS_DIM[N.OBS_REPR[self.obs_repr]] + N.NEIGHBOR_DIM[N.NEIGHBOR[self.neighbor_obs_type]] * \
+            self.k_neighbors
+
+    @property
+    def act_dim(self):
+        return 2 if self.flavor == "A" else 4
 
     def validate(self):
+        if self.flavor not in ("A", "B"):
+            raise ValueError(f"flavor must be 'A' or 'B', got {self.flavor!r}")
         if self.obs_repr not in N.OBS_REPR:
-            raise NotImplementedError(f"obs_repr {self.obs_repr!r}: flavor-A representations are not implemented yet")
-        if self.neighbor_obs_type not in ("pos_vel", "none"):
+            raise NotImplementedError(f"obs_repr {self.obs_repr!r} not implemented")
+        rid = N.OBS_REPR[self.obs_repr]
+        if rid not in (N.OBS_REPR_A if self.flavor == "A" else N.OBS_REPR_B):
+            raise ValueError(f"obs_repr {self.obs_repr!r} does not belong to flavor {self.flavor}")
+        if self.neighbor_obs_type not in N.NEIGHBOR:
             raise NotImplementedError(f"neighbor_obs_type {self.neighbor_obs_type!r} not implemented")
-        if self.quads_mode != "static_same_goal":
-            raise NotImplementedError(f"quads_mode {self.quads_mode!r} not implemented (static_same_goal only)")
+        if self.flavor == "B" and self.neighbor_obs_type not in ("pos_vel", "none"):
+            raise NotImplementedError(f"flavor B implements neighbor_obs_type pos_vel / none")
+        if self.flavor == "B" and self.quads_mode != "static_same_goal":
+            raise NotImplementedError(f"quads_mode {self.quads_mode!r} not implemented for flavor B (static_same_goal)")
+        if self.flavor == "A":
+            if self.quads_mode not in N.SCENARIO:
+                raise NotImplementedError(f"quads_mode {self.quads_mode!r} not implemented for flavor A "
+                                          "(dynamic_repulsive, static_same_goal)")
+            if self.use_downwash:
+                raise NotImplementedError("flavor A with downwash is not implemented")
         if not 1 <= self.num_agents <= N.MAX_AGENTS:
             raise ValueError(f"num_agents must be in [1, {N.MAX_AGENTS}]")
         k = self.k_neighbors
-        if self.neighbor_obs_type == "pos_vel" and self.num_agents > 1 and not 1 <= k <= self.num_agents - 1:
+        if self.neighbor_obs_type != "none" and self.num_agents > 1 and not 1 <= k <= self.num_agents - 1:
             raise ValueError("neighbor_visible_num out of range")
 
     def to_qs_config(self):
@@ -109,16 +166,22 @@ class QuadSwarmConfig:
         rc = N.lib().qs_config_default(c, int(self.num_envs), int(self.num_agents))
         N.check(rc, "qs_config_default")
         k = dynamics_constants(crazyflie_params(), dt=self.dt, thrust_noise_ratio=self.thrust_noise_ratio)
+        c.flavor = N.FLAVOR_A if self.flavor == "A" else N.FLAVOR_B
         c.obs_repr = N.OBS_REPR[self.obs_repr]
         kn = self.k_neighbors
-        c.neighbor_obs = N.NEIGHBOR_POS_VEL if kn > 0 else N.NEIGHBOR_NONE
+        c.neighbor_obs = N.NEIGHBOR[self.neighbor_obs_type] if kn > 0 else N.NEIGHBOR_NONE
         c.k_neighbors = kn
+        c.scenario = N.SCENARIO.get(self.quads_mode, 0)
+        c.ticks_per_step = int(self.ticks_per_step)
+        c.capture_radius = float(self.initial_capture_radius)
+        c.cam_size, c.cam_focal, c.cam_px_noise = self.neighbour_size_cam, self.focal_length_cam, self.pixel_noise_cam
+        c.n_cameras = int(self.n_cameras)
         c.ep_len = self.ep_len
         c.sim_steps = self.sim_steps
         c.svd_every = svd_every(self.dt, 0.5)
         c.sense_noise = 0 if self.sense_noise is None else 1
         c.use_downwash = int(bool(self.use_downwash))
-        c.apply_collision_force = int(bool(self.apply_collision_force))
+        c.apply_collision_force = int(bool(self.apply_collision_force)) if self.flavor == "B" else 0
         c.seed = int(self.seed) & 0xFFFFFFFF
         c.drone_id_offset = int(self.drone_id_offset)
         c.dt = self.dt

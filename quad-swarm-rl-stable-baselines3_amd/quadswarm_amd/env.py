@@ -1,9 +1,11 @@
-"""Batched, HBM-resident QuadrotorEnvMulti (flavor B): E envs x N drones stepped by one HIP launch.
+"""Batched, HBM-resident QuadrotorEnvMulti: E envs x N drones stepped by one HIP launch.
 
-Semantics per env follow QuadrotorEnvMulti.step / reset (gym_art/quadrotor_multi/quadrotor_multi.py:440-841)
-with the in-env auto-reset of :739-838 and the SubprocVecEnvCustom terminal_observation contract
-(swarm_rl/env_wrappers/subproc_vec_env_custom.py:33-52).  All buffers are torch tensors viewing one
-device workspace that libquadswarm.so reads and writes in place (zero-copy).
+Flavor B follows quadrotor_multi.QuadrotorEnvMulti.step / reset (gym_art/quadrotor_multi/quadrotor_multi.py:
+440-841) with its in-env auto-reset (:739-838); flavor A follows quadrotor_multi_rewards.QuadrotorEnvMulti
+(quadrotor_multi_rewards.py:541-991) plus the worker-side reset on done.  Both keep the SubprocVecEnvCustom
+terminal_observation / reset_infos contract (swarm_rl/env_wrappers/subproc_vec_env_custom.py:33-52).
+All buffers are torch tensors viewing one device workspace that libquadswarm.so reads and writes in place
+(zero-copy).
 """
 import ctypes
 
@@ -45,11 +47,15 @@ class QuadSwarmEnv:
         self.state = view(lay.state, 4 * N.NF * I, torch.float32, (N.NF, I))
         self.istate = view(lay.istate, 4 * N.NI * I, torch.int32, (N.NI, I))
         self.env_state = view(lay.env, 4 * N.NE * E, torch.int32, (N.NE, E))
+        self.env_f = view(lay.env_f, 4 * N.NENVF * E, torch.float32, (N.NENVF, E))
+        self.reset_info = view(lay.reset_info, E, torch.uint8, (E,))
         self.stale_vel = view(lay.stale_vel, 4 * 3 * I, torch.float32, (3, I))
         self.obs = view(lay.obs, 4 * I * od, torch.float32, (I, od))
         self.term_obs = view(lay.term_obs, 4 * I * od, torch.float32, (I, od))
         self.rew = view(lay.rew, 4 * I, torch.float32, (I,))
         self.done = view(lay.done, I, torch.uint8, (I,))
+        self.act_dim = cfg.act_dim
+        self._align = 8 if cfg.flavor == "A" else 16
         self._torch = torch
 
     # ------------------------------------------------------------------------------------------
@@ -69,15 +75,17 @@ class QuadSwarmEnv:
         return self.obs
 
     def step(self, actions):
-        """One control step of every env.  actions: [E*N, 4] (or [E, N, 4]) raw policy output.
+        """One control step of every env.  actions: [E*N, act_dim] (or [E, N, act_dim]) raw policy output
+        (act_dim 4 for flavor B, 2 for flavor A).
 
-        Returns device views (obs, rew, done, term_obs); they are overwritten by the next call."""
+        Returns device views (obs, rew, done, term_obs); they are overwritten by the next call.
+        reset_info[e] (0 none, 1 {"success": False}, 2 {"success": True}) says which envs were reset."""
         a = actions
         if not (self._torch.is_tensor(a) and a.device == self.device and a.dtype == self._torch.float32
-                and a.is_contiguous() and a.data_ptr() % 16 == 0):
+                and a.is_contiguous() and a.data_ptr() % self._align == 0):
             a = self._torch.as_tensor(a, device=self.device, dtype=self._torch.float32).contiguous()
-        if a.numel() != self.I * 4:
-            raise ValueError(f"actions must have {self.I * 4} elements, got {a.numel()}")
+        if a.numel() != self.I * self.act_dim:
+            raise ValueError(f"actions must have {self.I * self.act_dim} elements, got {a.numel()}")
         self._act_keepalive = a
         N.check(N.lib().qs_step(self._h, ctypes.c_void_p(a.data_ptr()), self._stream()), "qs_step")
         return self.obs, self.rew, self.done, self.term_obs
@@ -90,6 +98,17 @@ class QuadSwarmEnv:
         v = ctypes.c_double()
         N.check(N.lib().qs_get_param(self._h, key.encode(), ctypes.byref(v)), "qs_get_param")
         return v.value
+
+    def set_capture_radius(self, value, env_indices=None):
+        """QuadrotorEnvMulti.set_capture_radius (quadrotor_multi_rewards.py:212-213) for all envs or a subset;
+        the radius lives in device memory, so captured graphs see it."""
+        if self.cfg.flavor != "A":
+            raise N.QuadSwarmError("set_capture_radius is a flavor-A method")
+        if env_indices is None:
+            self.set_param("capture_radius", value)
+        else:
+            idx = self._torch.as_tensor(list(env_indices), dtype=self._torch.long, device=self.device)
+            self.env_f[N.ENVF_CAPTURE].index_fill_(0, idx, float(value))
 
     def get_state(self):
         """Host snapshot (bytes) of the full env state + RNG counter (checkpoint / replay)."""
@@ -110,7 +129,8 @@ class QuadSwarmEnv:
         s = self.state
         return dict(pos=s[N.F_POS:N.F_POS + 3].T, vel=s[N.F_VEL:N.F_VEL + 3].T, rot=s[N.F_ROT:N.F_ROT + 9].T.reshape(-1, 3, 3),
                     omega=s[N.F_OMEGA:N.F_OMEGA + 3].T, rot_damp=s[N.F_ROT_DAMP:N.F_ROT_DAMP + 4].T,
-                    cmd_damp=s[N.F_CMD_DAMP:N.F_CMD_DAMP + 4].T, ou=s[N.F_OU:N.F_OU + 4].T, goal=s[N.F_GOAL:N.F_GOAL + 3].T)
+                    cmd_damp=s[N.F_CMD_DAMP:N.F_CMD_DAMP + 4].T, ou=s[N.F_OU:N.F_OU + 4].T, goal=s[N.F_GOAL:N.F_GOAL + 3].T,
+                    pid=s[N.F_PID:N.F_PID + 20].T, angle=s[N.F_ANGLE], ang_vel=s[N.F_ANGVEL], heading=s[N.F_HEADING])
 
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:
@@ -126,10 +146,27 @@ class QuadSwarmEnv:
 
 
 def observation_bounds(cfg: QuadSwarmConfig):
-    """Observation-space box (QuadrotorSingle.make_observation_space, quadrotor_single.py:278-349)."""
+    """Observation-space box (QuadrotorSingle.make_observation_space, quadrotor_single.py:278-349 for
+    flavor B, quadrotor_single_rewards.py:267-344 for flavor A)."""
     rd = np.array(cfg.room_dims, dtype=np.float64)
     room_range = np.array([rd[0], rd[1], rd[2]])
     vmax, omax = 3.0, 40.0
+    if cfg.flavor == "A":
+        L = rd[0]
+        comp = {"aw": ([-np.pi], [np.pi]), "awdot": ([-omax], [omax]), "cdist": ([0.0], [L / 2]),
+                "cdistdot": ([-vmax], [vmax]), "dist": ([-L / 2], [L / 2]), "ndist": ([-L / 2], [L / 2]),
+                "distdot": ([-vmax], [vmax]), "angle": ([-np.pi], [np.pi]), "sangle": ([-1.0, -1.0], [1.0, 1.0]),
+                "nsangle": ([-1.0, -1.0], [1.0, 1.0]), "angledot": ([-omax], [omax]),
+                "rxyz": (list(-room_range), list(room_range)), "rvxyz": ([-2 * vmax] * 3, [2 * vmax] * 3)}
+        names = cfg.obs_repr.split("_")
+        nb = {"pos_vel": ["rxyz", "rvxyz"], "pos": ["rxyz"], "npos": ["rxyz"], "dist_angle": ["dist", "angle"],
+              "dist_sangle": ["dist", "sangle"], "ndist_nsangle": ["dist", "sangle"],
+              "dist_angle_heading": ["dist", "angle", "angle"], "dist_sangle_sheading": ["dist", "sangle", "sangle"],
+              "none": []}[cfg.neighbor_obs_type]
+        names = names + nb * cfg.k_neighbors
+        lo = np.concatenate([comp[n][0] for n in names])
+        hi = np.concatenate([comp[n][1] for n in names])
+        return lo.astype(np.float32), hi.astype(np.float32)
     lo = [-room_range, -vmax * np.ones(3), -np.ones(9), -omax * np.ones(3)]
     hi = [room_range, vmax * np.ones(3), np.ones(9), omax * np.ones(3)]
     if cfg.obs_repr.endswith("floor"):

@@ -7,7 +7,9 @@ swapped for `GpuQuadVecEnv(cfg)`:
   step_async(actions (num_envs, act_dim))                 (:141-147)
   step_wait() -> obs, rews, dones, infos                  (:149-153)
   infos[i]["terminal_observation"] for every agent of a finished env, which is reset (:42-46)
-  reset_infos: per env, {} after a reset else None        (:152, :162)
+  reset_infos: per env, after a reset {} (flavor B) or {"success": bool} (flavor A,
+               quadrotor_multi_rewards.py:625-627), else None (:152, :162)
+  env_method("set_capture_radius", r, indices=...)      (custom_callbacks.py:455-462, flavor A)
   env_method / get_attr / set_attr / has_attr over ENV indices (:212-237)
 Two modes:
   * compat (default): numpy in/out, exactly the reference's types (obs float32 instead of float64;
@@ -88,7 +90,8 @@ class GpuQuadVecEnv:
         self.num_envs = cfg.num_envs * cfg.num_agents
         lo, hi = observation_bounds(cfg)
         self.observation_space = make_box(lo, hi)
-        self.action_space = make_box(-np.ones(4, np.float32), np.ones(4, np.float32))
+        ad = cfg.act_dim   # CustomPidControl.action_space (quadrotor_control.py:74-86) is (2,) in flavor A
+        self.action_space = make_box(-np.ones(ad, np.float32), np.ones(ad, np.float32))
         self.as_torch = as_torch
         self.batch = 0
         self.waiting = False
@@ -100,7 +103,11 @@ class GpuQuadVecEnv:
     # ---- VecEnv API ----
     def reset(self):
         obs = self.env.reset()
-        self.reset_infos = tuple({} for _ in range(self.cfg.num_envs))
+        if self.cfg.flavor == "A":
+            ri = self.env.reset_info.cpu().numpy()
+            self.reset_infos = tuple({"success": bool(v == 2)} for v in ri)
+        else:
+            self.reset_infos = tuple({} for _ in range(self.cfg.num_envs))
         return obs if self.as_torch else obs.cpu().numpy()
 
     def step_async(self, actions):
@@ -126,8 +133,19 @@ class GpuQuadVecEnv:
         return self.step_wait()
 
     def _set_reset_infos(self, done_rows):
-        envs = set(int(r) // self.agents_per_env for r in np.asarray(done_rows).tolist())
-        self.reset_infos = tuple(({} if e in envs else None) for e in range(self.cfg.num_envs))
+        if len(done_rows) == 0:
+            self.reset_infos = (None,) * self.cfg.num_envs
+            return
+        envs = sorted(set(int(r) // self.agents_per_env for r in np.asarray(done_rows).tolist()))
+        ri = [None] * self.cfg.num_envs
+        if self.cfg.flavor == "A":
+            flags = self.env.reset_info.cpu().numpy()
+            for e in envs:
+                ri[e] = {"success": bool(flags[e] == 2)}
+        else:
+            for e in envs:
+                ri[e] = {}
+        self.reset_infos = tuple(ri)
 
     def close(self):
         if not self.closed:
@@ -153,7 +171,8 @@ class GpuQuadVecEnv:
             self.env.set_param(*method_args, **method_kwargs)
             return [None] * len(idx)
         if method_name == "set_capture_radius":
-            raise NotImplementedError("set_capture_radius is a flavor-A (capture) env method; flavor A is not built yet")
+            self.env.set_capture_radius(*method_args, env_indices=None if indices is None else idx)
+            return [None] * len(idx)
         raise AttributeError(f"unknown env method {method_name}")
 
     def get_attr(self, attr_name, indices=None):
@@ -162,6 +181,9 @@ class GpuQuadVecEnv:
             return [self.cfg.num_agents] * len(idx)
         if attr_name == "cfg":
             return [self.cfg] * len(idx)
+        if attr_name == "capture_radius" and self.cfg.flavor == "A":
+            r = self.env.env_f[N.ENVF_CAPTURE].cpu().numpy()
+            return [float(r[i]) for i in idx]
         if hasattr(self.cfg, attr_name):
             return [getattr(self.cfg, attr_name)] * len(idx)
         raise AttributeError(attr_name)

@@ -188,3 +188,133 @@ def assert_obs_match(gpu_obs, want_obs, oenv, so_dim, K, atol=2e-4, rtol=1e-4, k
             j = int(np.argmin(d))
             assert d[j] <= atol + rtol * np.abs(got[s]).max(), f"row {r} slot {s}: no neighbour matches"
             assert keys[j] <= kth * (1 + key_tol) + key_tol, f"row {r} slot {s}: neighbour {j} is not among the K nearest"
+
+
+# ---------------------------------------------------------------------------------------------
+# flavor A
+# ---------------------------------------------------------------------------------------------
+def oracle_params_a(cfg: QuadSwarmConfig):
+    """OrParams (flavor A) with the constants the GPU handle was built from."""
+    k = dynamics_constants(crazyflie_params(), dt=cfg.dt, thrust_noise_ratio=cfg.thrust_noise_ratio)
+    p = O.params_a(num_agents=cfg.num_agents, num_envs=cfg.num_envs, k=cfg.k_neighbors, obs_repr=cfg.obs_repr,
+                   ntype=cfg.neighbor_obs_type if cfg.neighbor_obs_type != "none" else "dist_angle",
+                   room=tuple(float(x) for x in cfg.room_dims))
+    if cfg.neighbor_obs_type == "none":
+        p.k_neighbors = 0
+    p.mass = k["mass"]
+    for i in range(3):
+        p.inertia[i] = k["inertia"][i]
+    for j in range(4):
+        p.thrust_max[j] = k["thrust_max"][j]
+        p.torque_max[j] = k["torque_max"][j]
+        p.prop_ccw[j] = k["prop_ccw"][j]
+        for a in range(3):
+            p.prop_cross[j][a] = k["prop_cross"][j][a]
+    p.motor_tau_up, p.motor_tau_down = k["motor_tau_up"], k["motor_tau_down"]
+    p.arm = k["arm"]
+    p.ou_theta = float(np.float32(0.15))
+    p.ou_sigma = float(np.float32(k["ou_sigma"]))
+    p.sense_noise = 0 if cfg.sense_noise is None else 1
+    p.ep_len = cfg.ep_len
+    p.ticks_per_step = cfg.ticks_per_step
+    p.scenario_a = NAT.SCENARIO[cfg.quads_mode]
+    p.cam_size, p.cam_focal, p.cam_px_noise = cfg.neighbour_size_cam, cfg.focal_length_cam, cfg.pixel_noise_cam
+    p.n_cameras = cfg.n_cameras
+    p.control_dt = cfg.dt * cfg.sim_steps
+    return p
+
+
+def gpu_to_oracle_a(env, oenv):
+    gpu_to_oracle(env, oenv)
+    st = env.state.double().cpu().numpy()
+    es = env.env_state.cpu().numpy()
+    ef = env.env_f.double().cpu().numpy()
+    stale = env.stale_vel.double().cpu().numpy()
+    N, E = env.N, env.E
+    for g in range(env.I):
+        d = oenv.drones[g]
+        for q in range(20):
+            d.pid[q] = st[NAT.F_PID + q, g]
+        d.angle, d.ang_vel = st[NAT.F_ANGLE, g], st[NAT.F_ANGVEL, g]
+    for e in range(E):
+        ev = oenv.envs[e]
+        fl = int(es[NAT.E_FLAGS, e])
+        ev.success = int(bool(fl & NAT.EF_SUCCESS))
+        ev.has_pos = int(bool(fl & NAT.EF_HAS_POS))
+        ev.target[0], ev.target[1] = ef[NAT.ENVF_TARGET_X, e], ef[NAT.ENVF_TARGET_Y, e]
+        ev.capture_radius = ef[NAT.ENVF_CAPTURE, e]
+        for i in range(N):
+            g = e * N + i
+            ev.heading[i] = st[NAT.F_HEADING, g] if fl & NAT.EF_STALE else st[NAT.F_ANGLE, g]
+            for c in range(3):
+                ev.obs_vel[i][c] = stale[c, g] if fl & NAT.EF_STALE else st[3 + c, g]
+
+
+def oracle_to_gpu_a(oenv, env):
+    import torch
+    oracle_to_gpu(oenv, env)
+    N, E, I = env.N, env.E, env.I
+    st = env.state.cpu().numpy().copy()
+    es = env.env_state.cpu().numpy().copy()
+    ef = env.env_f.cpu().numpy().copy()
+    for g in range(I):
+        d = oenv.drones[g]
+        st[NAT.F_PID:NAT.F_PID + 20, g] = d.pid[:]
+        st[NAT.F_ANGLE, g], st[NAT.F_ANGVEL, g] = d.angle, d.ang_vel
+    for e in range(E):
+        ev = oenv.envs[e]
+        es[NAT.E_FLAGS, e] = NAT.EF_STALE | (NAT.EF_SUCCESS if ev.success else 0) | (NAT.EF_HAS_POS if ev.has_pos else 0)
+        ef[NAT.ENVF_TARGET_X, e], ef[NAT.ENVF_TARGET_Y, e] = ev.target[0], ev.target[1]
+        ef[NAT.ENVF_CAPTURE, e] = ev.capture_radius
+        for i in range(N):
+            st[NAT.F_HEADING, e * N + i] = ev.heading[i]
+    env.state.copy_(torch.from_numpy(st))
+    env.env_state.copy_(torch.from_numpy(es))
+    env.env_f.copy_(torch.from_numpy(ef))
+
+
+def angle_columns_a(cfg):
+    """Columns of a flavor-A obs row that are angles in [-pi, pi) (compared modulo 2 pi: fp32 and fp64
+    may wrap a value within an ulp of pi to opposite ends)."""
+    cols = []
+    so = NAT.SELF_OBS_DIM[NAT.OBS_REPR[cfg.obs_repr]]
+    if cfg.obs_repr.startswith("aw_"):
+        cols += [0, 4]
+    elif "_angle_" in cfg.obs_repr:
+        cols += [4]
+    per = {"dist_angle": [1], "dist_angle_heading": [1, 2]}.get(cfg.neighbor_obs_type, [])
+    F = NAT.NEIGHBOR_DIM[NAT.NEIGHBOR[cfg.neighbor_obs_type]]
+    for s in range(cfg.k_neighbors):
+        cols += [so + s * F + c for c in per]
+    return np.array(cols, dtype=int)
+
+
+def assert_obs_match_a(got, want, cfg, atol=3e-4, rtol=2e-4, oenv=None, max_bad_rows=0, what="obs"):
+    """Compare flavor-A obs: angle columns modulo 2 pi; neighbour blocks of drone pairs closer than the
+    camera's marker radius + 5 cm are skipped for camera features (the model's sqrt(r^2 - a^2) is
+    ill-conditioned there: fp32 and fp64 may land on opposite sides of the NaN -> 0 boundary)."""
+    got = np.array(got, dtype=np.float64)
+    want = np.array(want, dtype=np.float64)
+    ac = angle_columns_a(cfg)
+    if len(ac):
+        diff = got[:, ac] - want[:, ac]
+        wd = (diff + np.pi) % (2 * np.pi) - np.pi
+        got[:, ac] = want[:, ac] + np.where(np.isnan(diff), diff, wd)
+    bad = ~np.isclose(got, want, atol=atol, rtol=rtol, equal_nan=True)
+    if "ndist" in cfg.neighbor_obs_type or "ndist" in cfg.obs_repr:
+        if oenv is not None:
+            N = cfg.num_agents
+            so = NAT.SELF_OBS_DIM[NAT.OBS_REPR[cfg.obs_repr]]
+            for r in np.flatnonzero(bad.any(1)):
+                e, i = divmod(int(r), N)
+                ev = oenv.envs[e]
+                P = np.array([ev.obs_pos[j][:2] for j in range(N)])
+                dmin = np.sort(np.linalg.norm(P - P[i], axis=1))[1] if N > 1 else 1e9
+                if dmin < cfg.neighbour_size_cam / 2 + 0.05:
+                    bad[r, so:] = False
+    rows = np.flatnonzero(bad.any(1))
+    if len(rows) > max_bad_rows:
+        r = rows[0]
+        c = np.flatnonzero(bad[r])
+        raise AssertionError(f"{what}: {len(rows)} rows differ; first row {r} cols {c[:8]}: got {got[r, c[:8]]} "
+                             f"want {want[r, c[:8]]}")

@@ -9,6 +9,7 @@ import numpy as np
 import pytest
 
 from quadswarm_amd import QuadSwarmConfig, _native as N
+from quadswarm_amd.env import observation_bounds
 from quadswarm_amd.params import dynamics_constants, svd_every
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -87,11 +88,83 @@ def test_validation_errors_are_reported():
         N.check(L.qs_layout_query(bad, lay), "qs_layout_query")
 
 
-def test_config_rejects_unbuilt_flavors():
-    with pytest.raises(NotImplementedError):
+def test_config_rejects_unbuilt_or_mixed_flavors():
+    with pytest.raises(ValueError):   # a flavor-A repr on a flavor-B env
         QuadSwarmConfig(obs_repr="cdist_cdistdot_dist_distdot_sangle_angledot").to_qs_config()
     with pytest.raises(NotImplementedError):
         QuadSwarmConfig(quads_mode="mix").to_qs_config()
+    with pytest.raises(NotImplementedError):
+        QuadSwarmConfig.sb_train(use_downwash=True).to_qs_config()
+    with pytest.raises(NotImplementedError):
+        QuadSwarmConfig.sb_train(neighbor_obs_type="pos_vel_R").to_qs_config()
+
+
+@pytest.mark.parametrize("N_,ntype,k,repr_,od", [
+    (4, "ndist_nsangle", -1, "cdist_cdistdot_dist_distdot_sangle_angledot", 7 + 3 * 3),
+    (8, "ndist_nsangle", -1, "cdist_cdistdot_dist_distdot_sangle_angledot", 7 + 7 * 3),
+    (8, "dist_sangle_sheading", 3, "cdist_cdistdot_ndist_distdot_nsangle_angledot", 7 + 3 * 5),
+    (8, "dist_angle", 6, "aw_awdot_dist_distdot_angle_angledot", 6 + 6 * 2),
+    (8, "pos_vel", -1, "cdist_cdistdot_dist_distdot_angle_angledot", 6 + 7 * 6),
+    (1, "none", -1, "cdist_cdistdot_dist_distdot_sangle_angledot", 7),
+])
+def test_layout_flavor_a(N_, ntype, k, repr_, od):
+    """obs dims of flavor A (QUADS_OBS_REPR / QUADS_NEIGHBOR_OBS_TYPE, quad_utils.py:30-58) and the
+    reference's own observation_space shape for the sb_train config."""
+    cfg = QuadSwarmConfig.sb_train(num_envs=5, num_agents=N_, neighbor_obs_type=ntype, neighbor_visible_num=k,
+                                   obs_repr=repr_)
+    c = cfg.to_qs_config()
+    lay = N.QsLayout()
+    N.check(N.lib().qs_layout_query(c, lay))
+    assert lay.obs_dim == od == cfg.obs_dim
+    lo, hi = observation_bounds(cfg)
+    assert lo.shape == (od,)
+    assert lay.env_f >= lay.env and lay.stale_vel > lay.env_f and lay.reset_info > lay.done
+    assert lay.total_bytes >= lay.reset_info + 5
+
+
+def test_sb_train_observation_space_matches_reference():
+    """Box bounds of the sb_train flavor-A config: 7 self + 3 per neighbour (cdist 0..7.5, cdistdot +-3,
+    dist +-7.5, distdot +-3, sangle +-1, angledot +-40; neighbour dist +-7.5, sangle +-1)."""
+    cfg = QuadSwarmConfig.sb_train(num_envs=1, num_agents=4)
+    lo, hi = observation_bounds(cfg)
+    np.testing.assert_allclose(lo[:7], [0, -3, -7.5, -3, -1, -1, -40])
+    np.testing.assert_allclose(hi[:7], [7.5, 3, 7.5, 3, 1, 1, 40])
+    np.testing.assert_allclose(lo[7:], [-7.5, -1, -1] * 3)
+
+
+def test_config_default_a():
+    c = N.QsConfig()
+    N.check(N.lib().qs_config_default_a(c, 16, 8))
+    assert c.flavor == N.FLAVOR_A and c.scenario == N.SCENARIO["dynamic_repulsive"]
+    assert c.k_neighbors == 7 and c.neighbor_obs == N.NEIGHBOR["ndist_nsangle"] and c.ep_len == 3000
+    assert c.apply_collision_force == 0 and c.ticks_per_step == 8 and c.cam_px_noise == 0.0
+    mine = QuadSwarmConfig.sb_train(num_envs=16, num_agents=8).to_qs_config()
+    for f in ("flavor", "scenario", "obs_repr", "neighbor_obs", "k_neighbors", "ep_len", "ticks_per_step",
+              "n_cameras", "apply_collision_force"):
+        assert getattr(mine, f) == getattr(c, f), f
+    assert list(mine.room_hi) == list(c.room_hi)
+
+
+def test_from_reference_cfg_flavor_a():
+    class Cfg:  # swarm_rl/global_cfg.py QuadrotorEnvConfig defaults (flavor A, sb_train)
+        num_agents = 4
+        obs_repr = "cdist_cdistdot_dist_distdot_angle_angledot"
+        episode_duration = 30.0
+        neighbor_visible_num = -1
+        neighbor_obs_type = "dist_angle"
+        dim_mode = "2D_horizontal"
+        quads_mode = "dynamic_repulsive"
+        room_dims = [15, 15, 3]
+        initial_capture_radius = 3.0
+        pixel_noise_cam = 3.0
+        thrust_noise_ratio = 0.3     # ignored by the reference's flavor A
+        dynamics_change = None
+        use_downwash = False
+    c = QuadSwarmConfig.from_reference_cfg(Cfg(), num_envs=13)
+    assert c.flavor == "A" and c.thrust_noise_ratio == 0.05 and not c.apply_collision_force
+    assert c.obs_dim == 6 + 3 * 2 and c.ep_len == 3000
+    q = c.to_qs_config()
+    assert q.capture_radius == 3.0 and q.cam_px_noise == 3.0
 
 
 def test_from_reference_cfg_names():

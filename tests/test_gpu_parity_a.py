@@ -1,0 +1,268 @@
+"""GPU parity for flavor A (quadrotor_multi_rewards: PID pre-controller, capture reward, camera model,
+dynamic_repulsive target) -- the HIP step through the C ABI against the CPU oracle (identical Philox
+draws) and against the reference's own noise-free trajectory.  Needs an MI355X: every test is gpu.
+
+Tolerances (fp32 GPU vs fp64 oracle):
+  * one step (8 controller+physics ticks) from an identical state: obs / state within 3e-4 abs
+    (+2e-4 rel); angle features compared modulo 2 pi; done / reset_info / capture rewards identical;
+    camera features of drone pairs within 5 cm of the marker radius skipped (see parity_utils);
+  * reference noise-free trajectory (a_traj_n4quiet, 150 steps = 1200 ticks): obs within 2e-3.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("no HIP device", allow_module_level=True)
+
+import oracle as O  # noqa: E402
+from parity_utils import (assert_obs_match_a, gpu_to_oracle_a, oracle_params_a, oracle_to_gpu_a)  # noqa: E402
+from quadswarm_amd import QuadSwarmConfig, _native as NAT  # noqa: E402
+from quadswarm_amd.env import QuadSwarmEnv  # noqa: E402
+from quadswarm_amd.vec_env import GpuQuadVecEnv  # noqa: E402
+
+CONFIGS = {
+    "sb4": dict(num_agents=4),
+    "sb8": dict(num_agents=8),
+    "cam8k3": dict(num_agents=8, neighbor_visible_num=3, pixel_noise_cam=3.0,
+                   obs_repr="cdist_cdistdot_ndist_distdot_nsangle_angledot"),
+    "hd8": dict(num_agents=8, neighbor_obs_type="dist_sangle_sheading"),
+    "aw8k5": dict(num_agents=8, neighbor_obs_type="dist_angle_heading", neighbor_visible_num=5,
+                  obs_repr="aw_awdot_dist_distdot_angle_angledot"),
+    "pv8": dict(num_agents=8, neighbor_obs_type="pos_vel", obs_repr="cdist_cdistdot_dist_distdot_angle_angledot"),
+    "n1": dict(num_agents=1, neighbor_obs_type="none"),
+    "n32k6": dict(num_agents=32, neighbor_visible_num=6, neighbor_obs_type="dist_sangle"),
+    "static4": dict(num_agents=4, quads_mode="static_same_goal", neighbor_obs_type="pos"),
+}
+
+
+def make_pair(name, E=None, seed=11, **kw):
+    over = dict(CONFIGS[name])
+    over.update(kw)
+    N = over["num_agents"]
+    cfg = QuadSwarmConfig.sb_train(num_envs=E or max(2048 // N, 8), seed=seed, **over)
+    env = QuadSwarmEnv(cfg)
+    oenv = O.OracleEnvA(oracle_params_a(cfg), seed=seed)
+    oenv.set_capture_radius(cfg.initial_capture_radius)
+    return cfg, env, oenv
+
+
+def np_(t):
+    return t.double().cpu().numpy()
+
+
+def ostate(oenv, field):
+    return np.array([np.ctypeslib.as_array(getattr(oenv.drones[g], field)).copy() for g in range(oenv.E * oenv.N)])
+
+
+@pytest.mark.parametrize("name", list(CONFIGS))
+def test_reset_matches_oracle(name):
+    cfg, env, oenv = make_pair(name)
+    obs = np_(env.reset())
+    want, ri = oenv.reset()
+    assert_obs_match_a(obs, want, cfg, atol=5e-5, rtol=2e-5, oenv=oenv, what="reset obs")
+    f = env.drone_fields()
+    np.testing.assert_allclose(np_(f["pos"]), ostate(oenv, "pos"), atol=3e-6)
+    np.testing.assert_allclose(np_(f["rot"]).reshape(-1, 9), ostate(oenv, "rot"), atol=3e-6)
+    np.testing.assert_allclose(np_(f["angle"]), [oenv.drones[g].angle for g in range(env.I)], atol=3e-6)
+    tgt = np_(env.env_f[:2]).T
+    np.testing.assert_allclose(tgt, [list(oenv.envs[e].target) for e in range(env.E)], atol=3e-6)
+    np.testing.assert_array_equal(env.reset_info.cpu().numpy(), ri)
+
+
+def _perturb(oenv, cfg, rng, step):
+    """Exercise every branch: per-env capture radii (immediate captures in some envs), envs whose
+    episode ends inside the 8-tick loop, random PID / heading states."""
+    for e in range(oenv.E):
+        ev = oenv.envs[e]
+        ev.capture_radius = [0.3, 3.0, 1.2, 0.0][(e + step) % 4]
+        if (e + step) % 7 == 3:
+            ev.tick = cfg.ep_len - 1 - (e % 5)
+    for g in range(oenv.E * oenv.N):
+        d = oenv.drones[g]
+        d.ang_vel = rng.uniform(-1, 1)
+
+
+@pytest.mark.parametrize("name", list(CONFIGS))
+def test_one_step_from_identical_state(name):
+    """Re-sync the GPU to the oracle's fp64 state before every step: tight per-step parity of the 8-tick
+    controller/physics loop, captures, timeouts, target motion, neighbour features and worker resets."""
+    cfg, env, oenv = make_pair(name)
+    env.reset()
+    oenv.reset()
+    rng = np.random.default_rng(5)
+    stats = dict(done=0, cap=0)
+    for t in range(8):
+        _perturb(oenv, cfg, rng, t)
+        oracle_to_gpu_a(oenv, env)
+        a = rng.uniform(-1.2, 1.2, (env.I, 2)).astype(np.float32)
+        obs, rew, done, term = env.step(torch.from_numpy(a).cuda())
+        w_obs, w_rew, w_done, w_term, w_ri = oenv.step(a.astype(np.float64))
+        np.testing.assert_array_equal(done.cpu().numpy().astype(bool), w_done, err_msg=f"done step {t}")
+        np.testing.assert_array_equal(env.reset_info.cpu().numpy(), w_ri, err_msg=f"reset_info step {t}")
+        np.testing.assert_allclose(np_(rew), w_rew, atol=1e-5, err_msg=f"rew step {t}")
+        assert_obs_match_a(np_(obs), w_obs, cfg, oenv=oenv, what=f"obs step {t}")
+        if w_done.any():
+            assert_obs_match_a(np_(term)[w_done], w_term[w_done], cfg, what=f"term step {t}")
+        stats["done"] += int(w_done.sum())
+        stats["cap"] += int((w_rew > 50).sum())
+        f = env.drone_fields()
+        np.testing.assert_allclose(np_(f["pos"]), ostate(oenv, "pos"), atol=3e-5, err_msg=f"pos step {t}")
+        np.testing.assert_allclose(np_(f["vel"]), ostate(oenv, "vel"), atol=5e-4, rtol=1e-3, err_msg=f"vel step {t}")
+        np.testing.assert_allclose(np_(f["pid"]), ostate(oenv, "pid"), atol=2e-3, rtol=2e-3, err_msg=f"pid step {t}")
+        tgt = np_(env.env_f[:2]).T
+        np.testing.assert_allclose(tgt, [list(oenv.envs[e].target) for e in range(env.E)], atol=3e-5)
+        gpu_to_oracle_a(env, oenv)   # continue from the GPU's state (keeps both on the same branch)
+    assert stats["done"] > 0
+    assert stats["cap"] > 0
+
+
+def load_golden_into_gpu(golden, name, E=1):
+    g = golden("a_traj_" + name)
+    n = int(g["n"])
+    ntypes = ["dist_angle", "dist_sangle", "ndist_nsangle", "dist_angle_heading", "dist_sangle_sheading",
+              "pos", "npos", "pos_vel"]
+    cfg = QuadSwarmConfig.sb_train(num_envs=E, num_agents=n, obs_repr=O.A_REPRS[int(g["obs_repr"])],
+                                   neighbor_obs_type=ntypes[int(g["ntype"])], neighbor_visible_num=int(g["k"]),
+                                   sense_noise="default" if int(g["sense"]) else None,
+                                   thrust_noise_ratio=float(g["thrust_noise"]), pixel_noise_cam=float(g["px_noise"]),
+                                   episode_duration=(int(g["ep_len"]) + 0.5) * 0.01)
+    env = QuadSwarmEnv(cfg)
+    oenv = O.OracleEnvA(oracle_params_a(cfg), seed=0)
+    for e in range(E):
+        for i in range(n):
+            d = oenv.drones[e * n + i]
+            O.set_drone(d, pos=g["init_pos"][i], vel=g["init_vel"][i], rot=g["init_rot"][i], omega=g["init_omega"][i],
+                        thrust_rot_damp=g["init_rd"][i], thrust_cmds_damp=g["init_cd"][i], ou=g["init_ou"][i],
+                        goal=g["init_goal"][i], pid=g["init_pid"][i])
+            d.since_last_svd = float(g["init_since"][i])
+            d.on_floor = int(g["init_on_floor"][i])
+            d.angle, d.ang_vel = float(g["init_angle"][i]), float(g["init_angvel"][i])
+            ev = oenv.envs[e]
+            for a in range(3):
+                ev.obs_vel[i][a] = g["init_env_vel"][i][a]
+                ev.obs_pos[i][a] = g["init_env_pos"][i][a]
+            ev.heading[i] = g["init_heading"][i]
+        ev = oenv.envs[e]
+        ev.tick = int(g["init_tick"])
+        ev.target[0], ev.target[1] = g["init_target"]
+        ev.capture_radius = float(g["init_capture"])
+        ev.has_pos = 1
+    oracle_to_gpu_a(oenv, env)
+    return g, cfg, env
+
+
+def test_reference_quiet_trajectory(golden):
+    """GPU against the reference itself: the noise-free flavor-A trajectory (no sensor, thrust or camera
+    noise, so no draws), 150 env steps = 1200 controller ticks, captures disabled by a tiny radius."""
+    g, cfg, env = load_golden_into_gpu(golden, "n4quiet")
+    worst = 0.0
+    for t in range(len(g["actions"])):
+        env.set_capture_radius(float(g["capture"][t]))
+        a = torch.from_numpy(np.ascontiguousarray(g["actions"][t], dtype=np.float32).reshape(-1, 2)).cuda()
+        obs, rew, done, _ = env.step(a)
+        np.testing.assert_array_equal(done.cpu().numpy().astype(bool), g["done"][t].astype(bool))
+        np.testing.assert_allclose(np_(rew), g["rew"][t], atol=1e-5)
+        assert_obs_match_a(np_(obs), g["obs"][t], cfg, atol=2e-3, rtol=1e-3, what=f"step {t}")
+        worst = max(worst, float(np.abs(np_(obs) - g["obs"][t]).max()))
+    f = env.drone_fields()
+    np.testing.assert_allclose(np_(f["pos"]), g["final_pos"], atol=2e-3)
+    print(f"max |obs - reference| over 150 steps: {worst:.2e}")
+
+
+def test_full_size_sb_train_properties():
+    """sb_train config at the BASELINE size (4096 envs x 8 drones): invariants the reference guarantees."""
+    cfg = QuadSwarmConfig.sb_train(num_envs=4096, num_agents=8, seed=3)
+    env = QuadSwarmEnv(cfg)
+    obs = env.reset()
+    assert torch.isfinite(obs).all()
+    assert (env.reset_info == 1).all()
+    rng = torch.Generator(device="cuda").manual_seed(0)
+    total_done = 0
+    for t in range(40):
+        if t == 20:
+            env.set_capture_radius(0.5)
+        a = torch.rand(env.I, 2, device="cuda", generator=rng) * 2 - 1
+        obs, rew, done, term = env.step(a)
+        assert torch.isfinite(obs).all()
+        r = rew.cpu().numpy()
+        assert np.all(np.isin(r, np.float32([-0.1, 99.9]))), np.unique(r)
+        d = done.cpu().numpy().reshape(4096, 8).astype(bool)
+        assert np.all(d.all(1) == d.any(1))              # an env finishes as a whole (:936-937)
+        ri = env.reset_info.cpu().numpy()
+        np.testing.assert_array_equal(ri > 0, d[:, 0])   # reset exactly the finished envs
+        cap_env = (r.reshape(4096, 8) > 50).any(1)
+        np.testing.assert_array_equal(ri == 2, cap_env & d[:, 0])
+        total_done += int(d[:, 0].sum())
+        if d[:, 0].any():
+            assert torch.isfinite(term.view(4096, 8, -1)[torch.from_numpy(d[:, 0]).cuda()]).all()
+    assert total_done > 0
+    tgt = env.env_f[:2].cpu().numpy()
+    assert np.all(np.hypot(tgt[0], tgt[1]) < 8.0)
+
+
+def test_deterministic_and_shard_invariant():
+    cfg = QuadSwarmConfig.sb_train(num_envs=64, num_agents=8, seed=9, pixel_noise_cam=3.0)
+    a = [QuadSwarmEnv(cfg) for _ in range(2)]
+    shards = []
+    for r in range(2):
+        c = QuadSwarmConfig.sb_train(num_envs=32, num_agents=8, seed=9, pixel_noise_cam=3.0,
+                                     drone_id_offset=r * 32 * 8)
+        shards.append(QuadSwarmEnv(c))
+    outs = [[e.reset().clone()] for e in a]
+    so = [[s.reset().clone()] for s in shards]
+    rng = np.random.default_rng(0)
+    for t in range(6):
+        act = torch.from_numpy(rng.uniform(-1, 1, (64 * 8, 2)).astype(np.float32)).cuda()
+        for e, o in zip(a, outs):
+            o.append(e.step(act)[0].clone())
+        for r, (s, o) in enumerate(zip(shards, so)):
+            o.append(s.step(act[r * 256:(r + 1) * 256].contiguous())[0].clone())
+    for x, y in zip(outs[0], outs[1]):
+        assert torch.equal(x, y)
+    for t in range(len(outs[0])):
+        assert torch.equal(outs[0][t], torch.cat([so[0][t], so[1][t]]))
+
+
+def test_partial_reset_and_snapshot():
+    cfg, env, oenv = make_pair("sb8", E=64)
+    env.reset()
+    oenv.reset()
+    mask = np.zeros(64, dtype=np.uint8)
+    mask[::3] = 1
+    blob = env.get_state()
+    obs = np_(env.reset(mask))
+    want, ri = oenv.reset(mask)
+    sel = np.repeat(mask.astype(bool), 8)
+    assert_obs_match_a(obs[sel], want[sel], cfg, atol=5e-5, rtol=2e-5, oenv=oenv, what="partial reset")
+    np.testing.assert_array_equal(env.reset_info.cpu().numpy(), ri)
+    env.set_state(blob)   # snapshot restores the pre-reset state exactly, RNG counters included
+    o1 = env.step(torch.zeros(env.I, 2, device="cuda"))[0].clone()
+    env.set_state(blob)
+    o2 = env.step(torch.zeros(env.I, 2, device="cuda"))[0].clone()
+    assert torch.equal(o1, o2)
+
+
+def test_vec_env_surface_flavor_a():
+    venv = GpuQuadVecEnv(QuadSwarmConfig.sb_train(num_envs=16, num_agents=4, seed=1))
+    assert venv.num_envs == 64 and venv.action_space.shape == (2,) and venv.observation_space.shape == (16,)
+    obs = venv.reset()
+    assert obs.shape == (64, 16) and obs.dtype == np.float32
+    assert venv.reset_infos == tuple({"success": False} for _ in range(16))
+    assert venv.get_attr("capture_radius", indices=[0, 5]) == [3.0, 3.0]
+    venv.env_method("set_capture_radius", 0.0, indices=list(range(8, 16)))
+    assert venv.get_attr("capture_radius", indices=[7, 8]) == [3.0, 0.0]
+    obs, rew, dones, infos = venv.step(np.zeros((64, 2), np.float32))
+    assert len(infos) == 64
+    # spawn within 0.5 m of the origin, target 2-5 m away: radius 3 captures some envs at once
+    d = dones.reshape(16, 4)
+    assert d[:8].any() and not d[8:].any()
+    for e in range(16):
+        if d[e, 0]:
+            assert venv.reset_infos[e] == {"success": True}
+            assert "terminal_observation" in infos[4 * e]
+        else:
+            assert venv.reset_infos[e] is None
+    venv.close()
