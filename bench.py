@@ -23,21 +23,42 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "quad-swarm-rl-stable-baselines3_amd"))
 
-# BASELINE.json configs -> (envs per GPU, agents, visible neighbours, downwash)
+# BASELINE.json configs -> (envs per GPU, agents, visible neighbours, downwash); "a*" = flavor A as
+# swarm_rl/sb_train.py trains it (QuadSwarmConfig.sb_train), capture radius at a late curriculum stage
 CONFIGS = {
     "c2": dict(num_envs=16384, num_agents=1, neighbor_visible_num=0, neighbor_obs_type="none"),
     "c3": dict(num_envs=4096, num_agents=8, neighbor_visible_num=6, neighbor_obs_type="pos_vel"),
     "c5": dict(num_envs=1024, num_agents=32, neighbor_visible_num=6, neighbor_obs_type="pos_vel"),
+    "a8": dict(flavor="A", num_envs=4096, num_agents=8, initial_capture_radius=0.5),
+    "a4": dict(flavor="A", num_envs=8192, num_agents=4, initial_capture_radius=0.5),
 }
 WORKLOAD = {"c2": "single_quad x 16384 envs", "c3": "8-drone swarm static_same_goal x 4096 envs (pos_vel k=6)",
-            "c5": "32-drone swarm x 1024 envs per GPU (pos_vel k=6)"}
+            "c5": "32-drone swarm x 1024 envs per GPU (pos_vel k=6)",
+            "a8": "flavor A (sb_train env: PID pre-controller x 8 ticks, dynamic_repulsive target, ndist_nsangle "
+                  "camera neighbours k=7) 8 drones x 4096 envs, capture radius 0.5",
+            "a4": "flavor A sb_train default 4 drones x 8192 envs (k=3), capture radius 0.5"}
+
+
+def make_cfg(kw, **extra):
+    from quadswarm_amd import QuadSwarmConfig
+    kw = dict(kw)
+    if kw.pop("flavor", "B") == "A":
+        return QuadSwarmConfig.sb_train(**kw, **extra)
+    return QuadSwarmConfig(**kw, **extra)
+
+
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 
 
-def algorithmic_bytes_per_agent_step(obs_dim, n_agents):
+def algorithmic_bytes_per_agent_step(obs_dim, n_agents, flavor="B"):
     """B = 4 (S_r + S_w + A + O + 1) + 1 with S_r = 33 persistent fp32 state
     (pos3 vel3 rot9 omega3 cmd_damp4 rot_damp4 OU4 goal3), S_w = 30, A = 4, O = obs_dim, +1 reward,
-    +1 byte done.  C3: 489 B, C2: 345 B."""
+    +1 byte done.  C3: 489 B, C2: 345 B.
+    Flavor A: S_r = S_w = 55 (+ PID 20, heading, heading rate; the goal moves with the target), A = 2,
+    plus per env (tick/flags/episode r+w 24 B, target r+w 16 B, capture radius 4 B, reset_info 1 B) / N.
+    A8 (obs 28): 570.6 B."""
+    if flavor == "A":
+        return 4 * (55 + 55 + 2 + obs_dim + 1) + 1 + 45.0 / n_agents
     return 4 * (33 + 30 + 4 + obs_dim + 1) + 1
 
 
@@ -47,15 +68,18 @@ def cpu_baseline(cfg_kw, seconds=10.0):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle as O
-    from parity_utils import oracle_params
-    from quadswarm_amd import QuadSwarmConfig
+    from parity_utils import oracle_params, oracle_params_a
 
     cores = len(os.sched_getaffinity(0))
     cores = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
-    cfg = QuadSwarmConfig(**cfg_kw)
-    env = O.OracleEnv(oracle_params(cfg), seed=0)
+    cfg = make_cfg(cfg_kw)
+    if cfg.flavor == "A":
+        env = O.OracleEnvA(oracle_params_a(cfg), seed=0)
+        env.set_capture_radius(cfg.initial_capture_radius)
+    else:
+        env = O.OracleEnv(oracle_params(cfg), seed=0)
     env.reset()
-    a = np.random.default_rng(1234).uniform(-1.0, 1.0, (cfg.num_envs * cfg.num_agents, 4))
+    a = np.random.default_rng(1234).uniform(-1.0, 1.0, (cfg.num_envs * cfg.num_agents, cfg.act_dim))
     env.step(a, nthreads=cores)
     steps, t0 = 0, time.perf_counter()
     while True:
@@ -76,6 +100,13 @@ def cpu_baseline(cfg_kw, seconds=10.0):
             "kind": "port",
             "sample": f"{steps} steps x {cfg.num_envs} envs x {cfg.num_agents} drones, fp64 C oracle, "
                       f"{cores} OpenMP threads, {el:.1f} s on '{model}'"}
+
+
+def npad(n):
+    p = 1
+    while p < n:
+        p <<= 1
+    return p
 
 
 def pmc_traffic(config):
@@ -113,16 +144,15 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    from quadswarm_amd import QuadSwarmConfig
     from quadswarm_amd.env import QuadSwarmEnv
 
     kw = CONFIGS[args.config]
-    cfg = QuadSwarmConfig(**kw, seed=0)
+    cfg = make_cfg(kw, seed=0)
     I = cfg.num_envs * cfg.num_agents
     cfg.drone_id_offset = rank * I
     env = QuadSwarmEnv(cfg, device=dev)
     gen = torch.Generator(device=dev).manual_seed(1234)
-    actions = (torch.rand(I, 4, device=dev, generator=gen) * 2.0 - 1.0).contiguous()
+    actions = (torch.rand(I, cfg.act_dim, device=dev, generator=gen) * 2.0 - 1.0).contiguous()
     env.reset()
 
     stream = torch.cuda.current_stream(dev)
@@ -180,7 +210,7 @@ def main():
 
     if rank == 0:
         value = world * I * args.steps / el
-        bpa = algorithmic_bytes_per_agent_step(cfg.obs_dim, cfg.num_agents)
+        bpa = algorithmic_bytes_per_agent_step(cfg.obs_dim, cfg.num_agents, cfg.flavor)
         achieved = bpa * I / (k_ms * 1e-3) / 1e9
         traffic = pmc_traffic(args.config)
         out = {
@@ -197,16 +227,19 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic: U(-1,1) actions (seed 1234) from a fixed device buffer; Crazyflie constants; "
-                    "static_same_goal spawns (Philox seed 0)",
+                    + ("static_same_goal spawns (Philox seed 0)" if cfg.flavor == "B" else
+                       "dynamic_repulsive target and spawns (Philox seed 0)"),
             "config": {"workload": WORKLOAD[args.config], "envs_per_gpu": cfg.num_envs,
                        "agents_per_env": cfg.num_agents, "visible_neighbors": cfg.k_neighbors,
                        "obs_dim": cfg.obs_dim, "global_batch": world * I, "parallelism": f"env-shard x{world}",
+                       "flavor": cfg.flavor,
                        "launch": f"hipGraph of {chunk} steps" if chunk else "eager"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic, "kernel": "qs::step_kernel<8>" if cfg.num_agents == 8 else "qs::step_kernel",
-                         "kernel_us": round(k_ms * 1e3, 3), "bytes_per_agent_step": bpa,
-                         "bytes_per_launch": bpa * I},
+                         "traffic": traffic,
+                         "kernel": f"qs::step_kernel{'_a' if cfg.flavor == 'A' else ''}<{npad(cfg.num_agents)}>",
+                         "kernel_us": round(k_ms * 1e3, 3), "bytes_per_agent_step": round(bpa, 1),
+                         "bytes_per_launch": round(bpa * I)},
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:

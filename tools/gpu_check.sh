@@ -22,12 +22,21 @@ for s in "$@"; do
     testsall) step gpu_tests 900 python -m pytest tests -m gpu -q ;;
     bench) step bench 400 python bench.py ;;
     benchfast) step bench 300 python bench.py --steps 1000 --cpu-seconds 5 ;;
+    bencha) step bench_a8 400 python bench.py --config a8 --steps 1000 --cpu-seconds 10 ;;
+    bencha4) step bench_a4 400 python bench.py --config a4 --steps 1000 --cpu-seconds 5 ;;
     prof)
       export TMPDIR=/tmp
       step prof_kt 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_kt -o kt --output-format csv -- python bench.py --steps 1000 --no-cpu-baseline --graph 0
       step prof_fetch 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof_fetch -o f --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu-baseline --graph 0
       step prof_write 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof_write -o w --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu-baseline --graph 0
       step prof_sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INSTS_LDS -d gpurun_out/prof_sq -o s --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu-baseline --graph 0
+      ;;
+    profa)
+      export TMPDIR=/tmp
+      step profa_kt 400 rocprofv3 --kernel-trace --stats -d gpurun_out/profa_kt -o kt --output-format csv -- python bench.py --config a8 --steps 1000 --no-cpu-baseline --graph 0
+      step profa_fetch 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/profa_fetch -o f --output-format csv -- python bench.py --config a8 --steps 100 --warmup 10 --no-cpu-baseline --graph 0
+      step profa_write 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/profa_write -o w --output-format csv -- python bench.py --config a8 --steps 100 --warmup 10 --no-cpu-baseline --graph 0
+      step profa_sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INSTS_LDS -d gpurun_out/profa_sq -o s --output-format csv -- python bench.py --config a8 --steps 100 --warmup 10 --no-cpu-baseline --graph 0
       ;;
     stamps) step stamps 300 python tools/phase_stamps.py ;;
     calib)

@@ -42,15 +42,16 @@ def main():
     ap.add_argument("--round", type=int, default=1)
     ap.add_argument("--config", default="c3")
     ap.add_argument("--kernel", default="step_kernel")
+    ap.add_argument("--prefix", default="prof", help="gpurun_out/<prefix>_{kt,fetch,write,sq} (profa for flavor A)")
     args = ap.parse_args()
     tag = f"r{args.round:02d}_{args.config}"
     os.makedirs(PROF, exist_ok=True)
-    ks = glob.glob(os.path.join(OUT, "prof_kt", "*kernel_stats.csv"))
+    ks = glob.glob(os.path.join(OUT, f"{args.prefix}_kt", "*kernel_stats.csv"))
     stats = {}
     if ks:
         shutil.copy(ks[0], os.path.join(PROF, f"{tag}_kernel_stats.csv"))
         for r in csv.DictReader(open(ks[0])):
-            if args.kernel in r["Name"]:
+            if args.kernel + "<" in r["Name"] or args.kernel + "I" in r["Name"]:
                 stats = {"name": r["Name"], "calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
                          "min_ns": float(r["MinNs"]), "max_ns": float(r["MaxNs"])}
                 break
@@ -65,8 +66,10 @@ def main():
                 calib[f"{short}:{kind}"] = (sorted(v)[len(v) // 2] * 1024.0) / CALIB_BYTES
 
     res = {"kernel": stats.get("name"), "config": args.config, "kernel_trace": stats, "calibration_ratio": calib}
-    for pat in ("prof_fetch/*counter_collection.csv", "prof_write/*counter_collection.csv", "prof_sq/*counter_collection.csv"):
-        for (kname, cname), v in counters(pat, args.kernel).items():
+    for pat in ("_fetch/*counter_collection.csv", "_write/*counter_collection.csv", "_sq/*counter_collection.csv"):
+        for (kname, cname), v in counters(args.prefix + pat, args.kernel).items():
+            if not (args.kernel + "<" in kname or args.kernel + "I" in kname):
+                continue
             res.setdefault("counters_per_launch", {})[cname] = sum(v) / len(v)
             res.setdefault("launches_sampled", {})[cname] = len(v)
     c = res.get("counters_per_launch", {})
