@@ -45,6 +45,8 @@ class OrParams(ctypes.Structure):
         ("m_mass", D), ("m_g", D), ("m_kf", D), ("m_min_rpm", D), ("m_max_rpm", D), ("m_n_motors", I),
         ("w_captor", D), ("w_helper", D), ("existence", D),
         ("target_vmax", D), ("target_dt", D), ("arena_size", D), ("target_z", D),
+        ("use_obstacles", I), ("num_obstacles", I), ("obst_area", I), ("obst_scenario", I),
+        ("obst_size", D), ("obst_z", D), ("sdf_resolution", D), ("rew_quadcol_bin_obst", D),
     ]
 
 
@@ -56,14 +58,15 @@ class OrDrone(ctypes.Structure):
         ("on_floor", I), ("crashed_floor", I), ("crashed_wall", I), ("crashed_ceiling", I),
         ("prev_wall", I), ("prev_ceiling", I),
         ("goal", D * 3),
-        ("pid", D * 20), ("angle", D), ("ang_vel", D),
+        ("pid", D * 20), ("angle", D), ("ang_vel", D), ("prev_obst", I),
     ]
 
 
 class OrEnv(ctypes.Structure):
     _fields_ = [("tick", I), ("episode", ctypes.c_uint32), ("prev_pair_bits", ctypes.c_ubyte * (64 * 64)),
                 ("obs_pos", (D * 3) * 64), ("obs_vel", (D * 3) * 64),
-                ("heading", D * 64), ("target", D * 2), ("capture_radius", D), ("success", I), ("has_pos", I)]
+                ("heading", D * 64), ("target", D * 2), ("capture_radius", D), ("success", I), ("has_pos", I),
+                ("n_obst", I), ("obst", (D * 2) * 64), ("obst_mode", I)]
 
 
 class OrRng(ctypes.Structure):
@@ -125,6 +128,11 @@ def lib():
         L.or_step_all_a.argtypes = [P(OrParams), P(OrDrone), P(OrEnv), P(D), ctypes.c_uint32, P(D), P(D), U8,
                                     P(D), U8, I]
         L.or_obs_dim_a.argtypes = [P(OrParams)]
+        L.or_obst_sdf.argtypes = [P(OrParams), P(OrEnv), P(D), P(D)]
+        L.or_obst_detect.argtypes = [P(OrParams), P(OrEnv), P(D)]
+        L.or_collide_obstacle.argtypes = [P(OrParams), P(OrDrone), P(D), P(OrRng), ctypes.c_uint32]
+        L.or_max_square_center.argtypes = [P(ctypes.c_ubyte), I, P(D)]
+        L.or_cell_xy.argtypes = [I, I, I, P(D)]
         L.or_philox4x32_10.argtypes = [P(ctypes.c_uint32), P(ctypes.c_uint32), P(ctypes.c_uint32)]
         L.or_philox_normal.argtypes = [ctypes.c_uint32] * 3 + [ctypes.c_uint64, ctypes.c_uint32]
         L.or_philox_normal.restype = D

@@ -188,6 +188,9 @@ void or_params_default(or_params* p) {
     p->use_downwash = 0; p->apply_collision_force = 1;
     p->spawn_box = 2.0;
     p->goal[0] = 0; p->goal[1] = 0; p->goal[2] = 2.0;
+    /* obstacles off; C4 values when enabled (swarm_rl/runs/obstacles/quad_obstacle_baseline.py) */
+    p->use_obstacles = 0; p->num_obstacles = 12; p->obst_area = 8; p->obst_scenario = 0;
+    p->obst_size = 0.6; p->obst_z = 5.0; p->sdf_resolution = 0.1; p->rew_quadcol_bin_obst = 5.0;
 }
 
 /* OUNoiseNumba.noise (numba_utils.py:101-105): x <- x + theta(mu - x) + sigma randn(4) */
@@ -384,7 +387,7 @@ void or_sensor_noise(const or_params* p, const double pos[3], const double vel[3
 
 static int self_obs_dim(const or_params* p) { return p->obs_repr == 0 ? 18 : (p->obs_repr == 1 ? 19 : 24); }
 
-int or_obs_dim(const or_params* p) { return self_obs_dim(p) + 6 * p->k_neighbors; }
+int or_obs_dim(const or_params* p) { return self_obs_dim(p) + 6 * p->k_neighbors + (p->use_obstacles ? 9 : 0); }
 
 /* get_state.state_xyz_vxyz_R_omega[_floor|_wall] (get_state.py:226-292) */
 static void self_obs(const or_params* p, const or_drone* d, or_rng* r, uint32_t gid, uint32_t st, double* out) {
@@ -608,6 +611,183 @@ static int downwash(const or_params* p, or_drone* dr, int N, uint32_t gbase, or_
 }
 
 /* ------------------------------------------------------------------------------------------ */
+/* obstacles (flavor B)                                                            */
+/* ------------------------------------------------------------------------------------------ */
+/* get_cell_centers (obstacles/utils.py:46-58) as the env indexes it: grid cell (row, col) of the
+ * n x n spawn area -> cell_centers[row + n*col] (quadrotor_multi.py:422, o_base.py:89-92) */
+void or_cell_xy(int row, int col, int n, double out[2]) {
+    const double h = (double)(n / 2);
+    out[0] = (double)col + 0.5 - h;
+    out[1] = (double)(n - 1 - row) + 0.5 - h;
+}
+
+/* get_surround_sdfs (obstacles/utils.py:4-27): 3x3 grid at +-resolution, min distance - radius */
+void or_obst_sdf(const or_params* p, const or_env* ev, const double xy[2], double out[9]) {
+    const double res = p->sdf_resolution, rad = p->obst_size / 2.0;
+    const double gx[3] = {xy[0] - res, xy[0], xy[0] + res}, gy[3] = {xy[1] - res, xy[1], xy[1] + res};
+    for (int a = 0; a < 3; ++a)
+        for (int b = 0; b < 3; ++b) {
+            double md = 100.0;
+            for (int o = 0; o < ev->n_obst; ++o) {
+                double dx = gx[a] - ev->obst[o][0], dy = gy[b] - ev->obst[o][1];
+                double d = sqrt(dx * dx + dy * dy);
+                if (d < md) md = d;
+            }
+            out[a * 3 + b] = md - rad;
+        }
+}
+
+/* collision_detection (obstacles/utils.py:30-43): first obstacle within arm + radius (xy) */
+int or_obst_detect(const or_params* p, const or_env* ev, const double xy[2]) {
+    const double thr = p->arm + p->obst_size / 2.0;
+    for (int o = 0; o < ev->n_obst; ++o) {
+        double dx = xy[0] - ev->obst[o][0], dy = xy[1] - ev->obst[o][1];
+        if (sqrt(dx * dx + dy * dy) <= thr) return o;
+    }
+    return -1;
+}
+
+/* perform_collision_with_obstacle (collisions/obstacles.py:23-50) with
+ * compute_col_norm_and_new_vel_obst (:8-20).  Philox indices (stream OBST): normals t*6+0..2 (0.1),
+ * t*6+3..5 (0.05) for try t; uniforms 0 decay ratio, 1-3 omega direction, 4 omega magnitude. */
+void or_collide_obstacle(const or_params* p, or_drone* d, const double opos[3], or_rng* r, uint32_t gid) {
+    double n[3] = {d->pos[0] - opos[0], d->pos[1] - opos[1], 0.0};
+    double nm = norm3(n);
+    double den = nm == 0.0 ? nm + EPS_UTIL : nm;
+    for (int c = 0; c < 3; ++c) n[c] /= den;
+    const double vm = norm3(d->vel);
+    double nv[3] = {vm * n[0], vm * n[1], vm * n[2]};
+    double noise[3] = {0, 0, 0};
+    for (int t = 0; t < 3; ++t) {
+        double cons[3], tmp[3];
+        for (int c = 0; c < 3; ++c) cons[c] = rn(r, gid, OR_S_OBST, (uint32_t)(t * 6 + c), 0.0, 0.1);
+        for (int c = 0; c < 3; ++c) tmp[c] = cons[c] + rn(r, gid, OR_S_OBST, (uint32_t)(t * 6 + 3 + c), 0.0, 0.05);
+        if ((nv[0] + tmp[0]) * n[0] + (nv[1] + tmp[1]) * n[1] + (nv[2] + tmp[2]) * n[2] > 0) {
+            memcpy(noise, tmp, sizeof tmp);
+            break;
+        }
+    }
+    const double max_v = norm3(d->vel);
+    double dp[3] = {d->pos[0] - opos[0], d->pos[1] - opos[1], d->pos[2] - opos[2]};
+    const int inside = norm3(dp) < p->obst_size / 2.0;
+    double shift[3];
+    for (int c = 0; c < 3; ++c) shift[c] = nv[c] - d->vel[c] + noise[c];
+    double ratio = inside ? ru(r, gid, OR_S_OBST, 0, 1.0, 1.0) : ru(r, gid, OR_S_OBST, 0, 0.2, 0.8);
+    new_vel(max_v, d->vel, shift, ratio);
+    double w[3];
+    new_omega(r, gid, OR_S_OBST, 1, 1.0, w);
+    for (int c = 0; c < 3; ++c) d->omega[c] += w[c];
+}
+
+/* Scenario_o_base.max_square_area_center (o_base.py:125-153), quirks included: dp's first row and
+ * column start as the obstacle map itself, the centre is (i - (s-1)//2, j - (s-1)//2). */
+void or_max_square_center(const unsigned char* map, int n, double out_xy[2]) {
+    int dp[64][64];
+    memset(dp, 0, sizeof dp);
+    for (int j = 0; j < n; ++j) dp[0][j] = map[j];
+    for (int i = 0; i < n; ++i) dp[i][0] = map[i * n];
+    int ms = 0, cx = 0, cy = 0;
+    for (int i = 1; i < n; ++i)
+        for (int j = 1; j < n; ++j)
+            if (map[i * n + j] == 0) {
+                int a = dp[i - 1][j], b = dp[i][j - 1], c = dp[i - 1][j - 1];
+                int m = a < b ? a : b;
+                m = m < c ? m : c;
+                dp[i][j] = m + 1;
+                if (dp[i][j] > ms) {
+                    ms = dp[i][j];
+                    cx = i - (ms - 1) / 2;
+                    cy = j - (ms - 1) / 2;
+                }
+            }
+    /* cell_centers[cx + n*cy] */
+    or_cell_xy(cx, cy, n, out_xy);
+}
+
+/* partial Fisher-Yates: the first k of a uniformly random permutation of 0..n-1 (Philox stand-in for
+ * np.random.choice(n, k, replace=False), same distribution) */
+static void choose_k(or_rng* r, uint32_t gid, uint32_t st, uint32_t u0, int n, int k, int* out) {
+    int a[64];
+    for (int i = 0; i < n; ++i) a[i] = i;
+    for (int i = 0; i < k; ++i) {
+        double u = or_philox_uniform(r->seed, gid, st | OR_UNIF_BIT, r->step, u0 + (uint32_t)i);
+        int j = i + (int)(u * (double)(n - i));
+        if (j > n - 1) j = n - 1;
+        int t = a[i]; a[i] = a[j]; a[j] = t;
+        out[i] = a[i];
+    }
+}
+
+/* obstacle map + scenario for one env reset (quadrotor_multi.py:405-426, 449-452; scenarios/mix.py:78-99;
+ * o_random.py:26-51; o_static_same_goal.py:28-48; o_base.py:58-92).  Fills per-drone spawn points
+ * and goals. */
+static void obstacle_reset(const or_params* p, or_env* ev, uint32_t gbase, or_rng* r, double spawn[][3],
+                           double goal[][3]) {
+    const int n = p->obst_area, M = p->num_obstacles, N = p->num_agents, tape = r->mode == OR_RNG_TAPE;
+    unsigned char map[64 * 64];
+    memset(map, 0, sizeof map);
+    int ids[64];
+    if (tape) for (int o = 0; o < M; ++o) ids[o] = (int)tape_next(r);
+    else choose_k(r, gbase, OR_S_OBSTMAP, 0, n * n, M, ids);
+    ev->n_obst = M;
+    for (int o = 0; o < M; ++o) {
+        int rid = ids[o] / n, cid = ids[o] % n;
+        map[rid * n + cid] = 1;
+        or_cell_xy(rid, cid, n, ev->obst[o]);
+    }
+    int mode;
+    if (p->obst_scenario == 0) mode = tape ? ((int)spawn_next(r)) % 2
+                                           : (or_philox_uniform(r->seed, gbase, OR_S_OSCEN | OR_UNIF_BIT, r->step, 0) < 0.5 ? 0 : 1);
+    else mode = p->obst_scenario - 1;
+    ev->obst_mode = mode;
+    int fr[64 * 64], F = 0;
+    for (int i = 0; i < n * n; ++i) if (!map[i]) fr[F++] = i;   /* np.where(map == 0): row-major */
+    int sp[64], gl[64];
+    double sz[64], gz[64], ez = 0.0;
+    if (mode == 0) {   /* o_random */
+        if (tape) {
+            for (int k = 0; k < 2 * N; ++k) { (void)tape_next(r); (void)tape_next(r); }   /* generate_pos_obst_map x2N */
+            for (int i = 0; i < N; ++i) sp[i] = (int)tape_next(r);
+            for (int i = 0; i < N; ++i) sz[i] = tape_next(r);
+            for (int i = 0; i < N; ++i) gl[i] = (int)tape_next(r);
+            for (int i = 0; i < N; ++i) gz[i] = tape_next(r);
+            (void)tape_next(r);   /* duration_step */
+        } else {
+            choose_k(r, gbase, OR_S_OSCEN, 1, F, N, sp);
+            choose_k(r, gbase, OR_S_OSCEN, 1 + (uint32_t)N, F, N, gl);
+            for (int i = 0; i < N; ++i) {
+                sz[i] = 1.0 + 2.0 * or_philox_uniform(r->seed, gbase + (uint32_t)i, OR_S_RESET | OR_UNIF_BIT, r->step, 3);
+                gz[i] = 1.0 + 2.0 * or_philox_uniform(r->seed, gbase + (uint32_t)i, OR_S_RESET | OR_UNIF_BIT, r->step, 4);
+            }
+        }
+        for (int i = 0; i < N; ++i) {
+            int a = fr[sp[i]], b = fr[gl[i]];
+            or_cell_xy(a / n, a % n, n, spawn[i]); spawn[i][2] = sz[i];
+            or_cell_xy(b / n, b % n, n, goal[i]); goal[i][2] = gz[i];
+        }
+    } else {           /* o_static_same_goal */
+        if (tape) {
+            (void)tape_next(r);   /* duration_time */
+            for (int i = 0; i < N; ++i) sp[i] = (int)tape_next(r);
+            for (int i = 0; i < N; ++i) sz[i] = tape_next(r);
+            ez = tape_next(r);
+        } else {
+            choose_k(r, gbase, OR_S_OSCEN, 1, F, N, sp);
+            for (int i = 0; i < N; ++i)
+                sz[i] = 1.0 + 2.0 * or_philox_uniform(r->seed, gbase + (uint32_t)i, OR_S_RESET | OR_UNIF_BIT, r->step, 3);
+            ez = 1.5 + 1.5 * or_philox_uniform(r->seed, gbase, OR_S_OSCEN | OR_UNIF_BIT, r->step, 2 * (uint32_t)N + 1);
+        }
+        double exy[2];
+        or_max_square_center(map, n, exy);
+        for (int i = 0; i < N; ++i) {
+            int a = fr[sp[i]];
+            or_cell_xy(a / n, a % n, n, spawn[i]); spawn[i][2] = sz[i];
+            goal[i][0] = exy[0]; goal[i][1] = exy[1]; goal[i][2] = ez;
+        }
+    }
+}
+
+/* ------------------------------------------------------------------------------------------ */
 /* env step / reset                                                                            */
 /* ------------------------------------------------------------------------------------------ */
 /* QuadrotorSingle._reset (quadrotor_single.py:401-469), static_same_goal goals
@@ -616,16 +796,24 @@ void or_env_reset(const or_params* p, or_drone* drones, or_env* envs, int e, or_
     const int N = p->num_agents, od = or_obs_dim(p);
     or_env* ev = &envs[e];
     r->step = ((uint64_t)ev->episode << 32) | (uint32_t)ev->tick;   /* env Philox counter */
+    const uint32_t gbase = p->id_offset + (uint32_t)((size_t)e * N);
+    double spawn[64][3], goal[64][3];
+    if (p->use_obstacles) {
+        obstacle_reset(p, ev, gbase, r, spawn, goal);
+    } else {
+        for (int i = 0; i < N; ++i)
+            for (int c = 0; c < 3; ++c) spawn[i][c] = goal[i][c] = p->goal[c];
+    }
     for (int i = 0; i < N; ++i) {
         or_drone* d = &drones[(size_t)e * N + i];
-        uint32_t gid = p->id_offset + (uint32_t)((size_t)e * N + i);
-        for (int c = 0; c < 3; ++c) d->goal[c] = p->goal[c];
+        uint32_t gid = gbase + (uint32_t)i;
+        for (int c = 0; c < 3; ++c) d->goal[c] = goal[i][c];
         double xyz[3];
         for (int c = 0; c < 3; ++c) {
             double u = (r->mode == OR_RNG_TAPE) ? spawn_next(r)
                                                 : -p->spawn_box + 2 * p->spawn_box *
                                                       or_philox_uniform(r->seed, gid, OR_S_RESET | OR_UNIF_BIT, r->step, (uint32_t)c);
-            xyz[c] = u + d->goal[c];
+            xyz[c] = u + spawn[i][c];
         }
         if (xyz[2] < 0.75) xyz[2] = 0.75;
         for (int c = 0; c < 3; ++c) { d->pos[c] = xyz[c]; d->vel[c] = 0.0; d->omega[c] = 0.0; d->acc[c] = 0.0; }
@@ -641,7 +829,7 @@ void or_env_reset(const or_params* p, or_drone* drones, or_env* envs, int e, or_
         }
         for (int k = 0; k < 4; ++k) { d->thrust_cmds_damp[k] = 0.0; d->thrust_rot_damp[k] = 0.0; }
         d->on_floor = 0; d->crashed_floor = 0; d->crashed_wall = 0; d->crashed_ceiling = 0;
-        d->prev_wall = 0; d->prev_ceiling = 0;
+        d->prev_wall = 0; d->prev_ceiling = 0; d->prev_obst = 0;
         self_obs(p, d, r, gid, OR_S_RESET_SENSOR, obs + (size_t)i * od);
         for (int c = 0; c < 3; ++c) ev->obs_pos[i][c] = d->pos[c];
     }
@@ -649,6 +837,8 @@ void or_env_reset(const or_params* p, or_drone* drones, or_env* envs, int e, or_
     ev->episode += 1;
     memset(ev->prev_pair_bits, 0, sizeof ev->prev_pair_bits);
     neighbor_obs(p, ev, obs, od);   /* uses fresh obs_pos and the stale obs_vel (:477) */
+    if (p->use_obstacles)           /* MultiObstacles.reset (obstacles/obstacles.py:15-26) */
+        for (int i = 0; i < N; ++i) or_obst_sdf(p, ev, ev->obs_pos[i], obs + (size_t)i * od + od - 9);
 }
 
 /* QuadrotorEnvMulti.step (quadrotor_multi.py:521-841) with QuadrotorSingle._step
@@ -724,10 +914,17 @@ void or_env_step(const or_params* p, or_drone* drones, or_env* envs, int e, cons
         dr[i].prev_wall = wall_new[i];
         dr[i].prev_ceiling = ceil_new[i];
     }
+    /* 2) obstacles (quadrotor_multi.py:570-589): first obstacle hit per drone, new vs previous step */
+    int ocol[64], onew[64];
+    for (int i = 0; i < N; ++i) {
+        ocol[i] = p->use_obstacles ? or_obst_detect(p, ev, ev->obs_pos[i]) : -1;
+        onew[i] = ocol[i] >= 0 && !dr[i].prev_obst;
+    }
     for (int i = 0; i < N; ++i) {
         double rc = (any_nonzero && in_cur[i] && !in_prev[i]) ? -1.0 : 0.0;
         rw[i] += p->rew_quadcol_bin * rc;
         rw[i] += any_near ? -1.0 * (p->control_dt * pen[i]) : 0.0;
+        if (p->use_obstacles) rw[i] += p->rew_quadcol_bin_obst * (onew[i] ? -1.0 : 0.0);
     }
     /* 3. random forces (quadrotor_multi.py:659-698) */
     int flag = 0;
@@ -740,17 +937,26 @@ void or_env_step(const or_params* p, or_drone* drones, or_env* envs, int e, cons
                     or_collide_drones(dr[i].pos, dr[i].vel, dr[i].omega, dr[j].pos, dr[j].vel, dr[j].omega,
                                       r, gbase + (uint32_t)i, (uint32_t)j);
                 }
+        for (int i = 0; i < N; ++i)   /* 3) obstacles, curr_quad_col ascending (:680-689) */
+            if (onew[i]) {
+                flag = 1;
+                const double op[3] = {ev->obst[ocol[i]][0], ev->obst[ocol[i]][1], p->obst_z};
+                or_collide_obstacle(p, &dr[i], op, r, gbase + (uint32_t)i);
+            }
         for (int i = 0; i < N; ++i) if (wall_new[i]) { flag = 1; or_collide_wall(p, &dr[i], r, gbase + (uint32_t)i); }
         for (int i = 0; i < N; ++i) if (ceil_new[i]) { flag = 1; or_collide_ceiling(&dr[i], r, gbase + (uint32_t)i); }
     }
     for (int i = 0; i < N; ++i)
         for (int j = i + 1; j < N; ++j) ev->prev_pair_bits[i * 64 + j] = cur[i][j];
+    for (int i = 0; i < N; ++i) dr[i].prev_obst = ocol[i] >= 0;
     /* 5. refresh and observations (:704-716) */
     for (int i = 0; i < N; ++i)
         for (int c = 0; c < 3; ++c) { ev->obs_pos[i][c] = dr[i].pos[c]; ev->obs_vel[i][c] = dr[i].vel[c]; }
     if (flag)
         for (int i = 0; i < N; ++i) self_obs(p, &dr[i], r, gbase + (uint32_t)i, OR_S_SENSOR, o + (size_t)i * od);
     neighbor_obs(p, ev, o, od);
+    if (p->use_obstacles)   /* MultiObstacles.step (obstacles/obstacles.py:28-35) */
+        for (int i = 0; i < N; ++i) or_obst_sdf(p, ev, ev->obs_pos[i], o + (size_t)i * od + od - 9);
     for (int i = 0; i < N; ++i) done[(size_t)e * N + i] = (unsigned char)is_done;
     if (is_done) {
         if (term_obs) memcpy(term_obs + (size_t)e * N * od, o, sizeof(double) * (size_t)N * od);

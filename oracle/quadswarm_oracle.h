@@ -45,6 +45,9 @@ enum {
     OR_S_RESET_CAM = 18,
     OR_S_RESET_CAM_SEL = 19,
     OR_S_RESET_SELF_CAM = 20,
+    /* obstacles (flavor B) */
+    OR_S_OBSTMAP = 21,    /* per env: uniforms 0..M-1 partial Fisher-Yates over the grid cells     */
+    OR_S_OSCEN = 22,      /* per env: uniform 0 mode, 1..N spawn cells, N+1..2N goal cells, 2N+1 goal z */
     OR_UNIF_BIT = 0x80    /* uniform draws use stream | OR_UNIF_BIT           */
 };
 
@@ -117,6 +120,15 @@ typedef struct {
     int m_n_motors;
     double w_captor, w_helper, existence;
     double target_vmax, target_dt, arena_size, target_z;
+    /* ---- obstacles (flavor B): quadrotor_multi.py:128-140, 405-426; obstacles/; scenarios/obstacles/ ---- */
+    int use_obstacles;
+    int num_obstacles;         /* int(density * area_l * area_w)                          */
+    int obst_area;             /* spawn area side (8), 1 m grid cells                     */
+    int obst_scenario;         /* 0 = mix (o_random / o_static_same_goal), 1 = o_random, 2 = o_static_same_goal */
+    double obst_size;          /* diameter (0.6); radius = size / 2                        */
+    double obst_z;             /* pillar centre z = room height / 2 (only the 3-D inside test) */
+    double sdf_resolution;     /* 0.1                                                      */
+    double rew_quadcol_bin_obst;
 } or_params;
 
 /* Per-drone state (QuadrotorDynamics attributes + QuadrotorSingle bookkeeping). */
@@ -131,6 +143,7 @@ typedef struct {
     /* flavor A: Controller state (PIDs that reach an output, heading, last command) */
     double pid[2 * OR_NPID];
     double angle, ang_vel;
+    int prev_obst;             /* in prev_obst_quad_collisions (quadrotor_multi.py:585) */
 } or_drone;
 
 typedef struct {
@@ -144,6 +157,10 @@ typedef struct {
     double capture_radius;
     int success;                             /* episode_success                                 */
     int has_pos;                             /* dynamics.pos exists (hasattr check, :38)        */
+    /* obstacles */
+    int n_obst;
+    double obst[64][2];                      /* MultiObstacles.pos_arr xy, in generation order   */
+    int obst_mode;                           /* 0 o_random, 1 o_static_same_goal                 */
 } or_env;
 
 /* ---- low level pieces (exported for per-function golden tests) ---- */
@@ -179,6 +196,14 @@ void or_step_all(const or_params* p, or_drone* drones, or_env* envs, const doubl
                  double* term_obs, int nthreads);
 
 void or_neighbor_obs(const or_params* p, const or_env* ev, double* obs, int obs_dim);
+
+/* obstacles: get_surround_sdfs (obstacles/utils.py:4-27), collision_detection (:30-43),
+ * perform_collision_with_obstacle (collisions/obstacles.py:23-50), max_square_area_center (o_base.py:125-153) */
+void or_obst_sdf(const or_params* p, const or_env* ev, const double xy[2], double out[9]);
+int or_obst_detect(const or_params* p, const or_env* ev, const double xy[2]);
+void or_collide_obstacle(const or_params* p, or_drone* d, const double opos[3], or_rng* r, uint32_t gid);
+void or_max_square_center(const unsigned char* map, int n, double out_xy[2]);
+void or_cell_xy(int row, int col, int n, double out_xy[2]);
 
 /* ---- flavor A (quadrotor_multi_rewards.QuadrotorEnvMulti) ---- */
 void or_params_default_a(or_params* p);     /* Controller/ModelParams constants, camera, rewards */
