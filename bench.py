@@ -28,11 +28,14 @@ sys.path.insert(0, os.path.join(ROOT, "quad-swarm-rl-stable-baselines3_amd"))
 CONFIGS = {
     "c2": dict(num_envs=16384, num_agents=1, neighbor_visible_num=0, neighbor_obs_type="none"),
     "c3": dict(num_envs=4096, num_agents=8, neighbor_visible_num=6, neighbor_obs_type="pos_vel"),
+    "c4": dict(preset="c4", num_envs=4096, num_agents=8),
     "c5": dict(num_envs=1024, num_agents=32, neighbor_visible_num=6, neighbor_obs_type="pos_vel"),
     "a8": dict(flavor="A", num_envs=4096, num_agents=8, initial_capture_radius=0.5),
     "a4": dict(flavor="A", num_envs=8192, num_agents=4, initial_capture_radius=0.5),
 }
 WORKLOAD = {"c2": "single_quad x 16384 envs", "c3": "8-drone swarm static_same_goal x 4096 envs (pos_vel k=6)",
+            "c4": "8-drone swarm + obstacles x 4096 envs (12 pillars, SDF obs, pos_vel k=2, floor obs, downwash, "
+                  "mix of o_random / o_static_same_goal)",
             "c5": "32-drone swarm x 1024 envs per GPU (pos_vel k=6)",
             "a8": "flavor A (sb_train env: PID pre-controller x 8 ticks, dynamic_repulsive target, ndist_nsangle "
                   "camera neighbours k=7) 8 drones x 4096 envs, capture radius 0.5",
@@ -42,6 +45,8 @@ WORKLOAD = {"c2": "single_quad x 16384 envs", "c3": "8-drone swarm static_same_g
 def make_cfg(kw, **extra):
     from quadswarm_amd import QuadSwarmConfig
     kw = dict(kw)
+    if kw.pop("preset", None) == "c4":
+        return QuadSwarmConfig.c4(**kw, **extra)
     if kw.pop("flavor", "B") == "A":
         return QuadSwarmConfig.sb_train(**kw, **extra)
     return QuadSwarmConfig(**kw, **extra)
@@ -50,16 +55,16 @@ def make_cfg(kw, **extra):
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 
 
-def algorithmic_bytes_per_agent_step(obs_dim, n_agents, flavor="B"):
+def algorithmic_bytes_per_agent_step(obs_dim, n_agents, flavor="B", n_obst=0):
     """B = 4 (S_r + S_w + A + O + 1) + 1 with S_r = 33 persistent fp32 state
     (pos3 vel3 rot9 omega3 cmd_damp4 rot_damp4 OU4 goal3), S_w = 30, A = 4, O = obs_dim, +1 reward,
     +1 byte done.  C3: 489 B, C2: 345 B.
     Flavor A: S_r = S_w = 55 (+ PID 20, heading, heading rate; the goal moves with the target), A = 2,
     plus per env (tick/flags/episode r+w 24 B, target r+w 16 B, capture radius 4 B, reset_info 1 B) / N.
-    A8 (obs 28): 570.6 B."""
+    A8 (obs 28): 570.6 B.  Obstacles add the env's pillar list once per env: 8 M / N (C4: 445 B)."""
     if flavor == "A":
         return 4 * (55 + 55 + 2 + obs_dim + 1) + 1 + 45.0 / n_agents
-    return 4 * (33 + 30 + 4 + obs_dim + 1) + 1
+    return 4 * (33 + 30 + 4 + obs_dim + 1) + 1 + 8.0 * n_obst / n_agents
 
 
 def cpu_baseline(cfg_kw, seconds=10.0):
@@ -210,7 +215,8 @@ def main():
 
     if rank == 0:
         value = world * I * args.steps / el
-        bpa = algorithmic_bytes_per_agent_step(cfg.obs_dim, cfg.num_agents, cfg.flavor)
+        bpa = algorithmic_bytes_per_agent_step(cfg.obs_dim, cfg.num_agents, cfg.flavor,
+                                               cfg.num_obstacles if cfg.use_obstacles else 0)
         achieved = bpa * I / (k_ms * 1e-3) / 1e9
         traffic = pmc_traffic(args.config)
         out = {
@@ -227,8 +233,9 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic: U(-1,1) actions (seed 1234) from a fixed device buffer; Crazyflie constants; "
-                    + ("static_same_goal spawns (Philox seed 0)" if cfg.flavor == "B" else
-                       "dynamic_repulsive target and spawns (Philox seed 0)"),
+                    + ("dynamic_repulsive target and spawns (Philox seed 0)" if cfg.flavor == "A" else
+                       "random 12-pillar maps + o_random/o_static_same_goal spawns (Philox seed 0)" if cfg.use_obstacles
+                       else "static_same_goal spawns (Philox seed 0)"),
             "config": {"workload": WORKLOAD[args.config], "envs_per_gpu": cfg.num_envs,
                        "agents_per_env": cfg.num_agents, "visible_neighbors": cfg.k_neighbors,
                        "obs_dim": cfg.obs_dim, "global_batch": world * I, "parallelism": f"env-shard x{world}",

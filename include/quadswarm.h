@@ -75,6 +75,10 @@ enum qs_neighbor_obs {              /* quad_utils.py:40-58 (QUADS_NEIGHBOR_OBS_T
 enum qs_scenario {
     QS_SCEN_STATIC_SAME_GOAL = 0,      /* scenarios/static_same_goal.py (flavor A: spawn at the goal)  */
     QS_SCEN_DYNAMIC_REPULSIVE = 1,     /* scenarios/dynamic_repulsive.py, flavor A only (float-fixed)  */
+    /* flavor B with obstacles (use_obstacles = 1): scenarios/mix.py over QUADS_MODE_LIST_OBSTACLES */
+    QS_SCEN_OBST_MIX = 2,              /* o_random or o_static_same_goal, drawn per reset (mix.py:78-99) */
+    QS_SCEN_O_RANDOM = 3,              /* scenarios/obstacles/o_random.py                              */
+    QS_SCEN_O_STATIC_SAME_GOAL = 4,    /* scenarios/obstacles/o_static_same_goal.py                    */
 };
 
 /* Environment + physical configuration.  Physical constants are derived on the host exactly like
@@ -121,6 +125,13 @@ typedef struct qs_config {
     int32_t n_cameras;              /* camera model (global_cfg.py:14-18) */
     float capture_radius;           /* initial_capture_radius (global_cfg.py:37); per env at run time */
     float cam_size, cam_focal, cam_px_noise, cam_fov_deg, cam_res;
+    /* ---- obstacles (flavor B; quadrotor_multi.py:128-140, quad_obstacle_baseline.py) ---- */
+    int32_t use_obstacles;
+    int32_t num_obstacles;          /* int(obst_density * area^2), the pillars per env (C4: 12) */
+    int32_t obst_area;              /* spawn area side in 1 m cells (8); area^2 <= 64 */
+    float obst_size;                /* pillar diameter (0.6) */
+    float sdf_resolution;           /* 0.1 (obstacles/obstacles.py:12) */
+    float rew_quadcol_bin_obst;     /* quadcol_bin_obst reward coefficient */
 } qs_config;
 
 /* Device buffers of a handle.  State is structure-of-arrays: field f of drone g lives at
@@ -138,7 +149,8 @@ enum qs_state_field {
 enum qs_istate_field { QS_I_SVD = 0, QS_I_FLAGS = 1, QS_I_PREV_LO = 2, QS_I_PREV_HI = 3, QS_NI = 4 };
 enum qs_drone_flags {
     QS_FL_ON_FLOOR = 1, QS_FL_PREV_WALL = 2, QS_FL_PREV_CEIL = 4,
-    QS_FL_CRASH_FLOOR = 8, QS_FL_CRASH_WALL = 16, QS_FL_CRASH_CEIL = 32
+    QS_FL_CRASH_FLOOR = 8, QS_FL_CRASH_WALL = 16, QS_FL_CRASH_CEIL = 32,
+    QS_FL_PREV_OBST = 64            /* in prev_obst_quad_collisions (quadrotor_multi.py:585) */
 };
 /* per env: tick, flags, episode.  {tick, episode} is the env's Philox counter: every step and reset
  * of an env draws a fresh stream.  Flavor A counts QuadrotorSingle ticks (8 per step). */
@@ -154,7 +166,7 @@ enum qs_env_ffield { QS_ENVF_TARGET_X = 0, QS_ENVF_TARGET_Y = 1, QS_ENVF_CAPTURE
 
 typedef struct qs_layout {          /* byte offsets inside one workspace allocation */
     size_t params;                  /* kernel parameter block (device copy of the config + runtime params) */
-    size_t state, istate, env, env_f, stale_vel, obs, term_obs, rew, done, reset_info, total_bytes;
+    size_t state, istate, env, env_f, obst, stale_vel, obs, term_obs, rew, done, reset_info, total_bytes;
     int32_t obs_dim, num_drones;
 } qs_layout;
 
@@ -163,6 +175,7 @@ typedef struct qs_buffers {         /* device pointers (valid for the handle's l
     int32_t* istate;                /* [QS_NI, I] */
     int32_t* env;                   /* [QS_NE, E] */
     float* env_f;                   /* [QS_NENVF, E] */
+    float* obst;                    /* [E, num_obstacles, 2] pillar xy (MultiObstacles.pos_arr order) */
     float* stale_vel;               /* [3, I]  QuadrotorEnvMulti.vel as last seen by a reset */
     float* obs;                     /* [I, obs_dim] */
     float* term_obs;                /* [I, obs_dim] rows of envs that finished this step */
@@ -201,7 +214,7 @@ int qs_reset(qs_handle* h, const uint8_t* d_env_mask, void* stream);
 int qs_step(qs_handle* h, const float* d_actions, void* stream);
 
 /* Runtime-tunable scalars: "rew_pos", "rew_effort", "rew_crash", "rew_orient", "rew_spin",
- * "quadcol_bin", "quadcol_bin_smooth_max", "ep_len", "seed", "capture_radius" (flavor A, all envs;
+ * "quadcol_bin", "quadcol_bin_smooth_max", "quadcol_bin_obst", "ep_len", "seed", "capture_radius" (flavor A, all envs;
  * write buffers.env_f[QS_ENVF_CAPTURE * E + e] for one env). */
 int qs_set_param(qs_handle* h, const char* key, double value);
 int qs_get_param(qs_handle* h, const char* key, double* value);

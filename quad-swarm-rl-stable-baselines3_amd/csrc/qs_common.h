@@ -40,6 +40,9 @@ struct KP {
     float w_captor, w_helper, existence;
     float tgt_vmax, tgt_dt, arena, tgt_z;
     float nclip_lo[8], nclip_hi[8];
+    // ---- obstacles (flavor B) ----
+    int obst, M, obst_n, obst_scen;                 // on, obstacles per env, grid side, scenario
+    float obst_r, obst_thr, obst_z, sdf_res, quadcol_obst;
 };
 
 struct Bufs {
@@ -47,6 +50,7 @@ struct Bufs {
     int32_t* ist;
     int32_t* env;
     float* envf;
+    float2* obst;     // [E, M] obstacle xy
     float* stale;
     float* obs;
     float* term;

@@ -267,15 +267,17 @@ __device__ void collide_room(const KP& kp, Drone& d, const Rng& rng, uint32_t gi
 }
 
 // ---------------------------------------------------------------------------------------------
-// reset (QuadrotorSingle._reset quadrotor_single.py:401-469 with static_same_goal goals)
+// reset (QuadrotorSingle._reset quadrotor_single.py:401-469): spawn = spawn point + U(-box, box)^3
+// (static_same_goal: the goal, box 2; obstacle scenarios: a free grid cell, box 0.1)
 // ---------------------------------------------------------------------------------------------
-__device__ void reset_drone(const KP& kp, Drone& d, const Rng& rng, uint32_t gid) {
+__device__ __forceinline__ void reset_drone(const KP& kp, Drone& d, const Rng& rng, uint32_t gid, const float* spawn,
+                            const float* goal) {
     float u[4];
     uniforms4(rng, gid, S_RESET, 0, u);
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-        d.goal[i] = kp.goal[i];
-        d.pos[i] = (-kp.spawn_box + 2.f * kp.spawn_box * u[i]) + d.goal[i];
+        d.goal[i] = goal[i];
+        d.pos[i] = (-kp.spawn_box + 2.f * kp.spawn_box * u[i]) + spawn[i];
         d.vel[i] = 0.f;
         d.om[i] = 0.f;
     }
@@ -296,7 +298,7 @@ __device__ void reset_drone(const KP& kp, Drone& d, const Rng& rng, uint32_t gid
             if (found) continue;
             const float cand = -3.14159265358979f + 6.28318530717959f * y[i];
             float s, c;
-            sincosf(cand, &s, &c);
+            sincos_hw(cand, &s, &c);
             yaw = cand;
             if (c * tx + s * ty >= 0.5f || degenerate) found = true;
         }
@@ -309,7 +311,172 @@ __device__ void reset_drone(const KP& kp, Drone& d, const Rng& rng, uint32_t gid
     d.prev = 0;
 }
 
-template <int NPAD>
+// ---------------------------------------------------------------------------------------------
+// obstacles: pillars on an n x n grid of 1 m cells, xy only
+// ---------------------------------------------------------------------------------------------
+// grid cell (row, col) -> cell_centers[row + n*col] (obstacles/utils.py:46-58, quadrotor_multi.py:422)
+__device__ __forceinline__ float2 cell_xy(int cell, int n) {
+    const int row = cell / n, col = cell % n;
+    const float h = (float)(n / 2);
+    return make_float2((float)col + 0.5f - h, (float)(n - 1 - row) + 0.5f - h);
+}
+
+__device__ __forceinline__ uint32_t ubits(const Rng& r, uint32_t id, uint32_t st, uint32_t idx) {
+    return word_of(block(r, id, st | UNIF_BIT, idx >> 2), idx & 3);
+}
+// floor(u * m) exactly for u = ((w >> 8) + 0.5) / 2^24 (the oracle evaluates it in double, exactly)
+__device__ __forceinline__ int ufloor(uint32_t w, int m) {
+    return (int)((((uint64_t)(w >> 8) * 2u + 1u) * (uint64_t)m) >> 25);
+}
+
+// partial Fisher-Yates (the first k of a random permutation of 0..n-1): the Philox stand-in for
+// np.random.choice(n, k, replace=False); a: LDS scratch of n bytes, out: k picks
+__device__ __forceinline__ void choose_k(const Rng& r, uint32_t id, uint32_t st, uint32_t u0, int n, int k, uint8_t* a, uint8_t* out) {
+    for (int i = 0; i < n; ++i) a[i] = (uint8_t)i;
+    for (int i = 0; i < k; ++i) {
+        int j = i + ufloor(ubits(r, id, st, u0 + (uint32_t)i), n - i);
+        j = min(j, n - 1);
+        const uint8_t t = a[i];
+        a[i] = a[j];
+        a[j] = t;
+        out[i] = a[i];
+    }
+}
+
+// per-env reset scratch in LDS (QS_OBST_SCRATCH bytes per env)
+constexpr int QS_OBST_SCRATCH = 400;
+struct ObstScratch {
+    uint8_t perm[64], map[64], fr[64], dp[64], sp[32], gl[32], ids[64];
+    float ez;
+    int mode;
+};
+static_assert(sizeof(ObstScratch) <= QS_OBST_SCRATCH, "obstacle scratch");
+
+// Obstacle map + scenario of one env (quadrotor_multi.py:405-426, 449-452; scenarios/mix.py:78-99;
+// o_random.py:26-51; o_static_same_goal.py:28-48; o_base.py:58-153).  One lane per env runs it;
+// the other lanes of the env read sp/gl/mode/ez after a barrier.  Writes the env's obstacle list.
+__device__ __forceinline__ void obstacle_reset_env(const KP& kp, const Rng& r, uint32_t genv, ObstScratch* sc, float2* ob) {
+    const int n = kp.obst_n, nn = n * n, M = kp.M, N = kp.N;
+    for (int c = 0; c < nn; ++c) sc->map[c] = 0;
+    choose_k(r, genv, S_OBSTMAP, 0, nn, M, sc->perm, sc->ids);
+    for (int o = 0; o < M; ++o) {
+        sc->map[sc->ids[o]] = 1;
+        ob[o] = cell_xy(sc->ids[o], n);
+    }
+    int mode = kp.obst_scen == 0 ? (int)(ubits(r, genv, S_OSCEN, 0) >> 31) : kp.obst_scen - 1;
+    int F = 0;
+    for (int c = 0; c < nn; ++c)
+        if (!sc->map[c]) sc->fr[F++] = (uint8_t)c;
+    choose_k(r, genv, S_OSCEN, 1, F, N, sc->perm, sc->sp);
+    for (int i = 0; i < N; ++i) sc->sp[i] = sc->fr[sc->sp[i]];
+    if (mode == 0) {   // o_random: own goal cell per drone
+        choose_k(r, genv, S_OSCEN, 1 + (uint32_t)N, F, N, sc->perm, sc->gl);
+        for (int i = 0; i < N; ++i) sc->gl[i] = sc->fr[sc->gl[i]];
+    } else {           // o_static_same_goal: Scenario_o_base.max_square_area_center (o_base.py:125-153)
+        for (int c = 0; c < nn; ++c) sc->dp[c] = 0;
+        for (int j = 0; j < n; ++j) sc->dp[j] = sc->map[j];
+        for (int i = 0; i < n; ++i) sc->dp[i * n] = sc->map[i * n];
+        int ms = 0, cx = 0, cy = 0;
+        for (int i = 1; i < n; ++i)
+            for (int j = 1; j < n; ++j)
+                if (sc->map[i * n + j] == 0) {
+                    const int v = min(min(sc->dp[(i - 1) * n + j], sc->dp[i * n + j - 1]), sc->dp[(i - 1) * n + j - 1]) + 1;
+                    sc->dp[i * n + j] = (uint8_t)v;
+                    if (v > ms) { ms = v; cx = i - (ms - 1) / 2; cy = j - (ms - 1) / 2; }
+                }
+        for (int i = 0; i < N; ++i) sc->gl[i] = (uint8_t)(cx * n + cy);
+        sc->ez = 1.5f + 1.5f * uniform1(r, genv, S_OSCEN, 2 * (uint32_t)N + 1);
+    }
+    sc->mode = mode;
+}
+
+// spawn point and goal of drone `di` after obstacle_reset_env (o_base.py:81-92: z ~ U(1, 3))
+__device__ __forceinline__ void obstacle_spawn_goal(const KP& kp, const ObstScratch* sc, int di, const Rng& r,
+                                                    uint32_t gid, float* spawn, float* goal) {
+    float u[4];
+    uniforms4(r, gid, S_RESET, 0, u);   // u[3] = start z, block 1 word 0 = goal z
+    const float2 s = cell_xy(sc->sp[di], kp.obst_n), g = cell_xy(sc->gl[di], kp.obst_n);
+    spawn[0] = s.x; spawn[1] = s.y; spawn[2] = 1.f + 2.f * u[3];
+    goal[0] = g.x; goal[1] = g.y;
+    goal[2] = sc->mode == 0 ? 1.f + 2.f * uniform1(r, gid, S_RESET, 4) : sc->ez;
+}
+
+// get_surround_sdfs (obstacles/utils.py:4-27)
+__device__ __forceinline__ void sdf_obs(const KP& kp, const float2* ob, float x, float y, float* out) {
+    const float res = kp.sdf_res;
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+            const float gx = x + (float)(a - 1) * res, gy = y + (float)(b - 1) * res;
+            float m2 = 1.0e4f;   // (100 m)^2
+            for (int o = 0; o < kp.M; ++o) {
+                const float dx = gx - ob[o].x, dy = gy - ob[o].y;
+                m2 = fminf(m2, dx * dx + dy * dy);
+            }
+            out[a * 3 + b] = fsqrt(m2) - kp.obst_r;
+        }
+}
+
+// collision_detection (obstacles/utils.py:30-43): first obstacle within arm + radius
+__device__ __forceinline__ int obst_detect(const KP& kp, const float2* ob, float x, float y) {
+    for (int o = 0; o < kp.M; ++o) {
+        const float dx = x - ob[o].x, dy = y - ob[o].y;
+        if (fsqrt(dx * dx + dy * dy) <= kp.obst_thr) return o;
+    }
+    return -1;
+}
+
+// perform_collision_with_obstacle (collisions/obstacles.py:23-50); Philox indices as the oracle's
+__device__ __forceinline__ void collide_obstacle(const KP& kp, Drone& d, float ox, float oy, const Rng& rng, uint32_t gid) {
+    float n[3] = {d.pos[0] - ox, d.pos[1] - oy, 0.f};
+    const float nm = fsqrt(n[0] * n[0] + n[1] * n[1]);
+    const float inm = frcp(nm == 0.f ? 1e-5f : nm);
+    n[0] *= inm; n[1] *= inm;
+    const float vm = fsqrt(d.vel[0] * d.vel[0] + d.vel[1] * d.vel[1] + d.vel[2] * d.vel[2]);
+    const float nv[3] = {vm * n[0], vm * n[1], 0.f};
+    float noise[3] = {0.f, 0.f, 0.f};
+    for (int t = 0; t < 3; ++t) {
+        float z[12];
+        const uint32_t b0 = (uint32_t)(t * 6) >> 2, off = (uint32_t)(t * 6) & 3;
+        normals4(rng, gid, S_OBST, b0, z);
+        normals4(rng, gid, S_OBST, b0 + 1, z + 4);
+        float tmp[3], dt_ = 0.f;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            tmp[c] = 0.1f * z[off + c] + 0.05f * z[off + 3 + c];
+            dt_ += (nv[c] + tmp[c]) * n[c];
+        }
+        if (dt_ > 0.f) {
+            noise[0] = tmp[0]; noise[1] = tmp[1]; noise[2] = tmp[2];
+            break;
+        }
+    }
+    const float dz = d.pos[2] - kp.obst_z;
+    const bool inside = fsqrt(nm * nm + dz * dz) < kp.obst_r;
+    float u[8];
+    uniforms4(rng, gid, S_OBST, 0, u);
+    uniforms4(rng, gid, S_OBST, 1, u + 4);
+    float sh[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) sh[c] = nv[c] - d.vel[c] + noise[c];
+    new_vel(vm, d.vel, sh, inside ? 1.f : 0.2f + 0.6f * u[0]);
+    const float om = 3.14159265358979f;   // compute_new_omega(magn_scale=1.0)
+    float w[3] = {-1.f + 2.f * u[1], -1.f + 2.f * u[2], -1.f + 2.f * u[3]};
+    const float wm = fsqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+    const float iw = frcp(wm == 0.f ? 1e-5f : wm);
+    const float mg = om * 0.5f + (om - om * 0.5f) * u[4];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) d.om[c] += w[c] * iw * mg;
+}
+
+// LDS: obs tile [64, obs_dim] | exchange tile [64 x 2 float4] | 64 words | obstacle tiles [EPB, M]
+// float2 | obstacle reset scratch [EPB] (shm_bytes() in qs_step.hip sizes it)
+__device__ __forceinline__ float2* obst_tile(float* lds, const KP& kp) {
+    return reinterpret_cast<float2*>(lds + 64 * kp.obs_dim + 64 * 8 + 64);
+}
+
+template <int NPAD, bool OBST>
 __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bufs b, uint32_t seed) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const KP& kp = *kpp;
@@ -328,6 +495,11 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     const int rows = nenv_blk * kp.N;
     float* row = lds + (size_t)(el * kp.N + di) * kp.obs_dim;
     float4* xch = reinterpret_cast<float4*>(lds + 64 * kp.obs_dim);
+    float2* otile = obst_tile(lds, kp);
+    ObstScratch* oscr = reinterpret_cast<ObstScratch*>(otile + EPB * kp.M);
+    const float2* myob = otile + el * kp.M;
+    if (OBST)   // the block's obstacle lists -> LDS (ordered by the first lds_sync below)
+        for (int q = lane; q < nenv_blk * kp.M; q += 64) otile[q] = b.obst[(size_t)env0 * kp.M + q];
 
     Drone d;
     load_drone(kp, b, g, d);
@@ -396,6 +568,15 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     const bool ceil_new = (d.flags & QS_FL_CRASH_CEIL) && !(d.flags & QS_FL_PREV_CEIL);
     d.flags = (d.flags & ~(uint32_t)(QS_FL_PREV_WALL | QS_FL_PREV_CEIL)) | (wall_new ? QS_FL_PREV_WALL : 0u) |
               (ceil_new ? QS_FL_PREV_CEIL : 0u);
+    // obstacles (quadrotor_multi.py:570-589): first pillar hit, new vs the previous step's set
+    int ohit = -1;
+    bool onew = false;
+    if (OBST) {
+        ohit = obst_detect(kp, myob, d.pos[0], d.pos[1]);
+        onew = active && ohit >= 0 && !(d.flags & QS_FL_PREV_OBST);
+        rw += kp.quadcol_obst * (onew ? -1.f : 0.f);
+        d.flags = (d.flags & ~(uint32_t)QS_FL_PREV_OBST) | (ohit >= 0 ? (uint32_t)QS_FL_PREV_OBST : 0u);
+    }
 
     QS_STAMP(3);
     // ---- random forces (:659-698) ----
@@ -463,6 +644,10 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
             }
             if (eb != 0 && di == istar) pend &= ~(1ull << jstar);
         }
+        if (OBST && onew) {   // perform_collision_with_obstacle, drones in ascending order (:680-689)
+            collide_obstacle(kp, d, myob[ohit].x, myob[ohit].y, rng, gid);
+            vchanged = true;
+        }
         if (active && wall_new) collide_room(kp, d, rng, gid, true);
         if (active && ceil_new) collide_room(kp, d, rng, gid, false);
         vchanged |= active && (wall_new || ceil_new);
@@ -481,6 +666,7 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     if (active) self_obs(kp, d, rng, gid, S_SENSOR, row);
     QS_STAMP(6);
     if (nbr) neighbor_obs<NPAD>(kp, xch, base, di, d.pos, d.vel, active, row);
+    if (OBST && active) sdf_obs(kp, myob, d.pos[0], d.pos[1], row + kp.obs_dim - 9);   // MultiObstacles.step
     QS_STAMP(7);
 
     const uint64_t dball = __ballot(active && done);
@@ -494,17 +680,29 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
         }
         lds_sync();
         float sv[3] = {d.vel[0], d.vel[1], d.vel[2]};  // QuadrotorEnvMulti.vel seen by the reset (:477)
+        if (OBST) {   // new obstacle map + scenario per finished env (one lane each)
+            if (active && done && di == 0)
+                obstacle_reset_env(kp, rng, kp.id0 + (uint32_t)(env * kp.N), oscr + el, otile + el * kp.M);
+            lds_sync();
+        }
         if (active && done) {
             b.stale[0 * kp.I + g] = sv[0];
             b.stale[1 * kp.I + g] = sv[1];
             b.stale[2 * kp.I + g] = sv[2];
-            reset_drone(kp, d, rng, gid);
+            float spawn[3] = {kp.goal[0], kp.goal[1], kp.goal[2]}, goal[3] = {kp.goal[0], kp.goal[1], kp.goal[2]};
+            if (OBST) obstacle_spawn_goal(kp, oscr + el, di, rng, gid, spawn, goal);
+            reset_drone(kp, d, rng, gid, spawn, goal);
             self_obs(kp, d, rng, gid, S_RESET_SENSOR, row);
         }
         if (nbr) {
             xch_put(xch, lane, d.pos, sv);
             lds_sync();
             neighbor_obs<NPAD>(kp, xch, base, di, d.pos, sv, active && done, row);
+        }
+        if (OBST && active && done) {
+            sdf_obs(kp, myob, d.pos[0], d.pos[1], row + kp.obs_dim - 9);   // MultiObstacles.reset
+            if (di == 0)
+                for (int o = 0; o < kp.M; ++o) b.obst[(size_t)env * kp.M + o] = myob[o];
         }
     }
     lds_sync();
@@ -530,7 +728,7 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
 }
 
 // explicit reset of masked envs (QuadrotorEnvMulti.reset quadrotor_multi.py:440-517)
-template <int NPAD>
+template <int NPAD, bool OBST>
 __global__ __launch_bounds__(64) void reset_kernel(const KP* __restrict__ kpp, Bufs b, uint32_t seed) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const KP& kp = *kpp;
@@ -554,8 +752,16 @@ __global__ __launch_bounds__(64) void reset_kernel(const KP* __restrict__ kpp, B
     float sv[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) sv[c] = stale_valid ? b.stale[c * kp.I + g] : d.vel[c];
+    float2* otile = obst_tile(lds, kp);
+    ObstScratch* oscr = reinterpret_cast<ObstScratch*>(otile + EPB * kp.M);
+    if (OBST) {
+        if (sel && di == 0) obstacle_reset_env(kp, rng, kp.id0 + (uint32_t)(env * kp.N), oscr + el, otile + el * kp.M);
+        lds_sync();
+    }
     if (sel) {
-        reset_drone(kp, d, rng, kp.id0 + (uint32_t)g);
+        float spawn[3] = {kp.goal[0], kp.goal[1], kp.goal[2]}, goal[3] = {kp.goal[0], kp.goal[1], kp.goal[2]};
+        if (OBST) obstacle_spawn_goal(kp, oscr + el, di, rng, kp.id0 + (uint32_t)g, spawn, goal);
+        reset_drone(kp, d, rng, kp.id0 + (uint32_t)g, spawn, goal);
         self_obs(kp, d, rng, kp.id0 + (uint32_t)g, S_RESET_SENSOR, row);
     }
     if (kp.neighbor == QS_NEIGHBOR_POS_VEL && kp.K > 0) {
@@ -563,6 +769,12 @@ __global__ __launch_bounds__(64) void reset_kernel(const KP* __restrict__ kpp, B
         xch_put(xch, lane, d.pos, sv);
         lds_sync();
         neighbor_obs<NPAD>(kp, xch, base, di, d.pos, sv, sel, row);
+    }
+    if (OBST && sel) {
+        const float2* myob = otile + el * kp.M;
+        sdf_obs(kp, myob, d.pos[0], d.pos[1], row + kp.obs_dim - 9);   // MultiObstacles.reset
+        if (di == 0)
+            for (int o = 0; o < kp.M; ++o) b.obst[(size_t)env * kp.M + o] = myob[o];
     }
     lds_sync();
     const int nenv_blk = min(EPB, kp.E - env0);

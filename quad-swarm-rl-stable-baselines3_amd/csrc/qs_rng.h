@@ -20,6 +20,8 @@ enum : uint32_t {
     // flavor A: camera pixel noise (normals 0 = u1, 1 = u2; | neighbour j << 8), spawn / heading draws
     S_CAM = 13, S_CAM_SEL = 14, S_SELF_CAM = 15, S_RESET_A = 16, S_SCEN = 17, S_RESET_CAM = 18,
     S_RESET_CAM_SEL = 19, S_RESET_SELF_CAM = 20,
+    // obstacles: per-env map (partial Fisher-Yates uniforms) and scenario draws (mode, cells, goal z)
+    S_OBSTMAP = 21, S_OSCEN = 22,
     UNIF_BIT = 0x80
 };
 
@@ -70,10 +72,18 @@ __device__ __forceinline__ void normals4(const Rng& r, uint32_t id, uint32_t str
     box_muller(q.w[2], q.w[3], z[2], z[3]);
 }
 
+// word k of a block without a dynamically indexed private array (which would live in scratch)
+__device__ __forceinline__ uint32_t word_of(const W4& q, uint32_t k) {
+    return k == 0 ? q.w[0] : (k == 1 ? q.w[1] : (k == 2 ? q.w[2] : q.w[3]));
+}
+__device__ __forceinline__ float pick4(const float* z, uint32_t k) {
+    return k == 0 ? z[0] : (k == 1 ? z[1] : (k == 2 ? z[2] : z[3]));
+}
+
 __device__ __forceinline__ float normal1(const Rng& r, uint32_t id, uint32_t stream, uint32_t idx) {
     float z[4];
     normals4(r, id, stream, idx >> 2, z);
-    return z[idx & 3];
+    return pick4(z, idx & 3);
 }
 
 // 4 uniforms of block blk of stream | UNIF_BIT
@@ -85,7 +95,7 @@ __device__ __forceinline__ void uniforms4(const Rng& r, uint32_t id, uint32_t st
 
 __device__ __forceinline__ float uniform1(const Rng& r, uint32_t id, uint32_t stream, uint32_t idx) {
     const W4 q = block(r, id, stream | UNIF_BIT, idx >> 2);
-    return u01(q.w[idx & 3]);
+    return u01(word_of(q, idx & 3));
 }
 
 }  // namespace qs

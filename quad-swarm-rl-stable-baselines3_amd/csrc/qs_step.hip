@@ -113,8 +113,18 @@ static int validate(const qs_config* c) {
         if (c->obs_repr < 0 || c->obs_repr > 2) return fail(QS_E_INVALID, "obs_repr is not a flavor-B repr");
         if (c->neighbor_obs != QS_NEIGHBOR_NONE && c->neighbor_obs != QS_NEIGHBOR_POS_VEL)
             return fail(QS_E_UNSUPPORTED, "flavor B implements neighbor_obs none / pos_vel");
-        if (c->scenario != QS_SCEN_STATIC_SAME_GOAL) return fail(QS_E_UNSUPPORTED, "flavor B implements static_same_goal");
+        if (c->use_obstacles) {
+            if (c->scenario < QS_SCEN_OBST_MIX || c->scenario > QS_SCEN_O_STATIC_SAME_GOAL)
+                return fail(QS_E_UNSUPPORTED, "obstacles need scenario obst_mix / o_random / o_static_same_goal");
+            if (c->obst_area < 1 || c->obst_area > 8) return fail(QS_E_UNSUPPORTED, "obst_area must be in [1, 8]");
+            if (c->num_obstacles < 1 || c->num_obstacles + c->num_agents > c->obst_area * c->obst_area)
+                return fail(QS_E_INVALID, "num_obstacles must leave a free cell per drone");
+            if (c->obst_size <= 0.f || c->sdf_resolution <= 0.f) return fail(QS_E_INVALID, "bad obst_size / sdf_resolution");
+        } else if (c->scenario != QS_SCEN_STATIC_SAME_GOAL) {
+            return fail(QS_E_UNSUPPORTED, "flavor B without obstacles implements static_same_goal");
+        }
     } else {
+        if (c->use_obstacles) return fail(QS_E_UNSUPPORTED, "flavor A with obstacles is not implemented");
         if (c->obs_repr < 3 || c->obs_repr > 6) return fail(QS_E_INVALID, "obs_repr is not a flavor-A repr");
         if (c->scenario != QS_SCEN_STATIC_SAME_GOAL && c->scenario != QS_SCEN_DYNAMIC_REPULSIVE)
             return fail(QS_E_INVALID, "unknown scenario");
@@ -129,12 +139,17 @@ static int validate(const qs_config* c) {
     return QS_OK;
 }
 
+static int npad_of(int n);
+static size_t shm_bytes(const qs_config& c, int obs_dim, int npad);
+static int neighbor_dim(int t);
+
 static qs_layout make_layout(const qs_config* c) {
     qs_layout L;
     memset(&L, 0, sizeof L);
     const size_t I = (size_t)c->num_envs * c->num_agents, E = (size_t)c->num_envs;
     const int od = self_obs_dim(c->obs_repr) +
-                   (c->neighbor_obs != QS_NEIGHBOR_NONE ? neighbor_dim(c->neighbor_obs) * c->k_neighbors : 0);
+                   (c->neighbor_obs != QS_NEIGHBOR_NONE ? neighbor_dim(c->neighbor_obs) * c->k_neighbors : 0) +
+                   (c->use_obstacles ? 9 : 0);
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     size_t o = 0;
     L.params = o; o = al(o + sizeof(qs::KP));
@@ -142,6 +157,7 @@ static qs_layout make_layout(const qs_config* c) {
     L.istate = o; o = al(o + sizeof(int32_t) * QS_NI * I);
     L.env = o; o = al(o + sizeof(int32_t) * QS_NE * E);
     L.env_f = o; o = al(o + sizeof(float) * QS_NENVF * E);
+    L.obst = o; o = al(o + sizeof(float) * 2 * (c->use_obstacles ? (size_t)c->num_obstacles : 0) * E);
     L.stale_vel = o; o = al(o + sizeof(float) * 3 * I);
     L.obs = o; o = al(o + sizeof(float) * I * od);
     L.term_obs = o; o = al(o + sizeof(float) * I * od);
@@ -280,6 +296,15 @@ static qs::KP make_kp(const qs_config* c, const qs_layout& L) {
     k.spawn_box = c->spawn_box;
     k.flavor = c->flavor;
     if (c->flavor == QS_FLAVOR_A) make_kp_a(c, k);
+    if (c->use_obstacles) {
+        k.obst = 1; k.M = c->num_obstacles; k.obst_n = c->obst_area;
+        k.obst_scen = c->scenario == QS_SCEN_OBST_MIX ? 0 : (c->scenario == QS_SCEN_O_RANDOM ? 1 : 2);
+        k.obst_r = 0.5f * c->obst_size;
+        k.obst_thr = (float)((double)c->arm + 0.5 * (double)c->obst_size);   // quad arm + pillar radius
+        k.obst_z = 0.5f * c->room_hi[2];                                       // pillar centre (:423)
+        k.sdf_res = c->sdf_resolution;
+        k.quadcol_obst = c->rew_quadcol_bin_obst;
+    }
     return k;
 }
 
@@ -331,6 +356,13 @@ extern "C" int qs_config_default(qs_config* c, int32_t num_envs, int32_t num_age
     c->n_cameras = 3;
     c->capture_radius = 3.f;
     c->cam_size = 0.2f; c->cam_focal = 0.035f; c->cam_px_noise = 3.f; c->cam_fov_deg = 70.f; c->cam_res = 640.f;
+    // obstacle fields (used once use_obstacles = 1): the C4 run (swarm_rl/runs/obstacles/quad_obstacle_baseline.py)
+    c->use_obstacles = 0;
+    c->num_obstacles = 12;
+    c->obst_area = 8;
+    c->obst_size = 0.6f;
+    c->sdf_resolution = 0.1f;
+    c->rew_quadcol_bin_obst = 5.f;
     return QS_OK;
 }
 
@@ -353,12 +385,29 @@ extern "C" int qs_config_default_a(qs_config* c, int32_t num_envs, int32_t num_a
     return QS_OK;
 }
 
+static int check_lds(const qs_config* c) {
+    const qs_layout L = make_layout(c);
+    if (shm_bytes(*c, L.obs_dim, npad_of(c->num_agents)) > 65536)
+        return fail(QS_E_UNSUPPORTED, "observation / obstacle tiles exceed 64 KB of LDS per workgroup");
+    return QS_OK;
+}
+
 extern "C" int qs_layout_query(const qs_config* c, qs_layout* out) {
     int rc = validate(c);
+    if (!rc) rc = check_lds(c);
     if (rc) return rc;
     if (!out) return fail(QS_E_INVALID, "layout is NULL");
     *out = make_layout(c);
     return QS_OK;
+}
+
+// dynamic LDS of a launch: obs tile + neighbour exchange tile + 64 words (flavor-A flags) + obstacle
+// tiles and per-env reset scratch (qs_flavor_b.h obst_tile)
+static size_t shm_bytes(const qs_config& c, int obs_dim, int npad) {
+    const size_t epb = 64 / (size_t)npad;
+    size_t b = sizeof(float) * 64 * (size_t)obs_dim + sizeof(float) * 64 * 8 + sizeof(float) * 64;
+    if (c.use_obstacles) b += epb * (sizeof(float) * 2 * (size_t)c.num_obstacles + (size_t)qs::QS_OBST_SCRATCH);
+    return b;
 }
 
 static int npad_of(int n) {
@@ -369,6 +418,7 @@ static int npad_of(int n) {
 
 extern "C" int qs_create(const qs_config* c, int dev, void* ws, qs_handle** out) {
     int rc = validate(c);
+    if (!rc) rc = check_lds(c);
     if (rc) return rc;
     if (!out) return fail(QS_E_INVALID, "out handle is NULL");
     *out = nullptr;
@@ -424,6 +474,7 @@ static qs::Bufs bufs_of(qs_handle* h) {
     b.ist = (int32_t*)(w + h->lay.istate);
     b.env = (int32_t*)(w + h->lay.env);
     b.envf = (float*)(w + h->lay.env_f);
+    b.obst = (float2*)(w + h->lay.obst);
     b.stale = (float*)(w + h->lay.stale_vel);
     b.obs = (float*)(w + h->lay.obs);
     b.term = (float*)(w + h->lay.term_obs);
@@ -438,7 +489,7 @@ static qs::Bufs bufs_of(qs_handle* h) {
 extern "C" int qs_buffers_get(qs_handle* h, qs_buffers* o) {
     if (!h || !o) return fail(QS_E_INVALID, "NULL argument");
     qs::Bufs b = bufs_of(h);
-    o->state = b.st; o->istate = b.ist; o->env = b.env; o->env_f = b.envf; o->stale_vel = b.stale;
+    o->state = b.st; o->istate = b.ist; o->env = b.env; o->env_f = b.envf; o->obst = (float*)b.obst; o->stale_vel = b.stale;
     o->obs = b.obs; o->term_obs = b.term; o->rew = b.rew; o->done = b.done; o->reset_info = b.rinfo;
     return QS_OK;
 }
@@ -451,17 +502,19 @@ static int launch(qs_handle* h, bool step, const float* act, const uint8_t* mask
     const qs::KP* kpd = (const qs::KP*)((char*)h->ws + h->lay.params);
     const int epb = 64 / h->npad;
     const dim3 grid((unsigned)((h->kp.E + epb - 1) / epb)), block(64);
-    // obs tile + neighbour exchange tile + per-env flags
-    const size_t shm = sizeof(float) * 64 * (size_t)h->kp.obs_dim + sizeof(float) * 64 * 8 + sizeof(int) * 64;
-    const bool a = h->cfg.flavor == QS_FLAVOR_A;
+    const size_t shm = shm_bytes(h->cfg, h->kp.obs_dim, h->npad);
+    const bool a = h->cfg.flavor == QS_FLAVOR_A, ob = h->kp.obst != 0;
 #define QS_LAUNCH(NP)                                                                                           \
     case NP:                                                                                                   \
         if (a) {                                                                                               \
             if (step) hipLaunchKernelGGL(qs::step_kernel_a<NP>, grid, block, shm, s, kpd, b, seed);            \
             else hipLaunchKernelGGL(qs::reset_kernel_a<NP>, grid, block, shm, s, kpd, b, seed);                \
+        } else if (ob) {                                                                                       \
+            if (step) hipLaunchKernelGGL((qs::step_kernel<NP, true>), grid, block, shm, s, kpd, b, seed);      \
+            else hipLaunchKernelGGL((qs::reset_kernel<NP, true>), grid, block, shm, s, kpd, b, seed);          \
         } else {                                                                                               \
-            if (step) hipLaunchKernelGGL(qs::step_kernel<NP>, grid, block, shm, s, kpd, b, seed);              \
-            else hipLaunchKernelGGL(qs::reset_kernel<NP>, grid, block, shm, s, kpd, b, seed);                  \
+            if (step) hipLaunchKernelGGL((qs::step_kernel<NP, false>), grid, block, shm, s, kpd, b, seed);     \
+            else hipLaunchKernelGGL((qs::reset_kernel<NP, false>), grid, block, shm, s, kpd, b, seed);         \
         }                                                                                                      \
         break;
     switch (h->npad) {
@@ -501,7 +554,7 @@ static float* param_slot(qs_handle* h, const char* key) {
     struct { const char* n; float* p; } t[] = {
         {"rew_pos", &k.rew_pos}, {"rew_effort", &k.rew_effort}, {"rew_crash", &k.rew_crash},
         {"rew_orient", &k.rew_orient}, {"rew_spin", &k.rew_spin}, {"quadcol_bin", &k.quadcol},
-        {"quadcol_bin_smooth_max", &k.prox_max}};
+        {"quadcol_bin_smooth_max", &k.prox_max}, {"quadcol_bin_obst", &k.quadcol_obst}};
     for (auto& e : t)
         if (strcmp(e.n, key) == 0) return e.p;
     return nullptr;

@@ -25,11 +25,12 @@ NEIGHBOR_NONE, NEIGHBOR_POS_VEL = 0, 1
 NEIGHBOR = {"none": 0, "pos_vel": 1, "dist_angle": 2, "dist_sangle": 3, "ndist_nsangle": 4, "dist_angle_heading": 5,
             "dist_sangle_sheading": 6, "pos": 7, "npos": 8}
 NEIGHBOR_DIM = {0: 0, 1: 6, 2: 2, 3: 3, 4: 3, 5: 3, 6: 5, 7: 3, 8: 3}
-SCENARIO = {"static_same_goal": 0, "dynamic_repulsive": 1}
+SCENARIO = {"static_same_goal": 0, "dynamic_repulsive": 1, "obst_mix": 2, "o_random": 3, "o_static_same_goal": 4}
 F_POS, F_VEL, F_ROT, F_OMEGA, F_ROT_DAMP, F_CMD_DAMP, F_OU, F_GOAL = 0, 3, 6, 15, 18, 22, 26, 30
 F_PID, F_ANGLE, F_ANGVEL, F_HEADING, NF = 33, 53, 54, 55, 56
 I_SVD, I_FLAGS, I_PREV_LO, I_PREV_HI, NI = 0, 1, 2, 3, 4
 FL_ON_FLOOR, FL_PREV_WALL, FL_PREV_CEIL, FL_CRASH_FLOOR, FL_CRASH_WALL, FL_CRASH_CEIL = 1, 2, 4, 8, 16, 32
+FL_PREV_OBST = 64
 E_TICK, E_FLAGS, E_EPISODE, NE = 0, 1, 2, 3
 EF_STALE, EF_SUCCESS, EF_HAS_POS = 1, 2, 4
 ENVF_TARGET_X, ENVF_TARGET_Y, ENVF_CAPTURE, NENVF = 0, 1, 2, 3
@@ -55,18 +56,21 @@ class QsConfig(ctypes.Structure):
         ("spawn_box", F), ("goal", F * 3),
         ("flavor", I32), ("scenario", I32), ("ticks_per_step", I32), ("n_cameras", I32),
         ("capture_radius", F), ("cam_size", F), ("cam_focal", F), ("cam_px_noise", F), ("cam_fov_deg", F), ("cam_res", F),
+        ("use_obstacles", I32), ("num_obstacles", I32), ("obst_area", I32), ("obst_size", F), ("sdf_resolution", F),
+        ("rew_quadcol_bin_obst", F),
     ]
 
 
 class QsLayout(ctypes.Structure):
-    _fields_ = [("params", SZ), ("state", SZ), ("istate", SZ), ("env", SZ), ("env_f", SZ), ("stale_vel", SZ), ("obs", SZ),
+    _fields_ = [("params", SZ), ("state", SZ), ("istate", SZ), ("env", SZ), ("env_f", SZ), ("obst", SZ), ("stale_vel", SZ),
+                ("obs", SZ),
                 ("term_obs", SZ), ("rew", SZ), ("done", SZ), ("reset_info", SZ), ("total_bytes", SZ), ("obs_dim", I32),
                 ("num_drones", I32)]
 
 
 class QsBuffers(ctypes.Structure):
-    _fields_ = [(n, ctypes.c_void_p) for n in ("state", "istate", "env", "env_f", "stale_vel", "obs", "term_obs", "rew",
-                                               "done", "reset_info")]
+    _fields_ = [(n, ctypes.c_void_p) for n in ("state", "istate", "env", "env_f", "obst", "stale_vel", "obs", "term_obs",
+                                               "rew", "done", "reset_info")]
 
 
 class QuadSwarmError(RuntimeError):

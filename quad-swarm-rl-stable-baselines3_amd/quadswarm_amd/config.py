@@ -51,6 +51,24 @@ class QuadSwarmConfig:
     neighbour_size_cam: float = 0.2
     pixel_noise_cam: float = 3.0
     ticks_per_step: int = 8                   # QuadrotorSingle._step calls per env step (:636)
+    # ---- obstacles (flavor B; quadrotor_params.py quads_obst_*, quad_obstacle_baseline.py) ----
+    use_obstacles: bool = False
+    obst_density: float = 0.2
+    obst_size: float = 0.6
+    obst_spawn_area: tuple = (8, 8)
+    obst_collision_reward: float = 5.0        # quadcol_bin_obst
+
+    @classmethod
+    def c4(cls, num_envs=4096, num_agents=8, **over):
+        """8 drones + obstacles (8x8 m area, density 0.2 -> 12 pillars of 0.6 m),
+        xyz_vxyz_R_omega_floor + pos_vel k=2 + 9 SDF = 40 obs, downwash, quads_mode mix
+        (o_random / o_static_same_goal), 15 s episodes (swarm_rl/runs/obstacles/quad_obstacle_baseline.py)."""
+        c = cls(num_envs=num_envs, num_agents=num_agents, obs_repr="xyz_vxyz_R_omega_floor", neighbor_visible_num=2,
+                neighbor_obs_type="pos_vel", use_obstacles=True, use_downwash=True, quads_mode="mix",
+                collision_smooth_max_penalty=4.0)
+        for k, v in over.items():
+            setattr(c, k, v)
+        return c
 
     @classmethod
     def sb_train(cls, num_envs=4096, num_agents=8, **over):
@@ -94,7 +112,12 @@ class QuadSwarmConfig:
             sense_noise=g("sense_noise", default="default"),
             thrust_noise_ratio=g("thrust_noise_ratio", default=0.05),
             sim_freq=g("sim_freq", default=200.0), sim_steps=g("sim_steps", default=2),
-            seed=g("seed", default=0) or 0, device=g("device", default="cuda"), flavor=flavor)
+            seed=g("seed", default=0) or 0, device=g("device", default="cuda"), flavor=flavor,
+            use_obstacles=bool(g("use_obstacles", "quads_use_obstacles", default=False)),
+            obst_density=g("obst_density", "quads_obst_density", default=0.2),
+            obst_size=g("obst_size", "quads_obst_size", default=0.6),
+            obst_spawn_area=tuple(g("obst_spawn_area", "quads_obst_spawn_area", default=(8, 8))),
+            obst_collision_reward=g("obst_collision_reward", "quads_obst_collision_reward", default=5.0))
         if flavor == "A":
             # quadrotor_multi_rewards builds its dynamics from cfg.dynamics_change only (the
             # thrust_noise_ratio it computes at :46-49 is never used), default Crazyflie noise 0.05
@@ -128,7 +151,18 @@ class QuadSwarmConfig:
     @property
     def obs_dim(self):
         return N.SELF_OBS_DIM[N.OBS_REPR[self.obs_repr]] + N.NEIGHBOR_DIM[N.NEIGHBOR[self.neighbor_obs_type]] * \
-            self.k_neighbors
+            self.k_neighbors + (9 if self.use_obstacles else 0)
+
+    @property
+    def num_obstacles(self):   # quadrotor_multi.py:138
+        return int(self.obst_density * self.obst_spawn_area[0] * self.obst_spawn_area[1])
+
+    @property
+    def scenario_id(self):
+        if self.use_obstacles:
+            return {"mix": N.SCENARIO["obst_mix"], "o_random": N.SCENARIO["o_random"],
+                    "o_static_same_goal": N.SCENARIO["o_static_same_goal"]}[self.quads_mode]
+        return N.SCENARIO[self.quads_mode]
 
     @property
     def act_dim(self):
@@ -146,8 +180,17 @@ class QuadSwarmConfig:
             raise NotImplementedError(f"neighbor_obs_type {self.neighbor_obs_type!r} not implemented")
         if self.flavor == "B" and self.neighbor_obs_type not in ("pos_vel", "none"):
             raise NotImplementedError(f"flavor B implements neighbor_obs_type pos_vel / none")
-        if self.flavor == "B" and self.quads_mode != "static_same_goal":
+        if self.flavor == "B" and not self.use_obstacles and self.quads_mode != "static_same_goal":
             raise NotImplementedError(f"quads_mode {self.quads_mode!r} not implemented for flavor B (static_same_goal)")
+        if self.use_obstacles:
+            if self.flavor != "B":
+                raise NotImplementedError("obstacles are implemented for flavor B")
+            if self.quads_mode not in ("mix", "o_random", "o_static_same_goal"):
+                raise NotImplementedError(f"quads_mode {self.quads_mode!r} with obstacles (mix, o_random, "
+                                          "o_static_same_goal)")
+            a = self.obst_spawn_area
+            if a[0] != a[1] or int(a[0]) != a[0] or not 1 <= a[0] <= 8:
+                raise NotImplementedError("obst_spawn_area must be a square of 1..8 cells")
         if self.flavor == "A":
             if self.quads_mode not in N.SCENARIO:
                 raise NotImplementedError(f"quads_mode {self.quads_mode!r} not implemented for flavor A "
@@ -171,7 +214,7 @@ class QuadSwarmConfig:
         kn = self.k_neighbors
         c.neighbor_obs = N.NEIGHBOR[self.neighbor_obs_type] if kn > 0 else N.NEIGHBOR_NONE
         c.k_neighbors = kn
-        c.scenario = N.SCENARIO.get(self.quads_mode, 0)
+        c.scenario = self.scenario_id
         c.ticks_per_step = int(self.ticks_per_step)
         c.capture_radius = float(self.initial_capture_radius)
         c.cam_size, c.cam_focal, c.cam_px_noise = self.neighbour_size_cam, self.focal_length_cam, self.pixel_noise_cam
@@ -211,4 +254,11 @@ class QuadSwarmConfig:
         c.rew_orient, c.rew_spin = r.get("orient", 1.0), r.get("spin", 0.1)
         c.rew_quadcol_bin = self.collision_reward
         c.rew_quadcol_smooth_max = self.collision_smooth_max_penalty
+        if self.use_obstacles:
+            c.use_obstacles = 1
+            c.num_obstacles = self.num_obstacles
+            c.obst_area = int(self.obst_spawn_area[0])
+            c.obst_size = self.obst_size
+            c.rew_quadcol_bin_obst = self.obst_collision_reward
+            c.spawn_box = 0.1   # QuadrotorSingle.box with obstacles (quadrotor_single.py:238-241)
         return c

@@ -49,6 +49,8 @@ class QuadSwarmEnv:
         self.env_state = view(lay.env, 4 * N.NE * E, torch.int32, (N.NE, E))
         self.env_f = view(lay.env_f, 4 * N.NENVF * E, torch.float32, (N.NENVF, E))
         self.reset_info = view(lay.reset_info, E, torch.uint8, (E,))
+        M = cfg.num_obstacles if cfg.use_obstacles else 0
+        self.obstacles = view(lay.obst, 8 * M * E, torch.float32, (E, M, 2)) if M else None
         self.stale_vel = view(lay.stale_vel, 4 * 3 * I, torch.float32, (3, I))
         self.obs = view(lay.obs, 4 * I * od, torch.float32, (I, od))
         self.term_obs = view(lay.term_obs, 4 * I * od, torch.float32, (I, od))
@@ -176,4 +178,6 @@ def observation_bounds(cfg: QuadSwarmConfig):
     for _ in range(cfg.k_neighbors):
         lo += [-room_range, -2 * vmax * np.ones(3)]
         hi += [room_range, 2 * vmax * np.ones(3)]
+    if cfg.use_obstacles:   # "octmap" (quadrotor_single.py:331)
+        lo.append(-10 * np.ones(9)); hi.append(10 * np.ones(9))
     return np.concatenate(lo).astype(np.float32), np.concatenate(hi).astype(np.float32)

@@ -189,7 +189,7 @@ class GpuQuadVecEnv:
         raise AttributeError(attr_name)
 
     def set_attr(self, attr_name, value, indices=None):
-        if attr_name.startswith("rew_") or attr_name in ("quadcol_bin", "quadcol_bin_smooth_max", "ep_len"):
+        if attr_name.startswith("rew_") or attr_name in ("quadcol_bin", "quadcol_bin_smooth_max", "quadcol_bin_obst", "ep_len"):
             self.env.set_param(attr_name, value)
             return
         setattr(self.cfg, attr_name, value)

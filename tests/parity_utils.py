@@ -45,6 +45,16 @@ def oracle_params(cfg: QuadSwarmConfig):
     rd = cfg.room_dims
     for i, (lo, hi) in enumerate([(-rd[0] / 2, rd[0] / 2), (-rd[1] / 2, rd[1] / 2), (0.0, rd[2])]):
         p.room_lo[i], p.room_hi[i] = lo, hi
+    if cfg.use_obstacles:
+        p.use_obstacles = 1
+        p.num_obstacles = cfg.num_obstacles
+        p.obst_area = int(cfg.obst_spawn_area[0])
+        p.obst_scenario = {"mix": 0, "o_random": 1, "o_static_same_goal": 2}[cfg.quads_mode]
+        p.obst_size = cfg.obst_size
+        p.obst_z = rd[2] / 2.0
+        p.sdf_resolution = 0.1
+        p.rew_quadcol_bin_obst = cfg.obst_collision_reward
+        p.spawn_box = 0.1
     return p
 
 
@@ -65,10 +75,16 @@ def gpu_to_oracle(env, oenv):
         d.on_floor = int(bool(fl & NAT.FL_ON_FLOOR))
         d.prev_wall = int(bool(fl & NAT.FL_PREV_WALL))
         d.prev_ceiling = int(bool(fl & NAT.FL_PREV_CEIL))
+        d.prev_obst = int(bool(fl & NAT.FL_PREV_OBST))
+    ob = env.obstacles.double().cpu().numpy() if env.obstacles is not None else None
     for e in range(E):
         ev = oenv.envs[e]
         ev.tick = int(es[NAT.E_TICK, e])
         ev.episode = int(es[NAT.E_EPISODE, e])
+        if ob is not None:
+            ev.n_obst = ob.shape[1]
+            for o in range(ob.shape[1]):
+                ev.obst[o][0], ev.obst[o][1] = ob[e, o, 0], ob[e, o, 1]
         stale_valid = bool(es[NAT.E_FLAGS, e] & 1)
         for i in range(N):
             g = e * N + i
@@ -102,7 +118,7 @@ def oracle_to_gpu(oenv, env):
         st[30:33, g] = d.goal[:]
         ist[NAT.I_SVD, g] = int(round(d.since_last_svd / dt))
         ist[NAT.I_FLAGS, g] = (NAT.FL_ON_FLOOR if d.on_floor else 0) | (NAT.FL_PREV_WALL if d.prev_wall else 0) | \
-            (NAT.FL_PREV_CEIL if d.prev_ceiling else 0)
+            (NAT.FL_PREV_CEIL if d.prev_ceiling else 0) | (NAT.FL_PREV_OBST if d.prev_obst else 0)
     for e in range(E):
         ev = oenv.envs[e]
         es[NAT.E_TICK, e] = ev.tick
@@ -122,6 +138,11 @@ def oracle_to_gpu(oenv, env):
     env.istate.copy_(torch.from_numpy(ist.astype(np.uint32).view(np.int32)))
     env.env_state.copy_(torch.from_numpy(es))
     env.stale_vel.copy_(torch.from_numpy(stale))
+    if env.obstacles is not None:
+        M = env.obstacles.shape[1]
+        ob = np.array([[[oenv.envs[e].obst[o][0], oenv.envs[e].obst[o][1]] for o in range(M)] for e in range(E)],
+                      dtype=np.float32)
+        env.obstacles.copy_(torch.from_numpy(ob))
 
 
 def oracle_state_arrays(oenv):

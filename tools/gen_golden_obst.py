@@ -131,7 +131,8 @@ def gen_impulse(n=200, seed=43):
                         tape_len=np.array([len(t) for t in tapes]))
 
 
-def make_env_obst(n=8, k=2, seed=0, ep_time=15.0, obs_type="pos_vel", downwash=True):
+def make_env_obst(n=8, k=2, seed=0, ep_time=15.0, obs_type="pos_vel", downwash=True, sense="default",
+                  thrust_noise=0.05):
     from gym_art.quadrotor_multi.quadrotor_multi import QuadrotorEnvMulti
 
     class Cfg:
@@ -146,8 +147,8 @@ def make_env_obst(n=8, k=2, seed=0, ep_time=15.0, obs_type="pos_vel", downwash=T
         room_dims=[10, 10, 10], use_replay_buffer=False, quads_view_mode=[], quads_render=False,
         dynamics_params="Crazyflie", raw_control=True, raw_control_zero_middle=True,
         dynamics_randomize_every=None,
-        dynamics_change=dict(noise=dict(thrust_noise_ratio=0.05), damp=dict(vel=0, omega_quadratic=0)),
-        dyn_sampler_1=None, sense_noise="default", init_random_state=False)
+        dynamics_change=dict(noise=dict(thrust_noise_ratio=thrust_noise), damp=dict(vel=0, omega_quadratic=0)),
+        dyn_sampler_1=None, sense_noise=sense, init_random_state=False)
     px = GenProxyObst(env.rng)
     env.rng = px
     env.scenario.rng = px
@@ -184,7 +185,7 @@ def setup_obst(env, rng):
         ds[5].pos = ds[4].pos + np.array([0.05, 0.03, 0.0])
 
 
-def gen_traj(name, n, k, steps, seed, ep_time, setup=None, **kw):
+def gen_traj(name, n, k, steps, seed, ep_time, setup=None, hover=False, **kw):
     np.random.seed(seed)
     env = make_env_obst(n, k, seed=seed, ep_time=ep_time, **kw)
     G.begin()
@@ -195,6 +196,8 @@ def gen_traj(name, n, k, steps, seed, ep_time, setup=None, **kw):
     init = snapshot(env)
     act_rng = np.random.default_rng(seed + 200)
     actions = np.clip(act_rng.uniform(-1.0, 1.0, (steps, n, 4)) * 0.6 + 0.3, -1, 1)
+    if hover:   # ~hover thrust with small perturbations: no contacts, no random impulses
+        actions = 0.0526 + 0.1 * act_rng.uniform(-1.0, 1.0, (steps, n, 4))
     obs, rew, done = [], [], []
     G.begin()
     for t in range(steps):
@@ -207,7 +210,8 @@ def gen_traj(name, n, k, steps, seed, ep_time, setup=None, **kw):
     np.savez_compressed(os.path.join(OUT, f"obst_traj_{name}.npz"), actions=actions, obs=np.stack(obs),
                         rew=np.stack(rew), done=np.stack(done), tape=tv, spawn=sp, tape0=tv0, spawn0=sp0,
                         obs0=np.array(obs0, dtype=np.float64), n=n, k=k, ep_len=env.envs[0].ep_len,
-                        downwash=int(kw.get("downwash", True)),
+                        downwash=int(kw.get("downwash", True)), sense=int(kw.get("sense", "default") == "default"),
+                        thrust_noise=kw.get("thrust_noise", 0.05),
                         **{"init_" + a: b for a, b in init.items()}, **{"final_" + a: b for a, b in final.items()})
 
 
@@ -220,6 +224,8 @@ def main():
     # episodes so the run crosses several in-env resets (new maps and scenario modes)
     gen_traj("c4", 8, 2, 90, seed=51, ep_time=0.3, setup=setup_obst)
     gen_traj("n4none", 4, 0, 60, seed=52, ep_time=0.25, obs_type="none", downwash=False, setup=setup_obst)
+    # noise-free, contact-free: the GPU replays it directly (SDF obs over a 150-step flight)
+    gen_traj("quiet", 8, 2, 150, seed=53, ep_time=15.0, hover=True, sense=None, thrust_noise=0.0, downwash=False)
     for f in sorted(os.listdir(OUT)):
         if f.startswith("obst_"):
             print(f, os.path.getsize(os.path.join(OUT, f)))
