@@ -13,6 +13,9 @@ collective on the data path; value = all ranks' agent-steps / max-over-ranks wal
 Besides the required fields the JSON line carries:
   roofline      algorithmic bytes per launch / HIP-event kernel time vs 8 TB/s
   cpu_baseline  the C oracle (oracle/, OpenMP over envs) on this host, bounded ~10 s sample
+  end_to_end    SURVEY §8 d(ii): PPO agent-steps/s of the GPU trainer (quadswarm_amd/ppo.py) --
+                rollout over the same env shard + HIP GAE + minibatch update with one RCCL all-reduce
+                of the flat gradient bucket per minibatch (N>1), max-over-ranks wall time
 """
 import argparse
 import json
@@ -126,6 +129,83 @@ def pmc_traffic(config):
         return None
 
 
+# end-to-end PPO leg per workload family: policy / PPO settings of the reference run that trains it
+#   flavor A: swarm_rl/sb_train.py parameter_sweep (SB3 PPO, global_cfg.py:21-29): n_steps 512, 10 epochs,
+#             gamma 0.99, lambda 0.95, clip 0.2, max_grad_norm 0.5, lr 1e-4; attention encoder, 6x128 MLP core.
+#             The reference's 12 envs x 4 agents x 512 steps / batch 1024 = 24 minibatches per epoch; the GPU
+#             rollout is ~700x larger, so the minibatch is scaled to keep 24 minibatches per epoch.
+#   flavor B: runs/quad_multi_mix_baseline.py (rollout 128, lambda 1.0, max_grad_norm 5.0, rnn 256,
+#             attention 256, identity core, 1 pass per sample); 16 minibatches per rollout.
+def e2e_settings(cfg):
+    from quadswarm_amd.ppo import PolicyConfig, PPOConfig
+    if cfg.flavor == "A":
+        return PolicyConfig.sb_train(cfg), PPOConfig(), 24
+    pc = PolicyConfig.for_env(cfg, rnn_size=256, neighbor_hidden_size=256, obst_hidden_size=256)
+    return pc, PPOConfig(n_steps=128, n_epochs=1, gae_lambda=1.0, max_grad_norm=5.0), 16
+
+
+def end_to_end(env, cfg, dev, world, iters, n_steps=None, log=None):
+    """Timed PPO iterations (rollout + GAE + update) on the bench's env shard."""
+    import torch
+    import torch.distributed as dist
+    from quadswarm_amd.ppo import PPOTrainer, SwarmActorCritic
+
+    pc, pcfg, n_mb = e2e_settings(cfg)
+    if n_steps:
+        pcfg.n_steps = n_steps
+    samples = pcfg.n_steps * env.I
+    pcfg.batch_size = -(-samples // n_mb)
+    torch.manual_seed(0)
+    pol = SwarmActorCritic(pc).to(dev)
+    tr = PPOTrainer(env, pol, pcfg, seed=0)
+    tr.reset()
+
+    def sync():
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+
+    # warm-up: one rollout + one epoch cut short (allocator, rocBLAS/hipBLASLt kernel selection)
+    tr.collect_rollouts()
+    tr.train(max_updates=3)
+    sync()
+    t_roll = t_train = 0.0
+    t0 = time.perf_counter()
+    stats = {}
+    for it in range(iters):
+        a = time.perf_counter()
+        tr.collect_rollouts()
+        torch.cuda.synchronize(dev)
+        b = time.perf_counter()
+        stats = tr.train()
+        torch.cuda.synchronize(dev)
+        t_roll += b - a
+        t_train += time.perf_counter() - b
+        if log:
+            log(f"e2e iteration {it + 1}/{iters}: rollout {b - a:.2f} s, update {time.perf_counter() - b:.2f} s")
+    sync()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el, t_roll, t_train], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el, t_roll, t_train = (float(x) for x in t.tolist())
+    nparam = sum(p.numel() for p in pol.parameters())
+    return {
+        "metric": "end-to-end PPO agent-steps/s (rollout + GAE + update; weak scaling, one gradient "
+                  "all-reduce per minibatch)",
+        "value": round(world * iters * samples / el, 1), "unit": "agent-steps/s", "iterations": iters,
+        "s_per_iteration": round(el / iters, 3), "rollout_s": round(t_roll / iters, 3),
+        "update_s": round(t_train / iters, 3),
+        "n_steps": pcfg.n_steps, "n_epochs": pcfg.n_epochs, "batch_size_per_rank": pcfg.batch_size,
+        "minibatches_per_epoch": n_mb, "policy_params": nparam,
+        "policy": f"ActorCriticPolicyCustomSeparateWeights: {pc.neighbor_encoder_type} k={pc.num_use_neighbor_obs}, "
+                  f"rnn {pc.rnn_size}, core {pc.rnn_type or 'identity'} x{pc.rnn_num_layers if pc.rnn_type else 0}, "
+                  f"fp32 (torch/hipBLASLt GEMMs)",
+        "last_update": {k: (round(v, 6) if isinstance(v, float) else v) for k, v in stats.items()},
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -135,6 +215,8 @@ def main():
     ap.add_argument("--graph", type=int, default=100, help="steps per captured hipGraph (0 = eager launches)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--e2e-iters", type=int, default=2, help="timed PPO iterations for end_to_end (0 = skip)")
+    ap.add_argument("--e2e-steps", type=int, default=0, help="override the PPO rollout length n_steps")
     args = ap.parse_args()
 
     import torch
@@ -213,6 +295,16 @@ def main():
     torch.cuda.synchronize(dev)
     k_ms = sum(s.elapsed_time(e) for s, e in evs) / nk
 
+    e2e = None
+    if args.e2e_iters > 0:
+        log = (lambda m: print(m, file=sys.stderr, flush=True)) if rank == 0 else None
+        try:
+            e2e = end_to_end(env, cfg, dev, world, args.e2e_iters, args.e2e_steps or None, log)
+        except Exception as e:  # never let the PPO leg kill the env number
+            if world > 1:
+                raise
+            e2e = {"error": repr(e)}
+
     if rank == 0:
         value = world * I * args.steps / el
         bpa = algorithmic_bytes_per_agent_step(cfg.obs_dim, cfg.num_agents, cfg.flavor,
@@ -248,6 +340,7 @@ def main():
                          "kernel_us": round(k_ms * 1e3, 3), "bytes_per_agent_step": round(bpa, 1),
                          "bytes_per_launch": round(bpa * I)},
             "cpu_baseline": None,
+            "end_to_end": e2e,
         }
         if world == 1 and not args.no_cpu_baseline:
             try:

@@ -225,6 +225,14 @@ size_t qs_state_bytes(qs_handle* h);
 int qs_get_state(qs_handle* h, void* host_dst, size_t bytes, void* stream);
 int qs_set_state(qs_handle* h, const void* host_src, size_t bytes, void* stream);
 
+/* Generalized advantage estimation over a device-resident rollout (replaces stable_baselines3
+ * RolloutBuffer.compute_returns_and_advantage, the PPO of swarm_rl/sb_train.py:53-64).  Arrays are
+ * [n_steps, n_cols] fp32 / u8, time-major; episode_starts[t] = done of step t-1; last_* = after the
+ * final step.  Asynchronous on `stream`. */
+int qs_gae(const float* d_rewards, const float* d_values, const uint8_t* d_episode_starts,
+           const float* d_last_values, const uint8_t* d_last_dones, float* d_advantages, float* d_returns,
+           int32_t n_steps, int32_t n_cols, float gamma, float gae_lambda, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

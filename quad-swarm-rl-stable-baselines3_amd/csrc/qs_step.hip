@@ -32,6 +32,7 @@
 #include "qs_common.h"
 #include "qs_flavor_b.h"
 #include "qs_flavor_a.h"
+#include "qs_gae.h"
 
 // =============================================================================================
 // C ABI
@@ -636,5 +637,19 @@ extern "C" int qs_set_state(qs_handle* h, const void* src, size_t bytes, void* s
     QS_HIP(hipMemcpyAsync((char*)h->ws + h->lay.state, src, qs_state_bytes(h), hipMemcpyHostToDevice,
                           (hipStream_t)stream));
     QS_HIP(hipStreamSynchronize((hipStream_t)stream));
+    return QS_OK;
+}
+
+// GAE over a device rollout (qs_gae.h); all pointers device memory, [T, I] time-major
+extern "C" int qs_gae(const float* rewards, const float* values, const uint8_t* episode_starts,
+                      const float* last_values, const uint8_t* last_dones, float* advantages, float* returns,
+                      int32_t n_steps, int32_t n_cols, float gamma, float gae_lambda, void* stream) {
+    if (!rewards || !values || !episode_starts || !last_values || !last_dones || !advantages || !returns)
+        return fail(QS_E_INVALID, "NULL argument");
+    if (n_steps < 1 || n_cols < 1) return fail(QS_E_INVALID, "n_steps and n_cols must be >= 1");
+    const dim3 block(256), grid((unsigned)((n_cols + 255) / 256));
+    hipLaunchKernelGGL(qs::gae_kernel, grid, block, 0, (hipStream_t)stream, rewards, values, episode_starts,
+                       last_values, last_dones, advantages, returns, n_steps, n_cols, gamma, gae_lambda);
+    QS_HIP(hipGetLastError());
     return QS_OK;
 }

@@ -81,7 +81,7 @@ class QuadSwarmError(RuntimeError):
 EXPORTS = ["qs_abi_version", "qs_last_error", "qs_struct_sizes", "qs_config_default", "qs_config_default_a",
            "qs_layout_query", "qs_create", "qs_destroy",
            "qs_buffers_get", "qs_reset", "qs_step", "qs_set_param",
-           "qs_get_param", "qs_state_bytes", "qs_get_state", "qs_set_state"]
+           "qs_get_param", "qs_state_bytes", "qs_get_state", "qs_set_state", "qs_gae"]
 
 _lib = None
 
@@ -105,6 +105,7 @@ def lib():
         "qs_set_param": ([V, ctypes.c_char_p, ctypes.c_double], I32),
         "qs_get_param": ([V, ctypes.c_char_p, P(ctypes.c_double)], I32),
         "qs_state_bytes": ([V], SZ), "qs_get_state": ([V, V, SZ, V], I32), "qs_set_state": ([V, V, SZ, V], I32),
+        "qs_gae": ([V, V, V, V, V, V, V, I32, I32, F, F, V], I32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

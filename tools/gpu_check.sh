@@ -20,7 +20,11 @@ for s in "$@"; do
     smoke) step smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) step gpu_tests 900 python -m pytest tests -m gpu -q -x ;;
     testsall) step gpu_tests 900 python -m pytest tests -m gpu -q ;;
-    bench) step bench 400 python bench.py ;;
+    bench) step bench 600 python bench.py ;;
+    ppotests) step ppo_tests 600 python -m pytest tests/test_gpu_ppo.py -q -x ;;
+    e2ea) step e2e_a8 600 python bench.py --config a8 --steps 500 --no-cpu-baseline --e2e-iters 1 --e2e-steps 64 ;;
+    e2ec3) step e2e_c3 600 python bench.py --config c3 --steps 500 --no-cpu-baseline --e2e-iters 1 ;;
+    e2ea512) step e2e_a8_512 900 python bench.py --config a8 --steps 500 --no-cpu-baseline --e2e-iters 2 ;;
     benchfast) step bench 300 python bench.py --steps 1000 --cpu-seconds 5 ;;
     bencha) step bench_a8 400 python bench.py --config a8 --steps 1000 --cpu-seconds 10 ;;
     bencha4) step bench_a4 400 python bench.py --config a4 --steps 1000 --cpu-seconds 5 ;;
@@ -28,17 +32,17 @@ for s in "$@"; do
     benchc3) step bench_c3 400 python bench.py --config c3 --steps 2000 --cpu-seconds 10 ;;
     prof)
       export TMPDIR=/tmp
-      step prof_kt 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_kt -o kt --output-format csv -- python bench.py --steps 1000 --no-cpu-baseline --graph 0
-      step prof_fetch 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof_fetch -o f --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu-baseline --graph 0
-      step prof_write 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof_write -o w --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu-baseline --graph 0
-      step prof_sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INSTS_LDS -d gpurun_out/prof_sq -o s --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu-baseline --graph 0
+      step prof_kt 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_kt -o kt --output-format csv -- python bench.py --steps 1000 --no-cpu-baseline --graph 0 --e2e-iters 0
+      step prof_fetch 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof_fetch -o f --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu-baseline --graph 0 --e2e-iters 0
+      step prof_write 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof_write -o w --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu-baseline --graph 0 --e2e-iters 0
+      step prof_sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INSTS_LDS -d gpurun_out/prof_sq -o s --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu-baseline --graph 0 --e2e-iters 0
       ;;
     profa)
       export TMPDIR=/tmp
-      step profa_kt 400 rocprofv3 --kernel-trace --stats -d gpurun_out/profa_kt -o kt --output-format csv -- python bench.py --config a8 --steps 1000 --no-cpu-baseline --graph 0
-      step profa_fetch 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/profa_fetch -o f --output-format csv -- python bench.py --config a8 --steps 100 --warmup 10 --no-cpu-baseline --graph 0
-      step profa_write 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/profa_write -o w --output-format csv -- python bench.py --config a8 --steps 100 --warmup 10 --no-cpu-baseline --graph 0
-      step profa_sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INSTS_LDS -d gpurun_out/profa_sq -o s --output-format csv -- python bench.py --config a8 --steps 100 --warmup 10 --no-cpu-baseline --graph 0
+      step profa_kt 400 rocprofv3 --kernel-trace --stats -d gpurun_out/profa_kt -o kt --output-format csv -- python bench.py --config a8 --steps 1000 --no-cpu-baseline --graph 0 --e2e-iters 0
+      step profa_fetch 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/profa_fetch -o f --output-format csv -- python bench.py --config a8 --steps 100 --warmup 10 --no-cpu-baseline --graph 0 --e2e-iters 0
+      step profa_write 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/profa_write -o w --output-format csv -- python bench.py --config a8 --steps 100 --warmup 10 --no-cpu-baseline --graph 0 --e2e-iters 0
+      step profa_sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INSTS_LDS -d gpurun_out/profa_sq -o s --output-format csv -- python bench.py --config a8 --steps 100 --warmup 10 --no-cpu-baseline --graph 0 --e2e-iters 0
       ;;
     stamps) step stamps 300 python tools/phase_stamps.py ;;
     calib)
