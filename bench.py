@@ -148,9 +148,10 @@ def end_to_end(env, cfg, dev, world, iters, n_steps=None, log=None):
     """Timed PPO iterations (rollout + GAE + update) on the bench's env shard."""
     import torch
     import torch.distributed as dist
-    from quadswarm_amd.ppo import PPOTrainer, SwarmActorCritic
+    from quadswarm_amd.ppo import PPOTrainer, SwarmActorCritic, use_gemm_table
 
     pc, pcfg, n_mb = e2e_settings(cfg)
+    tuned = use_gemm_table() if os.environ.get("PYTORCH_TUNABLEOP_TUNING") != "1" else "tuning"
     if n_steps:
         pcfg.n_steps = n_steps
     samples = pcfg.n_steps * env.I
@@ -202,6 +203,7 @@ def end_to_end(env, cfg, dev, world, iters, n_steps=None, log=None):
         "policy": f"ActorCriticPolicyCustomSeparateWeights: {pc.neighbor_encoder_type} k={pc.num_use_neighbor_obs}, "
                   f"rnn {pc.rnn_size}, core {pc.rnn_type or 'identity'} x{pc.rnn_num_layers if pc.rnn_type else 0}, "
                   f"fp32 (torch/hipBLASLt GEMMs)",
+        "gemm_table": tuned,
         "last_update": {k: (round(v, 6) if isinstance(v, float) else v) for k, v in stats.items()},
     }
 
@@ -336,7 +338,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
-                         "kernel": f"qs::step_kernel{'_a' if cfg.flavor == 'A' else ''}<{npad(cfg.num_agents)}>",
+                         "kernel": (f"qs::step_kernel_a<{npad(cfg.num_agents)}>" if cfg.flavor == "A" else
+                                    f"qs::step_kernel<{npad(cfg.num_agents)}, {'true' if cfg.use_obstacles else 'false'}>"),
                          "kernel_us": round(k_ms * 1e3, 3), "bytes_per_agent_step": round(bpa, 1),
                          "bytes_per_launch": round(bpa * I)},
             "cpu_baseline": None,

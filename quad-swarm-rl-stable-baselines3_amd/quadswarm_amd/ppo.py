@@ -22,6 +22,7 @@ all_reduce (RCCL over xGMI; gloo in the CPU tests).  Weights are broadcast from 
 """
 import ctypes
 import math
+import os
 from dataclasses import dataclass, field
 from typing import List, Optional
 
@@ -282,6 +283,26 @@ def gae(rewards, values, episode_starts, last_values, last_dones, gamma=0.99, ga
                                p(advantages), p(returns), T, I, float(gamma), float(gae_lambda),
                                ctypes.c_void_p(s)), "qs_gae")
     return advantages, returns
+
+
+# ----------------------------------------------------------------------------------------------
+# GEMM solution table
+# ----------------------------------------------------------------------------------------------
+GEMM_TABLE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuning", "tunableop_gfx950.csv")
+
+
+def use_gemm_table(path=GEMM_TABLE):
+    """Pin the policy's fp32 GEMMs to the hipBLASLt/rocBLAS solutions measured fastest on MI355X for the
+    bench shapes (PyTorch TunableOp in read-only mode; tools/gpu_check.sh `tune*` regenerates the table).
+    Shapes not in the table keep the library default.  Returns True when the table was loaded."""
+    if not (torch.cuda.is_available() and os.path.exists(path)):
+        return False
+    if "gfx950" not in torch.cuda.get_device_properties(torch.cuda.current_device()).gcnArchName:
+        return False
+    tun = torch.cuda.tunable
+    tun.enable(True)
+    tun.tuning_enable(False)
+    return bool(tun.read_file(path))
 
 
 # ----------------------------------------------------------------------------------------------

@@ -44,6 +44,22 @@ for s in "$@"; do
       step profa_write 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/profa_write -o w --output-format csv -- python bench.py --config a8 --steps 100 --warmup 10 --no-cpu-baseline --graph 0 --e2e-iters 0
       step profa_sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INSTS_LDS -d gpurun_out/profa_sq -o s --output-format csv -- python bench.py --config a8 --steps 100 --warmup 10 --no-cpu-baseline --graph 0 --e2e-iters 0
       ;;
+    profe2e)
+      export TMPDIR=/tmp
+      step profe2e_kt 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profe2e_kt -o kt --output-format csv -- python bench.py --config a8 --steps 200 --no-cpu-baseline --e2e-iters 1 --e2e-steps 64
+      step profe2e_c3_kt 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profe2e_c3_kt -o kt --output-format csv -- python bench.py --config c3 --steps 200 --no-cpu-baseline --e2e-iters 1
+      rm -f gpurun_out/profe2e_kt/*kernel_trace.csv gpurun_out/profe2e_c3_kt/*kernel_trace.csv
+      ;;
+    tune)
+      step tune_a8 900 env PYTORCH_TUNABLEOP_ENABLED=1 PYTORCH_TUNABLEOP_TUNING=1 PYTORCH_TUNABLEOP_VERBOSE=1 PYTORCH_TUNABLEOP_FILENAME=gpurun_out/tunableop_a8_%d.csv python bench.py --config a8 --steps 200 --no-cpu-baseline --e2e-iters 1 --e2e-steps 64
+      step tuned_a8 600 env PYTORCH_TUNABLEOP_ENABLED=1 PYTORCH_TUNABLEOP_TUNING=0 PYTORCH_TUNABLEOP_FILENAME=gpurun_out/tunableop_a8_%d.csv python bench.py --config a8 --steps 200 --no-cpu-baseline --e2e-iters 1 --e2e-steps 64
+      ;;
+    tunec3)
+      step tune_c3 1100 env PYTORCH_TUNABLEOP_ENABLED=1 PYTORCH_TUNABLEOP_TUNING=1 PYTORCH_TUNABLEOP_MAX_TUNING_ITERATIONS=20 PYTORCH_TUNABLEOP_FILENAME=gpurun_out/tunableop_c3_%d.csv python bench.py --config c3 --steps 200 --no-cpu-baseline --e2e-iters 1
+      ;;
+    tunea512)
+      step tune_a512 1100 env PYTORCH_TUNABLEOP_ENABLED=1 PYTORCH_TUNABLEOP_TUNING=1 PYTORCH_TUNABLEOP_MAX_TUNING_ITERATIONS=20 PYTORCH_TUNABLEOP_FILENAME=gpurun_out/tunableop_a512_%d.csv python bench.py --config a8 --steps 200 --no-cpu-baseline --e2e-iters 1
+      ;;
     stamps) step stamps 300 python tools/phase_stamps.py ;;
     calib)
       export TMPDIR=/tmp
