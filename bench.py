@@ -215,6 +215,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--graph", type=int, default=100, help="steps per captured hipGraph (0 = eager launches)")
+    ap.add_argument("--generic", action="store_true", help="generic kernels instead of qs_specialize (hipRTC)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--e2e-iters", type=int, default=2, help="timed PPO iterations for end_to_end (0 = skip)")
@@ -236,7 +237,7 @@ def main():
     from quadswarm_amd.env import QuadSwarmEnv
 
     kw = CONFIGS[args.config]
-    cfg = make_cfg(kw, seed=0)
+    cfg = make_cfg(kw, seed=0, specialize=not args.generic)
     I = cfg.num_envs * cfg.num_agents
     cfg.drone_id_offset = rank * I
     env = QuadSwarmEnv(cfg, device=dev)
@@ -334,7 +335,8 @@ def main():
                        "agents_per_env": cfg.num_agents, "visible_neighbors": cfg.k_neighbors,
                        "obs_dim": cfg.obs_dim, "global_batch": world * I, "parallelism": f"env-shard x{world}",
                        "flavor": cfg.flavor,
-                       "launch": f"hipGraph of {chunk} steps" if chunk else "eager"},
+                       "launch": (f"hipGraph of {chunk} steps" if chunk else "eager") +
+                                 (", specialised kernels (qs_specialize, hipRTC)" if env.specialized else ", generic kernels")},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,

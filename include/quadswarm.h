@@ -27,8 +27,10 @@
 #ifndef QUADSWARM_H
 #define QUADSWARM_H
 
+#ifndef __HIPCC_RTC__
 #include <stddef.h>
 #include <stdint.h>
+#endif
 
 #ifdef __cplusplus
 extern "C" {
@@ -224,6 +226,20 @@ int qs_get_param(qs_handle* h, const char* key, double* value);
 size_t qs_state_bytes(qs_handle* h);
 int qs_get_state(qs_handle* h, void* host_dst, size_t bytes, void* stream);
 int qs_set_state(qs_handle* h, const void* host_src, size_t bytes, void* stream);
+
+/* Runtime specialisation: recompile this handle's step/reset kernels with hipRTC, its whole parameter
+ * block baked in as constants (parameters qs_set_param can change stay live).  enable = 0 returns to the
+ * generic kernels.  Results are the generic kernels' (tests/test_gpu_specialize.py).  Compiled modules
+ * are cached per process.  No reference counterpart (the reference's numba JIT specialises on types only). */
+int qs_specialize(qs_handle* h, int enable);
+int qs_is_specialized(const qs_handle* h);
+/* Host-only: compile a config's specialised kernels without a device (build check); returns the
+ * code-object size in bytes or a negative error. */
+long long qs_specialize_compile(const qs_config* cfg);
+
+/* The kernel parameter block a config produces, as 32-bit words (host only, no device needed).
+ * Returns the word count or a negative error. */
+int qs_config_kp_words(const qs_config* cfg, uint32_t* out, size_t n_words);
 
 /* Generalized advantage estimation over a device-resident rollout (replaces stable_baselines3
  * RolloutBuffer.compute_returns_and_advantage, the PPO of swarm_rl/sb_train.py:53-64).  Arrays are

@@ -2,8 +2,10 @@
 // kernel parameters, SoA state I/O, the QuadrotorDynamics substep (quadrotor_dynamics.py:355-656),
 // LDS staging helpers and the per-env Philox counter.  Included by qs_step.hip only.
 #pragma once
+#ifndef __HIPCC_RTC__   // hipRTC (qs_specialize) provides these itself
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#endif
 
 #include "qs_rng.h"
 #include "quadswarm.h"
@@ -44,6 +46,32 @@ struct KP {
     int obst, M, obst_n, obst_scen;                 // on, obstacles per env, grid side, scenario
     float obst_r, obst_thr, obst_z, sdf_res, quadcol_obst;
 };
+
+// Runtime specialisation (qs_specialize, hipRTC): the whole parameter block is a compile-time constant,
+// so every physical constant folds into the instructions and config branches vanish; only the fields
+// qs_set_param may change after creation are still read from the device block.
+#ifdef QS_JIT
+struct KPWords { uint32_t w[sizeof(KP) / 4]; };
+static_assert(sizeof(KP) % 4 == 0, "KP must be a whole number of words");
+__device__ __forceinline__ KP bind_kp(const KP* __restrict__ p) {
+    constexpr KP c = __builtin_bit_cast(KP, KPWords{{QS_KP_WORDS}});
+    KP k = c;
+    k.ep_len = p->ep_len;
+    k.rew_pos = p->rew_pos;
+    k.rew_effort = p->rew_effort;
+    k.rew_crash = p->rew_crash;
+    k.rew_orient = p->rew_orient;
+    k.rew_spin = p->rew_spin;
+    k.quadcol = p->quadcol;
+    k.prox_max = p->prox_max;
+    k.prox_ratio = p->prox_ratio;
+    k.quadcol_obst = p->quadcol_obst;
+    return k;
+}
+#define QS_BIND_KP(p) const KP kp = bind_kp(p)
+#else
+#define QS_BIND_KP(p) const KP& kp = *(p)
+#endif
 
 struct Bufs {
     float* st;

@@ -414,7 +414,7 @@ __device__ __forceinline__ void reset_env_a(const KP& kp, Drone& d, Ctl& c, floa
 template <int NPAD>
 __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, Bufs b, uint32_t seed) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    const KP& kp = *kpp;
+    QS_BIND_KP(kpp);
     constexpr int EPB = 64 / NPAD;
     const int lane = threadIdx.x;
     const int el = lane / NPAD, di = lane % NPAD;
@@ -538,7 +538,7 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
 template <int NPAD>
 __global__ __launch_bounds__(64) void reset_kernel_a(const KP* __restrict__ kpp, Bufs b, uint32_t seed) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    const KP& kp = *kpp;
+    QS_BIND_KP(kpp);
     constexpr int EPB = 64 / NPAD;
     const int lane = threadIdx.x;
     const int el = lane / NPAD, di = lane % NPAD;

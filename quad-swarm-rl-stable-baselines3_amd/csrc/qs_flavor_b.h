@@ -479,7 +479,7 @@ __device__ __forceinline__ float2* obst_tile(float* lds, const KP& kp) {
 template <int NPAD, bool OBST>
 __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bufs b, uint32_t seed) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    const KP& kp = *kpp;
+    QS_BIND_KP(kpp);
     QS_STAMP_DECL
     QS_STAMP(0);
     constexpr int EPB = 64 / NPAD;
@@ -731,7 +731,7 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
 template <int NPAD, bool OBST>
 __global__ __launch_bounds__(64) void reset_kernel(const KP* __restrict__ kpp, Bufs b, uint32_t seed) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    const KP& kp = *kpp;
+    QS_BIND_KP(kpp);
     constexpr int EPB = 64 / NPAD;
     const int lane = threadIdx.x;
     const int el = lane / NPAD, di = lane % NPAD;

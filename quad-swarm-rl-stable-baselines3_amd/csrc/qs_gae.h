@@ -8,8 +8,10 @@
 // read per input and write per output; each lane carries its column's recurrence in registers.
 // HBM-bound: 17 B per element (r, V, start byte in; A, returns out).
 #pragma once
+#ifndef __HIPCC_RTC__   // hipRTC (qs_specialize) provides these itself
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#endif
 
 namespace qs {
 

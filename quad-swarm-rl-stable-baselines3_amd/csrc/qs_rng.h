@@ -9,8 +9,10 @@
 // Normals: Box-Muller on word pairs (0,1) and (2,3) of a block -> 4 normals per block.
 // Uniforms: stream | QS_UNIF_BIT, one word per draw.  The CPU oracle uses the same numbering.
 #pragma once
+#ifndef __HIPCC_RTC__   // hipRTC (qs_specialize) provides these itself
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#endif
 
 namespace qs {
 

@@ -23,6 +23,10 @@
 
 #include <math.h>
 
+#include <hip/hiprtc.h>
+
+#include <map>
+#include <mutex>
 #include <new>
 #include <string>
 #include <vector>
@@ -45,6 +49,8 @@ struct qs_handle {
     void* ws;
     bool owns_ws;
     int npad;
+    hipFunction_t jit_step = nullptr;    // qs_specialize: kernels compiled for this handle's parameters
+    hipFunction_t jit_reset = nullptr;
 };
 
 static thread_local std::string g_err;
@@ -505,6 +511,11 @@ static int launch(qs_handle* h, bool step, const float* act, const uint8_t* mask
     const dim3 grid((unsigned)((h->kp.E + epb - 1) / epb)), block(64);
     const size_t shm = shm_bytes(h->cfg, h->kp.obs_dim, h->npad);
     const bool a = h->cfg.flavor == QS_FLAVOR_A, ob = h->kp.obst != 0;
+    if (hipFunction_t f = step ? h->jit_step : h->jit_reset) {
+        void* args[] = {(void*)&kpd, (void*)&b, (void*)&seed};
+        QS_HIP(hipModuleLaunchKernel(f, grid.x, 1, 1, block.x, 1, 1, (unsigned)shm, s, args, nullptr));
+        return QS_OK;
+    }
 #define QS_LAUNCH(NP)                                                                                           \
     case NP:                                                                                                   \
         if (a) {                                                                                               \
@@ -653,3 +664,144 @@ extern "C" int qs_gae(const float* rewards, const float* values, const uint8_t* 
     QS_HIP(hipGetLastError());
     return QS_OK;
 }
+
+// the kernel parameter block a config produces (host only; runtime specialisation / diagnostics)
+extern "C" int qs_config_kp_words(const qs_config* c, uint32_t* out, size_t n_words) {
+    if (!c || !out) return fail(QS_E_INVALID, "NULL argument");
+    int rc = validate(c);
+    if (rc) return rc;
+    if (n_words < sizeof(qs::KP) / 4) return fail(QS_E_INVALID, "buffer too small for the parameter block");
+    const qs::KP k = make_kp(c, make_layout(c));
+    memcpy(out, &k, sizeof(qs::KP));
+    return (int)(sizeof(qs::KP) / 4);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Runtime specialisation (hipRTC).  The step/reset kernels are recompiled with this handle's whole
+// parameter block as a compile-time constant (QS_JIT, qs_common.h bind_kp): physical constants fold
+// into the instructions, config branches and unused feature paths vanish, and the kernel stops paying
+// scalar-cache round trips for parameters.  Fields qs_set_param may change stay in device memory.
+// Modules are cached per (device, parameter block, kernel) for the process lifetime.
+// ---------------------------------------------------------------------------------------------
+#include "qs_jit_sources.inc"
+
+namespace {
+struct JitEntry {
+    hipModule_t mod = nullptr;
+    hipFunction_t step = nullptr, reset = nullptr;
+};
+std::mutex g_jit_mu;
+std::map<std::string, JitEntry> g_jit_cache;
+}  // namespace
+
+static std::string kernel_names(const qs_config* c, const qs::KP& kp, int npad, std::string* reset) {
+    const std::string np = std::to_string(npad);
+    if (c->flavor == QS_FLAVOR_A) {
+        *reset = "qs::reset_kernel_a<" + np + ">";
+        return "qs::step_kernel_a<" + np + ">";
+    }
+    const char* ob = kp.obst ? "true" : "false";
+    *reset = "qs::reset_kernel<" + np + ", " + ob + ">";
+    return "qs::step_kernel<" + np + ", " + ob + ">";
+}
+
+static std::string kp_words(const qs::KP& kp) {
+    std::string words;
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(&kp);
+    char buf[16];
+    for (size_t i = 0; i < sizeof(qs::KP) / 4; ++i) {
+        snprintf(buf, sizeof buf, "0x%08xu,", w[i]);
+        words += buf;
+    }
+    words.pop_back();
+    return words;
+}
+
+// hipRTC compile of the step/reset kernels for one parameter block (host only)
+static int jit_compile(const qs_config* c, const qs::KP& kp, int npad, std::vector<char>& code, std::string& lstep,
+                       std::string& lreset) {
+    std::string reset_name;
+    const std::string step_name = kernel_names(c, kp, npad, &reset_name);
+    std::string src =
+        "typedef __hip_internal::uint8_t uint8_t;\n"
+        "typedef __hip_internal::int8_t int8_t;\n"
+        "typedef __hip_internal::uint16_t uint16_t;\n"
+        "typedef __hip_internal::int16_t int16_t;\n"
+        "typedef __hip_internal::uint32_t uint32_t;\n"
+        "typedef __hip_internal::int32_t int32_t;\n"
+        "typedef __hip_internal::uint64_t uint64_t;\n"
+        "typedef __hip_internal::int64_t int64_t;\n"
+        "typedef unsigned long uintptr_t;\n"
+        "#define QS_JIT 1\n#define QS_KP_WORDS " + kp_words(kp) + "\n";
+    src += c->flavor == QS_FLAVOR_A ? "#include \"qs_flavor_a.h\"\n" : "#include \"qs_flavor_b.h\"\n";
+    hiprtcProgram prog;
+    if (hiprtcCreateProgram(&prog, src.c_str(), "qs_jit.hip", kJitNumHeaders, kJitHeaderSources, kJitHeaderNames) !=
+        HIPRTC_SUCCESS)
+        return fail(QS_E_HIP, "hiprtcCreateProgram failed");
+    hiprtcAddNameExpression(prog, step_name.c_str());
+    hiprtcAddNameExpression(prog, reset_name.c_str());
+    const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=on",
+                          "-munsafe-fp-atomics"};
+    const hiprtcResult rc = hiprtcCompileProgram(prog, (int)(sizeof opts / sizeof opts[0]), opts);
+    if (rc != HIPRTC_SUCCESS) {
+        size_t n = 0;
+        hiprtcGetProgramLogSize(prog, &n);
+        std::string log(n + 1, '\0');
+        hiprtcGetProgramLog(prog, &log[0]);
+        hiprtcDestroyProgram(&prog);
+        return fail(QS_E_HIP, std::string("hipRTC compile failed: ") + hiprtcGetErrorString(rc) + "\n" + log);
+    }
+    const char *ls = nullptr, *lr = nullptr;
+    hiprtcGetLoweredName(prog, step_name.c_str(), &ls);
+    hiprtcGetLoweredName(prog, reset_name.c_str(), &lr);
+    lstep = ls ? ls : "";
+    lreset = lr ? lr : "";
+    size_t code_n = 0;
+    hiprtcGetCodeSize(prog, &code_n);
+    code.resize(code_n);
+    if (code_n) hiprtcGetCode(prog, code.data());
+    hiprtcDestroyProgram(&prog);
+    if (lstep.empty() || lreset.empty() || code.empty()) return fail(QS_E_HIP, "hipRTC produced no kernels");
+    return QS_OK;
+}
+
+extern "C" int qs_specialize(qs_handle* h, int enable) {
+    if (!h) return fail(QS_E_INVALID, "NULL handle");
+    if (!enable) {
+        h->jit_step = h->jit_reset = nullptr;
+        return QS_OK;
+    }
+    QS_HIP(hipSetDevice(h->device));
+    std::string rn;
+    const std::string key = std::to_string(h->device) + "|" + kernel_names(&h->cfg, h->kp, h->npad, &rn) + "|" +
+                            kp_words(h->kp);
+    std::lock_guard<std::mutex> lock(g_jit_mu);
+    auto it = g_jit_cache.find(key);
+    if (it == g_jit_cache.end()) {
+        std::vector<char> code;
+        std::string lstep, lreset;
+        if (int rc = jit_compile(&h->cfg, h->kp, h->npad, code, lstep, lreset)) return rc;
+        JitEntry e;
+        QS_HIP(hipModuleLoadData(&e.mod, code.data()));
+        QS_HIP(hipModuleGetFunction(&e.step, e.mod, lstep.c_str()));
+        QS_HIP(hipModuleGetFunction(&e.reset, e.mod, lreset.c_str()));
+        it = g_jit_cache.emplace(key, e).first;
+    }
+    h->jit_step = it->second.step;
+    h->jit_reset = it->second.reset;
+    return QS_OK;
+}
+
+// host-only check that a config's specialised kernels compile; returns the code-object size in bytes
+extern "C" long long qs_specialize_compile(const qs_config* c) {
+    if (!c) return fail(QS_E_INVALID, "NULL argument");
+    if (int rc = validate(c)) return rc;
+    const qs::KP kp = make_kp(c, make_layout(c));
+    std::vector<char> code;
+    std::string ls, lr;
+    if (int rc = jit_compile(c, kp, npad_of(c->num_agents), code, ls, lr)) return rc;
+    return (long long)code.size();
+}
+
+// 1 when the handle launches specialised kernels
+extern "C" int qs_is_specialized(const qs_handle* h) { return h && h->jit_step ? 1 : 0; }

@@ -81,7 +81,8 @@ class QuadSwarmError(RuntimeError):
 EXPORTS = ["qs_abi_version", "qs_last_error", "qs_struct_sizes", "qs_config_default", "qs_config_default_a",
            "qs_layout_query", "qs_create", "qs_destroy",
            "qs_buffers_get", "qs_reset", "qs_step", "qs_set_param",
-           "qs_get_param", "qs_state_bytes", "qs_get_state", "qs_set_state", "qs_gae"]
+           "qs_get_param", "qs_state_bytes", "qs_get_state", "qs_set_state", "qs_gae",
+           "qs_specialize", "qs_is_specialized", "qs_config_kp_words", "qs_specialize_compile"]
 
 _lib = None
 
@@ -106,6 +107,9 @@ def lib():
         "qs_get_param": ([V, ctypes.c_char_p, P(ctypes.c_double)], I32),
         "qs_state_bytes": ([V], SZ), "qs_get_state": ([V, V, SZ, V], I32), "qs_set_state": ([V, V, SZ, V], I32),
         "qs_gae": ([V, V, V, V, V, V, V, I32, I32, F, F, V], I32),
+        "qs_specialize": ([V, I32], I32), "qs_is_specialized": ([V], I32),
+        "qs_config_kp_words": ([P(QsConfig), V, SZ], I32),
+        "qs_specialize_compile": ([P(QsConfig)], ctypes.c_longlong),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

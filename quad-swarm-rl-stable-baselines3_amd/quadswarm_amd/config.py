@@ -40,6 +40,7 @@ class QuadSwarmConfig:
     sim_steps: int = 2
     seed: int = 0
     drone_id_offset: int = 0                  # global id of this shard's first drone (multi-GPU)
+    specialize: bool = True                   # qs_specialize: hipRTC kernels with this config's constants baked in
     apply_collision_force: bool = True
     rew_coeff: dict = field(default_factory=lambda: dict(DEFAULT_REW))
     device: str = "cuda"

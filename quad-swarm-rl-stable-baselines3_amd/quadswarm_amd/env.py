@@ -40,6 +40,12 @@ class QuadSwarmEnv:
         h = ctypes.c_void_p()
         N.check(L.qs_create(self.qcfg, self.device.index, ctypes.c_void_p(ws.data_ptr()), ctypes.byref(h)), "qs_create")
         self._h = h
+        if cfg.specialize:
+            try:
+                self.specialize(True)
+            except N.QuadSwarmError as e:   # the generic HIP kernels give the same results (bitwise)
+                import warnings
+                warnings.warn(f"qs_specialize failed, using the generic kernels: {e}")
 
         def view(o, nbytes, dtype, shape):
             return ws[o:o + nbytes].view(dtype).view(*shape)
@@ -91,6 +97,15 @@ class QuadSwarmEnv:
         self._act_keepalive = a
         N.check(N.lib().qs_step(self._h, ctypes.c_void_p(a.data_ptr()), self._stream()), "qs_step")
         return self.obs, self.rew, self.done, self.term_obs
+
+    def specialize(self, enable=True):
+        """Switch to kernels recompiled (hipRTC) with this env's parameters as constants (qs_specialize);
+        same results as the generic kernels, shorter per-step critical path."""
+        N.check(N.lib().qs_specialize(self._h, 1 if enable else 0), "qs_specialize")
+
+    @property
+    def specialized(self):
+        return bool(N.lib().qs_is_specialized(self._h))
 
     # ------------------------------------------------------------------------------------------
     def set_param(self, key, value):

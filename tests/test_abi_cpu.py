@@ -197,3 +197,26 @@ def test_create_without_device_fails_loudly():
     rc = L.qs_create(QuadSwarmConfig(num_envs=4, num_agents=8).to_qs_config(), 0, None, ctypes.byref(h))
     assert rc == -3 and not h.value
     assert L.qs_last_error()
+
+
+@pytest.mark.parametrize("make", [lambda: QuadSwarmConfig(num_envs=64, num_agents=8, neighbor_visible_num=6),
+                                  lambda: QuadSwarmConfig.c4(num_envs=64),
+                                  lambda: QuadSwarmConfig.sb_train(num_envs=64, num_agents=4)],
+                         ids=["c3", "c4", "a4"])
+def test_specialised_kernels_compile_on_the_host(make):
+    """qs_specialize's hipRTC path (kernel source embedded in the .so, parameter block baked in)
+    compiles for gfx950 without a device."""
+    L = N.lib()
+    n = L.qs_specialize_compile(make().to_qs_config())
+    assert n > 10000, L.qs_last_error()
+
+
+def test_config_kp_words():
+    L = N.lib()
+    buf = (ctypes.c_uint32 * 4096)()
+    qc = QuadSwarmConfig(num_envs=64, num_agents=8).to_qs_config()
+    n = L.qs_config_kp_words(qc, buf, 4096)
+    assert 100 < n < 4096
+    assert L.qs_config_kp_words(qc, buf, 10) < 0      # buffer too small
+    # the parameter block starts with E, N, I, obs_dim
+    assert list(buf[:4]) == [64, 8, 512, 54]

@@ -25,10 +25,12 @@ for s in "$@"; do
     e2ea) step e2e_a8 600 python bench.py --config a8 --steps 500 --no-cpu-baseline --e2e-iters 1 --e2e-steps 64 ;;
     e2ec3) step e2e_c3 600 python bench.py --config c3 --steps 500 --no-cpu-baseline --e2e-iters 1 ;;
     e2ea512) step e2e_a8_512 900 python bench.py --config a8 --steps 500 --no-cpu-baseline --e2e-iters 2 ;;
+    benchgen) step bench_generic 300 python bench.py --generic --steps 2000 --e2e-iters 0 --no-cpu-baseline ;;
+    benchspec) step bench_spec 300 python bench.py --steps 2000 --e2e-iters 0 --no-cpu-baseline ;;
     benchfast) step bench 300 python bench.py --steps 1000 --cpu-seconds 5 ;;
-    bencha) step bench_a8 400 python bench.py --config a8 --steps 1000 --cpu-seconds 10 ;;
+    bencha) step bench_a8 400 python bench.py --config a8 --steps 1000 --cpu-seconds 10 --e2e-iters 0 ;;
     bencha4) step bench_a4 400 python bench.py --config a4 --steps 1000 --cpu-seconds 5 ;;
-    benchc4) step bench_c4 400 python bench.py --config c4 --steps 1000 --cpu-seconds 10 ;;
+    benchc4) step bench_c4 400 python bench.py --config c4 --steps 1000 --cpu-seconds 10 --e2e-iters 0 ;;
     benchc3) step bench_c3 400 python bench.py --config c3 --steps 2000 --cpu-seconds 10 ;;
     prof)
       export TMPDIR=/tmp
@@ -36,6 +38,7 @@ for s in "$@"; do
       step prof_fetch 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof_fetch -o f --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu-baseline --graph 0 --e2e-iters 0
       step prof_write 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof_write -o w --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu-baseline --graph 0 --e2e-iters 0
       step prof_sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INSTS_LDS -d gpurun_out/prof_sq -o s --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu-baseline --graph 0 --e2e-iters 0
+      rm -f gpurun_out/prof_*/*kernel_trace.csv
       ;;
     profa)
       export TMPDIR=/tmp
@@ -59,6 +62,14 @@ for s in "$@"; do
       ;;
     tunea512)
       step tune_a512 1100 env PYTORCH_TUNABLEOP_ENABLED=1 PYTORCH_TUNABLEOP_TUNING=1 PYTORCH_TUNABLEOP_MAX_TUNING_ITERATIONS=20 PYTORCH_TUNABLEOP_FILENAME=gpurun_out/tunableop_a512_%d.csv python bench.py --config a8 --steps 200 --no-cpu-baseline --e2e-iters 1
+      ;;
+    profc4)
+      export TMPDIR=/tmp
+      step profc4_kt 400 rocprofv3 --kernel-trace --stats -d gpurun_out/profc4_kt -o kt --output-format csv -- python bench.py --config c4 --steps 1000 --no-cpu-baseline --graph 0 --e2e-iters 0
+      step profc4_fetch 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/profc4_fetch -o f --output-format csv -- python bench.py --config c4 --steps 100 --warmup 10 --no-cpu-baseline --graph 0 --e2e-iters 0
+      step profc4_write 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/profc4_write -o w --output-format csv -- python bench.py --config c4 --steps 100 --warmup 10 --no-cpu-baseline --graph 0 --e2e-iters 0
+      step profc4_sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INSTS_LDS -d gpurun_out/profc4_sq -o s --output-format csv -- python bench.py --config c4 --steps 100 --warmup 10 --no-cpu-baseline --graph 0 --e2e-iters 0
+      rm -f gpurun_out/profc4_*/*kernel_trace.csv
       ;;
     stamps) step stamps 300 python tools/phase_stamps.py ;;
     calib)
