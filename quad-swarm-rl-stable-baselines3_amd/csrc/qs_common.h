@@ -47,30 +47,22 @@ struct KP {
     float obst_r, obst_thr, obst_z, sdf_res, quadcol_obst;
 };
 
-// Runtime specialisation (qs_specialize, hipRTC): the whole parameter block is a compile-time constant,
-// so every physical constant folds into the instructions and config branches vanish; only the fields
-// qs_set_param may change after creation are still read from the device block.
+// Runtime specialisation (qs_specialize, hipRTC): the whole parameter block is a compile-time constant
+// object, so every physical constant folds into the instructions and config branches vanish; `kpm`
+// names the fields qs_set_param may change after creation, which are always read from the device block.
 #ifdef QS_JIT
 struct KPWords { uint32_t w[sizeof(KP) / 4]; };
 static_assert(sizeof(KP) % 4 == 0, "KP must be a whole number of words");
-__device__ __forceinline__ KP bind_kp(const KP* __restrict__ p) {
-    constexpr KP c = __builtin_bit_cast(KP, KPWords{{QS_KP_WORDS}});
-    KP k = c;
-    k.ep_len = p->ep_len;
-    k.rew_pos = p->rew_pos;
-    k.rew_effort = p->rew_effort;
-    k.rew_crash = p->rew_crash;
-    k.rew_orient = p->rew_orient;
-    k.rew_spin = p->rew_spin;
-    k.quadcol = p->quadcol;
-    k.prox_max = p->prox_max;
-    k.prox_ratio = p->prox_ratio;
-    k.quadcol_obst = p->quadcol_obst;
-    return k;
-}
-#define QS_BIND_KP(p) const KP kp = bind_kp(p)
+__device__ constexpr KP kKP = __builtin_bit_cast(KP, KPWords{{QS_KP_WORDS}});
+#define QS_BIND_KP(p)    \
+    const KP& kp = kKP;  \
+    const KP& kpm = *(p); \
+    (void)kpm
 #else
-#define QS_BIND_KP(p) const KP& kp = *(p)
+#define QS_BIND_KP(p)    \
+    const KP& kp = *(p); \
+    const KP& kpm = kp;  \
+    (void)kpm
 #endif
 
 struct Bufs {

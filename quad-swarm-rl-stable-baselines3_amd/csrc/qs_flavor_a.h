@@ -446,6 +446,7 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
     bool fin = false, success = eflags & QS_EF_SUCCESS;
     float rw = 0.f, gox = d.goal[0], goy = d.goal[1];
     bool dn = false;
+#pragma unroll 1   // 8 controller ticks: one copy of the body (I-cache), also when kp.ticks is a constant
     for (int sub = 0; sub < kp.ticks; ++sub) {
         if (fin) continue;   // the reference breaks out of its tick loop (:988); segment-uniform
         const Rng rng = env_rng(seed, tick, episode);
@@ -468,7 +469,7 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
         const float captor = cap && capi ? kp.w_captor : 0.f;
         const float helper = cap && capr < rel ? kp.w_helper : 0.f;
         rw = ((0.f + captor) + helper) + kp.existence;
-        dn = cap ? capi : (tick > kp.ep_len);
+        dn = cap ? capi : (tick > kpm.ep_len);
         fin = seg_any<NPAD>(active && dn, base);
         success = success || cap;
         if (repulsive) {   // scenario.step() (:797)

@@ -513,7 +513,7 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     const int episode = b.env[QS_E_EPISODE * kp.E + eidx];
     const Rng rng = env_rng(seed, tick0, episode);
     const int tick = tick0 + 1;
-    const bool done = tick > kp.ep_len;
+    const bool done = tick > kpm.ep_len;
 
     QS_STAMP(1);
     // ---- per-drone control + physics (QuadrotorSingle._step) ----
@@ -530,10 +530,10 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
         // compute_reward_weighted (quadrotor_single.py:34-66)
         const float gx = d.goal[0] - d.pos[0], gy = d.goal[1] - d.pos[1], gz = d.goal[2] - d.pos[2];
         const bool on_floor = d.flags & QS_FL_ON_FLOOR;
-        const float cost = kp.rew_pos * fsqrt(gx * gx + gy * gy + gz * gz) +
-                           kp.rew_effort * fsqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2] + a[3] * a[3]) +
-                           kp.rew_crash * (on_floor ? 1.f : 0.f) + kp.rew_orient * (on_floor ? 1.f : -d.rot[8]) +
-                           kp.rew_spin * fsqrt(d.om[0] * d.om[0] + d.om[1] * d.om[1] + d.om[2] * d.om[2]);
+        const float cost = kpm.rew_pos * fsqrt(gx * gx + gy * gy + gz * gz) +
+                           kpm.rew_effort * fsqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2] + a[3] * a[3]) +
+                           kpm.rew_crash * (on_floor ? 1.f : 0.f) + kpm.rew_orient * (on_floor ? 1.f : -d.rot[8]) +
+                           kpm.rew_spin * fsqrt(d.om[0] * d.om[0] + d.om[1] * d.om[1] + d.om[2] * d.om[2]);
         rw = -kp.dt * cost;
     }
 
@@ -551,7 +551,7 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
             const float dist = fsqrt(dx * dx + dy * dy + dz * dz);
             if (j != di && j < kp.N) {
                 if (dist <= kp.col_thr) cur |= 1ull << j;
-                if (dist <= kp.fall_thr) pen += kp.prox_ratio * dist + kp.prox_max;
+                if (dist <= kp.fall_thr) pen += kpm.prox_ratio * dist + kpm.prox_max;
             }
         }
     }
@@ -561,7 +561,7 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     const uint64_t ub = __ballot(uniq && di != 0);
     const uint64_t gmask = (NPAD == 64) ? ~0ull : ((1ull << NPAD) - 1ull);
     const bool any_uniq = ((ub >> base) & gmask) != 0;
-    rw += kp.quadcol * ((any_uniq && uniq) ? -1.f : 0.f);
+    rw += kpm.quadcol * ((any_uniq && uniq) ? -1.f : 0.f);
     rw += -(kp.cdt * pen);
     // room: new wall / ceiling crashes vs the previous NEW lists (:390-403, :604-605)
     const bool wall_new = (d.flags & QS_FL_CRASH_WALL) && !(d.flags & QS_FL_PREV_WALL);
@@ -574,7 +574,7 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     if (OBST) {
         ohit = obst_detect(kp, myob, d.pos[0], d.pos[1]);
         onew = active && ohit >= 0 && !(d.flags & QS_FL_PREV_OBST);
-        rw += kp.quadcol_obst * (onew ? -1.f : 0.f);
+        rw += kpm.quadcol_obst * (onew ? -1.f : 0.f);
         d.flags = (d.flags & ~(uint32_t)QS_FL_PREV_OBST) | (ohit >= 0 ? (uint32_t)QS_FL_PREV_OBST : 0u);
     }
 
@@ -674,7 +674,7 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
         lds_sync();
         for (int r = 0; r < rows; ++r) {
             const int e = env0 + r / kp.N;
-            if (b.env[QS_E_TICK * kp.E + e] + 1 <= kp.ep_len) continue;
+            if (b.env[QS_E_TICK * kp.E + e] + 1 <= kpm.ep_len) continue;
             for (int c = lane; c < kp.obs_dim; c += 64)
                 b.term[(size_t)(env0 * kp.N + r) * kp.obs_dim + c] = lds[(size_t)r * kp.obs_dim + c];
         }

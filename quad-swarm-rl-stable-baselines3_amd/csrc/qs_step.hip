@@ -800,6 +800,12 @@ extern "C" long long qs_specialize_compile(const qs_config* c) {
     std::vector<char> code;
     std::string ls, lr;
     if (int rc = jit_compile(c, kp, npad_of(c->num_agents), code, ls, lr)) return rc;
+    if (const char* dump = getenv("QS_JIT_DUMP")) {   // diagnostics: write the code object for llvm-objdump
+        if (FILE* f = fopen(dump, "wb")) {
+            fwrite(code.data(), 1, code.size(), f);
+            fclose(f);
+        }
+    }
     return (long long)code.size();
 }
 
