@@ -46,6 +46,7 @@ for s in "$@"; do
       step profa_fetch 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/profa_fetch -o f --output-format csv -- python bench.py --config a8 --steps 100 --warmup 10 --no-cpu-baseline --graph 0 --e2e-iters 0
       step profa_write 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/profa_write -o w --output-format csv -- python bench.py --config a8 --steps 100 --warmup 10 --no-cpu-baseline --graph 0 --e2e-iters 0
       step profa_sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INSTS_LDS -d gpurun_out/profa_sq -o s --output-format csv -- python bench.py --config a8 --steps 100 --warmup 10 --no-cpu-baseline --graph 0 --e2e-iters 0
+      rm -f gpurun_out/profa_*/*kernel_trace.csv
       ;;
     profe2e)
       export TMPDIR=/tmp
