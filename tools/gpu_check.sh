@@ -27,6 +27,9 @@ for s in "$@"; do
     e2ea512) step e2e_a8_512 900 python bench.py --config a8 --steps 500 --no-cpu-baseline --e2e-iters 2 ;;
     benchgen) step bench_generic 300 python bench.py --generic --steps 2000 --e2e-iters 0 --no-cpu-baseline ;;
     benchspec) step bench_spec 300 python bench.py --steps 2000 --e2e-iters 0 --no-cpu-baseline ;;
+    benchc2) step bench_c2 400 python bench.py --config c2 --steps 2000 --cpu-seconds 10 --e2e-iters 1 ;;
+    benchc5) step bench_c5 400 python bench.py --config c5 --steps 1000 --cpu-seconds 10 --e2e-iters 1 ;;
+    e2ea8) step e2e_a8_full 900 python bench.py --config a8 --steps 500 --no-cpu-baseline --e2e-iters 1 ;;
     benchfast) step bench 300 python bench.py --steps 1000 --cpu-seconds 5 ;;
     bencha) step bench_a8 400 python bench.py --config a8 --steps 1000 --cpu-seconds 10 --e2e-iters 0 ;;
     bencha4) step bench_a4 400 python bench.py --config a4 --steps 1000 --cpu-seconds 5 ;;
