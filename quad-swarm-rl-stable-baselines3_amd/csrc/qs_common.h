@@ -47,21 +47,41 @@ struct KP {
     float obst_r, obst_thr, obst_z, sdf_res, quadcol_obst;
 };
 
+// The fields qs_set_param may change after creation, read once per launch into registers (uniform):
+// kernels use `kpm.` for them so that neither build re-loads them inside loops.
+struct KPM {
+    int ep_len;
+    float rew_pos, rew_effort, rew_crash, rew_orient, rew_spin, quadcol, prox_max, prox_ratio, quadcol_obst;
+};
+__device__ __forceinline__ KPM load_kpm(const KP* __restrict__ p) {
+    KPM m;
+    m.ep_len = p->ep_len;
+    m.rew_pos = p->rew_pos;
+    m.rew_effort = p->rew_effort;
+    m.rew_crash = p->rew_crash;
+    m.rew_orient = p->rew_orient;
+    m.rew_spin = p->rew_spin;
+    m.quadcol = p->quadcol;
+    m.prox_max = p->prox_max;
+    m.prox_ratio = p->prox_ratio;
+    m.quadcol_obst = p->quadcol_obst;
+    return m;
+}
+
 // Runtime specialisation (qs_specialize, hipRTC): the whole parameter block is a compile-time constant
-// object, so every physical constant folds into the instructions and config branches vanish; `kpm`
-// names the fields qs_set_param may change after creation, which are always read from the device block.
+// object, so every physical constant folds into the instructions and config branches vanish.
 #ifdef QS_JIT
 struct KPWords { uint32_t w[sizeof(KP) / 4]; };
 static_assert(sizeof(KP) % 4 == 0, "KP must be a whole number of words");
 __device__ constexpr KP kKP = __builtin_bit_cast(KP, KPWords{{QS_KP_WORDS}});
-#define QS_BIND_KP(p)    \
-    const KP& kp = kKP;  \
-    const KP& kpm = *(p); \
+#define QS_BIND_KP(p)               \
+    const KP& kp = kKP;             \
+    const KPM kpm = load_kpm(p);    \
     (void)kpm
 #else
-#define QS_BIND_KP(p)    \
-    const KP& kp = *(p); \
-    const KP& kpm = kp;  \
+#define QS_BIND_KP(p)               \
+    const KP& kp = *(p);            \
+    const KPM kpm = load_kpm(p);    \
     (void)kpm
 #endif
 

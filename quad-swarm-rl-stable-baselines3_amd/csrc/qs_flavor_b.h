@@ -544,14 +544,23 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     xch_put(xch, lane, d.pos, d.vel);
     lds_sync();
     if (kp.N > 1) {
+        // chunks of 8 partners: all LDS reads of a chunk issue back to back, then branch-free tests
+        // (one basic block, so the reads pipeline instead of waiting one by one)
+        constexpr int CH = NPAD < 8 ? NPAD : 8;
 #pragma unroll
-        for (int j = 0; j < NPAD; ++j) {
-            const float4 pj = xch[2 * (base + j)];
-            const float dx = d.pos[0] - pj.x, dy = d.pos[1] - pj.y, dz = d.pos[2] - pj.z;
-            const float dist = fsqrt(dx * dx + dy * dy + dz * dz);
-            if (j != di && j < kp.N) {
-                if (dist <= kp.col_thr) cur |= 1ull << j;
-                if (dist <= kp.fall_thr) pen += kpm.prox_ratio * dist + kpm.prox_max;
+        for (int j0 = 0; j0 < NPAD; j0 += CH) {
+            float4 pj[CH];
+#pragma unroll
+            for (int q = 0; q < CH; ++q) pj[q] = xch[2 * (base + j0 + q)];
+#pragma unroll
+            for (int q = 0; q < CH; ++q) {
+                const int j = j0 + q;
+                const float dx = d.pos[0] - pj[q].x, dy = d.pos[1] - pj[q].y, dz = d.pos[2] - pj[q].z;
+                const float dist = fsqrt(dx * dx + dy * dy + dz * dz);
+                const bool ok = j != di && j < kp.N;
+                cur |= (ok && dist <= kp.col_thr) ? (1ull << j) : 0ull;
+                const float pterm = kpm.prox_ratio * dist + kpm.prox_max;
+                pen += (ok && dist <= kp.fall_thr) ? pterm : 0.f;   // pen >= 0: adding +0 is exact
             }
         }
     }
