@@ -22,7 +22,8 @@ NAMES = ["launch->loads issued", "state loads", "OU+physics+reward", "collisions
 
 
 def main():
-    cfg = QuadSwarmConfig(num_envs=int(os.environ.get("QS_E", 4096)), num_agents=int(os.environ.get("QS_N", 8)))
+    cfg = QuadSwarmConfig(num_envs=int(os.environ.get("QS_E", 4096)), num_agents=int(os.environ.get("QS_N", 8)),
+                          specialize=False)   # the stamps live in the generic kernels of this build
     env = QuadSwarmEnv(cfg)
     env.reset()
     a = torch.rand(env.I, 4, device="cuda") * 2 - 1
