@@ -113,6 +113,13 @@ __device__ uint64_t qs_dbg_stamps[65536 * 16];
         __builtin_amdgcn_sched_barrier(0);                                                            \
         stamps_[k] = t_;                                                                              \
     } while (0)
+// realtime (100 MHz, chip-wide) stamps in slots 12 (wave start) / 13 (wave end) for the launch timeline
+#define QS_RTSTAMP(k)                                                                                 \
+    do {                                                                                              \
+        uint64_t t_;                                                                                  \
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                \
+        stamps_[k] = t_;                                                                              \
+    } while (0)
 #define QS_STAMP_FLUSH()                                                                              \
     do {                                                                                              \
         if (threadIdx.x == 0 && blockIdx.x < 65536)                                                   \
@@ -121,6 +128,7 @@ __device__ uint64_t qs_dbg_stamps[65536 * 16];
 #define QS_STAMP_DECL uint64_t stamps_[16] = {0};
 #else
 #define QS_STAMP(k) do {} while (0)
+#define QS_RTSTAMP(k) do {} while (0)
 #define QS_STAMP_FLUSH() do {} while (0)
 #define QS_STAMP_DECL
 #endif
@@ -168,26 +176,52 @@ __device__ __forceinline__ void load_drone(const KP& kp, const Bufs& b, int g, D
     d.prev = (uint64_t)(uint32_t)is[QS_I_PREV_LO * I] | ((uint64_t)(uint32_t)is[QS_I_PREV_HI * I] << 32);
 }
 
+// Write-through (sc1) stores: the bytes leave the XCD's L2 during the kernel instead of being
+// written back by the end-of-kernel release (MI355X_MICROARCH "boundary": + dirty bytes / 6 TB/s).
+#ifndef QS_WT_OBS
+#define QS_WT_OBS 1
+#endif
+#ifndef QS_WT_STATE
+#define QS_WT_STATE 1
+#endif
+__device__ __forceinline__ void st_wt4(float4* p, float4 v) {
+#if QS_WT_OBS
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    const v4f x = {v.x, v.y, v.z, v.w};
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(x) : "memory");
+#else
+    *p = v;
+#endif
+}
+template <typename T>
+__device__ __forceinline__ void st_state(T* p, T v) {
+#if QS_WT_STATE
+    asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+#else
+    *p = v;
+#endif
+}
+
 __device__ __forceinline__ void store_drone(const KP& kp, const Bufs& b, int g, const Drone& d) {
     float* s = b.st + g;
     const int I = kp.I;
 #pragma unroll
-    for (int i = 0; i < 3; ++i) { s[(QS_F_POS + i) * I] = d.pos[i]; s[(QS_F_VEL + i) * I] = d.vel[i]; }
+    for (int i = 0; i < 3; ++i) { st_state(&s[(QS_F_POS + i) * I], d.pos[i]); st_state(&s[(QS_F_VEL + i) * I], d.vel[i]); }
 #pragma unroll
-    for (int i = 0; i < 9; ++i) s[(QS_F_ROT + i) * I] = d.rot[i];
+    for (int i = 0; i < 9; ++i) st_state(&s[(QS_F_ROT + i) * I], d.rot[i]);
 #pragma unroll
-    for (int i = 0; i < 3; ++i) { s[(QS_F_OMEGA + i) * I] = d.om[i]; s[(QS_F_GOAL + i) * I] = d.goal[i]; }
+    for (int i = 0; i < 3; ++i) { st_state(&s[(QS_F_OMEGA + i) * I], d.om[i]); st_state(&s[(QS_F_GOAL + i) * I], d.goal[i]); }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        s[(QS_F_ROT_DAMP + i) * I] = d.rd[i];
-        s[(QS_F_CMD_DAMP + i) * I] = d.cd[i];
-        s[(QS_F_OU + i) * I] = d.ou[i];
+        st_state(&s[(QS_F_ROT_DAMP + i) * I], d.rd[i]);
+        st_state(&s[(QS_F_CMD_DAMP + i) * I], d.cd[i]);
+        st_state(&s[(QS_F_OU + i) * I], d.ou[i]);
     }
     int32_t* is = b.ist + g;
-    is[QS_I_SVD * I] = d.svd;
-    is[QS_I_FLAGS * I] = (int32_t)d.flags;
-    is[QS_I_PREV_LO * I] = (int32_t)(uint32_t)d.prev;
-    is[QS_I_PREV_HI * I] = (int32_t)(uint32_t)(d.prev >> 32);
+    st_state(&is[QS_I_SVD * I], d.svd);
+    st_state(&is[QS_I_FLAGS * I], (int32_t)d.flags);
+    st_state(&is[QS_I_PREV_LO * I], (int32_t)(uint32_t)d.prev);
+    st_state(&is[QS_I_PREV_HI * I], (int32_t)(uint32_t)(d.prev >> 32));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -358,6 +392,77 @@ __device__ __forceinline__ void substep(const KP& kp, Drone& d, const float* cmd
 __device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // ---------------------------------------------------------------------------------------------
+// sub-lanes: the flavor-B step kernel gives each drone Q consecutive lanes (a quad for Q = 4, a
+// pair for Q = 2).  The drone's physics runs replicated on all Q lanes (bit-identical), while the
+// divisible work -- Philox blocks, partner tests, neighbour candidates -- is dealt over them and
+// exchanged through DPP quad permutes (a VALU modifier: no LDS round trip).  Every helper below
+// must be called with all Q lanes of the drone active (quad-uniform control flow).
+// ---------------------------------------------------------------------------------------------
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int x) { return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xF, 0xF, false); }
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float x) { return __int_as_float(dpp_i<CTRL>(__float_as_int(x))); }
+constexpr int quad_perm(int a, int b, int c, int d) { return a | (b << 2) | (c << 4) | (d << 6); }
+
+// value of sub-lane K of this lane's drone
+template <int Q, int K>
+__device__ __forceinline__ float qbc(float x) {
+    static_assert(K < Q, "sub-lane");
+    if constexpr (Q == 1) return x;
+    else if constexpr (Q == 2) return dpp_f<quad_perm(K, K, 2 + K, 2 + K)>(x);
+    else return dpp_f<quad_perm(K, K, K, K)>(x);
+}
+// sum over the drone's sub-lanes: every lane gets the same bits ((a+b)+(c+d) == (c+d)+(a+b))
+template <int Q>
+__device__ __forceinline__ float qsum(float x) {
+    if constexpr (Q >= 2) x += dpp_f<quad_perm(1, 0, 3, 2)>(x);
+    if constexpr (Q >= 4) x += dpp_f<quad_perm(2, 3, 0, 1)>(x);
+    return x;
+}
+// compile-time walk over the blocks of qdraws: block K lives on sub-lane K % Q, slot K / Q
+template <int Q, int K, int NN, int NU, int T>
+__device__ __forceinline__ void qdraws_gather(const float (&v)[T][4], float* z, float* u) {
+    if constexpr (K < NN + NU) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float x = qbc<Q, K % Q>(v[K / Q][i]);
+            if constexpr (K < NN) z[4 * K + i] = x;
+            else u[4 * (K - NN) + i] = x;
+        }
+        qdraws_gather<Q, K + 1, NN, NU, T>(v, z, u);
+    }
+}
+
+template <int Q>
+__device__ __forceinline__ uint64_t qor(uint64_t m) {
+    int lo = (int)(uint32_t)m, hi = (int)(uint32_t)(m >> 32);
+    if constexpr (Q >= 2) { lo |= dpp_i<quad_perm(1, 0, 3, 2)>(lo); hi |= dpp_i<quad_perm(1, 0, 3, 2)>(hi); }
+    if constexpr (Q >= 4) { lo |= dpp_i<quad_perm(2, 3, 0, 1)>(lo); hi |= dpp_i<quad_perm(2, 3, 0, 1)>(hi); }
+    return (uint64_t)(uint32_t)lo | ((uint64_t)(uint32_t)hi << 32);
+}
+
+// NN normal blocks (stream sn) and NU uniform blocks (stream su | UNIF_BIT) of one Philox key,
+// dealt over the Q sub-lanes (block k on sub-lane k % Q) and broadcast: z[4 NN], u[4 NU] on all of
+// them.  Every lane runs the same Philox + Box-Muller instructions (no divergence on the kind).
+template <int Q, int NN, int NU>
+__device__ __forceinline__ void qdraws(const Rng& r, uint32_t id, uint32_t sn, uint32_t su, int q, float* z, float* u) {
+    constexpr int L = NN + NU, T = (L + Q - 1) / Q;
+    float v[T][4];
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        const int k = q + Q * t;
+        const bool isn = k < NN;
+        const W4 w = block(r, id, isn ? sn : (su | UNIF_BIT), (uint32_t)(isn ? k : k - NN));
+        float n[4];
+        box_muller(w.w[0], w.w[1], n[0], n[1]);
+        box_muller(w.w[2], w.w[3], n[2], n[3]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[t][i] = isn ? n[i] : u01(w.w[i]);
+    }
+    qdraws_gather<Q, 0, NN, NU, T>(v, z, u);
+}
+
+// ---------------------------------------------------------------------------------------------
 // block-level obs staging: LDS tile [rows, obs_dim] -> contiguous global rows
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ void tile_store(const float* lds, float* dst, int nfloat, int lane) {
@@ -367,7 +472,7 @@ __device__ __forceinline__ void tile_store(const float* lds, float* dst, int nfl
         const int nvec = nfloat >> 2;
         const float4* lv = reinterpret_cast<const float4*>(lds);
         float4* dv = reinterpret_cast<float4*>(dst);
-        for (int v = lane; v < nvec; v += 64) dv[v] = lv[v];
+        for (int v = lane; v < nvec; v += 64) st_wt4(dv + v, lv[v]);
         const int t = (nvec << 2) + lane;
         if (t < nfloat) dst[t] = lds[t];
     } else {

@@ -10,13 +10,11 @@ namespace qs {
 // ---------------------------------------------------------------------------------------------
 // sensor noise (add_noise_numba sensor_noise.py:172-218) + state_xyz_vxyz_R_omega[_floor|_wall]
 // (get_state.py:226-292), written to an LDS row.
-__device__ void self_obs(const KP& kp, const Drone& d, const Rng& rng, uint32_t gid, uint32_t stream, float* out) {
+// z = the 12 normals of the stream's blocks 0..2 (drawn by the caller, possibly on other sub-lanes)
+__device__ void self_obs_z(const KP& kp, const Drone& d, const float* z, const Rng& rng, uint32_t gid, uint32_t stream,
+                           float* out) {
     float np_[3], nv[3], no[3], nr[9];
     if (kp.sense) {
-        float z[12];
-        normals4(rng, gid, stream, 0, z);
-        normals4(rng, gid, stream, 1, z + 4);
-        normals4(rng, gid, stream, 2, z + 8);
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
             np_[i] = d.pos[i] + kp.pos_std * z[i];
@@ -36,11 +34,9 @@ __device__ void self_obs(const KP& kp, const Drone& d, const Rng& rng, uint32_t 
                 th[i] = -kp.quat_unif + 2.f * kp.quat_unif * u[6 + i];
             }
         }
-        if (kp.quat_std != 0.f) {
-            float zq[4];
-            normals4(rng, gid, stream, 2, zq);  // normals 9..11 live in block 2, words 1..3
+        if (kp.quat_std != 0.f) {   // normals 9..11 (block 2, words 1..3)
 #pragma unroll
-            for (int i = 0; i < 3; ++i) th[i] = kp.quat_std * zq[1 + i] + th[i];
+            for (int i = 0; i < 3; ++i) th[i] = kp.quat_std * z[9 + i] + th[i];
         }
         // quat_from_small_angle (sensor_noise.py:11-23)
         const float q2 = (th[0] * th[0] + th[1] * th[1] + th[2] * th[2]) * 0.25f;
@@ -103,6 +99,17 @@ __device__ void self_obs(const KP& kp, const Drone& d, const Rng& rng, uint32_t 
     }
 }
 
+__device__ __forceinline__ void self_obs(const KP& kp, const Drone& d, const Rng& rng, uint32_t gid, uint32_t stream,
+                                         float* out) {
+    float z[12];
+    if (kp.sense) {
+        normals4(rng, gid, stream, 0, z);
+        normals4(rng, gid, stream, 1, z + 4);
+        normals4(rng, gid, stream, 2, z + 8);
+    }
+    self_obs_z(kp, d, z, rng, gid, stream, out);
+}
+
 __device__ __forceinline__ void xch_put(float4* xch, int lane, const float* P, const float* V) {
     xch[2 * lane] = make_float4(P[0], P[1], P[2], 0.f);
     xch[2 * lane + 1] = make_float4(V[0], V[1], V[2], 0.f);
@@ -111,41 +118,62 @@ __device__ __forceinline__ void xch_put(float4* xch, int lane, const float* P, c
 // pos_vel neighbour obs: neighborhood_indices (quadrotor_multi.py:344-375) + extend_obs_space
 // clip (:328-342).  Key = |[rel_pos, rel_vel]| clamped at 0.01 (compared squared, clamp 1e-4);
 // stable (index) tie-break like numpy's insertion sort; k == N-1 keeps index order (all keys 0).
-// Reads the exchange tile (caller has synchronised); only lanes with write == true store.
-template <int NPAD>
-__device__ void neighbor_obs(const KP& kp, const float4* xch, int base, int di, const float* P, const float* V,
+// Reads the exchange tile (caller has synchronised).  With Q sub-lanes per drone, sub-lane q owns
+// the candidates j = q + Q t: it builds their keys, gathers the other sub-lanes' keys by DPP, ranks
+// its own candidates and writes those that land among the K nearest.  Only write == true stores.
+template <int NPAD, int Q>
+__device__ void neighbor_obs(const KP& kp, const float4* xch, int dbase, int di, int q, const float* P, const float* V,
                              bool write, float* out) {
-    constexpr bool KEEP = NPAD <= 8;  // small swarms keep the relative vectors in VGPRs between passes
-    float key[NPAD];
-    float rel[KEEP ? NPAD : 1][6];
+    constexpr int PJ = (NPAD + Q - 1) / Q;   // candidates per sub-lane
+    constexpr bool KEEP = PJ <= 8;           // keep the relative vectors in VGPRs between passes
+    float key[PJ];
+    float rel[KEEP ? PJ : 1][6];
     const bool sorted = kp.K < kp.N - 1;
 #pragma unroll
-    for (int j = 0; j < NPAD; ++j) {
-        const float4 pj = xch[2 * (base + j)], vj = xch[2 * (base + j) + 1];
+    for (int t = 0; t < PJ; ++t) {
+        const int j = q + Q * t;
+        const int jj = j < NPAD ? j : NPAD - 1;
+        const float4 pj = xch[2 * (dbase + jj)], vj = xch[2 * (dbase + jj) + 1];
         const float r[6] = {pj.x - P[0], pj.y - P[1], pj.z - P[2], vj.x - V[0], vj.y - V[1], vj.z - V[2]};
         const float s = r[0] * r[0] + r[1] * r[1] + r[2] * r[2] + r[3] * r[3] + r[4] * r[4] + r[5] * r[5];
         const bool valid = (j != di) && (j < kp.N);
-        key[j] = valid ? (sorted ? fmaxf(s, 1e-4f) : 0.f) : __builtin_inff();
+        key[t] = valid ? (sorted ? fmaxf(s, 1e-4f) : 0.f) : __builtin_inff();
         if (KEEP) {
 #pragma unroll
-            for (int c = 0; c < 6; ++c) rel[KEEP ? j : 0][c] = r[c];
+            for (int c = 0; c < 6; ++c) rel[KEEP ? t : 0][c] = r[c];
+        }
+    }
+    float allk[PJ * Q];   // key of candidate m = q' + Q t' (sub-lane q', slot t')
+#pragma unroll
+    for (int t = 0; t < PJ; ++t) {
+        if constexpr (Q == 1) {
+            allk[t] = key[t];
+        } else if constexpr (Q == 2) {
+            allk[2 * t] = qbc<2, 0>(key[t]);
+            allk[2 * t + 1] = qbc<2, 1>(key[t]);
+        } else {
+            allk[4 * t] = qbc<4, 0>(key[t]);
+            allk[4 * t + 1] = qbc<4, 1>(key[t]);
+            allk[4 * t + 2] = qbc<4, 2>(key[t]);
+            allk[4 * t + 3] = qbc<4, 3>(key[t]);
         }
     }
     if (!write) return;
     const float vm = 2.f * kp.vxyz_max;
     const bool pairs = ((kp.so_dim | kp.obs_dim) & 1) == 0;   // 8-byte aligned slots: ds_write_b64
 #pragma unroll
-    for (int j = 0; j < NPAD; ++j) {
+    for (int t = 0; t < PJ; ++t) {
+        const int j = q + Q * t;
         int rank = 0;
 #pragma unroll
-        for (int m = 0; m < NPAD; ++m) rank += (key[m] < key[j]) || (m < j && key[m] == key[j]);
-        if (key[j] != __builtin_inff() && rank < kp.K) {
+        for (int m = 0; m < PJ * Q; ++m) rank += (allk[m] < key[t]) || (m < j && allk[m] == key[t]);
+        if (key[t] != __builtin_inff() && rank < kp.K) {
             float r[6];
             if (KEEP) {
 #pragma unroll
-                for (int c = 0; c < 6; ++c) r[c] = rel[KEEP ? j : 0][c];
+                for (int c = 0; c < 6; ++c) r[c] = rel[KEEP ? t : 0][c];
             } else {
-                const float4 pj = xch[2 * (base + j)], vj = xch[2 * (base + j) + 1];
+                const float4 pj = xch[2 * (dbase + j)], vj = xch[2 * (dbase + j) + 1];
                 r[0] = pj.x - P[0]; r[1] = pj.y - P[1]; r[2] = pj.z - P[2];
                 r[3] = vj.x - V[0]; r[4] = vj.y - V[1]; r[5] = vj.z - V[2];
             }
@@ -181,10 +209,10 @@ __device__ __forceinline__ void new_vel(float maxv, float* v, const float* sh, f
 }
 
 // perform_collision_between_drones (collisions/quadrotors.py:23-59) for the pair (1 = lower id).
-// Both lanes of the pair evaluate it with identical inputs and draws (key = lower drone, stream j).
+// Both drones of the pair evaluate it with identical inputs and draws (key = lower drone, stream j):
+// z = normals 0..27 (blocks 0..6: the 3 rejection tries use normals t*9 .. t*9+8), u = uniforms 0..7.
 __device__ void collide_pair(const float* p1, float* v1, float* w1, const float* p2, float* v2, float* w2,
-                             const Rng& rng, uint32_t gid, uint32_t j) {
-    const uint32_t st = S_PAIR | (j << 8);
+                             const float* z, const float* u) {
     float n[3] = {p1[0] - p2[0], p1[1] - p2[1], p1[2] - p2[2]};
     const float m = fsqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
     const float im = frcp(m == 0.f ? 1e-5f : m);
@@ -194,16 +222,12 @@ __device__ void collide_pair(const float* p1, float* v1, float* w1, const float*
     float vc[3], s1[3], s2[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) { vc[i] = (v2n - v1n) * n[i]; s1[i] = vc[i]; s2[i] = -vc[i]; }
+#pragma unroll
     for (int t = 0; t < 3; ++t) {  // "make sure new vel direction would be opposite" rejection, 3 tries
-        float z[12];  // normals t*9 .. t*9+8 lie in blocks (t*9)/4 .. (t*9+8)/4
-        const uint32_t b0 = (uint32_t)(t * 9) >> 2, off = (uint32_t)(t * 9) & 3;
-        normals4(rng, gid, st, b0, z);
-        normals4(rng, gid, st, b0 + 1, z + 4);
-        normals4(rng, gid, st, b0 + 2, z + 8);
         float d1 = 0.f, d2 = 0.f;
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
-            const float cons = 0.8f * z[off + i], a = 0.15f * z[off + 3 + i], bb = 0.15f * z[off + 6 + i];
+            const float cons = 0.8f * z[t * 9 + i], a = 0.15f * z[t * 9 + 3 + i], bb = 0.15f * z[t * 9 + 6 + i];
             s1[i] = vc[i] + (cons + a);
             s2[i] = -vc[i] + (-cons + bb);
             d1 += (v1[i] + s1[i]) * n[i];
@@ -213,9 +237,6 @@ __device__ void collide_pair(const float* p1, float* v1, float* w1, const float*
     }
     const float mx = fmaxf(fsqrt(v1[0] * v1[0] + v1[1] * v1[1] + v1[2] * v1[2]),
                            fsqrt(v2[0] * v2[0] + v2[1] * v2[1] + v2[2] * v2[2]));
-    float u[8];
-    uniforms4(rng, gid, st, 0, u);
-    uniforms4(rng, gid, st, 1, u + 4);
     new_vel(mx, v1, s1, 0.2f + 0.6f * u[0]);
     new_vel(mx, v2, s2, 0.2f + 0.6f * u[1]);
     // compute_new_omega (collisions/utils.py:23-33), magn_scale 20
@@ -232,13 +253,9 @@ __device__ void collide_pair(const float* p1, float* v1, float* w1, const float*
     }
 }
 
-// perform_collision_with_wall (collisions/room.py:6-44) / _with_ceiling (:91-113)
-__device__ void collide_room(const KP& kp, Drone& d, const Rng& rng, uint32_t gid, bool wall) {
-    const uint32_t st = wall ? S_WALL : S_CEIL;
-    float u[12];
-    uniforms4(rng, gid, st, 0, u);
-    uniforms4(rng, gid, st, 1, u + 4);
-    uniforms4(rng, gid, st, 2, u + 8);
+// perform_collision_with_wall (collisions/room.py:6-44) / _with_ceiling (:91-113); u = uniforms 0..11
+// of stream S_WALL / S_CEIL
+__device__ void collide_room(const KP& kp, Drone& d, const float* u, bool wall) {
     const float sp = fsqrt(d.vel[0] * d.vel[0] + d.vel[1] * d.vel[1] + d.vel[2] * d.vel[2]);
     const float real = clampf(0.2f * sp + (0.8f * sp - 0.2f * sp) * u[0], 0.1f, 6.0f);
     float dir[3] = {-1.f + 2.f * u[1], -1.f + 2.f * u[2], -1.f + 2.f * u[3]};
@@ -427,8 +444,10 @@ __device__ __forceinline__ int obst_detect(const KP& kp, const float2* ob, float
     return -1;
 }
 
-// perform_collision_with_obstacle (collisions/obstacles.py:23-50); Philox indices as the oracle's
-__device__ __forceinline__ void collide_obstacle(const KP& kp, Drone& d, float ox, float oy, const Rng& rng, uint32_t gid) {
+// perform_collision_with_obstacle (collisions/obstacles.py:23-50); Philox indices as the oracle's:
+// z = normals 0..19 of S_OBST (try t uses t*6 .. t*6+5), u = uniforms 0..7
+__device__ __forceinline__ void collide_obstacle(const KP& kp, Drone& d, float ox, float oy, const float* z,
+                                                 const float* u) {
     float n[3] = {d.pos[0] - ox, d.pos[1] - oy, 0.f};
     const float nm = fsqrt(n[0] * n[0] + n[1] * n[1]);
     const float inm = frcp(nm == 0.f ? 1e-5f : nm);
@@ -436,15 +455,12 @@ __device__ __forceinline__ void collide_obstacle(const KP& kp, Drone& d, float o
     const float vm = fsqrt(d.vel[0] * d.vel[0] + d.vel[1] * d.vel[1] + d.vel[2] * d.vel[2]);
     const float nv[3] = {vm * n[0], vm * n[1], 0.f};
     float noise[3] = {0.f, 0.f, 0.f};
+#pragma unroll
     for (int t = 0; t < 3; ++t) {
-        float z[12];
-        const uint32_t b0 = (uint32_t)(t * 6) >> 2, off = (uint32_t)(t * 6) & 3;
-        normals4(rng, gid, S_OBST, b0, z);
-        normals4(rng, gid, S_OBST, b0 + 1, z + 4);
         float tmp[3], dt_ = 0.f;
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-            tmp[c] = 0.1f * z[off + c] + 0.05f * z[off + 3 + c];
+            tmp[c] = 0.1f * z[t * 6 + c] + 0.05f * z[t * 6 + 3 + c];
             dt_ += (nv[c] + tmp[c]) * n[c];
         }
         if (dt_ > 0.f) {
@@ -454,9 +470,6 @@ __device__ __forceinline__ void collide_obstacle(const KP& kp, Drone& d, float o
     }
     const float dz = d.pos[2] - kp.obst_z;
     const bool inside = fsqrt(nm * nm + dz * dz) < kp.obst_r;
-    float u[8];
-    uniforms4(rng, gid, S_OBST, 0, u);
-    uniforms4(rng, gid, S_OBST, 1, u + 4);
     float sh[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) sh[c] = nv[c] - d.vel[c] + noise[c];
@@ -470,38 +483,52 @@ __device__ __forceinline__ void collide_obstacle(const KP& kp, Drone& d, float o
     for (int c = 0; c < 3; ++c) d.om[c] += w[c] * iw * mg;
 }
 
-// LDS: obs tile [64, obs_dim] | exchange tile [64 x 2 float4] | 64 words | obstacle tiles [EPB, M]
-// float2 | obstacle reset scratch [EPB] (shm_bytes() in qs_step.hip sizes it)
-__device__ __forceinline__ float2* obst_tile(float* lds, const KP& kp) {
-    return reinterpret_cast<float2*>(lds + 64 * kp.obs_dim + 64 * 8 + 64);
+// LDS of a launch with `slots` drone rows per workgroup: obs tile [slots, obs_dim] | exchange tile
+// [slots x 2 float4] | 64 words | obstacle tiles [EPB, M] float2 | obstacle reset scratch [EPB]
+// (qs_lds_bytes() in qs_step.hip sizes it)
+__device__ __forceinline__ float2* obst_tile(float* lds, const KP& kp, int slots) {
+    return reinterpret_cast<float2*>(lds + slots * kp.obs_dim + slots * 8 + 64);
 }
+
+// Geometry of the flavor-B step kernel: Q lanes per drone (Q * NPAD <= 64), EPB envs per wave.
+template <int NPAD>
+struct StepGeo {
+    static constexpr int Q = NPAD >= 32 ? 2 : 4;
+    static constexpr int LPE = NPAD * Q;        // lanes per env
+    static constexpr int EPB = 64 / LPE;        // envs per workgroup (one wave)
+    static constexpr int SLOTS = EPB * NPAD;    // drone slots per workgroup
+};
 
 template <int NPAD, bool OBST>
 __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bufs b, uint32_t seed) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     QS_BIND_KP(kpp);
     QS_STAMP_DECL
+    QS_RTSTAMP(12);
     QS_STAMP(0);
-    constexpr int EPB = 64 / NPAD;
+    using G = StepGeo<NPAD>;
+    constexpr int Q = G::Q, LPE = G::LPE, EPB = G::EPB, SLOTS = G::SLOTS;
     const int lane = threadIdx.x;
-    const int el = lane / NPAD, di = lane % NPAD;
+    const int el = lane / LPE, di = (lane % LPE) / Q, q = lane % Q;
     const int env0 = blockIdx.x * EPB;
     const int env = env0 + el;
     const bool active = env < kp.E && di < kp.N;
+    const bool lead = active && q == 0;   // the sub-lane that writes the drone's outputs
     const int g = active ? env * kp.N + di : 0;
     const uint32_t gid = kp.id0 + (uint32_t)g;
-    const int base = el * NPAD;
+    const int lbase = el * LPE;           // first lane of the env
+    const int dbase = el * NPAD;          // first drone slot of the env
     const int nenv_blk = min(EPB, kp.E - env0);
     const int rows = nenv_blk * kp.N;
     float* row = lds + (size_t)(el * kp.N + di) * kp.obs_dim;
-    float4* xch = reinterpret_cast<float4*>(lds + 64 * kp.obs_dim);
-    float2* otile = obst_tile(lds, kp);
+    float4* xch = reinterpret_cast<float4*>(lds + SLOTS * kp.obs_dim);
+    float2* otile = obst_tile(lds, kp, SLOTS);
     ObstScratch* oscr = reinterpret_cast<ObstScratch*>(otile + EPB * kp.M);
     const float2* myob = otile + el * kp.M;
     if (OBST)   // the block's obstacle lists -> LDS (ordered by the first lds_sync below)
-        for (int q = lane; q < nenv_blk * kp.M; q += 64) otile[q] = b.obst[(size_t)env0 * kp.M + q];
+        for (int k = lane; k < nenv_blk * kp.M; k += 64) otile[k] = b.obst[(size_t)env0 * kp.M + k];
 
-    Drone d;
+    Drone d;   // every sub-lane holds the whole drone
     load_drone(kp, b, g, d);
     float a[4];
     {
@@ -515,14 +542,31 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     const int tick = tick0 + 1;
     const bool done = tick > kpm.ep_len;
 
+    // The step's regular draws: Philox block k of {OU 0, sensor 0, sensor 1, sensor 2} on sub-lane
+    // k % Q, slot k / Q -- one block per lane for Q = 4 -- then broadcast by DPP.
+    float zou[4], zs[12];
+    {
+        float zr[4 / Q][4];
+#pragma unroll
+        for (int t = 0; t < 4 / Q; ++t) {
+            const int k = q + Q * t;
+            if (k == 0 || kp.sense) normals4(rng, gid, k == 0 ? S_OU : S_SENSOR, k == 0 ? 0u : (uint32_t)(k - 1), zr[t]);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            zou[i] = qbc<Q, 0>(zr[0][i]);
+            zs[i] = qbc<Q, 1 % Q>(zr[1 / Q][i]);
+            zs[4 + i] = qbc<Q, 2 % Q>(zr[2 / Q][i]);
+            zs[8 + i] = qbc<Q, 3 % Q>(zr[3 / Q][i]);
+        }
+    }
+
     QS_STAMP(1);
-    // ---- per-drone control + physics (QuadrotorSingle._step) ----
+    // ---- per-drone control + physics (QuadrotorSingle._step), replicated on the sub-lanes ----
     float rw = 0.f;
     {
-        float z[4];
-        normals4(rng, gid, S_OU, 0, z);  // OUNoiseNumba.noise, once per control step (:216)
 #pragma unroll
-        for (int k = 0; k < 4; ++k) d.ou[k] = d.ou[k] + (kp.ou_theta * (kp.ou_mu - d.ou[k]) + kp.ou_sigma * z[k]);
+        for (int k = 0; k < 4; ++k) d.ou[k] = d.ou[k] + (kp.ou_theta * (kp.ou_mu - d.ou[k]) + kp.ou_sigma * zou[k]);
         float cmds[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) cmds[k] = 0.5f * (clampf(a[k], -1.f, 1.f) + 1.f);
@@ -541,35 +585,37 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     // ---- swarm phase: collisions + proximity (quadrotor_multi.py:537-568, 608-622) ----
     uint64_t cur = 0;
     float pen = 0.f;
-    xch_put(xch, lane, d.pos, d.vel);
+    if (q == 0) xch_put(xch, dbase + di, d.pos, d.vel);
     lds_sync();
     if (kp.N > 1) {
-        // chunks of 8 partners: all LDS reads of a chunk issue back to back, then branch-free tests
-        // (one basic block, so the reads pipeline instead of waiting one by one)
-        constexpr int CH = NPAD < 8 ? NPAD : 8;
+        // sub-lane q tests the partners j = q + Q t (LDS reads issued back to back, branch-free
+        // tests), then the drone's collision row and proximity sum are reduced over the sub-lanes
+        constexpr int PJ = (NPAD + Q - 1) / Q;
+        float4 pj[PJ];
 #pragma unroll
-        for (int j0 = 0; j0 < NPAD; j0 += CH) {
-            float4 pj[CH];
-#pragma unroll
-            for (int q = 0; q < CH; ++q) pj[q] = xch[2 * (base + j0 + q)];
-#pragma unroll
-            for (int q = 0; q < CH; ++q) {
-                const int j = j0 + q;
-                const float dx = d.pos[0] - pj[q].x, dy = d.pos[1] - pj[q].y, dz = d.pos[2] - pj[q].z;
-                const float dist = fsqrt(dx * dx + dy * dy + dz * dz);
-                const bool ok = j != di && j < kp.N;
-                cur |= (ok && dist <= kp.col_thr) ? (1ull << j) : 0ull;
-                const float pterm = kpm.prox_ratio * dist + kpm.prox_max;
-                pen += (ok && dist <= kp.fall_thr) ? pterm : 0.f;   // pen >= 0: adding +0 is exact
-            }
+        for (int t = 0; t < PJ; ++t) {
+            const int j = q + Q * t;
+            pj[t] = xch[2 * (dbase + (j < NPAD ? j : NPAD - 1))];
         }
+#pragma unroll
+        for (int t = 0; t < PJ; ++t) {
+            const int j = q + Q * t;
+            const float dx = d.pos[0] - pj[t].x, dy = d.pos[1] - pj[t].y, dz = d.pos[2] - pj[t].z;
+            const float dist = fsqrt(dx * dx + dy * dy + dz * dz);
+            const bool ok = j != di && j < kp.N;
+            cur |= (ok && dist <= kp.col_thr) ? (1ull << j) : 0ull;
+            const float pterm = kpm.prox_ratio * dist + kpm.prox_max;
+            pen += (ok && dist <= kp.fall_thr) ? pterm : 0.f;   // pen >= 0: adding +0 is exact
+        }
+        cur = qor<Q>(cur);
+        pen = qsum<Q>(pen);
     }
     const uint64_t newpairs = cur & ~d.prev;
     // setdiff1d(flat(cur), flat(prev)) and its ".any()" (drone 0 alone does not count)
     const bool uniq = active && cur != 0 && d.prev == 0;
-    const uint64_t ub = __ballot(uniq && di != 0);
-    const uint64_t gmask = (NPAD == 64) ? ~0ull : ((1ull << NPAD) - 1ull);
-    const bool any_uniq = ((ub >> base) & gmask) != 0;
+    const uint64_t ub = __ballot(uniq && di != 0 && q == 0);
+    const uint64_t lmask = (LPE == 64) ? ~0ull : ((1ull << LPE) - 1ull);
+    const bool any_uniq = ((ub >> lbase) & lmask) != 0;
     rw += kpm.quadcol * ((any_uniq && uniq) ? -1.f : 0.f);
     rw += -(kp.cdt * pen);
     // room: new wall / ceiling crashes vs the previous NEW lists (:390-403, :604-605)
@@ -588,7 +634,7 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     }
 
     QS_STAMP(3);
-    // ---- random forces (:659-698) ----
+    // ---- random forces (:659-698), replicated on the sub-lanes ----
     bool vchanged = false;
     if (kp.downwash && kp.N > 1) {  // perform_downwash (aerodynamics/downwash.py:4-51)
         float dwu[4];
@@ -596,9 +642,10 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
         const float an = -0.1f + 0.2f * dwu[0], wn = -0.01f + 0.02f * dwu[1];
         const float P0 = d.pos[0], P1 = d.pos[1], P2 = d.pos[2];
         for (int i = 0; i < NPAD; ++i) {
-            const float zi0 = __shfl(d.rot[2], base + i), zi1 = __shfl(d.rot[5], base + i), zi2 = __shfl(d.rot[8], base + i);
-            const float pi0 = __shfl(P0, base + i), pi1 = __shfl(P1, base + i), pi2 = __shfl(P2, base + i);
-            const float ani = __shfl(an, base + i), wni = __shfl(wn, base + i);
+            const int src = lbase + i * Q + q;
+            const float zi0 = __shfl(d.rot[2], src), zi1 = __shfl(d.rot[5], src), zi2 = __shfl(d.rot[8], src);
+            const float pi0 = __shfl(P0, src), pi1 = __shfl(P1, src), pi2 = __shfl(P2, src);
+            const float ani = __shfl(an, src), wni = __shfl(wn, src);
             if (!active || i >= kp.N || i == di) continue;
             const float r0 = P0 - pi0, r1 = P1 - pi1, r2 = P2 - pi2;
             const float dist = fsqrt(r0 * r0 + r1 * r1 + r2 * r2);
@@ -627,38 +674,53 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
         }
     }
     if (kp.collide) {
-        // drone-drone impulses, pairs in (i, j) order; a wave-uniform loop over pending events
+        // drone-drone impulses, pairs in (i, j) order; a wave-uniform loop over pending events.
+        // Ballots read sub-lane 0 of each drone (bit lbase + i * Q).
         uint64_t pend = active ? (newpairs & ~((2ull << di) - 1ull)) : 0ull;
         for (;;) {
-            const uint64_t bal = __ballot(pend != 0ull);
+            const uint64_t bal = __ballot(pend != 0ull && q == 0);
             if (bal == 0ull) break;
-            const uint64_t eb = (bal >> base) & gmask;
-            const int istar = eb ? (__ffsll((long long)eb) - 1) : 0;
+            const uint64_t eb = (bal >> lbase) & lmask;
+            const int istar = eb ? (__ffsll((long long)eb) - 1) / Q : 0;
             const int myj = pend ? (__ffsll((long long)pend) - 1) : 0;
-            const int jstar = __shfl(myj, base + istar);
+            const int jstar = __shfl(myj, lbase + istar * Q);
             const int partner = (di == istar) ? jstar : istar;
             float pp[3], pv[3], pw[3];
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
-                pp[c] = __shfl(d.pos[c], base + partner);
-                pv[c] = __shfl(d.vel[c], base + partner);
-                pw[c] = __shfl(d.om[c], base + partner);
+                pp[c] = __shfl(d.pos[c], lbase + partner * Q + q);
+                pv[c] = __shfl(d.vel[c], lbase + partner * Q + q);
+                pw[c] = __shfl(d.om[c], lbase + partner * Q + q);
             }
             const bool involved = eb != 0 && (di == istar || di == jstar);
             vchanged |= involved;
-            if (involved) {
+            if (involved) {   // both drones' sub-lanes draw the pair's 9 Philox blocks in parallel
                 const uint32_t gi = kp.id0 + (uint32_t)(env * kp.N + istar);
-                if (di == istar) collide_pair(d.pos, d.vel, d.om, pp, pv, pw, rng, gi, (uint32_t)jstar);
-                else collide_pair(pp, pv, pw, d.pos, d.vel, d.om, rng, gi, (uint32_t)jstar);
+                const uint32_t st = S_PAIR | ((uint32_t)jstar << 8);
+                float z[28], u[8];
+                qdraws<Q, 7, 2>(rng, gi, st, st, q, z, u);
+                if (di == istar) collide_pair(d.pos, d.vel, d.om, pp, pv, pw, z, u);
+                else collide_pair(pp, pv, pw, d.pos, d.vel, d.om, z, u);
             }
             if (eb != 0 && di == istar) pend &= ~(1ull << jstar);
         }
         if (OBST && onew) {   // perform_collision_with_obstacle, drones in ascending order (:680-689)
-            collide_obstacle(kp, d, myob[ohit].x, myob[ohit].y, rng, gid);
+            float z[20], u[8];
+            qdraws<Q, 5, 2>(rng, gid, S_OBST, S_OBST, q, z, u);
+            collide_obstacle(kp, d, myob[ohit].x, myob[ohit].y, z, u);
             vchanged = true;
         }
-        if (active && wall_new) collide_room(kp, d, rng, gid, true);
-        if (active && ceil_new) collide_room(kp, d, rng, gid, false);
+        if (active && (wall_new || ceil_new)) {
+            float u[12];
+            if (wall_new) {
+                qdraws<Q, 0, 3>(rng, gid, S_WALL, S_WALL, q, nullptr, u);
+                collide_room(kp, d, u, true);
+            }
+            if (ceil_new) {
+                qdraws<Q, 0, 3>(rng, gid, S_CEIL, S_CEIL, q, nullptr, u);
+                collide_room(kp, d, u, false);
+            }
+        }
         vchanged |= active && (wall_new || ceil_new);
     }
     d.prev = cur;
@@ -668,14 +730,14 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     const bool nbr = kp.neighbor == QS_NEIGHBOR_POS_VEL && kp.K > 0;
     if (nbr && __ballot(vchanged)) {  // impulses changed velocities: refresh the tile
         lds_sync();
-        xch_put(xch, lane, d.pos, d.vel);
+        if (q == 0) xch_put(xch, dbase + di, d.pos, d.vel);
         lds_sync();
     }
     QS_STAMP(5);
-    if (active) self_obs(kp, d, rng, gid, S_SENSOR, row);
+    if (lead) self_obs_z(kp, d, zs, rng, gid, S_SENSOR, row);
     QS_STAMP(6);
-    if (nbr) neighbor_obs<NPAD>(kp, xch, base, di, d.pos, d.vel, active, row);
-    if (OBST && active) sdf_obs(kp, myob, d.pos[0], d.pos[1], row + kp.obs_dim - 9);   // MultiObstacles.step
+    if (nbr) neighbor_obs<NPAD, Q>(kp, xch, dbase, di, q, d.pos, d.vel, active, row);
+    if (OBST && lead) sdf_obs(kp, myob, d.pos[0], d.pos[1], row + kp.obs_dim - 9);   // MultiObstacles.step
     QS_STAMP(7);
 
     const uint64_t dball = __ballot(active && done);
@@ -690,25 +752,27 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
         lds_sync();
         float sv[3] = {d.vel[0], d.vel[1], d.vel[2]};  // QuadrotorEnvMulti.vel seen by the reset (:477)
         if (OBST) {   // new obstacle map + scenario per finished env (one lane each)
-            if (active && done && di == 0)
+            if (active && done && di == 0 && q == 0)
                 obstacle_reset_env(kp, rng, kp.id0 + (uint32_t)(env * kp.N), oscr + el, otile + el * kp.M);
             lds_sync();
         }
-        if (active && done) {
-            b.stale[0 * kp.I + g] = sv[0];
-            b.stale[1 * kp.I + g] = sv[1];
-            b.stale[2 * kp.I + g] = sv[2];
+        if (active && done) {   // replicated: every sub-lane needs the new pose for the neighbour pass
+            if (q == 0) {
+                b.stale[0 * kp.I + g] = sv[0];
+                b.stale[1 * kp.I + g] = sv[1];
+                b.stale[2 * kp.I + g] = sv[2];
+            }
             float spawn[3] = {kp.goal[0], kp.goal[1], kp.goal[2]}, goal[3] = {kp.goal[0], kp.goal[1], kp.goal[2]};
             if (OBST) obstacle_spawn_goal(kp, oscr + el, di, rng, gid, spawn, goal);
             reset_drone(kp, d, rng, gid, spawn, goal);
-            self_obs(kp, d, rng, gid, S_RESET_SENSOR, row);
+            if (q == 0) self_obs(kp, d, rng, gid, S_RESET_SENSOR, row);
         }
         if (nbr) {
-            xch_put(xch, lane, d.pos, sv);
+            if (q == 0) xch_put(xch, dbase + di, d.pos, sv);
             lds_sync();
-            neighbor_obs<NPAD>(kp, xch, base, di, d.pos, sv, active && done, row);
+            neighbor_obs<NPAD, Q>(kp, xch, dbase, di, q, d.pos, sv, active && done, row);
         }
-        if (OBST && active && done) {
+        if (OBST && lead && done) {
             sdf_obs(kp, myob, d.pos[0], d.pos[1], row + kp.obs_dim - 9);   // MultiObstacles.reset
             if (di == 0)
                 for (int o = 0; o < kp.M; ++o) b.obst[(size_t)env * kp.M + o] = myob[o];
@@ -719,7 +783,7 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     tile_store(lds, b.obs + (size_t)env0 * kp.N * kp.obs_dim, rows * kp.obs_dim, lane);
     QS_STAMP(9);
 
-    if (active) {
+    if (lead) {
         store_drone(kp, b, g, d);
         b.rew[g] = rw;
         b.done[g] = done ? 1 : 0;
@@ -733,6 +797,7 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     }
     QS_STAMP(10);
     QS_STAMP(11);
+    QS_RTSTAMP(13);
     QS_STAMP_FLUSH();
 }
 
@@ -761,7 +826,7 @@ __global__ __launch_bounds__(64) void reset_kernel(const KP* __restrict__ kpp, B
     float sv[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) sv[c] = stale_valid ? b.stale[c * kp.I + g] : d.vel[c];
-    float2* otile = obst_tile(lds, kp);
+    float2* otile = obst_tile(lds, kp, 64);
     ObstScratch* oscr = reinterpret_cast<ObstScratch*>(otile + EPB * kp.M);
     if (OBST) {
         if (sel && di == 0) obstacle_reset_env(kp, rng, kp.id0 + (uint32_t)(env * kp.N), oscr + el, otile + el * kp.M);
@@ -777,7 +842,7 @@ __global__ __launch_bounds__(64) void reset_kernel(const KP* __restrict__ kpp, B
         float4* xch = reinterpret_cast<float4*>(lds + 64 * kp.obs_dim);
         xch_put(xch, lane, d.pos, sv);
         lds_sync();
-        neighbor_obs<NPAD>(kp, xch, base, di, d.pos, sv, sel, row);
+        neighbor_obs<NPAD, 1>(kp, xch, base, di, 0, d.pos, sv, sel, row);
     }
     if (OBST && sel) {
         const float2* myob = otile + el * kp.M;

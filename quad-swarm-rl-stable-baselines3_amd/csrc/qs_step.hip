@@ -147,7 +147,7 @@ static int validate(const qs_config* c) {
 }
 
 static int npad_of(int n);
-static size_t shm_bytes(const qs_config& c, int obs_dim, int npad);
+static size_t shm_bytes(const qs_config& c, int obs_dim, int npad, bool step);
 static int neighbor_dim(int t);
 
 static qs_layout make_layout(const qs_config* c) {
@@ -394,7 +394,8 @@ extern "C" int qs_config_default_a(qs_config* c, int32_t num_envs, int32_t num_a
 
 static int check_lds(const qs_config* c) {
     const qs_layout L = make_layout(c);
-    if (shm_bytes(*c, L.obs_dim, npad_of(c->num_agents)) > 65536)
+    const int np = npad_of(c->num_agents);
+    if (shm_bytes(*c, L.obs_dim, np, true) > 65536 || shm_bytes(*c, L.obs_dim, np, false) > 65536)
         return fail(QS_E_UNSUPPORTED, "observation / obstacle tiles exceed 64 KB of LDS per workgroup");
     return QS_OK;
 }
@@ -408,11 +409,19 @@ extern "C" int qs_layout_query(const qs_config* c, qs_layout* out) {
     return QS_OK;
 }
 
-// dynamic LDS of a launch: obs tile + neighbour exchange tile + 64 words (flavor-A flags) + obstacle
-// tiles and per-env reset scratch (qs_flavor_b.h obst_tile)
-static size_t shm_bytes(const qs_config& c, int obs_dim, int npad) {
-    const size_t epb = 64 / (size_t)npad;
-    size_t b = sizeof(float) * 64 * (size_t)obs_dim + sizeof(float) * 64 * 8 + sizeof(float) * 64;
+// Flavor-B step launches give every drone Q lanes (qs::StepGeo); resets and flavor A one lane.
+static int step_lanes_per_drone(int npad) { return npad >= 32 ? 2 : 4; }
+static_assert(qs::StepGeo<8>::Q == 4 && qs::StepGeo<16>::Q == 4 && qs::StepGeo<32>::Q == 2, "step_lanes_per_drone");
+static int envs_per_block(const qs_config& c, int npad, bool step) {
+    const int q = (step && c.flavor != QS_FLAVOR_A) ? step_lanes_per_drone(npad) : 1;
+    return 64 / (npad * q);
+}
+
+// dynamic LDS of a launch with `slots` drone rows per workgroup: obs tile + neighbour exchange tile
+// + 64 words (flavor-A flags) + obstacle tiles and per-env reset scratch (qs_flavor_b.h obst_tile)
+static size_t shm_bytes(const qs_config& c, int obs_dim, int npad, bool step) {
+    const size_t epb = (size_t)envs_per_block(c, npad, step), slots = epb * (size_t)npad;
+    size_t b = sizeof(float) * slots * (size_t)obs_dim + sizeof(float) * slots * 8 + sizeof(float) * 64;
     if (c.use_obstacles) b += epb * (sizeof(float) * 2 * (size_t)c.num_obstacles + (size_t)qs::QS_OBST_SCRATCH);
     return b;
 }
@@ -507,9 +516,9 @@ static int launch(qs_handle* h, bool step, const float* act, const uint8_t* mask
     b.mask = mask;
     const uint32_t seed = h->cfg.seed;
     const qs::KP* kpd = (const qs::KP*)((char*)h->ws + h->lay.params);
-    const int epb = 64 / h->npad;
+    const int epb = envs_per_block(h->cfg, h->npad, step);
     const dim3 grid((unsigned)((h->kp.E + epb - 1) / epb)), block(64);
-    const size_t shm = shm_bytes(h->cfg, h->kp.obs_dim, h->npad);
+    const size_t shm = shm_bytes(h->cfg, h->kp.obs_dim, h->npad, step);
     const bool a = h->cfg.flavor == QS_FLAVOR_A, ob = h->kp.obst != 0;
     if (hipFunction_t f = step ? h->jit_step : h->jit_reset) {
         void* args[] = {(void*)&kpd, (void*)&b, (void*)&seed};
