@@ -262,13 +262,16 @@ __device__ __forceinline__ void substep(const KP& kp, Drone& d, const float* cmd
         d.rd[k] = tau * (fsqrt(cmd) - d.rd[k]) + d.rd[k];
         const float c = clampf(d.rd[k] * d.rd[k] + cmd * noise[k], 0.f, 1.f);
         d.cd[k] = c;
-        thrusts[k] = kp.thrust_max[k] * ((1.f - kp.lin) * c * c + kp.lin * c);
+        // c in [0, 1]: with lin == 1 (every reference config) the quadratic term is exactly +0, so the
+        // branch (folded in specialised builds) changes no bits -- it only drops the 0 * c * c work
+        thrusts[k] = kp.thrust_max[k] * (kp.lin == 1.f ? c : (1.f - kp.lin) * c * c + kp.lin * c);
     }
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {  // torques (:527-533)
-        tq0 += kp.pc0[k] * thrusts[k];
-        tq1 += kp.pc1[k] * thrusts[k];
-        tq2 += kp.pc2[k] * thrusts[k] + kp.torque_max[k] * kp.ccw[k] * d.cd[k];
+    for (int k = 0; k < 4; ++k) {  // torques (:527-533); zero arm coefficients add exactly +-0: skipped
+        if (kp.pc0[k] != 0.f) tq0 += kp.pc0[k] * thrusts[k];
+        if (kp.pc1[k] != 0.f) tq1 += kp.pc1[k] * thrusts[k];
+        if (kp.pc2[k] != 0.f) tq2 += kp.pc2[k] * thrusts[k];
+        tq2 += kp.torque_max[k] * kp.ccw[k] * d.cd[k];
         tsum += thrusts[k];
     }
     float* R = d.rot;
@@ -317,8 +320,10 @@ __device__ __forceinline__ void substep(const KP& kp, Drone& d, const float* cmd
         const float od0 = kp.inv_inertia[0] * (c0 + tq0);
         const float od1 = kp.inv_inertia[1] * (c1 + tq1);
         const float od2 = kp.inv_inertia[2] * (c2 + tq2);
-        const float dm0 = clampf(kp.dq * (o0 * o0), 0.f, 1.f), dm1 = clampf(kp.dq * (o1 * o1), 0.f, 1.f),
-                    dm2 = clampf(kp.dq * (o2 * o2), 0.f, 1.f);
+        // rotational damping (dq = 0 in every reference config: 1 - dm == 1 exactly)
+        const float dm0 = kp.dq != 0.f ? clampf(kp.dq * (o0 * o0), 0.f, 1.f) : 0.f,
+                    dm1 = kp.dq != 0.f ? clampf(kp.dq * (o1 * o1), 0.f, 1.f) : 0.f,
+                    dm2 = kp.dq != 0.f ? clampf(kp.dq * (o2 * o2), 0.f, 1.f) : 0.f;
         d.om[0] = clampf(o0 + (1.f - dm0) * dt * od0, -kp.omega_max, kp.omega_max);
         d.om[1] = clampf(o1 + (1.f - dm1) * dt * od1, -kp.omega_max, kp.omega_max);
         d.om[2] = clampf(o2 + (1.f - dm2) * dt * od2, -kp.omega_max, kp.omega_max);
@@ -363,7 +368,11 @@ __device__ __forceinline__ void substep(const KP& kp, Drone& d, const float* cmd
 #pragma unroll
             for (int i = 0; i < 3; ++i) { d.vel[i] = 0.f; d.om[i] = 0.f; }
             float theta = atan2f(R[3], R[0] + 1e-6f);
-            if (R[8] < 0.f) theta = -3.14159265358979f + 6.28318530717959f * uniform1(rng, gid, S_FLOOR | ((uint32_t)s << 8), 0);
+            if (R[8] < 0.f) {
+                uint32_t gid_ = gid;   // opaque: keeps the Philox key schedule out of the common path
+                asm volatile("" : "+v"(gid_));
+                theta = -3.14159265358979f + 6.28318530717959f * uniform1(rng, gid_, S_FLOOR | ((uint32_t)s << 8), 0);
+            }
             yaw_rot(theta, R);
 #pragma unroll
             for (int k = 0; k < 4; ++k) { d.cd[k] = 0.f; d.rd[k] = 0.f; }
