@@ -37,7 +37,7 @@ for s in "$@"; do
     benchc3) step bench_c3 400 python bench.py --config c3 --steps 2000 --cpu-seconds 10 ;;
     prof)
       export TMPDIR=/tmp
-      step prof_kt 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_kt -o kt --output-format csv -- python bench.py --steps 1000 --no-cpu-baseline --graph 0 --e2e-iters 0
+      step prof_kt 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_kt -o kt --output-format csv -- python bench.py --steps 1000 --no-cpu-baseline --e2e-iters 0
       step prof_fetch 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof_fetch -o f --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu-baseline --graph 0 --e2e-iters 0
       step prof_write 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof_write -o w --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu-baseline --graph 0 --e2e-iters 0
       step prof_sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INSTS_LDS -d gpurun_out/prof_sq -o s --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu-baseline --graph 0 --e2e-iters 0
@@ -45,7 +45,7 @@ for s in "$@"; do
       ;;
     profa)
       export TMPDIR=/tmp
-      step profa_kt 400 rocprofv3 --kernel-trace --stats -d gpurun_out/profa_kt -o kt --output-format csv -- python bench.py --config a8 --steps 1000 --no-cpu-baseline --graph 0 --e2e-iters 0
+      step profa_kt 400 rocprofv3 --kernel-trace --stats -d gpurun_out/profa_kt -o kt --output-format csv -- python bench.py --config a8 --steps 1000 --no-cpu-baseline --e2e-iters 0
       step profa_fetch 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/profa_fetch -o f --output-format csv -- python bench.py --config a8 --steps 100 --warmup 10 --no-cpu-baseline --graph 0 --e2e-iters 0
       step profa_write 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/profa_write -o w --output-format csv -- python bench.py --config a8 --steps 100 --warmup 10 --no-cpu-baseline --graph 0 --e2e-iters 0
       step profa_sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INSTS_LDS -d gpurun_out/profa_sq -o s --output-format csv -- python bench.py --config a8 --steps 100 --warmup 10 --no-cpu-baseline --graph 0 --e2e-iters 0
@@ -69,7 +69,7 @@ for s in "$@"; do
       ;;
     profc4)
       export TMPDIR=/tmp
-      step profc4_kt 400 rocprofv3 --kernel-trace --stats -d gpurun_out/profc4_kt -o kt --output-format csv -- python bench.py --config c4 --steps 1000 --no-cpu-baseline --graph 0 --e2e-iters 0
+      step profc4_kt 400 rocprofv3 --kernel-trace --stats -d gpurun_out/profc4_kt -o kt --output-format csv -- python bench.py --config c4 --steps 1000 --no-cpu-baseline --e2e-iters 0
       step profc4_fetch 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/profc4_fetch -o f --output-format csv -- python bench.py --config c4 --steps 100 --warmup 10 --no-cpu-baseline --graph 0 --e2e-iters 0
       step profc4_write 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/profc4_write -o w --output-format csv -- python bench.py --config c4 --steps 100 --warmup 10 --no-cpu-baseline --graph 0 --e2e-iters 0
       step profc4_sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INSTS_LDS -d gpurun_out/profc4_sq -o s --output-format csv -- python bench.py --config c4 --steps 100 --warmup 10 --no-cpu-baseline --graph 0 --e2e-iters 0
