@@ -47,7 +47,27 @@ class OrParams(ctypes.Structure):
         ("target_vmax", D), ("target_dt", D), ("arena_size", D), ("target_z", D),
         ("use_obstacles", I), ("num_obstacles", I), ("obst_area", I), ("obst_scenario", I),
         ("obst_size", D), ("obst_z", D), ("sdf_resolution", D), ("rew_quadcol_bin_obst", D),
+        ("scenario_b", I),
     ]
+
+
+class OrScen(ctypes.Structure):   # or_scen: the attributes of the reference's Scenario_* object
+    _fields_ = [("mode", I), ("formation", I), ("per_layer", I), ("period", I), ("increase", I),
+                ("size", D), ("lo", D), ("hi", D), ("layer", D), ("speed", D),
+                ("center", D * 3), ("bz", (D * 3) * 3), ("c1", D * 3), ("c2", D * 3)]
+
+
+class OrSDraw(ctypes.Structure):  # or_sdraw: scenario draw source (tape or Philox)
+    _fields_ = [("mode", I), ("seed", ctypes.c_uint32), ("key", ctypes.c_uint32), ("stream", ctypes.c_uint32),
+                ("count", ctypes.c_uint32), ("step", ctypes.c_uint64), ("tape", ctypes.POINTER(D)),
+                ("tape_n", ctypes.c_long), ("tape_pos", ctypes.c_long), ("overrun", I)]
+
+
+# flavor-B scenarios (OR_SC_*): QUADS_MODE_LIST order (scenarios/utils.py:7-10) + run_away; mix = 10
+SC_MODES = ["static_same_goal", "static_diff_goal", "ep_lissajous3D", "ep_rand_bezier", "dynamic_same_goal",
+            "dynamic_diff_goal", "dynamic_formations", "swap_goals", "swarm_vs_swarm", "run_away"]
+SC_NONE, SC_MIX = -1, 10
+S_SCN, S_SCN_RESET = 23, 24
 
 
 class OrDrone(ctypes.Structure):
@@ -66,7 +86,7 @@ class OrEnv(ctypes.Structure):
     _fields_ = [("tick", I), ("episode", ctypes.c_uint32), ("prev_pair_bits", ctypes.c_ubyte * (64 * 64)),
                 ("obs_pos", (D * 3) * 64), ("obs_vel", (D * 3) * 64),
                 ("heading", D * 64), ("target", D * 2), ("capture_radius", D), ("success", I), ("has_pos", I),
-                ("n_obst", I), ("obst", (D * 2) * 64), ("obst_mode", I)]
+                ("n_obst", I), ("obst", (D * 2) * 64), ("obst_mode", I), ("scen", OrScen)]
 
 
 class OrRng(ctypes.Structure):
@@ -133,6 +153,10 @@ def lib():
         L.or_collide_obstacle.argtypes = [P(OrParams), P(OrDrone), P(D), P(OrRng), ctypes.c_uint32]
         L.or_max_square_center.argtypes = [P(ctypes.c_ubyte), I, P(D)]
         L.or_cell_xy.argtypes = [I, I, I, P(D)]
+        L.or_scen_reset.argtypes = [P(OrParams), P(OrScen), P(OrSDraw), P(D)]
+        L.or_scen_step.argtypes = [P(OrParams), P(OrScen), I, P(OrSDraw), P(D)]
+        L.or_generate_goals.argtypes = [I, I, I, D, D, P(D), P(D)]
+        L.or_generate_goals.restype = I
         L.or_philox4x32_10.argtypes = [P(ctypes.c_uint32), P(ctypes.c_uint32), P(ctypes.c_uint32)]
         L.or_philox_normal.argtypes = [ctypes.c_uint32] * 3 + [ctypes.c_uint64, ctypes.c_uint32]
         L.or_philox_normal.restype = D
@@ -249,6 +273,26 @@ class TapeRng:
     @property
     def ref(self):
         return ctypes.byref(self.r)
+
+
+class ScenDraws:
+    """A scenario draw source (or_sdraw): tape mode holds the numpy array alive; Philox mode keys a
+    stream exactly like the GPU (key = env id, stream S_SCN / S_SCN_RESET, counter = env {tick, episode})."""
+
+    def __init__(self, tape=None, seed=0, key=0, stream=S_SCN_RESET, step=0):
+        self.s = OrSDraw()
+        if tape is not None:
+            self.tape = np.ascontiguousarray(tape, dtype=np.float64)
+            self.s.mode = RNG_TAPE
+            self.s.tape = dptr(self.tape)
+            self.s.tape_n = len(self.tape)
+        else:
+            self.s.mode = RNG_PHILOX
+            self.s.seed, self.s.key, self.s.stream, self.s.step = seed, key, stream, step
+
+    @property
+    def ref(self):
+        return ctypes.byref(self.s)
 
 
 def philox_rng(seed, step):

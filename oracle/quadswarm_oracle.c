@@ -141,6 +141,7 @@ void or_polar(double rot[9]) {
 /* ------------------------------------------------------------------------------------------ */
 void or_params_default(or_params* p) {
     memset(p, 0, sizeof *p);
+    p->scenario_b = OR_SC_NONE;
     /* crazyflie_params (quad_models.py:1-42) through QuadLink (inertia.py:182-310):
        values as the reference computes them (checked by tests/test_oracle_golden.py). */
     p->mass = 0.028000000000000008;
@@ -800,6 +801,12 @@ void or_env_reset(const or_params* p, or_drone* drones, or_env* envs, int e, or_
     double spawn[64][3], goal[64][3];
     if (p->use_obstacles) {
         obstacle_reset(p, ev, gbase, r, spawn, goal);
+    } else if (p->scenario_b != OR_SC_NONE) {   /* scenario.reset(); spawn points = goals (:459-472) */
+        or_sdraw sd;
+        memset(&sd, 0, sizeof sd);
+        sd.mode = OR_RNG_PHILOX; sd.seed = r->seed; sd.key = gbase; sd.stream = OR_S_SCN_RESET; sd.step = r->step;
+        or_scen_reset(p, &ev->scen, &sd, goal);
+        memcpy(spawn, goal, sizeof(double) * 3 * (size_t)N);
     } else {
         for (int i = 0; i < N; ++i)
             for (int c = 0; c < 3; ++c) spawn[i][c] = goal[i][c] = p->goal[c];
@@ -949,6 +956,17 @@ void or_env_step(const or_params* p, or_drone* drones, or_env* envs, int e, cons
     for (int i = 0; i < N; ++i)
         for (int j = i + 1; j < N; ++j) ev->prev_pair_bits[i * 64 + j] = cur[i][j];
     for (int i = 0; i < N; ++i) dr[i].prev_obst = ocol[i] >= 0;
+    /* 4. scenario.step() (:700-701): new goals; the observations above keep the old ones unless the
+     * state-update flag makes the reference recompute them below */
+    if (p->scenario_b != OR_SC_NONE && !p->use_obstacles) {
+        or_sdraw sd;
+        memset(&sd, 0, sizeof sd);
+        sd.mode = OR_RNG_PHILOX; sd.seed = r->seed; sd.key = gbase; sd.stream = OR_S_SCN; sd.step = r->step;
+        double g[64][3];
+        for (int i = 0; i < N; ++i) memcpy(g[i], dr[i].goal, sizeof g[i]);
+        or_scen_step(p, &ev->scen, ev->tick, &sd, g);
+        for (int i = 0; i < N; ++i) memcpy(dr[i].goal, g[i], sizeof g[i]);
+    }
     /* 5. refresh and observations (:704-716) */
     for (int i = 0; i < N; ++i)
         for (int c = 0; c < 3; ++c) { ev->obs_pos[i][c] = dr[i].pos[c]; ev->obs_vel[i][c] = dr[i].vel[c]; }

@@ -48,6 +48,9 @@ enum {
     /* obstacles (flavor B) */
     OR_S_OBSTMAP = 21,    /* per env: uniforms 0..M-1 partial Fisher-Yates over the grid cells     */
     OR_S_OSCEN = 22,      /* per env: uniform 0 mode, 1..N spawn cells, N+1..2N goal cells, 2N+1 goal z */
+    /* flavor-B goal scenarios (quadswarm_oracle_scen.c): per env (key = drone 0), one word per draw in call order */
+    OR_S_SCN = 23,        /* scenario.step() draws                                                  */
+    OR_S_SCN_RESET = 24,  /* mix mode + scenario __init__ / reset draws                             */
     OR_UNIF_BIT = 0x80    /* uniform draws use stream | OR_UNIF_BIT           */
 };
 
@@ -129,7 +132,34 @@ typedef struct {
     double obst_z;             /* pillar centre z = room height / 2 (only the 3-D inside test) */
     double sdf_resolution;     /* 0.1                                                      */
     double rew_quadcol_bin_obst;
+    /* ---- flavor-B goal scenarios (scenarios/ files): OR_SC_NONE = the fixed static_same_goal goal ---- */
+    int scenario_b;
 } or_params;
+
+/* flavor-B scenarios, QUADS_MODE_LIST order (scenarios/utils.py:7-10) + run_away; OR_SC_MIX draws one per
+ * reset (scenarios/mix.py) */
+enum { OR_SC_NONE = -1, OR_SC_STATIC_SAME_GOAL = 0, OR_SC_STATIC_DIFF_GOAL, OR_SC_EP_LISSAJOUS3D,
+       OR_SC_EP_RAND_BEZIER, OR_SC_DYNAMIC_SAME_GOAL, OR_SC_DYNAMIC_DIFF_GOAL, OR_SC_DYNAMIC_FORMATIONS,
+       OR_SC_SWAP_GOALS, OR_SC_SWARM_VS_SWARM, OR_SC_RUN_AWAY, OR_SC_MIX };
+
+/* per-env scenario state (the attributes of the reference's Scenario_* object) */
+typedef struct {
+    int mode, formation, per_layer, period, increase;
+    double size, lo, hi, layer, speed;   /* formation_size, lowest/highest_formation_size, layer_dist, control_speed */
+    double center[3];                    /* formation_center                                     */
+    double bz[3][3];                     /* ep_rand_bezier curve nodes (goals[0], new_pos[:, 0], new_pos[:, 1]) */
+    double c1[3], c2[3];                 /* swarm_vs_swarm goal_center_1 / _2                    */
+} or_scen;
+
+/* scenario draw source: tape (reference values in call order) or Philox (see quadswarm_oracle_scen.c) */
+typedef struct {
+    int mode;                            /* OR_RNG_PHILOX / OR_RNG_TAPE */
+    uint32_t seed, key, stream, count;
+    uint64_t step;
+    const double* tape;
+    long tape_n, tape_pos;
+    int overrun;
+} or_sdraw;
 
 /* Per-drone state (QuadrotorDynamics attributes + QuadrotorSingle bookkeeping). */
 typedef struct {
@@ -161,6 +191,7 @@ typedef struct {
     int n_obst;
     double obst[64][2];                      /* MultiObstacles.pos_arr xy, in generation order   */
     int obst_mode;                           /* 0 o_random, 1 o_static_same_goal                 */
+    or_scen scen;                            /* flavor-B goal scenario (p->scenario_b != OR_SC_NONE) */
 } or_env;
 
 /* ---- low level pieces (exported for per-function golden tests) ---- */
@@ -204,6 +235,15 @@ int or_obst_detect(const or_params* p, const or_env* ev, const double xy[2]);
 void or_collide_obstacle(const or_params* p, or_drone* d, const double opos[3], or_rng* r, uint32_t gid);
 void or_max_square_center(const unsigned char* map, int n, double out_xy[2]);
 void or_cell_xy(int row, int col, int n, double out_xy[2]);
+
+/* ---- flavor-B goal scenarios (quadswarm_oracle_scen.c) ---- */
+double or_sd_uniform(or_sdraw* s, double lo, double hi);
+int or_sd_int(or_sdraw* s, int lo, int hi);
+void or_sd_shuffle(or_sdraw* s, double (*g)[3], int n);
+int or_generate_goals(int formation, int n, int per_layer, double size, double layer_dist, const double* center,
+                      double (*g)[3]);
+void or_scen_reset(const or_params* p, or_scen* sc, or_sdraw* s, double (*goals)[3]);
+void or_scen_step(const or_params* p, or_scen* sc, int tick, or_sdraw* s, double (*goals)[3]);
 
 /* ---- flavor A (quadrotor_multi_rewards.QuadrotorEnvMulti) ---- */
 void or_params_default_a(or_params* p);     /* Controller/ModelParams constants, camera, rewards */

@@ -471,6 +471,13 @@ __device__ __forceinline__ void qdraws(const Rng& r, uint32_t id, uint32_t sn, u
     qdraws_gather<Q, 0, NN, NU, T>(v, z, u);
 }
 
+// XCD-aware block order: workgroups are dealt round-robin over the 8 XCDs (block b on XCD b % 8), so
+// consecutive blocks -- whose SoA fields share 128-B lines when a block covers only 64 B of a field --
+// would pull the same line into two L2s.  Hand each XCD a contiguous run of logical blocks instead.
+__device__ __forceinline__ int xcd_block(int b, int nblocks) {
+    return (nblocks & 7) ? b : (b & 7) * (nblocks >> 3) + (b >> 3);
+}
+
 // ---------------------------------------------------------------------------------------------
 // block-level obs staging: LDS tile [rows, obs_dim] -> contiguous global rows
 // ---------------------------------------------------------------------------------------------

@@ -510,7 +510,7 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     constexpr int Q = G::Q, LPE = G::LPE, EPB = G::EPB, SLOTS = G::SLOTS;
     const int lane = threadIdx.x;
     const int el = lane / LPE, di = (lane % LPE) / Q, q = lane % Q;
-    const int env0 = blockIdx.x * EPB;
+    const int env0 = xcd_block((int)blockIdx.x, (int)gridDim.x) * EPB;
     const int env = env0 + el;
     const bool active = env < kp.E && di < kp.N;
     const bool lead = active && q == 0;   // the sub-lane that writes the drone's outputs
