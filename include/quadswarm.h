@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define QS_ABI_VERSION 2
+#define QS_ABI_VERSION 3
 #define QS_MAX_AGENTS 32            /* drones per env: one env lives inside one 64-lane wavefront */
 
 enum qs_status {
@@ -81,6 +81,17 @@ enum qs_scenario {
     QS_SCEN_OBST_MIX = 2,              /* o_random or o_static_same_goal, drawn per reset (mix.py:78-99) */
     QS_SCEN_O_RANDOM = 3,              /* scenarios/obstacles/o_random.py                              */
     QS_SCEN_O_STATIC_SAME_GOAL = 4,    /* scenarios/obstacles/o_static_same_goal.py                    */
+    /* flavor B without obstacles: the goal scenarios of scenarios/ (one .py each), QUADS_MODE_LIST order + run_away */
+    QS_SCEN_MIX = 5,                   /* one of the 9 below (5 for one drone) drawn per reset, mix.py  */
+    QS_SCEN_STATIC_DIFF_GOAL = 6,      /* static_diff_goal.py                                          */
+    QS_SCEN_EP_LISSAJOUS3D = 7,        /* ep_lissajous3D.py                                            */
+    QS_SCEN_EP_RAND_BEZIER = 8,        /* ep_rand_bezier.py                                            */
+    QS_SCEN_DYNAMIC_SAME_GOAL = 9,     /* dynamic_same_goal.py                                         */
+    QS_SCEN_DYNAMIC_DIFF_GOAL = 10,    /* dynamic_diff_goal.py                                         */
+    QS_SCEN_DYNAMIC_FORMATIONS = 11,   /* dynamic_formations.py                                        */
+    QS_SCEN_SWAP_GOALS = 12,           /* swap_goals.py                                                */
+    QS_SCEN_SWARM_VS_SWARM = 13,       /* swarm_vs_swarm.py                                            */
+    QS_SCEN_RUN_AWAY = 14,             /* run_away.py                                                  */
 };
 
 /* Environment + physical configuration.  Physical constants are derived on the host exactly like
@@ -156,7 +167,14 @@ enum qs_drone_flags {
 };
 /* per env: tick, flags, episode.  {tick, episode} is the env's Philox counter: every step and reset
  * of an env draws a fresh stream.  Flavor A counts QuadrotorSingle ticks (8 per step). */
-enum qs_env_field { QS_E_TICK = 0, QS_E_FLAGS = 1, QS_E_EPISODE = 2, QS_NE = 3 };
+enum qs_env_field {
+    QS_E_TICK = 0, QS_E_FLAGS = 1, QS_E_EPISODE = 2,
+    /* flavor-B goal scenario of the env's episode (the reference's Scenario_* attributes): scenario
+     * (QUADS_MODE_LIST index), formation (QUADS_FORMATION_LIST index), control_step_for_sec,
+     * increase_formation_size */
+    QS_E_SC_MODE = 3, QS_E_SC_FORM = 4, QS_E_SC_PERIOD = 5, QS_E_SC_INC = 6,
+    QS_NE = 7
+};
 enum qs_env_flags {
     QS_EF_STALE = 1,                /* stale_vel / QS_F_HEADING hold QuadrotorEnvMulti.vel / .heading */
     QS_EF_SUCCESS = 2,              /* flavor A episode_success (a capture happened this episode)     */
@@ -164,7 +182,14 @@ enum qs_env_flags {
 };
 /* per env float state [QS_NENVF, E] (flavor A): target position of the dynamic_repulsive scenario and
  * the env's capture radius (set_capture_radius acts per env, custom_callbacks.py:455-462) */
-enum qs_env_ffield { QS_ENVF_TARGET_X = 0, QS_ENVF_TARGET_Y = 1, QS_ENVF_CAPTURE = 2, QS_NENVF = 3 };
+enum qs_env_ffield {
+    QS_ENVF_TARGET_X = 0, QS_ENVF_TARGET_Y = 1, QS_ENVF_CAPTURE = 2,
+    /* flavor-B goal scenario: formation_size, lowest/highest_formation_size, layer_dist, control_speed,
+     * formation_center xyz, ep_rand_bezier curve nodes (3 x xyz), swarm_vs_swarm goal centres (2 x xyz) */
+    QS_ENVF_SC_SIZE = 3, QS_ENVF_SC_LO = 4, QS_ENVF_SC_HI = 5, QS_ENVF_SC_LAYER = 6, QS_ENVF_SC_SPEED = 7,
+    QS_ENVF_SC_CENTER = 8, QS_ENVF_SC_BEZIER = 11, QS_ENVF_SC_C1 = 20, QS_ENVF_SC_C2 = 23,
+    QS_NENVF = 26
+};
 
 typedef struct qs_layout {          /* byte offsets inside one workspace allocation */
     size_t params;                  /* kernel parameter block (device copy of the config + runtime params) */

@@ -45,6 +45,8 @@ struct KP {
     // ---- obstacles (flavor B) ----
     int obst, M, obst_n, obst_scen;                 // on, obstacles per env, grid side, scenario
     float obst_r, obst_thr, obst_z, sdf_res, quadcol_obst;
+    // ---- flavor-B goal scenarios: -1 = the fixed static_same_goal goal, 0..9 a scenario, 10 = mix ----
+    int scen_b;
 };
 
 // The fields qs_set_param may change after creation, read once per launch into registers (uniform):

@@ -24,6 +24,8 @@ enum : uint32_t {
     S_RESET_CAM_SEL = 19, S_RESET_SELF_CAM = 20,
     // obstacles: per-env map (partial Fisher-Yates uniforms) and scenario draws (mode, cells, goal z)
     S_OBSTMAP = 21, S_OSCEN = 22,
+    // flavor-B goal scenarios, per env (key = drone 0): one word per draw in call order
+    S_SCN = 23, S_SCN_RESET = 24,
     UNIF_BIT = 0x80
 };
 

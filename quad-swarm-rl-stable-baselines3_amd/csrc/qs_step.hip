@@ -127,8 +127,11 @@ static int validate(const qs_config* c) {
             if (c->num_obstacles < 1 || c->num_obstacles + c->num_agents > c->obst_area * c->obst_area)
                 return fail(QS_E_INVALID, "num_obstacles must leave a free cell per drone");
             if (c->obst_size <= 0.f || c->sdf_resolution <= 0.f) return fail(QS_E_INVALID, "bad obst_size / sdf_resolution");
-        } else if (c->scenario != QS_SCEN_STATIC_SAME_GOAL) {
-            return fail(QS_E_UNSUPPORTED, "flavor B without obstacles implements static_same_goal");
+        } else if (c->scenario != QS_SCEN_STATIC_SAME_GOAL &&
+                   (c->scenario < QS_SCEN_MIX || c->scenario > QS_SCEN_RUN_AWAY)) {
+            return fail(QS_E_UNSUPPORTED, "flavor B without obstacles: static_same_goal, mix or a goal scenario");
+        } else if (c->scenario == QS_SCEN_RUN_AWAY && c->num_agents < 2) {
+            return fail(QS_E_INVALID, "run_away needs at least 2 drones (run_away.py:16-27)");
         }
     } else {
         if (c->use_obstacles) return fail(QS_E_UNSUPPORTED, "flavor A with obstacles is not implemented");
@@ -302,6 +305,10 @@ static qs::KP make_kp(const qs_config* c, const qs_layout& L) {
     k.rew_spin = c->rew_spin; k.quadcol = c->rew_quadcol_bin;
     k.spawn_box = c->spawn_box;
     k.flavor = c->flavor;
+    // goal scenarios (flavor B, no obstacles): QS_SCEN_MIX -> 10, QS_SCEN_STATIC_DIFF_GOAL.. -> 1..9
+    k.scen_b = -1;
+    if (c->flavor == QS_FLAVOR_B && !c->use_obstacles && c->scenario >= QS_SCEN_MIX)
+        k.scen_b = c->scenario == QS_SCEN_MIX ? 10 : c->scenario - QS_SCEN_MIX;
     if (c->flavor == QS_FLAVOR_A) make_kp_a(c, k);
     if (c->use_obstacles) {
         k.obst = 1; k.M = c->num_obstacles; k.obst_n = c->obst_area;
@@ -423,6 +430,8 @@ static size_t shm_bytes(const qs_config& c, int obs_dim, int npad, bool step) {
     const size_t epb = (size_t)envs_per_block(c, npad, step), slots = epb * (size_t)npad;
     size_t b = sizeof(float) * slots * (size_t)obs_dim + sizeof(float) * slots * 8 + sizeof(float) * 64;
     if (c.use_obstacles) b += epb * (sizeof(float) * 2 * (size_t)c.num_obstacles + (size_t)qs::QS_OBST_SCRATCH);
+    else if (c.flavor == QS_FLAVOR_B && c.scenario >= QS_SCEN_MIX)   // goal tables (qs::scen_stride)
+        b += epb * sizeof(float) * 2 * ((size_t)npad + 4) * 4;
     return b;
 }
 

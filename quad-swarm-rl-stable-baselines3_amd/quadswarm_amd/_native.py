@@ -9,7 +9,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("QUADSWARM_LIB", os.path.join(HERE, "lib", "libquadswarm.so"))
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 MAX_AGENTS = 32
 F, I32, U32, U64, SZ = ctypes.c_float, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_size_t
 
@@ -26,14 +26,21 @@ NEIGHBOR = {"none": 0, "pos_vel": 1, "dist_angle": 2, "dist_sangle": 3, "ndist_n
             "dist_sangle_sheading": 6, "pos": 7, "npos": 8}
 NEIGHBOR_DIM = {0: 0, 1: 6, 2: 2, 3: 3, 4: 3, 5: 3, 6: 5, 7: 3, 8: 3}
 SCENARIO = {"static_same_goal": 0, "dynamic_repulsive": 1, "obst_mix": 2, "o_random": 3, "o_static_same_goal": 4}
+# flavor B without obstacles: quads_mode -> qs_scenario (the goal scenarios of gym_art/quadrotor_multi/scenarios/)
+SCENARIO_B = {"static_same_goal": 0, "mix": 5, "static_diff_goal": 6, "ep_lissajous3D": 7, "ep_rand_bezier": 8,
+              "dynamic_same_goal": 9, "dynamic_diff_goal": 10, "dynamic_formations": 11, "swap_goals": 12,
+              "swarm_vs_swarm": 13, "run_away": 14}
 F_POS, F_VEL, F_ROT, F_OMEGA, F_ROT_DAMP, F_CMD_DAMP, F_OU, F_GOAL = 0, 3, 6, 15, 18, 22, 26, 30
 F_PID, F_ANGLE, F_ANGVEL, F_HEADING, NF = 33, 53, 54, 55, 56
 I_SVD, I_FLAGS, I_PREV_LO, I_PREV_HI, NI = 0, 1, 2, 3, 4
 FL_ON_FLOOR, FL_PREV_WALL, FL_PREV_CEIL, FL_CRASH_FLOOR, FL_CRASH_WALL, FL_CRASH_CEIL = 1, 2, 4, 8, 16, 32
 FL_PREV_OBST = 64
-E_TICK, E_FLAGS, E_EPISODE, NE = 0, 1, 2, 3
+E_TICK, E_FLAGS, E_EPISODE = 0, 1, 2
+E_SC_MODE, E_SC_FORM, E_SC_PERIOD, E_SC_INC, NE = 3, 4, 5, 6, 7
 EF_STALE, EF_SUCCESS, EF_HAS_POS = 1, 2, 4
-ENVF_TARGET_X, ENVF_TARGET_Y, ENVF_CAPTURE, NENVF = 0, 1, 2, 3
+ENVF_TARGET_X, ENVF_TARGET_Y, ENVF_CAPTURE = 0, 1, 2
+ENVF_SC_SIZE, ENVF_SC_LO, ENVF_SC_HI, ENVF_SC_LAYER, ENVF_SC_SPEED = 3, 4, 5, 6, 7
+ENVF_SC_CENTER, ENVF_SC_BEZIER, ENVF_SC_C1, ENVF_SC_C2, NENVF = 8, 11, 20, 23, 26
 
 
 class QsConfig(ctypes.Structure):

@@ -163,6 +163,8 @@ class QuadSwarmConfig:
         if self.use_obstacles:
             return {"mix": N.SCENARIO["obst_mix"], "o_random": N.SCENARIO["o_random"],
                     "o_static_same_goal": N.SCENARIO["o_static_same_goal"]}[self.quads_mode]
+        if self.flavor == "B":
+            return N.SCENARIO_B[self.quads_mode]
         return N.SCENARIO[self.quads_mode]
 
     @property
@@ -181,8 +183,11 @@ class QuadSwarmConfig:
             raise NotImplementedError(f"neighbor_obs_type {self.neighbor_obs_type!r} not implemented")
         if self.flavor == "B" and self.neighbor_obs_type not in ("pos_vel", "none"):
             raise NotImplementedError(f"flavor B implements neighbor_obs_type pos_vel / none")
-        if self.flavor == "B" and not self.use_obstacles and self.quads_mode != "static_same_goal":
-            raise NotImplementedError(f"quads_mode {self.quads_mode!r} not implemented for flavor B (static_same_goal)")
+        if self.flavor == "B" and not self.use_obstacles and self.quads_mode not in N.SCENARIO_B:
+            raise NotImplementedError(f"quads_mode {self.quads_mode!r} not implemented for flavor B "
+                                      f"({', '.join(N.SCENARIO_B)})")
+        if self.flavor == "B" and self.quads_mode == "run_away" and self.num_agents < 2:
+            raise ValueError("run_away needs at least 2 drones")
         if self.use_obstacles:
             if self.flavor != "B":
                 raise NotImplementedError("obstacles are implemented for flavor B")
@@ -193,7 +198,7 @@ class QuadSwarmConfig:
             if a[0] != a[1] or int(a[0]) != a[0] or not 1 <= a[0] <= 8:
                 raise NotImplementedError("obst_spawn_area must be a square of 1..8 cells")
         if self.flavor == "A":
-            if self.quads_mode not in N.SCENARIO:
+            if self.quads_mode not in ("dynamic_repulsive", "static_same_goal"):
                 raise NotImplementedError(f"quads_mode {self.quads_mode!r} not implemented for flavor A "
                                           "(dynamic_repulsive, static_same_goal)")
             if self.use_downwash:

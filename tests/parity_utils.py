@@ -55,7 +55,52 @@ def oracle_params(cfg: QuadSwarmConfig):
         p.sdf_resolution = 0.1
         p.rew_quadcol_bin_obst = cfg.obst_collision_reward
         p.spawn_box = 0.1
+    elif cfg.quads_mode != "static_same_goal":   # flavor-B goal scenarios
+        p.scenario_b = O.SC_MIX if cfg.quads_mode == "mix" else O.SC_MODES.index(cfg.quads_mode)
     return p
+
+
+SC_I = ("mode", "formation", "period", "increase")
+SC_F = ("size", "lo", "hi", "layer", "speed")
+
+
+def scen_gpu_to_oracle(env, oenv):
+    """Scenario attributes (env rows QS_E_SC_*, QS_ENVF_SC_*) -> the oracle envs' or_scen."""
+    es = env.env_state.cpu().numpy()
+    ef = env.env_f.double().cpu().numpy()
+    for e in range(env.E):
+        sc = oenv.envs[e].scen
+        for k, n in enumerate(SC_I):
+            setattr(sc, n, int(es[NAT.E_SC_MODE + k, e]))
+        sc.per_layer = 50 if sc.formation in (4, 5, 6) else 8
+        for k, n in enumerate(SC_F):
+            setattr(sc, n, float(ef[NAT.ENVF_SC_SIZE + k, e]))
+        for c in range(3):
+            sc.center[c] = ef[NAT.ENVF_SC_CENTER + c, e]
+            sc.c1[c] = ef[NAT.ENVF_SC_C1 + c, e]
+            sc.c2[c] = ef[NAT.ENVF_SC_C2 + c, e]
+            for j in range(3):
+                sc.bz[j][c] = ef[NAT.ENVF_SC_BEZIER + 3 * j + c, e]
+
+
+def scen_oracle_to_gpu(oenv, env):
+    import torch
+    es = env.env_state.cpu().numpy().copy()
+    ef = env.env_f.cpu().numpy().copy()
+    for e in range(env.E):
+        sc = oenv.envs[e].scen
+        for k, n in enumerate(SC_I):
+            es[NAT.E_SC_MODE + k, e] = getattr(sc, n)
+        for k, n in enumerate(SC_F):
+            ef[NAT.ENVF_SC_SIZE + k, e] = getattr(sc, n)
+        for c in range(3):
+            ef[NAT.ENVF_SC_CENTER + c, e] = sc.center[c]
+            ef[NAT.ENVF_SC_C1 + c, e] = sc.c1[c]
+            ef[NAT.ENVF_SC_C2 + c, e] = sc.c2[c]
+            for j in range(3):
+                ef[NAT.ENVF_SC_BEZIER + 3 * j + c, e] = sc.bz[j][c]
+    env.env_state.copy_(torch.from_numpy(es))
+    env.env_f.copy_(torch.from_numpy(ef))
 
 
 def gpu_to_oracle(env, oenv):

@@ -91,8 +91,23 @@ def test_validation_errors_are_reported():
 def test_config_rejects_unbuilt_or_mixed_flavors():
     with pytest.raises(ValueError):   # a flavor-A repr on a flavor-B env
         QuadSwarmConfig(obs_repr="cdist_cdistdot_dist_distdot_sangle_angledot").to_qs_config()
-    with pytest.raises(NotImplementedError):
-        QuadSwarmConfig(quads_mode="mix").to_qs_config()
+    with pytest.raises(NotImplementedError):   # not in QUADS_MODE_LIST (needs a trajectory csv)
+        QuadSwarmConfig(quads_mode="ep_trajectory").to_qs_config()
+    with pytest.raises(NotImplementedError):   # the goal scenarios are flavor B's
+        QuadSwarmConfig.sb_train(quads_mode="mix").to_qs_config()
+    with pytest.raises(ValueError):
+        QuadSwarmConfig(num_agents=1, quads_mode="run_away").to_qs_config()
+
+
+@pytest.mark.parametrize("mode", sorted(N.SCENARIO_B))
+def test_flavor_b_goal_scenarios_accepted(mode):
+    """Every quads_mode of QUADS_MODE_LIST (+ mix, run_away) builds a flavor-B config; the C side keeps the
+    layout and adds the goal tables to the LDS of the step kernel."""
+    c = QuadSwarmConfig(num_envs=3, num_agents=8, quads_mode=mode).to_qs_config()
+    assert c.scenario == N.SCENARIO_B[mode]
+    lay = N.QsLayout()
+    assert N.lib().qs_layout_query(ctypes.byref(c), ctypes.byref(lay)) == 0
+    assert lay.obs_dim == 54
     with pytest.raises(NotImplementedError):
         QuadSwarmConfig.sb_train(use_downwash=True).to_qs_config()
     with pytest.raises(NotImplementedError):
