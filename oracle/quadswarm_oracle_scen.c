@@ -220,6 +220,7 @@ static void vs_formations(const or_params* p, or_scen* sc, double (*g)[3], int s
 /* ---------------------------------------------------------------------------------------------- */
 void or_scen_reset(const or_params* p, or_scen* sc, or_sdraw* s, double (*g)[3]) {
     const int N = p->num_agents;
+    memset(sc, 0, sizeof *sc);   /* a fresh Scenario_* object per reset (mix.py:88) */
     const double cf = 1.0 / p->control_dt;                 /* control_freq (quadrotor_single.py:160) */
     sc->mode = p->scenario_b == OR_SC_MIX ? or_sd_int(s, 0, N == 1 ? 5 : 9) : p->scenario_b;  /* mix.py:46-56, 82 */
     double tmp[64][3];

@@ -642,6 +642,7 @@ __device__ void sc_vs_formations(const KP& kp, Scen& s, float* g, float* tmp, bo
 // Scenario_mix.reset (mix.py:79-99) -> <scenario>.__init__ + .reset: the N goals into g
 __device__ void scen_reset(const KP& kp, Scen& s, SDraw& sd, float* g, float* tmp) {
     const int N = kp.N;
+    s = Scen{};   // a fresh Scenario_* object per reset (mix.py:88)
     const float cf = 1.f / kp.cdt;
     s.mode = kp.scen_b == SC_MIX ? sd_int(sd, 0, N == 1 ? 5 : 9) : kp.scen_b;
     s.period = (int)(5.f * cf);
