@@ -32,11 +32,14 @@ CONFIGS = {
     "c2": dict(num_envs=16384, num_agents=1, neighbor_visible_num=0, neighbor_obs_type="none"),
     "c3": dict(num_envs=4096, num_agents=8, neighbor_visible_num=6, neighbor_obs_type="pos_vel"),
     "c4": dict(preset="c4", num_envs=4096, num_agents=8),
+    # the reference's own swarm training run (swarm_rl/runs/quad_multi_mix_baseline.py): C3 with quads_mode=mix
+    "c3mix": dict(num_envs=4096, num_agents=8, neighbor_visible_num=6, neighbor_obs_type="pos_vel", quads_mode="mix"),
     "c5": dict(num_envs=1024, num_agents=32, neighbor_visible_num=6, neighbor_obs_type="pos_vel"),
     "a8": dict(flavor="A", num_envs=4096, num_agents=8, initial_capture_radius=0.5),
     "a4": dict(flavor="A", num_envs=8192, num_agents=4, initial_capture_radius=0.5),
 }
 WORKLOAD = {"c2": "single_quad x 16384 envs", "c3": "8-drone swarm static_same_goal x 4096 envs (pos_vel k=6)",
+            "c3mix": "8-drone swarm, quads_mode mix (the 9 goal scenarios of QUADS_MODE_LIST) x 4096 envs (pos_vel k=6)",
             "c4": "8-drone swarm + obstacles x 4096 envs (12 pillars, SDF obs, pos_vel k=2, floor obs, downwash, "
                   "mix of o_random / o_static_same_goal)",
             "c5": "32-drone swarm x 1024 envs per GPU (pos_vel k=6)",
@@ -336,7 +339,7 @@ def main():
             "data": "synthetic: U(-1,1) actions (seed 1234) from a fixed device buffer; Crazyflie constants; "
                     + ("dynamic_repulsive target and spawns (Philox seed 0)" if cfg.flavor == "A" else
                        "random 12-pillar maps + o_random/o_static_same_goal spawns (Philox seed 0)" if cfg.use_obstacles
-                       else "static_same_goal spawns (Philox seed 0)"),
+                       else f"{cfg.quads_mode} goals and spawns (Philox seed 0)"),
             "config": {"workload": WORKLOAD[args.config], "envs_per_gpu": cfg.num_envs,
                        "agents_per_env": cfg.num_agents, "visible_neighbors": cfg.k_neighbors,
                        "obs_dim": cfg.obs_dim, "global_batch": world * I, "parallelism": f"env-shard x{world}",

@@ -35,6 +35,7 @@ for s in "$@"; do
     bencha4) step bench_a4 400 python bench.py --config a4 --steps 1000 --cpu-seconds 5 ;;
     benchc4) step bench_c4 400 python bench.py --config c4 --steps 1000 --cpu-seconds 10 --e2e-iters 0 ;;
     benchc3) step bench_c3 400 python bench.py --config c3 --steps 2000 --cpu-seconds 10 ;;
+    benchmix) step bench_c3mix 400 python bench.py --config c3mix --steps 2000 --cpu-seconds 10 --e2e-iters 0 ;;
     prof)
       export TMPDIR=/tmp
       step prof_kt 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_kt -o kt --output-format csv -- python bench.py --steps 1000 --no-cpu-baseline --e2e-iters 0
