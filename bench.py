@@ -34,12 +34,17 @@ CONFIGS = {
     "c4": dict(preset="c4", num_envs=4096, num_agents=8),
     # the reference's own swarm training run (swarm_rl/runs/quad_multi_mix_baseline.py): C3 with quads_mode=mix
     "c3mix": dict(num_envs=4096, num_agents=8, neighbor_visible_num=6, neighbor_obs_type="pos_vel", quads_mode="mix"),
+    # ... with its experience replay (replay_buffer_sample_prob=0.75, quad_experience_replay.py on device)
+    "c3mixr": dict(num_envs=4096, num_agents=8, neighbor_visible_num=6, neighbor_obs_type="pos_vel", quads_mode="mix",
+                   replay_buffer_sample_prob=0.75),
     "c5": dict(num_envs=1024, num_agents=32, neighbor_visible_num=6, neighbor_obs_type="pos_vel"),
     "a8": dict(flavor="A", num_envs=4096, num_agents=8, initial_capture_radius=0.5),
     "a4": dict(flavor="A", num_envs=8192, num_agents=4, initial_capture_radius=0.5),
 }
 WORKLOAD = {"c2": "single_quad x 16384 envs", "c3": "8-drone swarm static_same_goal x 4096 envs (pos_vel k=6)",
             "c3mix": "8-drone swarm, quads_mode mix (the 9 goal scenarios of QUADS_MODE_LIST) x 4096 envs (pos_vel k=6)",
+            "c3mixr": "8-drone swarm, quads_mode mix x 4096 envs (pos_vel k=6) + experience replay (p=0.75), the "
+                      "reference's swarm run (runs/quad_multi_mix_baseline.py)",
             "c4": "8-drone swarm + obstacles x 4096 envs (12 pillars, SDF obs, pos_vel k=2, floor obs, downwash, "
                   "mix of o_random / o_static_same_goal)",
             "c5": "32-drone swarm x 1024 envs per GPU (pos_vel k=6)",

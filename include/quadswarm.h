@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define QS_ABI_VERSION 3
+#define QS_ABI_VERSION 4
 #define QS_MAX_AGENTS 32            /* drones per env: one env lives inside one 64-lane wavefront */
 
 enum qs_status {
@@ -179,6 +179,10 @@ enum qs_env_flags {
     QS_EF_STALE = 1,                /* stale_vel / QS_F_HEADING hold QuadrotorEnvMulti.vel / .heading */
     QS_EF_SUCCESS = 2,              /* flavor A episode_success (a capture happened this episode)     */
     QS_EF_HAS_POS = 4,              /* drones have been placed once (dynamic_repulsive.py:38 hasattr) */
+    /* written by every flavor-B step, read by the replay kernel: */
+    QS_EF_NEWCOL = 8,               /* last_step_unique_collisions.any() or curr_quad_col non-empty
+                                       (quad_experience_replay.py:161-163) */
+    QS_EF_FLOOR0 = 16,              /* drone 0 on the floor after the step (its rew_crash, quadrotor_multi.py:725) */
 };
 /* per env float state [QS_NENVF, E] (flavor A): target position of the dynamic_repulsive scenario and
  * the env's capture radius (set_capture_radius acts per env, custom_callbacks.py:455-462) */
@@ -265,6 +269,69 @@ long long qs_specialize_compile(const qs_config* cfg);
 /* The kernel parameter block a config produces, as 32-bit words (host only, no device needed).
  * Returns the word count or a negative error. */
 int qs_config_kp_words(const qs_config* cfg, uint32_t* out, size_t n_words);
+
+/* ---- Experience replay on device: ExperienceReplayWrapper + ReplayBuffer
+ *      (gym_art/quadrotor_multi/quad_experience_replay.py:16-216, applied by swarm_rl/env_wrappers/quad_utils.py:68-71
+ *      when replay_buffer_sample_prob > 0; the reference's swarm runs use 0.75) and the env-side bookkeeping it
+ *      reads (quadrotor_multi.py:182-185, 382-388, 461-465, 722-725).  Flavor B.
+ * Per env: a ring of `keep` checkpoints (env snapshot + its obs) saved every cp_every ticks while the env is
+ * active and not a replay; on a new drone/obstacle collision after the grace period the checkpoint
+ * steps_ago back becomes an event of the env's buffer (bufsz slots, replaced round-robin once full); when an
+ * episode ends the env restarts from a random event with probability sample_prob (events replayed max_replays
+ * times are dropped).  Runs as a second kernel inside qs_step / qs_reset once enabled, on the same stream.
+ * Draws: Philox stream S_REPLAY (25) keyed by drone 0 of the env at the env's new {tick, episode}: word 0 is
+ * the sample_prob uniform, word 1 the event index.  A replayed env keeps its new episode counter, so its
+ * noise draws are fresh (the reference's numba RNG is global, not part of the copied env). */
+typedef struct qs_replay_config {
+    float sample_prob;              /* replay_buffer_sample_prob */
+    int32_t buffer_size;            /* ReplayBuffer buffer_size (20, :17)                                   */
+    int32_t keep;                   /* max_episode_checkpoints_to_keep = int(3.0 / cp_step_size) (6, :88)   */
+    int32_t steps_ago;              /* int(save_time_before_collision_sec / cp_step_size) (3, :170)         */
+    int32_t cp_every;               /* cp_step_size_freq = 0.5 s * control_freq, in ticks (50, :20)         */
+    int32_t grace_ticks;            /* collisions_grace_period_seconds * control_freq (150, :163)           */
+    int32_t min_gap_ticks;          /* 5 * control_freq (500, :167)                                          */
+    int32_t max_replays;            /* cleanup() keeps events replayed fewer times (10, :51)                 */
+    int32_t hist_len;               /* crashes_in_recent_episodes maxlen (100, quadrotor_multi.py:184)      */
+    int32_t hist_min;               /* can_drones_fly needs this many episodes (10, :387)                    */
+} qs_replay_config;
+
+/* per-env replay integers [QS_NR, E] */
+enum qs_replay_field {
+    QS_R_ACTIVE = 0,                /* activate_replay_buffer                       */
+    QS_R_SAVED = 1,                 /* saved_in_replay_buffer                       */
+    QS_R_CK_N = 2, QS_R_CK_HEAD = 3,    /* episode_checkpoints: length, next ring slot */
+    QS_R_BUF_N = 4, QS_R_BUF_IDX = 5,   /* len(replay_buffer.buffer), buffer_idx       */
+    QS_R_LAST_ADD = 6,              /* last_tick_added_to_buffer (-1e9 = none)      */
+    QS_R_EPISODES = 7,              /* episode_counter                              */
+    QS_R_REPLAYED = 8,              /* replayed_events                              */
+    QS_R_INDEX_ERR = 9,             /* the reference's IndexError (:171-173), counted */
+    QS_R_HIST_N = 10, QS_R_HIST_HEAD = 11,   /* crashes_in_recent_episodes ring       */
+    QS_R_RESTORED = 12,             /* buffer slot restored by the last call, -1 = none */
+    QS_R_PUSHED = 13,               /* buffer slot written by the last call, -1 = none  */
+    QS_NR = 14
+};
+
+typedef struct qs_replay_buffers {  /* device pointers, valid while replay is enabled */
+    int32_t* ri;                    /* [QS_NR, E]                                                    */
+    double* crash;                  /* [E] crashes_last_episode                                       */
+    double* hist;                   /* [hist_len, E] crashes_in_recent_episodes (ring)                */
+    int32_t* perm;                  /* [buffer_size, E] deque position -> slot (positions >= BUF_N: free) */
+    int32_t* nrep;                  /* [buffer_size, E] num_replayed per slot                          */
+    uint32_t* store;                /* [E, keep + buffer_size, snap_words]: ring slots, then buffer slots */
+    size_t snap_words;              /* words per snapshot: per drone (QS_NF + QS_NI + 3 + obs_dim) fields
+                                       drone-minor, then env ints QS_NE, env floats QS_NENVF, obstacle xy
+                                       2M, obs rows N x obs_dim */
+} qs_replay_buffers;
+
+/* The reference's values for a control period control_dt (quad_experience_replay.py:17-20, 88-92, 163-170). */
+int qs_replay_config_default(qs_replay_config* rc, float control_dt);
+/* Device bytes the replay state of this handle + config needs. */
+int qs_replay_workspace_bytes(qs_handle* h, const qs_replay_config* rc, size_t* bytes);
+/* Initialises the replay state in d_workspace (caller-owned device memory of qs_replay_workspace_bytes,
+ * 256-byte aligned; NULL: the library allocates it).  Replay off again: qs_replay_disable or qs_destroy. */
+int qs_replay_enable(qs_handle* h, const qs_replay_config* rc, void* d_workspace);
+int qs_replay_disable(qs_handle* h);
+int qs_replay_buffers_get(qs_handle* h, qs_replay_buffers* out);
 
 /* Generalized advantage estimation over a device-resident rollout (replaces stable_baselines3
  * RolloutBuffer.compute_returns_and_advantage, the PPO of swarm_rl/sb_train.py:53-64).  Arrays are

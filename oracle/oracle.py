@@ -86,7 +86,8 @@ class OrEnv(ctypes.Structure):
     _fields_ = [("tick", I), ("episode", ctypes.c_uint32), ("prev_pair_bits", ctypes.c_ubyte * (64 * 64)),
                 ("obs_pos", (D * 3) * 64), ("obs_vel", (D * 3) * 64),
                 ("heading", D * 64), ("target", D * 2), ("capture_radius", D), ("success", I), ("has_pos", I),
-                ("n_obst", I), ("obst", (D * 2) * 64), ("obst_mode", I), ("scen", OrScen)]
+                ("n_obst", I), ("obst", (D * 2) * 64), ("obst_mode", I), ("scen", OrScen),
+                ("last_col", I), ("last_floor0", I)]
 
 
 class OrRng(ctypes.Structure):

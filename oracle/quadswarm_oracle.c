@@ -881,6 +881,7 @@ void or_env_step(const or_params* p, or_drone* drones, or_env* envs, int e, cons
         double sum = cost_pos + cost_effort;
         sum += cost_crash; sum += cost_orient; sum += cost_spin;
         rw[i] = -p->dt * sum;
+        if (i == 0) ev->last_floor0 = d->on_floor;
         self_obs(p, d, r, gid, OR_S_SENSOR, o + (size_t)i * od);
         for (int c = 0; c < 3; ++c) ev->obs_pos[i][c] = d->pos[c];
     }
@@ -927,6 +928,8 @@ void or_env_step(const or_params* p, or_drone* drones, or_env* envs, int e, cons
         ocol[i] = p->use_obstacles ? or_obst_detect(p, ev, ev->obs_pos[i]) : -1;
         onew[i] = ocol[i] >= 0 && !dr[i].prev_obst;
     }
+    ev->last_col = any_nonzero;
+    for (int i = 0; i < N; ++i) if (onew[i]) ev->last_col = 1;
     for (int i = 0; i < N; ++i) {
         double rc = (any_nonzero && in_cur[i] && !in_prev[i]) ? -1.0 : 0.0;
         rw[i] += p->rew_quadcol_bin * rc;

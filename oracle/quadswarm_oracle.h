@@ -192,6 +192,9 @@ typedef struct {
     double obst[64][2];                      /* MultiObstacles.pos_arr xy, in generation order   */
     int obst_mode;                           /* 0 o_random, 1 o_static_same_goal                 */
     or_scen scen;                            /* flavor-B goal scenario (p->scenario_b != OR_SC_NONE) */
+    /* what the experience-replay wrapper reads of the last step (quad_experience_replay.py:161-163,
+     * quadrotor_multi.py:725): a new drone collision (.any() of the ids) or obstacle hit; drone 0 on the floor */
+    int last_col, last_floor0;
 } or_env;
 
 /* ---- low level pieces (exported for per-function golden tests) ---- */

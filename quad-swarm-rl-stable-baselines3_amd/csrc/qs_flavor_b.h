@@ -934,6 +934,7 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     QS_STAMP(1);
     // ---- per-drone control + physics (QuadrotorSingle._step), replicated on the sub-lanes ----
     float rw = 0.f;
+    bool floor_now = false;   // drone 0's on the env's flags: its rew_crash feeds the replay wrapper
     {
 #pragma unroll
         for (int k = 0; k < 4; ++k) d.ou[k] = d.ou[k] + (kp.ou_theta * (kp.ou_mu - d.ou[k]) + kp.ou_sigma * zou[k]);
@@ -944,6 +945,7 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
         // compute_reward_weighted (quadrotor_single.py:34-66)
         const float gx = d.goal[0] - d.pos[0], gy = d.goal[1] - d.pos[1], gz = d.goal[2] - d.pos[2];
         const bool on_floor = d.flags & QS_FL_ON_FLOOR;
+        floor_now = on_floor;
         const float cost = kpm.rew_pos * fsqrt(gx * gx + gy * gy + gz * gz) +
                            kpm.rew_effort * fsqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2] + a[3] * a[3]) +
                            kpm.rew_crash * (on_floor ? 1.f : 0.f) + kpm.rew_orient * (on_floor ? 1.f : -d.rot[8]) +
@@ -1002,6 +1004,8 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
         rw += kpm.quadcol_obst * (onew ? -1.f : 0.f);
         d.flags = (d.flags & ~(uint32_t)QS_FL_PREV_OBST) | (ohit >= 0 ? (uint32_t)QS_FL_PREV_OBST : 0u);
     }
+    bool any_onew = false;   // curr_quad_col non-empty (quadrotor_multi.py:576)
+    if (OBST) any_onew = ((__ballot(onew && q == 0) >> lbase) & lmask) != 0;
 
     QS_STAMP(3);
     // ---- random forces (:659-698), replicated on the sub-lanes ----
@@ -1205,7 +1209,10 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
             b.env[QS_E_TICK * kp.E + env] = done ? 0 : tick;
             if (done) b.env[QS_E_EPISODE * kp.E + env] = episode + 1;
             const int32_t ef = b.env[QS_E_FLAGS * kp.E + env];
-            const int32_t nf = done ? (ef | 1) : (ef & ~1);
+            int32_t nf = done ? (ef | QS_EF_STALE) : (ef & ~QS_EF_STALE);
+            // what the replay wrapper reads of this step (quad_experience_replay.py:161-163, quadrotor_multi.py:725)
+            nf = (nf & ~(QS_EF_NEWCOL | QS_EF_FLOOR0)) | ((any_uniq || any_onew) ? QS_EF_NEWCOL : 0) |
+                 (floor_now ? QS_EF_FLOOR0 : 0);
             if (nf != ef) b.env[QS_E_FLAGS * kp.E + env] = nf;
         }
     }

@@ -37,6 +37,7 @@
 #include "qs_flavor_b.h"
 #include "qs_flavor_a.h"
 #include "qs_gae.h"
+#include "qs_replay.h"
 
 // =============================================================================================
 // C ABI
@@ -51,6 +52,11 @@ struct qs_handle {
     int npad;
     hipFunction_t jit_step = nullptr;    // qs_specialize: kernels compiled for this handle's parameters
     hipFunction_t jit_reset = nullptr;
+    // experience replay (qs_replay_enable): one device allocation holding every RBufs array
+    void* rws = nullptr;
+    bool rws_owned = false;
+    qs::RBufs rb{};
+    qs::RP rp{};
 };
 
 static thread_local std::string g_err;
@@ -480,8 +486,15 @@ extern "C" int qs_create(const qs_config* c, int dev, void* ws, qs_handle** out)
     return QS_OK;
 }
 
+static void replay_free(qs_handle* h) {
+    if (h->rws && h->rws_owned) (void)hipFree(h->rws);
+    h->rws = nullptr;
+    h->rb = qs::RBufs{};
+}
+
 extern "C" int qs_destroy(qs_handle* h) {
     if (!h) return QS_OK;
+    replay_free(h);
     if (h->owns_ws && h->ws) {
         hipError_t e = hipFree(h->ws);
         delete h;
@@ -562,10 +575,159 @@ static int launch(qs_handle* h, bool step, const float* act, const uint8_t* mask
     return QS_OK;
 }
 
+// the replay wavefront per env after the step / reset kernel (qs_replay.h)
+static int launch_replay(qs_handle* h, bool step, const uint8_t* mask, hipStream_t s) {
+    qs::Bufs b = bufs_of(h);
+    b.mask = mask;
+    const qs::KP* kpd = (const qs::KP*)((char*)h->ws + h->lay.params);
+    const dim3 grid((unsigned)((h->kp.E + 3) / 4)), block(256);
+    if (step) hipLaunchKernelGGL(qs::replay_kernel<true>, grid, block, 0, s, kpd, b, h->rb, h->rp, h->cfg.seed);
+    else hipLaunchKernelGGL(qs::replay_kernel<false>, grid, block, 0, s, kpd, b, h->rb, h->rp, h->cfg.seed);
+    QS_HIP(hipGetLastError());
+    return QS_OK;
+}
+
+static size_t snap_words(const qs_config* c, int obs_dim) {
+    const size_t N = (size_t)c->num_agents;
+    return N * (QS_NF + QS_NI + 3 + (size_t)obs_dim) + QS_NE + QS_NENVF +
+           (c->use_obstacles ? 2 * (size_t)c->num_obstacles : 0);
+}
+
+extern "C" int qs_replay_config_default(qs_replay_config* rc, float control_dt) {
+    if (!rc || !(control_dt > 0.f)) return fail(QS_E_INVALID, "NULL config or control_dt <= 0");
+    const double freq = 1.0 / (double)control_dt;      // control_freq (quadrotor_single.py: sim_freq / sim_steps)
+    rc->sample_prob = 0.75f;                           // the reference's runs (runs/quad_multi_mix_baseline.py:17)
+    rc->buffer_size = 20;
+    rc->keep = 6;                                      // int(3.0 / 0.5)
+    rc->steps_ago = 3;                                 // int(1.5 / 0.5)
+    rc->cp_every = (int32_t)llround(0.5 * freq);
+    rc->grace_ticks = (int32_t)floor(1.5 * freq + 1e-9);
+    rc->min_gap_ticks = (int32_t)floor(5.0 * freq + 1e-9);
+    rc->max_replays = 10;
+    rc->hist_len = 100;
+    rc->hist_min = 10;
+    return QS_OK;
+}
+
+struct ReplayOffsets { size_t ri, crash, hist, perm, nrep, store, total; };
+static ReplayOffsets replay_offsets(const qs_handle* h, const qs_replay_config* rc) {
+    const size_t E = (size_t)h->cfg.num_envs, W = snap_words(&h->cfg, h->lay.obs_dim);
+    const size_t slots = (size_t)rc->keep + (size_t)rc->buffer_size;
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    ReplayOffsets o;
+    o.ri = 0;
+    o.crash = al(o.ri + 4 * QS_NR * E);
+    o.hist = al(o.crash + 8 * E);
+    o.perm = al(o.hist + 8 * (size_t)rc->hist_len * E);
+    o.nrep = al(o.perm + 4 * (size_t)rc->buffer_size * E);
+    o.store = al(o.nrep + 4 * (size_t)rc->buffer_size * E);
+    o.total = al(o.store + 4 * E * slots * W);
+    return o;
+}
+
+static int replay_check(const qs_handle* h, const qs_replay_config* rc) {
+    if (!h || !rc) return fail(QS_E_INVALID, "NULL argument");
+    if (h->cfg.flavor != QS_FLAVOR_B) return fail(QS_E_UNSUPPORTED, "experience replay is implemented for flavor B");
+    if (rc->buffer_size < 1 || rc->buffer_size > 1024 || rc->keep < 1 || rc->keep > 1024 || rc->steps_ago < 1 ||
+        rc->cp_every < 1 || rc->max_replays < 1 || rc->hist_len < 1 || rc->hist_len > 4096 || rc->hist_min < 0 ||
+        !(rc->sample_prob >= 0.f && rc->sample_prob <= 1.f))
+        return fail(QS_E_INVALID, "replay config out of range");
+    return QS_OK;
+}
+
+extern "C" int qs_replay_workspace_bytes(qs_handle* h, const qs_replay_config* rc, size_t* bytes) {
+    int r = replay_check(h, rc);
+    if (r) return r;
+    if (!bytes) return fail(QS_E_INVALID, "NULL argument");
+    *bytes = replay_offsets(h, rc).total;
+    return QS_OK;
+}
+
+extern "C" int qs_replay_enable(qs_handle* h, const qs_replay_config* rc, void* d_workspace) {
+    int r = replay_check(h, rc);
+    if (r) return r;
+    if (d_workspace && ((uintptr_t)d_workspace & 255) != 0) return fail(QS_E_INVALID, "workspace must be 256-byte aligned");
+    QS_HIP(hipSetDevice(h->device));
+    QS_HIP(hipDeviceSynchronize());
+    replay_free(h);
+    const size_t E = (size_t)h->cfg.num_envs, W = snap_words(&h->cfg, h->lay.obs_dim);
+    const ReplayOffsets off = replay_offsets(h, rc);
+    hipError_t e = hipSuccess;
+    if (d_workspace) {
+        h->rws = d_workspace;
+        h->rws_owned = false;
+    } else {
+        e = hipMalloc(&h->rws, off.total);
+        if (e != hipSuccess) { h->rws = nullptr; return fail(QS_E_HIP, std::string("hipMalloc(replay): ") + hipGetErrorString(e)); }
+        h->rws_owned = true;
+    }
+    const size_t total = off.total;
+    const size_t o_ri = off.ri, o_crash = off.crash, o_hist = off.hist, o_perm = off.perm, o_nrep = off.nrep,
+                 o_store = off.store;
+    char* w = (char*)h->rws;
+    h->rb.ri = (int32_t*)(w + o_ri);
+    h->rb.crash = (double*)(w + o_crash);
+    h->rb.hist = (double*)(w + o_hist);
+    h->rb.perm = (int32_t*)(w + o_perm);
+    h->rb.nrep = (int32_t*)(w + o_nrep);
+    h->rb.store = (uint32_t*)(w + o_store);
+    h->rp.prob = rc->sample_prob;
+    h->rp.bufsz = rc->buffer_size;
+    h->rp.keep = rc->keep;
+    h->rp.steps_ago = rc->steps_ago;
+    h->rp.cp_every = rc->cp_every;
+    h->rp.grace = rc->grace_ticks;
+    h->rp.gap = rc->min_gap_ticks;
+    h->rp.max_rep = rc->max_replays;
+    h->rp.hist_len = rc->hist_len;
+    h->rp.hist_min = rc->hist_min;
+    h->rp.W = (int)W;
+    // initial wrapper state: identity deque map, no last add, no restore / push yet
+    std::vector<int32_t> ri((size_t)QS_NR * E, 0), perm((size_t)rc->buffer_size * E);
+    for (size_t x = 0; x < E; ++x) {
+        ri[QS_R_LAST_ADD * E + x] = qs::LAST_ADD_NONE;
+        ri[QS_R_RESTORED * E + x] = -1;
+        ri[QS_R_PUSHED * E + x] = -1;
+    }
+    for (int p = 0; p < rc->buffer_size; ++p)
+        for (size_t x = 0; x < E; ++x) perm[(size_t)p * E + x] = p;
+    e = hipMemset(h->rws, 0, total);
+    if (e == hipSuccess) e = hipMemcpy(h->rb.ri, ri.data(), 4 * ri.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(h->rb.perm, perm.data(), 4 * perm.size(), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        replay_free(h);
+        return fail(QS_E_HIP, std::string("replay init: ") + hipGetErrorString(e));
+    }
+    return QS_OK;
+}
+
+extern "C" int qs_replay_disable(qs_handle* h) {
+    if (!h) return fail(QS_E_INVALID, "handle is NULL");
+    QS_HIP(hipSetDevice(h->device));
+    QS_HIP(hipDeviceSynchronize());
+    replay_free(h);
+    return QS_OK;
+}
+
+extern "C" int qs_replay_buffers_get(qs_handle* h, qs_replay_buffers* o) {
+    if (!h || !o) return fail(QS_E_INVALID, "NULL argument");
+    if (!h->rws) return fail(QS_E_INVALID, "replay is not enabled");
+    o->ri = h->rb.ri;
+    o->crash = h->rb.crash;
+    o->hist = h->rb.hist;
+    o->perm = h->rb.perm;
+    o->nrep = h->rb.nrep;
+    o->store = h->rb.store;
+    o->snap_words = (size_t)h->rp.W;
+    return QS_OK;
+}
+
 extern "C" int qs_reset(qs_handle* h, const uint8_t* d_mask, void* stream) {
     if (!h) return fail(QS_E_INVALID, "handle is NULL");
     QS_HIP(hipSetDevice(h->device));
-    return launch(h, false, nullptr, d_mask, (hipStream_t)stream);
+    int rc = launch(h, false, nullptr, d_mask, (hipStream_t)stream);
+    if (rc == QS_OK && h->rws) rc = launch_replay(h, false, d_mask, (hipStream_t)stream);
+    return rc;
 }
 
 extern "C" int qs_step(qs_handle* h, const float* d_actions, void* stream) {
@@ -576,7 +738,9 @@ extern "C" int qs_step(qs_handle* h, const float* d_actions, void* stream) {
         return fail(QS_E_INVALID, "actions must be 16-byte aligned [I,4] fp32");
     }
     QS_HIP(hipSetDevice(h->device));
-    return launch(h, true, d_actions, nullptr, (hipStream_t)stream);
+    int rc = launch(h, true, d_actions, nullptr, (hipStream_t)stream);
+    if (rc == QS_OK && h->rws) rc = launch_replay(h, true, nullptr, (hipStream_t)stream);
+    return rc;
 }
 
 static float* param_slot(qs_handle* h, const char* key) {

@@ -9,7 +9,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("QUADSWARM_LIB", os.path.join(HERE, "lib", "libquadswarm.so"))
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 MAX_AGENTS = 32
 F, I32, U32, U64, SZ = ctypes.c_float, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_size_t
 
@@ -37,7 +37,7 @@ FL_ON_FLOOR, FL_PREV_WALL, FL_PREV_CEIL, FL_CRASH_FLOOR, FL_CRASH_WALL, FL_CRASH
 FL_PREV_OBST = 64
 E_TICK, E_FLAGS, E_EPISODE = 0, 1, 2
 E_SC_MODE, E_SC_FORM, E_SC_PERIOD, E_SC_INC, NE = 3, 4, 5, 6, 7
-EF_STALE, EF_SUCCESS, EF_HAS_POS = 1, 2, 4
+EF_STALE, EF_SUCCESS, EF_HAS_POS, EF_NEWCOL, EF_FLOOR0 = 1, 2, 4, 8, 16
 ENVF_TARGET_X, ENVF_TARGET_Y, ENVF_CAPTURE = 0, 1, 2
 ENVF_SC_SIZE, ENVF_SC_LO, ENVF_SC_HI, ENVF_SC_LAYER, ENVF_SC_SPEED = 3, 4, 5, 6, 7
 ENVF_SC_CENTER, ENVF_SC_BEZIER, ENVF_SC_C1, ENVF_SC_C2, NENVF = 8, 11, 20, 23, 26
@@ -80,6 +80,20 @@ class QsBuffers(ctypes.Structure):
                                                "rew", "done", "reset_info")]
 
 
+class QsReplayConfig(ctypes.Structure):
+    _fields_ = [("sample_prob", F), ("buffer_size", I32), ("keep", I32), ("steps_ago", I32), ("cp_every", I32),
+                ("grace_ticks", I32), ("min_gap_ticks", I32), ("max_replays", I32), ("hist_len", I32), ("hist_min", I32)]
+
+
+class QsReplayBuffers(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("ri", "crash", "hist", "perm", "nrep", "store")] + [("snap_words", SZ)]
+
+
+# qs_replay_field
+R_ACTIVE, R_SAVED, R_CK_N, R_CK_HEAD, R_BUF_N, R_BUF_IDX, R_LAST_ADD, R_EPISODES, R_REPLAYED, R_INDEX_ERR = range(10)
+R_HIST_N, R_HIST_HEAD, R_RESTORED, R_PUSHED, NR = 10, 11, 12, 13, 14
+
+
 class QuadSwarmError(RuntimeError):
     pass
 
@@ -89,7 +103,8 @@ EXPORTS = ["qs_abi_version", "qs_last_error", "qs_struct_sizes", "qs_config_defa
            "qs_layout_query", "qs_create", "qs_destroy",
            "qs_buffers_get", "qs_reset", "qs_step", "qs_set_param",
            "qs_get_param", "qs_state_bytes", "qs_get_state", "qs_set_state", "qs_gae",
-           "qs_specialize", "qs_is_specialized", "qs_config_kp_words", "qs_specialize_compile"]
+           "qs_specialize", "qs_is_specialized", "qs_config_kp_words", "qs_specialize_compile",
+           "qs_replay_config_default", "qs_replay_workspace_bytes", "qs_replay_enable", "qs_replay_disable", "qs_replay_buffers_get"]
 
 _lib = None
 
@@ -117,6 +132,10 @@ def lib():
         "qs_specialize": ([V, I32], I32), "qs_is_specialized": ([V], I32),
         "qs_config_kp_words": ([P(QsConfig), V, SZ], I32),
         "qs_specialize_compile": ([P(QsConfig)], ctypes.c_longlong),
+        "qs_replay_config_default": ([P(QsReplayConfig), F], I32),
+        "qs_replay_workspace_bytes": ([V, P(QsReplayConfig), P(SZ)], I32),
+        "qs_replay_enable": ([V, P(QsReplayConfig), V], I32), "qs_replay_disable": ([V], I32),
+        "qs_replay_buffers_get": ([V, P(QsReplayBuffers)], I32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

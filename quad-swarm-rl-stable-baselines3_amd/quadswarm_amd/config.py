@@ -58,6 +58,8 @@ class QuadSwarmConfig:
     obst_size: float = 0.6
     obst_spawn_area: tuple = (8, 8)
     obst_collision_reward: float = 5.0        # quadcol_bin_obst
+    # ---- experience replay (quad_utils.py:34, 68-71: on when > 0; the reference's swarm runs use 0.75) ----
+    replay_buffer_sample_prob: float = 0.0
 
     @classmethod
     def c4(cls, num_envs=4096, num_agents=8, **over):
@@ -203,6 +205,10 @@ class QuadSwarmConfig:
                                           "(dynamic_repulsive, static_same_goal)")
             if self.use_downwash:
                 raise NotImplementedError("flavor A with downwash is not implemented")
+        if self.replay_buffer_sample_prob > 0 and self.flavor != "B":
+            raise NotImplementedError("experience replay is implemented for flavor B")
+        if not 0.0 <= self.replay_buffer_sample_prob <= 1.0:
+            raise ValueError("replay_buffer_sample_prob must be in [0, 1]")
         if not 1 <= self.num_agents <= N.MAX_AGENTS:
             raise ValueError(f"num_agents must be in [1, {N.MAX_AGENTS}]")
         k = self.k_neighbors

@@ -65,6 +65,45 @@ class QuadSwarmEnv:
         self.act_dim = cfg.act_dim
         self._align = 8 if cfg.flavor == "A" else 16
         self._torch = torch
+        self.replay = None
+        if cfg.replay_buffer_sample_prob > 0:
+            self.enable_replay(cfg.replay_buffer_sample_prob)
+
+    # ------------------------------------------------------------------------------------------
+    def enable_replay(self, sample_prob=0.75, **over):
+        """ExperienceReplayWrapper on device (quad_experience_replay.py:66-216): per-env checkpoints, collision
+        events and replayed episodes, run by qs_step / qs_reset from now on.  `over` overrides fields of the
+        reference-derived qs_replay_config (cp_every, grace_ticks, min_gap_ticks, buffer_size, ...)."""
+        rc = N.QsReplayConfig()
+        N.check(N.lib().qs_replay_config_default(ctypes.byref(rc), float(self.qcfg.control_dt)), "qs_replay_config_default")
+        rc.sample_prob = float(sample_prob)
+        for k, v in over.items():
+            setattr(rc, k, v)
+        nb = ctypes.c_size_t()
+        N.check(N.lib().qs_replay_workspace_bytes(self._h, ctypes.byref(rc), ctypes.byref(nb)), "qs_replay_workspace_bytes")
+        raw = self._torch.zeros(nb.value + 256, dtype=self._torch.uint8, device=self.device)
+        off = (-raw.data_ptr()) % 256
+        ws = raw[off:off + nb.value]
+        N.check(N.lib().qs_replay_enable(self._h, ctypes.byref(rc), ctypes.c_void_p(ws.data_ptr())), "qs_replay_enable")
+        rb = N.QsReplayBuffers()
+        N.check(N.lib().qs_replay_buffers_get(self._h, ctypes.byref(rb)), "qs_replay_buffers_get")
+        self.replay_config, self._replay_ws = rc, ws
+        self.replay = _replay_views(self._torch, ws, rb, rc, self.E)
+
+    def disable_replay(self):
+        self._torch.cuda.synchronize(self.device)
+        N.check(N.lib().qs_replay_disable(self._h), "qs_replay_disable")
+        self.replay = None
+
+    def replay_stats(self):
+        """The wrapper's episode_extra_stats "replay/*" values (quad_experience_replay.py:133-140), per env."""
+        if self.replay is None:
+            return None
+        ri = self.replay["ri"].cpu().numpy()
+        ep = np.maximum(ri[N.R_EPISODES], 1)
+        return {"replay/replay_rate": ri[N.R_REPLAYED] / ep,
+                "replay/new_episode_rate": (ri[N.R_EPISODES] - ri[N.R_REPLAYED]) / ep,
+                "replay/replay_buffer_size": ri[N.R_BUF_N].copy()}
 
     # ------------------------------------------------------------------------------------------
     def _stream(self):
@@ -160,6 +199,23 @@ class QuadSwarmEnv:
             self.close()
         except Exception:
             pass
+
+
+def _replay_views(torch, ws, rb, rc, E):
+    """Zero-copy torch views of the replay state (qs_replay_buffers) inside the torch-owned workspace."""
+    slots = rc.keep + rc.buffer_size
+    W = int(rb.snap_words)
+    base = ws.data_ptr()
+
+    def view(ptr, n, dtype, shape):
+        o = int(ptr) - base
+        nbytes = n * torch.tensor([], dtype=dtype).element_size()
+        return ws[o:o + nbytes].view(dtype).view(*shape)
+    return dict(ri=view(rb.ri, N.NR * E, torch.int32, (N.NR, E)), crash=view(rb.crash, E, torch.float64, (E,)),
+                hist=view(rb.hist, rc.hist_len * E, torch.float64, (rc.hist_len, E)),
+                perm=view(rb.perm, rc.buffer_size * E, torch.int32, (rc.buffer_size, E)),
+                nrep=view(rb.nrep, rc.buffer_size * E, torch.int32, (rc.buffer_size, E)),
+                store=view(rb.store, E * slots * W, torch.int32, (E, slots, W)), snap_words=W, slots=slots)
 
 
 def observation_bounds(cfg: QuadSwarmConfig):

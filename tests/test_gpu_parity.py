@@ -19,6 +19,7 @@ if not torch.cuda.is_available():  # pragma: no cover
 import oracle as O  # noqa: E402
 from parity_utils import assert_obs_match, crowd, gpu_to_oracle, oracle_params, oracle_to_gpu  # noqa: E402
 from quadswarm_amd import QuadSwarmConfig  # noqa: E402
+from quadswarm_amd import _native as N_  # noqa: E402
 from quadswarm_amd.env import QuadSwarmEnv  # noqa: E402
 from quadswarm_amd.vec_env import GpuQuadVecEnv  # noqa: E402
 
@@ -67,6 +68,11 @@ def test_one_step_from_identical_state(N, K, dw):
         assert_obs_match(np_(obs), w_obs, oenv, 18, cfg.k_neighbors)
         if w_done.any():
             np.testing.assert_allclose(np_(term)[w_done], w_term[w_done], atol=2e-4, rtol=1e-4)
+        # what the replay wrapper reads of the step: new collision, drone 0 on the floor
+        fl = env.env_state[N_.E_FLAGS].cpu().numpy()
+        np.testing.assert_array_equal((fl & N_.EF_NEWCOL) != 0, [oenv.envs[e].last_col != 0 for e in range(E)])
+        np.testing.assert_array_equal((fl & N_.EF_FLOOR0) != 0, [oenv.envs[e].last_floor0 != 0 for e in range(E)])
+        stats["newcol"] = stats.get("newcol", 0) + int(((fl & N_.EF_NEWCOL) != 0).sum())
         stats["done"] += int(w_done.sum())
         stats["coll"] += int((w_rew < -0.5).sum())
         # states agree after the step too
@@ -77,7 +83,7 @@ def test_one_step_from_identical_state(N, K, dw):
         np.testing.assert_allclose(np_(f["vel"]), vel, atol=5e-4, rtol=1e-4)
     assert stats["done"] > 0
     if N > 1:
-        assert stats["coll"] > 0
+        assert stats["coll"] > 0 and stats["newcol"] > 0
 
 
 def test_free_run_matches_oracle():
