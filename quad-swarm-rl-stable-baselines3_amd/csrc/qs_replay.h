@@ -2,11 +2,12 @@
 //
 // Replaces ExperienceReplayWrapper / ReplayBuffer (gym_art/quadrotor_multi/quad_experience_replay.py:16-216) and
 // the env-side bookkeeping they read (quadrotor_multi.py:182-185 state, :382-388 can_drones_fly, :461-465 reset
-// accounting, :722-725 crash accumulation).  One wavefront per env, launched after the step (or reset) kernel
-// on the same stream.  The decision logic is a handful of per-env integers: every lane evaluates it
-// redundantly from broadcast loads (so no cross-lane exchange is needed) and lane 0 writes the results; the
-// 64 lanes then move whole env snapshots (copy loops of snap_words 32-bit words) when a checkpoint is saved,
-// an event is written or an episode is replayed.  Snapshots are contiguous per (env, slot) in HBM
+// accounting, :722-725 crash accumulation).  RL = 16 lanes per env (4 envs per wavefront, 16 per workgroup),
+// launched after the step (or reset) kernel on the same stream.  The decision logic is a handful of per-env
+// integers: the env's lanes evaluate it redundantly from broadcast loads (no cross-lane exchange) and its
+// first lane writes what changed; the RL lanes then move whole env snapshots (copy loops of snap_words
+// 32-bit words) when a checkpoint is saved, an event is written or an episode is replayed.  A step with
+// nothing to do (the common case) costs the env's ~10 loads and no store.  Snapshots are contiguous per (env, slot) in HBM
 // ([E, keep + bufsz, W]) so each copy is a coalesced burst on the store side; the live side is the SoA state.
 // CPU restatement: oracle/replay_oracle.py (pinned to the reference's wrapper by tests/golden/replay_*.npz).
 #pragma once
@@ -57,15 +58,17 @@ __device__ __forceinline__ uint32_t* snap_word(const KP& kp, const Bufs& b, int 
     return reinterpret_cast<uint32_t*>(b.obs) + (size_t)e * N * kp.obs_dim + w;
 }
 
+constexpr int RL = 16;   // lanes per env
+
 __device__ __forceinline__ void snap_save(const KP& kp, const Bufs& b, int e, uint32_t* dst, int W, int lane) {
-    for (int w = lane; w < W; w += 64) {
+    for (int w = lane; w < W; w += RL) {
         bool ep;
         dst[w] = *snap_word(kp, b, e, w, &ep);
     }
 }
 
 __device__ __forceinline__ void snap_restore(const KP& kp, const Bufs& b, int e, const uint32_t* src, int W, int lane) {
-    for (int w = lane; w < W; w += 64) {
+    for (int w = lane; w < W; w += RL) {
         bool ep;
         uint32_t* p = snap_word(kp, b, e, w, &ep);
         if (!ep) *p = src[w];
@@ -90,15 +93,17 @@ __device__ __forceinline__ int hist_push(const RP& rp, const RBufs& r, int E, in
 template <bool STEP>
 __global__ __launch_bounds__(256) void replay_kernel(const KP* __restrict__ kpp, Bufs b, RBufs r, RP rp, uint32_t seed) {
     const KP& kp = *kpp;
-    const int lane = threadIdx.x & 63;
-    const int e = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (e >= kp.E) return;   // whole wavefronts leave together
+    const int lane = threadIdx.x % RL;
+    const int e = blockIdx.x * (256 / RL) + threadIdx.x / RL;
+    if (e >= kp.E) return;   // no barriers below: lanes of absent envs just leave
     const int E = kp.E;
     const bool w0 = lane == 0;
     int32_t* ri = r.ri;
     int active = ri[QS_R_ACTIVE * E + e];
     int hn = ri[QS_R_HIST_N * E + e], hh = ri[QS_R_HIST_HEAD * E + e];
     double crash = r.crash[e];
+    const int ri0_active = active, ri0_hn = hn, ri0_hh = hh;
+    const double crash0 = crash;
 
     if (!STEP) {
         if (b.mask != nullptr && b.mask[e] == 0) return;
@@ -124,6 +129,8 @@ __global__ __launch_bounds__(256) void replay_kernel(const KP* __restrict__ kpp,
     int ck_n = ri[QS_R_CK_N * E + e], ck_head = ri[QS_R_CK_HEAD * E + e];
     int buf_n = ri[QS_R_BUF_N * E + e], buf_idx = ri[QS_R_BUF_IDX * E + e];
     int last_add = ri[QS_R_LAST_ADD * E + e];
+    const int ri0_saved = saved, ri0_ck_n = ck_n, ri0_ck_head = ck_head, ri0_buf_n = buf_n, ri0_buf_idx = buf_idx,
+              ri0_last_add = last_add;
     int restored = -1, pushed = -1;
 
     if (!active)   // crashes_last_episode += infos[0]["rewards"]["rew_crash"] = dt * -(crash * on_floor) (:725)
@@ -187,11 +194,11 @@ __global__ __launch_bounds__(256) void replay_kernel(const KP* __restrict__ kpp,
                 const int phys = r.perm[(size_t)pos * E + e];
                 const uint32_t* from = st + (size_t)src * W;
                 uint32_t* to = st + (size_t)(rp.keep + phys) * W;
-                for (int w = lane; w < W; w += 64) to[w] = from[w];
+                for (int w = lane; w < W; w += RL) to[w] = from[w];
                 // the wrapper returns the checkpoint's obs for this step (`obs` rebound at :175, returned :180)
                 const int nod = N * kp.obs_dim;
                 uint32_t* obs_w = reinterpret_cast<uint32_t*>(b.obs) + (size_t)e * nod;   // bit copies
-                for (int k = lane; k < nod; k += 64) obs_w[k] = from[W - nod + k];
+                for (int k = lane; k < nod; k += RL) obs_w[k] = from[W - nod + k];
                 if (w0) r.nrep[(size_t)phys * E + e] = 0;
                 buf_idx = (buf_idx + 1) % rp.bufsz;
                 last_add = tick;
@@ -200,18 +207,19 @@ __global__ __launch_bounds__(256) void replay_kernel(const KP* __restrict__ kpp,
         }
     }
     if (w0) {
-        ri[QS_R_ACTIVE * E + e] = active;
-        ri[QS_R_SAVED * E + e] = saved;
-        ri[QS_R_CK_N * E + e] = ck_n;
-        ri[QS_R_CK_HEAD * E + e] = ck_head;
-        ri[QS_R_BUF_N * E + e] = buf_n;
-        ri[QS_R_BUF_IDX * E + e] = buf_idx;
-        ri[QS_R_LAST_ADD * E + e] = last_add;
-        ri[QS_R_HIST_N * E + e] = hn;
-        ri[QS_R_HIST_HEAD * E + e] = hh;
-        ri[QS_R_RESTORED * E + e] = restored;
-        ri[QS_R_PUSHED * E + e] = pushed;
-        r.crash[e] = crash;
+        auto put = [&](int f, int v, int was) { if (v != was) ri[f * E + e] = v; };
+        put(QS_R_ACTIVE, active, ri0_active);
+        put(QS_R_SAVED, saved, ri0_saved);
+        put(QS_R_CK_N, ck_n, ri0_ck_n);
+        put(QS_R_CK_HEAD, ck_head, ri0_ck_head);
+        put(QS_R_BUF_N, buf_n, ri0_buf_n);
+        put(QS_R_BUF_IDX, buf_idx, ri0_buf_idx);
+        put(QS_R_LAST_ADD, last_add, ri0_last_add);
+        put(QS_R_HIST_N, hn, ri0_hn);
+        put(QS_R_HIST_HEAD, hh, ri0_hh);
+        put(QS_R_RESTORED, restored, ri[QS_R_RESTORED * E + e]);
+        put(QS_R_PUSHED, pushed, ri[QS_R_PUSHED * E + e]);
+        if (crash != crash0) r.crash[e] = crash;
     }
 }
 

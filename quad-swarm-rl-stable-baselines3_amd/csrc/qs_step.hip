@@ -580,7 +580,8 @@ static int launch_replay(qs_handle* h, bool step, const uint8_t* mask, hipStream
     qs::Bufs b = bufs_of(h);
     b.mask = mask;
     const qs::KP* kpd = (const qs::KP*)((char*)h->ws + h->lay.params);
-    const dim3 grid((unsigned)((h->kp.E + 3) / 4)), block(256);
+    constexpr int epb = 256 / qs::RL;   // envs per workgroup
+    const dim3 grid((unsigned)((h->kp.E + epb - 1) / epb)), block(256);
     if (step) hipLaunchKernelGGL(qs::replay_kernel<true>, grid, block, 0, s, kpd, b, h->rb, h->rp, h->cfg.seed);
     else hipLaunchKernelGGL(qs::replay_kernel<false>, grid, block, 0, s, kpd, b, h->rb, h->rp, h->cfg.seed);
     QS_HIP(hipGetLastError());
