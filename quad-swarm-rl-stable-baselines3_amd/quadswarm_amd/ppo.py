@@ -119,13 +119,34 @@ class NeighborAttention(nn.Module):
         self.attention_mlp = nn.Sequential(nn.Linear(2 * H, H), _act(cfg), nn.Linear(H, H), _act(cfg),
                                            nn.Linear(H, 1))
 
+    # split=True evaluates the two concatenating layers by their weight column blocks:
+    #   cat(s.repeat(K,1), n) @ W^T + b   = n @ W_n^T + (s @ W_s^T + b)  broadcast over the K tiles
+    #   cat(e, e_m.repeat(K,1)) @ A^T + a = e @ A_e^T + (e_m @ A_m^T + a) broadcast over the K tiles
+    # (`Tensor.repeat(K, 1)` tiles batch-minor, so row j = (tile j // B, agent j % B) and the per-agent
+    # term broadcasts over the leading K of a [K, B, H] view).  Same parameters and the same function;
+    # the per-agent halves are computed once per agent instead of once per neighbour row, which removes
+    # H*H of the 409 k MACs per neighbour row at H = 256 (and the two concatenated copies).  Rounding
+    # differs from the concatenated GEMM only by summation order (tests/test_ppo_cpu.py pins it at fp64).
+    split = True
+
     def forward(self, self_obs, nbr):
         B, K, H = nbr.shape[0], self.cfg.num_use_neighbor_obs, self.cfg.neighbor_hidden_size
         rows = nbr.reshape(B * K, -1)
-        e = self.embedding_mlp(torch.cat((self_obs.repeat(K, 1), rows), dim=1))       # e_i
-        h = self.neighbor_value_mlp(e)                                                # h_i
-        e_mean = e.view(B, K, H).mean(dim=1)                                          # e_m
-        score = self.attention_mlp(torch.cat((e, e_mean.repeat(K, 1)), dim=1)).view(B, K)
+        if not self.split:
+            e = self.embedding_mlp(torch.cat((self_obs.repeat(K, 1), rows), dim=1))       # e_i
+            h = self.neighbor_value_mlp(e)                                                # h_i
+            e_mean = e.view(B, K, H).mean(dim=1)                                          # e_m
+            score = self.attention_mlp(torch.cat((e, e_mean.repeat(K, 1)), dim=1)).view(B, K)
+        else:
+            so = self_obs.shape[1]
+            l1, act = self.embedding_mlp[0], self.embedding_mlp[1]
+            pre = F.linear(rows, l1.weight[:, so:]).view(K, B, H) + F.linear(self_obs, l1.weight[:, :so], l1.bias)
+            e = self.embedding_mlp[2:](act(pre.view(B * K, H)))                           # e_i
+            h = self.neighbor_value_mlp(e)                                                # h_i
+            e_mean = e.view(B, K, H).mean(dim=1)                                          # e_m
+            a1 = self.attention_mlp[0]
+            pre = F.linear(e, a1.weight[:, :H]).view(K, B, H) + F.linear(e_mean, a1.weight[:, H:], a1.bias)
+            score = self.attention_mlp[1:](pre.view(B * K, H)).view(B, K)
         w = torch.softmax(score, dim=1).view(B * K, 1)
         return (w * h).view(B, K, H).sum(dim=1)
 

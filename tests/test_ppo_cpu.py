@@ -101,6 +101,28 @@ def test_attention_row_pairing_quirk():
     torch.testing.assert_close(got, want, rtol=1e-12, atol=1e-12)
 
 
+@pytest.mark.parametrize("B", [1, 5])
+def test_attention_split_weights_equal_concatenated(B):
+    """The split-weight evaluation (per-agent halves of the two concatenating layers computed once per
+    agent) is the reference's concatenated forward: same outputs and same parameter gradients at fp64."""
+    _, pc = sb_cfg()
+    torch.manual_seed(2)
+    att = NeighborAttention(pc).double()
+    K = pc.num_use_neighbor_obs
+    so = torch.randn(B, pc.self_obs_dim, dtype=torch.float64)
+    nb = torch.randn(B, K, pc.neighbor_obs_dim, dtype=torch.float64)
+    outs, grads = [], []
+    for split in (False, True):
+        att.split = split
+        att.zero_grad()
+        y = att(so, nb)
+        (y * torch.linspace(-1, 1, y.numel(), dtype=torch.float64).view_as(y)).sum().backward()
+        outs.append(y.detach())
+        grads.append(torch.cat([p.grad.flatten() for p in att.parameters()]))
+    torch.testing.assert_close(outs[1], outs[0], rtol=1e-12, atol=1e-12)
+    torch.testing.assert_close(grads[1], grads[0], rtol=1e-10, atol=1e-12)
+
+
 def test_initialisation_follows_reference():
     """Only action_net / value_net are xavier-initialised (type(layer) == nn.Linear check); log_std = 0."""
     _, pc = sb_cfg(policy_init_gain=1.0)
