@@ -37,6 +37,11 @@ CONFIGS = {
     # ... with its experience replay (replay_buffer_sample_prob=0.75, quad_experience_replay.py on device)
     "c3mixr": dict(num_envs=4096, num_agents=8, neighbor_visible_num=6, neighbor_obs_type="pos_vel", quads_mode="mix",
                    replay_buffer_sample_prob=0.75),
+    # C4 as the reference trains obstacle domain randomisation (runs/obstacles/obst_domain_random.py: replay 0.75,
+    # per-episode pillar density in {0.05 .. 0.2} and size in {0.3, 0.4, 0.5})
+    "c4dr": dict(preset="c4", num_envs=4096, num_agents=8, replay_buffer_sample_prob=0.75, domain_random=True,
+                 obst_density_random=True, obst_size_random=True, obst_density_min=0.05, obst_density_max=0.2,
+                 obst_size_min=0.3, obst_size_max=0.6),
     "c5": dict(num_envs=1024, num_agents=32, neighbor_visible_num=6, neighbor_obs_type="pos_vel"),
     "a8": dict(flavor="A", num_envs=4096, num_agents=8, initial_capture_radius=0.5),
     "a4": dict(flavor="A", num_envs=8192, num_agents=4, initial_capture_radius=0.5),
@@ -47,6 +52,8 @@ WORKLOAD = {"c2": "single_quad x 16384 envs", "c3": "8-drone swarm static_same_g
                       "reference's swarm run (runs/quad_multi_mix_baseline.py)",
             "c4": "8-drone swarm + obstacles x 4096 envs (12 pillars, SDF obs, pos_vel k=2, floor obs, downwash, "
                   "mix of o_random / o_static_same_goal)",
+            "c4dr": "8-drone swarm + obstacles x 4096 envs with experience replay (p=0.75) and obstacle domain "
+                    "randomisation (3-12 pillars of 0.3-0.5 m per episode), runs/obstacles/obst_domain_random.py",
             "c5": "32-drone swarm x 1024 envs per GPU (pos_vel k=6)",
             "a8": "flavor A (sb_train env: PID pre-controller x 8 ticks, dynamic_repulsive target, ndist_nsangle "
                   "camera neighbours k=7) 8 drones x 4096 envs, capture radius 0.5",

@@ -36,8 +36,9 @@
 extern "C" {
 #endif
 
-#define QS_ABI_VERSION 4
+#define QS_ABI_VERSION 5
 #define QS_MAX_AGENTS 32            /* drones per env: one env lives inside one 64-lane wavefront */
+#define QS_MAX_DR_CHOICES 8         /* entries per obstacle domain-randomisation list */
 
 enum qs_status {
     QS_OK = 0,
@@ -145,6 +146,15 @@ typedef struct qs_config {
     float obst_size;                /* pillar diameter (0.6) */
     float sdf_resolution;           /* 0.1 (obstacles/obstacles.py:12) */
     float rew_quadcol_bin_obst;     /* quadcol_bin_obst reward coefficient */
+    /* ---- obstacle domain randomisation: the experience-replay wrapper's reset draws one entry of each list
+     * per new episode and hands it to env.reset (quad_experience_replay.py:76-87, 106-118, 206-214;
+     * quadrotor_multi.py:440-450).  0 entries = off.  dr_counts[c] = int(area^2 * density_c) pillars, -1 for a
+     * 0.0 density (falsy there: the env keeps its current value); dr_sizes[c] = pillar diameter, 0 = keep.
+     * The env's current choice is part of its state (QS_E_OBST_M / QS_E_OBST_SZ), so replays restore it. */
+    int32_t dr_num_counts;
+    int32_t dr_counts[QS_MAX_DR_CHOICES];
+    int32_t dr_num_sizes;
+    float dr_sizes[QS_MAX_DR_CHOICES];
 } qs_config;
 
 /* Device buffers of a handle.  State is structure-of-arrays: field f of drone g lives at
@@ -173,7 +183,9 @@ enum qs_env_field {
      * (QUADS_MODE_LIST index), formation (QUADS_FORMATION_LIST index), control_step_for_sec,
      * increase_formation_size */
     QS_E_SC_MODE = 3, QS_E_SC_FORM = 4, QS_E_SC_PERIOD = 5, QS_E_SC_INC = 6,
-    QS_NE = 7
+    /* obstacle domain randomisation: the env's pillar count / size as 1 + its list entry, 0 = configured */
+    QS_E_OBST_M = 7, QS_E_OBST_SZ = 8,
+    QS_NE = 9
 };
 enum qs_env_flags {
     QS_EF_STALE = 1,                /* stale_vel / QS_F_HEADING hold QuadrotorEnvMulti.vel / .heading */
@@ -206,7 +218,8 @@ typedef struct qs_buffers {         /* device pointers (valid for the handle's l
     int32_t* istate;                /* [QS_NI, I] */
     int32_t* env;                   /* [QS_NE, E] */
     float* env_f;                   /* [QS_NENVF, E] */
-    float* obst;                    /* [E, num_obstacles, 2] pillar xy (MultiObstacles.pos_arr order) */
+    float* obst;                    /* [E, M, 2] pillar xy (MultiObstacles.pos_arr order); M = num_obstacles, or
+                                       the largest dr_counts entry (an env uses its first QS_E_OBST_M slots) */
     float* stale_vel;               /* [3, I]  QuadrotorEnvMulti.vel as last seen by a reset */
     float* obs;                     /* [I, obs_dim] */
     float* term_obs;                /* [I, obs_dim] rows of envs that finished this step */

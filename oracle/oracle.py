@@ -48,6 +48,7 @@ class OrParams(ctypes.Structure):
         ("use_obstacles", I), ("num_obstacles", I), ("obst_area", I), ("obst_scenario", I),
         ("obst_size", D), ("obst_z", D), ("sdf_resolution", D), ("rew_quadcol_bin_obst", D),
         ("scenario_b", I),
+        ("dr_n_counts", I), ("dr_counts", I * 9), ("dr_n_sizes", I), ("dr_sizes", D * 9),
     ]
 
 
@@ -68,6 +69,7 @@ SC_MODES = ["static_same_goal", "static_diff_goal", "ep_lissajous3D", "ep_rand_b
             "dynamic_diff_goal", "dynamic_formations", "swap_goals", "swarm_vs_swarm", "run_away"]
 SC_NONE, SC_MIX = -1, 10
 S_SCN, S_SCN_RESET = 23, 24
+S_DR = 26
 
 
 class OrDrone(ctypes.Structure):
@@ -87,7 +89,7 @@ class OrEnv(ctypes.Structure):
                 ("obs_pos", (D * 3) * 64), ("obs_vel", (D * 3) * 64),
                 ("heading", D * 64), ("target", D * 2), ("capture_radius", D), ("success", I), ("has_pos", I),
                 ("n_obst", I), ("obst", (D * 2) * 64), ("obst_mode", I), ("scen", OrScen),
-                ("last_col", I), ("last_floor0", I)]
+                ("last_col", I), ("last_floor0", I), ("obst_mi", I), ("obst_si", I)]
 
 
 class OrRng(ctypes.Structure):

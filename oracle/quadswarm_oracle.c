@@ -622,9 +622,15 @@ void or_cell_xy(int row, int col, int n, double out[2]) {
     out[1] = (double)(n - 1 - row) + 0.5 - h;
 }
 
+/* the env's pillar diameter: MultiObstacles(obstacle_size=self.obst_size) of its last reset
+ * (quadrotor_multi.py:445-450), i.e. the configured size or a domain-randomisation choice */
+double or_env_obst_size(const or_params* p, const or_env* ev) {
+    return ev->obst_si > 0 ? p->dr_sizes[ev->obst_si] : p->obst_size;
+}
+
 /* get_surround_sdfs (obstacles/utils.py:4-27): 3x3 grid at +-resolution, min distance - radius */
 void or_obst_sdf(const or_params* p, const or_env* ev, const double xy[2], double out[9]) {
-    const double res = p->sdf_resolution, rad = p->obst_size / 2.0;
+    const double res = p->sdf_resolution, rad = or_env_obst_size(p, ev) / 2.0;
     const double gx[3] = {xy[0] - res, xy[0], xy[0] + res}, gy[3] = {xy[1] - res, xy[1], xy[1] + res};
     for (int a = 0; a < 3; ++a)
         for (int b = 0; b < 3; ++b) {
@@ -640,7 +646,7 @@ void or_obst_sdf(const or_params* p, const or_env* ev, const double xy[2], doubl
 
 /* collision_detection (obstacles/utils.py:30-43): first obstacle within arm + radius (xy) */
 int or_obst_detect(const or_params* p, const or_env* ev, const double xy[2]) {
-    const double thr = p->arm + p->obst_size / 2.0;
+    const double thr = p->arm + or_env_obst_size(p, ev) / 2.0;
     for (int o = 0; o < ev->n_obst; ++o) {
         double dx = xy[0] - ev->obst[o][0], dy = xy[1] - ev->obst[o][1];
         if (sqrt(dx * dx + dy * dy) <= thr) return o;
@@ -651,7 +657,8 @@ int or_obst_detect(const or_params* p, const or_env* ev, const double xy[2]) {
 /* perform_collision_with_obstacle (collisions/obstacles.py:23-50) with
  * compute_col_norm_and_new_vel_obst (:8-20).  Philox indices (stream OBST): normals t*6+0..2 (0.1),
  * t*6+3..5 (0.05) for try t; uniforms 0 decay ratio, 1-3 omega direction, 4 omega magnitude. */
-void or_collide_obstacle(const or_params* p, or_drone* d, const double opos[3], or_rng* r, uint32_t gid) {
+static void collide_obstacle_sz(double size, or_drone* d, const double opos[3], or_rng* r,
+                                uint32_t gid) {
     double n[3] = {d->pos[0] - opos[0], d->pos[1] - opos[1], 0.0};
     double nm = norm3(n);
     double den = nm == 0.0 ? nm + EPS_UTIL : nm;
@@ -670,7 +677,7 @@ void or_collide_obstacle(const or_params* p, or_drone* d, const double opos[3], 
     }
     const double max_v = norm3(d->vel);
     double dp[3] = {d->pos[0] - opos[0], d->pos[1] - opos[1], d->pos[2] - opos[2]};
-    const int inside = norm3(dp) < p->obst_size / 2.0;
+    const int inside = norm3(dp) < size / 2.0;
     double shift[3];
     for (int c = 0; c < 3; ++c) shift[c] = nv[c] - d->vel[c] + noise[c];
     double ratio = inside ? ru(r, gid, OR_S_OBST, 0, 1.0, 1.0) : ru(r, gid, OR_S_OBST, 0, 0.2, 0.8);
@@ -678,6 +685,10 @@ void or_collide_obstacle(const or_params* p, or_drone* d, const double opos[3], 
     double w[3];
     new_omega(r, gid, OR_S_OBST, 1, 1.0, w);
     for (int c = 0; c < 3; ++c) d->omega[c] += w[c];
+}
+
+void or_collide_obstacle(const or_params* p, or_drone* d, const double opos[3], or_rng* r, uint32_t gid) {
+    collide_obstacle_sz(p->obst_size, d, opos, r, gid);
 }
 
 /* Scenario_o_base.max_square_area_center (o_base.py:125-153), quirks included: dp's first row and
@@ -724,7 +735,22 @@ static void choose_k(or_rng* r, uint32_t gid, uint32_t st, uint32_t u0, int n, i
  * and goals. */
 static void obstacle_reset(const or_params* p, or_env* ev, uint32_t gbase, or_rng* r, double spawn[][3],
                            double goal[][3]) {
-    const int n = p->obst_area, M = p->num_obstacles, N = p->num_agents, tape = r->mode == OR_RNG_TAPE;
+    const int tape = r->mode == OR_RNG_TAPE;
+    /* domain randomisation (quad_experience_replay.py:106-118, 206-214): the wrapper's reset picks
+     * np.random.choice(obst_densities) then np.random.choice(obst_sizes) and hands them to env.reset
+     * (quadrotor_multi.py:440-446).  Philox mode = the GPU's fused reset, which IS the wrapper's reset
+     * (DR needs the wrapper, i.e. replay on).  Tape mode replays the bare env, whose in-env resets keep
+     * the values: the caller sets obst_mi / obst_si as the wrapper chose them. */
+    if (!tape && p->dr_n_counts > 0) {
+        const int c = (int)(or_philox_uniform(r->seed, gbase, OR_S_DR | OR_UNIF_BIT, r->step, 0) * (double)p->dr_n_counts);
+        if (p->dr_counts[c + 1] >= 0) ev->obst_mi = c + 1;
+    }
+    if (!tape && p->dr_n_sizes > 0) {
+        const int c = (int)(or_philox_uniform(r->seed, gbase, OR_S_DR | OR_UNIF_BIT, r->step, 1) * (double)p->dr_n_sizes);
+        if (p->dr_sizes[c + 1] > 0.0) ev->obst_si = c + 1;
+    }
+    const int n = p->obst_area, N = p->num_agents;
+    const int M = ev->obst_mi > 0 ? p->dr_counts[ev->obst_mi] : p->num_obstacles;
     unsigned char map[64 * 64];
     memset(map, 0, sizeof map);
     int ids[64];
@@ -951,7 +977,7 @@ void or_env_step(const or_params* p, or_drone* drones, or_env* envs, int e, cons
             if (onew[i]) {
                 flag = 1;
                 const double op[3] = {ev->obst[ocol[i]][0], ev->obst[ocol[i]][1], p->obst_z};
-                or_collide_obstacle(p, &dr[i], op, r, gbase + (uint32_t)i);
+                collide_obstacle_sz(or_env_obst_size(p, ev), &dr[i], op, r, gbase + (uint32_t)i);
             }
         for (int i = 0; i < N; ++i) if (wall_new[i]) { flag = 1; or_collide_wall(p, &dr[i], r, gbase + (uint32_t)i); }
         for (int i = 0; i < N; ++i) if (ceil_new[i]) { flag = 1; or_collide_ceiling(&dr[i], r, gbase + (uint32_t)i); }

@@ -51,6 +51,7 @@ enum {
     /* flavor-B goal scenarios (quadswarm_oracle_scen.c): per env (key = drone 0), one word per draw in call order */
     OR_S_SCN = 23,        /* scenario.step() draws                                                  */
     OR_S_SCN_RESET = 24,  /* mix mode + scenario __init__ / reset draws                             */
+    OR_S_DR = 26,         /* per env (key = drone 0): uniform 0 density choice, 1 size choice (wrapper reset) */
     OR_UNIF_BIT = 0x80    /* uniform draws use stream | OR_UNIF_BIT           */
 };
 
@@ -134,6 +135,14 @@ typedef struct {
     double rew_quadcol_bin_obst;
     /* ---- flavor-B goal scenarios (scenarios/ files): OR_SC_NONE = the fixed static_same_goal goal ---- */
     int scenario_b;
+    /* ---- obstacle domain randomisation (ExperienceReplayWrapper, quad_experience_replay.py:76-87, 106-118,
+     * 206-214; env side quadrotor_multi.py:440-450).  Index 0 of each table is the configured value
+     * (num_obstacles / obst_size); choice c of the wrapper's np.arange list is index c + 1.  A choice whose
+     * density or size is 0.0 is falsy at quadrotor_multi.py:443-446 and keeps the env's current value:
+     * dr_counts[c + 1] = -1, dr_sizes[c + 1] = 0. ---- */
+    int dr_n_counts, dr_counts[9];
+    int dr_n_sizes;
+    double dr_sizes[9];
 } or_params;
 
 /* flavor-B scenarios, QUADS_MODE_LIST order (scenarios/utils.py:7-10) + run_away; OR_SC_MIX draws one per
@@ -195,6 +204,9 @@ typedef struct {
     /* what the experience-replay wrapper reads of the last step (quad_experience_replay.py:161-163,
      * quadrotor_multi.py:725): a new drone collision (.any() of the ids) or obstacle hit; drone 0 on the floor */
     int last_col, last_floor0;
+    /* obstacle domain randomisation: the env's current (obst_density, obst_size) as table indices
+     * (0 = the configured values) */
+    int obst_mi, obst_si;
 } or_env;
 
 /* ---- low level pieces (exported for per-function golden tests) ---- */
@@ -236,6 +248,7 @@ void or_neighbor_obs(const or_params* p, const or_env* ev, double* obs, int obs_
 void or_obst_sdf(const or_params* p, const or_env* ev, const double xy[2], double out[9]);
 int or_obst_detect(const or_params* p, const or_env* ev, const double xy[2]);
 void or_collide_obstacle(const or_params* p, or_drone* d, const double opos[3], or_rng* r, uint32_t gid);
+double or_env_obst_size(const or_params* p, const or_env* ev);
 void or_max_square_center(const unsigned char* map, int n, double out_xy[2]);
 void or_cell_xy(int row, int col, int n, double out_xy[2]);
 

@@ -43,8 +43,12 @@ struct KP {
     float tgt_vmax, tgt_dt, arena, tgt_z;
     float nclip_lo[8], nclip_hi[8];
     // ---- obstacles (flavor B) ----
-    int obst, M, obst_n, obst_scen;                 // on, obstacles per env, grid side, scenario
+    int obst, M, obst_n, obst_scen;                 // on, pillar slots per env, grid side, scenario
     float obst_r, obst_thr, obst_z, sdf_res, quadcol_obst;
+    // obstacle domain randomisation (replay wrapper reset): index 0 = configured, choice c = index c + 1;
+    // dr_m -1 / dr_r 0 = a falsy 0.0 choice that keeps the env's current value
+    int dr, dr_nm, dr_ns, dr_m[9];
+    float dr_r[9], dr_thr[9];
     // ---- flavor-B goal scenarios: -1 = the fixed static_same_goal goal, 0..9 a scenario, 10 = mix ----
     int scen_b;
 };

@@ -366,14 +366,36 @@ struct ObstScratch {
     uint8_t perm[64], map[64], fr[64], dp[64], sp[32], gl[32], ids[64];
     float ez;
     int mode;
+    int mi, si;   // domain randomisation: the env's pillar count / size table indices (in: current, out: new)
 };
+
+// The env's pillar geometry: count, radius, collision threshold (arm + radius).  Without domain
+// randomisation these are the (specialised) constants; with it, the env's table entries.
+struct OGeo {
+    int m;
+    float r, thr;
+};
+__device__ __forceinline__ OGeo ogeo(const KP& kp, int mi, int si) {
+    if (!kp.dr) return OGeo{kp.M, kp.obst_r, kp.obst_thr};
+    return OGeo{kp.dr_m[mi], kp.dr_r[si], kp.dr_thr[si]};
+}
 static_assert(sizeof(ObstScratch) <= QS_OBST_SCRATCH, "obstacle scratch");
 
 // Obstacle map + scenario of one env (quadrotor_multi.py:405-426, 449-452; scenarios/mix.py:78-99;
 // o_random.py:26-51; o_static_same_goal.py:28-48; o_base.py:58-153).  One lane per env runs it;
 // the other lanes of the env read sp/gl/mode/ez after a barrier.  Writes the env's obstacle list.
 __device__ __forceinline__ void obstacle_reset_env(const KP& kp, const Rng& r, uint32_t genv, ObstScratch* sc, float2* ob) {
-    const int n = kp.obst_n, nn = n * n, M = kp.M, N = kp.N;
+    if (kp.dr) {   // the replay wrapper's reset: np.random.choice of density, then of size (quad_experience_replay.py:106-118)
+        if (kp.dr_nm > 0) {
+            const int c = ufloor(ubits(r, genv, S_DR, 0), kp.dr_nm);
+            if (kp.dr_m[c + 1] >= 0) sc->mi = c + 1;   // a 0.0 density is falsy: keep (quadrotor_multi.py:443)
+        }
+        if (kp.dr_ns > 0) {
+            const int c = ufloor(ubits(r, genv, S_DR, 1), kp.dr_ns);
+            if (kp.dr_r[c + 1] > 0.f) sc->si = c + 1;
+        }
+    }
+    const int n = kp.obst_n, nn = n * n, M = ogeo(kp, sc->mi, sc->si).m, N = kp.N;
     for (int c = 0; c < nn; ++c) sc->map[c] = 0;
     choose_k(r, genv, S_OBSTMAP, 0, nn, M, sc->perm, sc->ids);
     for (int o = 0; o < M; ++o) {
@@ -789,7 +811,7 @@ __device__ __forceinline__ float* scen_tab(float* lds, const KP& kp, int slots) 
 }
 
 // get_surround_sdfs (obstacles/utils.py:4-27)
-__device__ __forceinline__ void sdf_obs(const KP& kp, const float2* ob, float x, float y, float* out) {
+__device__ __forceinline__ void sdf_obs(const KP& kp, const OGeo& og, const float2* ob, float x, float y, float* out) {
     const float res = kp.sdf_res;
 #pragma unroll
     for (int a = 0; a < 3; ++a)
@@ -797,27 +819,27 @@ __device__ __forceinline__ void sdf_obs(const KP& kp, const float2* ob, float x,
         for (int b = 0; b < 3; ++b) {
             const float gx = x + (float)(a - 1) * res, gy = y + (float)(b - 1) * res;
             float m2 = 1.0e4f;   // (100 m)^2
-            for (int o = 0; o < kp.M; ++o) {
+            for (int o = 0; o < og.m; ++o) {
                 const float dx = gx - ob[o].x, dy = gy - ob[o].y;
                 m2 = fminf(m2, dx * dx + dy * dy);
             }
-            out[a * 3 + b] = fsqrt(m2) - kp.obst_r;
+            out[a * 3 + b] = fsqrt(m2) - og.r;
         }
 }
 
 // collision_detection (obstacles/utils.py:30-43): first obstacle within arm + radius
-__device__ __forceinline__ int obst_detect(const KP& kp, const float2* ob, float x, float y) {
-    for (int o = 0; o < kp.M; ++o) {
+__device__ __forceinline__ int obst_detect(const OGeo& og, const float2* ob, float x, float y) {
+    for (int o = 0; o < og.m; ++o) {
         const float dx = x - ob[o].x, dy = y - ob[o].y;
-        if (fsqrt(dx * dx + dy * dy) <= kp.obst_thr) return o;
+        if (fsqrt(dx * dx + dy * dy) <= og.thr) return o;
     }
     return -1;
 }
 
 // perform_collision_with_obstacle (collisions/obstacles.py:23-50); Philox indices as the oracle's:
 // z = normals 0..19 of S_OBST (try t uses t*6 .. t*6+5), u = uniforms 0..7
-__device__ __forceinline__ void collide_obstacle(const KP& kp, Drone& d, float ox, float oy, const float* z,
-                                                 const float* u) {
+__device__ __forceinline__ void collide_obstacle(const KP& kp, const OGeo& og, Drone& d, float ox, float oy,
+                                                 const float* z, const float* u) {
     float n[3] = {d.pos[0] - ox, d.pos[1] - oy, 0.f};
     const float nm = fsqrt(n[0] * n[0] + n[1] * n[1]);
     const float inm = frcp(nm == 0.f ? 1e-5f : nm);
@@ -839,7 +861,7 @@ __device__ __forceinline__ void collide_obstacle(const KP& kp, Drone& d, float o
         }
     }
     const float dz = d.pos[2] - kp.obst_z;
-    const bool inside = fsqrt(nm * nm + dz * dz) < kp.obst_r;
+    const bool inside = fsqrt(nm * nm + dz * dz) < og.r;
     float sh[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) sh[c] = nv[c] - d.vel[c] + noise[c];
@@ -911,6 +933,9 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     const Rng rng = env_rng(seed, tick0, episode);
     const int tick = tick0 + 1;
     const bool done = tick > kpm.ep_len;
+    int omi = 0, osi = 0;   // the env's domain-randomisation choice (QS_E_OBST_M / _SZ)
+    if (OBST && kp.dr) { omi = b.env[QS_E_OBST_M * kp.E + eidx]; osi = b.env[QS_E_OBST_SZ * kp.E + eidx]; }
+    OGeo og = ogeo(kp, omi, osi);
 
     // The step's regular draws: Philox block k of {OU 0, sensor 0, sensor 1, sensor 2} on sub-lane
     // k % Q, slot k / Q -- one block per lane for Q = 4 -- then broadcast by DPP.
@@ -999,7 +1024,7 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     int ohit = -1;
     bool onew = false;
     if (OBST) {
-        ohit = obst_detect(kp, myob, d.pos[0], d.pos[1]);
+        ohit = obst_detect(og, myob, d.pos[0], d.pos[1]);
         onew = active && ohit >= 0 && !(d.flags & QS_FL_PREV_OBST);
         rw += kpm.quadcol_obst * (onew ? -1.f : 0.f);
         d.flags = (d.flags & ~(uint32_t)QS_FL_PREV_OBST) | (ohit >= 0 ? (uint32_t)QS_FL_PREV_OBST : 0u);
@@ -1081,7 +1106,7 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
         if (OBST && onew) {   // perform_collision_with_obstacle, drones in ascending order (:680-689)
             float z[20], u[8];
             qdraws<Q, 5, 2>(rng, gid, S_OBST, S_OBST, q, z, u);
-            collide_obstacle(kp, d, myob[ohit].x, myob[ohit].y, z, u);
+            collide_obstacle(kp, og, d, myob[ohit].x, myob[ohit].y, z, u);
             vchanged = true;
         }
         if (active && (wall_new || ceil_new)) {
@@ -1144,7 +1169,7 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     }
     QS_STAMP(6);
     if (nbr) neighbor_obs<NPAD, Q>(kp, xch, dbase, di, q, d.pos, d.vel, active, row);
-    if (OBST && lead) sdf_obs(kp, myob, d.pos[0], d.pos[1], row + kp.obs_dim - 9);   // MultiObstacles.step
+    if (OBST && lead) sdf_obs(kp, og, myob, d.pos[0], d.pos[1], row + kp.obs_dim - 9);   // MultiObstacles.step
     QS_STAMP(7);
 
     const uint64_t dball = __ballot(active && done);
@@ -1159,9 +1184,17 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
         lds_sync();
         float sv[3] = {d.vel[0], d.vel[1], d.vel[2]};  // QuadrotorEnvMulti.vel seen by the reset (:477)
         if (OBST) {   // new obstacle map + scenario per finished env (one lane each)
-            if (active && done && di == 0 && q == 0)
+            if (active && done && di == 0 && q == 0) {
+                oscr[el].mi = omi;
+                oscr[el].si = osi;
                 obstacle_reset_env(kp, rng, kp.id0 + (uint32_t)(env * kp.N), oscr + el, otile + el * kp.M);
+                if (kp.dr) {
+                    b.env[QS_E_OBST_M * kp.E + env] = oscr[el].mi;
+                    b.env[QS_E_OBST_SZ * kp.E + env] = oscr[el].si;
+                }
+            }
             lds_sync();
+            if (active && done && kp.dr) og = ogeo(kp, oscr[el].mi, oscr[el].si);
         }
         if (SCEN) {   // scenario.reset() of every finished env (its lead lane), goals into the LDS table
             if (active && done && di == 0 && q == 0) {
@@ -1191,7 +1224,7 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
             neighbor_obs<NPAD, Q>(kp, xch, dbase, di, q, d.pos, sv, active && done, row);
         }
         if (OBST && lead && done) {
-            sdf_obs(kp, myob, d.pos[0], d.pos[1], row + kp.obs_dim - 9);   // MultiObstacles.reset
+            sdf_obs(kp, og, myob, d.pos[0], d.pos[1], row + kp.obs_dim - 9);   // MultiObstacles.reset
             if (di == 0)
                 for (int o = 0; o < kp.M; ++o) b.obst[(size_t)env * kp.M + o] = myob[o];
         }
@@ -1250,7 +1283,15 @@ __global__ __launch_bounds__(64) void reset_kernel(const KP* __restrict__ kpp, B
     float2* otile = obst_tile(lds, kp, 64);
     ObstScratch* oscr = reinterpret_cast<ObstScratch*>(otile + EPB * kp.M);
     if (OBST) {
-        if (sel && di == 0) obstacle_reset_env(kp, rng, kp.id0 + (uint32_t)(env * kp.N), oscr + el, otile + el * kp.M);
+        if (sel && di == 0) {
+            oscr[el].mi = kp.dr ? b.env[QS_E_OBST_M * kp.E + env] : 0;
+            oscr[el].si = kp.dr ? b.env[QS_E_OBST_SZ * kp.E + env] : 0;
+            obstacle_reset_env(kp, rng, kp.id0 + (uint32_t)(env * kp.N), oscr + el, otile + el * kp.M);
+            if (kp.dr) {
+                b.env[QS_E_OBST_M * kp.E + env] = oscr[el].mi;
+                b.env[QS_E_OBST_SZ * kp.E + env] = oscr[el].si;
+            }
+        }
         lds_sync();
     }
     float* stab = scen_tab(lds, kp, 64) + el * scen_stride<NPAD>();
@@ -1280,7 +1321,7 @@ __global__ __launch_bounds__(64) void reset_kernel(const KP* __restrict__ kpp, B
     }
     if (OBST && sel) {
         const float2* myob = otile + el * kp.M;
-        sdf_obs(kp, myob, d.pos[0], d.pos[1], row + kp.obs_dim - 9);   // MultiObstacles.reset
+        sdf_obs(kp, ogeo(kp, oscr[el].mi, oscr[el].si), myob, d.pos[0], d.pos[1], row + kp.obs_dim - 9);   // MultiObstacles.reset
         if (di == 0)
             for (int o = 0; o < kp.M; ++o) b.obst[(size_t)env * kp.M + o] = myob[o];
     }

@@ -26,6 +26,8 @@ enum : uint32_t {
     S_OBSTMAP = 21, S_OSCEN = 22,
     // flavor-B goal scenarios, per env (key = drone 0): one word per draw in call order
     S_SCN = 23, S_SCN_RESET = 24,
+    // obstacle domain randomisation, per env (key = drone 0): uniform 0 density choice, 1 size choice
+    S_DR = 26,
     UNIF_BIT = 0x80
 };
 

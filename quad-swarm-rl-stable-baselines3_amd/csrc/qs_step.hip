@@ -133,6 +133,15 @@ static int validate(const qs_config* c) {
             if (c->num_obstacles < 1 || c->num_obstacles + c->num_agents > c->obst_area * c->obst_area)
                 return fail(QS_E_INVALID, "num_obstacles must leave a free cell per drone");
             if (c->obst_size <= 0.f || c->sdf_resolution <= 0.f) return fail(QS_E_INVALID, "bad obst_size / sdf_resolution");
+            if (c->dr_num_counts < 0 || c->dr_num_counts > QS_MAX_DR_CHOICES || c->dr_num_sizes < 0 ||
+                c->dr_num_sizes > QS_MAX_DR_CHOICES)
+                return fail(QS_E_INVALID, "dr_num_counts / dr_num_sizes must be in [0, QS_MAX_DR_CHOICES]");
+            for (int i = 0; i < c->dr_num_counts; ++i)
+                if (c->dr_counts[i] != -1 &&
+                    (c->dr_counts[i] < 1 || c->dr_counts[i] + c->num_agents > c->obst_area * c->obst_area))
+                    return fail(QS_E_INVALID, "dr_counts entries: -1 (keep) or pillars leaving a free cell per drone");
+            for (int i = 0; i < c->dr_num_sizes; ++i)
+                if (!(c->dr_sizes[i] >= 0.f)) return fail(QS_E_INVALID, "dr_sizes entries must be >= 0 (0 = keep)");
         } else if (c->scenario != QS_SCEN_STATIC_SAME_GOAL &&
                    (c->scenario < QS_SCEN_MIX || c->scenario > QS_SCEN_RUN_AWAY)) {
             return fail(QS_E_UNSUPPORTED, "flavor B without obstacles: static_same_goal, mix or a goal scenario");
@@ -159,6 +168,13 @@ static int npad_of(int n);
 static size_t shm_bytes(const qs_config& c, int obs_dim, int npad, bool step);
 static int neighbor_dim(int t);
 
+// pillar slots per env: the configured count, or the largest domain-randomisation choice
+static int obst_slots(const qs_config* c) {
+    int m = c->num_obstacles;
+    for (int i = 0; i < c->dr_num_counts && i < QS_MAX_DR_CHOICES; ++i) m = c->dr_counts[i] > m ? c->dr_counts[i] : m;
+    return m;
+}
+
 static qs_layout make_layout(const qs_config* c) {
     qs_layout L;
     memset(&L, 0, sizeof L);
@@ -173,7 +189,7 @@ static qs_layout make_layout(const qs_config* c) {
     L.istate = o; o = al(o + sizeof(int32_t) * QS_NI * I);
     L.env = o; o = al(o + sizeof(int32_t) * QS_NE * E);
     L.env_f = o; o = al(o + sizeof(float) * QS_NENVF * E);
-    L.obst = o; o = al(o + sizeof(float) * 2 * (c->use_obstacles ? (size_t)c->num_obstacles : 0) * E);
+    L.obst = o; o = al(o + sizeof(float) * 2 * (c->use_obstacles ? (size_t)obst_slots(c) : 0) * E);
     L.stale_vel = o; o = al(o + sizeof(float) * 3 * I);
     L.obs = o; o = al(o + sizeof(float) * I * od);
     L.term_obs = o; o = al(o + sizeof(float) * I * od);
@@ -317,10 +333,20 @@ static qs::KP make_kp(const qs_config* c, const qs_layout& L) {
         k.scen_b = c->scenario == QS_SCEN_MIX ? 10 : c->scenario - QS_SCEN_MIX;
     if (c->flavor == QS_FLAVOR_A) make_kp_a(c, k);
     if (c->use_obstacles) {
-        k.obst = 1; k.M = c->num_obstacles; k.obst_n = c->obst_area;
+        k.obst = 1; k.M = obst_slots(c); k.obst_n = c->obst_area;
         k.obst_scen = c->scenario == QS_SCEN_OBST_MIX ? 0 : (c->scenario == QS_SCEN_O_RANDOM ? 1 : 2);
         k.obst_r = 0.5f * c->obst_size;
         k.obst_thr = (float)((double)c->arm + 0.5 * (double)c->obst_size);   // quad arm + pillar radius
+        // domain randomisation tables: index 0 = the configured pillars, choice c = index c + 1
+        k.dr_nm = c->dr_num_counts; k.dr_ns = c->dr_num_sizes;
+        k.dr = (k.dr_nm > 0 || k.dr_ns > 0) ? 1 : 0;
+        k.dr_m[0] = c->num_obstacles; k.dr_r[0] = k.obst_r; k.dr_thr[0] = k.obst_thr;
+        for (int i = 0; i < k.dr_nm; ++i) k.dr_m[i + 1] = c->dr_counts[i];
+        for (int i = 0; i < k.dr_ns; ++i) {
+            const float sz = c->dr_sizes[i];
+            k.dr_r[i + 1] = sz > 0.f ? 0.5f * sz : 0.f;   // 0 = a falsy 0.0 choice: keep the env's size
+            k.dr_thr[i + 1] = sz > 0.f ? (float)((double)c->arm + 0.5 * (double)sz) : 0.f;
+        }
         k.obst_z = 0.5f * c->room_hi[2];                                       // pillar centre (:423)
         k.sdf_res = c->sdf_resolution;
         k.quadcol_obst = c->rew_quadcol_bin_obst;
@@ -435,7 +461,7 @@ static int envs_per_block(const qs_config& c, int npad, bool step) {
 static size_t shm_bytes(const qs_config& c, int obs_dim, int npad, bool step) {
     const size_t epb = (size_t)envs_per_block(c, npad, step), slots = epb * (size_t)npad;
     size_t b = sizeof(float) * slots * (size_t)obs_dim + sizeof(float) * slots * 8 + sizeof(float) * 64;
-    if (c.use_obstacles) b += epb * (sizeof(float) * 2 * (size_t)c.num_obstacles + (size_t)qs::QS_OBST_SCRATCH);
+    if (c.use_obstacles) b += epb * (sizeof(float) * 2 * (size_t)obst_slots(&c) + (size_t)qs::QS_OBST_SCRATCH);
     else if (c.flavor == QS_FLAVOR_B && c.scenario >= QS_SCEN_MIX)   // goal tables (qs::scen_stride)
         b += epb * sizeof(float) * 2 * ((size_t)npad + 4) * 4;
     return b;
@@ -589,9 +615,9 @@ static int launch_replay(qs_handle* h, bool step, const uint8_t* mask, hipStream
 }
 
 static size_t snap_words(const qs_config* c, int obs_dim) {
+    const size_t M = c->use_obstacles ? (size_t)obst_slots(c) : 0;
     const size_t N = (size_t)c->num_agents;
-    return N * (QS_NF + QS_NI + 3 + (size_t)obs_dim) + QS_NE + QS_NENVF +
-           (c->use_obstacles ? 2 * (size_t)c->num_obstacles : 0);
+    return N * (QS_NF + QS_NI + 3 + (size_t)obs_dim) + QS_NE + QS_NENVF + 2 * M;
 }
 
 extern "C" int qs_replay_config_default(qs_replay_config* rc, float control_dt) {

@@ -9,8 +9,9 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("QUADSWARM_LIB", os.path.join(HERE, "lib", "libquadswarm.so"))
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 MAX_AGENTS = 32
+MAX_DR_CHOICES = 8
 F, I32, U32, U64, SZ = ctypes.c_float, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_size_t
 
 # enum values (quadswarm.h)
@@ -36,7 +37,8 @@ I_SVD, I_FLAGS, I_PREV_LO, I_PREV_HI, NI = 0, 1, 2, 3, 4
 FL_ON_FLOOR, FL_PREV_WALL, FL_PREV_CEIL, FL_CRASH_FLOOR, FL_CRASH_WALL, FL_CRASH_CEIL = 1, 2, 4, 8, 16, 32
 FL_PREV_OBST = 64
 E_TICK, E_FLAGS, E_EPISODE = 0, 1, 2
-E_SC_MODE, E_SC_FORM, E_SC_PERIOD, E_SC_INC, NE = 3, 4, 5, 6, 7
+E_SC_MODE, E_SC_FORM, E_SC_PERIOD, E_SC_INC = 3, 4, 5, 6
+E_OBST_M, E_OBST_SZ, NE = 7, 8, 9
 EF_STALE, EF_SUCCESS, EF_HAS_POS, EF_NEWCOL, EF_FLOOR0 = 1, 2, 4, 8, 16
 ENVF_TARGET_X, ENVF_TARGET_Y, ENVF_CAPTURE = 0, 1, 2
 ENVF_SC_SIZE, ENVF_SC_LO, ENVF_SC_HI, ENVF_SC_LAYER, ENVF_SC_SPEED = 3, 4, 5, 6, 7
@@ -65,6 +67,8 @@ class QsConfig(ctypes.Structure):
         ("capture_radius", F), ("cam_size", F), ("cam_focal", F), ("cam_px_noise", F), ("cam_fov_deg", F), ("cam_res", F),
         ("use_obstacles", I32), ("num_obstacles", I32), ("obst_area", I32), ("obst_size", F), ("sdf_resolution", F),
         ("rew_quadcol_bin_obst", F),
+        ("dr_num_counts", I32), ("dr_counts", I32 * MAX_DR_CHOICES), ("dr_num_sizes", I32),
+        ("dr_sizes", F * MAX_DR_CHOICES),
     ]
 
 

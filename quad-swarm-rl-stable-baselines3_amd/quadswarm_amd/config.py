@@ -60,6 +60,16 @@ class QuadSwarmConfig:
     obst_collision_reward: float = 5.0        # quadcol_bin_obst
     # ---- experience replay (quad_utils.py:34, 68-71: on when > 0; the reference's swarm runs use 0.75) ----
     replay_buffer_sample_prob: float = 0.0
+    # ---- obstacle domain randomisation (quadrotor_params.py:62-72 / global_cfg.py:85-91), applied by the replay
+    # wrapper's reset (quad_experience_replay.py:76-87, 106-118, 206-214): only with replay on, as the
+    # reference only builds the wrapper then (quad_utils.py:68-71) ----
+    domain_random: bool = False
+    obst_density_random: bool = False
+    obst_density_min: float = 0.05
+    obst_density_max: float = 0.2
+    obst_size_random: bool = False
+    obst_size_min: float = 0.3
+    obst_size_max: float = 0.6
 
     @classmethod
     def c4(cls, num_envs=4096, num_agents=8, **over):
@@ -120,7 +130,15 @@ class QuadSwarmConfig:
             obst_density=g("obst_density", "quads_obst_density", default=0.2),
             obst_size=g("obst_size", "quads_obst_size", default=0.6),
             obst_spawn_area=tuple(g("obst_spawn_area", "quads_obst_spawn_area", default=(8, 8))),
-            obst_collision_reward=g("obst_collision_reward", "quads_obst_collision_reward", default=5.0))
+            obst_collision_reward=g("obst_collision_reward", "quads_obst_collision_reward", default=5.0),
+            replay_buffer_sample_prob=g("replay_buffer_sample_prob", default=0.0) or 0.0,
+            domain_random=bool(g("domain_random", "quads_domain_random", default=False)),
+            obst_density_random=bool(g("obst_density_random", "quads_obst_density_random", default=False)),
+            obst_density_min=g("obst_density_min", "quads_obst_density_min", default=0.05),
+            obst_density_max=g("obst_density_max", "quads_obst_density_max", default=0.2),
+            obst_size_random=bool(g("obst_size_random", "quads_obst_size_random", default=False)),
+            obst_size_min=g("obst_size_min", "quads_obst_size_min", default=0.3),
+            obst_size_max=g("obst_size_max", "quads_obst_size_max", default=0.6))
         if flavor == "A":
             # quadrotor_multi_rewards builds its dynamics from cfg.dynamics_change only (the
             # thrust_noise_ratio it computes at :46-49 is never used), default Crazyflie noise 0.05
@@ -161,6 +179,30 @@ class QuadSwarmConfig:
         return int(self.obst_density * self.obst_spawn_area[0] * self.obst_spawn_area[1])
 
     @property
+    def domain_random_active(self):
+        return bool(self.use_obstacles and self.replay_buffer_sample_prob > 0 and self.domain_random
+                    and (self.obst_density_random or self.obst_size_random))
+
+    def domain_random_tables(self):
+        """(densities, pillar counts, sizes) of the replay wrapper's choice lists: np.arange(min, max, 0.05) /
+        np.arange(min, max, 0.1) (quad_experience_replay.py:82, 86), count = int(area^2 * density)
+        (quadrotor_multi.py:414).  A 0.0 choice is falsy at quadrotor_multi.py:443-446, i.e. the env keeps its
+        current value: count -1 / size 0.0.  Empty lists when that randomisation is off."""
+        import numpy as np
+        dens = np.arange(self.obst_density_min, self.obst_density_max, 0.05) if self.obst_density_random else np.zeros(0)
+        sizes = np.arange(self.obst_size_min, self.obst_size_max, 0.1) if self.obst_size_random else np.zeros(0)
+        cells = int(self.obst_spawn_area[0]) * int(self.obst_spawn_area[1])
+        counts = [int(cells * d) if d else -1 for d in dens]
+        return dens, counts, sizes
+
+    @property
+    def max_obstacles(self):
+        """Pillar slots per env: the configured count or the largest domain-randomisation choice."""
+        if not self.domain_random_active:
+            return self.num_obstacles
+        return max([self.num_obstacles] + self.domain_random_tables()[1])
+
+    @property
     def scenario_id(self):
         if self.use_obstacles:
             return {"mix": N.SCENARIO["obst_mix"], "o_random": N.SCENARIO["o_random"],
@@ -199,6 +241,12 @@ class QuadSwarmConfig:
             a = self.obst_spawn_area
             if a[0] != a[1] or int(a[0]) != a[0] or not 1 <= a[0] <= 8:
                 raise NotImplementedError("obst_spawn_area must be a square of 1..8 cells")
+            if self.domain_random_active:
+                dens, counts, sizes = self.domain_random_tables()
+                if len(dens) > N.MAX_DR_CHOICES or len(sizes) > N.MAX_DR_CHOICES:
+                    raise NotImplementedError(f"at most {N.MAX_DR_CHOICES} domain-randomisation choices per list")
+                if any(c == 0 for c in counts):
+                    raise ValueError("a density choice gives 0 pillars (the reference's obstacle arrays break)")
         if self.flavor == "A":
             if self.quads_mode not in ("dynamic_repulsive", "static_same_goal"):
                 raise NotImplementedError(f"quads_mode {self.quads_mode!r} not implemented for flavor A "
@@ -273,4 +321,12 @@ class QuadSwarmConfig:
             c.obst_size = self.obst_size
             c.rew_quadcol_bin_obst = self.obst_collision_reward
             c.spawn_box = 0.1   # QuadrotorSingle.box with obstacles (quadrotor_single.py:238-241)
+            if self.domain_random_active:
+                dens, counts, sizes = self.domain_random_tables()
+                c.dr_num_counts = len(counts)
+                for i, v in enumerate(counts):
+                    c.dr_counts[i] = v
+                c.dr_num_sizes = len(sizes)
+                for i, v in enumerate(sizes):
+                    c.dr_sizes[i] = float(v)
         return c

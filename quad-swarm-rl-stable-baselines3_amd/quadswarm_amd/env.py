@@ -55,7 +55,7 @@ class QuadSwarmEnv:
         self.env_state = view(lay.env, 4 * N.NE * E, torch.int32, (N.NE, E))
         self.env_f = view(lay.env_f, 4 * N.NENVF * E, torch.float32, (N.NENVF, E))
         self.reset_info = view(lay.reset_info, E, torch.uint8, (E,))
-        M = cfg.num_obstacles if cfg.use_obstacles else 0
+        M = cfg.max_obstacles if cfg.use_obstacles else 0   # pillar slots (an env uses its first QS_E_OBST_M)
         self.obstacles = view(lay.obst, 8 * M * E, torch.float32, (E, M, 2)) if M else None
         self.stale_vel = view(lay.stale_vel, 4 * 3 * I, torch.float32, (3, I))
         self.obs = view(lay.obs, 4 * I * od, torch.float32, (I, od))

@@ -55,6 +55,13 @@ def oracle_params(cfg: QuadSwarmConfig):
         p.sdf_resolution = 0.1
         p.rew_quadcol_bin_obst = cfg.obst_collision_reward
         p.spawn_box = 0.1
+        if cfg.domain_random_active:   # table index 0 = the configured value, choice c = index c + 1
+            _, counts, sizes = cfg.domain_random_tables()
+            p.dr_n_counts, p.dr_n_sizes = len(counts), len(sizes)
+            for c, v in enumerate(counts):
+                p.dr_counts[c + 1] = v
+            for c, v in enumerate(sizes):
+                p.dr_sizes[c + 1] = float(v)
     elif cfg.quads_mode != "static_same_goal":   # flavor-B goal scenarios
         p.scenario_b = O.SC_MIX if cfg.quads_mode == "mix" else O.SC_MODES.index(cfg.quads_mode)
     return p
@@ -127,7 +134,8 @@ def gpu_to_oracle(env, oenv):
         ev.tick = int(es[NAT.E_TICK, e])
         ev.episode = int(es[NAT.E_EPISODE, e])
         if ob is not None:
-            ev.n_obst = ob.shape[1]
+            ev.obst_mi, ev.obst_si = int(es[NAT.E_OBST_M, e]), int(es[NAT.E_OBST_SZ, e])
+            ev.n_obst = oenv.p.dr_counts[ev.obst_mi] if ev.obst_mi > 0 else oenv.p.num_obstacles
             for o in range(ob.shape[1]):
                 ev.obst[o][0], ev.obst[o][1] = ob[e, o, 0], ob[e, o, 1]
         stale_valid = bool(es[NAT.E_FLAGS, e] & 1)
@@ -169,6 +177,7 @@ def oracle_to_gpu(oenv, env):
         es[NAT.E_TICK, e] = ev.tick
         es[NAT.E_EPISODE, e] = ev.episode
         es[NAT.E_FLAGS, e] = 1      # neighbour reset obs read stale_vel (== oracle obs_vel)
+        es[NAT.E_OBST_M, e], es[NAT.E_OBST_SZ, e] = ev.obst_mi, ev.obst_si
         for i in range(N):
             g = e * N + i
             prev = 0

@@ -156,3 +156,63 @@ def test_full_size_c4_properties():
         assert torch.isfinite(obs).all()
         dones += int(done.sum())
     assert dones == 32768   # ep_len 50: every env reset once inside the run
+
+
+# ---------------------------------------------------------------- obstacle domain randomisation
+DR_RUN = dict(replay_buffer_sample_prob=0.75, domain_random=True, obst_density_random=True, obst_size_random=True,
+              obst_density_min=0.05, obst_density_max=0.2, obst_size_min=0.3, obst_size_max=0.6)   # obst_domain_random.py
+DR_ZERO = dict(DR_RUN, obst_density_min=0.0, obst_size_min=0.0)   # 0.0 choices: falsy, the env keeps its value
+
+
+def assert_obstacles_match(env, oenv):
+    """Per env: the domain-randomisation indices, then the env's first n pillar slots."""
+    es = env.env_state.cpu().numpy()
+    ob = np_(env.obstacles)
+    for e in range(oenv.E):
+        ev = oenv.envs[e]
+        assert (int(es[NAT.E_OBST_M, e]), int(es[NAT.E_OBST_SZ, e])) == (ev.obst_mi, ev.obst_si), e
+        want = np.array([[ev.obst[o][0], ev.obst[o][1]] for o in range(ev.n_obst)])
+        np.testing.assert_array_equal(ob[e, :ev.n_obst], want)
+
+
+@pytest.mark.parametrize("dr", [DR_RUN, DR_ZERO], ids=["run", "zero_choices"])
+def test_domain_random_resets_match_oracle(dr):
+    cfg, env, oenv = make_pair(E=512, **dr)
+    assert env.obstacles.shape[1] == cfg.max_obstacles
+    for r in range(3):   # explicit resets: each draws a (density, size) pair per env (wrapper.reset)
+        obs = np_(env.reset())
+        want = oenv.reset()
+        assert_obstacles_match(env, oenv)
+        np.testing.assert_allclose(obs, want, atol=2e-5, rtol=1e-5)
+    counts = {oenv.envs[e].n_obst for e in range(oenv.E)}
+    sizes = {oenv.envs[e].obst_si for e in range(oenv.E)}
+    assert len(counts) >= 3 and len(sizes) >= 3
+
+
+def test_domain_random_steps_from_identical_state():
+    """Fused auto-resets draw new (density, size) pairs (the replay wrapper's new_episode); SDF obs, pillar
+    hits and impulses use each env's own pillar count and radius."""
+    cfg, env, oenv = make_pair(E=256, episode_duration=0.3, **DR_RUN)
+    env.reset()
+    oenv.reset()
+    rng = np.random.default_rng(7)
+    crowd(oenv, rng, walls=False)
+    aim_at_obstacles(oenv, rng)
+    K = cfg.k_neighbors
+    so = NAT.SELF_OBS_DIM[NAT.OBS_REPR[cfg.obs_repr]]
+    stats = dict(done=0, obst=0)
+    for t in range(12):
+        oracle_to_gpu(oenv, env)
+        a = rng.uniform(-1, 1, (env.I, 4)).astype(np.float32)
+        obs, rew, done, term = env.step(torch.from_numpy(a).cuda())
+        w_obs, w_rew, w_done, w_term = oenv.step(a.astype(np.float64))
+        np.testing.assert_array_equal(done.cpu().numpy().astype(bool), w_done)
+        np.testing.assert_allclose(np_(rew), w_rew, atol=2e-4, rtol=1e-4)
+        g_obs = np_(obs)
+        np.testing.assert_allclose(g_obs[:, -9:], w_obs[:, -9:], atol=2e-4, rtol=1e-4)
+        assert_obs_match(g_obs[:, :-9], w_obs[:, :-9], oenv, so, K)
+        assert_obstacles_match(env, oenv)
+        stats["done"] += int(w_done.sum())
+        stats["obst"] += int((w_rew < -2.0).sum())
+        gpu_to_oracle(env, oenv)
+    assert stats["done"] > 0 and stats["obst"] > 0

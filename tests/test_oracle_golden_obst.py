@@ -102,6 +102,18 @@ def test_obstacle_impulse(golden):
     assert inside > 5
 
 
+def apply_dr(p, envs, g):
+    """A fixture reset with env.reset(obst_density, obst_size) (the domain-randomisation wrapper's choice):
+    the pair becomes table entry 1 and the env's current indices point at it.  Tape mode replays the bare
+    env, so the oracle does not draw the choice; the env's in-env resets keep it."""
+    if "dr_density" not in g or float(g["dr_density"]) == 0.0:
+        return
+    p.dr_n_counts, p.dr_n_sizes = 1, 1
+    p.dr_counts[1] = int(p.obst_area * p.obst_area * float(g["dr_density"]))   # quadrotor_multi.py:414
+    p.dr_sizes[1] = float(g["dr_size"])
+    envs[0].obst_mi, envs[0].obst_si = 1, 1
+
+
 def load_traj_obst(golden, name, which="init"):
     g = golden("obst_traj_" + name)
     n, k = int(g["n"]), int(g["k"])
@@ -127,15 +139,17 @@ def load_traj_obst(golden, name, which="init"):
         envs[0].obst[o][0], envs[0].obst[o][1] = ob[o][0], ob[o][1]
     envs[0].obst_mode = int(g[w + "mode"])
     envs[0].tick = int(g[w + "tick"])
+    apply_dr(p, envs, g)
     return g, p, drones, envs
 
 
-@pytest.mark.parametrize("name", ["c4", "n4none"])
+@pytest.mark.parametrize("name", ["c4", "n4none", "dr3", "dr9"])
 def test_first_reset_with_obstacles(golden, name):
     g, p, _, _ = load_traj_obst(golden, name)
     n = p.num_agents
     od = O.lib().or_obs_dim(ctypes.byref(p))
     drones, envs = O.drones_array(n), O.envs_array(1)
+    apply_dr(p, envs, g)
     tape = O.TapeRng(g["tape0"], g["spawn0"])
     obs = np.zeros((n, od))
     O.lib().or_env_reset(ctypes.byref(p), drones, envs, 0, tape.ref, O.dptr(obs))
@@ -147,7 +161,7 @@ def test_first_reset_with_obstacles(golden, name):
     assert envs[0].obst_mode == int(g["init_mode"])
 
 
-@pytest.mark.parametrize("name", ["c4", "n4none"])
+@pytest.mark.parametrize("name", ["c4", "n4none", "dr3", "dr9"])
 def test_trajectory_with_obstacles(golden, name):
     g, p, drones, envs = load_traj_obst(golden, name)
     n = p.num_agents
@@ -168,3 +182,21 @@ def test_trajectory_with_obstacles(golden, name):
     assert tape.r.tape_pos == len(g["tape"])
     assert tape.r.spawn_pos == len(g["spawn"])
     assert n_obst_hits >= 1
+
+
+def test_domain_random_tables(golden):
+    """The wrapper's choice lists (np.arange, quad_experience_replay.py:82, 86) and the pillar counts the env
+    makes of them (int(area^2 * density), quadrotor_multi.py:414), as the host config computes them; a 0.0
+    choice is falsy at quadrotor_multi.py:443-446 and keeps the env's value (-1 / 0 in the tables)."""
+    from quadswarm_amd import QuadSwarmConfig
+    t = golden("obst_dr_tables")
+    for i in range(int(t["n_ranges"])):
+        dlo, dhi, slo, shi = t["range_%d" % i]
+        cfg = QuadSwarmConfig.c4(num_envs=4, replay_buffer_sample_prob=0.75, domain_random=True,
+                                 obst_density_random=True, obst_size_random=True, obst_density_min=dlo,
+                                 obst_density_max=dhi, obst_size_min=slo, obst_size_max=shi)
+        dens, counts, sizes = cfg.domain_random_tables()
+        np.testing.assert_array_equal(dens, t["densities_%d" % i])
+        np.testing.assert_array_equal(sizes, t["sizes_%d" % i])
+        want = [c if d != 0.0 else -1 for c, d in zip(t["counts_%d" % i], t["densities_%d" % i])]
+        assert counts == want

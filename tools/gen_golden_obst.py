@@ -185,11 +185,11 @@ def setup_obst(env, rng):
         ds[5].pos = ds[4].pos + np.array([0.05, 0.03, 0.0])
 
 
-def gen_traj(name, n, k, steps, seed, ep_time, setup=None, hover=False, **kw):
+def gen_traj(name, n, k, steps, seed, ep_time, setup=None, hover=False, reset_kw=None, **kw):
     np.random.seed(seed)
     env = make_env_obst(n, k, seed=seed, ep_time=ep_time, **kw)
     G.begin()
-    obs0, _ = env.reset()
+    obs0, _ = env.reset(**(reset_kw or {}))
     tv0, sp0 = G.end()
     if setup is not None:
         setup(env, np.random.default_rng(seed + 100))
@@ -212,11 +212,47 @@ def gen_traj(name, n, k, steps, seed, ep_time, setup=None, hover=False, **kw):
                         obs0=np.array(obs0, dtype=np.float64), n=n, k=k, ep_len=env.envs[0].ep_len,
                         downwash=int(kw.get("downwash", True)), sense=int(kw.get("sense", "default") == "default"),
                         thrust_noise=kw.get("thrust_noise", 0.05),
+                        dr_density=float((reset_kw or {}).get("obst_density") or 0.0),
+                        dr_size=float((reset_kw or {}).get("obst_size") or 0.0),
                         **{"init_" + a: b for a, b in init.items()}, **{"final_" + a: b for a, b in final.items()})
+
+
+DR_RANGES = [(0.05, 0.2, 0.3, 0.6),    # runs/obstacles/obst_domain_random.py (= the quadrotor_params defaults)
+             (0.0, 0.2, 0.0, 0.6),     # a zero choice: falsy at quadrotor_multi.py:443-446, keeps the env's value
+             (0.1, 0.35, 0.2, 0.9)]
+
+
+def gen_dr():
+    """Obstacle domain randomisation (quad_experience_replay.py:76-87, 106-118): the choice lists the reference's
+    wrapper builds (np.arange) for DR_RANGES, then env.reset(obst_density, obst_size) with a chosen pair followed by
+    a trajectory whose in-env resets keep the pair (quadrotor_multi.py:440-450, 836)."""
+    import gym_art.quadrotor_multi.quad_experience_replay as XR
+    env = make_env_obst(8, 2, seed=60)
+    tabs = {}
+    for i, (dlo, dhi, slo, shi) in enumerate(DR_RANGES):
+        w = XR.ExperienceReplayWrapper(env, 0.75, 0.2, 0.6, True, True, True, dlo, dhi, slo, shi)
+        tabs[f"range_{i}"] = np.array([dlo, dhi, slo, shi])
+        tabs[f"densities_{i}"] = np.asarray(w.obst_densities, dtype=np.float64)
+        tabs[f"sizes_{i}"] = np.asarray(w.obst_sizes, dtype=np.float64)
+        # int(num_room_grids * density) of obst_generation_given_density (quadrotor_multi.py:414)
+        counts = []
+        for d in w.obst_densities:
+            env.obst_density = d
+            counts.append(len(env.obst_generation_given_density()[1]))
+        tabs[f"counts_{i}"] = np.array(counts, dtype=np.int64)
+    np.savez_compressed(os.path.join(OUT, "obst_dr_tables.npz"), n_ranges=len(DR_RANGES), **tabs)
+    d0, s0 = tabs["densities_0"], tabs["sizes_0"]
+    gen_traj("dr3", 8, 2, 90, seed=61, ep_time=0.3, setup=setup_obst,
+             reset_kw=dict(obst_density=d0[0], obst_size=s0[1]))
+    gen_traj("dr9", 8, 2, 90, seed=62, ep_time=0.3, setup=setup_obst,
+             reset_kw=dict(obst_density=d0[2], obst_size=s0[2]))
 
 
 def main():
     os.makedirs(OUT, exist_ok=True)
+    if len(sys.argv) > 1 and sys.argv[1] == "dr":
+        gen_dr()
+        return
     gen_sdf()
     gen_maps()
     gen_impulse()

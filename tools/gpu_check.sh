@@ -37,6 +37,7 @@ for s in "$@"; do
     benchc3) step bench_c3 400 python bench.py --config c3 --steps 2000 --cpu-seconds 10 ;;
     replay) step gpu_replay 600 python -u -m pytest tests/test_gpu_replay.py tests/test_gpu_parity.py -x -v --timeout 300 --timeout-method thread ;;
     benchmixr) step bench_c3mixr 400 python bench.py --config c3mixr --steps 2000 --cpu-seconds 5 --e2e-iters 0 ;;
+    benchc4dr) step bench_c4dr 400 python bench.py --config c4dr --steps 1000 --cpu-seconds 5 --e2e-iters 0 ;;
     benchmix) step bench_c3mix 400 python bench.py --config c3mix --steps 2000 --cpu-seconds 10 --e2e-iters 0 ;;
     prof)
       export TMPDIR=/tmp
