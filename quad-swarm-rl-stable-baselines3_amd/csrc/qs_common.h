@@ -161,25 +161,35 @@ __device__ __forceinline__ void sincos_hw(float x, float* s, float* c) {
 // ---------------------------------------------------------------------------------------------
 // state I/O (SoA, coalesced per field)
 // ---------------------------------------------------------------------------------------------
+// SoA field f of drone g as (uniform field base, 32-bit byte offset g * 4): the base lives in SGPRs and
+// every field shares one offset VGPR, so the loads/stores use the saddr form (global_load_dword v, voff,
+// s[base]) instead of one 64-bit VGPR address per field.
+template <typename T>
+__device__ __forceinline__ T ld_field(const T* base, int f, int I, uint32_t boff) {
+    return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base + (size_t)f * (size_t)I) + boff);
+}
+
 __device__ __forceinline__ void load_drone(const KP& kp, const Bufs& b, int g, Drone& d) {
-    const float* s = b.st + g;
+    const float* s = b.st;
     const int I = kp.I;
+    const uint32_t bo = (uint32_t)g * 4u;
 #pragma unroll
-    for (int i = 0; i < 3; ++i) { d.pos[i] = s[(QS_F_POS + i) * I]; d.vel[i] = s[(QS_F_VEL + i) * I]; }
+    for (int i = 0; i < 3; ++i) { d.pos[i] = ld_field(s, QS_F_POS + i, I, bo); d.vel[i] = ld_field(s, QS_F_VEL + i, I, bo); }
 #pragma unroll
-    for (int i = 0; i < 9; ++i) d.rot[i] = s[(QS_F_ROT + i) * I];
+    for (int i = 0; i < 9; ++i) d.rot[i] = ld_field(s, QS_F_ROT + i, I, bo);
 #pragma unroll
-    for (int i = 0; i < 3; ++i) { d.om[i] = s[(QS_F_OMEGA + i) * I]; d.goal[i] = s[(QS_F_GOAL + i) * I]; }
+    for (int i = 0; i < 3; ++i) { d.om[i] = ld_field(s, QS_F_OMEGA + i, I, bo); d.goal[i] = ld_field(s, QS_F_GOAL + i, I, bo); }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        d.rd[i] = s[(QS_F_ROT_DAMP + i) * I];
-        d.cd[i] = s[(QS_F_CMD_DAMP + i) * I];
-        d.ou[i] = s[(QS_F_OU + i) * I];
+        d.rd[i] = ld_field(s, QS_F_ROT_DAMP + i, I, bo);
+        d.cd[i] = ld_field(s, QS_F_CMD_DAMP + i, I, bo);
+        d.ou[i] = ld_field(s, QS_F_OU + i, I, bo);
     }
-    const int32_t* is = b.ist + g;
-    d.svd = is[QS_I_SVD * I];
-    d.flags = (uint32_t)is[QS_I_FLAGS * I];
-    d.prev = (uint64_t)(uint32_t)is[QS_I_PREV_LO * I] | ((uint64_t)(uint32_t)is[QS_I_PREV_HI * I] << 32);
+    const int32_t* is = b.ist;
+    d.svd = ld_field(is, QS_I_SVD, I, bo);
+    d.flags = (uint32_t)ld_field(is, QS_I_FLAGS, I, bo);
+    d.prev = (uint64_t)(uint32_t)ld_field(is, QS_I_PREV_LO, I, bo) |
+             ((uint64_t)(uint32_t)ld_field(is, QS_I_PREV_HI, I, bo) << 32);
 }
 
 // Write-through (sc1) stores: the bytes leave the XCD's L2 during the kernel instead of being
@@ -199,35 +209,40 @@ __device__ __forceinline__ void st_wt4(float4* p, float4 v) {
     *p = v;
 #endif
 }
+// field f of a SoA array at (uniform base, lane byte offset), write-through, saddr form.  The s_nop 4:
+// the base SGPRs may have just been written by a VALU (v_readlane of a spilled SGPR), and a VMEM read of
+// such an SGPR needs 5 wait states, which the compiler's hazard recognizer does not insert for inline asm.
 template <typename T>
-__device__ __forceinline__ void st_state(T* p, T v) {
+__device__ __forceinline__ void st_field(T* base, int f, int I, uint32_t boff, T v) {
+    T* fb = base + (size_t)f * (size_t)I;   // uniform
 #if QS_WT_STATE
-    asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+    asm volatile("s_nop 4\n\tglobal_store_dword %0, %1, %2 sc1" ::"v"(boff), "v"(v), "s"(fb) : "memory");
 #else
-    *p = v;
+    *reinterpret_cast<T*>(reinterpret_cast<char*>(fb) + boff) = v;
 #endif
 }
 
 __device__ __forceinline__ void store_drone(const KP& kp, const Bufs& b, int g, const Drone& d) {
-    float* s = b.st + g;
+    float* s = b.st;
     const int I = kp.I;
+    const uint32_t bo = (uint32_t)g * 4u;
 #pragma unroll
-    for (int i = 0; i < 3; ++i) { st_state(&s[(QS_F_POS + i) * I], d.pos[i]); st_state(&s[(QS_F_VEL + i) * I], d.vel[i]); }
+    for (int i = 0; i < 3; ++i) { st_field(s, QS_F_POS + i, I, bo, d.pos[i]); st_field(s, QS_F_VEL + i, I, bo, d.vel[i]); }
 #pragma unroll
-    for (int i = 0; i < 9; ++i) st_state(&s[(QS_F_ROT + i) * I], d.rot[i]);
+    for (int i = 0; i < 9; ++i) st_field(s, QS_F_ROT + i, I, bo, d.rot[i]);
 #pragma unroll
-    for (int i = 0; i < 3; ++i) { st_state(&s[(QS_F_OMEGA + i) * I], d.om[i]); st_state(&s[(QS_F_GOAL + i) * I], d.goal[i]); }
+    for (int i = 0; i < 3; ++i) { st_field(s, QS_F_OMEGA + i, I, bo, d.om[i]); st_field(s, QS_F_GOAL + i, I, bo, d.goal[i]); }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        st_state(&s[(QS_F_ROT_DAMP + i) * I], d.rd[i]);
-        st_state(&s[(QS_F_CMD_DAMP + i) * I], d.cd[i]);
-        st_state(&s[(QS_F_OU + i) * I], d.ou[i]);
+        st_field(s, QS_F_ROT_DAMP + i, I, bo, d.rd[i]);
+        st_field(s, QS_F_CMD_DAMP + i, I, bo, d.cd[i]);
+        st_field(s, QS_F_OU + i, I, bo, d.ou[i]);
     }
-    int32_t* is = b.ist + g;
-    st_state(&is[QS_I_SVD * I], d.svd);
-    st_state(&is[QS_I_FLAGS * I], (int32_t)d.flags);
-    st_state(&is[QS_I_PREV_LO * I], (int32_t)(uint32_t)d.prev);
-    st_state(&is[QS_I_PREV_HI * I], (int32_t)(uint32_t)(d.prev >> 32));
+    int32_t* is = b.ist;
+    st_field(is, QS_I_SVD, I, bo, d.svd);
+    st_field(is, QS_I_FLAGS, I, bo, (int32_t)d.flags);
+    st_field(is, QS_I_PREV_LO, I, bo, (int32_t)(uint32_t)d.prev);
+    st_field(is, QS_I_PREV_HI, I, bo, (int32_t)(uint32_t)(d.prev >> 32));
 }
 
 // ---------------------------------------------------------------------------------------------

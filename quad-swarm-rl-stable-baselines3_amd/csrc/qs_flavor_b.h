@@ -883,6 +883,104 @@ __device__ __forceinline__ float2* obst_tile(float* lds, const KP& kp, int slots
 }
 
 // Geometry of the flavor-B step kernel: Q lanes per drone (Q * NPAD <= 64), EPB envs per wave.
+// Cooperative state load / store of the Q sub-lanes of a drone (flavor-B step).  The drone's 37 state
+// words (33 fp32 fields QS_F_POS .. QS_F_GOAL, then 4 int fields QS_I_*) are dealt over the sub-lanes:
+// instruction t moves word t*Q + q on sub-lane q, so a wave instruction covers Q fields x its drones and
+// the drone needs ceil(37 / Q) load / store instructions instead of 37.  Loaded words are broadcast to
+// every sub-lane by DPP (every sub-lane holds the whole drone).  Addresses are b.st (SGPRs) + a 32-bit
+// per-lane byte offset: the int fields are reached through their offset from b.st (istate follows state
+// in the handle's workspace, qs_step.hip layout).
+#ifndef QS_COOP_STATE
+#define QS_COOP_STATE 1
+#endif
+constexpr int DRONE_WORDS = QS_F_GOAL + 3 + 4;
+
+template <int Q, int W, int T>
+__device__ __forceinline__ void qbc_words(const uint32_t (&r)[T], uint32_t* wv) {
+    if constexpr (W < DRONE_WORDS) {
+        wv[W] = (uint32_t)__float_as_int(qbc<Q, W % Q>(__int_as_float((int)r[W / Q])));
+        qbc_words<Q, W + 1, T>(r, wv);
+    }
+}
+
+__device__ __forceinline__ uint32_t drone_word_off(const KP& kp, const Bufs& b, int w, uint32_t go) {
+    const uint32_t I4 = (uint32_t)kp.I * 4u;
+    const uint32_t ist0 = (uint32_t)((const char*)b.ist - (const char*)b.st);
+    return (w < QS_F_GOAL + 3 ? (uint32_t)w * I4 : ist0 + (uint32_t)(w - QS_F_GOAL - 3) * I4) + go;
+}
+
+template <int Q>
+__device__ __forceinline__ void load_drone_q(const KP& kp, const Bufs& b, int g, int q, Drone& d) {
+    constexpr int T = (DRONE_WORDS + Q - 1) / Q;
+    const uint32_t go = (uint32_t)g * 4u;
+    uint32_t r[T];
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        const int w = t * Q + q;
+        r[t] = w < DRONE_WORDS ? *reinterpret_cast<const uint32_t*>((const char*)b.st + drone_word_off(kp, b, w, go)) : 0u;
+    }
+    uint32_t wv[DRONE_WORDS];
+    qbc_words<Q, 0, T>(r, wv);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        d.pos[i] = __int_as_float((int)wv[QS_F_POS + i]); d.vel[i] = __int_as_float((int)wv[QS_F_VEL + i]);
+        d.om[i] = __int_as_float((int)wv[QS_F_OMEGA + i]); d.goal[i] = __int_as_float((int)wv[QS_F_GOAL + i]);
+    }
+#pragma unroll
+    for (int i = 0; i < 9; ++i) d.rot[i] = __int_as_float((int)wv[QS_F_ROT + i]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        d.rd[i] = __int_as_float((int)wv[QS_F_ROT_DAMP + i]);
+        d.cd[i] = __int_as_float((int)wv[QS_F_CMD_DAMP + i]);
+        d.ou[i] = __int_as_float((int)wv[QS_F_OU + i]);
+    }
+    constexpr int IW = QS_F_GOAL + 3;
+    d.svd = (int32_t)wv[IW + QS_I_SVD];
+    d.flags = wv[IW + QS_I_FLAGS];
+    d.prev = (uint64_t)wv[IW + QS_I_PREV_LO] | ((uint64_t)wv[IW + QS_I_PREV_HI] << 32);
+}
+
+template <int Q>
+__device__ __forceinline__ void store_drone_q(const KP& kp, const Bufs& b, int g, int q, bool active, const Drone& d) {
+    uint32_t wv[DRONE_WORDS];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        wv[QS_F_POS + i] = (uint32_t)__float_as_int(d.pos[i]); wv[QS_F_VEL + i] = (uint32_t)__float_as_int(d.vel[i]);
+        wv[QS_F_OMEGA + i] = (uint32_t)__float_as_int(d.om[i]); wv[QS_F_GOAL + i] = (uint32_t)__float_as_int(d.goal[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < 9; ++i) wv[QS_F_ROT + i] = (uint32_t)__float_as_int(d.rot[i]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        wv[QS_F_ROT_DAMP + i] = (uint32_t)__float_as_int(d.rd[i]);
+        wv[QS_F_CMD_DAMP + i] = (uint32_t)__float_as_int(d.cd[i]);
+        wv[QS_F_OU + i] = (uint32_t)__float_as_int(d.ou[i]);
+    }
+    constexpr int IW = QS_F_GOAL + 3;
+    wv[IW + QS_I_SVD] = (uint32_t)d.svd;
+    wv[IW + QS_I_FLAGS] = d.flags;
+    wv[IW + QS_I_PREV_LO] = (uint32_t)d.prev;
+    wv[IW + QS_I_PREV_HI] = (uint32_t)(d.prev >> 32);
+    constexpr int T = (DRONE_WORDS + Q - 1) / Q;
+    const uint32_t go = (uint32_t)g * 4u;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        const int w = t * Q + q;
+        uint32_t v = wv[t * Q];
+#pragma unroll
+        for (int k = 1; k < Q; ++k)
+            if (q == k && t * Q + k < DRONE_WORDS) v = wv[t * Q + k];
+        if (active && w < DRONE_WORDS) {
+            const uint32_t off = drone_word_off(kp, b, w, go);
+#if QS_WT_STATE
+            asm volatile("s_nop 4\n\tglobal_store_dword %0, %1, %2 sc1" ::"v"(off), "v"(v), "s"(b.st) : "memory");
+#else
+            *reinterpret_cast<uint32_t*>((char*)b.st + off) = v;
+#endif
+        }
+    }
+}
+
 template <int NPAD>
 struct StepGeo {
     static constexpr int Q = NPAD >= 32 ? 2 : 4;
@@ -921,7 +1019,11 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
         for (int k = lane; k < nenv_blk * kp.M; k += 64) otile[k] = b.obst[(size_t)env0 * kp.M + k];
 
     Drone d;   // every sub-lane holds the whole drone
+#if QS_COOP_STATE
+    load_drone_q<Q>(kp, b, g, q, d);
+#else
     load_drone(kp, b, g, d);
+#endif
     float a[4];
     {
         const float4 av = reinterpret_cast<const float4*>(b.act)[g];
@@ -1234,8 +1336,12 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     tile_store(lds, b.obs + (size_t)env0 * kp.N * kp.obs_dim, rows * kp.obs_dim, lane);
     QS_STAMP(9);
 
+#if QS_COOP_STATE
+    store_drone_q<Q>(kp, b, g, q, active, d);
+#else
+    if (lead) store_drone(kp, b, g, d);
+#endif
     if (lead) {
-        store_drone(kp, b, g, d);
         b.rew[g] = rw;
         b.done[g] = done ? 1 : 0;
         if (di == 0) {
