@@ -2,6 +2,7 @@
 // rewards, drone/room impulses, pos_vel neighbour obs, in-env auto-reset).  Included by qs_step.hip.
 #pragma once
 #include "qs_common.h"
+#include "qs_replay.h"
 
 namespace qs {
 
@@ -990,7 +991,7 @@ struct StepGeo {
 };
 
 template <int NPAD, bool OBST>
-__global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bufs b, uint32_t seed) {
+__global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bufs b, uint32_t seed, RBufs r, RP rp) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     QS_BIND_KP(kpp);
     QS_STAMP_DECL
@@ -1356,6 +1357,13 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
         }
     }
     QS_STAMP(10);
+    if (r.ri != nullptr) {   // experience replay on (uniform): ExperienceReplayWrapper.step of every env (:124-180)
+        // the step's global stores above are read back by other lanes of the wave: workgroup-scope
+        // release/acquire (one wave per workgroup, one L1)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        if (env < kp.E) replay_env<true>(kp, b, r, rp, seed, env, lane % LPE, LPE);
+    }
     QS_STAMP(11);
     QS_RTSTAMP(13);
     QS_STAMP_FLUSH();

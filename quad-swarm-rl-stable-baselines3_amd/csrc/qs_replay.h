@@ -2,8 +2,9 @@
 //
 // Replaces ExperienceReplayWrapper / ReplayBuffer (gym_art/quadrotor_multi/quad_experience_replay.py:16-216) and
 // the env-side bookkeeping they read (quadrotor_multi.py:182-185 state, :382-388 can_drones_fly, :461-465 reset
-// accounting, :722-725 crash accumulation).  RL = 16 lanes per env (4 envs per wavefront, 16 per workgroup),
-// launched after the step (or reset) kernel on the same stream.  The decision logic is a handful of per-env
+// accounting, :722-725 crash accumulation).  replay_env() runs one env on RL of its lanes: fused into the tail
+// of the flavor-B step kernel (the env's RL = Q * NPAD lanes, after the step's stores and a workgroup fence),
+// and as replay_kernel<false> (RL = 16, 4 envs per wavefront) after qs_reset.  The decision logic is a handful of per-env
 // integers: the env's lanes evaluate it redundantly from broadcast loads (no cross-lane exchange) and its
 // first lane writes what changed; the RL lanes then move whole env snapshots (copy loops of snap_words
 // 32-bit words) when a checkpoint is saved, an event is written or an episode is replayed.  A step with
@@ -58,16 +59,17 @@ __device__ __forceinline__ uint32_t* snap_word(const KP& kp, const Bufs& b, int 
     return reinterpret_cast<uint32_t*>(b.obs) + (size_t)e * N * kp.obs_dim + w;
 }
 
-constexpr int RL = 16;   // lanes per env
+constexpr int RL = 16;   // lanes per env of the standalone replay kernel
 
-__device__ __forceinline__ void snap_save(const KP& kp, const Bufs& b, int e, uint32_t* dst, int W, int lane) {
+__device__ __forceinline__ void snap_save(const KP& kp, const Bufs& b, int e, uint32_t* dst, int W, int lane, int RL) {
     for (int w = lane; w < W; w += RL) {
         bool ep;
         dst[w] = *snap_word(kp, b, e, w, &ep);
     }
 }
 
-__device__ __forceinline__ void snap_restore(const KP& kp, const Bufs& b, int e, const uint32_t* src, int W, int lane) {
+__device__ __forceinline__ void snap_restore(const KP& kp, const Bufs& b, int e, const uint32_t* src, int W, int lane,
+                                             int RL) {
     for (int w = lane; w < W; w += RL) {
         bool ep;
         uint32_t* p = snap_word(kp, b, e, w, &ep);
@@ -90,12 +92,10 @@ __device__ __forceinline__ int hist_push(const RP& rp, const RBufs& r, int E, in
 
 // STEP: after step_kernel (one ExperienceReplayWrapper.step per env, :124-180).
 // !STEP: after reset_kernel (ExperienceReplayWrapper.reset -> env.reset accounting, :109-122) of the masked envs.
+// One env on RL of its lanes (lane in [0, RL)): no barriers or cross-lane exchange inside.
 template <bool STEP>
-__global__ __launch_bounds__(256) void replay_kernel(const KP* __restrict__ kpp, Bufs b, RBufs r, RP rp, uint32_t seed) {
-    const KP& kp = *kpp;
-    const int lane = threadIdx.x % RL;
-    const int e = blockIdx.x * (256 / RL) + threadIdx.x / RL;
-    if (e >= kp.E) return;   // no barriers below: lanes of absent envs just leave
+__device__ __forceinline__ void replay_env(const KP& kp, const Bufs& b, const RBufs& r, const RP& rp, uint32_t seed,
+                                           int e, int lane, int RL) {
     const int E = kp.E;
     const bool w0 = lane == 0;
     int32_t* ri = r.ri;
@@ -154,7 +154,7 @@ __global__ __launch_bounds__(256) void replay_kernel(const KP* __restrict__ kpp,
             const int pos = (int)(((2ull * (q.w[1] >> 8) + 1ull) * (uint64_t)buf_n) >> 25);
             const int phys = r.perm[(size_t)pos * E + e];
             const int nr = r.nrep[(size_t)phys * E + e] + 1;
-            snap_restore(kp, b, e, st + (size_t)(rp.keep + phys) * W, W, lane);
+            snap_restore(kp, b, e, st + (size_t)(rp.keep + phys) * W, W, lane, RL);
             // cleanup (:47-54) keeps the events replayed fewer than max_rep times, in order.  Every other
             // event is already below the limit, so only the sampled one can go: it moves to the first free
             // position and the later events shift down one.
@@ -179,7 +179,7 @@ __global__ __launch_bounds__(256) void replay_kernel(const KP* __restrict__ kpp,
         if (w0) ri[QS_R_EPISODES * E + e] = episodes;
     } else {
         if (active && !saved && tick % rp.cp_every == 0) {   // save_checkpoint (:97-102, :157-159)
-            snap_save(kp, b, e, st + (size_t)ck_head * W, W, lane);
+            snap_save(kp, b, e, st + (size_t)ck_head * W, W, lane, RL);
             ck_head = (ck_head + 1) % rp.keep;
             ck_n = min(ck_n + 1, rp.keep);
         }
@@ -221,6 +221,14 @@ __global__ __launch_bounds__(256) void replay_kernel(const KP* __restrict__ kpp,
         put(QS_R_PUSHED, pushed, ri[QS_R_PUSHED * E + e]);
         if (crash != crash0) r.crash[e] = crash;
     }
+}
+
+template <bool STEP>
+__global__ __launch_bounds__(256) void replay_kernel(const KP* __restrict__ kpp, Bufs b, RBufs r, RP rp, uint32_t seed) {
+    const KP& kp = *kpp;
+    const int e = blockIdx.x * (256 / RL) + threadIdx.x / RL;
+    if (e >= kp.E) return;   // no barriers: lanes of absent envs just leave
+    replay_env<STEP>(kp, b, r, rp, seed, e, threadIdx.x % RL, RL);
 }
 
 }  // namespace qs

@@ -568,8 +568,11 @@ static int launch(qs_handle* h, bool step, const float* act, const uint8_t* mask
     const dim3 grid((unsigned)((h->kp.E + epb - 1) / epb)), block(64);
     const size_t shm = shm_bytes(h->cfg, h->kp.obs_dim, h->npad, step);
     const bool a = h->cfg.flavor == QS_FLAVOR_A, ob = h->kp.obst != 0;
+    // the flavor-B step kernel runs the replay wrapper in its tail (qs_replay.h); rb.ri == NULL: replay off
+    qs::RBufs rb = h->rws ? h->rb : qs::RBufs{};
+    qs::RP rp = h->rp;
     if (hipFunction_t f = step ? h->jit_step : h->jit_reset) {
-        void* args[] = {(void*)&kpd, (void*)&b, (void*)&seed};
+        void* args[] = {(void*)&kpd, (void*)&b, (void*)&seed, (void*)&rb, (void*)&rp};   // the last two: B step only
         QS_HIP(hipModuleLaunchKernel(f, grid.x, 1, 1, block.x, 1, 1, (unsigned)shm, s, args, nullptr));
         return QS_OK;
     }
@@ -579,10 +582,10 @@ static int launch(qs_handle* h, bool step, const float* act, const uint8_t* mask
             if (step) hipLaunchKernelGGL(qs::step_kernel_a<NP>, grid, block, shm, s, kpd, b, seed);            \
             else hipLaunchKernelGGL(qs::reset_kernel_a<NP>, grid, block, shm, s, kpd, b, seed);                \
         } else if (ob) {                                                                                       \
-            if (step) hipLaunchKernelGGL((qs::step_kernel<NP, true>), grid, block, shm, s, kpd, b, seed);      \
+            if (step) hipLaunchKernelGGL((qs::step_kernel<NP, true>), grid, block, shm, s, kpd, b, seed, rb, rp); \
             else hipLaunchKernelGGL((qs::reset_kernel<NP, true>), grid, block, shm, s, kpd, b, seed);          \
         } else {                                                                                               \
-            if (step) hipLaunchKernelGGL((qs::step_kernel<NP, false>), grid, block, shm, s, kpd, b, seed);     \
+            if (step) hipLaunchKernelGGL((qs::step_kernel<NP, false>), grid, block, shm, s, kpd, b, seed, rb, rp); \
             else hipLaunchKernelGGL((qs::reset_kernel<NP, false>), grid, block, shm, s, kpd, b, seed);         \
         }                                                                                                      \
         break;
@@ -765,9 +768,8 @@ extern "C" int qs_step(qs_handle* h, const float* d_actions, void* stream) {
         return fail(QS_E_INVALID, "actions must be 16-byte aligned [I,4] fp32");
     }
     QS_HIP(hipSetDevice(h->device));
-    int rc = launch(h, true, d_actions, nullptr, (hipStream_t)stream);
-    if (rc == QS_OK && h->rws) rc = launch_replay(h, true, nullptr, (hipStream_t)stream);
-    return rc;
+    // with replay on, the flavor-B step kernel runs the wrapper in its tail (no second launch)
+    return launch(h, true, d_actions, nullptr, (hipStream_t)stream);
 }
 
 static float* param_slot(qs_handle* h, const char* key) {
