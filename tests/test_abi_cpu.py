@@ -88,6 +88,39 @@ def test_validation_errors_are_reported():
         N.check(L.qs_layout_query(bad, lay), "qs_layout_query")
 
 
+DR = dict(replay_buffer_sample_prob=0.75, domain_random=True, obst_density_random=True, obst_size_random=True)
+
+
+def test_domain_random_config_and_layout():
+    """Obstacle domain randomisation: on only with replay (the reference builds the wrapper only then),
+    pillar slots = the largest count, tables in qs_config, bad entries rejected by the library."""
+    L = N.lib()
+    off = QuadSwarmConfig.c4(num_envs=16, domain_random=True, obst_density_random=True)   # no replay
+    assert not off.domain_random_active and off.to_qs_config().dr_num_counts == 0
+    cfg = QuadSwarmConfig.c4(num_envs=16, obst_density_max=0.35, **DR)
+    dens, counts, sizes = cfg.domain_random_tables()
+    assert counts == [3, 6, 9, 12, 16, 19] and cfg.max_obstacles == 19
+    c = cfg.to_qs_config()
+    assert c.dr_num_counts == 6 and list(c.dr_counts[:6]) == counts
+    assert c.dr_num_sizes == 3 and np.allclose(list(c.dr_sizes[:3]), [0.3, 0.4, 0.5])
+    lay, lay0 = N.QsLayout(), N.QsLayout()
+    assert L.qs_layout_query(c, lay) == 0
+    assert L.qs_layout_query(QuadSwarmConfig.c4(num_envs=16).to_qs_config(), lay0) == 0
+    assert lay.stale_vel - lay.obst >= 8 * 19 * 16 > lay0.stale_vel - lay0.obst - 256
+    for field, val in (("dr_num_counts", 9), ("dr_num_sizes", -1)):
+        bad = N.QsConfig.from_buffer_copy(c)
+        setattr(bad, field, val)
+        assert L.qs_layout_query(bad, lay) == -1
+    bad = N.QsConfig.from_buffer_copy(c)
+    bad.dr_counts[0] = 60          # no free cell left for 8 drones
+    assert L.qs_layout_query(bad, lay) == -1 and b"dr_counts" in L.qs_last_error()
+    bad = N.QsConfig.from_buffer_copy(c)
+    bad.dr_counts[0] = -1          # a 0.0 density choice: keep
+    assert L.qs_layout_query(bad, lay) == 0
+    with pytest.raises(ValueError):   # a density choice with 0 pillars
+        QuadSwarmConfig.c4(num_envs=4, obst_density_min=0.01, obst_density_max=0.02, **DR).to_qs_config()
+
+
 def test_config_rejects_unbuilt_or_mixed_flavors():
     with pytest.raises(ValueError):   # a flavor-A repr on a flavor-B env
         QuadSwarmConfig(obs_repr="cdist_cdistdot_dist_distdot_sangle_angledot").to_qs_config()
