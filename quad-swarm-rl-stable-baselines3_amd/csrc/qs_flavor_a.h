@@ -299,9 +299,11 @@ __device__ __forceinline__ void rel_features(const KP& kp, const float4& pj, con
 // neighborhood_indices (:445-476) + extend_obs_space clip (:422-443).  k < N-1: selection by the norm
 // of the feature vector (clamped at 0.01, stable, NaN last) with its own camera noise, then the
 // selected pairs' features again with the obs-pass noise (the reference calls the camera twice).
-template <int NPAD>
+// Q > 1: the drone's sub-lane q writes the neighbours j with j % Q == q (same draws, same slots).
+template <int NPAD, int Q = 1>
 __device__ __forceinline__ void neighbor_obs_a(const KP& kp, const float4* xch, int base, int di, const float* P, float H, float aw,
-                               const float* V, const Rng& rng, uint32_t gid, bool reset, bool write, float* out) {
+                               const float* V, const Rng& rng, uint32_t gid, bool reset, bool write, float* out,
+                               int q = 0) {
     const bool sorted = kp.K < kp.N - 1;
     const uint32_t st_obs = reset ? S_RESET_CAM : S_CAM, st_sel = reset ? S_RESET_CAM_SEL : S_CAM_SEL;
     const int F = kp.nfd;
@@ -328,7 +330,7 @@ __device__ __forceinline__ void neighbor_obs_a(const KP& kp, const float4* xch, 
         } else {
             rank = j < di ? j : j - 1;
         }
-        if (valid && rank < kp.K) {
+        if (valid && rank < kp.K && (Q == 1 || j % Q == q)) {
             float* o = out + kp.so_dim + rank * F;
             rel_features(kp, xch[2 * (base + j)], xch[2 * (base + j) + 1], P, H, aw, V, rng, gid,
                          st_obs | ((uint32_t)j << 8),
@@ -337,27 +339,29 @@ __device__ __forceinline__ void neighbor_obs_a(const KP& kp, const float4* xch, 
     }
 }
 
-// segment (= env) helpers over the NPAD lanes of an env
-template <int NPAD>
+// segment (= env) helpers over the LPE = NPAD * Q lanes of an env (Q sub-lanes per drone)
+template <int LPE>
 __device__ __forceinline__ bool seg_any(bool x, int base) {
-    const uint64_t gm = (NPAD == 64) ? ~0ull : ((1ull << NPAD) - 1ull);
+    const uint64_t gm = (LPE == 64) ? ~0ull : ((1ull << LPE) - 1ull);
     return ((__ballot(x) >> base) & gm) != 0ull;
 }
-template <int NPAD>
-__device__ __forceinline__ float seg_sum(float v) {   // butterfly: every lane ends with the same bits
+// butterfly over the drones (lane distance Q .. LPE/2): every lane ends with the same bits, and the
+// summation tree is the one-lane-per-drone tree whatever Q is
+template <int NPAD, int Q = 1>
+__device__ __forceinline__ float seg_sum(float v) {
 #pragma unroll
-    for (int m = 1; m < NPAD; m <<= 1) v += __shfl_xor(v, m);
+    for (int m = Q; m < NPAD * Q; m <<= 1) v += __shfl_xor(v, m);
     return v;
 }
 
 // Scenario_dynamic_repulsive.step (dynamic_repulsive.py:37-62): target flees the chasers (1/d each)
 // and the arena edge, speed <= v_max.  Every lane of the env computes the same update.
-template <int NPAD>
+template <int NPAD, int Q = 1>
 __device__ __forceinline__ void target_step(const KP& kp, float& tx, float& ty, const float* pos, bool contrib) {
     const float r0 = tx - pos[0], r1 = ty - pos[1];
     const float d2 = r0 * r0 + r1 * r1;
-    const float fx = seg_sum<NPAD>(contrib ? r0 / d2 : 0.f);
-    const float fy = seg_sum<NPAD>(contrib ? r1 / d2 : 0.f);
+    const float fx = seg_sum<NPAD, Q>(contrib ? r0 / d2 : 0.f);
+    const float fy = seg_sum<NPAD, Q>(contrib ? r1 / d2 : 0.f);
     const float de = fsqrt(tx * tx + ty * ty);
     const float den = de * fmaxf(kp.arena - de, 0.1f);
     const float vx = fx - tx / den, vy = fy - ty / den;
@@ -371,7 +375,7 @@ __device__ __forceinline__ void target_step(const KP& kp, float& tx, float& ty, 
 // Scenario_dynamic_repulsive.reset (dynamic_repulsive.py:64-74, its step() sees the pre-reset chaser
 // positions) and QuadrotorSingle._reset (quadrotor_single_rewards.py:480-549).  All lanes of the
 // segment must call it (the target update is a segment reduction); `sel` lanes take the new state.
-template <int NPAD>
+template <int NPAD, int Q = 1>
 __device__ __forceinline__ void reset_env_a(const KP& kp, Drone& d, Ctl& c, float& tx, float& ty, bool has_pos, bool active,
                             bool sel, const Rng& rng, uint32_t gid, uint32_t genv) {
     float ru[4], ue[4];
@@ -380,7 +384,7 @@ __device__ __forceinline__ void reset_env_a(const KP& kp, Drone& d, Ctl& c, floa
         uniforms4(rng, genv, S_SCEN, 0, ue);
         const float a = ue[1] - 0.5f, b = ue[2] - 0.5f, in = rsqrtf(a * a + b * b), tr = ue[3] * 3.f + 2.f;
         float ntx = a * in * tr, nty = b * in * tr;
-        target_step<NPAD>(kp, ntx, nty, d.pos, active && has_pos);
+        target_step<NPAD, Q>(kp, ntx, nty, d.pos, active && has_pos);
         if (sel) {
             tx = ntx;
             ty = nty;
@@ -411,24 +415,56 @@ __device__ __forceinline__ void reset_env_a(const KP& kp, Drone& d, Ctl& c, floa
     d.flags = 0;
 }
 
+// Step geometry of flavor A: Q sub-lanes per drone (QS_QA, 2 by default; 64 / NPAD when an env would
+// not fit a wave).  4096 x 8 drones are then 1024 waves (one per SIMD) instead of 512.  The tick
+// chain (controller, physics) is replicated on the sub-lanes; the divisible work is dealt over them:
+// the per-tick OU blocks (sub-lane q draws tick t + q's block, DPP broadcast) and the neighbour
+// features (neighbour j on sub-lane j % Q).  Reductions over the env keep the one-lane-per-drone tree.
+#ifndef QS_QA
+#define QS_QA 2
+#endif
+// tick (t + k)'s OU normals from sub-lane k: k = 0 -> z, k >= 1 -> zn[k - 1]
+template <int Q, int K = 0>
+__device__ __forceinline__ void qbc_ticks(const float (&zr)[4], float (&z)[4], float (&zn)[Q > 1 ? Q - 1 : 1][4]) {
+    if constexpr (K < Q) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float v = qbc<Q, K>(zr[k]);
+            if constexpr (K == 0) z[k] = v;
+            else zn[K - 1][k] = v;
+        }
+        qbc_ticks<Q, K + 1>(zr, z, zn);
+    }
+}
+template <int NPAD>
+struct StepGeoA {
+    static constexpr int Q = NPAD * QS_QA <= 64 ? QS_QA : 64 / NPAD;
+    static constexpr int LPE = NPAD * Q;        // lanes per env
+    static constexpr int EPB = 64 / LPE;        // envs per workgroup (one wave)
+    static constexpr int SLOTS = EPB * NPAD;    // drone slots (LDS rows) per workgroup
+};
+
 template <int NPAD>
 __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, Bufs b, uint32_t seed) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     QS_BIND_KP(kpp);
-    constexpr int EPB = 64 / NPAD;
+    using G = StepGeoA<NPAD>;
+    constexpr int Q = G::Q, LPE = G::LPE, EPB = G::EPB, SLOTS = G::SLOTS;
     const int lane = threadIdx.x;
-    const int el = lane / NPAD, di = lane % NPAD;
+    const int el = lane / LPE, di = (lane % LPE) / Q, q = lane % Q;
     const int env0 = blockIdx.x * EPB;
     const int env = env0 + el;
     const bool active = env < kp.E && di < kp.N;
+    const bool lead = active && q == 0;   // the sub-lane that writes the drone's outputs
     const int g = active ? env * kp.N + di : 0;
     const uint32_t gid = kp.id0 + (uint32_t)g;
-    const int base = el * NPAD;
+    const int base = el * LPE;            // first lane of the env
+    const int sbase = el * NPAD;          // first drone slot of the env
     const int nenv_blk = min(EPB, kp.E - env0);
     const int rows = nenv_blk * kp.N;
     float* row = lds + (size_t)(el * kp.N + di) * kp.obs_dim;
-    float4* xch = reinterpret_cast<float4*>(lds + 64 * kp.obs_dim);
-    int* efin = reinterpret_cast<int*>(lds + 64 * kp.obs_dim + 64 * 8);
+    float4* xch = reinterpret_cast<float4*>(lds + SLOTS * kp.obs_dim);
+    int* efin = reinterpret_cast<int*>(lds + SLOTS * kp.obs_dim + SLOTS * 8);
 
     Drone d;
     load_drone(kp, b, g, d);
@@ -446,14 +482,28 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
     bool fin = false, success = eflags & QS_EF_SUCCESS;
     float rw = 0.f, gox = d.goal[0], goy = d.goal[1];
     bool dn = false;
+    float zn[Q > 1 ? Q - 1 : 1][4] = {};   // OU normals of the next Q - 1 ticks, drawn by sub-lanes 1 .. Q-1
 #pragma unroll 1   // 8 controller ticks: one copy of the body (I-cache), also when kp.ticks is a constant
     for (int sub = 0; sub < kp.ticks; ++sub) {
         if (fin) continue;   // the reference breaks out of its tick loop (:988); segment-uniform
         const Rng rng = env_rng(seed, tick, episode);
         float u[4];
         controller(kp, d, c, a0, d.goal[2], u);
-        float z[4];
-        normals4(rng, gid, S_OU, 0, z);  // QuadrotorDynamics.step: one OU draw per tick (:216)
+        float z[4];   // QuadrotorDynamics.step: one OU draw per tick (:216)
+        if constexpr (Q == 1) {
+            normals4(rng, gid, S_OU, 0, z);
+        } else if (sub % Q == 0) {   // wave-uniform: sub-lane q draws tick (tick + q)'s block
+            float zr[4];
+            normals4(env_rng(seed, tick + q, episode), gid, S_OU, 0, zr);
+            qbc_ticks<Q>(zr, z, zn);
+        } else {   // the next buffered tick, then shift the buffer (register moves, no dynamic index)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) z[k] = zn[0][k];
+#pragma unroll
+            for (int t = 0; t + 1 < Q - 1; ++t)
+#pragma unroll
+                for (int k = 0; k < 4; ++k) zn[t][k] = zn[t + 1][k];
+        }
 #pragma unroll
         for (int k = 0; k < 4; ++k) d.ou[k] = d.ou[k] + (kp.ou_theta * (kp.ou_mu - d.ou[k]) + kp.ou_sigma * z[k]);
         for (int s = 0; s < kp.sim_steps; ++s) substep(kp, d, u, d.ou, rng, gid, s);
@@ -465,15 +515,15 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
         const float dx = g0x - d.pos[0], dy = g0y - d.pos[1];
         const float rel = fsqrt(dx * dx + dy * dy);
         const bool capi = capr > rel;
-        const bool cap = seg_any<NPAD>(active && capi, base);
+        const bool cap = seg_any<LPE>(active && capi, base);
         const float captor = cap && capi ? kp.w_captor : 0.f;
         const float helper = cap && capr < rel ? kp.w_helper : 0.f;
         rw = ((0.f + captor) + helper) + kp.existence;
         dn = cap ? capi : (tick > kpm.ep_len);
-        fin = seg_any<NPAD>(active && dn, base);
+        fin = seg_any<LPE>(active && dn, base);
         success = success || cap;
         if (repulsive) {   // scenario.step() (:797)
-            target_step<NPAD>(kp, tx, ty, d.pos, active);
+            target_step<NPAD, Q>(kp, tx, ty, d.pos, active);
             d.goal[0] = tx;
             d.goal[1] = ty;
         }
@@ -481,12 +531,13 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
 
     // ---- observations of the final tick (self obs of the last _step, neighbours after the loop) ----
     const Rng rng_last = env_rng(seed, tick - 1, episode);
-    xch_put_a(xch, lane, d.pos, c.angle, d.vel);
+    if (q == 0) xch_put_a(xch, sbase + di, d.pos, c.angle, d.vel);
     if (lane < EPB) efin[lane] = 0;
     lds_sync();
-    if (fin && di == 0) efin[el] = 1;
-    if (active) self_obs_a(kp, d, c, gox, goy, rng_last, gid, S_SENSOR, S_SELF_CAM, row);
-    if (kp.K > 0) neighbor_obs_a<NPAD>(kp, xch, base, di, d.pos, c.angle, c.angle, d.vel, rng_last, gid, false, active, row);
+    if (fin && di == 0 && q == 0) efin[el] = 1;
+    if (lead) self_obs_a(kp, d, c, gox, goy, rng_last, gid, S_SENSOR, S_SELF_CAM, row);
+    if (kp.K > 0)
+        neighbor_obs_a<NPAD, Q>(kp, xch, sbase, di, d.pos, c.angle, c.angle, d.vel, rng_last, gid, false, active, row, q);
 
     const uint64_t fball = __ballot(active && fin);
     if (fball) {  // some env finished: terminal obs + the worker's reset (subproc_vec_env_custom.py:42-46)
@@ -499,8 +550,8 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
         lds_sync();
         const float sh = c.angle, sv[3] = {d.vel[0], d.vel[1], d.vel[2]};  // QuadrotorEnvMulti.heading / .vel
         const Rng rr = env_rng(seed, tick, episode);
-        reset_env_a<NPAD>(kp, d, c, tx, ty, true, active, active && fin, rr, gid, kp.id0 + (uint32_t)(env * kp.N));
-        if (active && fin) {
+        reset_env_a<NPAD, Q>(kp, d, c, tx, ty, true, active, active && fin, rr, gid, kp.id0 + (uint32_t)(env * kp.N));
+        if (lead && fin) {
             self_obs_a(kp, d, c, d.goal[0], d.goal[1], rr, gid, S_RESET_SENSOR, S_RESET_SELF_CAM, row);
             b.stale[0 * kp.I + g] = sv[0];
             b.stale[1 * kp.I + g] = sv[1];
@@ -508,15 +559,15 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
             b.st[QS_F_HEADING * kp.I + g] = sh;
         }
         if (kp.K > 0) {
-            xch_put_a(xch, lane, d.pos, sh, sv);
+            if (q == 0) xch_put_a(xch, sbase + di, d.pos, sh, sv);
             lds_sync();
-            neighbor_obs_a<NPAD>(kp, xch, base, di, d.pos, sh, c.angle, sv, rr, gid, true, active && fin, row);
+            neighbor_obs_a<NPAD, Q>(kp, xch, sbase, di, d.pos, sh, c.angle, sv, rr, gid, true, active && fin, row, q);
         }
     }
     lds_sync();
     tile_store(lds, b.obs + (size_t)env0 * kp.N * kp.obs_dim, rows * kp.obs_dim, lane);
 
-    if (active) {
+    if (lead) {
         store_drone(kp, b, g, d);
         store_ctl(kp, b, g, c);
         b.rew[g] = rw;

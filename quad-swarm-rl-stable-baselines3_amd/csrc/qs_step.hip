@@ -451,8 +451,12 @@ extern "C" int qs_layout_query(const qs_config* c, qs_layout* out) {
 // Flavor-B step launches give every drone Q lanes (qs::StepGeo); resets and flavor A one lane.
 static int step_lanes_per_drone(int npad) { return npad >= 32 ? 2 : 4; }
 static_assert(qs::StepGeo<8>::Q == 4 && qs::StepGeo<16>::Q == 4 && qs::StepGeo<32>::Q == 2, "step_lanes_per_drone");
+// flavor-A step launches: qs::StepGeoA (QS_QA sub-lanes per drone)
+static int step_lanes_per_drone_a(int npad) { return npad * QS_QA <= 64 ? QS_QA : 64 / npad; }
+static_assert(qs::StepGeoA<8>::Q == QS_QA && qs::StepGeoA<32>::Q == 2 && qs::StepGeoA<4>::Q == QS_QA,
+              "step_lanes_per_drone_a");
 static int envs_per_block(const qs_config& c, int npad, bool step) {
-    const int q = (step && c.flavor != QS_FLAVOR_A) ? step_lanes_per_drone(npad) : 1;
+    const int q = !step ? 1 : (c.flavor == QS_FLAVOR_A ? step_lanes_per_drone_a(npad) : step_lanes_per_drone(npad));
     return 64 / (npad * q);
 }
 
