@@ -18,6 +18,7 @@ Besides the required fields the JSON line carries:
                 of the flat gradient bucket per minibatch (N>1), max-over-ranks wall time
 """
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -70,6 +71,7 @@ def make_cfg(kw, **extra):
     return QuadSwarmConfig(**kw, **extra)
 
 
+STREAM_BLOCKS = {"c3": 4, "c3mix": 4, "c3mixr": 4, "c4": 4, "c4dr": 4}
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 
 
@@ -230,6 +232,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--graph", type=int, default=100, help="steps per captured hipGraph (0 = eager launches)")
+    ap.add_argument("--streams", type=int, default=0,
+                    help="env blocks per GPU, each its own handle on its own HIP stream (0 = 4 for flavor B, 1 for A)")
     ap.add_argument("--generic", action="store_true", help="generic kernels instead of qs_specialize (hipRTC)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -261,30 +265,82 @@ def main():
     env.reset()
 
     stream = torch.cuda.current_stream(dev)
-    graph = None
     chunk = args.graph if args.graph > 0 else 0
+    # 4 env blocks pay where a block still fills the chip (8-drone flavor B at 4096 envs: C3 8.4 -> 7.7 us,
+    # C4 13.6 -> 11.1 us per step); C2 (5.5 -> 6.1), C5 (14.7 -> 15.3) and flavor A (issue-bound, 29 -> 33)
+    # lose, so they keep one handle (profiles/r01_c3_streams.txt)
+    S = args.streams or STREAM_BLOCKS.get(args.config, 1)
+    if S > 1 and (cfg.num_envs % S or not chunk):
+        S = 1
+    # The shard is split into S env blocks, each its own handle keyed by its global drone ids (so the
+    # union draws exactly what the one big handle would) on its own HIP stream. Step t+1 of a block only
+    # waits for step t of the same block, so one block's next launch fills the CUs that another block's
+    # last waves leave idle (the launch tail is ~25 % of a one-handle step).
+    blocks = []
+    if S == 1:
+        blocks.append((env, actions, stream))
+    else:
+        Eb = cfg.num_envs // S
+        # HIP maps streams onto GPU_MAX_HW_QUEUES (= 4) hardware queues. Measured on MI355X
+        # (tools/exp_streams.py, profiles/r01_c3_streams.txt): the first user streams of a process take
+        # queues of their own and the one after them shares a queue with an earlier one (two blocks then
+        # serialise: 16 us instead of 7.6); once three streams exist, S = 4 consecutive new streams land on
+        # four different queues. So three streams are created and used once before the block streams.
+        hip = ctypes.CDLL("libamdhip64.so")
+
+        def raw_stream():
+            p = ctypes.c_void_p()
+            if hip.hipStreamCreateWithFlags(ctypes.byref(p), ctypes.c_uint(1)) != 0:  # hipStreamNonBlocking
+                raise RuntimeError("hipStreamCreateWithFlags failed")
+            return torch.cuda.ExternalStream(p.value, device=dev)
+        spare = [raw_stream() for _ in range(3)]
+        for st in spare:
+            with torch.cuda.stream(st):
+                torch.zeros(1, device=dev).add_(1)
+        torch.cuda.synchronize(dev)
+        bstreams = [raw_stream() for _ in range(S)]
+        for s in range(S):
+            cb = make_cfg(dict(kw, num_envs=Eb), seed=0, specialize=not args.generic)
+            cb.drone_id_offset = rank * I + s * Eb * cfg.num_agents
+            st = bstreams[s]
+            st.wait_stream(stream)
+            with torch.cuda.stream(st):
+                eb = QuadSwarmEnv(cb, device=dev)
+                eb.reset()
+            blocks.append((eb, actions[s * Eb * cfg.num_agents:(s + 1) * Eb * cfg.num_agents].contiguous(), st))
+        torch.cuda.synchronize(dev)
+    graphs = []
     if chunk:
-        # capture `chunk` steps into one hipGraph on a side stream (the RNG counter lives on the device)
-        for _ in range(3):
-            env.step(actions)
-        torch.cuda.synchronize(dev)
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            for _ in range(chunk):
-                env.step(actions)
-        torch.cuda.synchronize(dev)
+        # capture `chunk` steps per block into one hipGraph on the block's stream (the RNG counter lives
+        # on the device)
+        for eb, ab, st in blocks:
+            with torch.cuda.stream(st):
+                for _ in range(3):
+                    eb.step(ab)
+            torch.cuda.synchronize(dev)
+            g = torch.cuda.CUDAGraph()
+            # one block: capture on torch's side stream, replay on the current stream (as before)
+            with torch.cuda.graph(g, stream=st if S > 1 else None):
+                for _ in range(chunk):
+                    eb.step(ab)
+            torch.cuda.synchronize(dev)
+            graphs.append(g)
 
     def run(n):
-        if graph is None:
+        if not graphs:
             for _ in range(n):
                 env.step(actions)
             return n
         done = 0
         while done + chunk <= n:
-            graph.replay()
+            for (eb, ab, st), g in zip(blocks, graphs):
+                with torch.cuda.stream(st):
+                    g.replay()
             done += chunk
         for _ in range(n - done):
-            env.step(actions)
+            for eb, ab, st in blocks:
+                with torch.cuda.stream(st):
+                    eb.step(ab)
         return n
 
     run(args.warmup)
@@ -298,7 +354,11 @@ def main():
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(stream)
+    for _, _, st in blocks:
+        st.wait_stream(stream)
     run(args.steps)
+    for _, _, st in blocks:
+        stream.wait_stream(st)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
@@ -357,17 +417,22 @@ def main():
                        "obs_dim": cfg.obs_dim, "global_batch": world * I, "parallelism": f"env-shard x{world}",
                        "flavor": cfg.flavor,
                        "launch": (f"hipGraph of {chunk} steps" if chunk else "eager") +
+                                 (f" per env block, {S} blocks of {cfg.num_envs // S} envs on {S} HIP streams" if S > 1 else "") +
                                  (", specialised kernels (qs_specialize, hipRTC)" if env.specialized else ", generic kernels")},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
+                         "traffic_scope": "HBM bytes of one whole-shard step (PMC, one handle)",
                          "kernel": (f"qs::step_kernel_a<{npad(cfg.num_agents)}>" if cfg.flavor == "A" else
                                     f"qs::step_kernel<{npad(cfg.num_agents)}, {'true' if cfg.use_obstacles else 'false'}>"),
                          "kernel_us": round(k_ms * 1e3, 3),
-                         "kernel_us_source": "HIP events on the launch stream over the timed region / steps",
+                         "kernel_us_source": "HIP events on the launch stream over the timed region / steps"
+                         + (f" (one step = {S} concurrent launches of {cfg.num_envs // S} envs; achieved = bytes per"
+                            " step / step time, the aggregate rate of the overlapping launches)" if S > 1 else ""),
+                         "launches_per_step": S,
                          "kernel_us_eager_single": round(k_eager_ms * 1e3, 3),
                          "bytes_per_agent_step": round(bpa, 1),
-                         "bytes_per_launch": round(bpa * I)},
+                         "bytes_per_launch": round(bpa * I / S)},
             "cpu_baseline": None,
             "end_to_end": e2e,
         }
