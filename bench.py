@@ -247,7 +247,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    use_dist = world > 1 or os.environ.get("QS_BENCH_DIST") == "1"   # QS_BENCH_DIST: RCCL path at N=1 (rehearsal)
+    if use_dist:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
@@ -443,7 +444,7 @@ def main():
                 out["cpu_baseline"] = {"error": repr(e)}
         print(json.dumps(out), flush=True)
     env.close()
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 
