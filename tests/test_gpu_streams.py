@@ -11,6 +11,15 @@ pytestmark = pytest.mark.gpu
 
 
 def _cfg(kind, E, **over):
+    if kind == "c4dr":
+        return QuadSwarmConfig.c4(num_envs=E, num_agents=8, seed=5, episode_duration=0.3,
+                                  replay_buffer_sample_prob=0.75, domain_random=True, obst_density_random=True,
+                                  obst_size_random=True, obst_density_min=0.05, obst_density_max=0.2,
+                                  obst_size_min=0.3, obst_size_max=0.6, **over)
+    if kind == "c3mixr":
+        return QuadSwarmConfig(num_envs=E, num_agents=8, neighbor_visible_num=6, neighbor_obs_type="pos_vel",
+                               seed=5, episode_duration=0.3, quads_mode="mix", replay_buffer_sample_prob=0.75,
+                               **over)
     if kind == "c4":
         return QuadSwarmConfig.c4(num_envs=E, num_agents=8, seed=5, episode_duration=0.3, **over)
     if kind == "a8":
@@ -19,7 +28,7 @@ def _cfg(kind, E, **over):
                            seed=5, episode_duration=0.3, **over)
 
 
-@pytest.mark.parametrize("kind", ["c3", "c4", "a8"])
+@pytest.mark.parametrize("kind", ["c3", "c4", "a8", "c3mixr", "c4dr"])
 def test_stream_blocks_equal_one_handle(kind):
     E, S, N = 128, 4, 8
     big = QuadSwarmEnv(_cfg(kind, E))
@@ -34,7 +43,7 @@ def test_stream_blocks_equal_one_handle(kind):
     assert torch.equal(torch.cat(parts), ob)
     g = torch.Generator(device="cuda").manual_seed(3)
     rows = (E // S) * N
-    for t in range(30):
+    for t in range(60):
         act = (torch.rand(E * N, big.cfg.act_dim, device="cuda", generator=g) * 2 - 1).contiguous()
         ref = [x.clone() for x in big.step(act)[:3]]
         torch.cuda.synchronize()
