@@ -21,6 +21,7 @@ import argparse
 import ctypes
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -87,17 +88,18 @@ def algorithmic_bytes_per_agent_step(obs_dim, n_agents, flavor="B", n_obst=0):
     return 4 * (33 + 30 + 4 + obs_dim + 1) + 1 + 8.0 * n_obst / n_agents
 
 
-def cpu_baseline(cfg_kw, seconds=10.0):
-    """The C oracle (fp64, OpenMP over envs) on the same workload shape, time-bounded sample."""
+def cpu_worker(config, seconds):
+    """One cpu_baseline leg, run as a child process (bench.py --cpu-worker): the C oracle on this host's cores,
+    fp64 (liboracle.so) or its fp32 twin (liboracle_f32.so, QS_ORACLE_F32=1), OpenMP over envs with
+    OMP_NUM_THREADS threads, on the same workload shape as the GPU line; time-bounded sample."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle as O
     from parity_utils import oracle_params, oracle_params_a
 
-    cores = len(os.sched_getaffinity(0))
-    cores = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
-    cfg = make_cfg(cfg_kw)
+    threads = int(os.environ.get("OMP_NUM_THREADS", "1"))
+    cfg = make_cfg(CONFIGS[config])
     if cfg.flavor == "A":
         env = O.OracleEnvA(oracle_params_a(cfg), seed=0)
         env.set_capture_radius(cfg.initial_capture_radius)
@@ -105,14 +107,24 @@ def cpu_baseline(cfg_kw, seconds=10.0):
         env = O.OracleEnv(oracle_params(cfg), seed=0)
     env.reset()
     a = np.random.default_rng(1234).uniform(-1.0, 1.0, (cfg.num_envs * cfg.num_agents, cfg.act_dim))
-    env.step(a, nthreads=cores)
+    env.step(a, nthreads=threads)
     steps, t0 = 0, time.perf_counter()
     while True:
-        env.step(a, nthreads=cores)
+        env.step(a, nthreads=threads)
         steps += 1
         el = time.perf_counter() - t0
         if el >= seconds or steps >= 4000:
             break
+    print(json.dumps({"value": round(steps * cfg.num_envs * cfg.num_agents / el, 1), "steps": steps,
+                      "seconds": round(el, 2), "threads": threads, "fp32": O.F32}), flush=True)
+
+
+def cpu_baseline(config, seconds=6.0):
+    """SURVEY §8d CPU baseline: the oracle restatement on the GPU box's host cores, in three legs -- fp32
+    on 1 thread, fp32 on all usable threads (the headline `value`), fp64 on all threads (the parity
+    checker itself) -- each a child process with its own bounded sample."""
+    cores = len(os.sched_getaffinity(0))
+    cores = min(cores, int(os.environ.get("OMP_NUM_THREADS", cores)))
     model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -121,10 +133,22 @@ def cpu_baseline(cfg_kw, seconds=10.0):
                 break
     except OSError:
         pass
-    return {"value": round(steps * cfg.num_envs * cfg.num_agents / el, 1), "unit": "agent-steps/s", "cores": cores,
-            "kind": "port",
-            "sample": f"{steps} steps x {cfg.num_envs} envs x {cfg.num_agents} drones, fp64 C oracle, "
-                      f"{cores} OpenMP threads, {el:.1f} s on '{model}'"}
+    legs = {}
+    for name, f32, th in (("fp32_1t", True, 1), (f"fp32_{cores}t", True, cores), (f"fp64_{cores}t", False, cores)):
+        env = dict(os.environ, OMP_NUM_THREADS=str(th), QS_ORACLE_F32="1" if f32 else "0")
+        r = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-worker", "--config", config,
+                            "--cpu-seconds", str(seconds)], env=env, capture_output=True, text=True, timeout=600)
+        if r.returncode != 0:
+            raise RuntimeError(f"cpu leg {name} failed: {r.stderr[-400:]}")
+        legs[name] = json.loads(r.stdout.strip().splitlines()[-1])
+    cfg = make_cfg(CONFIGS[config])
+    head = legs[f"fp32_{cores}t"]
+    return {"value": head["value"], "unit": "agent-steps/s", "cores": cores, "kind": "port",
+            "precision": "fp32",
+            "sample": f"{head['steps']} steps x {cfg.num_envs} envs x {cfg.num_agents} drones, the C oracle's fp32 twin "
+                      f"(oracle/liboracle_f32.so), {cores} OpenMP threads, {head['seconds']} s on '{model}'",
+            "legs": {k: {"value": v["value"], "threads": v["threads"], "steps": v["steps"], "seconds": v["seconds"]}
+                     for k, v in legs.items()}}
 
 
 def npad(n):
@@ -225,21 +249,116 @@ def end_to_end(env, cfg, dev, world, iters, n_steps=None, log=None):
     }
 
 
+class Blocks:
+    """The GPU's env shard as S env blocks, each its own handle on its own HIP stream, stepped from
+    captured hipGraphs (or eagerly through qs_step_blocks).  S = 1 is the one handle on torch's
+    current stream."""
+
+    def __init__(self, torch, dev, entries, chunk):
+        self.torch, self.dev = torch, dev
+        self.entries = entries      # [(env, actions, stream)]
+        self.chunk = chunk
+        self.graphs = {}            # (block, steps) -> CUDAGraph
+        self.replays = self.eager_steps = 0
+
+    def _graph(self, i, n):
+        key = (i, n)
+        if key not in self.graphs:
+            eb, ab, st = self.entries[i]
+            g = self.torch.cuda.CUDAGraph()
+            # captured on the block's stream (one block: torch's capture side stream), replayed on it
+            with self.torch.cuda.graph(g, stream=st if len(self.entries) > 1 else None):
+                for _ in range(n):
+                    eb.step(ab)
+            self.torch.cuda.synchronize(self.dev)
+            self.graphs[key] = g
+        return self.graphs[key]
+
+    def prepare(self, lengths):
+        """capture every graph a run will replay before anything is timed"""
+        for n in lengths:
+            q, r = divmod(n, self.chunk) if self.chunk else (0, 0)
+            for i in range(len(self.entries)):
+                if q:
+                    self._graph(i, self.chunk)
+                if r:
+                    self._graph(i, r)
+
+    def run(self, n):
+        from quadswarm_amd.env import step_blocks
+        if not self.chunk:
+            envs = [e for e, _, _ in self.entries]
+            acts = [a for _, a, _ in self.entries]
+            sts = [s for _, _, s in self.entries]
+            for _ in range(n):
+                step_blocks(envs, acts, sts)
+            self.eager_steps += n
+            return
+        q, r = divmod(n, self.chunk)
+        for L, times in ((self.chunk, q), (r, 1 if r else 0)):
+            for _ in range(times):
+                for i, (_, _, st) in enumerate(self.entries):
+                    with self.torch.cuda.stream(st):
+                        self._graph(i, L).replay()
+                self.replays += 1
+
+    def timed(self, n, stream):
+        """n steps bracketed by HIP events on `stream` (the blocks' streams join it on both sides)"""
+        ev0, ev1 = self.torch.cuda.Event(enable_timing=True), self.torch.cuda.Event(enable_timing=True)
+        ev0.record(stream)
+        for _, _, st in self.entries:
+            st.wait_stream(stream)
+        self.run(n)
+        for _, _, st in self.entries:
+            stream.wait_stream(st)
+        ev1.record(stream)
+        return ev0, ev1
+
+
+def raw_streams(torch, dev, n, spare):
+    """n non-blocking HIP streams (after `spare` streams used once: DESIGN.md §4, queue mapping)."""
+    hip = ctypes.CDLL("libamdhip64.so")
+    made = []
+
+    def mk():
+        p = ctypes.c_void_p()
+        if hip.hipStreamCreateWithFlags(ctypes.byref(p), ctypes.c_uint(1)) != 0:  # hipStreamNonBlocking
+            raise RuntimeError("hipStreamCreateWithFlags failed")
+        made.append(p.value)
+        return torch.cuda.ExternalStream(p.value, device=dev)
+    for _ in range(spare):
+        st = mk()
+        with torch.cuda.stream(st):
+            torch.zeros(1, device=dev).add_(1)
+    torch.cuda.synchronize(dev)
+    streams = [mk() for _ in range(n)]
+
+    def destroy():
+        torch.cuda.synchronize(dev)
+        for p in made:
+            hip.hipStreamDestroy(ctypes.c_void_p(p))
+    return streams, destroy
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
-    ap.add_argument("--graph", type=int, default=100, help="steps per captured hipGraph (0 = eager launches)")
+    ap.add_argument("--graph", type=int, default=100, help="max steps per captured hipGraph (0 = eager launches)")
     ap.add_argument("--streams", type=int, default=0,
-                    help="env blocks per GPU, each its own handle on its own HIP stream (0 = 4 for flavor B, 1 for A)")
+                    help="env blocks per GPU, each its own handle on its own HIP stream (0 = 4 for 8-drone flavor "
+                         "B, 1 otherwise); the bench keeps the blocks only if they measure faster than one handle")
     ap.add_argument("--generic", action="store_true", help="generic kernels instead of qs_specialize (hipRTC)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds", type=float, default=6.0, help="seconds per cpu_baseline leg (3 legs)")
+    ap.add_argument("--cpu-worker", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--e2e-iters", type=int, default=2, help="timed PPO iterations for end_to_end (0 = skip)")
     ap.add_argument("--e2e-steps", type=int, default=0, help="override the PPO rollout length n_steps")
     args = ap.parse_args()
+    if args.cpu_worker:
+        return cpu_worker(args.config, args.cpu_seconds)
 
     import torch
     import torch.distributed as dist
@@ -264,113 +383,81 @@ def main():
     gen = torch.Generator(device=dev).manual_seed(1234)
     actions = (torch.rand(I, cfg.act_dim, device=dev, generator=gen) * 2.0 - 1.0).contiguous()
     env.reset()
-
     stream = torch.cuda.current_stream(dev)
-    chunk = args.graph if args.graph > 0 else 0
-    # 4 env blocks pay where a block still fills the chip (8-drone flavor B at 4096 envs: C3 8.4 -> 7.7 us,
-    # C4 13.6 -> 11.1 us per step); C2 (5.5 -> 6.1), C5 (14.7 -> 15.3) and flavor A (issue-bound, 29 -> 33)
-    # lose, so they keep one handle (profiles/r01_c3_streams.txt)
-    S = args.streams or STREAM_BLOCKS.get(args.config, 1)
-    if S > 1 and (cfg.num_envs % S or not chunk):
-        S = 1
-    # The shard is split into S env blocks, each its own handle keyed by its global drone ids (so the
-    # union draws exactly what the one big handle would) on its own HIP stream. Step t+1 of a block only
-    # waits for step t of the same block, so one block's next launch fills the CUs that another block's
-    # last waves leave idle (the launch tail is ~25 % of a one-handle step).
-    blocks = []
-    if S == 1:
-        blocks.append((env, actions, stream))
-    else:
-        Eb = cfg.num_envs // S
-        # HIP maps streams onto GPU_MAX_HW_QUEUES (= 4) hardware queues. Measured on MI355X
-        # (tools/exp_streams.py, profiles/r01_c3_streams.txt): the first user streams of a process take
-        # queues of their own and the one after them shares a queue with an earlier one (two blocks then
-        # serialise: 16 us instead of 7.6); once three streams exist, S = 4 consecutive new streams land on
-        # four different queues. So three streams are created and used once before the block streams.
-        hip = ctypes.CDLL("libamdhip64.so")
+    # graphs of min(--graph, steps) steps, the remainder of a run in one more graph: every warm-up and
+    # timed step of any --steps / --warmup is a graph replay (the driver runs --steps 20 --warmup 5)
+    chunk = min(args.graph, args.steps) if args.graph > 0 else 0
+    one = Blocks(torch, dev, [(env, actions, stream)], chunk)
 
-        def raw_stream():
-            p = ctypes.c_void_p()
-            if hip.hipStreamCreateWithFlags(ctypes.byref(p), ctypes.c_uint(1)) != 0:  # hipStreamNonBlocking
-                raise RuntimeError("hipStreamCreateWithFlags failed")
-            return torch.cuda.ExternalStream(p.value, device=dev)
-        spare = [raw_stream() for _ in range(3)]
-        for st in spare:
-            with torch.cuda.stream(st):
-                torch.zeros(1, device=dev).add_(1)
-        torch.cuda.synchronize(dev)
-        bstreams = [raw_stream() for _ in range(S)]
-        for s in range(S):
+    # Env blocks: envs are independent, so the shard is split into S blocks of E/S envs, each
+    # its own handle keyed by its global drone ids (the union draws exactly what the one handle draws) on
+    # its own HIP stream: one block's next launch fills the CUs another block's last waves leave idle.
+    # Whether that pays depends on the config and on HIP's stream -> hardware-queue mapping, so it is
+    # measured here against the one handle (same graphs, same step count) and kept only if faster.
+    S = args.streams or STREAM_BLOCKS.get(args.config, 1)
+    if S > 1 and cfg.num_envs % S:
+        S = 1
+    blocks, destroy_streams, ab = None, None, None
+    if S > 1:
+        Eb = cfg.num_envs // S
+        bstreams, destroy_streams = raw_streams(torch, dev, S, spare=3)
+        entries = []
+        for s_ in range(S):
             cb = make_cfg(dict(kw, num_envs=Eb), seed=0, specialize=not args.generic)
-            cb.drone_id_offset = rank * I + s * Eb * cfg.num_agents
-            st = bstreams[s]
+            cb.drone_id_offset = rank * I + s_ * Eb * cfg.num_agents
+            st = bstreams[s_]
             st.wait_stream(stream)
             with torch.cuda.stream(st):
                 eb = QuadSwarmEnv(cb, device=dev)
                 eb.reset()
-            blocks.append((eb, actions[s * Eb * cfg.num_agents:(s + 1) * Eb * cfg.num_agents].contiguous(), st))
+            entries.append((eb, actions[s_ * Eb * cfg.num_agents:(s_ + 1) * Eb * cfg.num_agents].contiguous(), st))
         torch.cuda.synchronize(dev)
-    graphs = []
-    if chunk:
-        # capture `chunk` steps per block into one hipGraph on the block's stream (the RNG counter lives
-        # on the device)
-        for eb, ab, st in blocks:
-            with torch.cuda.stream(st):
-                for _ in range(3):
-                    eb.step(ab)
+        blocks = Blocks(torch, dev, entries, chunk)
+        # A/B on the configuration's own graphs: 2 x max(chunk, 20) steps each, after one warm pass
+        n_ab = max(chunk, 20) if chunk else 20
+        for cand in (one, blocks):
+            cand.prepare([n_ab])
+            cand.run(n_ab)
+        torch.cuda.synchronize(dev)
+        times = {}
+        for name, cand in (("one_handle", one), ("blocks", blocks)):
+            ev = cand.timed(2 * n_ab, stream)
             torch.cuda.synchronize(dev)
-            g = torch.cuda.CUDAGraph()
-            # one block: capture on torch's side stream, replay on the current stream (as before)
-            with torch.cuda.graph(g, stream=st if S > 1 else None):
-                for _ in range(chunk):
-                    eb.step(ab)
-            torch.cuda.synchronize(dev)
-            graphs.append(g)
+            times[name] = ev[0].elapsed_time(ev[1]) * 1e3 / (2 * n_ab)
+        if world > 1:   # every rank takes the same decision (rank 0's measurement)
+            t = torch.tensor([times["one_handle"], times["blocks"]], device=dev, dtype=torch.float64)
+            dist.broadcast(t, 0)
+            times = {"one_handle": float(t[0]), "blocks": float(t[1])}
+        ab = {k: round(v, 3) for k, v in times.items()}
+        if times["blocks"] >= times["one_handle"]:
+            S = 1
+        ab["chosen"] = "blocks" if S > 1 else "one_handle"
+    run = blocks if S > 1 else one
+    run.replays = run.eager_steps = 0
+    run.prepare([args.warmup, args.steps])
 
-    def run(n):
-        if not graphs:
-            for _ in range(n):
-                env.step(actions)
-            return n
-        done = 0
-        while done + chunk <= n:
-            for (eb, ab, st), g in zip(blocks, graphs):
-                with torch.cuda.stream(st):
-                    g.replay()
-            done += chunk
-        for _ in range(n - done):
-            for eb, ab, st in blocks:
-                with torch.cuda.stream(st):
-                    eb.step(ab)
-        return n
-
-    run(args.warmup)
+    run.run(args.warmup)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    # HIP events on the stream the kernels are launched on (graph replays and eager launches both go
-    # to torch's current stream), bracketing the timed region: back to back step kernels, so the
-    # average launch duration (what rocprofv3 --kernel-trace reports for the same command) = span / K
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    # HIP events on the stream the launches are ordered on (graph replays and eager launches both go to
+    # torch's current stream, or to the block streams that join it), bracketing the timed region: back to
+    # back step kernels, so the average step time = span / K (rocprofv3 --kernel-trace, one handle, agrees)
+    replays0, eager0 = run.replays, run.eager_steps
     t0 = time.perf_counter()
-    ev0.record(stream)
-    for _, _, st in blocks:
-        st.wait_stream(stream)
-    run(args.steps)
-    for _, _, st in blocks:
-        stream.wait_stream(st)
-    ev1.record(stream)
+    ev0, ev1 = run.timed(args.steps, stream)
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
     k_ms = ev0.elapsed_time(ev1) / args.steps
+    timed_replays, timed_eager = run.replays - replays0, run.eager_steps - eager0
     if world > 1:
         dist.barrier()
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
 
-    # secondary: one eager launch bracketed by its own events (includes the host launch gap)
+    # secondary: one eager launch of the one handle bracketed by its own events (includes the host launch gap)
     nk = min(200, max(20, args.steps // 10))
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(nk)]
     for s_ev, e_ev in evs:
@@ -379,6 +466,7 @@ def main():
         e_ev.record(stream)
     torch.cuda.synchronize(dev)
     k_eager_ms = sum(s.elapsed_time(e) for s, e in evs) / nk
+    guard = env.counters()
 
     e2e = None
     if args.e2e_iters > 0:
@@ -396,6 +484,13 @@ def main():
                                                cfg.num_obstacles if cfg.use_obstacles else 0)
         achieved = bpa * I / (k_ms * 1e-3) / 1e9
         traffic = pmc_traffic(args.config)
+        if chunk:
+            launch = f"{timed_replays} hipGraph replays ({timed_replays * len(run.entries)} graphs) for {args.steps} timed steps"
+        else:
+            launch = f"eager: {timed_eager} qs_step_blocks calls"
+        if S > 1:
+            launch += f", {S} env blocks of {cfg.num_envs // S} envs on {S} HIP streams"
+        launch += ", specialised kernels (qs_specialize, hipRTC)" if env.specialized else ", generic kernels"
         out = {
             "metric": "agent-steps/sec, 8-drone swarm x 4096 envs, at 1/2/4/8 MI355X" if args.config == "c3"
             else f"agent-steps/sec, {WORKLOAD[args.config]}",
@@ -416,10 +511,7 @@ def main():
             "config": {"workload": WORKLOAD[args.config], "envs_per_gpu": cfg.num_envs,
                        "agents_per_env": cfg.num_agents, "visible_neighbors": cfg.k_neighbors,
                        "obs_dim": cfg.obs_dim, "global_batch": world * I, "parallelism": f"env-shard x{world}",
-                       "flavor": cfg.flavor,
-                       "launch": (f"hipGraph of {chunk} steps" if chunk else "eager") +
-                                 (f" per env block, {S} blocks of {cfg.num_envs // S} envs on {S} HIP streams" if S > 1 else "") +
-                                 (", specialised kernels (qs_specialize, hipRTC)" if env.specialized else ", generic kernels")},
+                       "flavor": cfg.flavor, "launch": launch, "blocks_ab_us_per_step": ab},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
@@ -434,16 +526,22 @@ def main():
                          "kernel_us_eager_single": round(k_eager_ms * 1e3, 3),
                          "bytes_per_agent_step": round(bpa, 1),
                          "bytes_per_launch": round(bpa * I / S)},
+            "nonfinite_guard": guard,
             "cpu_baseline": None,
             "end_to_end": e2e,
         }
         if world == 1 and not args.no_cpu_baseline:
             try:
-                out["cpu_baseline"] = cpu_baseline(kw, seconds=args.cpu_seconds)
+                out["cpu_baseline"] = cpu_baseline(args.config, seconds=args.cpu_seconds)
             except Exception as e:  # never let the baseline leg kill the GPU number
                 out["cpu_baseline"] = {"error": repr(e)}
         print(json.dumps(out), flush=True)
+    if blocks is not None:
+        for eb, _, _ in blocks.entries:
+            eb.close()
     env.close()
+    if destroy_streams is not None:
+        destroy_streams()
     if use_dist:
         dist.destroy_process_group()
 

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define QS_ABI_VERSION 5
+#define QS_ABI_VERSION 6
 #define QS_MAX_AGENTS 32            /* drones per env: one env lives inside one 64-lane wavefront */
 #define QS_MAX_DR_CHOICES 8         /* entries per obstacle domain-randomisation list */
 
@@ -209,7 +209,7 @@ enum qs_env_ffield {
 
 typedef struct qs_layout {          /* byte offsets inside one workspace allocation */
     size_t params;                  /* kernel parameter block (device copy of the config + runtime params) */
-    size_t state, istate, env, env_f, obst, stale_vel, obs, term_obs, rew, done, reset_info, total_bytes;
+    size_t state, istate, env, env_f, obst, stale_vel, obs, term_obs, rew, done, reset_info, stats, total_bytes;
     int32_t obs_dim, num_drones;
 } qs_layout;
 
@@ -226,7 +226,21 @@ typedef struct qs_buffers {         /* device pointers (valid for the handle's l
     float* rew;                     /* [I] */
     uint8_t* done;                  /* [I] */
     uint8_t* reset_info;            /* [E] 0: no reset this call; 1: reset, {"success": False}; 2: True */
+    uint64_t* stats;                /* [QS_NSTAT] non-finite guard counters (qs_counters)              */
 } qs_buffers;
+
+/* Non-finite guard.  The reference raises ValueError on a NaN reward (gym_art/quadrotor_multi/
+ * quadrotor_single.py:87-90); a batched step cannot raise per env, so every step kernel counts what it
+ * produced non-finite -- observation values written, rewards, drone states after the step (before a
+ * fused reset replaces them) -- into device counters (one ballot per wave; atomics only on a hit).
+ * The counters accumulate across launches (also inside captured graphs) until qs_counters_reset. */
+enum qs_stat { QS_ST_OBS = 0, QS_ST_REW = 1, QS_ST_STATE = 2, QS_NSTAT = 4 };
+typedef struct qs_stats {
+    uint64_t nonfinite_obs;         /* observation values (obs rows of every step)                      */
+    uint64_t nonfinite_rew;         /* rewards                                                          */
+    uint64_t nonfinite_state;       /* drones whose pos / vel / rotation / omega was non-finite          */
+    uint64_t reserved;
+} qs_stats;
 
 typedef struct qs_handle qs_handle;
 
@@ -256,6 +270,15 @@ int qs_reset(qs_handle* h, const uint8_t* d_env_mask, void* stream);
  * flavor A) are reset in the same launch, their final observation goes to term_obs, obs holds the
  * reset observation and reset_info[e] says so (SubprocVecEnvCustom semantics). */
 int qs_step(qs_handle* h, const float* d_actions, void* stream);
+/* qs_step of n handles (env blocks of one device, e.g. a GPU's shard split into blocks that overlap on
+ * separate streams): handle i steps with d_actions[i] on streams[i].  One C call, one device check. */
+int qs_step_blocks(qs_handle* const* hs, int n, const float* const* d_actions, void* const* streams);
+
+/* Non-finite guard counters (qs_stats) accumulated since creation / the last qs_counters_reset.
+ * qs_counters synchronises `stream` and copies them to the host; qs_counters_reset zeroes them
+ * asynchronously on `stream`. */
+int qs_counters(qs_handle* h, qs_stats* out, void* stream);
+int qs_counters_reset(qs_handle* h, void* stream);
 
 /* Runtime-tunable scalars: "rew_pos", "rew_effort", "rew_crash", "rew_orient", "rew_spin",
  * "quadcol_bin", "quadcol_bin_smooth_max", "quadcol_bin_obst", "ep_len", "seed", "capture_radius" (flavor A, all envs;

@@ -10,9 +10,12 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_build", "liboracle.so")
+# QS_ORACLE_F32=1 (set only by bench.py's cpu_baseline subprocess): the fp32 twin of the same sources
+F32 = os.environ.get("QS_ORACLE_F32") == "1"
+LIB_PATH = os.path.join(HERE, "_build", "liboracle_f32.so" if F32 else "liboracle.so")
 
-D = ctypes.c_double
+D = ctypes.c_float if F32 else ctypes.c_double
+FT = np.float32 if F32 else np.float64
 I = ctypes.c_int
 
 
@@ -264,8 +267,8 @@ class TapeRng:
     """Holds the numpy arrays alive for an OrRng in tape mode."""
 
     def __init__(self, tape, spawn=None):
-        self.tape = np.ascontiguousarray(tape, dtype=np.float64)
-        self.spawn = np.ascontiguousarray(spawn if spawn is not None else np.zeros(1), dtype=np.float64)
+        self.tape = np.ascontiguousarray(tape, dtype=FT)
+        self.spawn = np.ascontiguousarray(spawn if spawn is not None else np.zeros(1), dtype=FT)
         self.r = OrRng()
         self.r.mode = RNG_TAPE
         self.r.tape = dptr(self.tape)
@@ -285,7 +288,7 @@ class ScenDraws:
     def __init__(self, tape=None, seed=0, key=0, stream=S_SCN_RESET, step=0):
         self.s = OrSDraw()
         if tape is not None:
-            self.tape = np.ascontiguousarray(tape, dtype=np.float64)
+            self.tape = np.ascontiguousarray(tape, dtype=FT)
             self.s.mode = RNG_TAPE
             self.s.tape = dptr(self.tape)
             self.s.tape_n = len(self.tape)
@@ -342,7 +345,7 @@ class OracleEnv:
         self.seed = seed
 
     def reset(self, mask=None):
-        obs = np.zeros((self.E * self.N, self.obs_dim))
+        obs = np.zeros((self.E * self.N, self.obs_dim), dtype=FT)
         if mask is None:
             lib().or_reset_all(ctypes.byref(self.p), self.drones, self.envs, self.seed, dptr(obs))
         else:
@@ -353,10 +356,10 @@ class OracleEnv:
         return obs
 
     def step(self, actions, nthreads=0):
-        a = np.ascontiguousarray(actions, dtype=np.float64).reshape(self.E * self.N, 4)
-        obs = np.zeros((self.E * self.N, self.obs_dim))
+        a = np.ascontiguousarray(actions, dtype=FT).reshape(self.E * self.N, 4)
+        obs = np.zeros((self.E * self.N, self.obs_dim), dtype=FT)
         term = np.zeros_like(obs)
-        rew = np.zeros(self.E * self.N)
+        rew = np.zeros(self.E * self.N, dtype=FT)
         done = np.zeros(self.E * self.N, dtype=np.uint8)
         lib().or_step_all(ctypes.byref(self.p), self.drones, self.envs, dptr(a), self.seed,
                           dptr(obs), dptr(rew), done.ctypes.data_as(ctypes.POINTER(ctypes.c_ubyte)),
@@ -380,7 +383,7 @@ class OracleEnvA:
             self.envs[e].capture_radius = float(r)
 
     def reset(self, mask=None):
-        obs = np.zeros((self.E * self.N, self.obs_dim))
+        obs = np.zeros((self.E * self.N, self.obs_dim), dtype=FT)
         ri = np.zeros(self.E, dtype=np.uint8)
         u8 = ri.ctypes.data_as(ctypes.POINTER(ctypes.c_ubyte))
         if mask is None:
@@ -394,10 +397,10 @@ class OracleEnvA:
         return obs, ri
 
     def step(self, actions, nthreads=0):
-        a = np.ascontiguousarray(actions, dtype=np.float64).reshape(self.E * self.N, 2)
-        obs = np.zeros((self.E * self.N, self.obs_dim))
+        a = np.ascontiguousarray(actions, dtype=FT).reshape(self.E * self.N, 2)
+        obs = np.zeros((self.E * self.N, self.obs_dim), dtype=FT)
         term = np.zeros_like(obs)
-        rew = np.zeros(self.E * self.N)
+        rew = np.zeros(self.E * self.N, dtype=FT)
         done = np.zeros(self.E * self.N, dtype=np.uint8)
         ri = np.zeros(self.E, dtype=np.uint8)
         lib().or_step_all_a(ctypes.byref(self.p), self.drones, self.envs, dptr(a), self.seed,

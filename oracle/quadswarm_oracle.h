@@ -18,6 +18,19 @@
 #define QUADSWARM_ORACLE_H
 #include <stdint.h>
 
+/* OR_F32: the same sources as an fp32 twin (liboracle_f32.so, built with -fsingle-precision-constant),
+ * used only as the bench's fp32 cpu_baseline leg ("C++ restatement, fp32, same SoA").
+ * Every double becomes float and <tgmath.h> maps the libm calls to their float versions.  Parity
+ * tests use the fp64 build only. */
+#ifdef OR_F32
+#include <math.h>
+#include <omp.h>
+#include <string.h>
+#include <tgmath.h>
+#undef I   /* complex.h's imaginary unit (pulled in by tgmath.h) */
+#define double float
+#endif
+
 #ifdef __cplusplus
 extern "C" {
 #endif

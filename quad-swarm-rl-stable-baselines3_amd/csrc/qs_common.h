@@ -22,6 +22,7 @@ enum : int {
 struct KP {
     int E, N, I, obs_dim, so_dim, K, neighbor, obs_repr, ep_len, sim_steps, svd_every, sense, downwash, collide;
     uint32_t id0;  // global id of drone 0 (RNG key offset)
+    uint32_t seed; // Philox seed: read per launch through KPM (qs_set_param("seed") reaches captured graphs)
     float dt, cdt, mass, inv_mass, inertia[3], inv_inertia[3];
     float thrust_max[4], torque_max[4], pc0[4], pc1[4], pc2[4], ccw[4];
     float tau_up, tau_down, lin, arm, grav, omega_max, vel_damp, dq, vxyz_max;
@@ -57,11 +58,13 @@ struct KP {
 // kernels use `kpm.` for them so that neither build re-loads them inside loops.
 struct KPM {
     int ep_len;
+    uint32_t seed;
     float rew_pos, rew_effort, rew_crash, rew_orient, rew_spin, quadcol, prox_max, prox_ratio, quadcol_obst;
 };
 __device__ __forceinline__ KPM load_kpm(const KP* __restrict__ p) {
     KPM m;
     m.ep_len = p->ep_len;
+    m.seed = p->seed;
     m.rew_pos = p->rew_pos;
     m.rew_effort = p->rew_effort;
     m.rew_crash = p->rew_crash;
@@ -105,6 +108,7 @@ struct Bufs {
     uint8_t* rinfo;
     const float* act;
     const uint8_t* mask;
+    unsigned long long* stats;   // [QS_NSTAT] non-finite guard counters (qs_counters)
 };
 
 // Diagnostic phase stamps (build with -DQS_STAMPS=1 only; never in the shipped library): lane 0 of
@@ -145,6 +149,29 @@ struct Drone {
     uint32_t flags;
     uint64_t prev;
 };
+
+// ---------------------------------------------------------------------------------------------
+// Non-finite guard (qs_counters): the reference raises on a NaN reward
+// (quadrotor_single.py:87-90); the batched step counts non-finite observations, rewards and drone
+// states per launch instead.  x * 0 is 0 for finite x and NaN for NaN / inf, so a chain of fma(x, 0, acc)
+// and one compare tests a whole vector.  The common case costs one ballot; atomics only when something
+// is non-finite.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ float fin_acc(float acc, float x) { return __builtin_fmaf(x, 0.f, acc); }
+__device__ __forceinline__ bool drone_nonfinite(const Drone& d) {
+    float a = 0.f;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) { a = fin_acc(a, d.pos[i]); a = fin_acc(a, d.vel[i]); a = fin_acc(a, d.om[i]); }
+#pragma unroll
+    for (int i = 0; i < 9; ++i) a = fin_acc(a, d.rot[i]);
+    return !(a == 0.f);
+}
+__device__ __forceinline__ void guard_count(const Bufs& b, int obs_bad, bool rew_bad, bool state_bad) {
+    if (__ballot(obs_bad != 0 || rew_bad || state_bad) == 0ull) return;
+    if (obs_bad) atomicAdd(b.stats + QS_ST_OBS, (unsigned long long)obs_bad);
+    if (rew_bad) atomicAdd(b.stats + QS_ST_REW, 1ull);
+    if (state_bad) atomicAdd(b.stats + QS_ST_STATE, 1ull);
+}
 
 __device__ __forceinline__ float clampf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
 // single-instruction sqrt / reciprocal (v_sqrt_f32 / v_rcp_f32, ~1 ulp): the step is compared with the
@@ -194,32 +221,36 @@ __device__ __forceinline__ void load_drone(const KP& kp, const Bufs& b, int g, D
 
 // Write-through (sc1) stores: the bytes leave the XCD's L2 during the kernel instead of being
 // written back by the end-of-kernel release (MI355X_MICROARCH "boundary": + dirty bytes / 6 TB/s).
+// They are raw buffer stores with the sc1 cache-policy bit (aux 16): compiler-visible builtins, so the
+// hazard recognizer schedules the wait states of the SGPR descriptor like for any other store.
 #ifndef QS_WT_OBS
 #define QS_WT_OBS 1
 #endif
 #ifndef QS_WT_STATE
 #define QS_WT_STATE 1
 #endif
-__device__ __forceinline__ void st_wt4(float4* p, float4 v) {
-#if QS_WT_OBS
-    typedef float v4f __attribute__((ext_vector_type(4)));
-    const v4f x = {v.x, v.y, v.z, v.w};
-    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(x) : "memory");
-#else
-    *p = v;
-#endif
+constexpr int QS_AUX_SC1 = 16;
+typedef uint32_t qs_v4u __attribute__((ext_vector_type(4)));
+// buffer descriptor over a uniform base (raw, stride 0, 32-bit offsets; gfx950 dword3 0x00020000)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t qs_rsrc(const void* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
 }
-// field f of a SoA array at (uniform base, lane byte offset), write-through, saddr form.  The s_nop 4:
-// the base SGPRs may have just been written by a VALU (v_readlane of a spilled SGPR), and a VMEM read of
-// such an SGPR needs 5 wait states, which the compiler's hazard recognizer does not insert for inline asm.
+// 16-B store at byte offset voff (per lane) of a uniform base
+__device__ __forceinline__ void st_wt4(__amdgpu_buffer_rsrc_t r, uint32_t voff, float4 v) {
+    const qs_v4u x = {(uint32_t)__float_as_int(v.x), (uint32_t)__float_as_int(v.y), (uint32_t)__float_as_int(v.z),
+                      (uint32_t)__float_as_int(v.w)};
+    __builtin_amdgcn_raw_buffer_store_b128(x, r, (int)voff, 0, QS_WT_OBS ? QS_AUX_SC1 : 0);
+}
+// 4-B store of word `v` at (uniform soff + per-lane voff) bytes from the descriptor's base
+__device__ __forceinline__ void st_wt1(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, uint32_t v) {
+    __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)voff, (int)soff, QS_WT_STATE ? QS_AUX_SC1 : 0);
+}
+// field f of a SoA array at (uniform base, lane byte offset): the field offset rides in soffset
 template <typename T>
 __device__ __forceinline__ void st_field(T* base, int f, int I, uint32_t boff, T v) {
-    T* fb = base + (size_t)f * (size_t)I;   // uniform
-#if QS_WT_STATE
-    asm volatile("s_nop 4\n\tglobal_store_dword %0, %1, %2 sc1" ::"v"(boff), "v"(v), "s"(fb) : "memory");
-#else
-    *reinterpret_cast<T*>(reinterpret_cast<char*>(fb) + boff) = v;
-#endif
+    uint32_t w;
+    __builtin_memcpy(&w, &v, 4);
+    st_wt1(qs_rsrc(base), boff, (uint32_t)f * (uint32_t)I * 4u, w);
 }
 
 __device__ __forceinline__ void store_drone(const KP& kp, const Bufs& b, int g, const Drone& d) {
@@ -502,19 +533,33 @@ __device__ __forceinline__ int xcd_block(int b, int nblocks) {
 // ---------------------------------------------------------------------------------------------
 // block-level obs staging: LDS tile [rows, obs_dim] -> contiguous global rows
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ void tile_store(const float* lds, float* dst, int nfloat, int lane) {
+// Returns how many of the values this lane stored are non-finite (the obs guard of qs_counters).
+__device__ __forceinline__ int tile_store(const float* lds, float* dst, int nfloat, int lane) {
     // dst = first row of the block; rows are contiguous in HBM.  obs is 256-B aligned and a block owns
     // 64/NPAD*N rows, so the start is 16-B aligned whenever rows*obs_dim*4 is: b128 in, dwordx4 out.
+    int bad = 0;
     if ((((uintptr_t)dst) & 15) == 0) {
         const int nvec = nfloat >> 2;
         const float4* lv = reinterpret_cast<const float4*>(lds);
-        float4* dv = reinterpret_cast<float4*>(dst);
-        for (int v = lane; v < nvec; v += 64) st_wt4(dv + v, lv[v]);
+        const __amdgpu_buffer_rsrc_t r = qs_rsrc(dst);
+        for (int v = lane; v < nvec; v += 64) {
+            const float4 x = lv[v];
+            st_wt4(r, (uint32_t)v * 16u, x);
+            if (!(fin_acc(fin_acc(fin_acc(x.x * 0.f, x.y), x.z), x.w) == 0.f))
+                bad += !(x.x * 0.f == 0.f) + !(x.y * 0.f == 0.f) + !(x.z * 0.f == 0.f) + !(x.w * 0.f == 0.f);
+        }
         const int t = (nvec << 2) + lane;
-        if (t < nfloat) dst[t] = lds[t];
+        if (t < nfloat) {
+            dst[t] = lds[t];
+            bad += !(lds[t] * 0.f == 0.f);
+        }
     } else {
-        for (int f = lane; f < nfloat; f += 64) dst[f] = lds[f];
+        for (int f = lane; f < nfloat; f += 64) {
+            dst[f] = lds[f];
+            bad += !(lds[f] * 0.f == 0.f);
+        }
     }
+    return bad;
 }
 
 // ---------------------------------------------------------------------------------------------

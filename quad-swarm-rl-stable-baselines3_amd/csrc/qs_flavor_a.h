@@ -445,9 +445,10 @@ struct StepGeoA {
 };
 
 template <int NPAD>
-__global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, Bufs b, uint32_t seed) {
+__global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, Bufs b) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     QS_BIND_KP(kpp);
+    const uint32_t seed = kpm.seed;
     using G = StepGeoA<NPAD>;
     constexpr int Q = G::Q, LPE = G::LPE, EPB = G::EPB, SLOTS = G::SLOTS;
     const int lane = threadIdx.x;
@@ -539,6 +540,7 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
     if (kp.K > 0)
         neighbor_obs_a<NPAD, Q>(kp, xch, sbase, di, d.pos, c.angle, c.angle, d.vel, rng_last, gid, false, active, row, q);
 
+    const bool state_bad = lead && drone_nonfinite(d), rew_bad = lead && !(rw * 0.f == 0.f);
     const uint64_t fball = __ballot(active && fin);
     if (fball) {  // some env finished: terminal obs + the worker's reset (subproc_vec_env_custom.py:42-46)
         lds_sync();
@@ -565,7 +567,8 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
         }
     }
     lds_sync();
-    tile_store(lds, b.obs + (size_t)env0 * kp.N * kp.obs_dim, rows * kp.obs_dim, lane);
+    const int obs_bad = tile_store(lds, b.obs + (size_t)env0 * kp.N * kp.obs_dim, rows * kp.obs_dim, lane);
+    guard_count(b, obs_bad, rew_bad, state_bad);
 
     if (lead) {
         store_drone(kp, b, g, d);
@@ -588,9 +591,10 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
 
 // explicit reset of masked envs (quadrotor_multi_rewards.QuadrotorEnvMulti.reset)
 template <int NPAD>
-__global__ __launch_bounds__(64) void reset_kernel_a(const KP* __restrict__ kpp, Bufs b, uint32_t seed) {
+__global__ __launch_bounds__(64) void reset_kernel_a(const KP* __restrict__ kpp, Bufs b) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     QS_BIND_KP(kpp);
+    const uint32_t seed = kpm.seed;
     constexpr int EPB = 64 / NPAD;
     const int lane = threadIdx.x;
     const int el = lane / NPAD, di = lane % NPAD;

@@ -964,6 +964,7 @@ __device__ __forceinline__ void store_drone_q(const KP& kp, const Bufs& b, int g
     wv[IW + QS_I_PREV_HI] = (uint32_t)(d.prev >> 32);
     constexpr int T = (DRONE_WORDS + Q - 1) / Q;
     const uint32_t go = (uint32_t)g * 4u;
+    const __amdgpu_buffer_rsrc_t rs = qs_rsrc(b.st);
 #pragma unroll
     for (int t = 0; t < T; ++t) {
         const int w = t * Q + q;
@@ -971,14 +972,7 @@ __device__ __forceinline__ void store_drone_q(const KP& kp, const Bufs& b, int g
 #pragma unroll
         for (int k = 1; k < Q; ++k)
             if (q == k && t * Q + k < DRONE_WORDS) v = wv[t * Q + k];
-        if (active && w < DRONE_WORDS) {
-            const uint32_t off = drone_word_off(kp, b, w, go);
-#if QS_WT_STATE
-            asm volatile("s_nop 4\n\tglobal_store_dword %0, %1, %2 sc1" ::"v"(off), "v"(v), "s"(b.st) : "memory");
-#else
-            *reinterpret_cast<uint32_t*>((char*)b.st + off) = v;
-#endif
-        }
+        if (active && w < DRONE_WORDS) st_wt1(rs, drone_word_off(kp, b, w, go), 0u, v);
     }
 }
 
@@ -991,9 +985,10 @@ struct StepGeo {
 };
 
 template <int NPAD, bool OBST>
-__global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bufs b, uint32_t seed, RBufs r, RP rp) {
+__global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bufs b, RBufs r, RP rp) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     QS_BIND_KP(kpp);
+    const uint32_t seed = kpm.seed;
     QS_STAMP_DECL
     QS_RTSTAMP(12);
     QS_STAMP(0);
@@ -1274,6 +1269,8 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     if (nbr) neighbor_obs<NPAD, Q>(kp, xch, dbase, di, q, d.pos, d.vel, active, row);
     if (OBST && lead) sdf_obs(kp, og, myob, d.pos[0], d.pos[1], row + kp.obs_dim - 9);   // MultiObstacles.step
     QS_STAMP(7);
+    // non-finite guard of the stepped drone and its reward (before a fused reset replaces the drone)
+    const bool state_bad = lead && drone_nonfinite(d), rew_bad = lead && !(rw * 0.f == 0.f);
 
     const uint64_t dball = __ballot(active && done);
     if (dball) {  // rare: some env of this block finished -> terminal obs + fused auto-reset (:739-838)
@@ -1334,7 +1331,7 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     }
     lds_sync();
     QS_STAMP(8);
-    tile_store(lds, b.obs + (size_t)env0 * kp.N * kp.obs_dim, rows * kp.obs_dim, lane);
+    const int obs_bad = tile_store(lds, b.obs + (size_t)env0 * kp.N * kp.obs_dim, rows * kp.obs_dim, lane);
     QS_STAMP(9);
 
 #if QS_COOP_STATE
@@ -1356,13 +1353,14 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
             if (nf != ef) b.env[QS_E_FLAGS * kp.E + env] = nf;
         }
     }
+    guard_count(b, obs_bad, rew_bad, state_bad);
     QS_STAMP(10);
     if (r.ri != nullptr) {   // experience replay on (uniform): ExperienceReplayWrapper.step of every env (:124-180)
         // the step's global stores above are read back by other lanes of the wave: workgroup-scope
         // release/acquire (one wave per workgroup, one L1)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        if (env < kp.E) replay_env<true>(kp, b, r, rp, seed, env, lane % LPE, LPE);
+        if (env < kp.E) replay_env<true>(kp, kpm, b, r, rp, seed, env, lane % LPE, LPE);
     }
     QS_STAMP(11);
     QS_RTSTAMP(13);
@@ -1371,9 +1369,10 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
 
 // explicit reset of masked envs (QuadrotorEnvMulti.reset quadrotor_multi.py:440-517)
 template <int NPAD, bool OBST>
-__global__ __launch_bounds__(64) void reset_kernel(const KP* __restrict__ kpp, Bufs b, uint32_t seed) {
+__global__ __launch_bounds__(64) void reset_kernel(const KP* __restrict__ kpp, Bufs b) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     QS_BIND_KP(kpp);
+    const uint32_t seed = kpm.seed;
     constexpr int EPB = 64 / NPAD;
     const int lane = threadIdx.x;
     const int el = lane / NPAD, di = lane % NPAD;

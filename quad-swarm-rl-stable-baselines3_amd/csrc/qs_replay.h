@@ -94,7 +94,7 @@ __device__ __forceinline__ int hist_push(const RP& rp, const RBufs& r, int E, in
 // !STEP: after reset_kernel (ExperienceReplayWrapper.reset -> env.reset accounting, :109-122) of the masked envs.
 // One env on RL of its lanes (lane in [0, RL)): no barriers or cross-lane exchange inside.
 template <bool STEP>
-__device__ __forceinline__ void replay_env(const KP& kp, const Bufs& b, const RBufs& r, const RP& rp, uint32_t seed,
+__device__ __forceinline__ void replay_env(const KP& kp, const KPM& kpm, const Bufs& b, const RBufs& r, const RP& rp, uint32_t seed,
                                            int e, int lane, int RL) {
     const int E = kp.E;
     const bool w0 = lane == 0;
@@ -134,7 +134,7 @@ __device__ __forceinline__ void replay_env(const KP& kp, const Bufs& b, const RB
     int restored = -1, pushed = -1;
 
     if (!active)   // crashes_last_episode += infos[0]["rewards"]["rew_crash"] = dt * -(crash * on_floor) (:725)
-        crash += -(double)kp.dt * (double)kp.rew_crash * ((flags & QS_EF_FLOOR0) ? 1.0 : 0.0);
+        crash += -(double)kp.dt * (double)kpm.rew_crash * ((flags & QS_EF_FLOOR0) ? 1.0 : 0.0);
 
     if (done) {
         // the env's own reset inside step (quadrotor_multi.py:836) ...
@@ -224,11 +224,13 @@ __device__ __forceinline__ void replay_env(const KP& kp, const Bufs& b, const RB
 }
 
 template <bool STEP>
-__global__ __launch_bounds__(256) void replay_kernel(const KP* __restrict__ kpp, Bufs b, RBufs r, RP rp, uint32_t seed) {
+__global__ __launch_bounds__(256) void replay_kernel(const KP* __restrict__ kpp, Bufs b, RBufs r, RP rp) {
     const KP& kp = *kpp;
+    const KPM kpm = load_kpm(kpp);
+    const uint32_t seed = kpm.seed;
     const int e = blockIdx.x * (256 / RL) + threadIdx.x / RL;
     if (e >= kp.E) return;   // no barriers: lanes of absent envs just leave
-    replay_env<STEP>(kp, b, r, rp, seed, e, threadIdx.x % RL, RL);
+    replay_env<STEP>(kp, kpm, b, r, rp, seed, e, threadIdx.x % RL, RL);
 }
 
 }  // namespace qs

@@ -61,6 +61,13 @@ struct qs_handle {
 
 static thread_local std::string g_err;
 
+// make h's device current; hipGetDevice is a thread-local read, hipSetDevice only when it differs
+static hipError_t use_device(const qs_handle* h) {
+    int cur = -1;
+    if (hipGetDevice(&cur) == hipSuccess && cur == h->device) return hipSuccess;
+    return hipSetDevice(h->device);
+}
+
 static int fail(int code, const std::string& msg) {
     g_err = msg;
     return code;
@@ -160,7 +167,8 @@ static int validate(const qs_config* c) {
     if (c->neighbor_obs != QS_NEIGHBOR_NONE && (c->k_neighbors < 1 || c->k_neighbors > c->num_agents - 1))
         return fail(QS_E_INVALID, "k_neighbors must be in [1, num_agents-1]");
     if (c->sim_steps < 1 || c->svd_every < 1 || c->ep_len < 0) return fail(QS_E_INVALID, "bad sim_steps/svd_every/ep_len");
-    if ((long long)c->num_envs * c->num_agents > (1ll << 31) / 64) return fail(QS_E_INVALID, "too many drones");
+    // SoA offsets are 32-bit byte offsets (buffer stores): 64 fields x 4 B x I must stay below 4 GB
+    if ((long long)c->num_envs * c->num_agents > (1ll << 32) / 256) return fail(QS_E_INVALID, "too many drones");
     return QS_OK;
 }
 
@@ -196,6 +204,7 @@ static qs_layout make_layout(const qs_config* c) {
     L.rew = o; o = al(o + sizeof(float) * I);
     L.done = o; o = al(o + I);
     L.reset_info = o; o = al(o + E);
+    L.stats = o; o = al(o + sizeof(uint64_t) * QS_NSTAT);
     L.total_bytes = o;
     L.obs_dim = od;
     L.num_drones = (int32_t)I;
@@ -297,6 +306,7 @@ static qs::KP make_kp(const qs_config* c, const qs_layout& L) {
     k.neighbor = c->neighbor_obs;
     k.K = c->neighbor_obs != QS_NEIGHBOR_NONE ? c->k_neighbors : 0;
     k.id0 = c->drone_id_offset;
+    k.seed = c->seed;
     k.obs_repr = c->obs_repr; k.ep_len = c->ep_len; k.sim_steps = c->sim_steps; k.svd_every = c->svd_every;
     k.sense = c->sense_noise; k.downwash = c->use_downwash; k.collide = c->apply_collision_force;
     k.dt = c->dt; k.cdt = c->control_dt; k.mass = c->mass; k.inv_mass = (float)(1.0 / (double)c->mass);
@@ -507,6 +517,9 @@ extern "C" int qs_create(const qs_config* c, int dev, void* ws, qs_handle** out)
         e = hipMemcpy((char*)h->ws + h->lay.env_f + sizeof(float) * QS_ENVF_CAPTURE * (size_t)c->num_envs, cr.data(),
                       sizeof(float) * cr.size(), hipMemcpyHostToDevice);
     }
+    // the initialisation ran on the null stream: complete it before any (possibly non-blocking) stream
+    // of the caller touches the workspace
+    if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e != hipSuccess) {
         if (h->owns_ws) (void)hipFree(h->ws);
         delete h;
@@ -551,6 +564,7 @@ static qs::Bufs bufs_of(qs_handle* h) {
     b.rinfo = (uint8_t*)(w + h->lay.reset_info);
     b.act = nullptr;
     b.mask = nullptr;
+    b.stats = (unsigned long long*)(w + h->lay.stats);
     return b;
 }
 
@@ -559,6 +573,7 @@ extern "C" int qs_buffers_get(qs_handle* h, qs_buffers* o) {
     qs::Bufs b = bufs_of(h);
     o->state = b.st; o->istate = b.ist; o->env = b.env; o->env_f = b.envf; o->obst = (float*)b.obst; o->stale_vel = b.stale;
     o->obs = b.obs; o->term_obs = b.term; o->rew = b.rew; o->done = b.done; o->reset_info = b.rinfo;
+    o->stats = (uint64_t*)b.stats;
     return QS_OK;
 }
 
@@ -566,7 +581,6 @@ static int launch(qs_handle* h, bool step, const float* act, const uint8_t* mask
     qs::Bufs b = bufs_of(h);
     b.act = act;
     b.mask = mask;
-    const uint32_t seed = h->cfg.seed;
     const qs::KP* kpd = (const qs::KP*)((char*)h->ws + h->lay.params);
     const int epb = envs_per_block(h->cfg, h->npad, step);
     const dim3 grid((unsigned)((h->kp.E + epb - 1) / epb)), block(64);
@@ -576,21 +590,21 @@ static int launch(qs_handle* h, bool step, const float* act, const uint8_t* mask
     qs::RBufs rb = h->rws ? h->rb : qs::RBufs{};
     qs::RP rp = h->rp;
     if (hipFunction_t f = step ? h->jit_step : h->jit_reset) {
-        void* args[] = {(void*)&kpd, (void*)&b, (void*)&seed, (void*)&rb, (void*)&rp};   // the last two: B step only
+        void* args[] = {(void*)&kpd, (void*)&b, (void*)&rb, (void*)&rp};   // the last two: B step only
         QS_HIP(hipModuleLaunchKernel(f, grid.x, 1, 1, block.x, 1, 1, (unsigned)shm, s, args, nullptr));
         return QS_OK;
     }
 #define QS_LAUNCH(NP)                                                                                           \
     case NP:                                                                                                   \
         if (a) {                                                                                               \
-            if (step) hipLaunchKernelGGL(qs::step_kernel_a<NP>, grid, block, shm, s, kpd, b, seed);            \
-            else hipLaunchKernelGGL(qs::reset_kernel_a<NP>, grid, block, shm, s, kpd, b, seed);                \
+            if (step) hipLaunchKernelGGL(qs::step_kernel_a<NP>, grid, block, shm, s, kpd, b);                  \
+            else hipLaunchKernelGGL(qs::reset_kernel_a<NP>, grid, block, shm, s, kpd, b);                      \
         } else if (ob) {                                                                                       \
-            if (step) hipLaunchKernelGGL((qs::step_kernel<NP, true>), grid, block, shm, s, kpd, b, seed, rb, rp); \
-            else hipLaunchKernelGGL((qs::reset_kernel<NP, true>), grid, block, shm, s, kpd, b, seed);          \
+            if (step) hipLaunchKernelGGL((qs::step_kernel<NP, true>), grid, block, shm, s, kpd, b, rb, rp);    \
+            else hipLaunchKernelGGL((qs::reset_kernel<NP, true>), grid, block, shm, s, kpd, b);                \
         } else {                                                                                               \
-            if (step) hipLaunchKernelGGL((qs::step_kernel<NP, false>), grid, block, shm, s, kpd, b, seed, rb, rp); \
-            else hipLaunchKernelGGL((qs::reset_kernel<NP, false>), grid, block, shm, s, kpd, b, seed);         \
+            if (step) hipLaunchKernelGGL((qs::step_kernel<NP, false>), grid, block, shm, s, kpd, b, rb, rp);   \
+            else hipLaunchKernelGGL((qs::reset_kernel<NP, false>), grid, block, shm, s, kpd, b);               \
         }                                                                                                      \
         break;
     switch (h->npad) {
@@ -615,8 +629,8 @@ static int launch_replay(qs_handle* h, bool step, const uint8_t* mask, hipStream
     const qs::KP* kpd = (const qs::KP*)((char*)h->ws + h->lay.params);
     constexpr int epb = 256 / qs::RL;   // envs per workgroup
     const dim3 grid((unsigned)((h->kp.E + epb - 1) / epb)), block(256);
-    if (step) hipLaunchKernelGGL(qs::replay_kernel<true>, grid, block, 0, s, kpd, b, h->rb, h->rp, h->cfg.seed);
-    else hipLaunchKernelGGL(qs::replay_kernel<false>, grid, block, 0, s, kpd, b, h->rb, h->rp, h->cfg.seed);
+    if (step) hipLaunchKernelGGL(qs::replay_kernel<true>, grid, block, 0, s, kpd, b, h->rb, h->rp);
+    else hipLaunchKernelGGL(qs::replay_kernel<false>, grid, block, 0, s, kpd, b, h->rb, h->rp);
     QS_HIP(hipGetLastError());
     return QS_OK;
 }
@@ -681,7 +695,7 @@ extern "C" int qs_replay_enable(qs_handle* h, const qs_replay_config* rc, void* 
     int r = replay_check(h, rc);
     if (r) return r;
     if (d_workspace && ((uintptr_t)d_workspace & 255) != 0) return fail(QS_E_INVALID, "workspace must be 256-byte aligned");
-    QS_HIP(hipSetDevice(h->device));
+    QS_HIP(use_device(h));
     QS_HIP(hipDeviceSynchronize());
     replay_free(h);
     const size_t E = (size_t)h->cfg.num_envs, W = snap_words(&h->cfg, h->lay.obs_dim);
@@ -728,6 +742,7 @@ extern "C" int qs_replay_enable(qs_handle* h, const qs_replay_config* rc, void* 
     e = hipMemset(h->rws, 0, total);
     if (e == hipSuccess) e = hipMemcpy(h->rb.ri, ri.data(), 4 * ri.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(h->rb.perm, perm.data(), 4 * perm.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipDeviceSynchronize();   // null-stream init complete before any caller stream
     if (e != hipSuccess) {
         replay_free(h);
         return fail(QS_E_HIP, std::string("replay init: ") + hipGetErrorString(e));
@@ -737,7 +752,7 @@ extern "C" int qs_replay_enable(qs_handle* h, const qs_replay_config* rc, void* 
 
 extern "C" int qs_replay_disable(qs_handle* h) {
     if (!h) return fail(QS_E_INVALID, "handle is NULL");
-    QS_HIP(hipSetDevice(h->device));
+    QS_HIP(use_device(h));
     QS_HIP(hipDeviceSynchronize());
     replay_free(h);
     return QS_OK;
@@ -758,22 +773,59 @@ extern "C" int qs_replay_buffers_get(qs_handle* h, qs_replay_buffers* o) {
 
 extern "C" int qs_reset(qs_handle* h, const uint8_t* d_mask, void* stream) {
     if (!h) return fail(QS_E_INVALID, "handle is NULL");
-    QS_HIP(hipSetDevice(h->device));
+    QS_HIP(use_device(h));
     int rc = launch(h, false, nullptr, d_mask, (hipStream_t)stream);
     if (rc == QS_OK && h->rws) rc = launch_replay(h, false, d_mask, (hipStream_t)stream);
     return rc;
 }
 
-extern "C" int qs_step(qs_handle* h, const float* d_actions, void* stream) {
+static int check_actions(const qs_handle* h, const float* d_actions) {
     if (!h || !d_actions) return fail(QS_E_INVALID, "NULL argument");
     if (h->cfg.flavor == QS_FLAVOR_A) {
         if (((uintptr_t)d_actions & 7) != 0) return fail(QS_E_INVALID, "actions must be 8-byte aligned [I,2] fp32");
     } else if (((uintptr_t)d_actions & 15) != 0) {
         return fail(QS_E_INVALID, "actions must be 16-byte aligned [I,4] fp32");
     }
-    QS_HIP(hipSetDevice(h->device));
+    return QS_OK;
+}
+
+extern "C" int qs_step(qs_handle* h, const float* d_actions, void* stream) {
+    if (int rc = check_actions(h, d_actions)) return rc;
+    QS_HIP(use_device(h));
     // with replay on, the flavor-B step kernel runs the wrapper in its tail (no second launch)
     return launch(h, true, d_actions, nullptr, (hipStream_t)stream);
+}
+
+extern "C" int qs_step_blocks(qs_handle* const* hs, int n, const float* const* d_actions, void* const* streams) {
+    if (!hs || !d_actions || !streams || n < 1) return fail(QS_E_INVALID, "NULL argument or n < 1");
+    for (int i = 0; i < n; ++i) {
+        if (int rc = check_actions(hs[i], d_actions[i])) return rc;
+        if (hs[i]->device != hs[0]->device) return fail(QS_E_INVALID, "qs_step_blocks: handles on different devices");
+    }
+    QS_HIP(use_device(hs[0]));
+    for (int i = 0; i < n; ++i)
+        if (int rc = launch(hs[i], true, d_actions[i], nullptr, (hipStream_t)streams[i])) return rc;
+    return QS_OK;
+}
+
+extern "C" int qs_counters(qs_handle* h, qs_stats* out, void* stream) {
+    if (!h || !out) return fail(QS_E_INVALID, "NULL argument");
+    QS_HIP(use_device(h));
+    uint64_t v[QS_NSTAT];
+    QS_HIP(hipMemcpyAsync(v, (char*)h->ws + h->lay.stats, sizeof v, hipMemcpyDeviceToHost, (hipStream_t)stream));
+    QS_HIP(hipStreamSynchronize((hipStream_t)stream));
+    out->nonfinite_obs = v[QS_ST_OBS];
+    out->nonfinite_rew = v[QS_ST_REW];
+    out->nonfinite_state = v[QS_ST_STATE];
+    out->reserved = 0;
+    return QS_OK;
+}
+
+extern "C" int qs_counters_reset(qs_handle* h, void* stream) {
+    if (!h) return fail(QS_E_INVALID, "NULL argument");
+    QS_HIP(use_device(h));
+    QS_HIP(hipMemsetAsync((char*)h->ws + h->lay.stats, 0, sizeof(uint64_t) * QS_NSTAT, (hipStream_t)stream));
+    return QS_OK;
 }
 
 static float* param_slot(qs_handle* h, const char* key) {
@@ -788,7 +840,7 @@ static float* param_slot(qs_handle* h, const char* key) {
 }
 
 static int upload_params(qs_handle* h) {
-    QS_HIP(hipSetDevice(h->device));
+    QS_HIP(use_device(h));
     QS_HIP(hipDeviceSynchronize());   // launches in flight read the old block
     QS_HIP(hipMemcpy((char*)h->ws + h->lay.params, &h->kp, sizeof(qs::KP), hipMemcpyHostToDevice));
     return QS_OK;
@@ -798,7 +850,7 @@ static int upload_params(qs_handle* h) {
 // are replayed from a captured hipGraph.
 static int set_capture_radius(qs_handle* h, float v) {
     if (h->cfg.flavor != QS_FLAVOR_A) return fail(QS_E_INVALID, "capture_radius is a flavor-A parameter");
-    QS_HIP(hipSetDevice(h->device));
+    QS_HIP(use_device(h));
     QS_HIP(hipDeviceSynchronize());
     std::vector<float> cr((size_t)h->cfg.num_envs, v);
     QS_HIP(hipMemcpy((char*)h->ws + h->lay.env_f + sizeof(float) * QS_ENVF_CAPTURE * (size_t)h->cfg.num_envs, cr.data(),
@@ -811,7 +863,7 @@ extern "C" int qs_set_param(qs_handle* h, const char* key, double v) {
     if (!h || !key) return fail(QS_E_INVALID, "NULL argument");
     if (strcmp(key, "capture_radius") == 0) return set_capture_radius(h, (float)v);
     if (strcmp(key, "ep_len") == 0) { h->kp.ep_len = (int)v; h->cfg.ep_len = (int)v; return upload_params(h); }
-    if (strcmp(key, "seed") == 0) { h->cfg.seed = (uint32_t)v; return QS_OK; }
+    if (strcmp(key, "seed") == 0) { h->kp.seed = h->cfg.seed = (uint32_t)v; return upload_params(h); }
     float* p = param_slot(h, key);
     if (!p) return fail(QS_E_INVALID, std::string("unknown param ") + key);
     *p = (float)v;
@@ -823,11 +875,11 @@ extern "C" int qs_set_param(qs_handle* h, const char* key, double v) {
 extern "C" int qs_get_param(qs_handle* h, const char* key, double* v) {
     if (!h || !key || !v) return fail(QS_E_INVALID, "NULL argument");
     if (strcmp(key, "ep_len") == 0) { *v = h->kp.ep_len; return QS_OK; }
-    if (strcmp(key, "seed") == 0) { *v = h->cfg.seed; return QS_OK; }
+    if (strcmp(key, "seed") == 0) { *v = h->kp.seed; return QS_OK; }
     if (strcmp(key, "capture_radius") == 0) {   // env 0's radius (set per env through buffers.env_f)
         if (h->cfg.flavor != QS_FLAVOR_A) return fail(QS_E_INVALID, "capture_radius is a flavor-A parameter");
         float r;
-        QS_HIP(hipSetDevice(h->device));
+        QS_HIP(use_device(h));
         QS_HIP(hipMemcpy(&r, (char*)h->ws + h->lay.env_f + sizeof(float) * QS_ENVF_CAPTURE * (size_t)h->cfg.num_envs,
                          sizeof(float), hipMemcpyDeviceToHost));
         *v = r;
@@ -849,7 +901,7 @@ extern "C" size_t qs_state_bytes(qs_handle* h) {
 extern "C" int qs_get_state(qs_handle* h, void* dst, size_t bytes, void* stream) {
     if (!h || !dst) return fail(QS_E_INVALID, "NULL argument");
     if (bytes < qs_state_bytes(h)) return fail(QS_E_INVALID, "buffer too small");
-    QS_HIP(hipSetDevice(h->device));
+    QS_HIP(use_device(h));
     QS_HIP(hipMemcpyAsync(dst, (char*)h->ws + h->lay.state, qs_state_bytes(h), hipMemcpyDeviceToHost,
                           (hipStream_t)stream));
     QS_HIP(hipStreamSynchronize((hipStream_t)stream));
@@ -859,7 +911,7 @@ extern "C" int qs_get_state(qs_handle* h, void* dst, size_t bytes, void* stream)
 extern "C" int qs_set_state(qs_handle* h, const void* src, size_t bytes, void* stream) {
     if (!h || !src) return fail(QS_E_INVALID, "NULL argument");
     if (bytes < qs_state_bytes(h)) return fail(QS_E_INVALID, "buffer too small");
-    QS_HIP(hipSetDevice(h->device));
+    QS_HIP(use_device(h));
     QS_HIP(hipMemcpyAsync((char*)h->ws + h->lay.state, src, qs_state_bytes(h), hipMemcpyHostToDevice,
                           (hipStream_t)stream));
     QS_HIP(hipStreamSynchronize((hipStream_t)stream));
@@ -920,7 +972,9 @@ static std::string kernel_names(const qs_config* c, const qs::KP& kp, int npad, 
     return "qs::step_kernel<" + np + ", " + ob + ">";
 }
 
-static std::string kp_words(const qs::KP& kp) {
+static std::string kp_words(const qs::KP& kp_in) {
+    qs::KP kp = kp_in;
+    kp.seed = 0;   // read per launch (KPM): one compiled module serves every seed
     std::string words;
     const uint32_t* w = reinterpret_cast<const uint32_t*>(&kp);
     char buf[16];
@@ -986,7 +1040,7 @@ extern "C" int qs_specialize(qs_handle* h, int enable) {
         h->jit_step = h->jit_reset = nullptr;
         return QS_OK;
     }
-    QS_HIP(hipSetDevice(h->device));
+    QS_HIP(use_device(h));
     std::string rn;
     const std::string key = std::to_string(h->device) + "|" + kernel_names(&h->cfg, h->kp, h->npad, &rn) + "|" +
                             kp_words(h->kp);

@@ -9,7 +9,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("QUADSWARM_LIB", os.path.join(HERE, "lib", "libquadswarm.so"))
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 MAX_AGENTS = 32
 MAX_DR_CHOICES = 8
 F, I32, U32, U64, SZ = ctypes.c_float, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_size_t
@@ -75,13 +75,22 @@ class QsConfig(ctypes.Structure):
 class QsLayout(ctypes.Structure):
     _fields_ = [("params", SZ), ("state", SZ), ("istate", SZ), ("env", SZ), ("env_f", SZ), ("obst", SZ), ("stale_vel", SZ),
                 ("obs", SZ),
-                ("term_obs", SZ), ("rew", SZ), ("done", SZ), ("reset_info", SZ), ("total_bytes", SZ), ("obs_dim", I32),
+                ("term_obs", SZ), ("rew", SZ), ("done", SZ), ("reset_info", SZ), ("stats", SZ), ("total_bytes", SZ),
+                ("obs_dim", I32),
                 ("num_drones", I32)]
 
 
 class QsBuffers(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in ("state", "istate", "env", "env_f", "obst", "stale_vel", "obs", "term_obs",
-                                               "rew", "done", "reset_info")]
+                                               "rew", "done", "reset_info", "stats")]
+
+
+# non-finite guard counters (qs_stat / qs_stats)
+ST_OBS, ST_REW, ST_STATE, NSTAT = 0, 1, 2, 4
+
+
+class QsStats(ctypes.Structure):
+    _fields_ = [("nonfinite_obs", U64), ("nonfinite_rew", U64), ("nonfinite_state", U64), ("reserved", U64)]
 
 
 class QsReplayConfig(ctypes.Structure):
@@ -105,7 +114,8 @@ class QuadSwarmError(RuntimeError):
 # every symbol include/quadswarm.h declares (tests check the library exports all of them)
 EXPORTS = ["qs_abi_version", "qs_last_error", "qs_struct_sizes", "qs_config_default", "qs_config_default_a",
            "qs_layout_query", "qs_create", "qs_destroy",
-           "qs_buffers_get", "qs_reset", "qs_step", "qs_set_param",
+           "qs_buffers_get", "qs_reset", "qs_step", "qs_step_blocks", "qs_counters", "qs_counters_reset",
+           "qs_set_param",
            "qs_get_param", "qs_state_bytes", "qs_get_state", "qs_set_state", "qs_gae",
            "qs_specialize", "qs_is_specialized", "qs_config_kp_words", "qs_specialize_compile",
            "qs_replay_config_default", "qs_replay_workspace_bytes", "qs_replay_enable", "qs_replay_disable", "qs_replay_buffers_get"]
@@ -129,6 +139,8 @@ def lib():
         "qs_layout_query": ([P(QsConfig), P(QsLayout)], I32),
         "qs_create": ([P(QsConfig), ctypes.c_int, V, P(V)], I32), "qs_destroy": ([V], I32),
         "qs_buffers_get": ([V, P(QsBuffers)], I32), "qs_reset": ([V, V, V], I32), "qs_step": ([V, V, V], I32),
+        "qs_step_blocks": ([P(V), ctypes.c_int, P(V), P(V)], I32),
+        "qs_counters": ([V, P(QsStats), V], I32), "qs_counters_reset": ([V, V], I32),
         "qs_set_param": ([V, ctypes.c_char_p, ctypes.c_double], I32),
         "qs_get_param": ([V, ctypes.c_char_p, P(ctypes.c_double)], I32),
         "qs_state_bytes": ([V], SZ), "qs_get_state": ([V, V, SZ, V], I32), "qs_set_state": ([V, V, SZ, V], I32),

@@ -33,10 +33,14 @@ class QuadSwarmEnv:
         self.E, self.N = cfg.num_envs, cfg.num_agents
         self.I = self.E * self.N
         self.obs_dim = lay.obs_dim
-        self._raw = torch.zeros(lay.total_bytes + 256, dtype=torch.uint8, device=self.device)
+        # qs_create zero-fills and initialises the workspace on the null stream: allocate without a fill
+        # kernel and drain the device first, so no pending work of another (non-blocking) stream on
+        # recycled caching-allocator memory can land after the initialisation
+        self._raw = torch.empty(lay.total_bytes + 256, dtype=torch.uint8, device=self.device)
         off = (-self._raw.data_ptr()) % 256
         ws = self._raw[off:off + lay.total_bytes]
         self._ws = ws
+        torch.cuda.synchronize(self.device)
         h = ctypes.c_void_p()
         N.check(L.qs_create(self.qcfg, self.device.index, ctypes.c_void_p(ws.data_ptr()), ctypes.byref(h)), "qs_create")
         self._h = h
@@ -62,6 +66,7 @@ class QuadSwarmEnv:
         self.term_obs = view(lay.term_obs, 4 * I * od, torch.float32, (I, od))
         self.rew = view(lay.rew, 4 * I, torch.float32, (I,))
         self.done = view(lay.done, I, torch.uint8, (I,))
+        self.stats = view(lay.stats, 8 * N.NSTAT, torch.int64, (N.NSTAT,))
         self.act_dim = cfg.act_dim
         self._align = 8 if cfg.flavor == "A" else 16
         self._torch = torch
@@ -81,9 +86,10 @@ class QuadSwarmEnv:
             setattr(rc, k, v)
         nb = ctypes.c_size_t()
         N.check(N.lib().qs_replay_workspace_bytes(self._h, ctypes.byref(rc), ctypes.byref(nb)), "qs_replay_workspace_bytes")
-        raw = self._torch.zeros(nb.value + 256, dtype=self._torch.uint8, device=self.device)
+        raw = self._torch.empty(nb.value + 256, dtype=self._torch.uint8, device=self.device)
         off = (-raw.data_ptr()) % 256
         ws = raw[off:off + nb.value]
+        self._torch.cuda.synchronize(self.device)   # qs_replay_enable initialises it synchronously
         N.check(N.lib().qs_replay_enable(self._h, ctypes.byref(rc), ctypes.c_void_p(ws.data_ptr())), "qs_replay_enable")
         rb = N.QsReplayBuffers()
         N.check(N.lib().qs_replay_buffers_get(self._h, ctypes.byref(rb)), "qs_replay_buffers_get")
@@ -136,6 +142,17 @@ class QuadSwarmEnv:
         self._act_keepalive = a
         N.check(N.lib().qs_step(self._h, ctypes.c_void_p(a.data_ptr()), self._stream()), "qs_step")
         return self.obs, self.rew, self.done, self.term_obs
+
+    def counters(self):
+        """Non-finite guard counters (qs_counters): {"nonfinite_obs", "nonfinite_rew", "nonfinite_state"}
+        accumulated by every step since creation / reset_counters().  Synchronises the current stream."""
+        st = N.QsStats()
+        N.check(N.lib().qs_counters(self._h, ctypes.byref(st), self._stream()), "qs_counters")
+        return {"nonfinite_obs": st.nonfinite_obs, "nonfinite_rew": st.nonfinite_rew,
+                "nonfinite_state": st.nonfinite_state}
+
+    def reset_counters(self):
+        N.check(N.lib().qs_counters_reset(self._h, self._stream()), "qs_counters_reset")
 
     def specialize(self, enable=True):
         """Switch to kernels recompiled (hipRTC) with this env's parameters as constants (qs_specialize);
@@ -252,3 +269,13 @@ def observation_bounds(cfg: QuadSwarmConfig):
     if cfg.use_obstacles:   # "octmap" (quadrotor_single.py:331)
         lo.append(-10 * np.ones(9)); hi.append(10 * np.ones(9))
     return np.concatenate(lo).astype(np.float32), np.concatenate(hi).astype(np.float32)
+
+
+def step_blocks(envs, actions, streams):
+    """qs_step_blocks: step several env blocks of one device in one C call, block i with actions[i]
+    (contiguous fp32 device tensors, checked once by the caller) on streams[i] (torch streams)."""
+    n = len(envs)
+    hs = (ctypes.c_void_p * n)(*[e._h.value for e in envs])
+    acts = (ctypes.c_void_p * n)(*[a.data_ptr() for a in actions])
+    sts = (ctypes.c_void_p * n)(*[s.cuda_stream for s in streams])
+    N.check(N.lib().qs_step_blocks(hs, n, acts, sts), "qs_step_blocks")
