@@ -72,7 +72,6 @@ def make_cfg(kw, **extra):
     return QuadSwarmConfig(**kw, **extra)
 
 
-STREAM_BLOCKS = {"c3": 4, "c3mix": 4, "c3mixr": 4, "c4": 4, "c4dr": 4}
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 
 
@@ -348,8 +347,9 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--graph", type=int, default=100, help="max steps per captured hipGraph (0 = eager launches)")
     ap.add_argument("--streams", type=int, default=0,
-                    help="env blocks per GPU, each its own handle on its own HIP stream (0 = 4 for 8-drone flavor "
-                         "B, 1 otherwise); the bench keeps the blocks only if they measure faster than one handle")
+                    help="env blocks per GPU, each its own handle on its own HIP stream (default 1 = one handle, "
+                         "the launch rocprofv3 profiles); with S > 1 the bench keeps the blocks only if an A/B "
+                         "measures them faster than the one handle")
     ap.add_argument("--generic", action="store_true", help="generic kernels instead of qs_specialize (hipRTC)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="seconds per cpu_baseline leg (3 legs)")
@@ -394,7 +394,7 @@ def main():
     # its own HIP stream: one block's next launch fills the CUs another block's last waves leave idle.
     # Whether that pays depends on the config and on HIP's stream -> hardware-queue mapping, so it is
     # measured here against the one handle (same graphs, same step count) and kept only if faster.
-    S = args.streams or STREAM_BLOCKS.get(args.config, 1)
+    S = max(1, args.streams)
     if S > 1 and cfg.num_envs % S:
         S = 1
     blocks, destroy_streams, ab = None, None, None

@@ -18,8 +18,11 @@ step() {  # name timeout cmd...
 for s in "$@"; do
   case $s in
     smoke) step smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests) step gpu_tests 900 python -m pytest tests -m gpu -q -x ;;
-    testsall) step gpu_tests 900 python -m pytest tests -m gpu -q ;;
+    tests) step gpu_tests 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
+    testsall) step gpu_tests 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread ;;
+    testsnew) step gpu_tests_new 600 python -u -m pytest tests/test_gpu_guard_params.py -v --timeout 120 --timeout-method thread ;;
+    benchdrv) step bench_driver 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    benchblocks) step bench_blocks 600 python bench.py --steps 2000 --streams 4 --no-cpu-baseline --e2e-iters 0 ;;
     bench) step bench 600 python bench.py ;;
     ppotests) step ppo_tests 600 python -m pytest tests/test_gpu_ppo.py -q -x ;;
     e2ea) step e2e_a8 600 python bench.py --config a8 --steps 500 --no-cpu-baseline --e2e-iters 1 --e2e-steps 64 ;;
@@ -42,9 +45,9 @@ for s in "$@"; do
     prof)
       export TMPDIR=/tmp
       step prof_kt 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_kt -o kt --output-format csv -- python bench.py --steps 1000 --no-cpu-baseline --e2e-iters 0
-      step prof_fetch 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof_fetch -o f --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu-baseline --graph 0 --e2e-iters 0
-      step prof_write 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof_write -o w --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu-baseline --graph 0 --e2e-iters 0
-      step prof_sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INSTS_LDS -d gpurun_out/prof_sq -o s --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu-baseline --graph 0 --e2e-iters 0
+      step prof_fetch 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof_fetch -o f --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu-baseline --graph 0 --e2e-iters 0 --streams 1
+      step prof_write 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof_write -o w --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu-baseline --graph 0 --e2e-iters 0 --streams 1
+      step prof_sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INSTS_LDS -d gpurun_out/prof_sq -o s --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu-baseline --graph 0 --e2e-iters 0 --streams 1
       rm -f gpurun_out/prof_*/*kernel_trace.csv
       ;;
     profa)
