@@ -51,18 +51,19 @@ def test_nonfinite_guard_counts(flavor):
     env.reset_counters()
     assert env.counters() == {"nonfinite_obs": 0, "nonfinite_rew": 0, "nonfinite_state": 0}
 
-    # a drone whose state went non-finite: counted once per step as a state, its reward, and every
-    # non-finite obs value the step wrote (its own row and the neighbour rows that see it)
+    # a drone whose attitude went non-finite (a non-finite position or velocity is sanitised by the room
+    # clip and the wall bounce, like in the reference): counted as a state, its reward (flavor B's orient
+    # term reads R22; flavor A's capture reward does not), and every non-finite obs value the step wrote
     g0 = 8 * 5 + 3
-    env.state[N.F_VEL, g0] = float("inf")
+    env.state[N.F_ROT + 4, g0] = float("nan")
     a = _acts(env, g)
     obs, rew, _, _ = env.step(a)
     torch.cuda.synchronize()
     c = env.counters()
     want_obs = int((~torch.isfinite(obs)).sum().item())
     assert c["nonfinite_state"] == int((~torch.isfinite(env.state[:N.F_ROT_DAMP])).any(0).sum().item()) >= 1
-    assert c["nonfinite_rew"] == int((~torch.isfinite(rew)).sum().item()) >= 1
-    assert c["nonfinite_obs"] == want_obs >= 3
+    assert c["nonfinite_rew"] == int((~torch.isfinite(rew)).sum().item()) >= (1 if flavor == "B" else 0)
+    assert c["nonfinite_obs"] == want_obs >= 1
     # only the poisoned env is affected
     bad_envs = set((torch.nonzero(~torch.isfinite(obs).all(1)).flatten() // 8).tolist())
     assert bad_envs == {5}
@@ -130,7 +131,10 @@ def test_specialised_replay_tail_reads_live_rew_crash():
     assert (gen.replay["hist"] != 0).any()
     for k in ("ri", "crash", "hist", "perm", "nrep"):
         assert torch.equal(gen.replay[k], spc.replay[k]), k
-    assert torch.equal(gen.state, spc.state) and torch.equal(gen.obs, spc.obs)
+    for k in ("state", "obs", "rew"):
+        a, b = getattr(gen, k), getattr(spc, k)
+        same = (a == b) | (torch.isnan(a) & torch.isnan(b))
+        assert bool(same.all()), (k, torch.nonzero(~same)[:8].tolist())
 
 
 @pytest.mark.parametrize("steps,chunk", [(25, 20), (20, 100)])
