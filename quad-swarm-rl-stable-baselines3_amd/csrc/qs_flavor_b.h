@@ -976,9 +976,13 @@ __device__ __forceinline__ void store_drone_q(const KP& kp, const Bufs& b, int g
     }
 }
 
+// Sub-lanes per drone of the flavor-B step kernel (QS_QB; 64 / NPAD when an env would not fit a wave).
+#ifndef QS_QB
+#define QS_QB 4
+#endif
 template <int NPAD>
 struct StepGeo {
-    static constexpr int Q = NPAD >= 32 ? 2 : 4;
+    static constexpr int Q = NPAD * QS_QB <= 64 ? QS_QB : 64 / NPAD;
     static constexpr int LPE = NPAD * Q;        // lanes per env
     static constexpr int EPB = 64 / LPE;        // envs per workgroup (one wave)
     static constexpr int SLOTS = EPB * NPAD;    // drone slots per workgroup

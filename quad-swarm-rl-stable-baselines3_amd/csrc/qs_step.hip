@@ -52,6 +52,7 @@ struct qs_handle {
     int npad;
     hipFunction_t jit_step = nullptr;    // qs_specialize: kernels compiled for this handle's parameters
     hipFunction_t jit_reset = nullptr;
+    int qb = QS_QB, qa = QS_QA;          // sub-lanes per drone of the step kernels in use (flavor B / A)
     // experience replay (qs_replay_enable): one device allocation holding every RBufs array
     void* rws = nullptr;
     bool rws_owned = false;
@@ -173,7 +174,7 @@ static int validate(const qs_config* c) {
 }
 
 static int npad_of(int n);
-static size_t shm_bytes(const qs_config& c, int obs_dim, int npad, bool step);
+static size_t shm_bytes(const qs_config& c, int obs_dim, int npad, bool step, int qb = QS_QB, int qa = QS_QA);
 static int neighbor_dim(int t);
 
 // pillar slots per env: the configured count, or the largest domain-randomisation choice
@@ -458,22 +459,21 @@ extern "C" int qs_layout_query(const qs_config* c, qs_layout* out) {
     return QS_OK;
 }
 
-// Flavor-B step launches give every drone Q lanes (qs::StepGeo); resets and flavor A one lane.
-static int step_lanes_per_drone(int npad) { return npad >= 32 ? 2 : 4; }
-static_assert(qs::StepGeo<8>::Q == 4 && qs::StepGeo<16>::Q == 4 && qs::StepGeo<32>::Q == 2, "step_lanes_per_drone");
-// flavor-A step launches: qs::StepGeoA (QS_QA sub-lanes per drone)
-static int step_lanes_per_drone_a(int npad) { return npad * QS_QA <= 64 ? QS_QA : 64 / npad; }
-static_assert(qs::StepGeoA<8>::Q == QS_QA && qs::StepGeoA<32>::Q == 2 && qs::StepGeoA<4>::Q == QS_QA,
-              "step_lanes_per_drone_a");
-static int envs_per_block(const qs_config& c, int npad, bool step) {
-    const int q = !step ? 1 : (c.flavor == QS_FLAVOR_A ? step_lanes_per_drone_a(npad) : step_lanes_per_drone(npad));
+// Step launches give every drone Q lanes (qs::StepGeo for flavor B: QS_QB, qs::StepGeoA for A: QS_QA; fewer
+// when an env would not fit a wave); resets one lane.  Specialised kernels may be compiled with another Q
+// (qs_handle::qb / qa).
+static int step_lanes_per_drone(int npad, int q) { return npad * q <= 64 ? q : 64 / npad; }
+static_assert(qs::StepGeo<8>::Q == QS_QB && qs::StepGeo<32>::Q == 64 / 32 && qs::StepGeoA<8>::Q == QS_QA &&
+              qs::StepGeoA<32>::Q == 2, "step_lanes_per_drone");
+static int envs_per_block(const qs_config& c, int npad, bool step, int qb = QS_QB, int qa = QS_QA) {
+    const int q = !step ? 1 : step_lanes_per_drone(npad, c.flavor == QS_FLAVOR_A ? qa : qb);
     return 64 / (npad * q);
 }
 
 // dynamic LDS of a launch with `slots` drone rows per workgroup: obs tile + neighbour exchange tile
 // + 64 words (flavor-A flags) + obstacle tiles and per-env reset scratch (qs_flavor_b.h obst_tile)
-static size_t shm_bytes(const qs_config& c, int obs_dim, int npad, bool step) {
-    const size_t epb = (size_t)envs_per_block(c, npad, step), slots = epb * (size_t)npad;
+static size_t shm_bytes(const qs_config& c, int obs_dim, int npad, bool step, int qb, int qa) {
+    const size_t epb = (size_t)envs_per_block(c, npad, step, qb, qa), slots = epb * (size_t)npad;
     size_t b = sizeof(float) * slots * (size_t)obs_dim + sizeof(float) * slots * 8 + sizeof(float) * 64;
     if (c.use_obstacles) b += epb * (sizeof(float) * 2 * (size_t)obst_slots(&c) + (size_t)qs::QS_OBST_SCRATCH);
     else if (c.flavor == QS_FLAVOR_B && c.scenario >= QS_SCEN_MIX)   // goal tables (qs::scen_stride)
@@ -582,9 +582,9 @@ static int launch(qs_handle* h, bool step, const float* act, const uint8_t* mask
     b.act = act;
     b.mask = mask;
     const qs::KP* kpd = (const qs::KP*)((char*)h->ws + h->lay.params);
-    const int epb = envs_per_block(h->cfg, h->npad, step);
+    const int epb = envs_per_block(h->cfg, h->npad, step, h->qb, h->qa);
     const dim3 grid((unsigned)((h->kp.E + epb - 1) / epb)), block(64);
-    const size_t shm = shm_bytes(h->cfg, h->kp.obs_dim, h->npad, step);
+    const size_t shm = shm_bytes(h->cfg, h->kp.obs_dim, h->npad, step, h->qb, h->qa);
     const bool a = h->cfg.flavor == QS_FLAVOR_A, ob = h->kp.obst != 0;
     // the flavor-B step kernel runs the replay wrapper in its tail (qs_replay.h); rb.ri == NULL: replay off
     qs::RBufs rb = h->rws ? h->rb : qs::RBufs{};
@@ -987,8 +987,8 @@ static std::string kp_words(const qs::KP& kp_in) {
 }
 
 // hipRTC compile of the step/reset kernels for one parameter block (host only)
-static int jit_compile(const qs_config* c, const qs::KP& kp, int npad, std::vector<char>& code, std::string& lstep,
-                       std::string& lreset) {
+static int jit_compile(const qs_config* c, const qs::KP& kp, int npad, int qb, int qa, std::vector<char>& code,
+                       std::string& lstep, std::string& lreset) {
     std::string reset_name;
     const std::string step_name = kernel_names(c, kp, npad, &reset_name);
     std::string src =
@@ -1001,7 +1001,8 @@ static int jit_compile(const qs_config* c, const qs::KP& kp, int npad, std::vect
         "typedef __hip_internal::uint64_t uint64_t;\n"
         "typedef __hip_internal::int64_t int64_t;\n"
         "typedef unsigned long uintptr_t;\n"
-        "#define QS_JIT 1\n#define QS_KP_WORDS " + kp_words(kp) + "\n";
+        "#define QS_JIT 1\n#define QS_QB " + std::to_string(qb) + "\n#define QS_QA " + std::to_string(qa) +
+        "\n#define QS_KP_WORDS " + kp_words(kp) + "\n";
     src += c->flavor == QS_FLAVOR_A ? "#include \"qs_flavor_a.h\"\n" : "#include \"qs_flavor_b.h\"\n";
     hiprtcProgram prog;
     if (hiprtcCreateProgram(&prog, src.c_str(), "qs_jit.hip", kJitNumHeaders, kJitHeaderSources, kJitHeaderNames) !=
@@ -1034,22 +1035,40 @@ static int jit_compile(const qs_config* c, const qs::KP& kp, int npad, std::vect
     return QS_OK;
 }
 
+// sub-lanes per drone of the specialised step kernels: the build default, or QS_QB / QS_QA (1, 2, 4) from the
+// environment (geometry experiments; the results are bitwise the same for every Q)
+static void jit_lanes(int* qb, int* qa) {
+    *qb = QS_QB;
+    *qa = QS_QA;
+    for (auto kv : {std::make_pair("QS_QB", qb), std::make_pair("QS_QA", qa)})
+        if (const char* v = getenv(kv.first)) {
+            const int x = atoi(v);
+            if (x == 1 || x == 2 || x == 4) *kv.second = x;
+        }
+}
+
 extern "C" int qs_specialize(qs_handle* h, int enable) {
     if (!h) return fail(QS_E_INVALID, "NULL handle");
     if (!enable) {
         h->jit_step = h->jit_reset = nullptr;
+        h->qb = QS_QB;
+        h->qa = QS_QA;
         return QS_OK;
     }
     QS_HIP(use_device(h));
+    int qb, qa;
+    jit_lanes(&qb, &qa);
+    if (shm_bytes(h->cfg, h->lay.obs_dim, h->npad, true, qb, qa) > 65536)
+        return fail(QS_E_UNSUPPORTED, "QS_QB / QS_QA geometry exceeds 64 KB of LDS per workgroup");
     std::string rn;
     const std::string key = std::to_string(h->device) + "|" + kernel_names(&h->cfg, h->kp, h->npad, &rn) + "|" +
-                            kp_words(h->kp);
+                            std::to_string(qb) + "," + std::to_string(qa) + "|" + kp_words(h->kp);
     std::lock_guard<std::mutex> lock(g_jit_mu);
     auto it = g_jit_cache.find(key);
     if (it == g_jit_cache.end()) {
         std::vector<char> code;
         std::string lstep, lreset;
-        if (int rc = jit_compile(&h->cfg, h->kp, h->npad, code, lstep, lreset)) return rc;
+        if (int rc = jit_compile(&h->cfg, h->kp, h->npad, qb, qa, code, lstep, lreset)) return rc;
         JitEntry e;
         QS_HIP(hipModuleLoadData(&e.mod, code.data()));
         QS_HIP(hipModuleGetFunction(&e.step, e.mod, lstep.c_str()));
@@ -1058,6 +1077,8 @@ extern "C" int qs_specialize(qs_handle* h, int enable) {
     }
     h->jit_step = it->second.step;
     h->jit_reset = it->second.reset;
+    h->qb = qb;
+    h->qa = qa;
     return QS_OK;
 }
 
@@ -1068,7 +1089,9 @@ extern "C" long long qs_specialize_compile(const qs_config* c) {
     const qs::KP kp = make_kp(c, make_layout(c));
     std::vector<char> code;
     std::string ls, lr;
-    if (int rc = jit_compile(c, kp, npad_of(c->num_agents), code, ls, lr)) return rc;
+    int qb, qa;
+    jit_lanes(&qb, &qa);
+    if (int rc = jit_compile(c, kp, npad_of(c->num_agents), qb, qa, code, ls, lr)) return rc;
     if (const char* dump = getenv("QS_JIT_DUMP")) {   // diagnostics: write the code object for llvm-objdump
         if (FILE* f = fopen(dump, "wb")) {
             fwrite(code.data(), 1, code.size(), f);
