@@ -1019,7 +1019,11 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
         for (int k = lane; k < nenv_blk * kp.M; k += 64) otile[k] = b.obst[(size_t)env0 * kp.M + k];
 
     Drone d;   // every sub-lane holds the whole drone
-#if QS_COOP_STATE
+#if defined(QS_DIAG_NOLOAD)   // diagnostic builds only (QS_JIT_OPTS): phase-removal timing experiments
+    d = Drone{};
+    d.pos[2] = 2.f; d.rot[0] = d.rot[4] = d.rot[8] = 1.f; d.goal[2] = 2.f;
+    d.pos[0] = 0.01f * (float)(g % 97); d.pos[1] = 0.01f * (float)(g % 89);
+#elif QS_COOP_STATE
     load_drone_q<Q>(kp, b, g, q, d);
 #else
     load_drone(kp, b, g, d);
@@ -1047,7 +1051,11 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
 #pragma unroll
         for (int t = 0; t < 4 / Q; ++t) {
             const int k = q + Q * t;
+#ifdef QS_DIAG_NOPHILOX
+            for (int i = 0; i < 4; ++i) zr[t][i] = 0.001f * (float)(i + k);
+#else
             if (k == 0 || kp.sense) normals4(rng, gid, k == 0 ? S_OU : S_SENSOR, k == 0 ? 0u : (uint32_t)(k - 1), zr[t]);
+#endif
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -1068,7 +1076,11 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
         float cmds[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) cmds[k] = 0.5f * (clampf(a[k], -1.f, 1.f) + 1.f);
+#ifndef QS_DIAG_NOPHYS
         for (int s = 0; s < kp.sim_steps; ++s) substep(kp, d, cmds, d.ou, rng, gid, s);
+#else
+        for (int i = 0; i < 3; ++i) d.pos[i] += 0.01f * d.vel[i] + 0.001f * cmds[i];
+#endif
         // compute_reward_weighted (quadrotor_single.py:34-66)
         const float gx = d.goal[0] - d.pos[0], gy = d.goal[1] - d.pos[1], gz = d.goal[2] - d.pos[2];
         const bool on_floor = d.flags & QS_FL_ON_FLOOR;
@@ -1086,7 +1098,11 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     float pen = 0.f;
     if (q == 0) xch_put(xch, dbase + di, d.pos, d.vel);
     lds_sync();
+#ifndef QS_DIAG_NOCOLL
     if (kp.N > 1) {
+#else
+    if (false) {
+#endif
         // sub-lane q tests the partners j = q + Q t (LDS reads issued back to back, branch-free
         // tests), then the drone's collision row and proximity sum are reduced over the sub-lanes
         constexpr int PJ = (NPAD + Q - 1) / Q;
@@ -1260,7 +1276,11 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
         lds_sync();
     }
     QS_STAMP(5);
+#ifndef QS_DIAG_NOSELFOBS
     if (lead) {
+#else
+    if (false) {
+#endif
         if (SCEN) {   // the self obs measure against the goal the reference's observation saw
             Drone dv = d;
             for (int k = 0; k < 3; ++k) dv.goal[k] = obs_goal[k];
@@ -1270,7 +1290,9 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
         }
     }
     QS_STAMP(6);
+#ifndef QS_DIAG_NONBR
     if (nbr) neighbor_obs<NPAD, Q>(kp, xch, dbase, di, q, d.pos, d.vel, active, row);
+#endif
     if (OBST && lead) sdf_obs(kp, og, myob, d.pos[0], d.pos[1], row + kp.obs_dim - 9);   // MultiObstacles.step
     QS_STAMP(7);
     // non-finite guard of the stepped drone and its reward (before a fused reset replaces the drone)
@@ -1335,10 +1357,15 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     }
     lds_sync();
     QS_STAMP(8);
+#ifndef QS_DIAG_NOOBSSTORE
     const int obs_bad = tile_store(lds, b.obs + (size_t)env0 * kp.N * kp.obs_dim, rows * kp.obs_dim, lane);
+#else
+    const int obs_bad = 0;
+#endif
     QS_STAMP(9);
 
-#if QS_COOP_STATE
+#if defined(QS_DIAG_NOSTORE)
+#elif QS_COOP_STATE
     store_drone_q<Q>(kp, b, g, q, active, d);
 #else
     if (lead) store_drone(kp, b, g, d);
@@ -1357,7 +1384,9 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
             if (nf != ef) b.env[QS_E_FLAGS * kp.E + env] = nf;
         }
     }
+#ifndef QS_DIAG_NOGUARD
     guard_count(b, obs_bad, rew_bad, state_bad);
+#endif
     QS_STAMP(10);
     if (r.ri != nullptr) {   // experience replay on (uniform): ExperienceReplayWrapper.step of every env (:124-180)
         // the step's global stores above are read back by other lanes of the wave: workgroup-scope

@@ -986,6 +986,23 @@ static std::string kp_words(const qs::KP& kp_in) {
     return words;
 }
 
+static std::vector<std::string> jit_extra_opts() {
+    std::vector<std::string> v;
+    if (const char* e = getenv("QS_JIT_OPTS")) {
+        std::string cur;
+        for (const char* p = e;; ++p) {
+            if (*p == ' ' || *p == '\0') {
+                if (!cur.empty()) v.push_back(cur);
+                cur.clear();
+                if (!*p) break;
+            } else {
+                cur += *p;
+            }
+        }
+    }
+    return v;
+}
+
 // hipRTC compile of the step/reset kernels for one parameter block (host only)
 static int jit_compile(const qs_config* c, const qs::KP& kp, int npad, int qb, int qa, std::vector<char>& code,
                        std::string& lstep, std::string& lreset) {
@@ -1010,9 +1027,12 @@ static int jit_compile(const qs_config* c, const qs::KP& kp, int npad, int qb, i
         return fail(QS_E_HIP, "hiprtcCreateProgram failed");
     hiprtcAddNameExpression(prog, step_name.c_str());
     hiprtcAddNameExpression(prog, reset_name.c_str());
-    const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=on",
-                          "-munsafe-fp-atomics"};
-    const hiprtcResult rc = hiprtcCompileProgram(prog, (int)(sizeof opts / sizeof opts[0]), opts);
+    std::vector<const char*> opts = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=on",
+                                     "-munsafe-fp-atomics"};
+    // QS_JIT_OPTS: extra space-separated hipRTC options (kernel-variant experiments, e.g. -DQS_X=1)
+    std::vector<std::string> extra = jit_extra_opts();
+    for (const std::string& o : extra) opts.push_back(o.c_str());
+    const hiprtcResult rc = hiprtcCompileProgram(prog, (int)opts.size(), opts.data());
     if (rc != HIPRTC_SUCCESS) {
         size_t n = 0;
         hiprtcGetProgramLogSize(prog, &n);
@@ -1062,7 +1082,8 @@ extern "C" int qs_specialize(qs_handle* h, int enable) {
         return fail(QS_E_UNSUPPORTED, "QS_QB / QS_QA geometry exceeds 64 KB of LDS per workgroup");
     std::string rn;
     const std::string key = std::to_string(h->device) + "|" + kernel_names(&h->cfg, h->kp, h->npad, &rn) + "|" +
-                            std::to_string(qb) + "," + std::to_string(qa) + "|" + kp_words(h->kp);
+                            std::to_string(qb) + "," + std::to_string(qa) + "|" +
+                            (getenv("QS_JIT_OPTS") ? getenv("QS_JIT_OPTS") : "") + "|" + kp_words(h->kp);
     std::lock_guard<std::mutex> lock(g_jit_mu);
     auto it = g_jit_cache.find(key);
     if (it == g_jit_cache.end()) {
