@@ -26,6 +26,7 @@ struct KP {
     float dt, cdt, mass, inv_mass, inertia[3], inv_inertia[3];
     float thrust_max[4], torque_max[4], pc0[4], pc1[4], pc2[4], ccw[4];
     float tau_up, tau_down, lin, arm, grav, omega_max, vel_damp, dq, vxyz_max;
+    float mass_g;   // mass * gravity rounded once on the host (the floor friction: the same bits in both builds)
     float room_lo[3], room_hi[3], room_range[3];
     float ou_mu, ou_theta, ou_sigma;
     float pos_std, pos_unif, vel_std, vel_unif, gyro, quat_std, quat_unif;
@@ -287,6 +288,24 @@ __device__ __forceinline__ void yaw_rot(float theta, float* R) {
     R[6] = 0.f; R[7] = 0.f; R[8] = 1.f;
 }
 
+// yaw_rot(atan2(y, x)) without trigonometry: cos / sin of atan2(y, x) are x / |(x, y)| and y / |(x, y)|
+// (for (x, y) = (+-0, +-0): atan2 = 0 or +-pi by the signs, cos = +-1, sin = +-0)
+__device__ __forceinline__ void yaw_rot_xy(float x, float y, float* R) {
+    const float h2 = x * x + y * y;
+    float c, s;
+    if (h2 > 0.f) {
+        const float r = __builtin_amdgcn_rsqf(h2);
+        c = x * r;
+        s = y * r;
+    } else {
+        c = __builtin_copysignf(1.f, x);
+        s = __builtin_copysignf(0.f, y);
+    }
+    R[0] = c; R[1] = -s; R[2] = 0.f;
+    R[3] = s; R[4] = c; R[5] = 0.f;
+    R[6] = 0.f; R[7] = 0.f; R[8] = 1.f;
+}
+
 // polar factor (u @ vh of the SVD, :554-558): Newton X <- (X + X^-T)/2; R is within ~1e-5 of
 // orthonormal after 100 fp32 substeps, three iterations converge to fp32 precision.
 __device__ __forceinline__ void polar3(float* x) {
@@ -395,23 +414,32 @@ __device__ __forceinline__ void substep(const KP& kp, Drone& d, const float* cmd
     float ax, ay, az;
     if (d.pos[2] <= kp.arm) {
         d.pos[2] = kp.arm;
-        if (fl & QS_FL_ON_FLOOR) {
-            yaw_rot(atan2f(R[3], R[0] + 1e-6f), R);
-            const float fric = 0.6f * (kp.mass * kp.grav - fz);
+        if (fl & QS_FL_ON_FLOOR) {   // resting on the floor: the common case of an untrained swarm
+            // rot = yaw_rot(arctan2(R10, R00 + EPS)) and the friction directions cos / sin of arctan2 as
+            // normalised components (no atan2 / sin / cos)
+            yaw_rot_xy(R[0] + 1e-6f, R[3], R);
+            const float fric = 0.6f * (kp.mass_g - fz);
             const float vn = fsqrt(d.vel[0] * d.vel[0] + d.vel[1] * d.vel[1] + d.vel[2] * d.vel[2]);
             if (vn < 1e-6f) {
-                float fxy = fsqrt(fx * fx + fy * fy);
-                fxy = fmaxf(fxy - fric, 0.f);
+                const float f2 = fx * fx + fy * fy, fm = fsqrt(f2);
+                const float fxy = fmaxf(fm - fric, 0.f);
                 if (fxy == 0.f) {
                     fx = 0.f; fy = 0.f;
-                } else {
-                    float sa, ca;
-                    sincos_hw(atan2f(fy, fx), &sa, &ca);
-                    fx = fxy * ca; fy = fxy * sa;
+                } else {   // fm > fric >= 0
+                    const float k = fxy * __builtin_amdgcn_rsqf(f2);
+                    fx = k * fx; fy = k * fy;
                 }
             } else {
-                float sa, ca;
-                sincos_hw(atan2f(d.vel[1], d.vel[0]), &sa, &ca);
+                const float v2 = d.vel[0] * d.vel[0] + d.vel[1] * d.vel[1];
+                float ca, sa;
+                if (v2 > 0.f) {
+                    const float r = __builtin_amdgcn_rsqf(v2);
+                    ca = d.vel[0] * r;
+                    sa = d.vel[1] * r;
+                } else {
+                    ca = __builtin_copysignf(1.f, d.vel[0]);
+                    sa = __builtin_copysignf(0.f, d.vel[1]);
+                }
                 fx = fx - ca * fric;
                 fy = fy - sa * fric;
             }

@@ -1190,7 +1190,11 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
             }
         }
     }
+#ifndef QS_DIAG_NOIMPULSE
     if (kp.collide) {
+#else
+    if (false) {
+#endif
         // drone-drone impulses, pairs in (i, j) order; a wave-uniform loop over pending events.
         // Ballots read sub-lane 0 of each drone (bit lbase + i * Q).
         uint64_t pend = active ? (newpairs & ~((2ull << di) - 1ull)) : 0ull;

@@ -327,6 +327,7 @@ static qs::KP make_kp(const qs_config* c, const qs_layout& L) {
     k.tau_up = c->motor_tau_up; k.tau_down = c->motor_tau_down; k.lin = c->motor_linearity;
     k.arm = c->arm; k.grav = c->gravity; k.omega_max = c->omega_max; k.vel_damp = c->vel_damp;
     k.dq = c->damp_omega_quadratic; k.vxyz_max = c->vxyz_max;
+    k.mass_g = (float)((double)c->mass * (double)c->gravity);
     k.ou_mu = c->ou_mu; k.ou_theta = c->ou_theta; k.ou_sigma = c->ou_sigma;
     k.pos_std = c->pos_norm_std; k.pos_unif = c->pos_unif_range; k.vel_std = c->vel_norm_std;
     k.vel_unif = c->vel_unif_range; k.gyro = c->gyro_noise_density; k.quat_std = c->quat_norm_std;
