@@ -529,6 +529,15 @@ __device__ __forceinline__ float cos_any(float x) {
     return __builtin_amdgcn_cosf(r - rintf(r));
 }
 
+// The drone count as a run-time value: in the specialised build kp.N is a constant, and the compiler would
+// constant-fold the hardware transcendentals of the formation geometry exactly (sin / cos / log2 / exp2 of
+// constant arguments) where the generic build evaluates them on the approximate hardware units.
+__device__ __forceinline__ int sc_num(const KP& kp) {
+    int n = kp.N;
+    asm volatile("" : "+v"(n));
+    return n;
+}
+
 // QUADS_PARAMS_DICT (utils.py:33-53)
 __device__ __forceinline__ void sc_mode_params(int mode, int& nform, float& low, float& high) {
     if (mode == SC_STATIC_DIFF_GOAL || mode == SC_DYNAMIC_DIFF_GOAL || mode == SC_SWARM_VS_SWARM || mode == SC_RUN_AWAY) {
@@ -625,7 +634,7 @@ __device__ void sc_update_formation(const KP& kp, Scen& s, SDraw& sd) {
         const float k = 0.5f / __builtin_amdgcn_sinf(0.5f / (float)pl);
         s.lo = low * k; s.hi = high * k;
     } else if (s.form == F_SPHERE) {   // get_sphere_radius
-        const int n = s.mode == SC_SWARM_VS_SWARM ? kp.N / 2 : kp.N;
+        const int n = s.mode == SC_SWARM_VS_SWARM ? sc_num(kp) / 2 : sc_num(kp);
         const float ratio = (1.75388487222762f - 0.0920858134405214f) /
                                 (1.f + exp2f(0.860487305801679f * __log2f((float)n / 10.3632729642351f))) +
                             0.0920858134405214f;
@@ -653,7 +662,7 @@ __device__ float sc_z_value(const KP& kp, const Scen& s, SDraw& sd) {
 
 // swarm_vs_swarm create_formations (swarm_vs_swarm.py:49-54) [+ update_goals' shuffles]; tmp: scratch rows
 __device__ void sc_vs_formations(const KP& kp, Scen& s, float* g, float* tmp, bool shuffle, SDraw& sd) {
-    const int N = kp.N, pl = sc_per_layer(s.form);
+    const int N = sc_num(kp), pl = sc_per_layer(s.form);
     const int n1 = sc_generate(s.form, N / 2, pl, s.size, s.layer, s.c1, g);
     if (shuffle) sd_shuffle(sd, g, n1);
     const int n2 = sc_generate(s.form, N - N / 2, pl, s.size, s.layer, s.c2, tmp);
@@ -664,8 +673,8 @@ __device__ void sc_vs_formations(const KP& kp, Scen& s, float* g, float* tmp, bo
 
 // Scenario_mix.reset (mix.py:79-99) -> <scenario>.__init__ + .reset: the N goals into g
 __device__ void scen_reset(const KP& kp, Scen& s, SDraw& sd, float* g, float* tmp) {
-    const int N = kp.N;
     s = Scen{};   // a fresh Scenario_* object per reset (mix.py:88)
+    const int N = sc_num(kp);
     const float cf = 1.f / kp.cdt;
     s.mode = kp.scen_b == SC_MIX ? sd_int(sd, 0, N == 1 ? 5 : 9) : kp.scen_b;
     s.period = (int)(5.f * cf);
@@ -713,7 +722,7 @@ __device__ void scen_reset(const KP& kp, Scen& s, SDraw& sd, float* g, float* tm
 
 // <scenario>.step() after the drones stepped (quadrotor_multi.py:700-701), tick = envs[0].tick
 __device__ void scen_step(const KP& kp, Scen& s, int tick, SDraw& sd, float* g, float* tmp) {
-    const int N = kp.N;
+    const int N = sc_num(kp);
     const float box = kp.spawn_box, cf = 1.f / kp.cdt;
     const int pl = sc_per_layer(s.form);
     const bool ev = s.period > 0 && tick % s.period == 0 && tick > 0;
@@ -1215,9 +1224,41 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
             }
             const bool involved = eb != 0 && (di == istar || di == jstar);
             vchanged |= involved;
-            if (involved) {   // both drones' sub-lanes draw the pair's 9 Philox blocks in parallel
-                const uint32_t gi = kp.id0 + (uint32_t)(env * kp.N + istar);
-                const uint32_t st = S_PAIR | ((uint32_t)jstar << 8);
+            const uint32_t gi = kp.id0 + (uint32_t)(env * kp.N + istar);
+            const uint32_t st = S_PAIR | ((uint32_t)jstar << 8);
+            if constexpr (LPE >= 9) {
+                // The env's lanes draw the pair's 9 Philox blocks (7 normal, 2 uniform) in ONE round, lane le
+                // block le, and hand them to the pair's lanes through LDS (the obs tile is free until the obs
+                // phase).  An event is rare, but the wave that has one is the launch's last: keep it short.
+                float4* pscr = reinterpret_cast<float4*>(lds) + el * 9;
+                const int le = lane - lbase;
+                if (eb != 0 && le < 9) {
+                    const bool isn = le < 7;
+                    const W4 w = block(rng, gi, isn ? st : (st | UNIF_BIT), (uint32_t)(isn ? le : le - 7));
+                    float v[4];
+                    if (isn) {
+                        box_muller(w.w[0], w.w[1], v[0], v[1]);
+                        box_muller(w.w[2], w.w[3], v[2], v[3]);
+                    } else {
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) v[i] = u01(w.w[i]);
+                    }
+                    pscr[le] = make_float4(v[0], v[1], v[2], v[3]);
+                }
+                lds_sync();
+                if (involved) {
+                    float z[28], u[8];
+#pragma unroll
+                    for (int k = 0; k < 9; ++k) {
+                        const float4 x = pscr[k];
+                        float* o = k < 7 ? z + 4 * k : u + 4 * (k - 7);
+                        o[0] = x.x; o[1] = x.y; o[2] = x.z; o[3] = x.w;
+                    }
+                    if (di == istar) collide_pair(d.pos, d.vel, d.om, pp, pv, pw, z, u);
+                    else collide_pair(pp, pv, pw, d.pos, d.vel, d.om, z, u);
+                }
+                lds_sync();   // the scratch is rewritten by the next event
+            } else if (involved) {   // both drones' sub-lanes draw the pair's 9 Philox blocks in parallel
                 float z[28], u[8];
                 qdraws<Q, 7, 2>(rng, gi, st, st, q, z, u);
                 if (di == istar) collide_pair(d.pos, d.vel, d.om, pp, pv, pw, z, u);
@@ -1271,6 +1312,18 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
             }
     }
 
+    // The drone state is final here (unless its env resets below, which stores it again): storing it now
+    // lets its write-through bytes drain while the observations are computed.
+#if defined(QS_DIAG_NOSTORE)
+#elif QS_COOP_STATE
+    store_drone_q<Q>(kp, b, g, q, active, d);
+#else
+    if (lead) store_drone(kp, b, g, d);
+#endif
+    if (lead) {
+        b.rew[g] = rw;
+        b.done[g] = done ? 1 : 0;
+    }
     QS_STAMP(4);
     // ---- observations (post-impulse state; quadrotor_multi.py:704-720) ----
     const bool nbr = kp.neighbor == QS_NEIGHBOR_POS_VEL && kp.K > 0;
@@ -1348,6 +1401,12 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
             reset_drone(kp, d, rng, gid, spawn, goal);
             if (q == 0) self_obs(kp, d, rng, gid, S_RESET_SENSOR, row);
         }
+        // the reset drones' state (the stepped state was stored before the obs phase)
+#if QS_COOP_STATE
+        store_drone_q<Q>(kp, b, g, q, active && done, d);
+#else
+        if (lead && done) store_drone(kp, b, g, d);
+#endif
         if (nbr) {
             if (q == 0) xch_put(xch, dbase + di, d.pos, sv);
             lds_sync();
@@ -1368,15 +1427,7 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
 #endif
     QS_STAMP(9);
 
-#if defined(QS_DIAG_NOSTORE)
-#elif QS_COOP_STATE
-    store_drone_q<Q>(kp, b, g, q, active, d);
-#else
-    if (lead) store_drone(kp, b, g, d);
-#endif
     if (lead) {
-        b.rew[g] = rw;
-        b.done[g] = done ? 1 : 0;
         if (di == 0) {
             b.env[QS_E_TICK * kp.E + env] = done ? 0 : tick;
             if (done) b.env[QS_E_EPISODE * kp.E + env] = episode + 1;
