@@ -321,12 +321,18 @@ __device__ __forceinline__ void polar3(float* x) {
     }
 }
 
-__device__ __forceinline__ void substep(const KP& kp, Drone& d, const float* cmds, const float* noise, const Rng& rng, uint32_t gid,
-                        int s) {
-    const float dt = kp.dt;
-    float thrusts[4], tq0 = 0.f, tq1 = 0.f, tq2 = 0.f, tsum = 0.f;
+// The substep in three pieces (motors -> torques, Rodrigues attitude update, the rest), so that the
+// flavor-B step kernel can deal the first two over a drone's sub-lanes (substep_q in qs_flavor_b.h).
+struct Torque {
+    float t0, t1, t2, sum;   // body torque, total thrust
+};
+
+// motor filter in sqrt space + multiplicative OU noise (:511-524) and torques (:527-533), all 4 motors
+__device__ __forceinline__ Torque motors(const KP& kp, Drone& d, const float* cmds, const float* noise) {
+    float thrusts[4];
+    Torque t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {  // motor filter in sqrt space + multiplicative OU noise (:511-524)
+    for (int k = 0; k < 4; ++k) {
         const float cmd = cmds[k];
         float tau = cmd < d.cd[k] ? kp.tau_down : kp.tau_up;
         tau = fminf(tau, 1.0f);
@@ -338,48 +344,92 @@ __device__ __forceinline__ void substep(const KP& kp, Drone& d, const float* cmd
         thrusts[k] = kp.thrust_max[k] * (kp.lin == 1.f ? c : (1.f - kp.lin) * c * c + kp.lin * c);
     }
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {  // torques (:527-533); zero arm coefficients add exactly +-0: skipped
-        if (kp.pc0[k] != 0.f) tq0 += kp.pc0[k] * thrusts[k];
-        if (kp.pc1[k] != 0.f) tq1 += kp.pc1[k] * thrusts[k];
-        if (kp.pc2[k] != 0.f) tq2 += kp.pc2[k] * thrusts[k];
-        tq2 += kp.torque_max[k] * kp.ccw[k] * d.cd[k];
-        tsum += thrusts[k];
+    for (int k = 0; k < 4; ++k) {  // zero arm coefficients add exactly +-0: skipped
+        if (kp.pc0[k] != 0.f) t.t0 += kp.pc0[k] * thrusts[k];
+        if (kp.pc1[k] != 0.f) t.t1 += kp.pc1[k] * thrusts[k];
+        if (kp.pc2[k] != 0.f) t.t2 += kp.pc2[k] * thrusts[k];
+        t.t2 += kp.torque_max[k] * kp.ccw[k] * d.cd[k];
+        t.sum += thrusts[k];
     }
-    float* R = d.rot;
-    {  // Rodrigues with world-frame omega (:544-551):  dR = I + sin(a) K + (1 - cos a) K^2,
-       // K = skew(w)/|w|, a = |w| dt.  Written as I + dt S(a^2) skew(w) + dt^2 C(a^2) (w w^T - |w|^2 I)
-       // with S = sin(a)/a and C = (1 - cos a)/a^2: no sqrt, no division, no branch at w = 0 (where
-       // the reference skips the update: dR = I exactly as the series gives).
-        const float wx = R[0] * d.om[0] + R[1] * d.om[1] + R[2] * d.om[2];
-        const float wy = R[3] * d.om[0] + R[4] * d.om[1] + R[5] * d.om[2];
-        const float wz = R[6] * d.om[0] + R[7] * d.om[1] + R[8] * d.om[2];
-        const float w2 = wx * wx + wy * wy + wz * wz;
-        const float x = w2 * (dt * dt);
-        float sf, cf;
-        if (x < 0.36f) {  // a < 0.6: Taylor to a^8, truncation < 2e-10 (|omega| <= 40 per axis gives a <= 0.35)
-            sf = dt * (1.f + x * (-1.f / 6.f + x * (1.f / 120.f + x * (-1.f / 5040.f + x * (1.f / 362880.f)))));
-            cf = dt * dt * (0.5f + x * (-1.f / 24.f + x * (1.f / 720.f + x * (-1.f / 40320.f + x * (1.f / 3628800.f)))));
-        } else {          // after collision kicks (|omega| up to ~100 rad/s before the clip)
-            const float wn = fsqrt(w2), a = wn * dt;
-            float sa, ca;
-            sincos_hw(0.5f * a, &sa, &ca);
-            sf = 2.f * sa * ca / wn;
-            cf = 2.f * sa * sa / w2;
-        }
-        const float sx = sf * wx, sy = sf * wy, sz = sf * wz;
-        const float d0 = 1.f - cf * w2;
-        const float dR[9] = {d0 + cf * wx * wx, -sz + cf * wx * wy, sy + cf * wx * wz,
-                             sz + cf * wx * wy, d0 + cf * wy * wy, -sx + cf * wy * wz,
-                             -sy + cf * wx * wz, sx + cf * wy * wz, d0 + cf * wz * wz};
+    return t;
+}
+
+// Rodrigues with world-frame omega (:544-551):  dR = I + sin(a) K + (1 - cos a) K^2, K = skew(w)/|w|,
+// a = |w| dt.  Written as I + dt S(a^2) skew(w) + dt^2 C(a^2) (w w^T - |w|^2 I) with S = sin(a)/a and
+// C = (1 - cos a)/a^2: no sqrt, no division, no branch at w = 0 (where the reference skips the update:
+// dR = I exactly as the series gives).  rod_coef gives w, sx sy sz = S w, cf = C, d0 = 1 - C |w|^2.
+struct RodCoef {
+    float w[3], s[3], cf, d0;
+};
+__device__ __forceinline__ RodCoef rod_coef(const KP& kp, const float* R, const float* om) {
+    const float dt = kp.dt;
+    RodCoef r;
+    r.w[0] = R[0] * om[0] + R[1] * om[1] + R[2] * om[2];
+    r.w[1] = R[3] * om[0] + R[4] * om[1] + R[5] * om[2];
+    r.w[2] = R[6] * om[0] + R[7] * om[1] + R[8] * om[2];
+    const float w2 = r.w[0] * r.w[0] + r.w[1] * r.w[1] + r.w[2] * r.w[2];
+    const float x = w2 * (dt * dt);
+    float sf, cf;
+    if (x < 0.36f) {  // a < 0.6: Taylor to a^8, truncation < 2e-10 (|omega| <= 40 per axis gives a <= 0.35)
+        sf = dt * (1.f + x * (-1.f / 6.f + x * (1.f / 120.f + x * (-1.f / 5040.f + x * (1.f / 362880.f)))));
+        cf = dt * dt * (0.5f + x * (-1.f / 24.f + x * (1.f / 720.f + x * (-1.f / 40320.f + x * (1.f / 3628800.f)))));
+    } else {          // after collision kicks (|omega| up to ~100 rad/s before the clip)
+        const float wn = fsqrt(w2), a = wn * dt;
+        float sa, ca;
+        sincos_hw(0.5f * a, &sa, &ca);
+        sf = 2.f * sa * ca / wn;
+        cf = 2.f * sa * sa / w2;
+    }
+    r.s[0] = sf * r.w[0]; r.s[1] = sf * r.w[1]; r.s[2] = sf * r.w[2];
+    r.cf = cf;
+    r.d0 = 1.f - cf * w2;
+    return r;
+}
+// row i of dR
+__device__ __forceinline__ void rod_row(const RodCoef& r, int i, float* o) {
+    const float wi = r.w[i], cw = r.cf * wi;
+    // skew(s) row i: [0, -s2, s1] / [s2, 0, -s0] / [-s1, s0, 0], diagonal d0
+    const float a0 = i == 0 ? r.d0 : (i == 1 ? r.s[2] : -r.s[1]);
+    const float a1 = i == 0 ? -r.s[2] : (i == 1 ? r.d0 : r.s[0]);
+    const float a2 = i == 0 ? r.s[1] : (i == 1 ? -r.s[0] : r.d0);
+    o[0] = a0 + cw * r.w[0];
+    o[1] = a1 + cw * r.w[1];
+    o[2] = a2 + cw * r.w[2];
+}
+// row i of dR @ R
+__device__ __forceinline__ void rod_apply_row(const float* dr, const float* R, float* o) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) o[j] = dr[0] * R[j] + dr[1] * R[3 + j] + dr[2] * R[6 + j];
+}
+
+__device__ __forceinline__ void substep_tail(const KP& kp, Drone& d, const Torque& tq, const Rng& rng, uint32_t gid,
+                                             int s);
+
+// one substep == step1_numba (quadrotor_dynamics.py:355-390), everything on this lane
+__device__ __forceinline__ void substep(const KP& kp, Drone& d, const float* cmds, const float* noise, const Rng& rng, uint32_t gid,
+                        int s) {
+    const Torque tq = motors(kp, d, cmds, noise);
+    {
+        const RodCoef rc = rod_coef(kp, d.rot, d.om);
         float Rn[9];
 #pragma unroll
-        for (int i = 0; i < 3; ++i)
+        for (int i = 0; i < 3; ++i) {
+            float dr[3];
+            rod_row(rc, i, dr);
+            rod_apply_row(dr, d.rot, Rn + 3 * i);
+        }
 #pragma unroll
-            for (int j = 0; j < 3; ++j)
-                Rn[i * 3 + j] = dR[i * 3] * R[j] + dR[i * 3 + 1] * R[3 + j] + dR[i * 3 + 2] * R[6 + j];
-#pragma unroll
-        for (int i = 0; i < 9; ++i) R[i] = Rn[i];
+        for (int i = 0; i < 9; ++i) d.rot[i] = Rn[i];
     }
+    substep_tail(kp, d, tq, rng, gid, s);
+}
+
+// polar re-orthonormalisation, omega, position + room clip, floor, velocity (:553-656)
+__device__ __forceinline__ void substep_tail(const KP& kp, Drone& d, const Torque& tq, const Rng& rng, uint32_t gid,
+                                             int s) {
+    const float dt = kp.dt;
+    float* R = d.rot;
+    const float tq0 = tq.t0, tq1 = tq.t1, tq2 = tq.t2, tsum = tq.sum;
     if (++d.svd >= kp.svd_every) {  // since_last_svd > 0.5 s (:553-558)
         polar3(R);
         d.svd = 0;

@@ -997,6 +997,108 @@ struct StepGeo {
     static constexpr int SLOTS = EPB * NPAD;    // drone slots per workgroup
 };
 
+// ---------------------------------------------------------------------------------------------
+// The physics dealt over a drone's Q sub-lanes (QS_DEAL_PHYS): sub-lane q owns motors q + Q t (their
+// filter state, thrust and torque contributions, summed over the sub-lanes by DPP) and rows q + Q t of
+// the Rodrigues update (dR row @ R, rows broadcast by DPP).  The rest of the substep stays replicated.
+// Same expressions per element as substep(); the torque sums run in the pairwise order of qsum.
+// ---------------------------------------------------------------------------------------------
+#ifndef QS_DEAL_PHYS
+#define QS_DEAL_PHYS 1
+#endif
+__device__ __forceinline__ float pick4(int k, float a0, float a1, float a2, float a3) {
+    return k == 0 ? a0 : (k == 1 ? a1 : (k == 2 ? a2 : a3));
+}
+template <int Q>
+struct OwnMotors {
+    static constexpr int T = 4 / Q;
+    float cmd[T], scmd[T], noise[T], rd[T], cd[T], tmax[T], pc0[T], pc1[T], pc2[T], tmc[T];
+};
+template <int Q>
+__device__ __forceinline__ void own_motors(const KP& kp, const Drone& d, const float* cmds, int q, OwnMotors<Q>& o) {
+#pragma unroll
+    for (int t = 0; t < OwnMotors<Q>::T; ++t) {
+        const int m = q + Q * t;
+        o.cmd[t] = pick4(m, cmds[0], cmds[1], cmds[2], cmds[3]);
+        o.scmd[t] = fsqrt(o.cmd[t]);
+        o.noise[t] = pick4(m, d.ou[0], d.ou[1], d.ou[2], d.ou[3]);
+        o.rd[t] = pick4(m, d.rd[0], d.rd[1], d.rd[2], d.rd[3]);
+        o.cd[t] = pick4(m, d.cd[0], d.cd[1], d.cd[2], d.cd[3]);
+        o.tmax[t] = pick4(m, kp.thrust_max[0], kp.thrust_max[1], kp.thrust_max[2], kp.thrust_max[3]);
+        o.pc0[t] = pick4(m, kp.pc0[0], kp.pc0[1], kp.pc0[2], kp.pc0[3]);
+        o.pc1[t] = pick4(m, kp.pc1[0], kp.pc1[1], kp.pc1[2], kp.pc1[3]);
+        o.pc2[t] = pick4(m, kp.pc2[0], kp.pc2[1], kp.pc2[2], kp.pc2[3]);
+        o.tmc[t] = pick4(m, kp.torque_max[0] * kp.ccw[0], kp.torque_max[1] * kp.ccw[1], kp.torque_max[2] * kp.ccw[2],
+                         kp.torque_max[3] * kp.ccw[3]);
+    }
+}
+template <int Q>
+__device__ __forceinline__ Torque motors_q(const KP& kp, OwnMotors<Q>& o) {
+    const bool p0 = kp.pc0[0] != 0.f || kp.pc0[1] != 0.f || kp.pc0[2] != 0.f || kp.pc0[3] != 0.f;
+    const bool p1 = kp.pc1[0] != 0.f || kp.pc1[1] != 0.f || kp.pc1[2] != 0.f || kp.pc1[3] != 0.f;
+    const bool p2 = kp.pc2[0] != 0.f || kp.pc2[1] != 0.f || kp.pc2[2] != 0.f || kp.pc2[3] != 0.f;
+    Torque t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < OwnMotors<Q>::T; ++k) {   // motors() for the owned motors
+        const float cmd = o.cmd[k];
+        float tau = cmd < o.cd[k] ? kp.tau_down : kp.tau_up;
+        tau = fminf(tau, 1.0f);
+        o.rd[k] = tau * (o.scmd[k] - o.rd[k]) + o.rd[k];
+        const float c = clampf(o.rd[k] * o.rd[k] + cmd * o.noise[k], 0.f, 1.f);
+        o.cd[k] = c;
+        const float thr = o.tmax[k] * (kp.lin == 1.f ? c : (1.f - kp.lin) * c * c + kp.lin * c);
+        if (p0) t.t0 += o.pc0[k] * thr;
+        if (p1) t.t1 += o.pc1[k] * thr;
+        if (p2) t.t2 += o.pc2[k] * thr;
+        t.t2 += o.tmc[k] * c;
+        t.sum += thr;
+    }
+    t.t0 = qsum<Q>(t.t0);
+    t.t1 = qsum<Q>(t.t1);
+    t.t2 = qsum<Q>(t.t2);
+    t.sum = qsum<Q>(t.sum);
+    return t;
+}
+template <int Q, int TR>
+__device__ __forceinline__ void bcast_rows(const float (&rows)[TR][3], float* R) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        R[j] = qbc<Q, 0 % Q>(rows[0 / Q][j]);
+        R[3 + j] = qbc<Q, 1 % Q>(rows[1 / Q][j]);
+        R[6 + j] = qbc<Q, 2 % Q>(rows[2 / Q][j]);
+    }
+}
+// the step's sim_steps substeps; cmds = the clipped motor commands, d.ou = this tick's OU noise
+template <int Q>
+__device__ __forceinline__ void physics_q(const KP& kp, Drone& d, const float* cmds, int q, const Rng& rng, uint32_t gid) {
+    constexpr int TR = (3 + Q - 1) / Q;
+    OwnMotors<Q> o;
+    own_motors<Q>(kp, d, cmds, q, o);
+    for (int s = 0; s < kp.sim_steps; ++s) {
+        const Torque tq = motors_q<Q>(kp, o);
+        const RodCoef rc = rod_coef(kp, d.rot, d.om);
+        float rows[TR][3];
+#pragma unroll
+        for (int t = 0; t < TR; ++t) {
+            const int r = min(q + Q * t, 2);
+            float dr[3];
+            rod_row(rc, r, dr);
+            rod_apply_row(dr, d.rot, rows[t]);
+        }
+        bcast_rows<Q, TR>(rows, d.rot);
+        substep_tail(kp, d, tq, rng, gid, s);
+        if (d.flags & QS_FL_CRASH_FLOOR) {   // the floor contact zeroed the filters (replicated copy too)
+#pragma unroll
+            for (int t = 0; t < OwnMotors<Q>::T; ++t) { o.rd[t] = 0.f; o.cd[t] = 0.f; }
+        }
+    }
+    // the owners' filter state back on every sub-lane (state store)
+    d.rd[0] = qbc<Q, 0 % Q>(o.rd[0 / Q]); d.cd[0] = qbc<Q, 0 % Q>(o.cd[0 / Q]);
+    d.rd[1] = qbc<Q, 1 % Q>(o.rd[1 / Q]); d.cd[1] = qbc<Q, 1 % Q>(o.cd[1 / Q]);
+    d.rd[2] = qbc<Q, 2 % Q>(o.rd[2 / Q]); d.cd[2] = qbc<Q, 2 % Q>(o.cd[2 / Q]);
+    d.rd[3] = qbc<Q, 3 % Q>(o.rd[3 / Q]); d.cd[3] = qbc<Q, 3 % Q>(o.cd[3 / Q]);
+}
+
 template <int NPAD, bool OBST>
 __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bufs b, RBufs r, RP rp) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -1085,9 +1187,15 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
         float cmds[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) cmds[k] = 0.5f * (clampf(a[k], -1.f, 1.f) + 1.f);
-#ifndef QS_DIAG_NOPHYS
-        for (int s = 0; s < kp.sim_steps; ++s) substep(kp, d, cmds, d.ou, rng, gid, s);
+#if defined(QS_DIAG_NOPHYS)
+        for (int i = 0; i < 3; ++i) d.pos[i] += 0.01f * d.vel[i] + 0.001f * cmds[i];
+#elif QS_DEAL_PHYS
+        if constexpr (Q > 1) physics_q<Q>(kp, d, cmds, q, rng, gid);
+        else for (int s = 0; s < kp.sim_steps; ++s) substep(kp, d, cmds, d.ou, rng, gid, s);
 #else
+        for (int s = 0; s < kp.sim_steps; ++s) substep(kp, d, cmds, d.ou, rng, gid, s);
+#endif
+#if 0
         for (int i = 0; i < 3; ++i) d.pos[i] += 0.01f * d.vel[i] + 0.001f * cmds[i];
 #endif
         // compute_reward_weighted (quadrotor_single.py:34-66)
