@@ -1004,7 +1004,7 @@ struct StepGeo {
 // Same expressions per element as substep(); the torque sums run in the pairwise order of qsum.
 // ---------------------------------------------------------------------------------------------
 #ifndef QS_DEAL_PHYS
-#define QS_DEAL_PHYS 1
+#define QS_DEAL_PHYS 0   // measured slower on MI355X (C3 7.95 -> 8.47 us): the DPP hops lengthen the chain
 #endif
 __device__ __forceinline__ float pick4(int k, float a0, float a1, float a2, float a3) {
     return k == 0 ? a0 : (k == 1 ? a1 : (k == 2 ? a2 : a3));
@@ -1463,14 +1463,21 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     // non-finite guard of the stepped drone and its reward (before a fused reset replaces the drone)
     const bool state_bad = lead && drone_nonfinite(d), rew_bad = lead && !(rw * 0.f == 0.f);
 
+#ifdef QS_DIAG_NODONE
+    const uint64_t dball = 0;
+#else
     const uint64_t dball = __ballot(active && done);
+#endif
     if (dball) {  // rare: some env of this block finished -> terminal obs + fused auto-reset (:739-838)
         lds_sync();
-        for (int r = 0; r < rows; ++r) {
-            const int e = env0 + r / kp.N;
-            if (b.env[QS_E_TICK * kp.E + e] + 1 <= kpm.ep_len) continue;
-            for (int c = lane; c < kp.obs_dim; c += 64)
-                b.term[(size_t)(env0 * kp.N + r) * kp.obs_dim + c] = lds[(size_t)r * kp.obs_dim + c];
+        // terminal obs: the finished envs' rows (contiguous in the tile and in HBM), all lanes of the wave;
+        // an env's done flag is its lead lane's bit of the ballot (no memory access)
+        const int nrow = kp.N * kp.obs_dim;
+        for (int e = 0; e < nenv_blk; ++e) {
+            if (!((dball >> (e * LPE)) & 1ull)) continue;
+            float* dst = b.term + (size_t)(env0 + e) * nrow;
+            const float* src = lds + (size_t)e * nrow;
+            for (int c = lane; c < nrow; c += 64) dst[c] = src[c];
         }
         lds_sync();
         float sv[3] = {d.vel[0], d.vel[1], d.vel[2]};  // QuadrotorEnvMulti.vel seen by the reset (:477)
@@ -1507,7 +1514,13 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
             if (SCEN)   // spawn point = goal (quadrotor_multi.py:469-470)
                 for (int k = 0; k < 3; ++k) spawn[k] = goal[k] = stab[4 * di + k];
             reset_drone(kp, d, rng, gid, spawn, goal);
-            if (q == 0) self_obs(kp, d, rng, gid, S_RESET_SENSOR, row);
+        }
+        if (kp.sense) {   // the reset obs' 3 sensor blocks dealt over the sub-lanes (all lanes: DPP)
+            float zr[12], uu[1];
+            qdraws<Q, 3, 0>(rng, gid, S_RESET_SENSOR, S_RESET_SENSOR, q, zr, uu);
+            if (active && done && q == 0) self_obs_z(kp, d, zr, rng, gid, S_RESET_SENSOR, row);
+        } else if (active && done && q == 0) {
+            self_obs(kp, d, rng, gid, S_RESET_SENSOR, row);
         }
         // the reset drones' state (the stepped state was stored before the obs phase)
 #if QS_COOP_STATE
