@@ -1314,7 +1314,15 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
 #endif
         // drone-drone impulses, pairs in (i, j) order; a wave-uniform loop over pending events.
         // Ballots read sub-lane 0 of each drone (bit lbase + i * Q).
+#if defined(QS_DIAG_NOPAIR)
+        uint64_t pend = 0ull;
+#elif defined(QS_DIAG_PAIRNEVER)   // the loop stays in the code, no event ever runs it
+        uint32_t zero_ = 0u;
+        asm volatile("" : "+v"(zero_));
+        uint64_t pend = active ? (newpairs & ~((2ull << di) - 1ull)) & (uint64_t)zero_ : 0ull;
+#else
         uint64_t pend = active ? (newpairs & ~((2ull << di) - 1ull)) : 0ull;
+#endif
         for (;;) {
             const uint64_t bal = __ballot(pend != 0ull && q == 0);
             if (bal == 0ull) break;
@@ -1380,7 +1388,11 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
             collide_obstacle(kp, og, d, myob[ohit].x, myob[ohit].y, z, u);
             vchanged = true;
         }
+#ifdef QS_DIAG_NOWALL
+        if (false) {
+#else
         if (active && (wall_new || ceil_new)) {
+#endif
             float u[12];
             if (wall_new) {
                 qdraws<Q, 0, 3>(rng, gid, S_WALL, S_WALL, q, nullptr, u);
