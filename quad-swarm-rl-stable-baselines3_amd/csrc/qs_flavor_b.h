@@ -920,15 +920,24 @@ __device__ __forceinline__ uint32_t drone_word_off(const KP& kp, const Bufs& b, 
 }
 
 template <int Q>
-__device__ __forceinline__ void load_drone_q(const KP& kp, const Bufs& b, int g, int q, Drone& d) {
-    constexpr int T = (DRONE_WORDS + Q - 1) / Q;
-    const uint32_t go = (uint32_t)g * 4u;
+struct DroneWords {
+    static constexpr int T = (DRONE_WORDS + Q - 1) / Q;
     uint32_t r[T];
+};
+// issue the sub-lane's state-word loads (no wait)
+template <int Q>
+__device__ __forceinline__ void load_words_q(const KP& kp, const Bufs& b, int g, int q, DroneWords<Q>& dw) {
+    const uint32_t go = (uint32_t)g * 4u;
 #pragma unroll
-    for (int t = 0; t < T; ++t) {
+    for (int t = 0; t < DroneWords<Q>::T; ++t) {
         const int w = t * Q + q;
-        r[t] = w < DRONE_WORDS ? *reinterpret_cast<const uint32_t*>((const char*)b.st + drone_word_off(kp, b, w, go)) : 0u;
+        dw.r[t] = w < DRONE_WORDS ? *reinterpret_cast<const uint32_t*>((const char*)b.st + drone_word_off(kp, b, w, go)) : 0u;
     }
+}
+template <int Q>
+__device__ __forceinline__ void unpack_words_q(const DroneWords<Q>& dw, Drone& d) {
+    constexpr int T = DroneWords<Q>::T;
+    const uint32_t (&r)[T] = dw.r;
     uint32_t wv[DRONE_WORDS];
     qbc_words<Q, 0, T>(r, wv);
 #pragma unroll
@@ -948,6 +957,12 @@ __device__ __forceinline__ void load_drone_q(const KP& kp, const Bufs& b, int g,
     d.svd = (int32_t)wv[IW + QS_I_SVD];
     d.flags = wv[IW + QS_I_FLAGS];
     d.prev = (uint64_t)wv[IW + QS_I_PREV_LO] | ((uint64_t)wv[IW + QS_I_PREV_HI] << 32);
+}
+template <int Q>
+__device__ __forceinline__ void load_drone_q(const KP& kp, const Bufs& b, int g, int q, Drone& d) {
+    DroneWords<Q> dw;
+    load_words_q<Q>(kp, b, g, q, dw);
+    unpack_words_q<Q>(dw, d);
 }
 
 template <int Q>
@@ -988,6 +1003,9 @@ __device__ __forceinline__ void store_drone_q(const KP& kp, const Bufs& b, int g
 // Sub-lanes per drone of the flavor-B step kernel (QS_QB; 64 / NPAD when an env would not fit a wave).
 #ifndef QS_QB
 #define QS_QB 4
+#endif
+#ifndef QS_LOADS_FIRST
+#define QS_LOADS_FIRST 1
 #endif
 template <int NPAD>
 struct StepGeo {
@@ -1129,24 +1147,29 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     if (OBST)   // the block's obstacle lists -> LDS (ordered by the first lds_sync below)
         for (int k = lane; k < nenv_blk * kp.M; k += 64) otile[k] = b.obst[(size_t)env0 * kp.M + k];
 
+    // Every global load of the step is issued up front, back to back -- the action, the env's counters, the
+    // drone's state words -- before anything waits: their HBM latencies overlap instead of adding up (the
+    // scheduler otherwise sank the action load behind the state's waits).
+    const float4 av = reinterpret_cast<const float4*>(b.act)[g];
+    const int eidx = active ? env : 0;
+    const int tick0 = b.env[QS_E_TICK * kp.E + eidx];
+    const int episode = b.env[QS_E_EPISODE * kp.E + eidx];
     Drone d;   // every sub-lane holds the whole drone
 #if defined(QS_DIAG_NOLOAD)   // diagnostic builds only (QS_JIT_OPTS): phase-removal timing experiments
     d = Drone{};
     d.pos[2] = 2.f; d.rot[0] = d.rot[4] = d.rot[8] = 1.f; d.goal[2] = 2.f;
     d.pos[0] = 0.01f * (float)(g % 97); d.pos[1] = 0.01f * (float)(g % 89);
 #elif QS_COOP_STATE
-    load_drone_q<Q>(kp, b, g, q, d);
+    DroneWords<Q> dw;
+    load_words_q<Q>(kp, b, g, q, dw);
+#if QS_LOADS_FIRST
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+    unpack_words_q<Q>(dw, d);
 #else
     load_drone(kp, b, g, d);
 #endif
-    float a[4];
-    {
-        const float4 av = reinterpret_cast<const float4*>(b.act)[g];
-        a[0] = av.x; a[1] = av.y; a[2] = av.z; a[3] = av.w;
-    }
-    const int eidx = active ? env : 0;
-    const int tick0 = b.env[QS_E_TICK * kp.E + eidx];
-    const int episode = b.env[QS_E_EPISODE * kp.E + eidx];
+    float a[4] = {av.x, av.y, av.z, av.w};
     const Rng rng = env_rng(seed, tick0, episode);
     const int tick = tick0 + 1;
     const bool done = tick > kpm.ep_len;
