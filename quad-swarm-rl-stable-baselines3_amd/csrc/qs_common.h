@@ -113,14 +113,15 @@ struct Bufs {
 };
 
 // Diagnostic phase stamps (build with -DQS_STAMPS=1 only; never in the shipped library): lane 0 of
-// each block records s_memtime at phase boundaries; tools/phase_stamps.py reads them back.
+// each block records s_memtime at phase boundaries; tools/phase_stamps.py reads them back.  A stamp waits
+// for nothing but its own counter read: a phase's time includes the memory waits its own code has.
 #ifdef QS_STAMPS
 __device__ uint64_t qs_dbg_stamps[65536 * 16];
 #define QS_STAMP(k)                                                                                   \
     do {                                                                                              \
         uint64_t t_;                                                                                  \
         __builtin_amdgcn_sched_barrier(0);                                                            \
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");               \
         __builtin_amdgcn_sched_barrier(0);                                                            \
         stamps_[k] = t_;                                                                              \
     } while (0)

@@ -16,9 +16,9 @@ import torch  # noqa: E402
 from quadswarm_amd import QuadSwarmConfig, _native as N  # noqa: E402
 from quadswarm_amd.env import QuadSwarmEnv  # noqa: E402
 
-NAMES = ["launch->loads issued", "state loads", "OU+physics+reward", "collisions+proximity", "forces/impulses",
-         "tile refresh", "self obs (sensor noise)", "neighbour obs", "done path+sync", "obs tile store",
-         "state stores", "counter atomic"]
+NAMES = ["launch->loads issued", "loads + draws", "OU+physics+reward", "collisions+proximity",
+         "impulses+scenario+state store", "tile refresh", "self obs (sensor noise)", "neighbour obs", "done path+sync",
+         "obs tile store", "env ints + guard", "replay tail"]
 
 
 def main():
@@ -33,7 +33,7 @@ def main():
     L = N.lib()
     L.qs_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
     npad = 1 << (cfg.num_agents - 1).bit_length()
-    epb = 64 // (npad * (2 if npad >= 32 else 4))      # flavor-B step geometry (qs::StepGeo)
+    epb = 64 // (npad * min(4, 64 // npad))          # flavor-B step geometry (qs::StepGeo, QS_QB = 4)
     nb = min((cfg.num_envs + epb - 1) // epb, 65536)
     buf = np.zeros(65536 * 16, np.uint64)
     assert L.qs_debug_stamps(buf.ctypes.data, buf.size) == 0
