@@ -1147,6 +1147,9 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     if (OBST)   // the block's obstacle lists -> LDS (ordered by the first lds_sync below)
         for (int k = lane; k < nenv_blk * kp.M; k += 64) otile[k] = b.obst[(size_t)env0 * kp.M + k];
 
+#ifdef QS_STAGGER   // experiment: odd workgroups start later (phases of co-resident waves overlap)
+    if (blockIdx.x & 1) __builtin_amdgcn_s_sleep(QS_STAGGER);
+#endif
     // Every global load of the step is issued up front, back to back -- the action, the env's counters, the
     // drone's state words -- before anything waits: their HBM latencies overlap instead of adding up (the
     // scheduler otherwise sank the action load behind the state's waits).
