@@ -244,8 +244,11 @@ __device__ __forceinline__ void st_wt4(__amdgpu_buffer_rsrc_t r, uint32_t voff, 
     __builtin_amdgcn_raw_buffer_store_b128(x, r, (int)voff, 0, QS_WT_OBS ? QS_AUX_SC1 : 0);
 }
 // 4-B store of word `v` at (uniform soff + per-lane voff) bytes from the descriptor's base
+#ifndef QS_STATE_AUX   // cache policy of the state stores: sc1 (write-through), or QS_STATE_AUX=2 (nt) / 0 (plain)
+#define QS_STATE_AUX (QS_WT_STATE ? QS_AUX_SC1 : 0)
+#endif
 __device__ __forceinline__ void st_wt1(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, uint32_t v) {
-    __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)voff, (int)soff, QS_WT_STATE ? QS_AUX_SC1 : 0);
+    __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)voff, (int)soff, QS_STATE_AUX);
 }
 // field f of a SoA array at (uniform base, lane byte offset): the field offset rides in soffset
 template <typename T>
