@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define QS_ABI_VERSION 6
+#define QS_ABI_VERSION 7
 #define QS_MAX_AGENTS 32            /* drones per env: one env lives inside one 64-lane wavefront */
 #define QS_MAX_DR_CHOICES 8         /* entries per obstacle domain-randomisation list */
 
@@ -155,6 +155,9 @@ typedef struct qs_config {
     int32_t dr_counts[QS_MAX_DR_CHOICES];
     int32_t dr_num_sizes;
     float dr_sizes[QS_MAX_DR_CHOICES];
+    /* ---- episode_extra_stats (flavor B; quadrotor_multi.py:153-216, 541-657, 739-831): 1 = the step kernels
+     * keep the reference's per-episode counters and write each finished env's rows to buffers.estats ---- */
+    int32_t episode_stats;
 } qs_config;
 
 /* Device buffers of a handle.  State is structure-of-arrays: field f of drone g lives at
@@ -167,13 +170,19 @@ enum qs_state_field {
      * x y z, attitude x y z, rate x y z; heading angle and last heading-rate command; the
      * QuadrotorEnvMulti.heading value a reset sees (stale, like stale_vel) */
     QS_F_PID = 33, QS_F_ANGLE = 53, QS_F_ANGVEL = 54, QS_F_HEADING = 55,
-    QS_NF = 56
+    /* episode_extra_stats (flavor B): distance_to_goal[i] as its last 5 entries (dt * |goal - pos|, ring by
+     * tick % 5) and its sums over the final 100 / 300 / 500 entries of the episode */
+    QS_F_DRING = 56, QS_F_DSUM = 61,
+    QS_NF = 64
 };
 enum qs_istate_field { QS_I_SVD = 0, QS_I_FLAGS = 1, QS_I_PREV_LO = 2, QS_I_PREV_HI = 3, QS_NI = 4 };
 enum qs_drone_flags {
     QS_FL_ON_FLOOR = 1, QS_FL_PREV_WALL = 2, QS_FL_PREV_CEIL = 4,
     QS_FL_CRASH_FLOOR = 8, QS_FL_CRASH_WALL = 16, QS_FL_CRASH_CEIL = 32,
-    QS_FL_PREV_OBST = 64            /* in prev_obst_quad_collisions (quadrotor_multi.py:585) */
+    QS_FL_PREV_OBST = 64,           /* in prev_obst_quad_collisions (quadrotor_multi.py:585) */
+    /* episode_extra_stats: in prev_crashed_room (:606); agent_col_agent / agent_col_obst cleared (:563, :589);
+     * reached_goal (:652-655) */
+    QS_FL_PREV_ROOM = 128, QS_FL_HIT_AGENT = 256, QS_FL_HIT_OBST = 512, QS_FL_REACHED = 1024
 };
 /* per env: tick, flags, episode.  {tick, episode} is the env's Philox counter: every step and reset
  * of an env draws a fresh stream.  Flavor A counts QuadrotorSingle ticks (8 per step). */
@@ -185,7 +194,24 @@ enum qs_env_field {
     QS_E_SC_MODE = 3, QS_E_SC_FORM = 4, QS_E_SC_PERIOD = 5, QS_E_SC_INC = 6,
     /* obstacle domain randomisation: the env's pillar count / size as 1 + its list entry, 0 = configured */
     QS_E_OBST_M = 7, QS_E_OBST_SZ = 8,
-    QS_NE = 9
+    /* episode_extra_stats counters of the running episode (quadrotor_multi.py:153-171): collisions_per_episode,
+     * collisions_room / floor / wall / ceiling_per_episode, collisions_after_settle, collisions_final_5s,
+     * obst_quad_collisions_per_episode, obst_quad_collisions_after_settle, distance_to_goal_3_5, _5 */
+    QS_E_ST_COL = 9, QS_E_ST_ROOM = 10, QS_E_ST_FLOOR = 11, QS_E_ST_WALL = 12, QS_E_ST_CEIL = 13,
+    QS_E_ST_COL_SETTLE = 14, QS_E_ST_COL_FINAL = 15, QS_E_ST_OCOL = 16, QS_E_ST_OCOL_SETTLE = 17,
+    QS_E_ST_O35 = 18, QS_E_ST_O5 = 19,
+    QS_NE = 20
+};
+/* columns of a buffers.estats row (one per drone of a finished env, written by the step that ends the episode):
+ * the env's counters, the agent rates, the scenario (QUADS_MODE_LIST index, 16 + mode for the obstacle
+ * scenarios), the drone's own distance_to_goal_1s / 3s / 5s and whether the episode was a replay
+ * (saved_in_replay_buffer).  quadswarm_amd.stats turns a row into the reference's dict. */
+enum qs_estat {
+    QS_ES_COL = 0, QS_ES_ROOM = 1, QS_ES_FLOOR = 2, QS_ES_WALL = 3, QS_ES_CEIL = 4, QS_ES_COL_SETTLE = 5,
+    QS_ES_COL_FINAL = 6, QS_ES_OCOL = 7, QS_ES_OCOL_SETTLE = 8, QS_ES_O35 = 9, QS_ES_O5 = 10,
+    QS_ES_SUCCESS = 11, QS_ES_DEADLOCK = 12, QS_ES_COLRATE = 13, QS_ES_NCOLRATE = 14, QS_ES_OCOLRATE = 15,
+    QS_ES_SCEN = 16, QS_ES_D1 = 17, QS_ES_D3 = 18, QS_ES_D5 = 19, QS_ES_REPLAY = 20,
+    QS_NES = 24
 };
 enum qs_env_flags {
     QS_EF_STALE = 1,                /* stale_vel / QS_F_HEADING hold QuadrotorEnvMulti.vel / .heading */
@@ -209,7 +235,8 @@ enum qs_env_ffield {
 
 typedef struct qs_layout {          /* byte offsets inside one workspace allocation */
     size_t params;                  /* kernel parameter block (device copy of the config + runtime params) */
-    size_t state, istate, env, env_f, obst, stale_vel, obs, term_obs, rew, done, reset_info, stats, total_bytes;
+    size_t state, istate, env, env_f, obst, stale_vel, obs, term_obs, rew, done, reset_info, stats, estats,
+        total_bytes;
     int32_t obs_dim, num_drones;
 } qs_layout;
 
@@ -227,6 +254,8 @@ typedef struct qs_buffers {         /* device pointers (valid for the handle's l
     uint8_t* done;                  /* [I] */
     uint8_t* reset_info;            /* [E] 0: no reset this call; 1: reset, {"success": False}; 2: True */
     uint64_t* stats;                /* [QS_NSTAT] non-finite guard counters (qs_counters)              */
+    float* estats;                  /* [I, QS_NES] episode_extra_stats rows of the envs that finished (config
+                                       episode_stats; rows of other envs keep their previous contents)   */
 } qs_buffers;
 
 /* Non-finite guard.  The reference raises ValueError on a NaN reward (gym_art/quadrotor_multi/

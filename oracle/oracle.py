@@ -84,6 +84,8 @@ class OrDrone(ctypes.Structure):
         ("prev_wall", I), ("prev_ceiling", I),
         ("goal", D * 3),
         ("pid", D * 20), ("angle", D), ("ang_vel", D), ("prev_obst", I),
+        ("hit_agent", I), ("hit_obst", I), ("reached", I), ("prev_room", I),
+        ("dring", D * 5), ("dsum", D * 3), ("ep_dist", D * 3),
     ]
 
 
@@ -92,7 +94,19 @@ class OrEnv(ctypes.Structure):
                 ("obs_pos", (D * 3) * 64), ("obs_vel", (D * 3) * 64),
                 ("heading", D * 64), ("target", D * 2), ("capture_radius", D), ("success", I), ("has_pos", I),
                 ("n_obst", I), ("obst", (D * 2) * 64), ("obst_mode", I), ("scen", OrScen),
-                ("last_col", I), ("last_floor0", I), ("obst_mi", I), ("obst_si", I)]
+                ("last_col", I), ("last_floor0", I), ("obst_mi", I), ("obst_si", I),
+                ("st_col", I), ("st_room", I), ("st_floor", I), ("st_wall", I), ("st_ceil", I), ("st_col_settle", I),
+                ("st_col_final", I), ("st_ocol", I), ("st_ocol_settle", I), ("st_o35", I), ("st_o5", I),
+                ("ep_done", I), ("ep_stats", D * 24)]
+
+
+# episode_extra_stats (flavor B, quadrotor_multi.py:739-831): env-level columns of or_env.ep_stats (the GPU's
+# estats columns QS_ES_*), and the reference's key names; scenario ids: QUADS_MODE_LIST order (scenarios/utils.py)
+# for the goal scenarios, 16 + mode for the obstacle scenarios
+ES_COL, ES_ROOM, ES_FLOOR, ES_WALL, ES_CEIL, ES_COL_SETTLE, ES_COL_FINAL = range(7)
+ES_OCOL, ES_OCOL_SETTLE, ES_O35, ES_O5 = 7, 8, 9, 10
+ES_SUCCESS, ES_DEADLOCK, ES_COLRATE, ES_NCOLRATE, ES_OCOLRATE, ES_SCEN, ES_D1, ES_D3, ES_D5, ES_REPLAY, NES = \
+    11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 24
 
 
 class OrRng(ctypes.Structure):

@@ -819,6 +819,93 @@ static void obstacle_reset(const or_params* p, or_env* ev, uint32_t gbase, or_rn
 /* ------------------------------------------------------------------------------------------ */
 /* QuadrotorSingle._reset (quadrotor_single.py:401-469), static_same_goal goals
  * (scenarios/base.py:255-272 with formation size 0), QuadrotorEnvMulti.reset (quadrotor_multi.py:440-517) */
+/* episode_extra_stats bookkeeping of one step (quadrotor_multi.py:555-566, 575-589, 599-606, 631-656).
+ * tick = envs[0].tick after the drones' _step; time_remain = QuadrotorSingle.time_remain of the step. */
+static void episode_stats_step(const or_params* p, or_env* ev, or_drone* dr, int N, const int* in_cur, const int* in_prev,
+                               const int* onew, const int* wall_new, const int* ceil_new, const double* dist_goal,
+                               const double* obs, int od, int time_remain) {
+    const double freq = 1.0 / p->control_dt;
+    const int settle = (double)ev->tick >= 1.5 * freq;               /* collisions_grace_period_steps */
+    /* collisions_curr_tick = len(last_step_unique_collisions) // 2 */
+    int uniq = 0;
+    for (int i = 0; i < N; ++i) uniq += in_cur[i] && !in_prev[i];
+    const int cnt = uniq / 2;
+    ev->st_col += cnt;
+    if (cnt > 0 && settle) {
+        ev->st_col_settle += cnt;
+        for (int i = 0; i < N; ++i) if (in_cur[i] && !in_prev[i]) dr[i].hit_agent = 1;
+    }
+    if (cnt > 0 && (double)time_remain <= 5.0 * freq) ev->st_col_final += cnt;
+    if (p->use_obstacles) {
+        int oc = 0;
+        for (int i = 0; i < N; ++i) oc += onew[i];
+        ev->st_ocol += oc;
+        if (oc > 0 && settle) {
+            ev->st_ocol_settle += oc;
+            for (int i = 0; i < N; ++i)
+                if (onew[i]) {
+                    const double* q = obs + (size_t)i * od;   /* the step's obs[qid][0:3] (noisy pos - goal) */
+                    const double rd = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2]);
+                    if (rd > 3.5) ev->st_o35 += 1;
+                    if (rd > 5.0) ev->st_o5 += 1;
+                    dr[i].hit_obst = 1;
+                }
+        }
+    }
+    /* room: floor list (crashed_floor), new wall / ceiling lists; room list = their union minus the previous
+     * step's room list (which it then becomes) */
+    int nf = 0, nw = 0, nc = 0, nr = 0;
+    for (int i = 0; i < N; ++i) {
+        const int any = dr[i].crashed_floor || wall_new[i] || ceil_new[i];
+        const int room = any && !dr[i].prev_room;
+        dr[i].prev_room = room;
+        nf += dr[i].crashed_floor != 0; nw += wall_new[i]; nc += ceil_new[i]; nr += room;
+    }
+    if (settle) { ev->st_room += nr; ev->st_floor += nf; ev->st_wall += nw; ev->st_ceil += nc; }
+    /* distance_to_goal[i].append(dt * dist); reached_goal (mean of the last 5 entries / dt < 0.5) */
+    const int T = p->ep_len + 1;                                    /* the entry count when the episode ends */
+    const int win[3] = {(int)(1.0 * freq), (int)(3.0 * freq), (int)(5.0 * freq)};
+    for (int i = 0; i < N; ++i) {
+        or_drone* d = &dr[i];
+        const double v = p->dt * dist_goal[i];
+        d->dring[ev->tick % 5] = v;
+        for (int k = 0; k < 3; ++k) if (ev->tick > T - win[k]) d->dsum[k] += v;
+        if (ev->tick >= 5 && !d->reached) {
+            double m = 0.0;
+            for (int j = 4; j >= 0; --j) m += d->dring[(ev->tick - j) % 5];   /* oldest first, like np.mean */
+            if (m / 5.0 / p->dt < 0.5) d->reached = 1;                      /* approch_goal_metric */
+        }
+    }
+}
+
+/* the stats of the episode that just finished (quadrotor_multi.py:739-831), before the in-env reset */
+static void episode_stats_done(const or_params* p, or_env* ev, or_drone* dr, int N) {
+    const double freq = 1.0 / p->control_dt;
+    const int T = p->ep_len + 1;
+    double* s = ev->ep_stats;
+    memset(s, 0, sizeof ev->ep_stats);
+    s[OR_ES_COL] = ev->st_col; s[OR_ES_ROOM] = ev->st_room; s[OR_ES_FLOOR] = ev->st_floor; s[OR_ES_WALL] = ev->st_wall;
+    s[OR_ES_CEIL] = ev->st_ceil; s[OR_ES_COL_SETTLE] = ev->st_col_settle; s[OR_ES_COL_FINAL] = ev->st_col_final;
+    s[OR_ES_OCOL] = ev->st_ocol; s[OR_ES_OCOL_SETTLE] = ev->st_ocol_settle; s[OR_ES_O35] = ev->st_o35;
+    s[OR_ES_O5] = ev->st_o5;
+    int n_ok = 0, n_succ = 0, n_dead = 0, n_ha = 0, n_ho = 0;
+    for (int i = 0; i < N; ++i) {
+        const int ok = !dr[i].hit_agent && !dr[i].hit_obst;   /* logical_and(agent_col_agent, agent_col_obst) */
+        n_ok += ok; n_succ += ok && dr[i].reached; n_dead += ok && !dr[i].reached;
+        n_ha += !dr[i].hit_agent; n_ho += !dr[i].hit_obst;
+    }
+    s[OR_ES_SUCCESS] = (double)n_succ / N;
+    s[OR_ES_DEADLOCK] = (double)n_dead / N;
+    s[OR_ES_COLRATE] = 1.0 - (double)n_ok / N;
+    s[OR_ES_NCOLRATE] = 1.0 - (double)n_ha / N;
+    s[OR_ES_OCOLRATE] = 1.0 - (double)n_ho / N;
+    s[OR_ES_SCEN] = p->use_obstacles ? 16 + ev->obst_mode : (p->scenario_b == OR_SC_NONE ? 0 : ev->scen.mode);
+    const int win[3] = {(int)(1.0 * freq), (int)(3.0 * freq), (int)(5.0 * freq)};
+    for (int i = 0; i < N; ++i)
+        for (int k = 0; k < 3; ++k) dr[i].ep_dist[k] = dr[i].dsum[k] / (double)(win[k] < T ? win[k] : T) / p->dt;
+    ev->ep_done += 1;
+}
+
 void or_env_reset(const or_params* p, or_drone* drones, or_env* envs, int e, or_rng* r, double* obs) {
     const int N = p->num_agents, od = or_obs_dim(p);
     or_env* ev = &envs[e];
@@ -869,6 +956,15 @@ void or_env_reset(const or_params* p, or_drone* drones, or_env* envs, int e, or_
     ev->tick = 0;
     ev->episode += 1;
     memset(ev->prev_pair_bits, 0, sizeof ev->prev_pair_bits);
+    /* QuadrotorEnvMulti.reset zeroes the episode statistics (quadrotor_multi.py:487-509) */
+    ev->st_col = ev->st_room = ev->st_floor = ev->st_wall = ev->st_ceil = ev->st_col_settle = ev->st_col_final = 0;
+    ev->st_ocol = ev->st_ocol_settle = ev->st_o35 = ev->st_o5 = 0;
+    for (int i = 0; i < N; ++i) {
+        or_drone* d = &drones[(size_t)e * N + i];
+        d->hit_agent = d->hit_obst = d->reached = d->prev_room = 0;
+        memset(d->dring, 0, sizeof d->dring);
+        memset(d->dsum, 0, sizeof d->dsum);
+    }
     neighbor_obs(p, ev, obs, od);   /* uses fresh obs_pos and the stale obs_vel (:477) */
     if (p->use_obstacles)           /* MultiObstacles.reset (obstacles/obstacles.py:15-26) */
         for (int i = 0; i < N; ++i) or_obst_sdf(p, ev, ev->obs_pos[i], obs + (size_t)i * od + od - 9);
@@ -887,6 +983,8 @@ void or_env_step(const or_params* p, or_drone* drones, or_env* envs, int e, cons
     double* o = obs + (size_t)e * N * od;
     double* rw = rew + (size_t)e * N;
     r->step = ((uint64_t)ev->episode << 32) | (uint32_t)ev->tick;   /* env Philox counter */
+    const int time_remain = p->ep_len - ev->tick;                  /* QuadrotorSingle.time_remain (:361) */
+    double dist_goal[64];
 
     for (int i = 0; i < N; ++i) {
         or_drone* d = &dr[i];
@@ -898,7 +996,8 @@ void or_env_step(const or_params* p, or_drone* drones, or_env* envs, int e, cons
         for (int s = 0; s < p->sim_steps; ++s) or_dyn_substep(p, d, cmds, d->ou, r, gid, s);
         /* reward (quadrotor_single.py:34-66) */
         double gp[3] = {d->goal[0] - d->pos[0], d->goal[1] - d->pos[1], d->goal[2] - d->pos[2]};
-        double cost_pos = p->rew_pos * norm3(gp);
+        dist_goal[i] = norm3(gp);
+        double cost_pos = p->rew_pos * dist_goal[i];
         double an = sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2] + a[3] * a[3]);
         double cost_effort = p->rew_effort * an;
         double cost_orient = p->rew_orient * (d->on_floor ? 1.0 : -d->rot[8]);
@@ -956,6 +1055,7 @@ void or_env_step(const or_params* p, or_drone* drones, or_env* envs, int e, cons
     }
     ev->last_col = any_nonzero;
     for (int i = 0; i < N; ++i) if (onew[i]) ev->last_col = 1;
+    episode_stats_step(p, ev, dr, N, in_cur, in_prev, onew, wall_new, ceil_new, dist_goal, o, od, time_remain);
     for (int i = 0; i < N; ++i) {
         double rc = (any_nonzero && in_cur[i] && !in_prev[i]) ? -1.0 : 0.0;
         rw[i] += p->rew_quadcol_bin * rc;
@@ -1006,6 +1106,7 @@ void or_env_step(const or_params* p, or_drone* drones, or_env* envs, int e, cons
         for (int i = 0; i < N; ++i) or_obst_sdf(p, ev, ev->obs_pos[i], o + (size_t)i * od + od - 9);
     for (int i = 0; i < N; ++i) done[(size_t)e * N + i] = (unsigned char)is_done;
     if (is_done) {
+        episode_stats_done(p, ev, dr, N);
         if (term_obs) memcpy(term_obs + (size_t)e * N * od, o, sizeof(double) * (size_t)N * od);
         ev->tick -= 1;                              /* the reset draws at the step's counter */
         or_env_reset(p, drones, envs, e, r, o);     /* in-env auto reset (:836) */

@@ -196,7 +196,20 @@ typedef struct {
     double pid[2 * OR_NPID];
     double angle, ang_vel;
     int prev_obst;             /* in prev_obst_quad_collisions (quadrotor_multi.py:585) */
+    /* episode_extra_stats (flavor B, quadrotor_multi.py:153-216, 541-657): agent_col_agent / agent_col_obst
+     * cleared (hit_* = 1), reached_goal, in prev_crashed_room; distance_to_goal[i] kept as its last 5
+     * entries (ring by tick % 5) and its sums over the final 100 / 300 / 500 entries of the episode */
+    int hit_agent, hit_obst, reached, prev_room;
+    double dring[5];
+    double dsum[3];
+    double ep_dist[3];         /* distance_to_goal_1s / _3s / _5s of the last finished episode */
 } or_drone;
+
+/* env-level episode_extra_stats values of a finished episode (quadrotor_multi.py:739-831), the GPU's
+ * qs estats columns (include/quadswarm.h QS_ES_*) */
+enum { OR_ES_COL = 0, OR_ES_ROOM, OR_ES_FLOOR, OR_ES_WALL, OR_ES_CEIL, OR_ES_COL_SETTLE, OR_ES_COL_FINAL,
+       OR_ES_OCOL, OR_ES_OCOL_SETTLE, OR_ES_O35, OR_ES_O5, OR_ES_SUCCESS, OR_ES_DEADLOCK, OR_ES_COLRATE,
+       OR_ES_NCOLRATE, OR_ES_OCOLRATE, OR_ES_SCEN, OR_ES_D1, OR_ES_D3, OR_ES_D5, OR_ES_REPLAY, OR_NES = 24 };
 
 typedef struct {
     int tick;
@@ -220,6 +233,13 @@ typedef struct {
     /* obstacle domain randomisation: the env's current (obst_density, obst_size) as table indices
      * (0 = the configured values) */
     int obst_mi, obst_si;
+    /* episode_extra_stats accumulators of the running episode (quadrotor_multi.py:153-171, 487-509):
+     * collisions_per_episode, _room_, _floor_, _wall_, _ceiling_, collisions_after_settle, collisions_final_5s,
+     * obst_quad_collisions_per_episode, _after_settle, distance_to_goal_3_5, distance_to_goal_5 */
+    int st_col, st_room, st_floor, st_wall, st_ceil, st_col_settle, st_col_final;
+    int st_ocol, st_ocol_settle, st_o35, st_o5;
+    int ep_done;                 /* episodes finished (ep_stats holds the last one's values) */
+    double ep_stats[OR_NES];
 } or_env;
 
 /* ---- low level pieces (exported for per-function golden tests) ---- */

@@ -53,6 +53,9 @@ struct KP {
     float dr_r[9], dr_thr[9];
     // ---- flavor-B goal scenarios: -1 = the fixed static_same_goal goal, 0..9 a scenario, 10 = mix ----
     int scen_b;
+    // ---- episode_extra_stats (flavor B): on; collisions_grace_period_steps (ticks >= settle count), the
+    // final-5-s window (time_remain <= final), distance windows of 1 / 3 / 5 s in ticks ----
+    int stats, st_settle, st_final, st_win[3];
 };
 
 // The fields qs_set_param may change after creation, read once per launch into registers (uniform):
@@ -110,6 +113,7 @@ struct Bufs {
     const float* act;
     const uint8_t* mask;
     unsigned long long* stats;   // [QS_NSTAT] non-finite guard counters (qs_counters)
+    float* estats;               // [I, QS_NES] episode_extra_stats rows of finished envs
 };
 
 // Diagnostic phase stamps (build with -DQS_STAMPS=1 only; never in the shipped library): lane 0 of

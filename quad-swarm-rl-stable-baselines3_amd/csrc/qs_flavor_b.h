@@ -1176,6 +1176,24 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     const Rng rng = env_rng(seed, tick0, episode);
     const int tick = tick0 + 1;
     const bool done = tick > kpm.ep_len;
+    // episode_extra_stats (kp.stats): distance_to_goal's last entries and window sums of this drone, loaded
+    // now (consumed after the physics) by its lead sub-lane while the ring is still needed / in the window
+    float dring[5] = {0.f, 0.f, 0.f, 0.f, 0.f}, dsum[3] = {0.f, 0.f, 0.f};
+    bool in_win[3] = {false, false, false};
+    if (kp.stats) {
+        const int T = kpm.ep_len + 1;   // the entry count when the episode ends
+#pragma unroll
+        for (int k = 0; k < 3; ++k) in_win[k] = tick > T - kp.st_win[k];
+        if (lead && !(d.flags & QS_FL_REACHED) && tick >= 5) {
+#pragma unroll
+            for (int k = 0; k < 5; ++k) dring[k] = b.st[(QS_F_DRING + k) * kp.I + g];
+        }
+        if (lead) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+                if (in_win[k]) dsum[k] = b.st[(QS_F_DSUM + k) * kp.I + g];
+        }
+    }
     int omi = 0, osi = 0;   // the env's domain-randomisation choice (QS_E_OBST_M / _SZ)
     if (OBST && kp.dr) { omi = b.env[QS_E_OBST_M * kp.E + eidx]; osi = b.env[QS_E_OBST_SZ * kp.E + eidx]; }
     OGeo og = ogeo(kp, omi, osi);
@@ -1228,7 +1246,28 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
         const float gx = d.goal[0] - d.pos[0], gy = d.goal[1] - d.pos[1], gz = d.goal[2] - d.pos[2];
         const bool on_floor = d.flags & QS_FL_ON_FLOOR;
         floor_now = on_floor;
-        const float cost = kpm.rew_pos * fsqrt(gx * gx + gy * gy + gz * gz) +
+        const float dist = fsqrt(gx * gx + gy * gy + gz * gz);
+        if (kp.stats && lead) {   // distance_to_goal[i].append(-rewraw_pos) and reached_goal (:651-655)
+            const float v = kp.dt * dist;
+            const int slot = tick % 5;
+            b.st[(QS_F_DRING + slot) * kp.I + g] = v;
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+                if (in_win[k]) {
+                    dsum[k] += v;
+                    b.st[(QS_F_DSUM + k) * kp.I + g] = dsum[k];
+                }
+            if (!(d.flags & QS_FL_REACHED) && tick >= 5) {
+                float m = 0.f;
+#pragma unroll
+                for (int j = 4; j >= 0; --j) {   // the last 5 entries, oldest first
+                    const int sl = (tick - j) % 5;
+                    m += sl == slot ? v : (sl == 0 ? dring[0] : sl == 1 ? dring[1] : sl == 2 ? dring[2] : sl == 3 ? dring[3] : dring[4]);
+                }
+                if (m / 5.f / kp.dt < 0.5f) d.flags |= QS_FL_REACHED;   // approch_goal_metric
+            }
+        }
+        const float cost = kpm.rew_pos * dist +
                            kpm.rew_effort * fsqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2] + a[3] * a[3]) +
                            kpm.rew_crash * (on_floor ? 1.f : 0.f) + kpm.rew_orient * (on_floor ? 1.f : -d.rot[8]) +
                            kpm.rew_spin * fsqrt(d.om[0] * d.om[0] + d.om[1] * d.om[1] + d.om[2] * d.om[2]);
@@ -1292,6 +1331,59 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     }
     bool any_onew = false;   // curr_quad_col non-empty (quadrotor_multi.py:576)
     if (OBST) any_onew = ((__ballot(onew && q == 0) >> lbase) & lmask) != 0;
+    if (kp.stats) {   // episode_extra_stats counters (quadrotor_multi.py:555-566, 575-589, 599-606, 631-635)
+        auto env_count = [&](bool x) { return __popcll((__ballot(x && q == 0) >> lbase) & lmask); };
+        const bool settle = tick >= kp.st_settle;
+        const int col = env_count(uniq) / 2;   // len(last_step_unique_collisions) // 2
+        if (col > 0 && settle && uniq) d.flags |= QS_FL_HIT_AGENT;
+        const bool cfloor = active && (d.flags & QS_FL_CRASH_FLOOR);
+        const bool room_new = active && (cfloor || wall_new || ceil_new) && !(d.flags & QS_FL_PREV_ROOM);
+        d.flags = (d.flags & ~(uint32_t)QS_FL_PREV_ROOM) | (room_new ? (uint32_t)QS_FL_PREV_ROOM : 0u);
+        const int nfl = env_count(cfloor), nw = env_count(active && wall_new), nc = env_count(active && ceil_new);
+        const int nr = env_count(room_new);
+        int oc = 0, o35 = 0, o5 = 0;
+        if (OBST) {
+            oc = env_count(onew);
+            bool f35 = false, f5 = false;
+            if (oc > 0 && settle && onew) {
+                d.flags |= QS_FL_HIT_OBST;
+                // the step's obs[qid][0:3]: the sensed position minus the goal (self obs before the forces)
+                float rr = 0.f;
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    const float x = d.pos[c] + (kp.sense ? kp.pos_std * zs[c] : 0.f) - d.goal[c];
+                    rr += x * x;
+                }
+                const float rd = fsqrt(rr);
+                f35 = rd > 3.5f;
+                f5 = rd > 5.f;
+            }
+            o35 = env_count(f35);
+            o5 = env_count(f5);
+        }
+        const bool fin5 = kpm.ep_len - tick0 <= kp.st_final;   // time_remain <= collisions_final_grace_period_steps
+        if (active && di == 0 && q == 0 && (col | nr | nfl | nw | nc | oc) != 0) {   // the env's lead lane
+            int32_t* ev = b.env + env;
+            const int E = kp.E;
+            ev[QS_E_ST_COL * E] += col;
+            if (col > 0 && settle) ev[QS_E_ST_COL_SETTLE * E] += col;
+            if (col > 0 && fin5) ev[QS_E_ST_COL_FINAL * E] += col;
+            if (settle) {
+                ev[QS_E_ST_ROOM * E] += nr;
+                ev[QS_E_ST_FLOOR * E] += nfl;
+                ev[QS_E_ST_WALL * E] += nw;
+                ev[QS_E_ST_CEIL * E] += nc;
+            }
+            if (OBST) {
+                ev[QS_E_ST_OCOL * E] += oc;
+                if (oc > 0 && settle) {
+                    ev[QS_E_ST_OCOL_SETTLE * E] += oc;
+                    ev[QS_E_ST_O35 * E] += o35;
+                    ev[QS_E_ST_O5 * E] += o5;
+                }
+            }
+        }
+    }
 
     QS_STAMP(3);
     // ---- random forces (:659-698), replicated on the sub-lanes ----
@@ -1518,6 +1610,45 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
             for (int c = lane; c < nrow; c += 64) dst[c] = src[c];
         }
         lds_sync();
+        if (kp.stats) {   // the finished episode's episode_extra_stats rows (quadrotor_multi.py:739-831)
+            // the env's counters were just updated by its lead lane: a workgroup-scope release / acquire (one
+            // wave per workgroup) before the other lanes read them back
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            auto env_bits = [&](bool x) { return (__ballot(x && q == 0) >> lbase) & lmask; };
+            const uint64_t hit_a = env_bits(active && (d.flags & QS_FL_HIT_AGENT));
+            const uint64_t hit_o = env_bits(active && (d.flags & QS_FL_HIT_OBST));
+            const uint64_t reach = env_bits(active && (d.flags & QS_FL_REACHED));
+            const uint64_t all = env_bits(active);
+            if (active && done && q == 0) {
+                const float n = (float)kp.N;
+                const uint64_t ok = all & ~hit_a & ~hit_o;   // logical_and(agent_col_agent, agent_col_obst)
+                float* row = b.estats + (size_t)g * QS_NES;
+                const int32_t* ev = b.env + env;
+                const int E = kp.E;
+                for (int k = 0; k < 11; ++k) row[QS_ES_COL + k] = (float)ev[(QS_E_ST_COL + k) * E];
+                row[QS_ES_SUCCESS] = (float)__popcll(ok & reach) / n;
+                row[QS_ES_DEADLOCK] = (float)__popcll(ok & ~reach) / n;
+                row[QS_ES_COLRATE] = 1.f - (float)__popcll(ok) / n;
+                row[QS_ES_NCOLRATE] = 1.f - (float)__popcll(all & ~hit_a) / n;
+                row[QS_ES_OCOLRATE] = 1.f - (float)__popcll(all & ~hit_o) / n;
+                row[QS_ES_SCEN] = (OBST || SCEN) ? (float)b.env[QS_E_SC_MODE * E + env] : 0.f;
+                const int T = kpm.ep_len + 1;
+#pragma unroll
+                for (int k = 0; k < 3; ++k) row[QS_ES_D1 + k] = dsum[k] / (float)min(kp.st_win[k], T) / kp.dt;
+                row[QS_ES_REPLAY] = (r.ri != nullptr && r.ri[QS_R_SAVED * E + env]) ? 1.f : 0.f;
+                // QuadrotorEnvMulti.reset zeroes the statistics (:487-509): the drone's entries here, the env's
+                // counters by its lead lane
+#pragma unroll
+                for (int k = 0; k < 5; ++k) b.st[(QS_F_DRING + k) * kp.I + g] = 0.f;
+#pragma unroll
+                for (int k = 0; k < 3; ++k) b.st[(QS_F_DSUM + k) * kp.I + g] = 0.f;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            if (active && done && di == 0 && q == 0)
+                for (int k = 0; k < 11; ++k) b.env[(QS_E_ST_COL + k) * kp.E + env] = 0;
+        }
         float sv[3] = {d.vel[0], d.vel[1], d.vel[2]};  // QuadrotorEnvMulti.vel seen by the reset (:477)
         if (OBST) {   // new obstacle map + scenario per finished env (one lane each)
             if (active && done && di == 0 && q == 0) {
@@ -1528,6 +1659,7 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
                     b.env[QS_E_OBST_M * kp.E + env] = oscr[el].mi;
                     b.env[QS_E_OBST_SZ * kp.E + env] = oscr[el].si;
                 }
+                if (kp.stats) b.env[QS_E_SC_MODE * kp.E + env] = 16 + oscr[el].mode;   // the stats' scenario name
             }
             lds_sync();
             if (active && done && kp.dr) og = ogeo(kp, oscr[el].mi, oscr[el].si);
@@ -1651,6 +1783,7 @@ __global__ __launch_bounds__(64) void reset_kernel(const KP* __restrict__ kpp, B
                 b.env[QS_E_OBST_M * kp.E + env] = oscr[el].mi;
                 b.env[QS_E_OBST_SZ * kp.E + env] = oscr[el].si;
             }
+            if (kp.stats) b.env[QS_E_SC_MODE * kp.E + env] = 16 + oscr[el].mode;
         }
         lds_sync();
     }
@@ -1698,10 +1831,18 @@ __global__ __launch_bounds__(64) void reset_kernel(const KP* __restrict__ kpp, B
 #pragma unroll
         for (int c = 0; c < 3; ++c) b.stale[c * kp.I + g] = sv[c];
         b.done[g] = 0;
+        if (kp.stats) {   // QuadrotorEnvMulti.reset zeroes the episode statistics (quadrotor_multi.py:487-509)
+#pragma unroll
+            for (int k = 0; k < 5; ++k) b.st[(QS_F_DRING + k) * kp.I + g] = 0.f;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) b.st[(QS_F_DSUM + k) * kp.I + g] = 0.f;
+        }
         if (di == 0) {
             b.env[QS_E_TICK * kp.E + env] = 0;
             b.env[QS_E_EPISODE * kp.E + env] = episode + 1;
             b.env[QS_E_FLAGS * kp.E + env] |= 1;
+            if (kp.stats)
+                for (int k = 0; k < 11; ++k) b.env[(QS_E_ST_COL + k) * kp.E + env] = 0;
         }
     }
 }

@@ -206,6 +206,7 @@ static qs_layout make_layout(const qs_config* c) {
     L.done = o; o = al(o + I);
     L.reset_info = o; o = al(o + E);
     L.stats = o; o = al(o + sizeof(uint64_t) * QS_NSTAT);
+    L.estats = o; o = al(o + sizeof(float) * QS_NES * (c->episode_stats ? I : 0));
     L.total_bytes = o;
     L.obs_dim = od;
     L.num_drones = (int32_t)I;
@@ -344,6 +345,14 @@ static qs::KP make_kp(const qs_config* c, const qs_layout& L) {
     if (c->flavor == QS_FLAVOR_B && !c->use_obstacles && c->scenario >= QS_SCEN_MIX)
         k.scen_b = c->scenario == QS_SCEN_MIX ? 10 : c->scenario - QS_SCEN_MIX;
     if (c->flavor == QS_FLAVOR_A) make_kp_a(c, k);
+    if (c->episode_stats && c->flavor == QS_FLAVOR_B) {   // quadrotor_multi.py:156-161, 651-655, 761-774
+        double freq = 1.0 / (double)c->control_dt;   // control_freq (100 for the reference's 0.01 s)
+        if (fabs(freq - (double)llround(freq)) < 1e-4) freq = (double)llround(freq);
+        k.stats = 1;
+        k.st_settle = (int)ceil(1.5 * freq - 1e-9);    // tick >= collisions_grace_period_steps
+        k.st_final = (int)floor(5.0 * freq + 1e-9);    // time_remain <= collisions_final_grace_period_steps
+        k.st_win[0] = (int)(1.0 * freq + 1e-9); k.st_win[1] = (int)(3.0 * freq + 1e-9); k.st_win[2] = (int)(5.0 * freq + 1e-9);
+    }
     if (c->use_obstacles) {
         k.obst = 1; k.M = obst_slots(c); k.obst_n = c->obst_area;
         k.obst_scen = c->scenario == QS_SCEN_OBST_MIX ? 0 : (c->scenario == QS_SCEN_O_RANDOM ? 1 : 2);
@@ -566,6 +575,7 @@ static qs::Bufs bufs_of(qs_handle* h) {
     b.act = nullptr;
     b.mask = nullptr;
     b.stats = (unsigned long long*)(w + h->lay.stats);
+    b.estats = (float*)(w + h->lay.estats);
     return b;
 }
 
@@ -575,6 +585,7 @@ extern "C" int qs_buffers_get(qs_handle* h, qs_buffers* o) {
     o->state = b.st; o->istate = b.ist; o->env = b.env; o->env_f = b.envf; o->obst = (float*)b.obst; o->stale_vel = b.stale;
     o->obs = b.obs; o->term_obs = b.term; o->rew = b.rew; o->done = b.done; o->reset_info = b.rinfo;
     o->stats = (uint64_t*)b.stats;
+    o->estats = h->cfg.episode_stats ? b.estats : nullptr;
     return QS_OK;
 }
 

@@ -9,7 +9,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("QUADSWARM_LIB", os.path.join(HERE, "lib", "libquadswarm.so"))
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 MAX_AGENTS = 32
 MAX_DR_CHOICES = 8
 F, I32, U32, U64, SZ = ctypes.c_float, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_size_t
@@ -32,13 +32,16 @@ SCENARIO_B = {"static_same_goal": 0, "mix": 5, "static_diff_goal": 6, "ep_lissaj
               "dynamic_same_goal": 9, "dynamic_diff_goal": 10, "dynamic_formations": 11, "swap_goals": 12,
               "swarm_vs_swarm": 13, "run_away": 14}
 F_POS, F_VEL, F_ROT, F_OMEGA, F_ROT_DAMP, F_CMD_DAMP, F_OU, F_GOAL = 0, 3, 6, 15, 18, 22, 26, 30
-F_PID, F_ANGLE, F_ANGVEL, F_HEADING, NF = 33, 53, 54, 55, 56
+F_PID, F_ANGLE, F_ANGVEL, F_HEADING = 33, 53, 54, 55
+F_DRING, F_DSUM, NF = 56, 61, 64
 I_SVD, I_FLAGS, I_PREV_LO, I_PREV_HI, NI = 0, 1, 2, 3, 4
 FL_ON_FLOOR, FL_PREV_WALL, FL_PREV_CEIL, FL_CRASH_FLOOR, FL_CRASH_WALL, FL_CRASH_CEIL = 1, 2, 4, 8, 16, 32
 FL_PREV_OBST = 64
+FL_PREV_ROOM, FL_HIT_AGENT, FL_HIT_OBST, FL_REACHED = 128, 256, 512, 1024
 E_TICK, E_FLAGS, E_EPISODE = 0, 1, 2
 E_SC_MODE, E_SC_FORM, E_SC_PERIOD, E_SC_INC = 3, 4, 5, 6
-E_OBST_M, E_OBST_SZ, NE = 7, 8, 9
+E_OBST_M, E_OBST_SZ = 7, 8
+E_ST_COL, NE_ST, NE = 9, 11, 20     # episode_extra_stats counters QS_E_ST_COL .. QS_E_ST_O5
 EF_STALE, EF_SUCCESS, EF_HAS_POS, EF_NEWCOL, EF_FLOOR0 = 1, 2, 4, 8, 16
 ENVF_TARGET_X, ENVF_TARGET_Y, ENVF_CAPTURE = 0, 1, 2
 ENVF_SC_SIZE, ENVF_SC_LO, ENVF_SC_HI, ENVF_SC_LAYER, ENVF_SC_SPEED = 3, 4, 5, 6, 7
@@ -69,20 +72,22 @@ class QsConfig(ctypes.Structure):
         ("rew_quadcol_bin_obst", F),
         ("dr_num_counts", I32), ("dr_counts", I32 * MAX_DR_CHOICES), ("dr_num_sizes", I32),
         ("dr_sizes", F * MAX_DR_CHOICES),
+        ("episode_stats", I32),
     ]
 
 
 class QsLayout(ctypes.Structure):
     _fields_ = [("params", SZ), ("state", SZ), ("istate", SZ), ("env", SZ), ("env_f", SZ), ("obst", SZ), ("stale_vel", SZ),
                 ("obs", SZ),
-                ("term_obs", SZ), ("rew", SZ), ("done", SZ), ("reset_info", SZ), ("stats", SZ), ("total_bytes", SZ),
+                ("term_obs", SZ), ("rew", SZ), ("done", SZ), ("reset_info", SZ), ("stats", SZ), ("estats", SZ),
+                ("total_bytes", SZ),
                 ("obs_dim", I32),
                 ("num_drones", I32)]
 
 
 class QsBuffers(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in ("state", "istate", "env", "env_f", "obst", "stale_vel", "obs", "term_obs",
-                                               "rew", "done", "reset_info", "stats")]
+                                               "rew", "done", "reset_info", "stats", "estats")]
 
 
 # non-finite guard counters (qs_stat / qs_stats)

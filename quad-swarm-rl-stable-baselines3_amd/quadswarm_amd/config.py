@@ -70,6 +70,9 @@ class QuadSwarmConfig:
     obst_size_random: bool = False
     obst_size_min: float = 0.3
     obst_size_max: float = 0.6
+    # ---- episode_extra_stats (flavor B, quadrotor_multi.py:739-831): the reference always keeps them; the
+    # step kernels do so when on (infos of finished envs, GpuQuadVecEnv) ----
+    episode_stats: bool = True
 
     @classmethod
     def c4(cls, num_envs=4096, num_agents=8, **over):
@@ -329,4 +332,5 @@ class QuadSwarmConfig:
                 c.dr_num_sizes = len(sizes)
                 for i, v in enumerate(sizes):
                     c.dr_sizes[i] = float(v)
+        c.episode_stats = 1 if (self.episode_stats and self.flavor == "B") else 0
         return c

@@ -67,6 +67,9 @@ class QuadSwarmEnv:
         self.rew = view(lay.rew, 4 * I, torch.float32, (I,))
         self.done = view(lay.done, I, torch.uint8, (I,))
         self.stats = view(lay.stats, 8 * N.NSTAT, torch.int64, (N.NSTAT,))
+        from .stats import NES
+        # episode_extra_stats rows [I, QS_NES] (written for the drones of envs that finished in a step)
+        self.estats = view(lay.estats, 4 * NES * I, torch.float32, (I, NES)) if self.qcfg.episode_stats else None
         self.act_dim = cfg.act_dim
         self._align = 8 if cfg.flavor == "A" else 16
         self._torch = torch

@@ -57,14 +57,16 @@ _EMPTY = types.MappingProxyType({})
 
 class StepInfos(Sequence):
     """infos of one step, len == num_envs (agent rows).  Rows of finished envs get a fresh dict with
-    terminal_observation; every other row is a shared read-only empty mapping, so a 32k-agent step
-    does not build 32k dicts."""
+    terminal_observation (and episode_extra_stats, quadrotor_multi.py:739-831, when the env keeps them); every
+    other row is a shared read-only empty mapping, so a 32k-agent step does not build 32k dicts."""
 
-    def __init__(self, n, done_rows=(), term=None):
+    def __init__(self, n, done_rows=(), term=None, extra=None):
         self._n = n
         self._d = {}
-        for r in done_rows:
+        for k, r in enumerate(done_rows):
             self._d[int(r)] = {"terminal_observation": term[int(r)], "TimeLimit.truncated": False}
+            if extra is not None:
+                self._d[int(r)]["episode_extra_stats"] = extra[k]
 
     def __len__(self):
         return self._n
@@ -80,7 +82,10 @@ class StepInfos(Sequence):
 
 
 class GpuQuadVecEnv:
-    def __init__(self, cfg: QuadSwarmConfig = None, as_torch=False, device=None, **cfg_over):
+    """raise_on_nan: like QuadrotorSingle's reward check (quadrotor_single.py:87-90), raise ValueError when a
+    step produced a non-finite reward (the kernels' qs_counters guard, read with the step's done rows)."""
+
+    def __init__(self, cfg: QuadSwarmConfig = None, as_torch=False, device=None, raise_on_nan=True, **cfg_over):
         cfg = cfg or QuadSwarmConfig()
         for k, v in cfg_over.items():
             setattr(cfg, k, v)
@@ -99,6 +104,8 @@ class GpuQuadVecEnv:
         self.reset_infos = tuple(None for _ in range(cfg.num_envs))
         self._actions = None
         self.render_mode = None
+        self.raise_on_nan = raise_on_nan
+        self._nan_seen = 0
 
     # ---- VecEnv API ----
     def reset(self):
@@ -121,12 +128,60 @@ class GpuQuadVecEnv:
         self.waiting = False
         self.batch += 1
         d = done.bool()
-        rows = torch.nonzero(d).flatten().cpu().numpy()   # one small D2H sync (like the pipes' recv)
+        # one small D2H sync (like the pipes' recv): the finished rows and the non-finite reward counter
+        h = torch.cat([torch.nonzero(d).flatten(), self.env.stats[N.ST_REW:N.ST_REW + 1]]).cpu().numpy()
+        rows, nan_rew = h[:-1], int(h[-1])
+        if self.raise_on_nan and nan_rew > self._nan_seen:
+            self._nan_seen = nan_rew
+            raise ValueError("QuadEnv: reward is Nan")
         self._set_reset_infos(rows)
+        extra = self._episode_extra_stats(rows) if len(rows) else None
         if self.as_torch:
-            return obs, rew, d, StepInfos(self.num_envs, rows, term)
+            return obs, rew, d, StepInfos(self.num_envs, rows, term, extra)
         term_np = term.cpu().numpy() if len(rows) else None
-        return obs.cpu().numpy(), rew.cpu().numpy(), d.cpu().numpy(), StepInfos(self.num_envs, rows, term_np)
+        return obs.cpu().numpy(), rew.cpu().numpy(), d.cpu().numpy(), StepInfos(self.num_envs, rows, term_np, extra)
+
+    def _episode_extra_stats(self, rows):
+        """infos[i]["episode_extra_stats"] of the finished rows: the env's counters (quadrotor_multi.py:739-831)
+        and, with experience replay on, the wrapper's "replay/*" values (quad_experience_replay.py:124-137)."""
+        from .stats import episode_extra_stats
+        out = [{} for _ in rows]
+        if self.env.estats is not None:
+            est = self.env.estats[torch.as_tensor(rows, device=self.env.device, dtype=torch.long)].cpu().numpy()
+            for k in range(len(rows)):
+                out[k] = episode_extra_stats(est[k], use_obstacles=self.cfg.use_obstacles)
+        if self.env.replay is not None:
+            rs = self.env.replay_stats()
+            envs = np.asarray(rows) // self.agents_per_env
+            nrep = self.env.replay["nrep"].cpu().numpy()
+            perm = self.env.replay["perm"].cpu().numpy()
+            es = self.env.env_state.cpu().numpy()
+            c = self.cfg
+            dens, sizes = [c.obst_density], [c.obst_size]     # table index 0 = the configured values
+            if c.use_obstacles and c.domain_random_active:
+                d, _, z = c.domain_random_tables()
+                dens, sizes = dens + [float(x) for x in d], sizes + [float(x) for x in z]
+            ri = self.env.replay["ri"].cpu().numpy()
+            for k, e in enumerate(envs):
+                n = int(rs["replay/replay_buffer_size"][e])
+                if c.use_obstacles:      # the density / size the env's new episode runs with (:113-116, :186-211)
+                    od, osz = dens[int(es[N.E_OBST_M, e])], sizes[int(es[N.E_OBST_SZ, e])]
+                else:                    # curr_obst_density drops to 0.0 at the env's first replay (:187-190)
+                    od, osz = (0.0 if ri[N.R_REPLAYED, e] > 0 else c.obst_density), c.obst_size
+                out[k].update({"replay/replay_rate": float(rs["replay/replay_rate"][e]),
+                               "replay/new_episode_rate": float(rs["replay/new_episode_rate"][e]),
+                               "replay/replay_buffer_size": n,
+                               "replay/avg_replayed": float(np.mean(nrep[perm[:n, e], e])) if n else 0,
+                               "replay/obst_density": od, "replay/obst_size": osz})
+        return out
+
+    def counters(self):
+        """The step kernels' non-finite guard counters (qs_counters) since creation or reset_counters()."""
+        return self.env.counters()
+
+    def reset_counters(self):
+        self.env.reset_counters()
+        self._nan_seen = 0
 
     def step(self, actions):
         self.step_async(actions)

@@ -110,6 +110,11 @@ def scen_oracle_to_gpu(oenv, env):
     env.env_f.copy_(torch.from_numpy(ef))
 
 
+# the oracle's episode_extra_stats counters in QS_E_ST_* order
+STAT_ENV_FIELDS = ["st_col", "st_room", "st_floor", "st_wall", "st_ceil", "st_col_settle", "st_col_final", "st_ocol",
+                   "st_ocol_settle", "st_o35", "st_o5"]
+
+
 def gpu_to_oracle(env, oenv):
     """Copy the GPU env state (fp32 SoA) into the oracle's drones/envs (fp64)."""
     st = env.state.double().cpu().numpy()
@@ -128,11 +133,21 @@ def gpu_to_oracle(env, oenv):
         d.prev_wall = int(bool(fl & NAT.FL_PREV_WALL))
         d.prev_ceiling = int(bool(fl & NAT.FL_PREV_CEIL))
         d.prev_obst = int(bool(fl & NAT.FL_PREV_OBST))
+        d.prev_room = int(bool(fl & NAT.FL_PREV_ROOM))        # episode_extra_stats state
+        d.hit_agent = int(bool(fl & NAT.FL_HIT_AGENT))
+        d.hit_obst = int(bool(fl & NAT.FL_HIT_OBST))
+        d.reached = int(bool(fl & NAT.FL_REACHED))
+        for k in range(5):
+            d.dring[k] = st[NAT.F_DRING + k, g]
+        for k in range(3):
+            d.dsum[k] = st[NAT.F_DSUM + k, g]
     ob = env.obstacles.double().cpu().numpy() if env.obstacles is not None else None
     for e in range(E):
         ev = oenv.envs[e]
         ev.tick = int(es[NAT.E_TICK, e])
         ev.episode = int(es[NAT.E_EPISODE, e])
+        for k, name in enumerate(STAT_ENV_FIELDS):
+            setattr(ev, name, int(es[NAT.E_ST_COL + k, e]))
         if ob is not None:
             ev.obst_mi, ev.obst_si = int(es[NAT.E_OBST_M, e]), int(es[NAT.E_OBST_SZ, e])
             ev.n_obst = oenv.p.dr_counts[ev.obst_mi] if ev.obst_mi > 0 else oenv.p.num_obstacles
@@ -171,13 +186,19 @@ def oracle_to_gpu(oenv, env):
         st[30:33, g] = d.goal[:]
         ist[NAT.I_SVD, g] = int(round(d.since_last_svd / dt))
         ist[NAT.I_FLAGS, g] = (NAT.FL_ON_FLOOR if d.on_floor else 0) | (NAT.FL_PREV_WALL if d.prev_wall else 0) | \
-            (NAT.FL_PREV_CEIL if d.prev_ceiling else 0) | (NAT.FL_PREV_OBST if d.prev_obst else 0)
+            (NAT.FL_PREV_CEIL if d.prev_ceiling else 0) | (NAT.FL_PREV_OBST if d.prev_obst else 0) | \
+            (NAT.FL_PREV_ROOM if d.prev_room else 0) | (NAT.FL_HIT_AGENT if d.hit_agent else 0) | \
+            (NAT.FL_HIT_OBST if d.hit_obst else 0) | (NAT.FL_REACHED if d.reached else 0)
+        st[NAT.F_DRING:NAT.F_DRING + 5, g] = d.dring[:]
+        st[NAT.F_DSUM:NAT.F_DSUM + 3, g] = d.dsum[:]
     for e in range(E):
         ev = oenv.envs[e]
         es[NAT.E_TICK, e] = ev.tick
         es[NAT.E_EPISODE, e] = ev.episode
         es[NAT.E_FLAGS, e] = 1      # neighbour reset obs read stale_vel (== oracle obs_vel)
         es[NAT.E_OBST_M, e], es[NAT.E_OBST_SZ, e] = ev.obst_mi, ev.obst_si
+        for k, name in enumerate(STAT_ENV_FIELDS):
+            es[NAT.E_ST_COL + k, e] = getattr(ev, name)
         for i in range(N):
             g = e * N + i
             prev = 0

@@ -6,9 +6,12 @@ The fixtures in tests/golden were produced by tools/gen_golden.py from the refer
 CPU-only; no GPU needed.
 """
 import ctypes
+import os
 
 import numpy as np
 import pytest
+
+from conftest import GOLDEN
 
 import oracle as O
 
@@ -180,9 +183,11 @@ def load_traj_env(golden, name):
     g = golden("traj_" + name)
     n, k = int(g["n"]), int(g["k"])
     k = n - 1 if k == -1 else k
+    self_dim = g["obs"].shape[-1] - 6 * k          # 18 / 19 / 24: xyz_vxyz_R_omega[_floor|_wall]
     p = O.params_from_golden(golden("params"), num_agents=n, num_envs=1, k_neighbors=k,
                              ep_len=int(g["ep_len"]), use_downwash=int(g["downwash"]),
-                             sense_noise=int(g["sense"]), ou_sigma=0.2 * float(g["thrust_noise"]))
+                             sense_noise=int(g["sense"]), ou_sigma=0.2 * float(g["thrust_noise"]),
+                             obs_repr={18: 0, 19: 1, 24: 2}[self_dim])
     drones = O.drones_array(n)
     envs = O.envs_array(1)
     for i in range(n):
@@ -198,7 +203,7 @@ def load_traj_env(golden, name):
     return g, p, drones, envs
 
 
-@pytest.mark.parametrize("name", ["n8k6", "n8k7", "n1", "n8dw", "n32k6", "n8quiet"])
+@pytest.mark.parametrize("name", ["n8k6", "n8k7", "n1", "n8dw", "n32k6", "n8quiet", "n8wall", "n4wallquiet", "n8stats"])
 def test_trajectory_tape_replay(golden, name):
     g, p, drones, envs = load_traj_env(golden, name)
     n = p.num_agents
@@ -222,5 +227,44 @@ def test_trajectory_tape_replay(golden, name):
     assert tape.r.tape_pos == len(g["tape"])
     assert tape.r.spawn_pos == len(g["spawn"])
     close(np.stack([O.get_arr(drones[i].pos) for i in range(n)]), g["final_pos"], RTOL_TRAJ, ATOL_TRAJ)
-    if name in ("n8k6", "n8k7", "n1", "n32k6"):
+    if name in ("n8k6", "n8k7", "n1", "n32k6", "n8wall", "n8stats"):
         assert n_done >= 1   # the auto-reset path was exercised
+    if name == "n8wall":     # the wall features saw contacts: clipped at 0 and at 5
+        w = g["obs"][:, :, 18:24]
+        assert (w == 0).any() and (w == 5).any()
+
+
+def test_episode_extra_stats_tape_replay(golden):
+    """episode_extra_stats of every finished episode (quadrotor_multi.py:739-831): the oracle's accumulators,
+    replayed on the reference's own draws, give the reference's dicts -- the same keys (built by the product's
+    quadswarm_amd.stats from the oracle's row) and the same values."""
+    import json
+    from quadswarm_amd.stats import ES_D1, ES_D3, ES_D5, NES, episode_extra_stats
+
+    ref = json.load(open(os.path.join(GOLDEN, "traj_n8stats_stats.json")))["events"]
+    g, p, drones, envs = load_traj_env(golden, "n8stats")
+    n = p.num_agents
+    od = O.lib().or_obs_dim(ctypes.byref(p))
+    tape = O.TapeRng(g["tape"], g["spawn"])
+    got = []
+    for t in range(len(g["actions"])):
+        a = np.ascontiguousarray(g["actions"][t], dtype=np.float64)
+        obs, term, rew = np.zeros((n, od)), np.zeros((n, od)), np.zeros(n)
+        done = np.zeros(n, dtype=np.uint8)
+        O.lib().or_env_step(ctypes.byref(p), drones, envs, 0, O.dptr(a), tape.ref, O.dptr(obs), O.dptr(rew),
+                            done.ctypes.data_as(ctypes.POINTER(ctypes.c_ubyte)), O.dptr(term))
+        if done.any():
+            rows = []
+            for i in range(n):
+                row = np.array(envs[0].ep_stats[:], dtype=np.float64)
+                assert len(row) == NES
+                row[ES_D1], row[ES_D3], row[ES_D5] = drones[i].ep_dist[0], drones[i].ep_dist[1], drones[i].ep_dist[2]
+                rows.append(episode_extra_stats(row))
+            got.append({"step": t, "agents": rows})
+    assert [e["step"] for e in got] == [e["step"] for e in ref] and len(ref) == 2
+    for eg, er in zip(got, ref):
+        for i in range(n):
+            a, b = eg["agents"][i], er["agents"][i]
+            assert sorted(a) == sorted(b)
+            for key in b:
+                assert a[key] == pytest.approx(b[key], rel=1e-9, abs=1e-12), (eg["step"], i, key)

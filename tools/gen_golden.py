@@ -361,7 +361,7 @@ def snapshot(env):
         env_vel=env.vel.copy())
 
 
-def gen_traj(name, n, k, steps, ep_time, seed, setup=None, hover=False, **kw):
+def gen_traj(name, n, k, steps, ep_time, seed, setup=None, hover=False, stats=False, **kw):
     np.random.seed(seed)
     env = make_env_B(n, k, ep_time=ep_time, seed=seed, **kw)
     env.reset()
@@ -375,13 +375,21 @@ def gen_traj(name, n, k, steps, ep_time, seed, setup=None, hover=False, **kw):
     elif n > 1:  # climbing thrust so drones stay airborne and interact
         actions = np.clip(actions * 0.6 + 0.3, -1, 1)
     obs, rew, done = [], [], []
+    events = []
     begin()
     for t in range(steps):
-        o, r, dn, _ = env.step(actions[t])
+        o, r, dn, info = env.step(actions[t])
         obs.append(np.array(o, dtype=np.float64))
         rew.append(np.array(r, dtype=np.float64))
         done.append(np.array(dn, dtype=np.float64))
+        if stats and any(dn):   # infos[i]["episode_extra_stats"] of every agent (quadrotor_multi.py:739-831)
+            events.append({"step": t, "agents": [{k_: float(v) for k_, v in info[i]["episode_extra_stats"].items()}
+                                                 for i in range(n)]})
     tv, sp = end()
+    if stats:
+        import json
+        with open(os.path.join(OUT, f"traj_{name}_stats.json"), "w") as f:
+            json.dump({"name": name, "events": events}, f, indent=0, sort_keys=True)
     final = snapshot(env)
     np.savez_compressed(os.path.join(OUT, f"traj_{name}.npz"), actions=actions, obs=np.stack(obs),
                         rew=np.stack(rew), done=np.stack(done), tape=tv, spawn=sp, n=n, k=k,
@@ -455,5 +463,22 @@ def gen_neighbors(seed=5):
     np.savez_compressed(os.path.join(OUT, "neighbors.npz"), **out)
 
 
+def main_extra(which):
+    """Fixtures added later, generated on their own (the ones above stay byte-identical):
+      wall   the xyz_vxyz_R_omega_wall self obs (get_state.py:270-292): a noisy 8-drone run with wall / ceiling
+             contacts and a noise-free 4-drone hover the GPU replays
+      stats  episode_extra_stats of every finished episode (quadrotor_multi.py:739-831) over 2-s episodes"""
+    os.makedirs(OUT, exist_ok=True)
+    if "wall" in which:
+        gen_traj("n8wall", 8, 6, 120, ep_time=0.5, seed=17, setup=setup_crowd, obs_repr="xyz_vxyz_R_omega_wall")
+        gen_traj("n4wallquiet", 4, 3, 150, ep_time=15.0, seed=18, hover=True, sense=None, thrust_noise=0.0,
+                 obs_repr="xyz_vxyz_R_omega_wall")
+    if "stats" in which:
+        gen_traj("n8stats", 8, 6, 420, ep_time=2.0, seed=19, setup=setup_crowd, stats=True)
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1:
+        main_extra(sys.argv[1:])
+    else:
+        main()
