@@ -381,6 +381,9 @@ class OracleEnv:
         return obs, rew, done.astype(bool), term
 
 
+NB_TRACE_W = 12   # OR_NB_TRACE_W
+
+
 class OracleEnvA:
     """Batched flavor-A env (quadrotor_multi_rewards) in Philox mode."""
 
@@ -391,6 +394,36 @@ class OracleEnvA:
         self.drones = drones_array(self.E * self.N)
         self.envs = envs_array(self.E)
         self.seed = seed
+        n = self.E * self.N + int(params.id_offset)
+        # inputs of the last call's neighbour-obs passes per drone (or_nb_trace* / or_key_trace* of
+        # quadswarm_oracle_a.c): trace["step"|"reset"][g, slot] = (j, pixel noise 1, 2, pr[3], vr[3], aw, h_i, h_j),
+        # keys["step"|"reset"][g, j] = selection key (K < N-1); NaN where the call ran no such pass
+        on = FT == np.float64
+        self.trace = {k: np.full((n, 64, NB_TRACE_W), np.nan) for k in ("step", "reset")} if on else None
+        self.keys = {k: np.full((n, 64), np.nan) for k in ("step", "reset")} if on else None
+
+    def _traced(self, fn):
+        if self.trace is None:
+            return fn()
+        ptrs = [(ctypes.c_void_p.in_dll(lib(), name), arr) for name, arr in (
+            ("or_nb_trace", self.trace["step"]), ("or_key_trace", self.keys["step"]),
+            ("or_nb_trace_reset", self.trace["reset"]), ("or_key_trace_reset", self.keys["reset"]))]
+        for v, arr in ptrs:
+            arr.fill(np.nan)
+            v.value = arr.ctypes.data
+        try:
+            return fn()
+        finally:
+            for v, _ in ptrs:
+                v.value = None
+
+    def rel_features(self, pr, aw, hi, hj, vr, n1=0.0, n2=0.0):
+        """or_rel_features_x: one neighbour's features (unclipped) on explicit inputs."""
+        f = np.zeros(8)
+        a, b = np.ascontiguousarray(pr, dtype=np.float64), np.ascontiguousarray(vr, dtype=np.float64)
+        n = lib().or_rel_features_x(ctypes.byref(self.p), dptr(a), ctypes.c_double(aw), ctypes.c_double(hi),
+                                    ctypes.c_double(hj), dptr(b), ctypes.c_double(n1), ctypes.c_double(n2), dptr(f))
+        return f[:n]
 
     def set_capture_radius(self, r):
         for e in range(self.E):
@@ -400,14 +433,16 @@ class OracleEnvA:
         obs = np.zeros((self.E * self.N, self.obs_dim), dtype=FT)
         ri = np.zeros(self.E, dtype=np.uint8)
         u8 = ri.ctypes.data_as(ctypes.POINTER(ctypes.c_ubyte))
-        if mask is None:
-            lib().or_reset_all_a(ctypes.byref(self.p), self.drones, self.envs, self.seed, dptr(obs), u8)
-        else:
+        def run():
+            if mask is None:
+                lib().or_reset_all_a(ctypes.byref(self.p), self.drones, self.envs, self.seed, dptr(obs), u8)
+                return
             for e in np.flatnonzero(mask):
                 r = philox_rng(self.seed, 0)
                 rows = obs[e * self.N:(e + 1) * self.N]
                 lib().or_env_reset_a(ctypes.byref(self.p), self.drones, self.envs, int(e), ctypes.byref(r),
                                      dptr(rows), u8)
+        self._traced(run)
         return obs, ri
 
     def step(self, actions, nthreads=0):
@@ -417,7 +452,8 @@ class OracleEnvA:
         rew = np.zeros(self.E * self.N, dtype=FT)
         done = np.zeros(self.E * self.N, dtype=np.uint8)
         ri = np.zeros(self.E, dtype=np.uint8)
-        lib().or_step_all_a(ctypes.byref(self.p), self.drones, self.envs, dptr(a), self.seed,
-                            dptr(obs), dptr(rew), done.ctypes.data_as(ctypes.POINTER(ctypes.c_ubyte)),
-                            dptr(term), ri.ctypes.data_as(ctypes.POINTER(ctypes.c_ubyte)), nthreads)
+        self._traced(lambda: lib().or_step_all_a(
+            ctypes.byref(self.p), self.drones, self.envs, dptr(a), self.seed, dptr(obs), dptr(rew),
+            done.ctypes.data_as(ctypes.POINTER(ctypes.c_ubyte)), dptr(term),
+            ri.ctypes.data_as(ctypes.POINTER(ctypes.c_ubyte)), nthreads))
         return obs, rew, done.astype(bool), term, ri

@@ -304,6 +304,13 @@ void or_camera(const or_params* p, double rx, double ry, double global_angle, do
                double* dist, double* angle);
 void or_self_obs_a(const or_params* p, const or_drone* d, or_rng* r, uint32_t gid, uint32_t st_sensor,
                    uint32_t st_cam, double* out);
+int or_rel_features_x(const or_params* p, const double pr[3], double aw, double hi, double hj, const double vr[3],
+                      double n1, double n2, double* f);
+#define OR_NB_TRACE_W 12
+extern double* or_nb_trace;    /* test hooks: see quadswarm_oracle_a.c */
+extern double* or_key_trace;
+extern double* or_nb_trace_reset;
+extern double* or_key_trace_reset;
 void or_neighbor_obs_a(const or_params* p, const or_env* ev, const or_drone* dr, or_rng* r, uint32_t gbase,
                        int reset, double* obs, int obs_dim);
 void or_target_step(const or_params* p, or_env* ev, or_drone* dr);

@@ -355,14 +355,22 @@ void or_self_obs_a(const or_params* p, const or_drone* d, or_rng* r, uint32_t gi
 /* ------------------------------------------------------------------------------------------ */
 /* neighbour obs (quadrotor_multi_rewards.py:326-476)                                          */
 /* ------------------------------------------------------------------------------------------ */
-/* get_rel_pos_vel_item for one (i, j) pair: features in the reference's concatenation order */
-static int rel_features(const or_params* p, const or_env* ev, const or_drone* dr, int i, int j, double n1,
-                        double n2, double* f) {
+/* Test hooks (tests/parity_utils.py, per-feature conditioning of the GPU-vs-oracle comparison): when set,
+ * the obs pass of or_neighbor_obs_a records the inputs of every (drone, slot) feature block in
+ * or_nb_trace[(gid * 64 + slot) * OR_NB_TRACE_W] = {j, n1, n2, pr[3], vr[3], aw, h_i, h_j}, and the selection
+ * pass the sort key of every candidate j in or_key_trace[gid * 64 + j]; the *_reset pair gets the passes of
+ * the resets (the obs a finished env returns), the other pair those of the step (its terminal obs). */
+double* or_nb_trace = NULL;
+double* or_key_trace = NULL;
+double* or_nb_trace_reset = NULL;
+double* or_key_trace_reset = NULL;
+
+/* get_rel_pos_vel_item for one (i, j) pair on explicit inputs: pr = pos_j - pos_i, aw = own heading angle,
+ * hi / hj = the stale headings, vr = vel_j - vel_i; features in the reference's concatenation order */
+int or_rel_features_x(const or_params* p, const double pr[3], double aw, double hi, double hj, const double vr[3],
+                      double n1, double n2, double* f) {
     const int m = p->nfeat;
-    double pr[3] = {ev->obs_pos[j][0] - ev->obs_pos[i][0], ev->obs_pos[j][1] - ev->obs_pos[i][1],
-                    ev->obs_pos[j][2] - ev->obs_pos[i][2]};
     double pn = sqrt(pr[0] * pr[0] + pr[1] * pr[1] + pr[2] * pr[2]);
-    const double aw = dr[i].angle;
     int n = 0;
     double nd = 0, na = 0;
     if (m & OR_NF_DIST) f[n++] = pn;
@@ -377,14 +385,24 @@ static int rel_features(const or_params* p, const or_env* ev, const or_drone* dr
     }
     if (m & OR_NF_NSANGLE) { f[n++] = cos(na); f[n++] = sin(na); }
     if (m & (OR_NF_HEADING | OR_NF_SHEADING)) {
-        double rh = wrap_pi(ev->heading[j] - ev->heading[i]);
+        double rh = wrap_pi(hj - hi);
         if (m & OR_NF_HEADING) f[n++] = rh;
         if (m & OR_NF_SHEADING) { f[n++] = cos(rh); f[n++] = sin(rh); }
     }
     if (m & OR_NF_NPOS) for (int c = 0; c < 3; ++c) f[n++] = pr[c];
     if (m & OR_NF_POS) for (int c = 0; c < 3; ++c) f[n++] = pr[c];
-    if (m & OR_NF_VEL) for (int c = 0; c < 3; ++c) f[n++] = ev->obs_vel[j][c] - ev->obs_vel[i][c];
+    if (m & OR_NF_VEL) for (int c = 0; c < 3; ++c) f[n++] = vr[c];
     return n;
+}
+
+static int rel_features(const or_params* p, const or_env* ev, const or_drone* dr, int i, int j, double n1,
+                        double n2, double* f) {
+    double pr[3], vr[3];
+    for (int c = 0; c < 3; ++c) {
+        pr[c] = ev->obs_pos[j][c] - ev->obs_pos[i][c];
+        vr[c] = ev->obs_vel[j][c] - ev->obs_vel[i][c];
+    }
+    return or_rel_features_x(p, pr, dr[i].angle, ev->heading[i], ev->heading[j], vr, n1, n2, f);
 }
 
 /* neighborhood_indices (:445-476) + extend_obs_space (:422-443) with the clip box.  The camera is
@@ -396,6 +414,8 @@ void or_neighbor_obs_a(const or_params* p, const or_env* ev, const or_drone* dr,
     const int N = p->num_agents, K = p->k_neighbors, F = p->nfeat_dim, so = self_dim_a(p);
     if (K <= 0) return;
     const int cam = (p->nfeat & OR_NF_NDIST) != 0;
+    double* nbt = reset ? or_nb_trace_reset : or_nb_trace;
+    double* kt = reset ? or_key_trace_reset : or_key_trace;
     const uint32_t st_obs = reset ? OR_S_RESET_CAM : OR_S_CAM, st_sel = reset ? OR_S_RESET_CAM_SEL : OR_S_CAM_SEL;
     int sel[64][64];
     for (int i = 0; i < N; ++i) {
@@ -420,6 +440,7 @@ void or_neighbor_obs_a(const or_params* p, const or_env* ev, const or_drone* dr,
                 for (int q = 0; q < nf; ++q) s += f[q] * f[q];
                 double k = sqrt(s);
                 key[c] = k > 0.01 ? k : (k == k ? 0.01 : k);
+                if (kt) kt[(size_t)(gbase + (uint32_t)i) * 64 + sel[i][c]] = key[c];
             }
             /* argsort (insertion sort for <= 16 keys: stable; NaN sorts last) */
             int order[64];
@@ -450,6 +471,16 @@ void or_neighbor_obs_a(const or_params* p, const or_env* ev, const or_drone* dr,
         double* o = obs + (size_t)i * od + so;
         for (int c = 0; c < K; ++c) {
             double f[8];
+            if (nbt) {
+                const int j = sel[i][c];
+                double* t = nbt + ((size_t)(gbase + (uint32_t)i) * 64 + c) * OR_NB_TRACE_W;
+                t[0] = j; t[1] = n1[c]; t[2] = n2[c];
+                for (int q = 0; q < 3; ++q) {
+                    t[3 + q] = ev->obs_pos[j][q] - ev->obs_pos[i][q];
+                    t[6 + q] = ev->obs_vel[j][q] - ev->obs_vel[i][q];
+                }
+                t[9] = dr[i].angle; t[10] = ev->heading[i]; t[11] = ev->heading[j];
+            }
             rel_features(p, ev, dr, i, sel[i][c], n1[c], n2[c], f);
             for (int q = 0; q < F; ++q) o[c * F + q] = clipd(f[q], p->nclip_lo[q], p->nclip_hi[q]);
         }

@@ -147,7 +147,7 @@ class GpuQuadVecEnv:
         from .stats import episode_extra_stats
         out = [{} for _ in rows]
         if self.env.estats is not None:
-            est = self.env.estats[torch.as_tensor(rows, device=self.env.device, dtype=torch.long)].cpu().numpy()
+            est = self.env.estats[self.env._torch.as_tensor(rows, device=self.env.device, dtype=self.env._torch.long)].cpu().numpy()
             for k in range(len(rows)):
                 out[k] = episode_extra_stats(est[k], use_obstacles=self.cfg.use_obstacles)
         if self.env.replay is not None:

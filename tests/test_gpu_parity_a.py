@@ -105,7 +105,8 @@ def test_one_step_from_identical_state(name):
         np.testing.assert_allclose(np_(rew), w_rew, atol=1e-5, err_msg=f"rew step {t}")
         assert_obs_match_a(np_(obs), w_obs, cfg, oenv=oenv, what=f"obs step {t}")
         if w_done.any():
-            assert_obs_match_a(np_(term)[w_done], w_term[w_done], cfg, what=f"term step {t}")
+            assert_obs_match_a(np_(term)[w_done], w_term[w_done], cfg, oenv=oenv, rows=np.flatnonzero(w_done),
+                               term=True, what=f"term step {t}")
         stats["done"] += int(w_done.sum())
         stats["cap"] += int((w_rew > 50).sum())
         f = env.drone_fields()
