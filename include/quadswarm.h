@@ -37,7 +37,7 @@ extern "C" {
 #endif
 
 #define QS_ABI_VERSION 7
-#define QS_MAX_AGENTS 32            /* drones per env: one env lives inside one 64-lane wavefront */
+#define QS_MAX_AGENTS 64            /* drones per env: one env lives inside one 64-lane wavefront */
 #define QS_MAX_DR_CHOICES 8         /* entries per obstacle domain-randomisation list */
 
 enum qs_status {

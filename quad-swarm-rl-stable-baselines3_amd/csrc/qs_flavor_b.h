@@ -144,11 +144,11 @@ __device__ void neighbor_obs(const KP& kp, const float4* xch, int dbase, int di,
             for (int c = 0; c < 6; ++c) rel[KEEP ? t : 0][c] = r[c];
         }
     }
-    float allk[PJ * Q];   // key of candidate m = q' + Q t' (sub-lane q', slot t')
+    float allk_[Q == 1 ? 1 : PJ * Q];   // key of candidate m = q' + Q t' (sub-lane q', slot t')
+    float* allk = Q == 1 ? key : allk_;
 #pragma unroll
     for (int t = 0; t < PJ; ++t) {
         if constexpr (Q == 1) {
-            allk[t] = key[t];
         } else if constexpr (Q == 2) {
             allk[2 * t] = qbc<2, 0>(key[t]);
             allk[2 * t + 1] = qbc<2, 1>(key[t]);
@@ -1288,21 +1288,24 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
         // sub-lane q tests the partners j = q + Q t (LDS reads issued back to back, branch-free
         // tests), then the drone's collision row and proximity sum are reduced over the sub-lanes
         constexpr int PJ = (NPAD + Q - 1) / Q;
-        float4 pj[PJ];
+        constexpr int CH = PJ < 16 ? PJ : 16;   // partners loaded per batch (bounds the VGPRs at N = 64)
+        for (int t0 = 0; t0 < PJ; t0 += CH) {
+            float4 pj[CH];
 #pragma unroll
-        for (int t = 0; t < PJ; ++t) {
-            const int j = q + Q * t;
-            pj[t] = xch[2 * (dbase + (j < NPAD ? j : NPAD - 1))];
-        }
+            for (int u = 0; u < CH; ++u) {
+                const int j = q + Q * (t0 + u);
+                pj[u] = xch[2 * (dbase + (j < NPAD ? j : NPAD - 1))];
+            }
 #pragma unroll
-        for (int t = 0; t < PJ; ++t) {
-            const int j = q + Q * t;
-            const float dx = d.pos[0] - pj[t].x, dy = d.pos[1] - pj[t].y, dz = d.pos[2] - pj[t].z;
-            const float dist = fsqrt(dx * dx + dy * dy + dz * dz);
-            const bool ok = j != di && j < kp.N;
-            cur |= (ok && dist <= kp.col_thr) ? (1ull << j) : 0ull;
-            const float pterm = kpm.prox_ratio * dist + kpm.prox_max;
-            pen += (ok && dist <= kp.fall_thr) ? pterm : 0.f;   // pen >= 0: adding +0 is exact
+            for (int u = 0; u < CH; ++u) {
+                const int j = q + Q * (t0 + u);
+                const float dx = d.pos[0] - pj[u].x, dy = d.pos[1] - pj[u].y, dz = d.pos[2] - pj[u].z;
+                const float dist = fsqrt(dx * dx + dy * dy + dz * dz);
+                const bool ok = j != di && j < kp.N;
+                cur |= (ok && dist <= kp.col_thr) ? (1ull << j) : 0ull;
+                const float pterm = kpm.prox_ratio * dist + kpm.prox_max;
+                pen += (ok && dist <= kp.fall_thr) ? pterm : 0.f;   // pen >= 0: adding +0 is exact
+            }
         }
         cur = qor<Q>(cur);
         pen = qsum<Q>(pen);

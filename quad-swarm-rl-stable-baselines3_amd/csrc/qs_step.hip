@@ -174,6 +174,9 @@ static int validate(const qs_config* c) {
 }
 
 static int npad_of(int n);
+// a gfx950 workgroup may allocate the CU's whole 160 KB of LDS (64-drone envs with all 63 neighbours visible
+// stage 64 rows of 396 floats)
+static constexpr size_t QS_LDS_MAX = 160 * 1024;
 static size_t shm_bytes(const qs_config& c, int obs_dim, int npad, bool step, int qb = QS_QB, int qa = QS_QA);
 static int neighbor_dim(int t);
 
@@ -455,8 +458,8 @@ extern "C" int qs_config_default_a(qs_config* c, int32_t num_envs, int32_t num_a
 static int check_lds(const qs_config* c) {
     const qs_layout L = make_layout(c);
     const int np = npad_of(c->num_agents);
-    if (shm_bytes(*c, L.obs_dim, np, true) > 65536 || shm_bytes(*c, L.obs_dim, np, false) > 65536)
-        return fail(QS_E_UNSUPPORTED, "observation / obstacle tiles exceed 64 KB of LDS per workgroup");
+    if (shm_bytes(*c, L.obs_dim, np, true) > QS_LDS_MAX || shm_bytes(*c, L.obs_dim, np, false) > QS_LDS_MAX)
+        return fail(QS_E_UNSUPPORTED, "observation / obstacle tiles exceed the 160 KB of LDS of a workgroup");
     return QS_OK;
 }
 
@@ -626,6 +629,7 @@ static int launch(qs_handle* h, bool step, const float* act, const uint8_t* mask
         QS_LAUNCH(8)
         QS_LAUNCH(16)
         QS_LAUNCH(32)
+        QS_LAUNCH(64)
         default:
             return fail(QS_E_UNSUPPORTED, "num_agents not supported");
     }
@@ -1090,7 +1094,7 @@ extern "C" int qs_specialize(qs_handle* h, int enable) {
     QS_HIP(use_device(h));
     int qb, qa;
     jit_lanes(&qb, &qa);
-    if (shm_bytes(h->cfg, h->lay.obs_dim, h->npad, true, qb, qa) > 65536)
+    if (shm_bytes(h->cfg, h->lay.obs_dim, h->npad, true, qb, qa) > QS_LDS_MAX)
         return fail(QS_E_UNSUPPORTED, "QS_QB / QS_QA geometry exceeds 64 KB of LDS per workgroup");
     std::string rn;
     const std::string key = std::to_string(h->device) + "|" + kernel_names(&h->cfg, h->kp, h->npad, &rn) + "|" +

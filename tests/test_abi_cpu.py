@@ -79,7 +79,7 @@ def test_validation_errors_are_reported():
     assert L.qs_layout_query(bad, lay) == -1
     assert b"k_neighbors" in L.qs_last_error()
     bad = N.QsConfig.from_buffer_copy(c)
-    bad.num_agents = 33
+    bad.num_agents = 65
     assert L.qs_layout_query(bad, lay) == -2
     bad = N.QsConfig.from_buffer_copy(c)
     bad.abi_version = 99

@@ -34,6 +34,7 @@ CONFIGS = {
     "pv8": dict(num_agents=8, neighbor_obs_type="pos_vel", obs_repr="cdist_cdistdot_dist_distdot_angle_angledot"),
     "n1": dict(num_agents=1, neighbor_obs_type="none"),
     "n32k6": dict(num_agents=32, neighbor_visible_num=6, neighbor_obs_type="dist_sangle"),
+    "n64k6": dict(num_agents=64, neighbor_visible_num=6, neighbor_obs_type="dist_sangle"),
     "static4": dict(num_agents=4, quads_mode="static_same_goal", neighbor_obs_type="pos"),
 }
 

@@ -444,12 +444,16 @@ def main():
 
 
 def gen_neighbors(seed=5):
+    gen_neighbors_sizes("neighbors.npz", [(8, 6), (8, 2), (8, 7), (32, 6)], seed)
+
+
+def gen_neighbors_sizes(fname, sizes, seed, count=40):
     rng = np.random.default_rng(seed)
     out = {}
-    for n, k in [(8, 6), (8, 2), (8, 7), (32, 6)]:
+    for n, k in sizes:
         env = make_env_B(n, k)
         P, V, O = [], [], []
-        for c in range(40):
+        for c in range(count):
             env.pos = rng.uniform(-6, 6, (n, 3))
             env.vel = rng.uniform(-4, 4, (n, 3))
             if c % 5 == 0:  # near-duplicates around the 0.01 key clamp
@@ -460,14 +464,15 @@ def gen_neighbors(seed=5):
         out[f"n{n}k{k}_pos"] = np.stack(P)
         out[f"n{n}k{k}_vel"] = np.stack(V)
         out[f"n{n}k{k}_obs"] = np.stack(O)
-    np.savez_compressed(os.path.join(OUT, "neighbors.npz"), **out)
+    np.savez_compressed(os.path.join(OUT, fname), **out)
 
 
 def main_extra(which):
     """Fixtures added later, generated on their own (the ones above stay byte-identical):
       wall   the xyz_vxyz_R_omega_wall self obs (get_state.py:270-292): a noisy 8-drone run with wall / ceiling
              contacts and a noise-free 4-drone hover the GPU replays
-      stats  episode_extra_stats of every finished episode (quadrotor_multi.py:739-831) over 2-s episodes"""
+      stats  episode_extra_stats of every finished episode (quadrotor_multi.py:739-831) over 2-s episodes
+      n64    a 64-drone crowded trajectory and 64-drone neighbour selections (k = 6 and all 63 visible)"""
     os.makedirs(OUT, exist_ok=True)
     if "wall" in which:
         gen_traj("n8wall", 8, 6, 120, ep_time=0.5, seed=17, setup=setup_crowd, obs_repr="xyz_vxyz_R_omega_wall")
@@ -475,6 +480,9 @@ def main_extra(which):
                  obs_repr="xyz_vxyz_R_omega_wall")
     if "stats" in which:
         gen_traj("n8stats", 8, 6, 420, ep_time=2.0, seed=19, setup=setup_crowd, stats=True)
+    if "n64" in which:   # 64-drone swarms: the first size past one drone per lane of a wave with Q > 1
+        gen_traj("n64k6", 64, 6, 25, ep_time=0.2, seed=20, setup=setup_crowd)
+        gen_neighbors_sizes("neighbors64.npz", [(64, 6), (64, 63)], seed=6, count=10)
 
 
 if __name__ == "__main__":

@@ -21,6 +21,7 @@ for s in "$@"; do
     tests) step gpu_tests 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     testsall) step gpu_tests 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread ;;
     testsnew) step gpu_tests_new 600 python -u -m pytest tests/test_gpu_stats.py tests/test_gpu_guard_params.py tests/test_gpu_c5.py -v --timeout 200 --timeout-method thread ;;
+    testspar) step gpu_tests_par 900 python -u -m pytest tests/test_gpu_stats.py tests/test_gpu_parity.py tests/test_gpu_parity_a.py -v --timeout 300 --timeout-method thread ;;
     benchdrv) step bench_driver 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     benchblocks) step bench_blocks 600 python bench.py --steps 2000 --streams 4 --no-cpu-baseline --e2e-iters 0 ;;
     bench) step bench 600 python bench.py ;;
