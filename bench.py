@@ -351,6 +351,8 @@ def main():
                          "the launch rocprofv3 profiles); with S > 1 the bench keeps the blocks only if an A/B "
                          "measures them faster than the one handle")
     ap.add_argument("--generic", action="store_true", help="generic kernels instead of qs_specialize (hipRTC)")
+    ap.add_argument("--no-episode-stats", action="store_true",
+                    help="A/B only: skip the episode_extra_stats accumulators the reference's step keeps")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="seconds per cpu_baseline leg (3 legs)")
     ap.add_argument("--cpu-worker", action="store_true", help=argparse.SUPPRESS)
@@ -376,6 +378,8 @@ def main():
     from quadswarm_amd.env import QuadSwarmEnv
 
     kw = CONFIGS[args.config]
+    if args.no_episode_stats:
+        kw = dict(kw, episode_stats=False)
     cfg = make_cfg(kw, seed=0, specialize=not args.generic)
     I = cfg.num_envs * cfg.num_agents
     cfg.drone_id_offset = rank * I
@@ -511,7 +515,8 @@ def main():
             "config": {"workload": WORKLOAD[args.config], "envs_per_gpu": cfg.num_envs,
                        "agents_per_env": cfg.num_agents, "visible_neighbors": cfg.k_neighbors,
                        "obs_dim": cfg.obs_dim, "global_batch": world * I, "parallelism": f"env-shard x{world}",
-                       "flavor": cfg.flavor, "launch": launch, "blocks_ab_us_per_step": ab},
+                       "flavor": cfg.flavor, "episode_stats": bool(cfg.episode_stats), "launch": launch,
+                       "blocks_ab_us_per_step": ab},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,

@@ -904,10 +904,14 @@ __device__ __forceinline__ float2* obst_tile(float* lds, const KP& kp, int slots
 #define QS_COOP_STATE 1
 #endif
 constexpr int DRONE_WORDS = QS_F_GOAL + 3 + 4;
+// with episode_extra_stats on, the step also loads the drone's distance ring and window sums (fields
+// QS_F_DRING .. QS_F_DSUM + 2) in the same batch: words DRONE_WORDS .. LOAD_WORDS - 1
+constexpr int STAT_WORDS = 8;
+constexpr int LOAD_WORDS = DRONE_WORDS + STAT_WORDS;
 
 template <int Q, int W, int T>
 __device__ __forceinline__ void qbc_words(const uint32_t (&r)[T], uint32_t* wv) {
-    if constexpr (W < DRONE_WORDS) {
+    if constexpr (W < LOAD_WORDS && W / Q < T) {
         wv[W] = (uint32_t)__float_as_int(qbc<Q, W % Q>(__int_as_float((int)r[W / Q])));
         qbc_words<Q, W + 1, T>(r, wv);
     }
@@ -916,30 +920,39 @@ __device__ __forceinline__ void qbc_words(const uint32_t (&r)[T], uint32_t* wv) 
 __device__ __forceinline__ uint32_t drone_word_off(const KP& kp, const Bufs& b, int w, uint32_t go) {
     const uint32_t I4 = (uint32_t)kp.I * 4u;
     const uint32_t ist0 = (uint32_t)((const char*)b.ist - (const char*)b.st);
+    if (w >= DRONE_WORDS) return (uint32_t)(QS_F_DRING + w - DRONE_WORDS) * I4 + go;
     return (w < QS_F_GOAL + 3 ? (uint32_t)w * I4 : ist0 + (uint32_t)(w - QS_F_GOAL - 3) * I4) + go;
 }
 
-template <int Q>
+template <int Q, int NW = DRONE_WORDS>
 struct DroneWords {
-    static constexpr int T = (DRONE_WORDS + Q - 1) / Q;
+    static constexpr int T = (NW + Q - 1) / Q;
     uint32_t r[T];
 };
-// issue the sub-lane's state-word loads (no wait)
-template <int Q>
-__device__ __forceinline__ void load_words_q(const KP& kp, const Bufs& b, int g, int q, DroneWords<Q>& dw) {
+// issue the sub-lane's state-word loads (no wait): the first nw <= NW words
+template <int Q, int NW>
+__device__ __forceinline__ void load_words_q(const KP& kp, const Bufs& b, int g, int q, DroneWords<Q, NW>& dw,
+                                             int nw = NW) {
     const uint32_t go = (uint32_t)g * 4u;
 #pragma unroll
-    for (int t = 0; t < DroneWords<Q>::T; ++t) {
+    for (int t = 0; t < DroneWords<Q, NW>::T; ++t) {
         const int w = t * Q + q;
-        dw.r[t] = w < DRONE_WORDS ? *reinterpret_cast<const uint32_t*>((const char*)b.st + drone_word_off(kp, b, w, go)) : 0u;
+        dw.r[t] = w < nw ? *reinterpret_cast<const uint32_t*>((const char*)b.st + drone_word_off(kp, b, w, go)) : 0u;
     }
 }
-template <int Q>
-__device__ __forceinline__ void unpack_words_q(const DroneWords<Q>& dw, Drone& d) {
-    constexpr int T = DroneWords<Q>::T;
+// the drone on every sub-lane; stw (if given) gets the STAT_WORDS words as floats
+template <int Q, int NW>
+__device__ __forceinline__ void unpack_words_q(const DroneWords<Q, NW>& dw, Drone& d, float* stw = nullptr) {
+    constexpr int T = DroneWords<Q, NW>::T;
     const uint32_t (&r)[T] = dw.r;
-    uint32_t wv[DRONE_WORDS];
+    uint32_t wv[T * Q > DRONE_WORDS ? T * Q : DRONE_WORDS];
     qbc_words<Q, 0, T>(r, wv);
+    if constexpr (NW > DRONE_WORDS) {
+        if (stw) {
+#pragma unroll
+            for (int k = 0; k < STAT_WORDS; ++k) stw[k] = __int_as_float((int)wv[DRONE_WORDS + k]);
+        }
+    }
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         d.pos[i] = __int_as_float((int)wv[QS_F_POS + i]); d.vel[i] = __int_as_float((int)wv[QS_F_VEL + i]);
@@ -961,13 +974,16 @@ __device__ __forceinline__ void unpack_words_q(const DroneWords<Q>& dw, Drone& d
 template <int Q>
 __device__ __forceinline__ void load_drone_q(const KP& kp, const Bufs& b, int g, int q, Drone& d) {
     DroneWords<Q> dw;
-    load_words_q<Q>(kp, b, g, q, dw);
-    unpack_words_q<Q>(dw, d);
+    load_words_q(kp, b, g, q, dw);
+    unpack_words_q(dw, d);
 }
 
-template <int Q>
-__device__ __forceinline__ void store_drone_q(const KP& kp, const Bufs& b, int g, int q, bool active, const Drone& d) {
-    uint32_t wv[DRONE_WORDS];
+// ST: also the stats words DRONE_WORDS + k whose bit k of stmask is set (stw = their values)
+template <int Q, bool ST = false>
+__device__ __forceinline__ void store_drone_q(const KP& kp, const Bufs& b, int g, int q, bool active, const Drone& d,
+                                              const float* stw = nullptr, uint32_t stmask = 0u) {
+    constexpr int NW = ST ? LOAD_WORDS : DRONE_WORDS;
+    uint32_t wv[NW];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         wv[QS_F_POS + i] = (uint32_t)__float_as_int(d.pos[i]); wv[QS_F_VEL + i] = (uint32_t)__float_as_int(d.vel[i]);
@@ -986,7 +1002,11 @@ __device__ __forceinline__ void store_drone_q(const KP& kp, const Bufs& b, int g
     wv[IW + QS_I_FLAGS] = d.flags;
     wv[IW + QS_I_PREV_LO] = (uint32_t)d.prev;
     wv[IW + QS_I_PREV_HI] = (uint32_t)(d.prev >> 32);
-    constexpr int T = (DRONE_WORDS + Q - 1) / Q;
+    if constexpr (ST) {
+#pragma unroll
+        for (int k = 0; k < STAT_WORDS; ++k) wv[DRONE_WORDS + k] = (uint32_t)__float_as_int(stw[k]);
+    }
+    constexpr int T = (NW + Q - 1) / Q;
     const uint32_t go = (uint32_t)g * 4u;
     const __amdgpu_buffer_rsrc_t rs = qs_rsrc(b.st);
 #pragma unroll
@@ -995,8 +1015,9 @@ __device__ __forceinline__ void store_drone_q(const KP& kp, const Bufs& b, int g
         uint32_t v = wv[t * Q];
 #pragma unroll
         for (int k = 1; k < Q; ++k)
-            if (q == k && t * Q + k < DRONE_WORDS) v = wv[t * Q + k];
-        if (active && w < DRONE_WORDS) st_wt1(rs, drone_word_off(kp, b, w, go), 0u, v);
+            if (q == k && t * Q + k < NW) v = wv[t * Q + k];
+        const bool wr = w < DRONE_WORDS || (w < NW && ((stmask >> (w - DRONE_WORDS)) & 1u));
+        if (active && wr) st_wt1(rs, drone_word_off(kp, b, w, go), 0u, v);
     }
 }
 
@@ -1157,42 +1178,56 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     const int eidx = active ? env : 0;
     const int tick0 = b.env[QS_E_TICK * kp.E + eidx];
     const int episode = b.env[QS_E_EPISODE * kp.E + eidx];
+    // episode_extra_stats: the env's 11 counters QS_E_ST_COL.. dealt over its lanes (lane li holds li + LPE t)
+    constexpr int NCNT = 11, CT = (NCNT + LPE - 1) / LPE;
+    const int li = lane - lbase;
+    const bool envok = env < kp.E;
+    int cnt[CT];
+#pragma unroll
+    for (int t = 0; t < CT; ++t) {
+        const int k = li + LPE * t;
+        cnt[t] = (kp.stats && envok && k < NCNT) ? b.env[(QS_E_ST_COL + k) * kp.E + env] : 0;
+    }
     Drone d;   // every sub-lane holds the whole drone
 #if defined(QS_DIAG_NOLOAD)   // diagnostic builds only (QS_JIT_OPTS): phase-removal timing experiments
     d = Drone{};
     d.pos[2] = 2.f; d.rot[0] = d.rot[4] = d.rot[8] = 1.f; d.goal[2] = 2.f;
     d.pos[0] = 0.01f * (float)(g % 97); d.pos[1] = 0.01f * (float)(g % 89);
+    float stw[STAT_WORDS] = {};
 #elif QS_COOP_STATE
-    DroneWords<Q> dw;
-    load_words_q<Q>(kp, b, g, q, dw);
+    DroneWords<Q, LOAD_WORDS> dw;
+    load_words_q(kp, b, g, q, dw, kp.stats ? LOAD_WORDS : DRONE_WORDS);
 #if QS_LOADS_FIRST
     __builtin_amdgcn_sched_barrier(0);
 #endif
-    unpack_words_q<Q>(dw, d);
+    float stw[STAT_WORDS];
+    unpack_words_q(dw, d, stw);
 #else
     load_drone(kp, b, g, d);
+    float stw[STAT_WORDS];
+    for (int k = 0; k < STAT_WORDS; ++k) stw[k] = kp.stats ? b.st[(QS_F_DRING + k) * kp.I + g] : 0.f;
 #endif
     float a[4] = {av.x, av.y, av.z, av.w};
     const Rng rng = env_rng(seed, tick0, episode);
     const int tick = tick0 + 1;
     const bool done = tick > kpm.ep_len;
-    // episode_extra_stats (kp.stats): distance_to_goal's last entries and window sums of this drone, loaded
-    // now (consumed after the physics) by its lead sub-lane while the ring is still needed / in the window
+    // episode_extra_stats (kp.stats): distance_to_goal's last entries and window sums of this drone (loaded
+    // with the state words; consumed after the physics) -- the ring while it is still needed, the sums in
+    // their windows
     float dring[5] = {0.f, 0.f, 0.f, 0.f, 0.f}, dsum[3] = {0.f, 0.f, 0.f};
     bool in_win[3] = {false, false, false};
+    uint32_t stmask = 0u;   // the stats words (stw) the state store writes back
     if (kp.stats) {
         const int T = kpm.ep_len + 1;   // the entry count when the episode ends
 #pragma unroll
         for (int k = 0; k < 3; ++k) in_win[k] = tick > T - kp.st_win[k];
-        if (lead && !(d.flags & QS_FL_REACHED) && tick >= 5) {
+        if (!(d.flags & QS_FL_REACHED) && tick >= 5) {
 #pragma unroll
-            for (int k = 0; k < 5; ++k) dring[k] = b.st[(QS_F_DRING + k) * kp.I + g];
+            for (int k = 0; k < 5; ++k) dring[k] = stw[k];
         }
-        if (lead) {
 #pragma unroll
-            for (int k = 0; k < 3; ++k)
-                if (in_win[k]) dsum[k] = b.st[(QS_F_DSUM + k) * kp.I + g];
-        }
+        for (int k = 0; k < 3; ++k)
+            if (in_win[k]) dsum[k] = stw[5 + k];
     }
     int omi = 0, osi = 0;   // the env's domain-randomisation choice (QS_E_OBST_M / _SZ)
     if (OBST && kp.dr) { omi = b.env[QS_E_OBST_M * kp.E + eidx]; osi = b.env[QS_E_OBST_SZ * kp.E + eidx]; }
@@ -1247,15 +1282,23 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
         const bool on_floor = d.flags & QS_FL_ON_FLOOR;
         floor_now = on_floor;
         const float dist = fsqrt(gx * gx + gy * gy + gz * gz);
-        if (kp.stats && lead) {   // distance_to_goal[i].append(-rewraw_pos) and reached_goal (:651-655)
+#ifdef QS_DIAG_NOST_RING   // diagnostic builds only (QS_JIT_OPTS)
+        if (false) {
+#else
+        if (kp.stats && active) {   // distance_to_goal[i].append(-rewraw_pos) and reached_goal (:651-655)
+#endif
+            // every sub-lane (the flags stay identical); the words reach HBM with the state's store burst
             const float v = kp.dt * dist;
             const int slot = tick % 5;
-            b.st[(QS_F_DRING + slot) * kp.I + g] = v;
+#pragma unroll
+            for (int k = 0; k < 5; ++k) stw[k] = k == slot ? v : stw[k];
+            stmask = 1u << slot;
 #pragma unroll
             for (int k = 0; k < 3; ++k)
                 if (in_win[k]) {
                     dsum[k] += v;
-                    b.st[(QS_F_DSUM + k) * kp.I + g] = dsum[k];
+                    stw[5 + k] = dsum[k];
+                    stmask |= 1u << (5 + k);
                 }
             if (!(d.flags & QS_FL_REACHED) && tick >= 5) {
                 float m = 0.f;
@@ -1334,7 +1377,11 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     }
     bool any_onew = false;   // curr_quad_col non-empty (quadrotor_multi.py:576)
     if (OBST) any_onew = ((__ballot(onew && q == 0) >> lbase) & lmask) != 0;
+#ifdef QS_DIAG_NOST_COUNT
+    if (false) {
+#else
     if (kp.stats) {   // episode_extra_stats counters (quadrotor_multi.py:555-566, 575-589, 599-606, 631-635)
+#endif
         auto env_count = [&](bool x) { return __popcll((__ballot(x && q == 0) >> lbase) & lmask); };
         const bool settle = tick >= kp.st_settle;
         const int col = env_count(uniq) / 2;   // len(last_step_unique_collisions) // 2
@@ -1365,25 +1412,19 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
             o5 = env_count(f5);
         }
         const bool fin5 = kpm.ep_len - tick0 <= kp.st_final;   // time_remain <= collisions_final_grace_period_steps
-        if (active && di == 0 && q == 0 && (col | nr | nfl | nw | nc | oc) != 0) {   // the env's lead lane
-            int32_t* ev = b.env + env;
-            const int E = kp.E;
-            ev[QS_E_ST_COL * E] += col;
-            if (col > 0 && settle) ev[QS_E_ST_COL_SETTLE * E] += col;
-            if (col > 0 && fin5) ev[QS_E_ST_COL_FINAL * E] += col;
-            if (settle) {
-                ev[QS_E_ST_ROOM * E] += nr;
-                ev[QS_E_ST_FLOOR * E] += nfl;
-                ev[QS_E_ST_WALL * E] += nw;
-                ev[QS_E_ST_CEIL * E] += nc;
-            }
-            if (OBST) {
-                ev[QS_E_ST_OCOL * E] += oc;
-                if (oc > 0 && settle) {
-                    ev[QS_E_ST_OCOL_SETTLE * E] += oc;
-                    ev[QS_E_ST_O35 * E] += o35;
-                    ev[QS_E_ST_O5 * E] += o5;
-                }
+        // counter QS_E_ST_COL + k lives on lane k (mod LPE) of the env: it adds its own increment (env-uniform
+        // values from the ballots) and stores only when that changed it
+#pragma unroll
+        for (int t = 0; t < CT; ++t) {
+            const int k = li + LPE * t;
+            const bool os = OBST && oc > 0 && settle;
+            const int inc = k == 0 ? col : k == 1 ? (settle ? nr : 0) : k == 2 ? (settle ? nfl : 0) :
+                            k == 3 ? (settle ? nw : 0) : k == 4 ? (settle ? nc : 0) :
+                            k == 5 ? (settle ? col : 0) : k == 6 ? (fin5 ? col : 0) : k == 7 ? oc :
+                            k == 8 ? (os ? oc : 0) : k == 9 ? (os ? o35 : 0) : k == 10 ? (os ? o5 : 0) : 0;
+            if (envok && k < NCNT && inc != 0) {
+                cnt[t] += inc;
+                b.env[(QS_E_ST_COL + k) * kp.E + env] = cnt[t];
             }
         }
     }
@@ -1557,9 +1598,13 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     // lets its write-through bytes drain while the observations are computed.
 #if defined(QS_DIAG_NOSTORE)
 #elif QS_COOP_STATE
-    store_drone_q<Q>(kp, b, g, q, active, d);
+    if (kp.stats) store_drone_q<Q, true>(kp, b, g, q, active, d, stw, stmask);
+    else store_drone_q<Q>(kp, b, g, q, active, d);
 #else
     if (lead) store_drone(kp, b, g, d);
+    if (lead)
+        for (int k = 0; k < STAT_WORDS; ++k)
+            if ((stmask >> k) & 1u) b.st[(QS_F_DRING + k) * kp.I + g] = stw[k];
 #endif
     if (lead) {
         b.rew[g] = rw;
@@ -1614,10 +1659,10 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
         }
         lds_sync();
         if (kp.stats) {   // the finished episode's episode_extra_stats rows (quadrotor_multi.py:739-831)
-            // the env's counters were just updated by its lead lane: a workgroup-scope release / acquire (one
-            // wave per workgroup) before the other lanes read them back
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            // the env's counters from the lanes that hold them (every lane takes part in the permutes)
+            float cv[NCNT];
+#pragma unroll
+            for (int k = 0; k < NCNT; ++k) cv[k] = (float)__shfl(cnt[k / LPE], lbase + k % LPE);
             auto env_bits = [&](bool x) { return (__ballot(x && q == 0) >> lbase) & lmask; };
             const uint64_t hit_a = env_bits(active && (d.flags & QS_FL_HIT_AGENT));
             const uint64_t hit_o = env_bits(active && (d.flags & QS_FL_HIT_OBST));
@@ -1627,9 +1672,9 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
                 const float n = (float)kp.N;
                 const uint64_t ok = all & ~hit_a & ~hit_o;   // logical_and(agent_col_agent, agent_col_obst)
                 float* row = b.estats + (size_t)g * QS_NES;
-                const int32_t* ev = b.env + env;
                 const int E = kp.E;
-                for (int k = 0; k < 11; ++k) row[QS_ES_COL + k] = (float)ev[(QS_E_ST_COL + k) * E];
+#pragma unroll
+                for (int k = 0; k < NCNT; ++k) row[QS_ES_COL + k] = cv[k];
                 row[QS_ES_SUCCESS] = (float)__popcll(ok & reach) / n;
                 row[QS_ES_DEADLOCK] = (float)__popcll(ok & ~reach) / n;
                 row[QS_ES_COLRATE] = 1.f - (float)__popcll(ok) / n;
@@ -1640,17 +1685,14 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
 #pragma unroll
                 for (int k = 0; k < 3; ++k) row[QS_ES_D1 + k] = dsum[k] / (float)min(kp.st_win[k], T) / kp.dt;
                 row[QS_ES_REPLAY] = (r.ri != nullptr && r.ri[QS_R_SAVED * E + env]) ? 1.f : 0.f;
-                // QuadrotorEnvMulti.reset zeroes the statistics (:487-509): the drone's entries here, the env's
-                // counters by its lead lane
-#pragma unroll
-                for (int k = 0; k < 5; ++k) b.st[(QS_F_DRING + k) * kp.I + g] = 0.f;
-#pragma unroll
-                for (int k = 0; k < 3; ++k) b.st[(QS_F_DSUM + k) * kp.I + g] = 0.f;
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            if (active && done && di == 0 && q == 0)
-                for (int k = 0; k < 11; ++k) b.env[(QS_E_ST_COL + k) * kp.E + env] = 0;
+            // QuadrotorEnvMulti.reset zeroes the statistics (:487-509): the drone's entries go out with the reset
+            // drone's state store below, the env's counters from the lanes that hold them
+#pragma unroll
+            for (int t = 0; t < CT; ++t) {
+                const int k = li + LPE * t;
+                if (envok && done && k < NCNT) b.env[(QS_E_ST_COL + k) * kp.E + env] = 0;
+            }
         }
         float sv[3] = {d.vel[0], d.vel[1], d.vel[2]};  // QuadrotorEnvMulti.vel seen by the reset (:477)
         if (OBST) {   // new obstacle map + scenario per finished env (one lane each)
@@ -1697,9 +1739,18 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
         }
         // the reset drones' state (the stepped state was stored before the obs phase)
 #if QS_COOP_STATE
-        store_drone_q<Q>(kp, b, g, q, active && done, d);
+        if (kp.stats) {
+            const float zero[STAT_WORDS] = {};
+            store_drone_q<Q, true>(kp, b, g, q, active && done, d, zero, (1u << STAT_WORDS) - 1u);
+        } else {
+            store_drone_q<Q>(kp, b, g, q, active && done, d);
+        }
 #else
-        if (lead && done) store_drone(kp, b, g, d);
+        if (lead && done) {
+            store_drone(kp, b, g, d);
+            if (kp.stats)
+                for (int k = 0; k < STAT_WORDS; ++k) b.st[(QS_F_DRING + k) * kp.I + g] = 0.f;
+        }
 #endif
         if (nbr) {
             if (q == 0) xch_put(xch, dbase + di, d.pos, sv);

@@ -114,7 +114,9 @@ def test_one_step_from_identical_state(N, K, dw, rep):
         np.testing.assert_allclose(g_rew, w_rew, atol=2e-4, rtol=1e-4)
         _close_rows(g_rew, w_rew, quiet, f"step {t} quiet rew", **QUIET_STATE)
         assert_obs_match(g_obs, w_obs, oenv, so, cfg.k_neighbors)
-        _close_rows(g_obs[:, :so], w_obs[:, :so], quiet, f"step {t} quiet self obs", **QUIET_OBS)
+        oc = np.r_[0:15, 18:so]        # the omega columns (15:18) carry omega's absolute bound
+        _close_rows(g_obs[:, oc], w_obs[:, oc], quiet, f"step {t} quiet self obs", **QUIET_OBS)
+        _close_rows(g_obs[:, 15:18], w_obs[:, 15:18], quiet, f"step {t} quiet obs omega", **QUIET_OMEGA)
         if rep.endswith("wall"):    # the six wall distances saw contacts (clipped at 0) this step
             stats["wall"] += int((w_obs[:, 18:24] == 0).any(1).sum())
         if w_done.any():

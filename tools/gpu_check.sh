@@ -23,6 +23,23 @@ for s in "$@"; do
     testsnew) step gpu_tests_new 600 python -u -m pytest tests/test_gpu_stats.py tests/test_gpu_guard_params.py tests/test_gpu_c5.py -v --timeout 200 --timeout-method thread ;;
     testspar) step gpu_tests_par 900 python -u -m pytest tests/test_gpu_stats.py tests/test_gpu_parity.py tests/test_gpu_parity_a.py -v --timeout 300 --timeout-method thread ;;
     benchdrv) step bench_driver 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    benchwarm)
+      step bw_20_5 200 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --e2e-iters 0
+      step bw_20_500 200 python bench.py --steps 20 --warmup 500 --no-cpu-baseline --e2e-iters 0
+      step bw_2000 200 python bench.py --steps 2000 --warmup 50 --no-cpu-baseline --e2e-iters 0
+      ;;
+    benchst)
+      step bst_on 200 python bench.py --steps 2000 --warmup 50 --no-cpu-baseline --e2e-iters 0
+      step bst_off 200 python bench.py --steps 2000 --warmup 50 --no-cpu-baseline --e2e-iters 0 --no-episode-stats
+      ;;
+    ktst)
+      export TMPDIR=/tmp
+      step kt_on 300 rocprofv3 --kernel-trace -d gpurun_out/kt_on -o kt --output-format csv -- python bench.py --steps 200 --warmup 10 --no-cpu-baseline --e2e-iters 0
+      step kt_off 300 rocprofv3 --kernel-trace -d gpurun_out/kt_off -o kt --output-format csv -- python bench.py --steps 200 --warmup 10 --no-cpu-baseline --e2e-iters 0 --no-episode-stats
+      python tools/kt_summary.py gpurun_out/kt_on gpurun_out/kt_off > gpurun_out/kt_summary.txt 2>&1
+      rm -f gpurun_out/kt_*/*/*kernel_trace.csv gpurun_out/kt_*/*kernel_trace.csv
+      ;;
+    par64) step gpu_tests_64 600 python -u -m pytest tests/test_gpu_parity.py -v -k "64" --timeout 300 --timeout-method thread ;;
     benchblocks) step bench_blocks 600 python bench.py --steps 2000 --streams 4 --no-cpu-baseline --e2e-iters 0 ;;
     bench) step bench 600 python bench.py ;;
     ppotests) step ppo_tests 600 python -m pytest tests/test_gpu_ppo.py -q -x ;;
