@@ -1178,15 +1178,23 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     const int eidx = active ? env : 0;
     const int tick0 = b.env[QS_E_TICK * kp.E + eidx];
     const int episode = b.env[QS_E_EPISODE * kp.E + eidx];
+#ifndef QS_DIAG_LATE_EF
+    const int32_t ef0 = b.env[QS_E_FLAGS * kp.E + eidx];   // the env's flags (rewritten at the end of the step)
+#endif
     // episode_extra_stats: the env's 11 counters QS_E_ST_COL.. dealt over its lanes (lane li holds li + LPE t)
     constexpr int NCNT = 11, CT = (NCNT + LPE - 1) / LPE;
     const int li = lane - lbase;
     const bool envok = env < kp.E;
     int cnt[CT];
+#ifdef QS_DIAG_CNT_AOS   // diagnostic builds only: the counters env-major in the estats rows (layout experiment)
+    auto cnt_at = [&](int k) -> int32_t* { return reinterpret_cast<int32_t*>(b.estats) + (size_t)env * kp.N * QS_NES + k; };
+#else
+    auto cnt_at = [&](int k) -> int32_t* { return b.env + (QS_E_ST_COL + k) * kp.E + env; };
+#endif
 #pragma unroll
     for (int t = 0; t < CT; ++t) {
         const int k = li + LPE * t;
-        cnt[t] = (kp.stats && envok && k < NCNT) ? b.env[(QS_E_ST_COL + k) * kp.E + env] : 0;
+        cnt[t] = (kp.stats && envok && k < NCNT) ? *cnt_at(k) : 0;
     }
     Drone d;   // every sub-lane holds the whole drone
 #if defined(QS_DIAG_NOLOAD)   // diagnostic builds only (QS_JIT_OPTS): phase-removal timing experiments
@@ -1301,12 +1309,10 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
                     stmask |= 1u << (5 + k);
                 }
             if (!(d.flags & QS_FL_REACHED) && tick >= 5) {
+                // the last 5 entries are the whole ring (this step's in its slot), summed in slot order
                 float m = 0.f;
 #pragma unroll
-                for (int j = 4; j >= 0; --j) {   // the last 5 entries, oldest first
-                    const int sl = (tick - j) % 5;
-                    m += sl == slot ? v : (sl == 0 ? dring[0] : sl == 1 ? dring[1] : sl == 2 ? dring[2] : sl == 3 ? dring[3] : dring[4]);
-                }
+                for (int k = 0; k < 5; ++k) m += k == slot ? v : dring[k];
                 if (m / 5.f / kp.dt < 0.5f) d.flags |= QS_FL_REACHED;   // approch_goal_metric
             }
         }
@@ -1422,9 +1428,13 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
                             k == 3 ? (settle ? nw : 0) : k == 4 ? (settle ? nc : 0) :
                             k == 5 ? (settle ? col : 0) : k == 6 ? (fin5 ? col : 0) : k == 7 ? oc :
                             k == 8 ? (os ? oc : 0) : k == 9 ? (os ? o35 : 0) : k == 10 ? (os ? o5 : 0) : 0;
+#ifdef QS_DIAG_NOST_CSTORE
+            if (false) {
+#else
             if (envok && k < NCNT && inc != 0) {
+#endif
                 cnt[t] += inc;
-                b.env[(QS_E_ST_COL + k) * kp.E + env] = cnt[t];
+                *cnt_at(k) = cnt[t];
             }
         }
     }
@@ -1598,6 +1608,9 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     // lets its write-through bytes drain while the observations are computed.
 #if defined(QS_DIAG_NOSTORE)
 #elif QS_COOP_STATE
+#ifdef QS_DIAG_NOST_RSTORE
+    stmask = 0u;
+#endif
     if (kp.stats) store_drone_q<Q, true>(kp, b, g, q, active, d, stw, stmask);
     else store_drone_q<Q>(kp, b, g, q, active, d);
 #else
@@ -1776,7 +1789,11 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
         if (di == 0) {
             b.env[QS_E_TICK * kp.E + env] = done ? 0 : tick;
             if (done) b.env[QS_E_EPISODE * kp.E + env] = episode + 1;
+#ifdef QS_DIAG_LATE_EF
             const int32_t ef = b.env[QS_E_FLAGS * kp.E + env];
+#else
+            const int32_t ef = ef0;
+#endif
             int32_t nf = done ? (ef | QS_EF_STALE) : (ef & ~QS_EF_STALE);
             // what the replay wrapper reads of this step (quad_experience_replay.py:161-163, quadrotor_multi.py:725)
             nf = (nf & ~(QS_EF_NEWCOL | QS_EF_FLOOR0)) | ((any_uniq || any_onew) ? QS_EF_NEWCOL : 0) |
