@@ -572,7 +572,7 @@ void or_collide_ceiling(or_drone* d, or_rng* r, uint32_t gid) {
 /* perform_downwash (aerodynamics/downwash.py:4-51) + get_vel_omega_norm (:54-66).
  * Philox: key = source drone i; OR_S_DW uniforms 0 acc noise, 1 omega noise;
  * OR_S_DWPAIR | j<<8 uniforms 0-2 z-axis noise, 3-5 omega direction. */
-static int downwash(const or_params* p, or_drone* dr, int N, uint32_t gbase, or_rng* r) {
+int or_downwash(const or_params* p, or_drone* dr, int N, uint32_t gbase, or_rng* r) {
     int applied = 0;
     double P[64][3];
     for (int i = 0; i < N; ++i) for (int c = 0; c < 3; ++c) P[i][c] = dr[i].pos[c];
@@ -1064,7 +1064,7 @@ void or_env_step(const or_params* p, or_drone* drones, or_env* envs, int e, cons
     }
     /* 3. random forces (quadrotor_multi.py:659-698) */
     int flag = 0;
-    if (p->use_downwash) flag |= downwash(p, dr, N, gbase, r);
+    if (p->use_downwash) flag |= or_downwash(p, dr, N, gbase, r);
     if (p->apply_collision_force) {
         for (int i = 0; i < N; ++i)
             for (int j = i + 1; j < N; ++j)

@@ -259,6 +259,7 @@ void or_collide_drones(double pos1[3], double vel1[3], double omega1[3],
                        double pos2[3], double vel2[3], double omega2[3],
                        or_rng* r, uint32_t gid, uint32_t j);
 void or_collide_wall(const or_params* p, or_drone* d, or_rng* r, uint32_t gid);
+int or_downwash(const or_params* p, or_drone* dr, int N, uint32_t gbase, or_rng* r);   /* 1 when applied */
 void or_collide_ceiling(or_drone* d, or_rng* r, uint32_t gid);
 
 /* ---- whole env (flavor B, QuadrotorEnvMulti quadrotor_multi.py) ---- */

@@ -643,7 +643,14 @@ void or_env_step_a(const or_params* p, or_drone* drones, or_env* envs, int e, co
             if (dn[i]) any_done = 1;
         }
         if (cap) ev->success = 1;
+        /* perform_downwash with the control dt (:810-815); when it touched a drone the reference rebuilds the
+         * tick's obs after scenario.step() (:848-859: state_vector, i.e. the moved goal and fresh sensor /
+         * camera noise) */
+        const int dw = p->use_downwash && N > 1 && or_downwash(p, dr, N, gbase, r);
         if (p->scenario_a == 1) or_target_step(p, ev, dr);   /* scenario.step() (:797) */
+        if (dw)
+            for (int i = 0; i < N; ++i)
+                or_self_obs_a(p, &dr[i], r, gbase + (uint32_t)i, OR_S_SENSOR, OR_S_SELF_CAM, o + (size_t)i * od);
         for (int i = 0; i < N; ++i)
             for (int c = 0; c < 3; ++c) { ev->obs_pos[i][c] = dr[i].pos[c]; ev->obs_vel[i][c] = dr[i].vel[c]; }
     }

@@ -6,6 +6,7 @@
 //                                                    Acceleration/Attitude/Rate controllers, Mixer, Pid.py)
 //         CustomPidControl.step + QuadrotorDynamics  quadrotor_control.py:90-94, quadrotor_dynamics.py:215-221
 //     capture reward / dones                         quadrotor_multi_rewards.py:711-735, 882-988
+//     perform_downwash per tick (use_downwash)       quadrotor_multi_rewards.py:810-815, aerodynamics/downwash.py
 //     Scenario_dynamic_repulsive.step / reset        scenarios/dynamic_repulsive.py:37-74 (float-fixed)
 //     neighbour obs + camera model                   quadrotor_multi_rewards.py:238-476
 //   SubprocVecEnvCustom worker reset on done         subproc_vec_env_custom.py:39-46 (reset_infos)
@@ -523,10 +524,20 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
         dn = cap ? capi : (tick > kpm.ep_len);
         fin = seg_any<LPE>(active && dn, base);
         success = success || cap;
+        // perform_downwash once per tick with the control dt (:810-815); the reference then rebuilds the
+        // tick's obs from the post-downwash state, which is what the final obs below read
+        bool dwa = false;
+        if (kp.downwash && kp.N > 1) dwa = downwash_env<NPAD, Q>(kp, d, rng, gid, env, base, di, q, active);
         if (repulsive) {   // scenario.step() (:797)
             target_step<NPAD, Q>(kp, tx, ty, d.pos, active);
             d.goal[0] = tx;
             d.goal[1] = ty;
+        }
+        // downwash anywhere in the env: the tick's obs are rebuilt after scenario.step (:848-859), i.e. they
+        // see the moved goal
+        if (kp.downwash && kp.N > 1 && seg_any<LPE>(active && dwa, base)) {
+            gox = d.goal[0];
+            goy = d.goal[1];
         }
     }
 

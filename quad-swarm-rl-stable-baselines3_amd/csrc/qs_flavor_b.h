@@ -1442,43 +1442,8 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     QS_STAMP(3);
     // ---- random forces (:659-698), replicated on the sub-lanes ----
     bool vchanged = false;
-    if (kp.downwash && kp.N > 1) {  // perform_downwash (aerodynamics/downwash.py:4-51)
-        float dwu[4];
-        uniforms4(rng, gid, S_DW, 0, dwu);
-        const float an = -0.1f + 0.2f * dwu[0], wn = -0.01f + 0.02f * dwu[1];
-        const float P0 = d.pos[0], P1 = d.pos[1], P2 = d.pos[2];
-        for (int i = 0; i < NPAD; ++i) {
-            const int src = lbase + i * Q + q;
-            const float zi0 = __shfl(d.rot[2], src), zi1 = __shfl(d.rot[5], src), zi2 = __shfl(d.rot[8], src);
-            const float pi0 = __shfl(P0, src), pi1 = __shfl(P1, src), pi2 = __shfl(P2, src);
-            const float ani = __shfl(an, src), wni = __shfl(wn, src);
-            if (!active || i >= kp.N || i == di) continue;
-            const float r0 = P0 - pi0, r1 = P1 - pi1, r2 = P2 - pi2;
-            const float dist = fsqrt(r0 * r0 + r1 * r1 + r2 * r2);
-            const float rz = r0 * zi0 + r1 * zi1 + r2 * zi2;
-            const float rxy = fsqrt(dist * dist - rz * rz);
-            if (-0.7f < rz && rz < 0.f && rxy < 0.1f) {
-                const float acc = fmaxf((6.f / 17.f) * (-10.f * dist + 7.f) + ani, 1e-6f);
-                const float wd = fmaxf(0.3f * (dist - 1.f) * (dist - 1.f) + wni, 1e-6f);
-                float u[8];
-                const uint32_t gi = kp.id0 + (uint32_t)(env * kp.N + i);
-                uniforms4(rng, gi, S_DWPAIR | ((uint32_t)di << 8), 0, u);
-                uniforms4(rng, gi, S_DWPAIR | ((uint32_t)di << 8), 1, u + 4);
-                float nz[3] = {zi0 - 0.1f + 0.2f * u[0], zi1 - 0.1f + 0.2f * u[1], zi2 - 0.1f + 0.2f * u[2]};
-                const float nm = fsqrt(nz[0] * nz[0] + nz[1] * nz[1] + nz[2] * nz[2]);
-                const float inz = frcp(nm == 0.f ? 1e-6f : nm);
-                float dw[3] = {-1.f + 2.f * u[3], -1.f + 2.f * u[4], -1.f + 2.f * u[5]};
-                const float dm = fsqrt(dw[0] * dw[0] + dw[1] * dw[1] + dw[2] * dw[2]);
-                const float idw = frcp(dm == 0.f ? 1e-6f : dm);
-#pragma unroll
-                for (int c = 0; c < 3; ++c) {
-                    d.vel[c] += acc * (-(nz[c] * inz)) * kp.cdt;
-                    d.om[c] += wd * (dw[c] * idw) * kp.cdt;
-                }
-                vchanged = true;
-            }
-        }
-    }
+    if (kp.downwash && kp.N > 1)   // perform_downwash (aerodynamics/downwash.py:4-51)
+        vchanged = downwash_env<NPAD, Q>(kp, d, rng, gid, env, lbase, di, q, active);
 #ifndef QS_DIAG_NOIMPULSE
     if (kp.collide) {
 #else

@@ -161,7 +161,6 @@ static int validate(const qs_config* c) {
         if (c->obs_repr < 3 || c->obs_repr > 6) return fail(QS_E_INVALID, "obs_repr is not a flavor-A repr");
         if (c->scenario != QS_SCEN_STATIC_SAME_GOAL && c->scenario != QS_SCEN_DYNAMIC_REPULSIVE)
             return fail(QS_E_INVALID, "unknown scenario");
-        if (c->use_downwash) return fail(QS_E_UNSUPPORTED, "flavor A with downwash is not implemented");
         if (c->ticks_per_step < 1) return fail(QS_E_INVALID, "ticks_per_step must be >= 1");
         if (c->n_cameras < 1) return fail(QS_E_INVALID, "n_cameras must be >= 1");
     }

@@ -254,8 +254,6 @@ class QuadSwarmConfig:
             if self.quads_mode not in ("dynamic_repulsive", "static_same_goal"):
                 raise NotImplementedError(f"quads_mode {self.quads_mode!r} not implemented for flavor A "
                                           "(dynamic_repulsive, static_same_goal)")
-            if self.use_downwash:
-                raise NotImplementedError("flavor A with downwash is not implemented")
         if self.replay_buffer_sample_prob > 0 and self.flavor != "B":
             raise NotImplementedError("experience replay is implemented for flavor B")
         if not 0.0 <= self.replay_buffer_sample_prob <= 1.0:

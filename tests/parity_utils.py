@@ -317,6 +317,7 @@ def oracle_params_a(cfg: QuadSwarmConfig):
     p.cam_size, p.cam_focal, p.cam_px_noise = cfg.neighbour_size_cam, cfg.focal_length_cam, cfg.pixel_noise_cam
     p.n_cameras = cfg.n_cameras
     p.control_dt = cfg.dt * cfg.sim_steps
+    p.use_downwash = int(bool(cfg.use_downwash))
     return p
 
 

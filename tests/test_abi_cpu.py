@@ -141,8 +141,7 @@ def test_flavor_b_goal_scenarios_accepted(mode):
     lay = N.QsLayout()
     assert N.lib().qs_layout_query(ctypes.byref(c), ctypes.byref(lay)) == 0
     assert lay.obs_dim == 54
-    with pytest.raises(NotImplementedError):
-        QuadSwarmConfig.sb_train(use_downwash=True).to_qs_config()
+    assert QuadSwarmConfig.sb_train(use_downwash=True).to_qs_config().use_downwash == 1   # flavor A: per tick
     with pytest.raises(NotImplementedError):
         QuadSwarmConfig.sb_train(neighbor_obs_type="pos_vel_R").to_qs_config()
 

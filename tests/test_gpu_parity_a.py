@@ -35,6 +35,8 @@ CONFIGS = {
     "n1": dict(num_agents=1, neighbor_obs_type="none"),
     "n32k6": dict(num_agents=32, neighbor_visible_num=6, neighbor_obs_type="dist_sangle"),
     "n64k6": dict(num_agents=64, neighbor_visible_num=6, neighbor_obs_type="dist_sangle"),
+    # use_downwash (quadrotor_multi_rewards.py:810-815): _perturb stacks the drones in vertical pairs
+    "dw8": dict(num_agents=8, neighbor_obs_type="dist_angle", use_downwash=True),
     "static4": dict(num_agents=4, quads_mode="static_same_goal", neighbor_obs_type="pos"),
 }
 
@@ -75,7 +77,16 @@ def test_reset_matches_oracle(name):
 
 def _perturb(oenv, cfg, rng, step):
     """Exercise every branch: per-env capture radii (immediate captures in some envs), envs whose
-    episode ends inside the 8-tick loop, random PID / heading states."""
+    episode ends inside the 8-tick loop, random PID / heading states; with downwash, drones stacked in
+    vertical pairs 0.2-0.5 m apart (inside perform_downwash's cone)."""
+    if cfg.use_downwash and step % 2 == 0:
+        for e in range(oenv.E):
+            for i in range(0, oenv.N - 1, 2):
+                lo, hi = oenv.drones[e * oenv.N + i], oenv.drones[e * oenv.N + i + 1]
+                gap = rng.uniform(0.2, 0.5)
+                for c in range(2):
+                    hi.pos[c] = lo.pos[c] + rng.uniform(-0.03, 0.03)
+                hi.pos[2] = lo.pos[2] + gap
     for e in range(oenv.E):
         ev = oenv.envs[e]
         ev.capture_radius = [0.3, 3.0, 1.2, 0.0][(e + step) % 4]
@@ -99,8 +110,18 @@ def test_one_step_from_identical_state(name):
         _perturb(oenv, cfg, rng, t)
         oracle_to_gpu_a(oenv, env)
         a = rng.uniform(-1.2, 1.2, (env.I, 2)).astype(np.float32)
+        if cfg.use_downwash and t == 0:   # the stacks do feel the downwash: a twin without it differs
+            p0 = oracle_params_a(cfg)
+            p0.use_downwash = 0
+            twin = O.OracleEnvA(p0, seed=11)
+            gpu_to_oracle_a(env, twin)
+            for e in range(env.E):
+                twin.envs[e].capture_radius = oenv.envs[e].capture_radius
+            no_dw = twin.step(a.astype(np.float64))[0]
         obs, rew, done, term = env.step(torch.from_numpy(a).cuda())
         w_obs, w_rew, w_done, w_term, w_ri = oenv.step(a.astype(np.float64))
+        if cfg.use_downwash and t == 0:
+            assert np.abs(no_dw - w_obs).max() > 1e-3
         np.testing.assert_array_equal(done.cpu().numpy().astype(bool), w_done, err_msg=f"done step {t}")
         np.testing.assert_array_equal(env.reset_info.cpu().numpy(), w_ri, err_msg=f"reset_info step {t}")
         np.testing.assert_allclose(np_(rew), w_rew, atol=1e-5, err_msg=f"rew step {t}")

@@ -136,6 +136,7 @@ def load_traj_a(golden, name, which="init"):
     p.sense_noise = int(g["sense"])
     p.ou_sigma = 0.2 * float(g["thrust_noise"])
     p.cam_px_noise = float(g["px_noise"])
+    p.use_downwash = int(name.endswith("dw"))     # use_downwash (quadrotor_multi_rewards.py:810-815)
     drones = O.drones_array(n)
     envs = O.envs_array(1)
     w = which + "_"
@@ -159,10 +160,10 @@ def load_traj_a(golden, name, which="init"):
     return g, p, drones, envs
 
 
-TRAJ = ["n4", "n8", "n8k3cam", "n1", "n4quiet"]
+TRAJ = ["n4", "n8", "n8k3cam", "n1", "n4quiet", "n8dw"]
 
 
-@pytest.mark.parametrize("name", TRAJ)
+@pytest.mark.parametrize("name", [t for t in TRAJ if t != "n8dw"])   # n8dw: stacked by hand after the reset
 def test_first_reset_tape_replay(golden, name):
     """QuadrotorEnvMulti.reset from construction (no dynamics.pos yet: no chaser force, :38)."""
     g, p, _, _ = load_traj_a(golden, name)

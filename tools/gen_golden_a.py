@@ -80,8 +80,9 @@ def end():
 
 
 def make_env_A(n, k=-1, repr_="cdist_cdistdot_dist_distdot_sangle_angledot", ntype="ndist_nsangle",
-               px_noise=0.0, ep_time=30.0, sense="default", thrust_noise=None, seed=0, capture=3.0):
+               px_noise=0.0, ep_time=30.0, sense="default", thrust_noise=None, seed=0, capture=3.0, downwash=False):
     cfg = QuadrotorEnvConfig()
+    cfg.use_downwash = downwash
     cfg.num_agents = n
     cfg.neighbor_visible_num = k
     cfg.obs_repr = repr_
@@ -260,12 +261,14 @@ def snapshot(env):
         capture=np.array(float(env.capture_radius)))
 
 
-def gen_traj(name, n, steps, seed, capture_schedule=None, act_scale=1.0, **kw):
+def gen_traj(name, n, steps, seed, capture_schedule=None, act_scale=1.0, setup=None, **kw):
     np.random.seed(seed)
     env = make_env_A(n, seed=seed, **kw)
     begin()
     obs0, info0 = env.reset()
     tv0, gt0 = end()
+    if setup is not None:   # state edits after the reset (the replayed steps start from the snapshot below)
+        setup(env)
     init = snapshot(env)
     act_rng = np.random.default_rng(seed + 200)
     actions = act_rng.uniform(-1.0, 1.0, (steps, n, 2)) * act_scale
@@ -322,5 +325,29 @@ def main():
             print(f, os.path.getsize(os.path.join(OUT, f)))
 
 
+def setup_stacks_a(env):
+    """Drones in vertical pairs (0.3 m apart, same xy): perform_downwash's cone (downwash.py:23-49)."""
+    for i, e in enumerate(env.envs):
+        d = e.dynamics
+        col = i // 2
+        d.pos = np.array([-1.5 + col * 1.0, 0.5, 1.2 + 0.3 * (i % 2)])
+        d.vel = np.zeros(3)
+        d.rot = np.eye(3)
+        d.omega = np.zeros(3)
+        env.pos[i] = d.pos
+
+
+def main_extra(which):
+    """Fixtures added later, generated on their own (the ones above stay byte-identical):
+      dw   use_downwash (quadrotor_multi_rewards.py:810-815) with stacked drone pairs, 8 drones"""
+    os.makedirs(OUT, exist_ok=True)
+    if "dw" in which:
+        gen_traj("n8dw", 8, 40, seed=36, ntype="dist_angle", repr_="cdist_cdistdot_dist_distdot_angle_angledot",
+                 capture_schedule=lambda t: 0.05, ep_time=30.0, downwash=True, setup=setup_stacks_a)
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1:
+        main_extra(sys.argv[1:])
+    else:
+        main()
