@@ -79,13 +79,19 @@ def _perturb(oenv, cfg, rng, step):
     """Exercise every branch: per-env capture radii (immediate captures in some envs), envs whose
     episode ends inside the 8-tick loop, random PID / heading states; with downwash, drones stacked in
     vertical pairs 0.2-0.5 m apart (inside perform_downwash's cone)."""
-    if cfg.use_downwash and step % 2 == 0:
+    if cfg.use_downwash:
         for e in range(oenv.E):
             for i in range(0, oenv.N - 1, 2):
                 lo, hi = oenv.drones[e * oenv.N + i], oenv.drones[e * oenv.N + i + 1]
+                # pairs 0.8 m apart (no accidental cones between pairs: drones at one height sit on the
+                # cone's rz = 0 edge, where fp32 and fp64 may decide differently)
+                lo.pos[0], lo.pos[1] = -1.2 + 0.8 * (i // 2), 0.3
                 gap = rng.uniform(0.2, 0.5)
-                for c in range(2):
-                    hi.pos[c] = lo.pos[c] + rng.uniform(-0.03, 0.03)
+                # 4-8 cm sideways: inside the 0.1 m cone, yet far enough that the pair's angle feature stays
+                # well conditioned after 8 fp32 ticks (atan2 of a mm-scale offset would not be)
+                r, phi = rng.uniform(0.04, 0.08), rng.uniform(-np.pi, np.pi)
+                hi.pos[0] = lo.pos[0] + r * np.cos(phi)
+                hi.pos[1] = lo.pos[1] + r * np.sin(phi)
                 hi.pos[2] = lo.pos[2] + gap
     for e in range(oenv.E):
         ev = oenv.envs[e]
@@ -134,7 +140,10 @@ def test_one_step_from_identical_state(name):
         f = env.drone_fields()
         np.testing.assert_allclose(np_(f["pos"]), ostate(oenv, "pos"), atol=3e-5, err_msg=f"pos step {t}")
         np.testing.assert_allclose(np_(f["vel"]), ostate(oenv, "vel"), atol=5e-4, rtol=1e-3, err_msg=f"vel step {t}")
-        np.testing.assert_allclose(np_(f["pid"]), ostate(oenv, "pid"), atol=2e-3, rtol=2e-3, err_msg=f"pid step {t}")
+        # the PID's derivative terms divide step-to-step error changes by the tick (x100); the downwash case
+        # re-stacks its pairs every step, i.e. makes those changes large
+        pid_tol = 5e-3 if cfg.use_downwash else 2e-3
+        np.testing.assert_allclose(np_(f["pid"]), ostate(oenv, "pid"), atol=pid_tol, rtol=2e-3, err_msg=f"pid step {t}")
         tgt = np_(env.env_f[:2]).T
         # the target's flee direction is ill-conditioned where chaser and arena forces nearly cancel
         np.testing.assert_allclose(tgt, [list(oenv.envs[e].target) for e in range(env.E)], atol=2e-4)
