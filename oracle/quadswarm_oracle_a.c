@@ -555,8 +555,18 @@ void or_env_reset_a(const or_params* p, or_drone* drones, or_env* envs, int e, o
         or_target_step(p, ev, dr);
         for (int i = 0; i < N; ++i) { dr[i].pos[0] = sp[i][0]; dr[i].pos[1] = sp[i][1]; }
     } else {   /* static_same_goal: goals at the formation centre (size 0), spawn_points None -> spawn at the goal */
+        double goal[64][3];
+        if (p->scenario_b != OR_SC_NONE) {   /* any other create_scenario goal scenario (:123, :560) */
+            or_sdraw sd;
+            memset(&sd, 0, sizeof sd);
+            sd.mode = OR_RNG_PHILOX; sd.seed = r->seed; sd.key = gbase; sd.stream = OR_S_SCN_RESET; sd.step = r->step;
+            or_scen_reset(p, &ev->scen, &sd, goal);
+        } else {
+            for (int i = 0; i < N; ++i)
+                for (int c = 0; c < 3; ++c) goal[i][c] = p->goal[c];
+        }
         for (int i = 0; i < N; ++i) {
-            for (int c = 0; c < 3; ++c) dr[i].goal[c] = p->goal[c];
+            for (int c = 0; c < 3; ++c) dr[i].goal[c] = goal[i][c];
             dr[i].pos[0] = dr[i].goal[0];
             dr[i].pos[1] = dr[i].goal[1];
         }
@@ -647,7 +657,17 @@ void or_env_step_a(const or_params* p, or_drone* drones, or_env* envs, int e, co
          * tick's obs after scenario.step() (:848-859: state_vector, i.e. the moved goal and fresh sensor /
          * camera noise) */
         const int dw = p->use_downwash && N > 1 && or_downwash(p, dr, N, gbase, r);
-        if (p->scenario_a == 1) or_target_step(p, ev, dr);   /* scenario.step() (:797) */
+        if (p->scenario_a == 1) {
+            or_target_step(p, ev, dr);   /* scenario.step() (:797) */
+        } else if (p->scenario_b != OR_SC_NONE) {   /* a goal scenario's step, every tick (:848) */
+            or_sdraw sd;
+            memset(&sd, 0, sizeof sd);
+            sd.mode = OR_RNG_PHILOX; sd.seed = r->seed; sd.key = gbase; sd.stream = OR_S_SCN; sd.step = r->step;
+            double g[64][3];
+            for (int i = 0; i < N; ++i) memcpy(g[i], dr[i].goal, sizeof g[i]);
+            or_scen_step(p, &ev->scen, ev->tick, &sd, g);
+            for (int i = 0; i < N; ++i) memcpy(dr[i].goal, g[i], sizeof g[i]);
+        }
         if (dw)
             for (int i = 0; i < N; ++i)
                 or_self_obs_a(p, &dr[i], r, gbase + (uint32_t)i, OR_S_SENSOR, OR_S_SELF_CAM, o + (size_t)i * od);

@@ -8,6 +8,7 @@
 //     capture reward / dones                         quadrotor_multi_rewards.py:711-735, 882-988
 //     perform_downwash per tick (use_downwash)       quadrotor_multi_rewards.py:810-815, aerodynamics/downwash.py
 //     Scenario_dynamic_repulsive.step / reset        scenarios/dynamic_repulsive.py:37-74 (float-fixed)
+//     any other quads_mode: create_scenario (:123)   the goal scenarios of qs_scen.h, step per tick (:848)
 //     neighbour obs + camera model                   quadrotor_multi_rewards.py:238-476
 //   SubprocVecEnvCustom worker reset on done         subproc_vec_env_custom.py:39-46 (reset_infos)
 //
@@ -18,6 +19,7 @@
 // two segment ballots (capture, done); neighbour features read an LDS exchange tile once per step.
 #pragma once
 #include "qs_common.h"
+#include "qs_scen.h"
 
 namespace qs {
 
@@ -394,8 +396,8 @@ __device__ __forceinline__ void reset_env_a(const KP& kp, Drone& d, Ctl& c, floa
             d.pos[0] = sa * isn * rad;
             d.pos[1] = sb * isn * rad;
         }
-    } else if (sel) {
-        d.goal[0] = kp.goal[0]; d.goal[1] = kp.goal[1]; d.goal[2] = kp.goal[2];
+    } else if (sel) {   // static_same_goal, or a goal scenario (goal from scen_reset_a): spawn at the goal
+        if (kp.scen_b < 0) { d.goal[0] = kp.goal[0]; d.goal[1] = kp.goal[1]; d.goal[2] = kp.goal[2]; }
         d.pos[0] = d.goal[0];
         d.pos[1] = d.goal[1];
     }
@@ -414,6 +416,24 @@ __device__ __forceinline__ void reset_env_a(const KP& kp, Drone& d, Ctl& c, floa
 #pragma unroll
     for (int k = 0; k < 4; ++k) { d.rd[k] = 0.f; d.cd[k] = 0.f; }
     d.flags = 0;
+}
+
+// scenario.reset() of the selected envs for the goal scenarios (:560, spawn_points None -> spawn at the
+// goal, :569-573): the env's lead lane fills the LDS goal table (draw key = the env's drone 0, stream
+// S_SCN_RESET) and stores the scenario state; every selected drone takes its goal.  Whole wave.
+template <int NPAD>
+__device__ __forceinline__ void scen_reset_a(const KP& kp, const Bufs& b, float* stab, int env, int di, bool lead_sel,
+                                             bool sel, const Rng& rng, uint32_t genv, Drone& d) {
+    if (lead_sel) {
+        Scen sc;
+        SDraw sd = sdraw(rng, genv, S_SCN_RESET);
+        scen_reset(kp, sc, sd, stab, stab + 4 * (NPAD + 4));
+        scen_store(kp, b, env, sc);
+    }
+    lds_sync();
+    if (sel)
+        for (int k = 0; k < 3; ++k) d.goal[k] = stab[4 * di + k];
+    lds_sync();
 }
 
 // Step geometry of flavor A: Q sub-lanes per drone (QS_QA, 2 by default; 64 / NPAD when an env would
@@ -480,6 +500,10 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
     float tx = b.envf[QS_ENVF_TARGET_X * kp.E + eidx], ty = b.envf[QS_ENVF_TARGET_Y * kp.E + eidx];
     const float capr = b.envf[QS_ENVF_CAPTURE * kp.E + eidx];
     const bool repulsive = kp.scenario == QS_SCEN_DYNAMIC_REPULSIVE;
+    const bool SCEN = kp.scen_b >= 0;   // a goal scenario of create_scenario: its state lives in the lead lane
+    float* stab = scen_tab(lds, kp, SLOTS) + el * scen_stride<NPAD>();
+    Scen sc;
+    if (SCEN && active && di == 0 && q == 0) scen_load(kp, b, env, sc);
 
     bool fin = false, success = eflags & QS_EF_SUCCESS;
     float rw = 0.f, gox = d.goal[0], goy = d.goal[1];
@@ -532,6 +556,17 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
             target_step<NPAD, Q>(kp, tx, ty, d.pos, active);
             d.goal[0] = tx;
             d.goal[1] = ty;
+        } else if (SCEN) {   // scenario.step() of a goal scenario (:848): the env's goal table in LDS
+            if (active && q == 0)
+                for (int k = 0; k < 3; ++k) stab[4 * di + k] = d.goal[k];
+            lds_sync();
+            if (active && di == 0 && q == 0) {
+                SDraw sd = sdraw(rng, gid, S_SCN);
+                scen_step(kp, sc, tick, sd, stab, stab + 4 * (NPAD + 4));
+            }
+            lds_sync();
+            if (active)
+                for (int k = 0; k < 3; ++k) d.goal[k] = stab[4 * di + k];
         }
         // downwash anywhere in the env: the tick's obs are rebuilt after scenario.step (:848-859), i.e. they
         // see the moved goal
@@ -541,6 +576,7 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
         }
     }
 
+    if (SCEN && active && di == 0 && q == 0 && !fin) scen_store(kp, b, env, sc);   // (a reset stores its own)
     // ---- observations of the final tick (self obs of the last _step, neighbours after the loop) ----
     const Rng rng_last = env_rng(seed, tick - 1, episode);
     if (q == 0) xch_put_a(xch, sbase + di, d.pos, c.angle, d.vel);
@@ -563,6 +599,9 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
         lds_sync();
         const float sh = c.angle, sv[3] = {d.vel[0], d.vel[1], d.vel[2]};  // QuadrotorEnvMulti.heading / .vel
         const Rng rr = env_rng(seed, tick, episode);
+        if (SCEN)
+            scen_reset_a<NPAD>(kp, b, stab, env, di, active && fin && di == 0 && q == 0, active && fin, rr,
+                               kp.id0 + (uint32_t)(env * kp.N), d);
         reset_env_a<NPAD, Q>(kp, d, c, tx, ty, true, active, active && fin, rr, gid, kp.id0 + (uint32_t)(env * kp.N));
         if (lead && fin) {
             self_obs_a(kp, d, c, d.goal[0], d.goal[1], rr, gid, S_RESET_SENSOR, S_RESET_SELF_CAM, row);
@@ -633,6 +672,9 @@ __global__ __launch_bounds__(64) void reset_kernel_a(const KP* __restrict__ kpp,
 #pragma unroll
     for (int q = 0; q < 3; ++q) sv[q] = stale_valid ? b.stale[q * kp.I + g] : d.vel[q];
     const bool success = eflags & QS_EF_SUCCESS;
+    if (kp.scen_b >= 0)
+        scen_reset_a<NPAD>(kp, b, scen_tab(lds, kp, 64) + el * scen_stride<NPAD>(), env, di, sel && di == 0, sel, rng,
+                           kp.id0 + (uint32_t)(env * kp.N), d);
     reset_env_a<NPAD>(kp, d, c, tx, ty, eflags & QS_EF_HAS_POS, inr, sel, rng, gid, kp.id0 + (uint32_t)(env * kp.N));
     if (sel) self_obs_a(kp, d, c, d.goal[0], d.goal[1], rng, gid, S_RESET_SENSOR, S_RESET_SELF_CAM, row);
     if (kp.K > 0) {

@@ -2,6 +2,7 @@
 // rewards, drone/room impulses, pos_vel neighbour obs, in-env auto-reset).  Included by qs_step.hip.
 #pragma once
 #include "qs_common.h"
+#include "qs_scen.h"
 #include "qs_replay.h"
 
 namespace qs {
@@ -339,13 +340,6 @@ __device__ __forceinline__ float2 cell_xy(int cell, int n) {
     return make_float2((float)col + 0.5f - h, (float)(n - 1 - row) + 0.5f - h);
 }
 
-__device__ __forceinline__ uint32_t ubits(const Rng& r, uint32_t id, uint32_t st, uint32_t idx) {
-    return word_of(block(r, id, st | UNIF_BIT, idx >> 2), idx & 3);
-}
-// floor(u * m) exactly for u = ((w >> 8) + 0.5) / 2^24 (the oracle evaluates it in double, exactly)
-__device__ __forceinline__ int ufloor(uint32_t w, int m) {
-    return (int)((((uint64_t)(w >> 8) * 2u + 1u) * (uint64_t)m) >> 25);
-}
 
 // partial Fisher-Yates (the first k of a random permutation of 0..n-1): the Philox stand-in for
 // np.random.choice(n, k, replace=False); a: LDS scratch of n bytes, out: k picks
@@ -441,384 +435,6 @@ __device__ __forceinline__ void obstacle_spawn_goal(const KP& kp, const ObstScra
     goal[2] = sc->mode == 0 ? 1.f + 2.f * uniform1(r, gid, S_RESET, 4) : sc->ez;
 }
 
-// ---------------------------------------------------------------------------------------------
-// flavor-B goal scenarios (gym_art/quadrotor_multi/scenarios/).  The env's lead lane runs
-// them serially (a reset, or an event every 4-6 s; per step only for ep_lissajous3D / ep_rand_bezier /
-// dynamic_formations) on goal tables in LDS (4 floats per drone); the drones then read their goal.
-// Mirrors oracle/quadswarm_oracle_scen.c draw for draw: Philox key = the env's drone 0, stream S_SCN
-// (step) / S_SCN_RESET (reset), one 32-bit word per draw in call order.
-// ---------------------------------------------------------------------------------------------
-enum { SC_STATIC_SAME_GOAL = 0, SC_STATIC_DIFF_GOAL, SC_EP_LISSAJOUS3D, SC_EP_RAND_BEZIER, SC_DYNAMIC_SAME_GOAL,
-       SC_DYNAMIC_DIFF_GOAL, SC_DYNAMIC_FORMATIONS, SC_SWAP_GOALS, SC_SWARM_VS_SWARM, SC_RUN_AWAY, SC_MIX };
-enum { F_CIRCLE_H = 0, F_CIRCLE_XZ, F_CIRCLE_YZ, F_SPHERE, F_GRID_H, F_GRID_XZ, F_GRID_YZ, F_CUBE };
-
-struct Scen {
-    int mode, form, period, inc;
-    float size, lo, hi, layer, speed, c[3], bz[9], c1[3], c2[3];
-};
-
-__device__ __forceinline__ void scen_load(const KP& kp, const Bufs& b, int env, Scen& s) {
-    const int E = kp.E;
-    s.mode = b.env[QS_E_SC_MODE * E + env]; s.form = b.env[QS_E_SC_FORM * E + env];
-    s.period = b.env[QS_E_SC_PERIOD * E + env]; s.inc = b.env[QS_E_SC_INC * E + env];
-    const float* f = b.envf;
-    s.size = f[QS_ENVF_SC_SIZE * E + env]; s.lo = f[QS_ENVF_SC_LO * E + env]; s.hi = f[QS_ENVF_SC_HI * E + env];
-    s.layer = f[QS_ENVF_SC_LAYER * E + env]; s.speed = f[QS_ENVF_SC_SPEED * E + env];
-    for (int i = 0; i < 3; ++i) {
-        s.c[i] = f[(QS_ENVF_SC_CENTER + i) * E + env];
-        s.c1[i] = f[(QS_ENVF_SC_C1 + i) * E + env];
-        s.c2[i] = f[(QS_ENVF_SC_C2 + i) * E + env];
-    }
-    for (int i = 0; i < 9; ++i) s.bz[i] = f[(QS_ENVF_SC_BEZIER + i) * E + env];
-}
-__device__ __forceinline__ void scen_store(const KP& kp, const Bufs& b, int env, const Scen& s) {
-    const int E = kp.E;
-    b.env[QS_E_SC_MODE * E + env] = s.mode; b.env[QS_E_SC_FORM * E + env] = s.form;
-    b.env[QS_E_SC_PERIOD * E + env] = s.period; b.env[QS_E_SC_INC * E + env] = s.inc;
-    float* f = b.envf;
-    f[QS_ENVF_SC_SIZE * E + env] = s.size; f[QS_ENVF_SC_LO * E + env] = s.lo; f[QS_ENVF_SC_HI * E + env] = s.hi;
-    f[QS_ENVF_SC_LAYER * E + env] = s.layer; f[QS_ENVF_SC_SPEED * E + env] = s.speed;
-    for (int i = 0; i < 3; ++i) {
-        f[(QS_ENVF_SC_CENTER + i) * E + env] = s.c[i];
-        f[(QS_ENVF_SC_C1 + i) * E + env] = s.c1[i];
-        f[(QS_ENVF_SC_C2 + i) * E + env] = s.c2[i];
-    }
-    for (int i = 0; i < 9; ++i) f[(QS_ENVF_SC_BEZIER + i) * E + env] = s.bz[i];
-}
-
-// draw source: one Philox word per draw, the last block cached (draws are sequential)
-struct SDraw {
-    Rng r;
-    uint32_t key, stream, k, blk;
-    W4 w;
-};
-__device__ __forceinline__ SDraw sdraw(const Rng& r, uint32_t key, uint32_t stream) {
-    SDraw s;
-    s.r = r; s.key = key; s.stream = stream | UNIF_BIT; s.k = 0; s.blk = 0xFFFFFFFFu;
-    return s;
-}
-__device__ __forceinline__ uint32_t sd_word(SDraw& s) {
-    const uint32_t k = s.k++;
-    if ((k >> 2) != s.blk) {
-        s.blk = k >> 2;
-        s.w = block(s.r, s.key, s.stream, s.blk);
-    }
-    return word_of(s.w, k & 3);
-}
-__device__ __forceinline__ float sd_uniform(SDraw& s, float lo, float hi) { return lo + (hi - lo) * u01(sd_word(s)); }
-__device__ __forceinline__ int sd_int(SDraw& s, int lo, int hi) { return lo + ufloor(sd_word(s), hi - lo); }
-// Generator.shuffle as Fisher-Yates from the top over LDS rows g[4 i ..]
-__device__ __forceinline__ void sd_shuffle(SDraw& s, float* g, int n) {
-    for (int i = n - 1; i >= 1; --i) {
-        const int j = sd_int(s, 0, i + 1);
-        for (int c = 0; c < 3; ++c) {
-            const float t = g[4 * i + c];
-            g[4 * i + c] = g[4 * j + c];
-            g[4 * j + c] = t;
-        }
-    }
-}
-
-// sin / cos of any angle on the hardware units, reduced to [-0.5, 0.5] revolutions first
-__device__ __forceinline__ float sin_any(float x) {
-    const float r = x * 0.15915494309189535f;
-    return __builtin_amdgcn_sinf(r - rintf(r));
-}
-__device__ __forceinline__ float cos_any(float x) {
-    const float r = x * 0.15915494309189535f;
-    return __builtin_amdgcn_cosf(r - rintf(r));
-}
-
-// The drone count as a run-time value: in the specialised build kp.N is a constant, and the compiler would
-// constant-fold the hardware transcendentals of the formation geometry exactly (sin / cos / log2 / exp2 of
-// constant arguments) where the generic build evaluates them on the approximate hardware units.
-__device__ __forceinline__ int sc_num(const KP& kp) {
-    int n = kp.N;
-    asm volatile("" : "+v"(n));
-    return n;
-}
-
-// QUADS_PARAMS_DICT (utils.py:33-53)
-__device__ __forceinline__ void sc_mode_params(int mode, int& nform, float& low, float& high) {
-    if (mode == SC_STATIC_DIFF_GOAL || mode == SC_DYNAMIC_DIFF_GOAL || mode == SC_SWARM_VS_SWARM || mode == SC_RUN_AWAY) {
-        nform = 8; low = 0.25f; high = 0.5f;
-    } else if (mode == SC_SWAP_GOALS) {
-        nform = 8; low = 0.4f; high = 0.8f;
-    } else if (mode == SC_DYNAMIC_FORMATIONS) {
-        nform = 8; low = 0.f; high = 1.0f;
-    } else {
-        nform = 1; low = 0.f; high = 0.f;
-    }
-}
-__device__ __forceinline__ int sc_per_layer(int f) { return (f == F_GRID_H || f == F_GRID_XZ || f == F_GRID_YZ) ? 50 : 8; }
-__device__ __forceinline__ void sc_grid_dims(int num, int& d1, int& d2) {   // get_grid_dim_number (utils.py:124-136)
-    int g = (int)floorf(fsqrt((float)num) + 1e-6f);
-    while (g > 1 && num % g != 0) --g;
-    d1 = g;
-    d2 = num / g;
-}
-__device__ __forceinline__ void sc_by_formation(int f, float p0, float p1, float layer, float* g) {   // utils.py:164-175
-    if (f == F_CIRCLE_H || f == F_GRID_H) { g[0] = p0; g[1] = p1; g[2] = layer; }
-    else if (f == F_CIRCLE_XZ || f == F_GRID_XZ) { g[0] = p0; g[1] = layer; g[2] = p1; }
-    else { g[0] = layer; g[1] = p0; g[2] = p1; }
-}
-
-// QuadrotorScenario.generate_goals (base.py:42-116) into LDS rows; returns the goal count (sphere >= 3)
-__device__ int sc_generate(int f, int n, int per_layer, float size, float layer, const float* c, float* g) {
-    if (f <= F_CIRCLE_YZ) {
-        const int whole = n / per_layer, rest = n % per_layer;
-        for (int i = 0; i < n; ++i) {
-            const int cur = n <= per_layer ? n : ((i / per_layer) < whole ? per_layer : rest);
-            const float rev = (float)(i % cur) / (float)cur;   // degree / 2 pi
-            float* gi = g + 4 * i;
-            sc_by_formation(f, size * __builtin_amdgcn_cosf(rev), size * __builtin_amdgcn_sinf(rev),
-                            (float)(i / per_layer) * layer, gi);
-            gi[0] += c[0]; gi[1] += c[1]; gi[2] += c[2];
-        }
-        return n;
-    }
-    if (f == F_SPHERE) {   // generate_points (utils.py:87-103)
-        const int m = n < 3 ? 3 : n;
-        const float x = 0.1f + 1.2f * (float)m;
-        const float start = -1.f + 1.f / ((float)m - 1.f), inc = (2.f - 2.f / ((float)m - 1.f)) / ((float)m - 1.f);
-        for (int j = 0; j < m; ++j) {
-            const float s = start + (float)j * inc;
-            const float sg = s > 0.f ? 1.f : (s < 0.f ? -1.f : 0.f);
-            const float a = s * x, bb = 1.5707963267948966f * sg * (1.f - fsqrt(1.f - fabsf(s)));
-            const float cb = cos_any(bb);
-            float* gj = g + 4 * j;
-            gj[0] = size * (cos_any(a) * cb) + c[0];
-            gj[1] = size * (sin_any(a) * cb) + c[1];
-            gj[2] = size * sin_any(bb) + c[2];
-        }
-        return m;
-    }
-    if (f == F_CUBE) {
-        // int(np.power(n, 1/3)) as float64 rounds it for n <= 32: 27 ** (1/3) = 2.9999999999999996 -> 2
-        const int fd = n < 8 ? 1 : (n <= 27 ? 2 : 3);
-        for (int i = 0; i < n; ++i) {
-            float* gi = g + 4 * i;
-            gi[0] = c[2] + size * (float)(i / (fd * fd));
-            gi[1] = size * (float)((i / fd) % fd);
-            gi[2] = size * (float)(i % fd);
-        }
-    } else {   // grid
-        int d1, d2, r1 = 1, r2 = 1;
-        sc_grid_dims(n <= per_layer ? n : per_layer, d1, d2);
-        if (n > per_layer && n % per_layer) sc_grid_dims(n % per_layer, r1, r2);
-        const int whole = n / per_layer;
-        for (int i = 0; i < n; ++i) {
-            const int L = i / per_layer;
-            const bool full = n <= per_layer || L < whole;
-            const int a = full ? d1 : r1, b2 = full ? d2 : r2;
-            sc_by_formation(f, size * (float)(i % b2), size * (float)((i / b2) % a), (float)L * layer, g + 4 * i);
-        }
-    }
-    float mean[3] = {0.f, 0.f, 0.f};
-    for (int i = 0; i < n; ++i)
-        for (int k = 0; k < 3; ++k) mean[k] += g[4 * i + k];
-    for (int k = 0; k < 3; ++k) mean[k] /= (float)n;
-    for (int i = 0; i < n; ++i)
-        for (int k = 0; k < 3; ++k) g[4 * i + k] = g[4 * i + k] - mean[k] + c[k];
-    return n;
-}
-
-// update_formation_and_relate_param (base.py:126-139) with get_formation_range (utils.py:139-161)
-__device__ void sc_update_formation(const KP& kp, Scen& s, SDraw& sd) {
-    int nform;
-    float low, high;
-    sc_mode_params(s.mode, nform, low, high);
-    s.form = sd_int(sd, 0, nform);
-    const int pl = sc_per_layer(s.form);
-    if (s.form <= F_CIRCLE_YZ) {   // get_circle_radius: 0.5 dist / sin(pi / per_layer)
-        const float k = 0.5f / __builtin_amdgcn_sinf(0.5f / (float)pl);
-        s.lo = low * k; s.hi = high * k;
-    } else if (s.form == F_SPHERE) {   // get_sphere_radius
-        const int n = s.mode == SC_SWARM_VS_SWARM ? sc_num(kp) / 2 : sc_num(kp);
-        const float ratio = (1.75388487222762f - 0.0920858134405214f) /
-                                (1.f + exp2f(0.860487305801679f * __log2f((float)n / 10.3632729642351f))) +
-                            0.0920858134405214f;
-        s.lo = low / ratio; s.hi = high / ratio;
-    } else {
-        s.lo = low; s.hi = high;
-    }
-    s.size = sd_uniform(sd, s.lo, s.hi);
-    s.layer = sd_uniform(sd, s.lo, s.hi);
-}
-
-// get_z_value (utils.py:178-189)
-__device__ float sc_z_value(const KP& kp, const Scen& s, SDraw& sd) {
-    const float box = kp.spawn_box;
-    const float z = sd_uniform(sd, -0.5f * box, 0.5f * box) + 2.0f;
-    float lb = 0.25f;
-    if (s.form == F_SPHERE || s.form == F_CIRCLE_XZ || s.form == F_CIRCLE_YZ) lb = s.size + 0.25f;
-    else if (s.form == F_GRID_XZ || s.form == F_GRID_YZ) {
-        int d1, d2;
-        sc_grid_dims(min(kp.N, sc_per_layer(s.form)), d1, d2);
-        lb = (float)d1 * s.size + 0.25f;
-    }
-    return fmaxf(z, lb);
-}
-
-// swarm_vs_swarm create_formations (swarm_vs_swarm.py:49-54) [+ update_goals' shuffles]; tmp: scratch rows
-__device__ void sc_vs_formations(const KP& kp, Scen& s, float* g, float* tmp, bool shuffle, SDraw& sd) {
-    const int N = sc_num(kp), pl = sc_per_layer(s.form);
-    const int n1 = sc_generate(s.form, N / 2, pl, s.size, s.layer, s.c1, g);
-    if (shuffle) sd_shuffle(sd, g, n1);
-    const int n2 = sc_generate(s.form, N - N / 2, pl, s.size, s.layer, s.c2, tmp);
-    if (shuffle) sd_shuffle(sd, tmp, n2);
-    for (int i = 0; i < n2 && n1 + i < N; ++i)
-        for (int k = 0; k < 3; ++k) g[4 * (n1 + i) + k] = tmp[4 * i + k];
-}
-
-// Scenario_mix.reset (mix.py:79-99) -> <scenario>.__init__ + .reset: the N goals into g
-__device__ void scen_reset(const KP& kp, Scen& s, SDraw& sd, float* g, float* tmp) {
-    s = Scen{};   // a fresh Scenario_* object per reset (mix.py:88)
-    const int N = sc_num(kp);
-    const float cf = 1.f / kp.cdt;
-    s.mode = kp.scen_b == SC_MIX ? sd_int(sd, 0, N == 1 ? 5 : 9) : kp.scen_b;
-    s.period = (int)(5.f * cf);
-    s.inc = 0;
-    if (s.mode == SC_DYNAMIC_FORMATIONS) {   // dynamic_formations.py:9-16, 42-48
-        s.speed = sd_uniform(sd, 1.f, 3.f);
-        s.inc = sd_uniform(sd, 0.f, 1.f) < 0.5f;
-        s.speed = sd_uniform(sd, 1.f, 3.f);
-    } else if (s.mode == SC_DYNAMIC_SAME_GOAL || s.mode == SC_DYNAMIC_DIFF_GOAL || s.mode == SC_SWAP_GOALS ||
-               s.mode == SC_SWARM_VS_SWARM) {
-        s.period = (int)(sd_uniform(sd, 4.f, 6.f) * cf);
-    }
-    sc_update_formation(kp, s, sd);
-    const int pl = sc_per_layer(s.form);
-    if (s.mode == SC_SWARM_VS_SWARM) {   // swarm_vs_swarm.py:125-139, formation_centers :11-47
-        const float box = kp.spawn_box;
-        const float x = sd_uniform(sd, -box, box), y = sd_uniform(sd, -box, box);
-        s.c1[0] = x; s.c1[1] = y; s.c1[2] = sc_z_value(kp, s, sd);
-        const float dist = sd_uniform(sd, box / 4.f, box);
-        const float phi = sd_uniform(sd, -3.14159265358979f, 3.14159265358979f);
-        const float th = sd_uniform(sd, -1.5707963267948966f, 1.5707963267948966f);
-        s.c2[0] = s.c1[0] + dist * (sin_any(th) * cos_any(phi));
-        s.c2[1] = s.c1[1] + dist * (sin_any(th) * sin_any(phi));
-        s.c2[2] = s.c1[2] + dist * cos_any(th);
-        const int f = s.form;
-        const int ax = (f == F_CIRCLE_H || f == F_GRID_H) ? 2 : (f == F_CIRCLE_XZ || f == F_GRID_XZ) ? 1
-                     : (f == F_CIRCLE_YZ || f == F_GRID_YZ) ? 0 : -1;
-        if (ax >= 0) {
-            const float dd = s.c2[ax] - s.c1[ax];
-            if (fabsf(dd) < s.lo) s.c2[ax] = (dd > 0.f ? 1.f : (dd < 0.f ? -1.f : 0.f)) * s.lo + s.c1[ax];
-        }
-        sc_vs_formations(kp, s, g, tmp, false, sd);
-        for (int k = 0; k < 3; ++k) s.c[k] = (s.c1[k] + s.c2[k]) * 0.5f;
-        return;
-    }
-    if (s.mode == SC_EP_LISSAJOUS3D) {   // ep_lissajous3D.py:31-38, no shuffle
-        s.c[0] = -2.f; s.c[1] = 0.f; s.c[2] = 2.f;
-        sc_generate(s.form, N, pl, s.size, 0.f, s.c, g);
-        return;
-    }
-    s.c[0] = 0.f; s.c[1] = 0.f; s.c[2] = 2.f;   // reset / standard_reset (base.py:144-173)
-    const int m = sc_generate(s.form, N, pl, s.size, s.layer, s.c, g);
-    sd_shuffle(sd, g, m);
-}
-
-// <scenario>.step() after the drones stepped (quadrotor_multi.py:700-701), tick = envs[0].tick
-__device__ void scen_step(const KP& kp, Scen& s, int tick, SDraw& sd, float* g, float* tmp) {
-    const int N = sc_num(kp);
-    const float box = kp.spawn_box, cf = 1.f / kp.cdt;
-    const int pl = sc_per_layer(s.form);
-    const bool ev = s.period > 0 && tick % s.period == 0 && tick > 0;
-    if (s.mode == SC_DYNAMIC_SAME_GOAL) {   // dynamic_same_goal.py:16-29
-        if (!ev) return;
-        const float x = sd_uniform(sd, -box, box), y = sd_uniform(sd, -box, box);
-        const float z = fmaxf(sd_uniform(sd, -0.5f * box, 0.5f * box) + 2.f, 0.25f);
-        s.c[0] = x; s.c[1] = y; s.c[2] = z;
-        sc_generate(s.form, N, pl, s.size, 0.f, s.c, g);
-    } else if (s.mode == SC_DYNAMIC_DIFF_GOAL) {   // dynamic_diff_goal.py:13-40
-        if (!ev) return;
-        const float x = sd_uniform(sd, -box, box), y = sd_uniform(sd, -box, box);
-        const float z = sc_z_value(kp, s, sd);
-        s.c[0] = x; s.c[1] = y; s.c[2] = z;
-        sc_update_formation(kp, s, sd);
-        const int m = sc_generate(s.form, N, sc_per_layer(s.form), s.size, s.layer, s.c, tmp);
-        sd_shuffle(sd, tmp, m);
-        for (int i = 0; i < 4 * N; ++i) g[i] = tmp[i];
-    } else if (s.mode == SC_SWAP_GOALS) {   // swap_goals.py:12-25
-        if (ev) sd_shuffle(sd, g, N);
-    } else if (s.mode == SC_DYNAMIC_FORMATIONS) {   // dynamic_formations.py:18-40
-        if (s.size <= -s.hi) {
-            s.inc = 1;
-            s.speed = sd_uniform(sd, 1.f, 3.f);
-        } else if (s.size >= s.hi) {
-            s.inc = 0;
-            s.speed = sd_uniform(sd, 1.f, 3.f);
-        }
-        s.size += (s.inc ? 0.001f : -0.001f) * s.speed;
-        sc_generate(s.form, N, pl, s.size, s.layer, s.c, g);
-    } else if (s.mode == SC_EP_LISSAJOUS3D) {   // ep_lissajous3D.py:8-26 (accumulates on goals[0])
-        const float t = (float)tick / cf;
-        const float nx = 0.03f * sin_any(t) + g[0], ny = 0.01f * sin_any(2.f * t + 90.f) + g[1],
-                    nz = 0.01f * cos_any(2.f * t + 90.f) + g[2];
-        for (int i = 0; i < N; ++i) { g[4 * i] = nx; g[4 * i + 1] = ny; g[4 * i + 2] = nz; }
-    } else if (s.mode == SC_EP_RAND_BEZIER) {   // ep_rand_bezier.py:6-47
-        const int steps = (int)(5.f * cf);
-        const int t = tick % steps;
-        float rd[3], hi[3], lo[3];
-        for (int k = 0; k < 3; ++k) rd[k] = kp.room_hi[k] - kp.room_lo[k] - s.size;
-        const float mx = fminf(fmaxf(fmaxf(rd[0], rd[1]), rd[2]), 30.f);
-        hi[0] = rd[0] * 0.5f; hi[1] = rd[1] * 0.5f; hi[2] = rd[2];
-        lo[0] = -hi[0]; lo[1] = -hi[1]; lo[2] = 0.f;
-        if (t == 0 || tick == 1) {
-            float np_[3][2];
-            for (int tries = 0;; ++tries) {   // uniform(size=(2, 3)).reshape(3, 2): [c][j] = flat 2c + j
-                float u[6];
-                for (int k = 0; k < 6; ++k) u[k] = sd_uniform(sd, -hi[k % 3], hi[k % 3]);
-                const float mag = (float)sd_int(sd, (int)ceilf(mx * 0.5f), (int)floorf(mx) + 1);
-                bool ok = true;
-                for (int j = 0; j < 2; ++j) {
-                    const float v0 = u[j], v1 = u[2 + j], v2 = u[4 + j];
-                    const float sc = mag / fsqrt(v0 * v0 + v1 * v1 + v2 * v2);
-                    np_[0][j] = v0 * sc + g[0]; np_[1][j] = v1 * sc + g[1]; np_[2][j] = v2 * sc + g[2];
-                    for (int k = 0; k < 3; ++k) ok = ok && np_[k][j] > lo[k] + 0.5f && np_[k][j] < hi[k] - 0.5f;
-                }
-                if (ok || tries >= 1023) break;   // the reference loops without a bound
-            }
-            for (int k = 0; k < 3; ++k) {
-                s.bz[k] = g[k];
-                s.bz[3 + k] = np_[k][0];
-                s.bz[6 + k] = np_[k][1];
-            }
-        }
-        if (t != 0 && tick > 1) {   // interp[:, t] of the degree-2 Bezier (bezier's Bernstein evaluation)
-            const float sp = t == steps - 1 ? 1.f : (float)t * (1.f / (float)(steps - 1));
-            const float l1 = 1.f - sp;
-            float pt[3];
-            for (int k = 0; k < 3; ++k) pt[k] = (l1 * s.bz[k] + 2.f * sp * s.bz[3 + k]) * l1 + sp * sp * s.bz[6 + k];
-            for (int i = 0; i < N; ++i) { g[4 * i] = pt[0]; g[4 * i + 1] = pt[1]; g[4 * i + 2] = pt[2]; }
-        }
-    } else if (s.mode == SC_SWARM_VS_SWARM) {   // swarm_vs_swarm.py:56-76
-        if (!ev) return;
-        for (int k = 0; k < 3; ++k) {
-            const float t3 = s.c1[k];
-            s.c1[k] = s.c2[k];
-            s.c2[k] = t3;
-        }
-        sc_update_formation(kp, s, sd);
-        sc_vs_formations(kp, s, g, tmp, true, sd);
-    } else if (s.mode == SC_RUN_AWAY) {   // run_away.py:16-27
-        if (tick % (int)(1.f * cf) == 0 && tick > 0 && N >= 2) {
-            const int a = sd_int(sd, 1, N), b2 = sd_int(sd, 1, N);
-            float ga[3], gb[3];
-            for (int k = 0; k < 3; ++k) { ga[k] = g[4 * a + k]; gb[k] = g[4 * b2 + k]; }
-            for (int k = 0; k < 3; ++k) { g[k] = ga[k]; g[4 + k] = gb[k]; }
-        }
-    }
-}
-
-// LDS goal tables of the env (2 x (NPAD + 4) rows of 4 floats), after the obs / exchange tiles
-template <int NPAD>
-constexpr int scen_stride() { return 2 * (NPAD + 4) * 4; }
-__device__ __forceinline__ float* scen_tab(float* lds, const KP& kp, int slots) {
-    return lds + slots * kp.obs_dim + slots * 8 + 64;
-}
 
 // get_surround_sdfs (obstacles/utils.py:4-27)
 __device__ __forceinline__ void sdf_obs(const KP& kp, const OGeo& og, const float2* ob, float x, float y, float* out) {

@@ -159,8 +159,11 @@ static int validate(const qs_config* c) {
     } else {
         if (c->use_obstacles) return fail(QS_E_UNSUPPORTED, "flavor A with obstacles is not implemented");
         if (c->obs_repr < 3 || c->obs_repr > 6) return fail(QS_E_INVALID, "obs_repr is not a flavor-A repr");
-        if (c->scenario != QS_SCEN_STATIC_SAME_GOAL && c->scenario != QS_SCEN_DYNAMIC_REPULSIVE)
-            return fail(QS_E_INVALID, "unknown scenario");
+        if (c->scenario != QS_SCEN_STATIC_SAME_GOAL && c->scenario != QS_SCEN_DYNAMIC_REPULSIVE &&
+            (c->scenario < QS_SCEN_MIX || c->scenario > QS_SCEN_RUN_AWAY))
+            return fail(QS_E_INVALID, "flavor A: static_same_goal, dynamic_repulsive or a goal scenario");
+        if (c->scenario == QS_SCEN_RUN_AWAY && c->num_agents < 2)
+            return fail(QS_E_INVALID, "run_away needs at least 2 drones (run_away.py:16-27)");
         if (c->ticks_per_step < 1) return fail(QS_E_INVALID, "ticks_per_step must be >= 1");
         if (c->n_cameras < 1) return fail(QS_E_INVALID, "n_cameras must be >= 1");
     }
@@ -344,7 +347,7 @@ static qs::KP make_kp(const qs_config* c, const qs_layout& L) {
     k.flavor = c->flavor;
     // goal scenarios (flavor B, no obstacles): QS_SCEN_MIX -> 10, QS_SCEN_STATIC_DIFF_GOAL.. -> 1..9
     k.scen_b = -1;
-    if (c->flavor == QS_FLAVOR_B && !c->use_obstacles && c->scenario >= QS_SCEN_MIX)
+    if (!c->use_obstacles && c->scenario >= QS_SCEN_MIX && c->scenario <= QS_SCEN_RUN_AWAY)
         k.scen_b = c->scenario == QS_SCEN_MIX ? 10 : c->scenario - QS_SCEN_MIX;
     if (c->flavor == QS_FLAVOR_A) make_kp_a(c, k);
     if (c->episode_stats && c->flavor == QS_FLAVOR_B) {   // quadrotor_multi.py:156-161, 651-655, 761-774
@@ -488,7 +491,7 @@ static size_t shm_bytes(const qs_config& c, int obs_dim, int npad, bool step, in
     const size_t epb = (size_t)envs_per_block(c, npad, step, qb, qa), slots = epb * (size_t)npad;
     size_t b = sizeof(float) * slots * (size_t)obs_dim + sizeof(float) * slots * 8 + sizeof(float) * 64;
     if (c.use_obstacles) b += epb * (sizeof(float) * 2 * (size_t)obst_slots(&c) + (size_t)qs::QS_OBST_SCRATCH);
-    else if (c.flavor == QS_FLAVOR_B && c.scenario >= QS_SCEN_MIX)   // goal tables (qs::scen_stride)
+    else if (c.scenario >= QS_SCEN_MIX && c.scenario <= QS_SCEN_RUN_AWAY)   // goal tables (qs::scen_stride)
         b += epb * sizeof(float) * 2 * ((size_t)npad + 4) * 4;
     return b;
 }

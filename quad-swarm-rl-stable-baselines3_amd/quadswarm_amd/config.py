@@ -210,8 +210,8 @@ class QuadSwarmConfig:
         if self.use_obstacles:
             return {"mix": N.SCENARIO["obst_mix"], "o_random": N.SCENARIO["o_random"],
                     "o_static_same_goal": N.SCENARIO["o_static_same_goal"]}[self.quads_mode]
-        if self.flavor == "B":
-            return N.SCENARIO_B[self.quads_mode]
+        if self.flavor == "B" or self.quads_mode not in N.SCENARIO:
+            return N.SCENARIO_B[self.quads_mode]   # goal scenarios (create_scenario) of either flavor
         return N.SCENARIO[self.quads_mode]
 
     @property
@@ -251,9 +251,9 @@ class QuadSwarmConfig:
                 if any(c == 0 for c in counts):
                     raise ValueError("a density choice gives 0 pillars (the reference's obstacle arrays break)")
         if self.flavor == "A":
-            if self.quads_mode not in ("dynamic_repulsive", "static_same_goal"):
+            if self.quads_mode not in ("dynamic_repulsive", "static_same_goal") and self.quads_mode not in N.SCENARIO_B:
                 raise NotImplementedError(f"quads_mode {self.quads_mode!r} not implemented for flavor A "
-                                          "(dynamic_repulsive, static_same_goal)")
+                                          "(dynamic_repulsive or a goal scenario of create_scenario)")
         if self.replay_buffer_sample_prob > 0 and self.flavor != "B":
             raise NotImplementedError("experience replay is implemented for flavor B")
         if not 0.0 <= self.replay_buffer_sample_prob <= 1.0:

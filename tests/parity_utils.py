@@ -313,11 +313,15 @@ def oracle_params_a(cfg: QuadSwarmConfig):
     p.sense_noise = 0 if cfg.sense_noise is None else 1
     p.ep_len = cfg.ep_len
     p.ticks_per_step = cfg.ticks_per_step
-    p.scenario_a = NAT.SCENARIO[cfg.quads_mode]
+    p.scenario_a = NAT.SCENARIO.get(cfg.quads_mode, 0)
     p.cam_size, p.cam_focal, p.cam_px_noise = cfg.neighbour_size_cam, cfg.focal_length_cam, cfg.pixel_noise_cam
     p.n_cameras = cfg.n_cameras
     p.control_dt = cfg.dt * cfg.sim_steps
     p.use_downwash = int(bool(cfg.use_downwash))
+    p.scenario_b = -1                                       # OR_SC_NONE
+    if cfg.quads_mode not in NAT.SCENARIO:                  # a create_scenario goal scenario (:123)
+        p.scenario_b = O.SC_MIX if cfg.quads_mode == "mix" else O.SC_MODES.index(cfg.quads_mode)
+        p.scenario_a = 0
     return p
 
 

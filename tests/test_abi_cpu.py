@@ -126,8 +126,13 @@ def test_config_rejects_unbuilt_or_mixed_flavors():
         QuadSwarmConfig(obs_repr="cdist_cdistdot_dist_distdot_sangle_angledot").to_qs_config()
     with pytest.raises(NotImplementedError):   # not in QUADS_MODE_LIST (needs a trajectory csv)
         QuadSwarmConfig(quads_mode="ep_trajectory").to_qs_config()
-    with pytest.raises(NotImplementedError):   # the goal scenarios are flavor B's
-        QuadSwarmConfig.sb_train(quads_mode="mix").to_qs_config()
+    with pytest.raises(NotImplementedError):   # not a create_scenario mode of either flavor
+        QuadSwarmConfig.sb_train(quads_mode="o_random").to_qs_config()
+    # flavor A builds every goal scenario through create_scenario (quadrotor_multi_rewards.py:123)
+    c = QuadSwarmConfig.sb_train(quads_mode="mix").to_qs_config()
+    assert c.scenario == N.SCENARIO_B["mix"]
+    lay = N.QsLayout()
+    assert N.lib().qs_layout_query(ctypes.byref(c), ctypes.byref(lay)) == 0
     with pytest.raises(ValueError):
         QuadSwarmConfig(num_agents=1, quads_mode="run_away").to_qs_config()
 

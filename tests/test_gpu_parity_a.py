@@ -37,6 +37,10 @@ CONFIGS = {
     "n64k6": dict(num_agents=64, neighbor_visible_num=6, neighbor_obs_type="dist_sangle"),
     # use_downwash (quadrotor_multi_rewards.py:810-815): _perturb stacks the drones in vertical pairs
     "dw8": dict(num_agents=8, neighbor_obs_type="dist_angle", use_downwash=True),
+    # goal scenarios through create_scenario (quadrotor_multi_rewards.py:123): mix draws one per env and reset
+    "mix8": dict(num_agents=8, neighbor_obs_type="dist_angle", quads_mode="mix"),
+    "liss8": dict(num_agents=8, neighbor_obs_type="dist_angle", quads_mode="ep_lissajous3D"),
+    "svs8": dict(num_agents=8, neighbor_obs_type="dist_angle", quads_mode="swarm_vs_swarm"),
     "static4": dict(num_agents=4, quads_mode="static_same_goal", neighbor_obs_type="pos"),
 }
 

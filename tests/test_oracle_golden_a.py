@@ -217,3 +217,32 @@ def test_trajectory_tape_replay_a(golden, name):
     close(np.stack([O.get_arr(drones[i].pid) for i in range(n)]), g["final_pid"], 1e-6, 1e-8)
     if name in ("n4", "n8", "n1"):
         assert resets >= 1
+
+
+@pytest.mark.parametrize("mode", ["mix", "static_diff_goal", "ep_lissajous3D", "dynamic_formations", "swap_goals",
+                                  "swarm_vs_swarm", "run_away"])
+def test_goal_scenarios_run_in_flavor_a(mode):
+    """create_scenario goal scenarios in the flavor-A env (quadrotor_multi_rewards.py:123, :560, :848): the
+    scenario functions are the ones pinned by the scenario tapes (test_oracle_scen.py); here their wiring --
+    goals from scenario.reset(), drones spawned at their goal, goals moved by scenario.step() every tick."""
+    from quadswarm_amd import QuadSwarmConfig
+    from parity_utils import oracle_params_a
+    cfg = QuadSwarmConfig.sb_train(num_envs=6, num_agents=8, neighbor_obs_type="dist_angle", quads_mode=mode,
+                                   episode_duration=1.0, seed=2)
+    oenv = O.OracleEnvA(oracle_params_a(cfg), seed=2)
+    oenv.set_capture_radius(0.0)
+    obs, _ = oenv.reset()
+    goals = np.array([oenv.drones[g].goal[:] for g in range(48)])
+    pos = np.array([oenv.drones[g].pos[:] for g in range(48)])
+    np.testing.assert_allclose(pos[:, :2], goals[:, :2])          # spawn at the goal (spawn_points None)
+    if mode in ("static_diff_goal", "swap_goals", "swarm_vs_swarm", "dynamic_formations"):   # a goal per drone
+        assert len({tuple(np.round(g, 6)) for g in goals[:8]}) > 1
+    rng = np.random.default_rng(0)
+    moved = False
+    for t in range(12):
+        obs, rew, done, _, _ = oenv.step(rng.uniform(-1, 1, (48, 2)))
+        assert np.isfinite(obs).all() and np.isfinite(rew).all()
+        g2 = np.array([oenv.drones[g].goal[:] for g in range(48)])
+        moved |= bool(np.abs(g2 - goals).max() > 1e-9)
+    if mode in ("ep_lissajous3D", "dynamic_formations"):
+        assert moved
