@@ -821,9 +821,9 @@ static void obstacle_reset(const or_params* p, or_env* ev, uint32_t gbase, or_rn
  * (scenarios/base.py:255-272 with formation size 0), QuadrotorEnvMulti.reset (quadrotor_multi.py:440-517) */
 /* episode_extra_stats bookkeeping of one step (quadrotor_multi.py:555-566, 575-589, 599-606, 631-656).
  * tick = envs[0].tick after the drones' _step; time_remain = QuadrotorSingle.time_remain of the step. */
-static void episode_stats_step(const or_params* p, or_env* ev, or_drone* dr, int N, const int* in_cur, const int* in_prev,
-                               const int* onew, const int* wall_new, const int* ceil_new, const double* dist_goal,
-                               const double* obs, int od, int time_remain) {
+void or_episode_stats_step(const or_params* p, or_env* ev, or_drone* dr, int N, const int* in_cur, const int* in_prev,
+                           const int* onew, const int* wall_new, const int* ceil_new, const double* dist_goal,
+                           const double* obs, int od, int time_remain) {
     const double freq = 1.0 / p->control_dt;
     const int settle = (double)ev->tick >= 1.5 * freq;               /* collisions_grace_period_steps */
     /* collisions_curr_tick = len(last_step_unique_collisions) // 2 */
@@ -836,7 +836,7 @@ static void episode_stats_step(const or_params* p, or_env* ev, or_drone* dr, int
         for (int i = 0; i < N; ++i) if (in_cur[i] && !in_prev[i]) dr[i].hit_agent = 1;
     }
     if (cnt > 0 && (double)time_remain <= 5.0 * freq) ev->st_col_final += cnt;
-    if (p->use_obstacles) {
+    if (p->use_obstacles && onew) {
         int oc = 0;
         for (int i = 0; i < N; ++i) oc += onew[i];
         ev->st_ocol += oc;
@@ -862,7 +862,9 @@ static void episode_stats_step(const or_params* p, or_env* ev, or_drone* dr, int
         nf += dr[i].crashed_floor != 0; nw += wall_new[i]; nc += ceil_new[i]; nr += room;
     }
     if (settle) { ev->st_room += nr; ev->st_floor += nf; ev->st_wall += nw; ev->st_ceil += nc; }
-    /* distance_to_goal[i].append(dt * dist); reached_goal (mean of the last 5 entries / dt < 0.5) */
+    /* distance_to_goal[i].append(dt * dist); reached_goal (mean of the last 5 entries / dt < 0.5); flavor A
+     * never appends (quadrotor_multi_rewards.py:797-802 commented out): dist_goal NULL */
+    if (!dist_goal) return;
     const int T = p->ep_len + 1;                                    /* the entry count when the episode ends */
     const int win[3] = {(int)(1.0 * freq), (int)(3.0 * freq), (int)(5.0 * freq)};
     for (int i = 0; i < N; ++i) {
@@ -879,7 +881,7 @@ static void episode_stats_step(const or_params* p, or_env* ev, or_drone* dr, int
 }
 
 /* the stats of the episode that just finished (quadrotor_multi.py:739-831), before the in-env reset */
-static void episode_stats_done(const or_params* p, or_env* ev, or_drone* dr, int N) {
+void or_episode_stats_done(const or_params* p, or_env* ev, or_drone* dr, int N) {
     const double freq = 1.0 / p->control_dt;
     const int T = p->ep_len + 1;
     double* s = ev->ep_stats;
@@ -1055,7 +1057,7 @@ void or_env_step(const or_params* p, or_drone* drones, or_env* envs, int e, cons
     }
     ev->last_col = any_nonzero;
     for (int i = 0; i < N; ++i) if (onew[i]) ev->last_col = 1;
-    episode_stats_step(p, ev, dr, N, in_cur, in_prev, onew, wall_new, ceil_new, dist_goal, o, od, time_remain);
+    or_episode_stats_step(p, ev, dr, N, in_cur, in_prev, onew, wall_new, ceil_new, dist_goal, o, od, time_remain);
     for (int i = 0; i < N; ++i) {
         double rc = (any_nonzero && in_cur[i] && !in_prev[i]) ? -1.0 : 0.0;
         rw[i] += p->rew_quadcol_bin * rc;
@@ -1106,7 +1108,7 @@ void or_env_step(const or_params* p, or_drone* drones, or_env* envs, int e, cons
         for (int i = 0; i < N; ++i) or_obst_sdf(p, ev, ev->obs_pos[i], o + (size_t)i * od + od - 9);
     for (int i = 0; i < N; ++i) done[(size_t)e * N + i] = (unsigned char)is_done;
     if (is_done) {
-        episode_stats_done(p, ev, dr, N);
+        or_episode_stats_done(p, ev, dr, N);
         if (term_obs) memcpy(term_obs + (size_t)e * N * od, o, sizeof(double) * (size_t)N * od);
         ev->tick -= 1;                              /* the reset draws at the step's counter */
         or_env_reset(p, drones, envs, e, r, o);     /* in-env auto reset (:836) */

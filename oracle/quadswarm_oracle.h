@@ -260,6 +260,12 @@ void or_collide_drones(double pos1[3], double vel1[3], double omega1[3],
                        or_rng* r, uint32_t gid, uint32_t j);
 void or_collide_wall(const or_params* p, or_drone* d, or_rng* r, uint32_t gid);
 int or_downwash(const or_params* p, or_drone* dr, int N, uint32_t gbase, or_rng* r);   /* 1 when applied */
+/* episode_extra_stats accumulators (quadrotor_multi.py:555-656) and the done row (:739-831); flavor A passes
+ * dist_goal = NULL (it never appends distance_to_goal) and onew = NULL (no obstacles) */
+void or_episode_stats_step(const or_params* p, or_env* ev, or_drone* dr, int N, const int* in_cur, const int* in_prev,
+                           const int* onew, const int* wall_new, const int* ceil_new, const double* dist_goal,
+                           const double* obs, int od, int time_remain);
+void or_episode_stats_done(const or_params* p, or_env* ev, or_drone* dr, int N);
 void or_collide_ceiling(or_drone* d, or_rng* r, uint32_t gid);
 
 /* ---- whole env (flavor B, QuadrotorEnvMulti quadrotor_multi.py) ---- */

@@ -595,6 +595,14 @@ void or_env_reset_a(const or_params* p, or_drone* drones, or_env* envs, int e, o
     ev->success = 0;
     ev->tick = 0;
     ev->episode += 1;
+    /* the episode statistics start over (:605-617) */
+    memset(ev->prev_pair_bits, 0, sizeof ev->prev_pair_bits);
+    ev->st_col = ev->st_room = ev->st_floor = ev->st_wall = ev->st_ceil = ev->st_col_settle = ev->st_col_final = 0;
+    ev->st_ocol = ev->st_ocol_settle = ev->st_o35 = ev->st_o5 = 0;
+    for (int i = 0; i < N; ++i) {
+        dr[i].hit_agent = dr[i].hit_obst = dr[i].reached = dr[i].prev_room = 0;
+        dr[i].prev_wall = dr[i].prev_ceiling = 0;
+    }
 }
 
 /* ------------------------------------------------------------------------------------------ */
@@ -630,8 +638,33 @@ void or_env_step_a(const or_params* p, or_drone* drones, or_env* envs, int e, co
             for (int c = 0; c < 3; ++c) ev->obs_pos[i][c] = d->pos[c];
             ev->heading[i] = d->angle;
         }
+        const int time_remain = p->ep_len - ev->tick;   /* QuadrotorSingle.time_remain, before tick += 1 */
         ev->tick += 1;
         const int tick_done = ev->tick > p->ep_len;
+        /* 1. collisions between drones and with the room (:649-720) -- no forces (apply_collision_force is
+         * False, :203), only the episode_extra_stats bookkeeping */
+        {
+            int in_cur[64] = {0}, in_prev[64] = {0}, wall_new[64], ceil_new[64];
+            unsigned char cur[64 * 64];
+            memset(cur, 0, sizeof cur);
+            for (int i = 0; i < N; ++i)
+                for (int j = i + 1; j < N; ++j) {
+                    const double dx = dr[i].pos[0] - dr[j].pos[0], dy = dr[i].pos[1] - dr[j].pos[1];
+                    const double dz = dr[i].pos[2] - dr[j].pos[2];
+                    if (sqrt(dx * dx + dy * dy + dz * dz) <= p->collision_threshold) {
+                        cur[i * 64 + j] = 1; in_cur[i] = in_cur[j] = 1;
+                    }
+                    if (ev->prev_pair_bits[i * 64 + j]) in_prev[i] = in_prev[j] = 1;
+                }
+            memcpy(ev->prev_pair_bits, cur, sizeof cur);
+            for (int i = 0; i < N; ++i) {   /* calculate_room_collision (:491-504): new wall / ceiling lists */
+                wall_new[i] = dr[i].crashed_wall && !dr[i].prev_wall;
+                ceil_new[i] = dr[i].crashed_ceiling && !dr[i].prev_ceiling;
+                dr[i].prev_wall = wall_new[i];
+                dr[i].prev_ceiling = ceil_new[i];
+            }
+            or_episode_stats_step(p, ev, dr, N, in_cur, in_prev, NULL, wall_new, ceil_new, NULL, NULL, od, time_remain);
+        }
         /* capture reward (:711-735): xy distance of every drone to env 0's goal */
         double rel[64];
         int cap = 0;
@@ -674,8 +707,13 @@ void or_env_step_a(const or_params* p, or_drone* drones, or_env* envs, int e, co
         for (int i = 0; i < N; ++i)
             for (int c = 0; c < 3; ++c) { ev->obs_pos[i][c] = dr[i].pos[c]; ev->obs_vel[i][c] = dr[i].vel[c]; }
     }
-    if (any_done)
+    if (any_done) {
         for (int i = 0; i < N; ++i) dn[i] = 1;
+        /* infos[i]["episode_extra_stats"] (:886-969): distance_to_goal is empty -> np.mean gives nan */
+        or_episode_stats_done(p, ev, dr, N);
+        if (p->scenario_a == 1) ev->ep_stats[OR_ES_SCEN] = 18;   /* Scenario_dynamic_repulsive */
+        for (int i = 0; i < N; ++i) for (int k = 0; k < 3; ++k) dr[i].ep_dist[k] = NAN;
+    }
     or_neighbor_obs_a(p, ev, dr, r, gbase, 0, o, od);
     if (any_done) {
         if (term_obs) memcpy(term_obs + (size_t)e * N * od, o, sizeof(double) * (size_t)N * od);

@@ -416,6 +416,7 @@ __device__ __forceinline__ void reset_env_a(const KP& kp, Drone& d, Ctl& c, floa
 #pragma unroll
     for (int k = 0; k < 4; ++k) { d.rd[k] = 0.f; d.cd[k] = 0.f; }
     d.flags = 0;
+    d.prev = 0;   // prev_drone_collisions = [] (:606)
 }
 
 // scenario.reset() of the selected envs for the goal scenarios (:560, spawn_points None -> spawn at the
@@ -505,6 +506,19 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
     Scen sc;
     if (SCEN && active && di == 0 && q == 0) scen_load(kp, b, env, sc);
 
+    // episode_extra_stats (kp.stats, quadrotor_multi_rewards.py:649-720, 886-969): the env's 11 counters
+    // QS_E_ST_COL.. dealt over its lanes (lane li holds li + LPE t), kept in registers over the ticks
+    constexpr int NCNT = 11, CT = (NCNT + LPE - 1) / LPE;
+    const int li = lane - base;
+    const bool envok = env < kp.E;
+    const uint64_t lmask = (LPE == 64) ? ~0ull : ((1ull << LPE) - 1ull);
+    int cnt[CT], cnt0[CT];
+#pragma unroll
+    for (int t = 0; t < CT; ++t) {
+        const int k = li + LPE * t;
+        cnt[t] = cnt0[t] = (kp.stats && envok && k < NCNT) ? b.env[(QS_E_ST_COL + k) * kp.E + env] : 0;
+    }
+
     bool fin = false, success = eflags & QS_EF_SUCCESS;
     float rw = 0.f, gox = d.goal[0], goy = d.goal[1];
     bool dn = false;
@@ -534,6 +548,43 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
         for (int k = 0; k < 4; ++k) d.ou[k] = d.ou[k] + (kp.ou_theta * (kp.ou_mu - d.ou[k]) + kp.ou_sigma * z[k]);
         for (int s = 0; s < kp.sim_steps; ++s) substep(kp, d, u, d.ou, rng, gid, s);
         ++tick;
+        if (kp.stats) {   // collisions between drones and with the room (:649-720): bookkeeping only
+            if (active && q == 0) xch[2 * (sbase + di)] = make_float4(d.pos[0], d.pos[1], d.pos[2], 0.f);
+            lds_sync();
+            uint64_t cur = 0;
+            constexpr int PJ = (NPAD + Q - 1) / Q;
+            for (int t = 0; t < PJ; ++t) {
+                const int j = q + Q * t;
+                const float4 pj = xch[2 * (sbase + (j < NPAD ? j : NPAD - 1))];
+                const float dx = d.pos[0] - pj.x, dy = d.pos[1] - pj.y, dz = d.pos[2] - pj.z;
+                if (j != di && j < kp.N && fsqrt(dx * dx + dy * dy + dz * dz) <= kp.col_thr) cur |= 1ull << j;
+            }
+            cur = qor<Q>(cur);
+            lds_sync();   // the tile is rewritten next tick
+            const bool uniq = active && cur != 0 && d.prev == 0;   // setdiff1d(flat(cur), flat(prev))
+            d.prev = cur;
+            auto env_count = [&](bool x) { return __popcll((__ballot(x && q == 0) >> base) & lmask); };
+            const bool settle = tick >= kp.st_settle;
+            const bool fin5 = kpm.ep_len - (tick - 1) <= kp.st_final;   // time_remain (before tick += 1)
+            const int col = env_count(uniq) / 2;
+            if (col > 0 && settle && uniq) d.flags |= QS_FL_HIT_AGENT;
+            const bool wall_new = (d.flags & QS_FL_CRASH_WALL) && !(d.flags & QS_FL_PREV_WALL);
+            const bool ceil_new = (d.flags & QS_FL_CRASH_CEIL) && !(d.flags & QS_FL_PREV_CEIL);
+            const bool cfloor = active && (d.flags & QS_FL_CRASH_FLOOR);
+            const bool room_new = active && (cfloor || wall_new || ceil_new) && !(d.flags & QS_FL_PREV_ROOM);
+            d.flags = (d.flags & ~(uint32_t)(QS_FL_PREV_WALL | QS_FL_PREV_CEIL | QS_FL_PREV_ROOM)) |
+                      (wall_new ? QS_FL_PREV_WALL : 0u) | (ceil_new ? QS_FL_PREV_CEIL : 0u) |
+                      (room_new ? (uint32_t)QS_FL_PREV_ROOM : 0u);
+            const int nfl = env_count(cfloor), nw = env_count(active && wall_new), nc = env_count(active && ceil_new);
+            const int nr = env_count(room_new);
+#pragma unroll
+            for (int t = 0; t < CT; ++t) {
+                const int k = li + LPE * t;
+                cnt[t] += k == 0 ? col : k == 1 ? (settle ? nr : 0) : k == 2 ? (settle ? nfl : 0) :
+                          k == 3 ? (settle ? nw : 0) : k == 4 ? (settle ? nc : 0) :
+                          k == 5 ? (settle ? col : 0) : k == 6 ? (fin5 ? col : 0) : 0;
+            }
+        }
         gox = d.goal[0];
         goy = d.goal[1];
         // capture reward (:711-735) against env 0's goal; dones (:882-988)
@@ -577,6 +628,12 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
     }
 
     if (SCEN && active && di == 0 && q == 0 && !fin) scen_store(kp, b, env, sc);   // (a reset stores its own)
+    if (kp.stats)
+#pragma unroll
+        for (int t = 0; t < CT; ++t) {
+            const int k = li + LPE * t;
+            if (envok && !fin && k < NCNT && cnt[t] != cnt0[t]) b.env[(QS_E_ST_COL + k) * kp.E + env] = cnt[t];
+        }
     // ---- observations of the final tick (self obs of the last _step, neighbours after the loop) ----
     const Rng rng_last = env_rng(seed, tick - 1, episode);
     if (q == 0) xch_put_a(xch, sbase + di, d.pos, c.angle, d.vel);
@@ -597,6 +654,36 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
                 b.term[(size_t)(env0 * kp.N + r) * kp.obs_dim + q] = lds[(size_t)r * kp.obs_dim + q];
         }
         lds_sync();
+        if (kp.stats) {   // the finished episodes' episode_extra_stats rows (:886-969)
+            float cv[NCNT];
+#pragma unroll
+            for (int k = 0; k < NCNT; ++k) cv[k] = (float)__shfl(cnt[k / LPE], base + k % LPE);
+            auto env_bits = [&](bool x) { return (__ballot(x && q == 0) >> base) & lmask; };
+            const uint64_t hit_a = env_bits(active && (d.flags & QS_FL_HIT_AGENT));
+            const uint64_t all = env_bits(active);
+            if (active && fin && q == 0) {
+                const float n = (float)kp.N;
+                const uint64_t ok = all & ~hit_a;   // agent_col_obst stays 1 (no obstacles in flavor A)
+                float* er = b.estats + (size_t)g * QS_NES;
+#pragma unroll
+                for (int k = 0; k < NCNT; ++k) er[QS_ES_COL + k] = cv[k];
+                er[QS_ES_SUCCESS] = 0.f;                           // reached_goal is never set (:797-802)
+                er[QS_ES_DEADLOCK] = (float)__popcll(ok) / n;
+                er[QS_ES_COLRATE] = 1.f - (float)__popcll(ok) / n;
+                er[QS_ES_NCOLRATE] = 1.f - (float)__popcll(all & ~hit_a) / n;
+                er[QS_ES_OCOLRATE] = 0.f;
+                er[QS_ES_SCEN] = repulsive ? 18.f : (SCEN ? (float)b.env[QS_E_SC_MODE * kp.E + env] : 0.f);
+                const float nan = __builtin_nanf("");                  // np.mean of the empty distance list
+                er[QS_ES_D1] = nan; er[QS_ES_D3] = nan; er[QS_ES_D5] = nan;
+                er[QS_ES_REPLAY] = 0.f;
+            }
+#pragma unroll
+            for (int t = 0; t < CT; ++t) {   // the episode statistics start over (:605-617)
+                const int k = li + LPE * t;
+                if (envok && fin && k < NCNT) b.env[(QS_E_ST_COL + k) * kp.E + env] = 0;
+            }
+            if (fin) d.prev = 0;
+        }
         const float sh = c.angle, sv[3] = {d.vel[0], d.vel[1], d.vel[2]};  // QuadrotorEnvMulti.heading / .vel
         const Rng rr = env_rng(seed, tick, episode);
         if (SCEN)
@@ -703,6 +790,8 @@ __global__ __launch_bounds__(64) void reset_kernel_a(const KP* __restrict__ kpp,
             b.env[QS_E_TICK * kp.E + env] = 0;
             b.env[QS_E_EPISODE * kp.E + env] = episode + 1;
             b.env[QS_E_FLAGS * kp.E + env] = QS_EF_STALE | QS_EF_HAS_POS;
+            if (kp.stats)
+                for (int k = 0; k < 11; ++k) b.env[(QS_E_ST_COL + k) * kp.E + env] = 0;
             b.envf[QS_ENVF_TARGET_X * kp.E + env] = tx;
             b.envf[QS_ENVF_TARGET_Y * kp.E + env] = ty;
         }

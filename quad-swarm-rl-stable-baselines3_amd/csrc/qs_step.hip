@@ -350,7 +350,7 @@ static qs::KP make_kp(const qs_config* c, const qs_layout& L) {
     if (!c->use_obstacles && c->scenario >= QS_SCEN_MIX && c->scenario <= QS_SCEN_RUN_AWAY)
         k.scen_b = c->scenario == QS_SCEN_MIX ? 10 : c->scenario - QS_SCEN_MIX;
     if (c->flavor == QS_FLAVOR_A) make_kp_a(c, k);
-    if (c->episode_stats && c->flavor == QS_FLAVOR_B) {   // quadrotor_multi.py:156-161, 651-655, 761-774
+    if (c->episode_stats) {   // quadrotor_multi.py:156-161, 651-655, 761-774; quadrotor_multi_rewards.py:131-136
         double freq = 1.0 / (double)c->control_dt;   // control_freq (100 for the reference's 0.01 s)
         if (fabs(freq - (double)llround(freq)) < 1e-4) freq = (double)llround(freq);
         k.stats = 1;

@@ -330,5 +330,5 @@ class QuadSwarmConfig:
                 c.dr_num_sizes = len(sizes)
                 for i, v in enumerate(sizes):
                     c.dr_sizes[i] = float(v)
-        c.episode_stats = 1 if (self.episode_stats and self.flavor == "B") else 0
+        c.episode_stats = 1 if self.episode_stats else 0
         return c

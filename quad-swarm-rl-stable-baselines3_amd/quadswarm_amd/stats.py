@@ -17,7 +17,8 @@ NES = 24
 # (scenarios/utils.py:7-10) + run_away for the goal scenarios, 16 + mode for the obstacle ones
 SCENARIO_NAMES = {0: "static_same_goal", 1: "static_diff_goal", 2: "ep_lissajous3D", 3: "ep_rand_bezier",
                   4: "dynamic_same_goal", 5: "dynamic_diff_goal", 6: "dynamic_formations", 7: "swap_goals",
-                  8: "swarm_vs_swarm", 9: "run_away", 16: "o_random", 17: "o_static_same_goal"}
+                  8: "swarm_vs_swarm", 9: "run_away", 16: "o_random", 17: "o_static_same_goal",
+                  18: "dynamic_repulsive"}   # flavor A's target-chasing scenario
 
 
 def episode_extra_stats(row, use_obstacles=False):

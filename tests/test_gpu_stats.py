@@ -153,3 +153,70 @@ def test_vec_env_raises_on_nan_reward():
         venv.step(a)
     assert venv.counters()["nonfinite_rew"] == 1
     venv.close()
+
+
+def test_flavor_a_episode_stats_match_oracle():
+    """Flavor A (quadrotor_multi_rewards.py:649-720 per tick, :886-969 at done): the A kernel's per-tick collision
+    and room bookkeeping against the oracle's (pinned to the reference's dicts by a_traj_n8stats), from identical
+    states every step; pairs 5 cm apart and drones driven into the ceiling / floor keep every counter busy."""
+    from parity_utils import gpu_to_oracle_a, oracle_params_a, oracle_to_gpu_a
+    E, N = 128, 8
+    cfg = QuadSwarmConfig.sb_train(num_envs=E, num_agents=N, neighbor_obs_type="dist_angle", seed=4,
+                                   episode_duration=3.0)
+    env = QuadSwarmEnv(cfg)
+    assert env.estats is not None
+    oenv = O.OracleEnvA(oracle_params_a(cfg), seed=4)
+    oenv.set_capture_radius(0.0)
+    env.reset()
+    oenv.reset()
+    ep = cfg.ep_len
+    top = float(cfg.room_dims[2])
+    for e in range(E):
+        oenv.envs[e].tick = ep - 120 + 8 * (e % 7)     # past the grace period, episodes end over ~15 steps
+        oenv.envs[e].capture_radius = 0.0
+    rng = np.random.default_rng(5)
+    n_done, seen = 0, np.zeros(len(COUNT_COLS))
+    for t in range(24):
+        for e in range(E):
+            dr = [oenv.drones[e * N + i] for i in range(N)]
+            if t % 3 == 0:
+                for c in range(3):
+                    dr[1].pos[c] = dr[0].pos[c] + (0.05 if c == 0 else 0.0)
+                dr[4].pos[2], dr[4].vel[2] = top - 0.02, 2.0
+                dr[5].pos[2], dr[5].vel[2] = 0.06, -2.0
+        oracle_to_gpu_a(oenv, env)
+        a = rng.uniform(-1, 1, (env.I, 2)).astype(np.float32)
+        _, _, done, _ = env.step(torch.from_numpy(a).cuda())
+        _, _, w_done, _, _ = oenv.step(a.astype(np.float64))
+        np.testing.assert_array_equal(done.cpu().numpy().astype(bool), w_done, err_msg=f"step {t}")
+        est = env.estats.double().cpu().numpy()
+        for e in np.flatnonzero(w_done.reshape(E, N)[:, 0]):
+            got, want = est[e * N:(e + 1) * N], _oracle_rows(oenv, e)
+            np.testing.assert_array_equal(got[:, COUNT_COLS], want[:, COUNT_COLS], err_msg=f"step {t} env {e}")
+            for c in (S.ES_SUCCESS, S.ES_DEADLOCK, S.ES_COLRATE, S.ES_NCOLRATE, S.ES_OCOLRATE):
+                np.testing.assert_allclose(got[:, c], want[:, c], rtol=1e-6, atol=1e-7, err_msg=f"{t} {e} col {c}")
+            assert np.isnan(got[:, [S.ES_D1, S.ES_D3, S.ES_D5]]).all()     # np.mean of the empty list
+            assert (got[:, S.ES_SCEN] == 18).all()                          # dynamic_repulsive
+            seen += got[0, COUNT_COLS] != 0
+            n_done += 1
+        gpu_to_oracle_a(env, oenv)
+    assert n_done >= E
+    for k, c in enumerate(COUNT_COLS[:7]):
+        if c not in (S.ES_FLOOR, S.ES_WALL):
+            assert seen[k] > 0, c
+
+
+def test_flavor_a_vec_env_infos():
+    venv = GpuQuadVecEnv(QuadSwarmConfig.sb_train(num_envs=16, num_agents=4, seed=1, episode_duration=0.4,
+                                                  initial_capture_radius=0.0))
+    venv.reset()
+    rng = np.random.default_rng(0)
+    n_done = 0
+    for t in range(12):
+        _, _, dones, infos = venv.step(rng.uniform(-1, 1, (64, 2)).astype(np.float32))
+        for i in np.flatnonzero(dones):
+            x = infos[int(i)]["episode_extra_stats"]
+            assert "dynamic_repulsive/num_collisions" in x and np.isnan(x["distance_to_goal_1s"])
+            n_done += 1
+    assert n_done >= 64
+    venv.close()

@@ -261,7 +261,7 @@ def snapshot(env):
         capture=np.array(float(env.capture_radius)))
 
 
-def gen_traj(name, n, steps, seed, capture_schedule=None, act_scale=1.0, setup=None, **kw):
+def gen_traj(name, n, steps, seed, capture_schedule=None, act_scale=1.0, setup=None, stats=False, **kw):
     np.random.seed(seed)
     env = make_env_A(n, seed=seed, **kw)
     begin()
@@ -275,10 +275,14 @@ def gen_traj(name, n, steps, seed, capture_schedule=None, act_scale=1.0, setup=N
     caps = np.array([capture_schedule(t) for t in range(steps)]) if capture_schedule else \
         np.full(steps, env.capture_radius)
     obs, rew, done, term, rinfo = [], [], [], [], []
+    events = []
     begin()
     for t in range(steps):
         env.set_capture_radius(float(caps[t]))
-        o, r, dn, _ = env.step(actions[t])
+        o, r, dn, info = env.step(actions[t])
+        if stats and any(dn):   # infos[i]["episode_extra_stats"] (quadrotor_multi_rewards.py:886-969)
+            events.append({"step": t, "agents": [{k_: float(v) for k_, v in info[i]["episode_extra_stats"].items()}
+                                                 for i in range(n)]})
         o = np.array(o, dtype=np.float64)
         term.append(o.copy())
         ri = -1.0
@@ -289,6 +293,10 @@ def gen_traj(name, n, steps, seed, capture_schedule=None, act_scale=1.0, setup=N
         obs.append(o); rew.append(np.array(r, dtype=np.float64)); done.append(np.array(dn, dtype=np.float64))
         rinfo.append(ri)
     tv, gt = end()
+    if stats:
+        import json
+        with open(os.path.join(OUT, f"a_traj_{name}_stats.json"), "w") as f:
+            json.dump({"name": name, "events": events}, f, indent=0, sort_keys=True)
     final = snapshot(env)
     c = env.cfg
     np.savez_compressed(
@@ -337,13 +345,31 @@ def setup_stacks_a(env):
         env.pos[i] = d.pos
 
 
+def setup_stats_a(env):
+    """Past the 1.5 s grace (tick 140 of a 3 s episode); drone pairs 4-6 cm apart (collisions after settle),
+    one drone rising into the 3 m ceiling and one dropping to the floor (room lists)."""
+    for e in env.envs:
+        e.tick = 140
+    ds = [e.dynamics for e in env.envs]
+    ds[1].pos = ds[0].pos + np.array([0.05, 0.0, 0.0])
+    ds[3].pos = ds[2].pos + np.array([0.0, 0.06, 0.0])
+    ds[4].pos = np.array([0.5, 0.5, 2.96]); ds[4].vel = np.array([0.0, 0.0, 3.0])
+    ds[5].pos = np.array([-0.5, 0.5, 0.08]); ds[5].vel = np.array([0.0, 0.0, -3.0])
+    for i, d in enumerate(ds):
+        env.pos[i] = d.pos
+
+
 def main_extra(which):
     """Fixtures added later, generated on their own (the ones above stay byte-identical):
-      dw   use_downwash (quadrotor_multi_rewards.py:810-815) with stacked drone pairs, 8 drones"""
+      dw     use_downwash (quadrotor_multi_rewards.py:810-815) with stacked drone pairs, 8 drones
+      stats  episode_extra_stats of the episodes that end (quadrotor_multi_rewards.py:886-969)"""
     os.makedirs(OUT, exist_ok=True)
     if "dw" in which:
         gen_traj("n8dw", 8, 40, seed=36, ntype="dist_angle", repr_="cdist_cdistdot_dist_distdot_angle_angledot",
                  capture_schedule=lambda t: 0.05, ep_time=30.0, downwash=True, setup=setup_stacks_a)
+    if "stats" in which:
+        gen_traj("n8stats", 8, 40, seed=37, ntype="dist_angle", repr_="cdist_cdistdot_dist_distdot_angle_angledot",
+                 capture_schedule=lambda t: 0.01, ep_time=3.0, setup=setup_stats_a, stats=True)
 
 
 if __name__ == "__main__":

@@ -39,6 +39,7 @@ for s in "$@"; do
       python tools/kt_summary.py gpurun_out/kt_on gpurun_out/kt_off > gpurun_out/kt_summary.txt 2>&1
       rm -f gpurun_out/kt_*/*/*kernel_trace.csv gpurun_out/kt_*/*kernel_trace.csv
       ;;
+    benchn64) step bench_n64 300 python bench.py --config n64 --steps 1000 --cpu-seconds 5 --e2e-iters 0 ;;
     par64) step gpu_tests_64 600 python -u -m pytest tests/test_gpu_parity.py -v -k "64" --timeout 300 --timeout-method thread ;;
     benchblocks) step bench_blocks 600 python bench.py --steps 2000 --streams 4 --no-cpu-baseline --e2e-iters 0 ;;
     bench) step bench 600 python bench.py ;;
