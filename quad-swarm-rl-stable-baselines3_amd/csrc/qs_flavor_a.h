@@ -419,6 +419,22 @@ __device__ __forceinline__ void reset_env_a(const KP& kp, Drone& d, Ctl& c, floa
     d.prev = 0;   // prev_drone_collisions = [] (:606)
 }
 
+// drone-drone collision row of this lane's drone (calculate_collision_matrix, collisions/quadrotors.py:62-91)
+// when the env is one 16-lane DPP row (8 drones x 2 sub-lanes): the row rotated by Q k lanes brings drone
+// di + k (mod 8) -- its position and its index -- to this lane, no LDS round trip.  Squared distances
+// against the squared threshold (the same order as |r| <= thr up to the last bit).
+template <int Q, int K>
+__device__ __forceinline__ void col_row16(const KP& kp, const Drone& d, int di, float thr2, uint64_t& cur) {
+    if constexpr (K * Q < 16) {
+        constexpr int C = 0x120 + K * Q;   // DPP row_ror:K*Q
+        const float dx = d.pos[0] - dpp_f<C>(d.pos[0]), dy = d.pos[1] - dpp_f<C>(d.pos[1]);
+        const float dz = d.pos[2] - dpp_f<C>(d.pos[2]);
+        const int j = dpp_i<C>(di);
+        if (j < kp.N && dx * dx + dy * dy + dz * dz <= thr2) cur |= 1ull << j;
+        col_row16<Q, K + 1>(kp, d, di, thr2, cur);
+    }
+}
+
 // scenario.reset() of the selected envs for the goal scenarios (:560, spawn_points None -> spawn at the
 // goal, :569-573): the env's lead lane fills the LDS goal table (draw key = the env's drone 0, stream
 // S_SCN_RESET) and stores the scenario state; every selected drone takes its goal.  Whole wave.
@@ -549,18 +565,25 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
         for (int s = 0; s < kp.sim_steps; ++s) substep(kp, d, u, d.ou, rng, gid, s);
         ++tick;
         if (kp.stats) {   // collisions between drones and with the room (:649-720): bookkeeping only
-            if (active && q == 0) xch[2 * (sbase + di)] = make_float4(d.pos[0], d.pos[1], d.pos[2], 0.f);
-            lds_sync();
             uint64_t cur = 0;
-            constexpr int PJ = (NPAD + Q - 1) / Q;
-            for (int t = 0; t < PJ; ++t) {
-                const int j = q + Q * t;
-                const float4 pj = xch[2 * (sbase + (j < NPAD ? j : NPAD - 1))];
-                const float dx = d.pos[0] - pj.x, dy = d.pos[1] - pj.y, dz = d.pos[2] - pj.z;
-                if (j != di && j < kp.N && fsqrt(dx * dx + dy * dy + dz * dz) <= kp.col_thr) cur |= 1ull << j;
+            const float thr2 = kp.col_thr * kp.col_thr;
+#ifndef QS_DIAG_A_NOCOL   // diagnostic builds only (QS_JIT_OPTS)
+            if constexpr (LPE == 16 && NPAD * Q == 16) {
+                col_row16<Q, 1>(kp, d, di, thr2, cur);
+            } else {
+                if (active && q == 0) xch[2 * (sbase + di)] = make_float4(d.pos[0], d.pos[1], d.pos[2], 0.f);
+                lds_sync();
+                constexpr int PJ = (NPAD + Q - 1) / Q;
+                for (int t = 0; t < PJ; ++t) {
+                    const int j = q + Q * t;
+                    const float4 pj = xch[2 * (sbase + (j < NPAD ? j : NPAD - 1))];
+                    const float dx = d.pos[0] - pj.x, dy = d.pos[1] - pj.y, dz = d.pos[2] - pj.z;
+                    if (j != di && j < kp.N && dx * dx + dy * dy + dz * dz <= thr2) cur |= 1ull << j;
+                }
+                cur = qor<Q>(cur);
+                lds_sync();   // the tile is rewritten next tick
             }
-            cur = qor<Q>(cur);
-            lds_sync();   // the tile is rewritten next tick
+#endif
             const bool uniq = active && cur != 0 && d.prev == 0;   // setdiff1d(flat(cur), flat(prev))
             d.prev = cur;
             auto env_count = [&](bool x) { return __popcll((__ballot(x && q == 0) >> base) & lmask); };
@@ -575,14 +598,16 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
             d.flags = (d.flags & ~(uint32_t)(QS_FL_PREV_WALL | QS_FL_PREV_CEIL | QS_FL_PREV_ROOM)) |
                       (wall_new ? QS_FL_PREV_WALL : 0u) | (ceil_new ? QS_FL_PREV_CEIL : 0u) |
                       (room_new ? (uint32_t)QS_FL_PREV_ROOM : 0u);
-            const int nfl = env_count(cfloor), nw = env_count(active && wall_new), nc = env_count(active && ceil_new);
-            const int nr = env_count(room_new);
+            if (__ballot(cfloor || wall_new || ceil_new || room_new || col > 0)) {   // rare: something to count
+                const int nfl = env_count(cfloor), nw = env_count(active && wall_new);
+                const int nc = env_count(active && ceil_new), nr = env_count(room_new);
 #pragma unroll
-            for (int t = 0; t < CT; ++t) {
-                const int k = li + LPE * t;
-                cnt[t] += k == 0 ? col : k == 1 ? (settle ? nr : 0) : k == 2 ? (settle ? nfl : 0) :
-                          k == 3 ? (settle ? nw : 0) : k == 4 ? (settle ? nc : 0) :
-                          k == 5 ? (settle ? col : 0) : k == 6 ? (fin5 ? col : 0) : 0;
+                for (int t = 0; t < CT; ++t) {
+                    const int k = li + LPE * t;
+                    cnt[t] += k == 0 ? col : k == 1 ? (settle ? nr : 0) : k == 2 ? (settle ? nfl : 0) :
+                              k == 3 ? (settle ? nw : 0) : k == 4 ? (settle ? nc : 0) :
+                              k == 5 ? (settle ? col : 0) : k == 6 ? (fin5 ? col : 0) : 0;
+                }
             }
         }
         gox = d.goal[0];

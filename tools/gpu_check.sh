@@ -40,6 +40,14 @@ for s in "$@"; do
       rm -f gpurun_out/kt_*/*/*kernel_trace.csv gpurun_out/kt_*/*kernel_trace.csv
       ;;
     benchn64) step bench_n64 300 python bench.py --config n64 --steps 1000 --cpu-seconds 5 --e2e-iters 0 ;;
+    abstatsa)
+      step a8_nost 300 python bench.py --config a8 --steps 1000 --no-cpu-baseline --e2e-iters 0 --no-episode-stats
+      CONFIG=a8 STEPS=1000 step a8_ab 600 bash tools/ab_jit.sh base: nocol:-DQS_DIAG_A_NOCOL
+      ;;
+    statsa)
+      step stats_a 600 python -u -m pytest tests/test_gpu_stats.py tests/test_gpu_parity_a.py -v --timeout 200 --timeout-method thread
+      step a8_after 300 python bench.py --config a8 --steps 1000 --no-cpu-baseline --e2e-iters 0
+      ;;
     par64) step gpu_tests_64 600 python -u -m pytest tests/test_gpu_parity.py -v -k "64" --timeout 300 --timeout-method thread ;;
     benchblocks) step bench_blocks 600 python bench.py --steps 2000 --streams 4 --no-cpu-baseline --e2e-iters 0 ;;
     bench) step bench 600 python bench.py ;;
