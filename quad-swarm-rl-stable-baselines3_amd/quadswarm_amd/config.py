@@ -143,6 +143,10 @@ class QuadSwarmConfig:
             obst_size_min=g("obst_size_min", "quads_obst_size_min", default=0.3),
             obst_size_max=g("obst_size_max", "quads_obst_size_max", default=0.6))
         if flavor == "A":
+            # sb_train wraps the env in ExperienceReplayWrapper(env, 0.5, ...) when cfg.use_replay_buffer
+            # (sb3_quad_env.py:43-45)
+            # only; its QuadrotorEnvConfig's replay_buffer_sample_prob (0.75) is the SF runs' knob, unused here
+            c.replay_buffer_sample_prob = 0.5 if g("use_replay_buffer", default=False) else 0.0
             # quadrotor_multi_rewards builds its dynamics from cfg.dynamics_change only (the
             # thrust_noise_ratio it computes at :46-49 is never used), default Crazyflie noise 0.05
             dc = g("dynamics_change", default=None) or {}
@@ -255,7 +259,13 @@ class QuadSwarmConfig:
                 raise NotImplementedError(f"quads_mode {self.quads_mode!r} not implemented for flavor A "
                                           "(dynamic_repulsive or a goal scenario of create_scenario)")
         if self.replay_buffer_sample_prob > 0 and self.flavor != "B":
-            raise NotImplementedError("experience replay is implemented for flavor B")
+            # The reference's flavor-A replay stack (sb3_quad_env.py:43-45) cannot step: its step reads
+            # infos[0]["rewards"]["rew_crash"] while the replay buffer is inactive (quadrotor_multi_rewards.py:
+            # 871-872), and flavor A's per-drone info carries an empty "rewards" dict (quadrotor_single_rewards.py:
+            # 457), so the first step raises KeyError (tests/golden/a_replay_outcome.json, from the reference
+            # itself).  There is no reference behaviour to reproduce, so the build refuses it the same way.
+            raise KeyError("rew_crash: the reference's flavor-A env cannot run the experience-replay wrapper "
+                           "(quadrotor_multi_rewards.py:872 reads a reward the flavor-A step does not report)")
         if not 0.0 <= self.replay_buffer_sample_prob <= 1.0:
             raise ValueError("replay_buffer_sample_prob must be in [0, 1]")
         if not 1 <= self.num_agents <= N.MAX_AGENTS:

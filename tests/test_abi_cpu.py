@@ -272,3 +272,43 @@ def test_config_kp_words():
     assert L.qs_config_kp_words(qc, buf, 10) < 0      # buffer too small
     # the parameter block starts with E, N, I, obs_dim
     assert list(buf[:4]) == [64, 8, 512, 54]
+
+
+def _reference_env_config(**over):
+    """The reference's own QuadrotorEnvConfig defaults (swarm_rl/global_cfg.py), as recorded by
+    tools/gen_golden_a_replay.py into tests/golden/quadrotor_env_config.json."""
+    import json
+    import types
+    with open(os.path.join(os.path.dirname(__file__), "golden", "quadrotor_env_config.json")) as f:
+        d = json.load(f)
+    d.update(over)
+    return types.SimpleNamespace(**d)
+
+
+def test_from_reference_cfg_real_field_set():
+    ref = _reference_env_config()
+    c = QuadSwarmConfig.from_reference_cfg(ref, num_envs=13)
+    assert c.flavor == "A" and c.num_envs == 13 and c.num_agents == ref.num_agents
+    assert c.obs_repr == ref.obs_repr and c.neighbor_obs_type == ref.neighbor_obs_type
+    assert c.quads_mode == ref.quads_mode and tuple(c.room_dims) == tuple(ref.room_dims)
+    # flavor A: the replay wrapper comes only from use_replay_buffer (sb3_quad_env.py:43-45), not from the
+    # SF runs' replay_buffer_sample_prob (0.75 in the same dataclass)
+    assert ref.replay_buffer_sample_prob == 0.75 and c.replay_buffer_sample_prob == 0.0
+    q = c.to_qs_config()
+    assert q.capture_radius == ref.initial_capture_radius and q.cam_px_noise == ref.pixel_noise_cam
+    assert c.ep_len == int(ref.episode_duration * ref.sim_freq / ref.sim_steps)
+
+
+def test_flavor_a_replay_refused_like_the_reference():
+    """The reference's flavor-A replay stack raises KeyError('rew_crash') on its first step
+    (tests/golden/a_replay_outcome.json, generated by running the reference's own wrapper + env)."""
+    import json
+    with open(os.path.join(os.path.dirname(__file__), "golden", "a_replay_outcome.json")) as f:
+        rec = json.load(f)
+    assert [c["n"] for c in rec["cases"]] == [8, 4, 2]
+    for case in rec["cases"]:
+        assert case["step_error"] == "KeyError: 'rew_crash'" and case["step_error_at"] == 0
+    c = QuadSwarmConfig.from_reference_cfg(_reference_env_config(use_replay_buffer=True), num_envs=4)
+    assert c.replay_buffer_sample_prob == 0.5
+    with pytest.raises(KeyError, match="rew_crash"):
+        c.to_qs_config()
