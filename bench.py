@@ -187,6 +187,20 @@ def e2e_settings(cfg):
     return pc, PPOConfig(n_steps=128, n_epochs=1, gae_lambda=1.0, max_grad_norm=5.0), 16
 
 
+def update_flops_per_sample(pol, obs_dim, act_dim, dev, rows=256):
+    """FLOPs of one sample's PPO update (evaluate_actions forward + backward), counted by torch's
+    FlopCounterMode (GEMM / addmm / bmm flops) on a small batch of the same policy."""
+    import torch
+    from torch.utils.flop_counter import FlopCounterMode
+    obs = torch.randn(rows, obs_dim, device=dev)
+    act = torch.rand(rows, act_dim, device=dev) * 1.8 - 0.9
+    with FlopCounterMode(display=False) as fc:
+        v, lp, _ = pol.evaluate_actions(obs, act)
+        (v.sum() + lp.sum()).backward()
+    pol.zero_grad(set_to_none=False)
+    return fc.get_total_flops() / rows
+
+
 def end_to_end(env, cfg, dev, world, iters, n_steps=None, log=None):
     """Timed PPO iterations (rollout + GAE + update) on the bench's env shard."""
     import torch
@@ -235,6 +249,10 @@ def end_to_end(env, cfg, dev, world, iters, n_steps=None, log=None):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el, t_roll, t_train = (float(x) for x in t.tolist())
     nparam = sum(p.numel() for p in pol.parameters())
+    # the update's GEMM work against the fp32 matrix-core peak (MI355X_MICROARCH: 157.3 TF dense f32)
+    fps = update_flops_per_sample(pol, env.obs_dim, env.act_dim, dev)
+    upd_tf = fps * samples * pcfg.n_epochs / (t_train / iters) / 1e12
+    tr.bucket.zero()
     return {
         "metric": "end-to-end PPO agent-steps/s (rollout + GAE + update; weak scaling, one gradient "
                   "all-reduce per minibatch)",
@@ -247,6 +265,8 @@ def end_to_end(env, cfg, dev, world, iters, n_steps=None, log=None):
                   f"rnn {pc.rnn_size}, core {pc.rnn_type or 'identity'} x{pc.rnn_num_layers if pc.rnn_type else 0}, "
                   f"fp32 (torch/hipBLASLt GEMMs)",
         "gemm_table": tuned,
+        "update_flop_per_sample": round(fps), "update_tflops": round(upd_tf, 2),
+        "update_frac_fp32_mfma_peak": round(upd_tf / 157.3, 3),
         "last_update": {k: (round(v, 6) if isinstance(v, float) else v) for k, v in stats.items()},
     }
 
@@ -304,14 +324,28 @@ class Blocks:
                         self._graph(i, L).replay()
                 self.replays += 1
 
+    def upload(self):
+        """hipGraphUpload every captured graph on its stream: the executable graph is made device-resident
+        before anything is timed (otherwise its first replay, inside the timed region, pays the upload)."""
+        import ctypes
+        hip = ctypes.CDLL("libamdhip64.so")
+        for (i, _), g in self.graphs.items():
+            st = self.entries[i][2]
+            rc = hip.hipGraphUpload(ctypes.c_void_p(g.raw_cuda_graph_exec()), ctypes.c_void_p(st.cuda_stream))
+            if rc != 0:
+                raise RuntimeError(f"hipGraphUpload failed ({rc})")
+        self.torch.cuda.synchronize(self.dev)
+
     def timed(self, n, stream):
-        """n steps bracketed by HIP events on `stream` (the blocks' streams join it on both sides)"""
+        """n steps bracketed by HIP events on `stream` (the blocks' streams join it on both sides; one
+        handle runs on `stream` itself, so no cross-stream waits sit in the timed region)"""
         ev0, ev1 = self.torch.cuda.Event(enable_timing=True), self.torch.cuda.Event(enable_timing=True)
+        joins = [st for _, _, st in self.entries if st is not stream]
         ev0.record(stream)
-        for _, _, st in self.entries:
+        for st in joins:
             st.wait_stream(stream)
         self.run(n)
-        for _, _, st in self.entries:
+        for st in joins:
             stream.wait_stream(st)
         ev1.record(stream)
         return ev0, ev1
@@ -442,6 +476,8 @@ def main():
     run = blocks if S > 1 else one
     run.replays = run.eager_steps = 0
     run.prepare([args.warmup, args.steps])
+    if run.chunk:
+        run.upload()
 
     run.run(args.warmup)
     torch.cuda.synchronize(dev)
