@@ -594,10 +594,14 @@ __device__ __forceinline__ void load_drone_q(const KP& kp, const Bufs& b, int g,
     unpack_words_q(dw, d);
 }
 
-// ST: also the stats words DRONE_WORDS + k whose bit k of stmask is set (stw = their values)
+// ST: also the stats words DRONE_WORDS + k whose bit k of stmask is set (stw = their values).
+// old (optional): the words this sub-lane loaded at the start of the step (DroneWords::r): a word whose bits
+// did not change is not written back -- the goal, the previous-collision row and, for a drone resting on the
+// floor, most of its state.  Only for the step's first store of the drone (a reset stores again, unconditionally).
 template <int Q, bool ST = false>
 __device__ __forceinline__ void store_drone_q(const KP& kp, const Bufs& b, int g, int q, bool active, const Drone& d,
-                                              const float* stw = nullptr, uint32_t stmask = 0u) {
+                                              const float* stw = nullptr, uint32_t stmask = 0u,
+                                              const uint32_t* old = nullptr) {
     constexpr int NW = ST ? LOAD_WORDS : DRONE_WORDS;
     uint32_t wv[NW];
 #pragma unroll
@@ -632,11 +636,16 @@ __device__ __forceinline__ void store_drone_q(const KP& kp, const Bufs& b, int g
 #pragma unroll
         for (int k = 1; k < Q; ++k)
             if (q == k && t * Q + k < NW) v = wv[t * Q + k];
-        const bool wr = w < DRONE_WORDS || (w < NW && ((stmask >> (w - DRONE_WORDS)) & 1u));
+        bool wr = w < DRONE_WORDS || (w < NW && ((stmask >> (w - DRONE_WORDS)) & 1u));
+        if (old) wr = wr && v != old[t];
         if (active && wr) st_wt1(rs, drone_word_off(kp, b, w, go), 0u, v);
     }
 }
 
+// Experiment knob: drone words unchanged by the step are not stored back (store_drone_q's `old`).
+#ifndef QS_STORE_CHANGED
+#define QS_STORE_CHANGED 0   // A/B on MI355X: C3 9.45 vs 9.22 us, C4 14.59 vs 14.01 with it on (slower)
+#endif
 // Sub-lanes per drone of the flavor-B step kernel (QS_QB; 64 / NPAD when an env would not fit a wave).
 #ifndef QS_QB
 #define QS_QB 4
@@ -1192,8 +1201,13 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
 #ifdef QS_DIAG_NOST_RSTORE
     stmask = 0u;
 #endif
-    if (kp.stats) store_drone_q<Q, true>(kp, b, g, q, active, d, stw, stmask);
-    else store_drone_q<Q>(kp, b, g, q, active, d);
+#if QS_STORE_CHANGED && !defined(QS_DIAG_NOLOAD)
+    const uint32_t* old_words = dw.r;
+#else
+    const uint32_t* old_words = nullptr;
+#endif
+    if (kp.stats) store_drone_q<Q, true>(kp, b, g, q, active, d, stw, stmask, old_words);
+    else store_drone_q<Q>(kp, b, g, q, active, d, nullptr, 0u, old_words);
 #else
     if (lead) store_drone(kp, b, g, d);
     if (lead)
