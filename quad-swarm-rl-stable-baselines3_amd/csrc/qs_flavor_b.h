@@ -642,6 +642,10 @@ __device__ __forceinline__ void store_drone_q(const KP& kp, const Bufs& b, int g
     }
 }
 
+// The env's episode-stat counters are stored once at the end of the step rather than where they change.
+#ifndef QS_CNT_DEFER
+#define QS_CNT_DEFER 1
+#endif
 // Experiment knob: drone words unchanged by the step are not stored back (store_drone_q's `old`).
 #ifndef QS_STORE_CHANGED
 #define QS_STORE_CHANGED 0   // A/B on MI355X: C3 9.45 vs 9.22 us, C4 14.59 vs 14.01 with it on (slower)
@@ -811,6 +815,7 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     const int li = lane - lbase;
     const bool envok = env < kp.E;
     int cnt[CT];
+    bool cdirty[CT];   // the counter changed this step: stored once, at the end of the step (QS_CNT_DEFER)
 #ifdef QS_DIAG_CNT_AOS   // diagnostic builds only: the counters env-major in the estats rows (layout experiment)
     auto cnt_at = [&](int k) -> int32_t* { return reinterpret_cast<int32_t*>(b.estats) + (size_t)env * kp.N * QS_NES + k; };
 #else
@@ -820,6 +825,7 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     for (int t = 0; t < CT; ++t) {
         const int k = li + LPE * t;
         cnt[t] = (kp.stats && envok && k < NCNT) ? *cnt_at(k) : 0;
+        cdirty[t] = false;
     }
     Drone d;   // every sub-lane holds the whole drone
 #if defined(QS_DIAG_NOLOAD)   // diagnostic builds only (QS_JIT_OPTS): phase-removal timing experiments
@@ -1059,7 +1065,11 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
             if (envok && k < NCNT && inc != 0) {
 #endif
                 cnt[t] += inc;
+#if QS_CNT_DEFER
+                cdirty[t] = true;
+#else
                 *cnt_at(k) = cnt[t];
+#endif
             }
         }
     }
@@ -1299,7 +1309,14 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
 #pragma unroll
             for (int t = 0; t < CT; ++t) {
                 const int k = li + LPE * t;
-                if (envok && done && k < NCNT) b.env[(QS_E_ST_COL + k) * kp.E + env] = 0;
+                if (envok && done && k < NCNT) {
+#if QS_CNT_DEFER
+                    cnt[t] = 0;
+                    cdirty[t] = true;
+#else
+                    b.env[(QS_E_ST_COL + k) * kp.E + env] = 0;
+#endif
+                }
             }
         }
         float sv[3] = {d.vel[0], d.vel[1], d.vel[2]};  // QuadrotorEnvMulti.vel seen by the reset (:477)
@@ -1396,6 +1413,17 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
             if (nf != ef) b.env[QS_E_FLAGS * kp.E + env] = nf;
         }
     }
+#if QS_CNT_DEFER
+    // the env's episode counters that changed this step (a finished env's zeroed ones included), after every
+    // other global access of the step: a store issued mid-step made the step's later memory waits wait for it
+    if (kp.stats) {
+#pragma unroll
+        for (int t = 0; t < CT; ++t) {
+            const int k = li + LPE * t;
+            if (envok && k < NCNT && cdirty[t]) *cnt_at(k) = cnt[t];
+        }
+    }
+#endif
 #ifndef QS_DIAG_NOGUARD
     guard_count(b, obs_bad, rew_bad, state_bad);
 #endif
