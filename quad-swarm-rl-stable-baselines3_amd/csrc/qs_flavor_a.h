@@ -435,6 +435,21 @@ __device__ __forceinline__ void col_row16(const KP& kp, const Drone& d, int di, 
     }
 }
 
+// The same row with the partners dealt over the drone's 2 sub-lanes: a rotation by 4k + 1 lanes brings drone
+// di + 2k (its sub-lane 1) to sub-lane 0 and drone di + 2k + 1 (its sub-lane 0) to sub-lane 1, so 4
+// rotations cover the 7 partners (and the drone itself once, skipped); the two halves are OR-ed by DPP.
+template <int K>
+__device__ __forceinline__ void col_row16_q2(const KP& kp, const Drone& d, int di, float thr2, uint64_t& cur) {
+    if constexpr (K < 4) {
+        constexpr int C = 0x120 + 4 * K + 1;   // DPP row_ror:4K+1
+        const float dx = d.pos[0] - dpp_f<C>(d.pos[0]), dy = d.pos[1] - dpp_f<C>(d.pos[1]);
+        const float dz = d.pos[2] - dpp_f<C>(d.pos[2]);
+        const int j = dpp_i<C>(di);
+        if (j != di && j < kp.N && dx * dx + dy * dy + dz * dz <= thr2) cur |= 1ull << j;
+        col_row16_q2<K + 1>(kp, d, di, thr2, cur);
+    }
+}
+
 // scenario.reset() of the selected envs for the goal scenarios (:560, spawn_points None -> spawn at the
 // goal, :569-573): the env's lead lane fills the LDS goal table (draw key = the env's drone 0, stream
 // S_SCN_RESET) and stores the scenario state; every selected drone takes its goal.  Whole wave.
@@ -460,6 +475,9 @@ __device__ __forceinline__ void scen_reset_a(const KP& kp, const Bufs& b, float*
 // features (neighbour j on sub-lane j % Q).  Reductions over the env keep the one-lane-per-drone tree.
 #ifndef QS_QA
 #define QS_QA 2
+#endif
+#ifndef QS_A_COLQ2   // the per-tick collision rows with the partners dealt over the 2 sub-lanes
+#define QS_A_COLQ2 1
 #endif
 // tick (t + k)'s OU normals from sub-lane k: k = 0 -> z, k >= 1 -> zn[k - 1]
 template <int Q, int K = 0>
@@ -544,13 +562,21 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
         if (fin) continue;   // the reference breaks out of its tick loop (:988); segment-uniform
         const Rng rng = env_rng(seed, tick, episode);
         float u[4];
+#ifdef QS_DIAG_A_NOCTRL   // diagnostic builds only (QS_JIT_OPTS): phase-removal timing
+        u[0] = u[1] = u[2] = u[3] = 0.5f + 0.01f * a0;
+#else
         controller(kp, d, c, a0, d.goal[2], u);
+#endif
         float z[4];   // QuadrotorDynamics.step: one OU draw per tick (:216)
         if constexpr (Q == 1) {
             normals4(rng, gid, S_OU, 0, z);
         } else if (sub % Q == 0) {   // wave-uniform: sub-lane q draws tick (tick + q)'s block
             float zr[4];
+#ifdef QS_DIAG_A_NOOU
+            for (int k = 0; k < 4; ++k) zr[k] = 0.001f * (float)(k + q);
+#else
             normals4(env_rng(seed, tick + q, episode), gid, S_OU, 0, zr);
+#endif
             qbc_ticks<Q>(zr, z, zn);
         } else {   // the next buffered tick, then shift the buffer (register moves, no dynamic index)
 #pragma unroll
@@ -562,14 +588,24 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
         }
 #pragma unroll
         for (int k = 0; k < 4; ++k) d.ou[k] = d.ou[k] + (kp.ou_theta * (kp.ou_mu - d.ou[k]) + kp.ou_sigma * z[k]);
+#ifdef QS_DIAG_A_NOPHYS
+        for (int i = 0; i < 3; ++i) d.pos[i] += 0.01f * d.vel[i] + 0.001f * u[i] + 0.0001f * d.ou[i];
+#else
         for (int s = 0; s < kp.sim_steps; ++s) substep(kp, d, u, d.ou, rng, gid, s);
+#endif
         ++tick;
         if (kp.stats) {   // collisions between drones and with the room (:649-720): bookkeeping only
             uint64_t cur = 0;
             const float thr2 = kp.col_thr * kp.col_thr;
 #ifndef QS_DIAG_A_NOCOL   // diagnostic builds only (QS_JIT_OPTS)
             if constexpr (LPE == 16 && NPAD * Q == 16) {
-                col_row16<Q, 1>(kp, d, di, thr2, cur);
+#if QS_A_COLQ2
+                if constexpr (Q == 2) {
+                    col_row16_q2<0>(kp, d, di, thr2, cur);
+                    cur = qor<Q>(cur);
+                } else
+#endif
+                    col_row16<Q, 1>(kp, d, di, thr2, cur);
             } else {
                 if (active && q == 0) xch[2 * (sbase + di)] = make_float4(d.pos[0], d.pos[1], d.pos[2], 0.f);
                 lds_sync();
