@@ -476,6 +476,9 @@ __device__ __forceinline__ void scen_reset_a(const KP& kp, const Bufs& b, float*
 #ifndef QS_QA
 #define QS_QA 2
 #endif
+#ifndef QS_DEAL_PHYS_A
+#define QS_DEAL_PHYS_A 0
+#endif
 #ifndef QS_A_COLQ2   // the per-tick collision rows with the partners dealt over the 2 sub-lanes
 #define QS_A_COLQ2 1
 #endif
@@ -591,7 +594,11 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
 #ifdef QS_DIAG_A_NOPHYS
         for (int i = 0; i < 3; ++i) d.pos[i] += 0.01f * d.vel[i] + 0.001f * u[i] + 0.0001f * d.ou[i];
 #else
-        for (int s = 0; s < kp.sim_steps; ++s) substep(kp, d, u, d.ou, rng, gid, s);
+#if QS_DEAL_PHYS_A   // the substeps dealt over the drone's sub-lanes (physics_q, qs_flavor_b.h)
+        if constexpr (Q > 1) physics_q<Q>(kp, d, u, q, rng, gid);
+        else
+#endif
+            for (int s = 0; s < kp.sim_steps; ++s) substep(kp, d, u, d.ou, rng, gid, s);
 #endif
         ++tick;
         if (kp.stats) {   // collisions between drones and with the room (:649-720): bookkeeping only
@@ -625,7 +632,8 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
             auto env_count = [&](bool x) { return __popcll((__ballot(x && q == 0) >> base) & lmask); };
             const bool settle = tick >= kp.st_settle;
             const bool fin5 = kpm.ep_len - (tick - 1) <= kp.st_final;   // time_remain (before tick += 1)
-            const int col = env_count(uniq) / 2;
+            const uint64_t ub = __ballot(uniq && q == 0);
+            const int col = ub ? (int)__popcll((ub >> base) & lmask) / 2 : 0;   // wave-uniform skip
             if (col > 0 && settle && uniq) d.flags |= QS_FL_HIT_AGENT;
             const bool wall_new = (d.flags & QS_FL_CRASH_WALL) && !(d.flags & QS_FL_PREV_WALL);
             const bool ceil_new = (d.flags & QS_FL_CRASH_CEIL) && !(d.flags & QS_FL_PREV_CEIL);

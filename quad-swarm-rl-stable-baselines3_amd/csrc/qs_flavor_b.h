@@ -646,6 +646,10 @@ __device__ __forceinline__ void store_drone_q(const KP& kp, const Bufs& b, int g
 #ifndef QS_CNT_DEFER
 #define QS_CNT_DEFER 1
 #endif
+// ... and counted only in steps where the wave saw an event to count
+#ifndef QS_CNT_GUARD
+#define QS_CNT_GUARD 1
+#endif
 // Experiment knob: drone words unchanged by the step are not stored back (store_drone_q's `old`).
 #ifndef QS_STORE_CHANGED
 #define QS_STORE_CHANGED 0   // A/B on MI355X: C3 9.45 vs 9.22 us, C4 14.59 vs 14.01 with it on (slower)
@@ -1021,11 +1025,18 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
 #endif
         auto env_count = [&](bool x) { return __popcll((__ballot(x && q == 0) >> lbase) & lmask); };
         const bool settle = tick >= kp.st_settle;
-        const int col = env_count(uniq) / 2;   // len(last_step_unique_collisions) // 2
-        if (col > 0 && settle && uniq) d.flags |= QS_FL_HIT_AGENT;
         const bool cfloor = active && (d.flags & QS_FL_CRASH_FLOOR);
         const bool room_new = active && (cfloor || wall_new || ceil_new) && !(d.flags & QS_FL_PREV_ROOM);
         d.flags = (d.flags & ~(uint32_t)QS_FL_PREV_ROOM) | (room_new ? (uint32_t)QS_FL_PREV_ROOM : 0u);
+        // every count below is zero unless one of these events happened somewhere in the wave (a new
+        // collision, a first floor contact, a new wall / ceiling / room crash, a new pillar hit): one
+        // wave-uniform test skips the per-env counting in the common step
+#if QS_CNT_GUARD
+        if (__ballot(q == 0 && (uniq || cfloor || (active && (wall_new || ceil_new)) || room_new || (OBST && onew))))
+#endif
+        {
+        const int col = env_count(uniq) / 2;   // len(last_step_unique_collisions) // 2
+        if (col > 0 && settle && uniq) d.flags |= QS_FL_HIT_AGENT;
         const int nfl = env_count(cfloor), nw = env_count(active && wall_new), nc = env_count(active && ceil_new);
         const int nr = env_count(room_new);
         int oc = 0, o35 = 0, o5 = 0;
@@ -1071,6 +1082,7 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
                 *cnt_at(k) = cnt[t];
 #endif
             }
+        }
         }
     }
 
