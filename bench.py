@@ -535,7 +535,7 @@ def main():
             launch += f", {S} env blocks of {cfg.num_envs // S} envs on {S} HIP streams"
         launch += ", specialised kernels (qs_specialize, hipRTC)" if env.specialized else ", generic kernels"
         out = {
-            "metric": "agent-steps/sec, 8-drone swarm x 4096 envs, at 1/2/4/8 MI355X" if args.config == "c3"
+            "metric": "agent-steps/sec, 8-drone swarm \u00d7 4096 envs, at 1/2/4/8 MI355X" if args.config == "c3"
             else f"agent-steps/sec, {WORKLOAD[args.config]}",
             "value": round(value, 1),
             "unit": "agent-steps/s",
