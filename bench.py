@@ -309,6 +309,12 @@ class Blocks:
     def run(self, n):
         from quadswarm_amd.env import step_blocks
         if not self.chunk:
+            if len(self.entries) == 1:   # one handle: the n launches from one C call (qs_step_n)
+                eb, ab, st = self.entries[0]
+                with self.torch.cuda.stream(st):
+                    eb.step_n(ab, n)
+                self.eager_steps += n
+                return
             envs = [e for e, _, _ in self.entries]
             acts = [a for _, a, _ in self.entries]
             sts = [s for _, _, s in self.entries]
@@ -530,7 +536,8 @@ def main():
         if chunk:
             launch = f"{timed_replays} hipGraph replays ({timed_replays * len(run.entries)} graphs) for {args.steps} timed steps"
         else:
-            launch = f"eager: {timed_eager} qs_step_blocks calls"
+            launch = (f"eager: {timed_eager} launches from one qs_step_n call" if len(run.entries) == 1
+                      else f"eager: {timed_eager} qs_step_blocks calls")
         if S > 1:
             launch += f", {S} env blocks of {cfg.num_envs // S} envs on {S} HIP streams"
         launch += ", specialised kernels (qs_specialize, hipRTC)" if env.specialized else ", generic kernels"

@@ -299,6 +299,11 @@ int qs_reset(qs_handle* h, const uint8_t* d_env_mask, void* stream);
  * flavor A) are reset in the same launch, their final observation goes to term_obs, obs holds the
  * reset observation and reset_info[e] says so (SubprocVecEnvCustom semantics). */
 int qs_step(qs_handle* h, const float* d_actions, void* stream);
+/* `steps` back-to-back qs_step launches on `stream` with the same action buffer, from one C call (no
+ * host language between the launches): the benchmark's launch loop, the eager equivalent of a captured
+ * graph of `steps` steps.  Each launch is a whole step; the actions are the caller's buffer as it is
+ * when each launch runs (a policy writing new actions orders itself on the same stream). */
+int qs_step_n(qs_handle* h, const float* d_actions, int steps, void* stream);
 /* qs_step of n handles (env blocks of one device, e.g. a GPU's shard split into blocks that overlap on
  * separate streams): handle i steps with d_actions[i] on streams[i].  One C call, one device check. */
 int qs_step_blocks(qs_handle* const* hs, int n, const float* const* d_actions, void* const* streams);

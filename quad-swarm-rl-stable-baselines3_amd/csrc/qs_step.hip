@@ -814,6 +814,15 @@ extern "C" int qs_step(qs_handle* h, const float* d_actions, void* stream) {
     return launch(h, true, d_actions, nullptr, (hipStream_t)stream);
 }
 
+extern "C" int qs_step_n(qs_handle* h, const float* d_actions, int steps, void* stream) {
+    if (steps < 1) return fail(QS_E_INVALID, "qs_step_n: steps < 1");
+    if (int rc = check_actions(h, d_actions)) return rc;
+    QS_HIP(use_device(h));
+    for (int i = 0; i < steps; ++i)
+        if (int rc = launch(h, true, d_actions, nullptr, (hipStream_t)stream)) return rc;
+    return QS_OK;
+}
+
 extern "C" int qs_step_blocks(qs_handle* const* hs, int n, const float* const* d_actions, void* const* streams) {
     if (!hs || !d_actions || !streams || n < 1) return fail(QS_E_INVALID, "NULL argument or n < 1");
     for (int i = 0; i < n; ++i) {

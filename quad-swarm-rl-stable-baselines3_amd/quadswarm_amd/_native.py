@@ -119,7 +119,7 @@ class QuadSwarmError(RuntimeError):
 # every symbol include/quadswarm.h declares (tests check the library exports all of them)
 EXPORTS = ["qs_abi_version", "qs_last_error", "qs_struct_sizes", "qs_config_default", "qs_config_default_a",
            "qs_layout_query", "qs_create", "qs_destroy",
-           "qs_buffers_get", "qs_reset", "qs_step", "qs_step_blocks", "qs_counters", "qs_counters_reset",
+           "qs_buffers_get", "qs_reset", "qs_step", "qs_step_n", "qs_step_blocks", "qs_counters", "qs_counters_reset",
            "qs_set_param",
            "qs_get_param", "qs_state_bytes", "qs_get_state", "qs_set_state", "qs_gae",
            "qs_specialize", "qs_is_specialized", "qs_config_kp_words", "qs_specialize_compile",
@@ -144,6 +144,7 @@ def lib():
         "qs_layout_query": ([P(QsConfig), P(QsLayout)], I32),
         "qs_create": ([P(QsConfig), ctypes.c_int, V, P(V)], I32), "qs_destroy": ([V], I32),
         "qs_buffers_get": ([V, P(QsBuffers)], I32), "qs_reset": ([V, V, V], I32), "qs_step": ([V, V, V], I32),
+        "qs_step_n": ([V, V, ctypes.c_int, V], I32),
         "qs_step_blocks": ([P(V), ctypes.c_int, P(V), P(V)], I32),
         "qs_counters": ([V, P(QsStats), V], I32), "qs_counters_reset": ([V, V], I32),
         "qs_set_param": ([V, ctypes.c_char_p, ctypes.c_double], I32),

@@ -146,6 +146,17 @@ class QuadSwarmEnv:
         N.check(N.lib().qs_step(self._h, ctypes.c_void_p(a.data_ptr()), self._stream()), "qs_step")
         return self.obs, self.rew, self.done, self.term_obs
 
+    def step_n(self, actions, steps):
+        """`steps` back-to-back steps with the same action buffer from one C call (qs_step_n): the
+        benchmark's eager launch loop.  actions must already be a contiguous aligned fp32 device tensor."""
+        a = actions
+        if not (self._torch.is_tensor(a) and a.device == self.device and a.dtype == self._torch.float32
+                and a.is_contiguous() and a.data_ptr() % self._align == 0 and a.numel() == self.I * self.act_dim):
+            raise ValueError("step_n: actions must be a contiguous, aligned fp32 device tensor of I * act_dim")
+        self._act_keepalive = a
+        N.check(N.lib().qs_step_n(self._h, ctypes.c_void_p(a.data_ptr()), int(steps), self._stream()), "qs_step_n")
+        return self.obs, self.rew, self.done, self.term_obs
+
     def counters(self):
         """Non-finite guard counters (qs_counters): {"nonfinite_obs", "nonfinite_rew", "nonfinite_state"}
         accumulated by every step since creation / reset_counters().  Synchronises the current stream."""

@@ -33,3 +33,30 @@ def test_bench_driver_arguments_replay_graphs():
     assert line["ms_per_step"] * 1e3 >= 0.95 * rf["kernel_us"]
     assert abs(line["value"] - 32768 / (line["ms_per_step"] * 1e-3)) <= 0.01 * line["value"]
     assert line["nonfinite_guard"] == {"nonfinite_obs": 0, "nonfinite_rew": 0, "nonfinite_state": 0}
+
+
+@pytest.mark.gpu
+def test_step_n_equals_repeated_steps():
+    """qs_step_n (the eager launch loop from one C call) == the same number of qs_step calls, bitwise."""
+    import torch
+    sys.path.insert(0, ROOT)
+    import bench
+    from quadswarm_amd.env import QuadSwarmEnv
+    dev = torch.device("cuda:0")
+    outs = []
+    for use_n in (False, True):
+        cfg = bench.make_cfg(dict(bench.CONFIGS["c3"], num_envs=64), seed=0, specialize=True)
+        env = QuadSwarmEnv(cfg, device=dev)
+        g = torch.Generator(device=dev).manual_seed(7)
+        acts = (torch.rand(env.I, 4, device=dev, generator=g) * 2 - 1).contiguous()
+        env.reset()
+        if use_n:
+            env.step_n(acts, 12)
+        else:
+            for _ in range(12):
+                env.step(acts)
+        torch.cuda.synchronize()
+        outs.append((env.obs.clone(), env.rew.clone(), env.done.clone()))
+        env.close()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)

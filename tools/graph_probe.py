@@ -53,8 +53,23 @@ def main():
         w = (time.perf_counter() - t0) * 1e6 / args.steps
         print(f"{tag}: wall {w:.2f} us/step, events {e0.elapsed_time(e1) * 1e3 / args.steps:.2f} us/step", flush=True)
 
+    def loop(tag):   # the same steps from one C call (qs_step_n) instead of a graph replay
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        e0.record(stream)
+        env.step_n(acts, args.steps)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        w = (time.perf_counter() - t0) * 1e6 / args.steps
+        print(f"{tag}: wall {w:.2f} us/step, events {e0.elapsed_time(e1) * 1e3 / args.steps:.2f} us/step", flush=True)
+
     for k in range(6):
         one(f"fresh replay {k}")
+    for k in range(6):
+        loop(f"C loop {k}")
+    for k in range(3):
+        one(f"replay again {k}")
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < 0.3:
         g.replay()
