@@ -348,10 +348,26 @@ __device__ __forceinline__ bool seg_any(bool x, int base) {
     const uint64_t gm = (LPE == 64) ? ~0ull : ((1ull << LPE) - 1ull);
     return ((__ballot(x) >> base) & gm) != 0ull;
 }
+#ifndef QS_SEG_DPP   // the env's sums by DPP when it is one 16-lane row (seg_sum)
+#define QS_SEG_DPP 1
+#endif
 // butterfly over the drones (lane distance Q .. LPE/2): every lane ends with the same bits, and the
 // summation tree is the one-lane-per-drone tree whatever Q is
 template <int NPAD, int Q = 1>
 __device__ __forceinline__ float seg_sum(float v) {
+#if QS_SEG_DPP
+    if constexpr (NPAD * Q == 16) {
+        // the env is one 16-lane DPP row: the same tree by DPP instead of LDS permutes.  At lane distance
+        // m the partner is any lane of the other half of the 2m-lane group (l ^ 1, l ^ 2 by quad_perm; 7 - l
+        // by row_half_mirror; 15 - l by row_mirror); every lane of a group holds the same bits, and each add
+        // is commutative, so every lane ends with the bits of the xor butterfly below
+        if constexpr (Q <= 1) v += dpp_f<quad_perm(1, 0, 3, 2)>(v);
+        if constexpr (Q <= 2) v += dpp_f<quad_perm(2, 3, 0, 1)>(v);
+        if constexpr (Q <= 4) v += dpp_f<0x141>(v);   // row_half_mirror
+        v += dpp_f<0x140>(v);                         // row_mirror
+        return v;
+    }
+#endif
 #pragma unroll
     for (int m = Q; m < NPAD * Q; m <<= 1) v += __shfl_xor(v, m);
     return v;
