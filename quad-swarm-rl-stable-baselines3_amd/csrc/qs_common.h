@@ -536,6 +536,9 @@ __device__ __forceinline__ void substep_tail(const KP& kp, Drone& d, const Torqu
 // workgroup barrier costs nothing but orders the LDS traffic).
 // LDS-only workgroup barrier: workgroups are one wave, so this just orders LDS traffic.  Unlike
 // __syncthreads() it does not wait for outstanding global stores (vmcnt) or fence global memory.
+#ifndef QS_DW_LDS   // downwash sources through an LDS scratch instead of LDS permutes (downwash_env)
+#define QS_DW_LDS 1
+#endif
 __device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // ---------------------------------------------------------------------------------------------
@@ -667,19 +670,36 @@ __device__ __forceinline__ Rng env_rng(uint32_t seed, int32_t tick, int32_t epis
 // z-axis points at it from above within 0.7 m and 0.1 m sideways pushes it down and spins it, with the
 // source's per-step noise (stream S_DW of drone i) and the pair's draws (stream S_DWPAIR | this drone).
 // Every lane of the env segment must execute it (the permutes read the env's lanes).  True when applied.
+// dwt (QS_DW_LDS): an LDS scratch of 2 float4 per drone slot of the workgroup (the obs tile, which is not in use
+// yet when the forces run); dbase = the env's first slot.  The sources' {z axis, noise} and {pos, noise} go
+// through it -- 2 ds_write_b128 + 2 broadcast ds_read_b128 per source instead of 8 LDS permutes.
 template <int NPAD, int Q>
 __device__ __forceinline__ bool downwash_env(const KP& kp, Drone& d, const Rng& rng, uint32_t gid, int env, int lbase,
-                                             int di, int q, bool active) {
+                                             int di, int q, bool active, float4* dwt = nullptr, int dbase = 0) {
     bool vchanged = false;
     float dwu[4];
     uniforms4(rng, gid, S_DW, 0, dwu);
     const float an = -0.1f + 0.2f * dwu[0], wn = -0.01f + 0.02f * dwu[1];
     const float P0 = d.pos[0], P1 = d.pos[1], P2 = d.pos[2];
+    if (dwt) {
+        if (q == 0) {
+            dwt[2 * (dbase + di)] = make_float4(d.rot[2], d.rot[5], d.rot[8], an);
+            dwt[2 * (dbase + di) + 1] = make_float4(P0, P1, P2, wn);
+        }
+        lds_sync();
+    }
     for (int i = 0; i < NPAD; ++i) {
-        const int src = lbase + i * Q + q;
-        const float zi0 = __shfl(d.rot[2], src), zi1 = __shfl(d.rot[5], src), zi2 = __shfl(d.rot[8], src);
-        const float pi0 = __shfl(P0, src), pi1 = __shfl(P1, src), pi2 = __shfl(P2, src);
-        const float ani = __shfl(an, src), wni = __shfl(wn, src);
+        float zi0, zi1, zi2, pi0, pi1, pi2, ani, wni;
+        if (dwt) {
+            const float4 a = dwt[2 * (dbase + i)], b = dwt[2 * (dbase + i) + 1];
+            zi0 = a.x; zi1 = a.y; zi2 = a.z; ani = a.w;
+            pi0 = b.x; pi1 = b.y; pi2 = b.z; wni = b.w;
+        } else {
+            const int src = lbase + i * Q + q;
+            zi0 = __shfl(d.rot[2], src); zi1 = __shfl(d.rot[5], src); zi2 = __shfl(d.rot[8], src);
+            pi0 = __shfl(P0, src); pi1 = __shfl(P1, src); pi2 = __shfl(P2, src);
+            ani = __shfl(an, src); wni = __shfl(wn, src);
+        }
         if (!active || i >= kp.N || i == di) continue;
         const float r0 = P0 - pi0, r1 = P1 - pi1, r2 = P2 - pi2;
         const float dist = fsqrt(r0 * r0 + r1 * r1 + r2 * r2);
@@ -706,6 +726,7 @@ __device__ __forceinline__ bool downwash_env(const KP& kp, Drone& d, const Rng& 
             vchanged = true;
         }
     }
+    if (dwt) lds_sync();   // the scratch is the obs tile: every read done before it is written
     return vchanged;
 }
 

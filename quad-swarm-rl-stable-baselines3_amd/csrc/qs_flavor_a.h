@@ -687,7 +687,9 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
         // perform_downwash once per tick with the control dt (:810-815); the reference then rebuilds the
         // tick's obs from the post-downwash state, which is what the final obs below read
         bool dwa = false;
-        if (kp.downwash && kp.N > 1) dwa = downwash_env<NPAD, Q>(kp, d, rng, gid, env, base, di, q, active);
+        if (kp.downwash && kp.N > 1)
+            dwa = downwash_env<NPAD, Q>(kp, d, rng, gid, env, base, di, q, active,
+                                        (QS_DW_LDS && kp.obs_dim >= 8) ? reinterpret_cast<float4*>(lds) : nullptr, sbase);
         if (repulsive) {   // scenario.step() (:797)
             target_step<NPAD, Q>(kp, tx, ty, d.pos, active);
             d.goal[0] = tx;

@@ -1090,7 +1090,8 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     // ---- random forces (:659-698), replicated on the sub-lanes ----
     bool vchanged = false;
     if (kp.downwash && kp.N > 1)   // perform_downwash (aerodynamics/downwash.py:4-51)
-        vchanged = downwash_env<NPAD, Q>(kp, d, rng, gid, env, lbase, di, q, active);
+        vchanged = downwash_env<NPAD, Q>(kp, d, rng, gid, env, lbase, di, q, active,
+                                         (QS_DW_LDS && kp.obs_dim >= 8) ? reinterpret_cast<float4*>(lds) : nullptr, dbase);
 #ifndef QS_DIAG_NOIMPULSE
     if (kp.collide) {
 #else
