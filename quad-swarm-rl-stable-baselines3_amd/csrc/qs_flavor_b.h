@@ -453,6 +453,27 @@ __device__ __forceinline__ void sdf_obs(const KP& kp, const OGeo& og, const floa
         }
 }
 
+// the same 9 points dealt over the drone's Q sub-lanes (point p on sub-lane p % Q), each written to its
+// slot of the drone's obs row by the sub-lane that computed it: the same arithmetic per point
+template <int Q>
+__device__ __forceinline__ void sdf_obs_q(const KP& kp, const OGeo& og, const float2* ob, float x, float y, float* out,
+                                          int q) {
+    const float res = kp.sdf_res;
+#pragma unroll
+    for (int t = 0; t < (9 + Q - 1) / Q; ++t) {
+        const int p = q + Q * t;
+        if (p >= 9) continue;
+        const int a = p / 3, b = p % 3;
+        const float gx = x + (float)(a - 1) * res, gy = y + (float)(b - 1) * res;
+        float m2 = 1.0e4f;   // (100 m)^2
+        for (int o = 0; o < og.m; ++o) {
+            const float dx = gx - ob[o].x, dy = gy - ob[o].y;
+            m2 = fminf(m2, dx * dx + dy * dy);
+        }
+        out[p] = fsqrt(m2) - og.r;
+    }
+}
+
 // collision_detection (obstacles/utils.py:30-43): first obstacle within arm + radius
 __device__ __forceinline__ int obst_detect(const OGeo& og, const float2* ob, float x, float y) {
     for (int o = 0; o < og.m; ++o) {
@@ -645,6 +666,10 @@ __device__ __forceinline__ void store_drone_q(const KP& kp, const Bufs& b, int g
 // The env's episode-stat counters are stored once at the end of the step rather than where they change.
 #ifndef QS_CNT_DEFER
 #define QS_CNT_DEFER 1
+#endif
+// The step's 3x3 SDF obs dealt over the drone's sub-lanes (sdf_obs_q)
+#ifndef QS_SDF_DEAL
+#define QS_SDF_DEAL 1
 #endif
 // ... and counted only in steps where the wave saw an event to count
 #ifndef QS_CNT_GUARD
@@ -1267,7 +1292,11 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
 #ifndef QS_DIAG_NONBR
     if (nbr) neighbor_obs<NPAD, Q>(kp, xch, dbase, di, q, d.pos, d.vel, active, row);
 #endif
+#if QS_SDF_DEAL
+    if (OBST && active) sdf_obs_q<Q>(kp, og, myob, d.pos[0], d.pos[1], row + kp.obs_dim - 9, q);   // MultiObstacles.step
+#else
     if (OBST && lead) sdf_obs(kp, og, myob, d.pos[0], d.pos[1], row + kp.obs_dim - 9);   // MultiObstacles.step
+#endif
     QS_STAMP(7);
     // non-finite guard of the stepped drone and its reward (before a fused reset replaces the drone)
     const bool state_bad = lead && drone_nonfinite(d), rew_bad = lead && !(rw * 0.f == 0.f);
