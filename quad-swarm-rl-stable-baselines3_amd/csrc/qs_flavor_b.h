@@ -483,6 +483,23 @@ __device__ __forceinline__ int obst_detect(const OGeo& og, const float2* ob, flo
     return -1;
 }
 
+// the same test dealt over the drone's Q sub-lanes: sub-lane q scans pillars q, q + Q, ... and the smallest
+// index hit over the sub-lanes (DPP min) is the first pillar of the sequential scan
+template <int Q>
+__device__ __forceinline__ int obst_detect_q(const OGeo& og, const float2* ob, float x, float y, int q) {
+    int first = 0x7fffffff;
+    for (int o = q; o < og.m; o += Q) {
+        const float dx = x - ob[o].x, dy = y - ob[o].y;
+        if (fsqrt(dx * dx + dy * dy) <= og.thr) {
+            first = o;
+            break;
+        }
+    }
+    if constexpr (Q >= 2) first = min(first, dpp_i<quad_perm(1, 0, 3, 2)>(first));
+    if constexpr (Q >= 4) first = min(first, dpp_i<quad_perm(2, 3, 0, 1)>(first));
+    return first == 0x7fffffff ? -1 : first;
+}
+
 // perform_collision_with_obstacle (collisions/obstacles.py:23-50); Philox indices as the oracle's:
 // z = normals 0..19 of S_OBST (try t uses t*6 .. t*6+5), u = uniforms 0..7
 __device__ __forceinline__ void collide_obstacle(const KP& kp, const OGeo& og, Drone& d, float ox, float oy,
@@ -1036,7 +1053,11 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     int ohit = -1;
     bool onew = false;
     if (OBST) {
+#if QS_SDF_DEAL
+        ohit = (Q == 2 || Q == 4) ? obst_detect_q<Q>(og, myob, d.pos[0], d.pos[1], q) : obst_detect(og, myob, d.pos[0], d.pos[1]);
+#else
         ohit = obst_detect(og, myob, d.pos[0], d.pos[1]);
+#endif
         onew = active && ohit >= 0 && !(d.flags & QS_FL_PREV_OBST);
         rw += kpm.quadcol_obst * (onew ? -1.f : 0.f);
         d.flags = (d.flags & ~(uint32_t)QS_FL_PREV_OBST) | (ohit >= 0 ? (uint32_t)QS_FL_PREV_OBST : 0u);

@@ -77,6 +77,11 @@ for s in "$@"; do
       step prof_sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INSTS_LDS -d gpurun_out/prof_sq -o s --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu-baseline --graph 0 --e2e-iters 0 --streams 1
       rm -f gpurun_out/prof_*/*kernel_trace.csv
       ;;
+    sweep)
+      for c in c2 c3 c3mix c3mixr c4 c4dr c5 a8 n64; do
+        step sweep_$c 200 python bench.py --config $c --steps 1000 --no-cpu-baseline --e2e-iters 0
+      done
+      ;;
     profdrv)
       export TMPDIR=/tmp
       step profdrv_kt 300 rocprofv3 --kernel-trace --stats -d gpurun_out/profdrv_kt -o kt --output-format csv -- python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --e2e-iters 0
