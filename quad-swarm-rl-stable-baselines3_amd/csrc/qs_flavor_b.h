@@ -117,6 +117,9 @@ __device__ __forceinline__ void xch_put(float4* xch, int lane, const float* P, c
     xch[2 * lane + 1] = make_float4(V[0], V[1], V[2], 0.f);
 }
 
+#ifndef QS_NBR_SELECT   // 64-drone envs: neighbours by K selection passes instead of full ranking
+#define QS_NBR_SELECT 1
+#endif
 // pos_vel neighbour obs: neighborhood_indices (quadrotor_multi.py:344-375) + extend_obs_space
 // clip (:328-342).  Key = |[rel_pos, rel_vel]| clamped at 0.01 (compared squared, clamp 1e-4);
 // stable (index) tie-break like numpy's insertion sort; k == N-1 keeps index order (all keys 0).
@@ -163,6 +166,39 @@ __device__ void neighbor_obs(const KP& kp, const float4* xch, int dbase, int di,
     if (!write) return;
     const float vm = 2.f * kp.vxyz_max;
     const bool pairs = ((kp.so_dim | kp.obs_dim) & 1) == 0;   // 8-byte aligned slots: ds_write_b64
+#if QS_NBR_SELECT
+    if constexpr (Q == 1 && NPAD >= 32) {
+        if (sorted && kp.K <= 16) {
+            // one lane per drone, many candidates, few neighbours: K passes of a (key, index) minimum above
+            // the previous pick instead of ranking every candidate against all the others -- the same
+            // strict (key, index) order, so the same neighbours in the same slots
+            float pk = -1.f;
+            int pjx = -1;
+            for (int r = 0; r < kp.K; ++r) {
+                float bk = __builtin_inff();
+                int bj = NPAD;
+#pragma unroll
+                for (int m = 0; m < PJ; ++m) {
+                    const bool above = key[m] > pk || (key[m] == pk && m > pjx);
+                    const bool below = key[m] < bk;   // m ascending: the first of equal keys wins
+                    if (above && below) { bk = key[m]; bj = m; }
+                }
+                if (bk == __builtin_inff()) break;
+                pk = bk;
+                pjx = bj;
+                const float4 pj = xch[2 * (dbase + bj)], vj = xch[2 * (dbase + bj) + 1];
+                const float o0 = clampf(pj.x - P[0], -kp.room_range[0], kp.room_range[0]);
+                const float o1 = clampf(pj.y - P[1], -kp.room_range[1], kp.room_range[1]);
+                const float o2 = clampf(pj.z - P[2], -kp.room_range[2], kp.room_range[2]);
+                const float o3 = clampf(vj.x - V[0], -vm, vm), o4 = clampf(vj.y - V[1], -vm, vm);
+                const float o5 = clampf(vj.z - V[2], -vm, vm);
+                float* o = out + kp.so_dim + r * 6;
+                o[0] = o0; o[1] = o1; o[2] = o2; o[3] = o3; o[4] = o4; o[5] = o5;
+            }
+            return;
+        }
+    }
+#endif
 #pragma unroll
     for (int t = 0; t < PJ; ++t) {
         const int j = q + Q * t;
