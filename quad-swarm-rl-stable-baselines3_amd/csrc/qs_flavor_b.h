@@ -120,6 +120,9 @@ __device__ __forceinline__ void xch_put(float4* xch, int lane, const float* P, c
 #ifndef QS_NBR_SELECT   // 64-drone envs: neighbours by K selection passes instead of full ranking
 #define QS_NBR_SELECT 1
 #endif
+#ifndef QS_NBR_SELECT2  // the same for 32-drone envs (2 sub-lanes per drone): experiment, off until measured
+#define QS_NBR_SELECT2 0
+#endif
 // pos_vel neighbour obs: neighborhood_indices (quadrotor_multi.py:344-375) + extend_obs_space
 // clip (:328-342).  Key = |[rel_pos, rel_vel]| clamped at 0.01 (compared squared, clamp 1e-4);
 // stable (index) tie-break like numpy's insertion sort; k == N-1 keeps index order (all keys 0).
@@ -167,7 +170,7 @@ __device__ void neighbor_obs(const KP& kp, const float4* xch, int dbase, int di,
     const float vm = 2.f * kp.vxyz_max;
     const bool pairs = ((kp.so_dim | kp.obs_dim) & 1) == 0;   // 8-byte aligned slots: ds_write_b64
 #if QS_NBR_SELECT
-    if constexpr (Q == 1 && NPAD >= 32) {
+    if constexpr (Q == 1 && NPAD >= 64) {
         if (sorted && kp.K <= 16) {
             // one lane per drone, many candidates, few neighbours: K passes of a (key, index) minimum above
             // the previous pick instead of ranking every candidate against all the others -- the same
@@ -194,6 +197,42 @@ __device__ void neighbor_obs(const KP& kp, const float4* xch, int dbase, int di,
                 const float o5 = clampf(vj.z - V[2], -vm, vm);
                 float* o = out + kp.so_dim + r * 6;
                 o[0] = o0; o[1] = o1; o[2] = o2; o[3] = o3; o[4] = o4; o[5] = o5;
+            }
+            return;
+        }
+    }
+    if constexpr (QS_NBR_SELECT2 && Q == 2 && NPAD >= 32) {
+        if (sorted && kp.K <= 16) {
+            // the same K passes with the candidates dealt over the drone's 2 sub-lanes (j = q + 2 t): each
+            // sub-lane takes its own (key, index) minimum above the previous pick, the pair keeps the smaller
+            // of the two by DPP; sub-lane 0 writes the slot
+            float pk = -1.f;
+            int pjx = -1;
+            for (int r = 0; r < kp.K; ++r) {
+                float bk = __builtin_inff();
+                int bj = NPAD;
+#pragma unroll
+                for (int t = 0; t < PJ; ++t) {
+                    const int m = q + 2 * t;
+                    const bool above = key[t] > pk || (key[t] == pk && m > pjx);
+                    if (above && key[t] < bk) { bk = key[t]; bj = m; }
+                }
+                const float ok = dpp_f<quad_perm(1, 0, 3, 2)>(bk);
+                const int oj = dpp_i<quad_perm(1, 0, 3, 2)>(bj);
+                if (ok < bk || (ok == bk && oj < bj)) { bk = ok; bj = oj; }
+                if (bk == __builtin_inff()) break;
+                pk = bk;
+                pjx = bj;
+                if (q == 0) {
+                    const float4 pj = xch[2 * (dbase + bj)], vj = xch[2 * (dbase + bj) + 1];
+                    const float o0 = clampf(pj.x - P[0], -kp.room_range[0], kp.room_range[0]);
+                    const float o1 = clampf(pj.y - P[1], -kp.room_range[1], kp.room_range[1]);
+                    const float o2 = clampf(pj.z - P[2], -kp.room_range[2], kp.room_range[2]);
+                    const float o3 = clampf(vj.x - V[0], -vm, vm), o4 = clampf(vj.y - V[1], -vm, vm);
+                    const float o5 = clampf(vj.z - V[2], -vm, vm);
+                    float* o = out + kp.so_dim + r * 6;
+                    o[0] = o0; o[1] = o1; o[2] = o2; o[3] = o3; o[4] = o4; o[5] = o5;
+                }
             }
             return;
         }
