@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define QS_ABI_VERSION 7
+#define QS_ABI_VERSION 8
 #define QS_MAX_AGENTS 64            /* drones per env: one env lives inside one 64-lane wavefront */
 #define QS_MAX_DR_CHOICES 8         /* entries per obstacle domain-randomisation list */
 
@@ -158,6 +158,10 @@ typedef struct qs_config {
     /* ---- episode_extra_stats (flavor B; quadrotor_multi.py:153-216, 541-657, 739-831): 1 = the step kernels
      * keep the reference's per-episode counters and write each finished env's rows to buffers.estats ---- */
     int32_t episode_stats;
+    /* ---- per-step infos (quadrotor_single.py:79-105, 371; quadrotor_multi.py:642-651; flavor A
+     * quadrotor_single_rewards.py:457): 1 = every step writes each drone's reward components to
+     * buffers.rew_info (QS_RI_*), from which the host builds infos[i]["rewards"] / infos[i]["goal_dist"] ---- */
+    int32_t step_infos;
 } qs_config;
 
 /* Device buffers of a handle.  State is structure-of-arrays: field f of drone g lives at
@@ -213,6 +217,18 @@ enum qs_estat {
     QS_ES_SCEN = 16, QS_ES_D1 = 17, QS_ES_D3 = 18, QS_ES_D5 = 19, QS_ES_REPLAY = 20,
     QS_NES = 24
 };
+/* rows of buffers.rew_info [QS_NRI, I] (config step_infos), written by every step before a fused reset.  Flavor B:
+ * compute_reward_weighted's raw terms (quadrotor_single.py:34-66) -- |goal - pos|, |action|, on_floor, the
+ * orientation term (1 on the floor, else -R[2][2]), |omega| -- then the swarm terms (quadrotor_multi.py:608-651):
+ * rew_collisions_raw (-1 for a drone in last_step_unique_collisions, else 0), the proximity reward
+ * (-control_dt * penalty) and the obstacle raw term (-1 on a new pillar hit).  infos[i]["rewards"] is these times the
+ * reward coefficients and dt (quadswarm_amd.infos).  Flavor A: row 0 = |pos - goal| after the last executed
+ * tick (infos[i]["goal_dist"]). */
+enum qs_rinfo {
+    QS_RI_DIST = 0, QS_RI_EFFORT = 1, QS_RI_CRASH = 2, QS_RI_ORIENT = 3, QS_RI_SPIN = 4, QS_RI_QUADCOL = 5,
+    QS_RI_PROX = 6, QS_RI_OBST = 7, QS_NRI = 8,
+    QS_RI_GOAL_DIST = 0             /* flavor A */
+};
 enum qs_env_flags {
     QS_EF_STALE = 1,                /* stale_vel / QS_F_HEADING hold QuadrotorEnvMulti.vel / .heading */
     QS_EF_SUCCESS = 2,              /* flavor A episode_success (a capture happened this episode)     */
@@ -236,7 +252,7 @@ enum qs_env_ffield {
 typedef struct qs_layout {          /* byte offsets inside one workspace allocation */
     size_t params;                  /* kernel parameter block (device copy of the config + runtime params) */
     size_t state, istate, env, env_f, obst, stale_vel, obs, term_obs, rew, done, reset_info, stats, estats,
-        total_bytes;
+        rew_info, total_bytes;
     int32_t obs_dim, num_drones;
 } qs_layout;
 
@@ -256,6 +272,7 @@ typedef struct qs_buffers {         /* device pointers (valid for the handle's l
     uint64_t* stats;                /* [QS_NSTAT] non-finite guard counters (qs_counters)              */
     float* estats;                  /* [I, QS_NES] episode_extra_stats rows of the envs that finished (config
                                        episode_stats; rows of other envs keep their previous contents)   */
+    float* rew_info;                /* [QS_NRI, I] the last step's reward components (config step_infos), or NULL */
 } qs_buffers;
 
 /* Non-finite guard.  The reference raises ValueError on a NaN reward (gym_art/quadrotor_multi/

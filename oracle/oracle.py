@@ -75,6 +75,11 @@ S_SCN, S_SCN_RESET = 23, 24
 S_DR = 26
 
 
+# reward components in or_drone.rinfo (OR_RI_*, quadswarm_oracle.h)
+RI_DIST, RI_EFFORT, RI_CRASH, RI_ORIENT, RI_SPIN, RI_QUADCOL, RI_PROX, RI_OBST, NRI = range(9)
+RI_GOAL_DIST = 0
+
+
 class OrDrone(ctypes.Structure):
     _fields_ = [
         ("pos", D * 3), ("vel", D * 3), ("rot", D * 9), ("omega", D * 3), ("acc", D * 3),
@@ -86,6 +91,7 @@ class OrDrone(ctypes.Structure):
         ("pid", D * 20), ("angle", D), ("ang_vel", D), ("prev_obst", I),
         ("hit_agent", I), ("hit_obst", I), ("reached", I), ("prev_room", I),
         ("dring", D * 5), ("dsum", D * 3), ("ep_dist", D * 3),
+        ("rinfo", D * 8),   # the step's reward components (OR_RI_*, quadswarm_oracle.h)
     ]
 
 

@@ -1008,6 +1008,12 @@ void or_env_step(const or_params* p, or_drone* drones, or_env* envs, int e, cons
         double sum = cost_pos + cost_effort;
         sum += cost_crash; sum += cost_orient; sum += cost_spin;
         rw[i] = -p->dt * sum;
+        /* compute_reward_weighted's raw terms (rew_info, quadrotor_single.py:79-105) */
+        d->rinfo[OR_RI_DIST] = dist_goal[i];
+        d->rinfo[OR_RI_EFFORT] = an;
+        d->rinfo[OR_RI_CRASH] = (double)d->on_floor;
+        d->rinfo[OR_RI_ORIENT] = d->on_floor ? 1.0 : -d->rot[8];
+        d->rinfo[OR_RI_SPIN] = pow(d->omega[0] * d->omega[0] + d->omega[1] * d->omega[1] + d->omega[2] * d->omega[2], 0.5);
         if (i == 0) ev->last_floor0 = d->on_floor;
         self_obs(p, d, r, gid, OR_S_SENSOR, o + (size_t)i * od);
         for (int c = 0; c < 3; ++c) ev->obs_pos[i][c] = d->pos[c];
@@ -1063,6 +1069,10 @@ void or_env_step(const or_params* p, or_drone* drones, or_env* envs, int e, cons
         rw[i] += p->rew_quadcol_bin * rc;
         rw[i] += any_near ? -1.0 * (p->control_dt * pen[i]) : 0.0;
         if (p->use_obstacles) rw[i] += p->rew_quadcol_bin_obst * (onew[i] ? -1.0 : 0.0);
+        /* the swarm terms of infos[i]["rewards"] (quadrotor_multi.py:642-651) */
+        dr[i].rinfo[OR_RI_QUADCOL] = rc;
+        dr[i].rinfo[OR_RI_PROX] = any_near ? -1.0 * (p->control_dt * pen[i]) : 0.0;
+        dr[i].rinfo[OR_RI_OBST] = (p->use_obstacles && onew[i]) ? -1.0 : 0.0;
     }
     /* 3. random forces (quadrotor_multi.py:659-698) */
     int flag = 0;

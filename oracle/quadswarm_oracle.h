@@ -203,7 +203,13 @@ typedef struct {
     double dring[5];
     double dsum[3];
     double ep_dist[3];         /* distance_to_goal_1s / _3s / _5s of the last finished episode */
+    /* the step's per-drone reward components (OR_RI_*): the raw terms behind infos[i]["rewards"]
+     * (quadrotor_single.py:34-105, quadrotor_multi.py:608-651); flavor A: OR_RI_GOAL_DIST = infos[i]["goal_dist"]
+     * of the last executed tick (quadrotor_single_rewards.py:457) */
+    double rinfo[8];
 } or_drone;
+enum { OR_RI_DIST = 0, OR_RI_EFFORT, OR_RI_CRASH, OR_RI_ORIENT, OR_RI_SPIN, OR_RI_QUADCOL, OR_RI_PROX, OR_RI_OBST,
+       OR_NRI, OR_RI_GOAL_DIST = 0 };
 
 /* env-level episode_extra_stats values of a finished episode (quadrotor_multi.py:739-831), the GPU's
  * qs estats columns (include/quadswarm.h QS_ES_*) */

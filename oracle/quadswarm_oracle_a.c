@@ -634,6 +634,10 @@ void or_env_step_a(const or_params* p, or_drone* drones, or_env* envs, int e, co
             or_motors_to_cmds(motors, u);
             or_ou_noise(p, d->ou, r, gid);
             for (int s = 0; s < p->sim_steps; ++s) or_dyn_substep(p, d, u, d->ou, r, gid, s);
+            {   /* infos[i]["goal_dist"] = |pos - goal| of this _step (quadrotor_single_rewards.py:457) */
+                const double gd[3] = {d->pos[0] - d->goal[0], d->pos[1] - d->goal[1], d->pos[2] - d->goal[2]};
+                d->rinfo[OR_RI_GOAL_DIST] = sqrt(gd[0] * gd[0] + gd[1] * gd[1] + gd[2] * gd[2]);
+            }
             or_self_obs_a(p, d, r, gid, OR_S_SENSOR, OR_S_SELF_CAM, o + (size_t)i * od);
             for (int c = 0; c < 3; ++c) ev->obs_pos[i][c] = d->pos[c];
             ev->heading[i] = d->angle;

@@ -56,6 +56,8 @@ struct KP {
     // ---- episode_extra_stats (flavor B): on; collisions_grace_period_steps (ticks >= settle count), the
     // final-5-s window (time_remain <= final), distance windows of 1 / 3 / 5 s in ticks ----
     int stats, st_settle, st_final, st_win[3];
+    // ---- per-step reward components (qs_config.step_infos): the step writes buffers.rew_info
+    int rcomp;
 };
 
 // The fields qs_set_param may change after creation, read once per launch into registers (uniform):
@@ -114,6 +116,7 @@ struct Bufs {
     const uint8_t* mask;
     unsigned long long* stats;   // [QS_NSTAT] non-finite guard counters (qs_counters)
     float* estats;               // [I, QS_NES] episode_extra_stats rows of finished envs
+    float* rcomp;                // [QS_NRI, I] the step's reward components (kp.rcomp)
 };
 
 // Diagnostic phase stamps (build with -DQS_STAMPS=1 only; never in the shipped library): lane 0 of
@@ -536,9 +539,6 @@ __device__ __forceinline__ void substep_tail(const KP& kp, Drone& d, const Torqu
 // workgroup barrier costs nothing but orders the LDS traffic).
 // LDS-only workgroup barrier: workgroups are one wave, so this just orders LDS traffic.  Unlike
 // __syncthreads() it does not wait for outstanding global stores (vmcnt) or fence global memory.
-#ifndef QS_DW_LDS   // downwash sources through an LDS scratch instead of LDS permutes (downwash_env)
-#define QS_DW_LDS 1
-#endif
 __device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // ---------------------------------------------------------------------------------------------
@@ -670,7 +670,7 @@ __device__ __forceinline__ Rng env_rng(uint32_t seed, int32_t tick, int32_t epis
 // z-axis points at it from above within 0.7 m and 0.1 m sideways pushes it down and spins it, with the
 // source's per-step noise (stream S_DW of drone i) and the pair's draws (stream S_DWPAIR | this drone).
 // Every lane of the env segment must execute it (the permutes read the env's lanes).  True when applied.
-// dwt (QS_DW_LDS): an LDS scratch of 2 float4 per drone slot of the workgroup (the obs tile, which is not in use
+// dwt: an LDS scratch of 2 float4 per drone slot of the workgroup (the obs tile, which is not in use
 // yet when the forces run); dbase = the env's first slot.  The sources' {z axis, noise} and {pos, noise} go
 // through it -- 2 ds_write_b128 + 2 broadcast ds_read_b128 per source instead of 8 LDS permutes.
 template <int NPAD, int Q>

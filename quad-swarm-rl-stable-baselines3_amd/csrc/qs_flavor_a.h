@@ -348,14 +348,10 @@ __device__ __forceinline__ bool seg_any(bool x, int base) {
     const uint64_t gm = (LPE == 64) ? ~0ull : ((1ull << LPE) - 1ull);
     return ((__ballot(x) >> base) & gm) != 0ull;
 }
-#ifndef QS_SEG_DPP   // the env's sums by DPP when it is one 16-lane row (seg_sum)
-#define QS_SEG_DPP 1
-#endif
 // butterfly over the drones (lane distance Q .. LPE/2): every lane ends with the same bits, and the
 // summation tree is the one-lane-per-drone tree whatever Q is
 template <int NPAD, int Q = 1>
 __device__ __forceinline__ float seg_sum(float v) {
-#if QS_SEG_DPP
     if constexpr (NPAD * Q == 16) {
         // the env is one 16-lane DPP row: the same tree by DPP instead of LDS permutes.  At lane distance
         // m the partner is any lane of the other half of the 2m-lane group (l ^ 1, l ^ 2 by quad_perm; 7 - l
@@ -367,7 +363,6 @@ __device__ __forceinline__ float seg_sum(float v) {
         v += dpp_f<0x140>(v);                         // row_mirror
         return v;
     }
-#endif
 #pragma unroll
     for (int m = Q; m < NPAD * Q; m <<= 1) v += __shfl_xor(v, m);
     return v;
@@ -492,12 +487,6 @@ __device__ __forceinline__ void scen_reset_a(const KP& kp, const Bufs& b, float*
 #ifndef QS_QA
 #define QS_QA 2
 #endif
-#ifndef QS_DEAL_PHYS_A
-#define QS_DEAL_PHYS_A 0
-#endif
-#ifndef QS_A_COLQ2   // the per-tick collision rows with the partners dealt over the 2 sub-lanes
-#define QS_A_COLQ2 1
-#endif
 // tick (t + k)'s OU normals from sub-lane k: k = 0 -> z, k >= 1 -> zn[k - 1]
 template <int Q, int K = 0>
 __device__ __forceinline__ void qbc_ticks(const float (&zr)[4], float (&z)[4], float (&zn)[Q > 1 ? Q - 1 : 1][4]) {
@@ -574,6 +563,7 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
 
     bool fin = false, success = eflags & QS_EF_SUCCESS;
     float rw = 0.f, gox = d.goal[0], goy = d.goal[1];
+    float gdist = 0.f;   // infos[i]["goal_dist"] of the last executed tick (per-step infos, kp.rcomp)
     bool dn = false;
     float zn[Q > 1 ? Q - 1 : 1][4] = {};   // OU normals of the next Q - 1 ticks, drawn by sub-lanes 1 .. Q-1
 #pragma unroll 1   // 8 controller ticks: one copy of the body (I-cache), also when kp.ticks is a constant
@@ -581,21 +571,13 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
         if (fin) continue;   // the reference breaks out of its tick loop (:988); segment-uniform
         const Rng rng = env_rng(seed, tick, episode);
         float u[4];
-#ifdef QS_DIAG_A_NOCTRL   // diagnostic builds only (QS_JIT_OPTS): phase-removal timing
-        u[0] = u[1] = u[2] = u[3] = 0.5f + 0.01f * a0;
-#else
         controller(kp, d, c, a0, d.goal[2], u);
-#endif
         float z[4];   // QuadrotorDynamics.step: one OU draw per tick (:216)
         if constexpr (Q == 1) {
             normals4(rng, gid, S_OU, 0, z);
         } else if (sub % Q == 0) {   // wave-uniform: sub-lane q draws tick (tick + q)'s block
             float zr[4];
-#ifdef QS_DIAG_A_NOOU
-            for (int k = 0; k < 4; ++k) zr[k] = 0.001f * (float)(k + q);
-#else
             normals4(env_rng(seed, tick + q, episode), gid, S_OU, 0, zr);
-#endif
             qbc_ticks<Q>(zr, z, zn);
         } else {   // the next buffered tick, then shift the buffer (register moves, no dynamic index)
 #pragma unroll
@@ -607,27 +589,20 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
         }
 #pragma unroll
         for (int k = 0; k < 4; ++k) d.ou[k] = d.ou[k] + (kp.ou_theta * (kp.ou_mu - d.ou[k]) + kp.ou_sigma * z[k]);
-#ifdef QS_DIAG_A_NOPHYS
-        for (int i = 0; i < 3; ++i) d.pos[i] += 0.01f * d.vel[i] + 0.001f * u[i] + 0.0001f * d.ou[i];
-#else
-#if QS_DEAL_PHYS_A   // the substeps dealt over the drone's sub-lanes (physics_q, qs_flavor_b.h)
-        if constexpr (Q > 1) physics_q<Q>(kp, d, u, q, rng, gid);
-        else
-#endif
             for (int s = 0; s < kp.sim_steps; ++s) substep(kp, d, u, d.ou, rng, gid, s);
-#endif
         ++tick;
+        if (kp.rcomp) {   // np.linalg.norm(self.dynamics.pos - self.goal) of this _step (quadrotor_single_rewards.py:457)
+            const float gx = d.pos[0] - d.goal[0], gy = d.pos[1] - d.goal[1], gz = d.pos[2] - d.goal[2];
+            gdist = fsqrt(gx * gx + gy * gy + gz * gz);
+        }
         if (kp.stats) {   // collisions between drones and with the room (:649-720): bookkeeping only
             uint64_t cur = 0;
             const float thr2 = kp.col_thr * kp.col_thr;
-#ifndef QS_DIAG_A_NOCOL   // diagnostic builds only (QS_JIT_OPTS)
             if constexpr (LPE == 16 && NPAD * Q == 16) {
-#if QS_A_COLQ2
                 if constexpr (Q == 2) {
                     col_row16_q2<0>(kp, d, di, thr2, cur);
                     cur = qor<Q>(cur);
                 } else
-#endif
                     col_row16<Q, 1>(kp, d, di, thr2, cur);
             } else {
                 if (active && q == 0) xch[2 * (sbase + di)] = make_float4(d.pos[0], d.pos[1], d.pos[2], 0.f);
@@ -642,7 +617,6 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
                 cur = qor<Q>(cur);
                 lds_sync();   // the tile is rewritten next tick
             }
-#endif
             const bool uniq = active && cur != 0 && d.prev == 0;   // setdiff1d(flat(cur), flat(prev))
             d.prev = cur;
             auto env_count = [&](bool x) { return __popcll((__ballot(x && q == 0) >> base) & lmask); };
@@ -689,7 +663,7 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
         bool dwa = false;
         if (kp.downwash && kp.N > 1)
             dwa = downwash_env<NPAD, Q>(kp, d, rng, gid, env, base, di, q, active,
-                                        (QS_DW_LDS && kp.obs_dim >= 8) ? reinterpret_cast<float4*>(lds) : nullptr, sbase);
+                                        kp.obs_dim >= 8 ? reinterpret_cast<float4*>(lds) : nullptr, sbase);
         if (repulsive) {   // scenario.step() (:797)
             target_step<NPAD, Q>(kp, tx, ty, d.pos, active);
             d.goal[0] = tx;
@@ -799,6 +773,7 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
         store_ctl(kp, b, g, c);
         b.rew[g] = rw;
         b.done[g] = fin ? 1 : 0;
+        if (kp.rcomp) b.rcomp[(size_t)QS_RI_GOAL_DIST * kp.I + g] = gdist;
         if (di == 0) {
             b.env[QS_E_TICK * kp.E + env] = fin ? 0 : tick;
             if (fin) b.env[QS_E_EPISODE * kp.E + env] = episode + 1;

@@ -117,12 +117,6 @@ __device__ __forceinline__ void xch_put(float4* xch, int lane, const float* P, c
     xch[2 * lane + 1] = make_float4(V[0], V[1], V[2], 0.f);
 }
 
-#ifndef QS_NBR_SELECT   // 64-drone envs: neighbours by K selection passes instead of full ranking
-#define QS_NBR_SELECT 1
-#endif
-#ifndef QS_NBR_SELECT2  // the same for 32-drone envs (2 sub-lanes per drone): experiment, off until measured
-#define QS_NBR_SELECT2 0
-#endif
 // pos_vel neighbour obs: neighborhood_indices (quadrotor_multi.py:344-375) + extend_obs_space
 // clip (:328-342).  Key = |[rel_pos, rel_vel]| clamped at 0.01 (compared squared, clamp 1e-4);
 // stable (index) tie-break like numpy's insertion sort; k == N-1 keeps index order (all keys 0).
@@ -169,7 +163,6 @@ __device__ void neighbor_obs(const KP& kp, const float4* xch, int dbase, int di,
     if (!write) return;
     const float vm = 2.f * kp.vxyz_max;
     const bool pairs = ((kp.so_dim | kp.obs_dim) & 1) == 0;   // 8-byte aligned slots: ds_write_b64
-#if QS_NBR_SELECT
     if constexpr (Q == 1 && NPAD >= 64) {
         if (sorted && kp.K <= 16) {
             // one lane per drone, many candidates, few neighbours: K passes of a (key, index) minimum above
@@ -201,43 +194,6 @@ __device__ void neighbor_obs(const KP& kp, const float4* xch, int dbase, int di,
             return;
         }
     }
-    if constexpr (QS_NBR_SELECT2 && Q == 2 && NPAD >= 32) {
-        if (sorted && kp.K <= 16) {
-            // the same K passes with the candidates dealt over the drone's 2 sub-lanes (j = q + 2 t): each
-            // sub-lane takes its own (key, index) minimum above the previous pick, the pair keeps the smaller
-            // of the two by DPP; sub-lane 0 writes the slot
-            float pk = -1.f;
-            int pjx = -1;
-            for (int r = 0; r < kp.K; ++r) {
-                float bk = __builtin_inff();
-                int bj = NPAD;
-#pragma unroll
-                for (int t = 0; t < PJ; ++t) {
-                    const int m = q + 2 * t;
-                    const bool above = key[t] > pk || (key[t] == pk && m > pjx);
-                    if (above && key[t] < bk) { bk = key[t]; bj = m; }
-                }
-                const float ok = dpp_f<quad_perm(1, 0, 3, 2)>(bk);
-                const int oj = dpp_i<quad_perm(1, 0, 3, 2)>(bj);
-                if (ok < bk || (ok == bk && oj < bj)) { bk = ok; bj = oj; }
-                if (bk == __builtin_inff()) break;
-                pk = bk;
-                pjx = bj;
-                if (q == 0) {
-                    const float4 pj = xch[2 * (dbase + bj)], vj = xch[2 * (dbase + bj) + 1];
-                    const float o0 = clampf(pj.x - P[0], -kp.room_range[0], kp.room_range[0]);
-                    const float o1 = clampf(pj.y - P[1], -kp.room_range[1], kp.room_range[1]);
-                    const float o2 = clampf(pj.z - P[2], -kp.room_range[2], kp.room_range[2]);
-                    const float o3 = clampf(vj.x - V[0], -vm, vm), o4 = clampf(vj.y - V[1], -vm, vm);
-                    const float o5 = clampf(vj.z - V[2], -vm, vm);
-                    float* o = out + kp.so_dim + r * 6;
-                    o[0] = o0; o[1] = o1; o[2] = o2; o[3] = o3; o[4] = o4; o[5] = o5;
-                }
-            }
-            return;
-        }
-    }
-#endif
 #pragma unroll
     for (int t = 0; t < PJ; ++t) {
         const int j = q + Q * t;
@@ -629,9 +585,6 @@ __device__ __forceinline__ float2* obst_tile(float* lds, const KP& kp, int slots
 // every sub-lane by DPP (every sub-lane holds the whole drone).  Addresses are b.st (SGPRs) + a 32-bit
 // per-lane byte offset: the int fields are reached through their offset from b.st (istate follows state
 // in the handle's workspace, qs_step.hip layout).
-#ifndef QS_COOP_STATE
-#define QS_COOP_STATE 1
-#endif
 constexpr int DRONE_WORDS = QS_F_GOAL + 3 + 4;
 // with episode_extra_stats on, the step also loads the drone's distance ring and window sums (fields
 // QS_F_DRING .. QS_F_DSUM + 2) in the same batch: words DRONE_WORDS .. LOAD_WORDS - 1
@@ -708,13 +661,9 @@ __device__ __forceinline__ void load_drone_q(const KP& kp, const Bufs& b, int g,
 }
 
 // ST: also the stats words DRONE_WORDS + k whose bit k of stmask is set (stw = their values).
-// old (optional): the words this sub-lane loaded at the start of the step (DroneWords::r): a word whose bits
-// did not change is not written back -- the goal, the previous-collision row and, for a drone resting on the
-// floor, most of its state.  Only for the step's first store of the drone (a reset stores again, unconditionally).
 template <int Q, bool ST = false>
 __device__ __forceinline__ void store_drone_q(const KP& kp, const Bufs& b, int g, int q, bool active, const Drone& d,
-                                              const float* stw = nullptr, uint32_t stmask = 0u,
-                                              const uint32_t* old = nullptr) {
+                                              const float* stw = nullptr, uint32_t stmask = 0u) {
     constexpr int NW = ST ? LOAD_WORDS : DRONE_WORDS;
     uint32_t wv[NW];
 #pragma unroll
@@ -749,34 +698,14 @@ __device__ __forceinline__ void store_drone_q(const KP& kp, const Bufs& b, int g
 #pragma unroll
         for (int k = 1; k < Q; ++k)
             if (q == k && t * Q + k < NW) v = wv[t * Q + k];
-        bool wr = w < DRONE_WORDS || (w < NW && ((stmask >> (w - DRONE_WORDS)) & 1u));
-        if (old) wr = wr && v != old[t];
+        const bool wr = w < DRONE_WORDS || (w < NW && ((stmask >> (w - DRONE_WORDS)) & 1u));
         if (active && wr) st_wt1(rs, drone_word_off(kp, b, w, go), 0u, v);
     }
 }
 
-// The env's episode-stat counters are stored once at the end of the step rather than where they change.
-#ifndef QS_CNT_DEFER
-#define QS_CNT_DEFER 1
-#endif
-// The step's 3x3 SDF obs dealt over the drone's sub-lanes (sdf_obs_q)
-#ifndef QS_SDF_DEAL
-#define QS_SDF_DEAL 1
-#endif
-// ... and counted only in steps where the wave saw an event to count
-#ifndef QS_CNT_GUARD
-#define QS_CNT_GUARD 1
-#endif
-// Experiment knob: drone words unchanged by the step are not stored back (store_drone_q's `old`).
-#ifndef QS_STORE_CHANGED
-#define QS_STORE_CHANGED 0   // A/B on MI355X: C3 9.45 vs 9.22 us, C4 14.59 vs 14.01 with it on (slower)
-#endif
 // Sub-lanes per drone of the flavor-B step kernel (QS_QB; 64 / NPAD when an env would not fit a wave).
 #ifndef QS_QB
 #define QS_QB 4
-#endif
-#ifndef QS_LOADS_FIRST
-#define QS_LOADS_FIRST 1
 #endif
 template <int NPAD>
 struct StepGeo {
@@ -786,107 +715,6 @@ struct StepGeo {
     static constexpr int SLOTS = EPB * NPAD;    // drone slots per workgroup
 };
 
-// ---------------------------------------------------------------------------------------------
-// The physics dealt over a drone's Q sub-lanes (QS_DEAL_PHYS): sub-lane q owns motors q + Q t (their
-// filter state, thrust and torque contributions, summed over the sub-lanes by DPP) and rows q + Q t of
-// the Rodrigues update (dR row @ R, rows broadcast by DPP).  The rest of the substep stays replicated.
-// Same expressions per element as substep(); the torque sums run in the pairwise order of qsum.
-// ---------------------------------------------------------------------------------------------
-#ifndef QS_DEAL_PHYS
-#define QS_DEAL_PHYS 0   // measured slower on MI355X (C3 7.95 -> 8.47 us): the DPP hops lengthen the chain
-#endif
-__device__ __forceinline__ float pick4(int k, float a0, float a1, float a2, float a3) {
-    return k == 0 ? a0 : (k == 1 ? a1 : (k == 2 ? a2 : a3));
-}
-template <int Q>
-struct OwnMotors {
-    static constexpr int T = 4 / Q;
-    float cmd[T], scmd[T], noise[T], rd[T], cd[T], tmax[T], pc0[T], pc1[T], pc2[T], tmc[T];
-};
-template <int Q>
-__device__ __forceinline__ void own_motors(const KP& kp, const Drone& d, const float* cmds, int q, OwnMotors<Q>& o) {
-#pragma unroll
-    for (int t = 0; t < OwnMotors<Q>::T; ++t) {
-        const int m = q + Q * t;
-        o.cmd[t] = pick4(m, cmds[0], cmds[1], cmds[2], cmds[3]);
-        o.scmd[t] = fsqrt(o.cmd[t]);
-        o.noise[t] = pick4(m, d.ou[0], d.ou[1], d.ou[2], d.ou[3]);
-        o.rd[t] = pick4(m, d.rd[0], d.rd[1], d.rd[2], d.rd[3]);
-        o.cd[t] = pick4(m, d.cd[0], d.cd[1], d.cd[2], d.cd[3]);
-        o.tmax[t] = pick4(m, kp.thrust_max[0], kp.thrust_max[1], kp.thrust_max[2], kp.thrust_max[3]);
-        o.pc0[t] = pick4(m, kp.pc0[0], kp.pc0[1], kp.pc0[2], kp.pc0[3]);
-        o.pc1[t] = pick4(m, kp.pc1[0], kp.pc1[1], kp.pc1[2], kp.pc1[3]);
-        o.pc2[t] = pick4(m, kp.pc2[0], kp.pc2[1], kp.pc2[2], kp.pc2[3]);
-        o.tmc[t] = pick4(m, kp.torque_max[0] * kp.ccw[0], kp.torque_max[1] * kp.ccw[1], kp.torque_max[2] * kp.ccw[2],
-                         kp.torque_max[3] * kp.ccw[3]);
-    }
-}
-template <int Q>
-__device__ __forceinline__ Torque motors_q(const KP& kp, OwnMotors<Q>& o) {
-    const bool p0 = kp.pc0[0] != 0.f || kp.pc0[1] != 0.f || kp.pc0[2] != 0.f || kp.pc0[3] != 0.f;
-    const bool p1 = kp.pc1[0] != 0.f || kp.pc1[1] != 0.f || kp.pc1[2] != 0.f || kp.pc1[3] != 0.f;
-    const bool p2 = kp.pc2[0] != 0.f || kp.pc2[1] != 0.f || kp.pc2[2] != 0.f || kp.pc2[3] != 0.f;
-    Torque t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int k = 0; k < OwnMotors<Q>::T; ++k) {   // motors() for the owned motors
-        const float cmd = o.cmd[k];
-        float tau = cmd < o.cd[k] ? kp.tau_down : kp.tau_up;
-        tau = fminf(tau, 1.0f);
-        o.rd[k] = tau * (o.scmd[k] - o.rd[k]) + o.rd[k];
-        const float c = clampf(o.rd[k] * o.rd[k] + cmd * o.noise[k], 0.f, 1.f);
-        o.cd[k] = c;
-        const float thr = o.tmax[k] * (kp.lin == 1.f ? c : (1.f - kp.lin) * c * c + kp.lin * c);
-        if (p0) t.t0 += o.pc0[k] * thr;
-        if (p1) t.t1 += o.pc1[k] * thr;
-        if (p2) t.t2 += o.pc2[k] * thr;
-        t.t2 += o.tmc[k] * c;
-        t.sum += thr;
-    }
-    t.t0 = qsum<Q>(t.t0);
-    t.t1 = qsum<Q>(t.t1);
-    t.t2 = qsum<Q>(t.t2);
-    t.sum = qsum<Q>(t.sum);
-    return t;
-}
-template <int Q, int TR>
-__device__ __forceinline__ void bcast_rows(const float (&rows)[TR][3], float* R) {
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-        R[j] = qbc<Q, 0 % Q>(rows[0 / Q][j]);
-        R[3 + j] = qbc<Q, 1 % Q>(rows[1 / Q][j]);
-        R[6 + j] = qbc<Q, 2 % Q>(rows[2 / Q][j]);
-    }
-}
-// the step's sim_steps substeps; cmds = the clipped motor commands, d.ou = this tick's OU noise
-template <int Q>
-__device__ __forceinline__ void physics_q(const KP& kp, Drone& d, const float* cmds, int q, const Rng& rng, uint32_t gid) {
-    constexpr int TR = (3 + Q - 1) / Q;
-    OwnMotors<Q> o;
-    own_motors<Q>(kp, d, cmds, q, o);
-    for (int s = 0; s < kp.sim_steps; ++s) {
-        const Torque tq = motors_q<Q>(kp, o);
-        const RodCoef rc = rod_coef(kp, d.rot, d.om);
-        float rows[TR][3];
-#pragma unroll
-        for (int t = 0; t < TR; ++t) {
-            const int r = min(q + Q * t, 2);
-            float dr[3];
-            rod_row(rc, r, dr);
-            rod_apply_row(dr, d.rot, rows[t]);
-        }
-        bcast_rows<Q, TR>(rows, d.rot);
-        substep_tail(kp, d, tq, rng, gid, s);
-        if (d.flags & QS_FL_CRASH_FLOOR) {   // the floor contact zeroed the filters (replicated copy too)
-#pragma unroll
-            for (int t = 0; t < OwnMotors<Q>::T; ++t) { o.rd[t] = 0.f; o.cd[t] = 0.f; }
-        }
-    }
-    // the owners' filter state back on every sub-lane (state store)
-    d.rd[0] = qbc<Q, 0 % Q>(o.rd[0 / Q]); d.cd[0] = qbc<Q, 0 % Q>(o.cd[0 / Q]);
-    d.rd[1] = qbc<Q, 1 % Q>(o.rd[1 / Q]); d.cd[1] = qbc<Q, 1 % Q>(o.cd[1 / Q]);
-    d.rd[2] = qbc<Q, 2 % Q>(o.rd[2 / Q]); d.cd[2] = qbc<Q, 2 % Q>(o.cd[2 / Q]);
-    d.rd[3] = qbc<Q, 3 % Q>(o.rd[3 / Q]); d.cd[3] = qbc<Q, 3 % Q>(o.cd[3 / Q]);
-}
 
 template <int NPAD, bool OBST>
 __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bufs b, RBufs r, RP rp) {
@@ -918,9 +746,6 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     if (OBST)   // the block's obstacle lists -> LDS (ordered by the first lds_sync below)
         for (int k = lane; k < nenv_blk * kp.M; k += 64) otile[k] = b.obst[(size_t)env0 * kp.M + k];
 
-#ifdef QS_STAGGER   // experiment: odd workgroups start later (phases of co-resident waves overlap)
-    if (blockIdx.x & 1) __builtin_amdgcn_s_sleep(QS_STAGGER);
-#endif
     // Every global load of the step is issued up front, back to back -- the action, the env's counters, the
     // drone's state words -- before anything waits: their HBM latencies overlap instead of adding up (the
     // scheduler otherwise sank the action load behind the state's waits).
@@ -928,20 +753,14 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     const int eidx = active ? env : 0;
     const int tick0 = b.env[QS_E_TICK * kp.E + eidx];
     const int episode = b.env[QS_E_EPISODE * kp.E + eidx];
-#ifndef QS_DIAG_LATE_EF
     const int32_t ef0 = b.env[QS_E_FLAGS * kp.E + eidx];   // the env's flags (rewritten at the end of the step)
-#endif
     // episode_extra_stats: the env's 11 counters QS_E_ST_COL.. dealt over its lanes (lane li holds li + LPE t)
     constexpr int NCNT = 11, CT = (NCNT + LPE - 1) / LPE;
     const int li = lane - lbase;
     const bool envok = env < kp.E;
     int cnt[CT];
-    bool cdirty[CT];   // the counter changed this step: stored once, at the end of the step (QS_CNT_DEFER)
-#ifdef QS_DIAG_CNT_AOS   // diagnostic builds only: the counters env-major in the estats rows (layout experiment)
-    auto cnt_at = [&](int k) -> int32_t* { return reinterpret_cast<int32_t*>(b.estats) + (size_t)env * kp.N * QS_NES + k; };
-#else
+    bool cdirty[CT];   // the counter changed this step: stored once, at the end of the step
     auto cnt_at = [&](int k) -> int32_t* { return b.env + (QS_E_ST_COL + k) * kp.E + env; };
-#endif
 #pragma unroll
     for (int t = 0; t < CT; ++t) {
         const int k = li + LPE * t;
@@ -949,24 +768,11 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
         cdirty[t] = false;
     }
     Drone d;   // every sub-lane holds the whole drone
-#if defined(QS_DIAG_NOLOAD)   // diagnostic builds only (QS_JIT_OPTS): phase-removal timing experiments
-    d = Drone{};
-    d.pos[2] = 2.f; d.rot[0] = d.rot[4] = d.rot[8] = 1.f; d.goal[2] = 2.f;
-    d.pos[0] = 0.01f * (float)(g % 97); d.pos[1] = 0.01f * (float)(g % 89);
-    float stw[STAT_WORDS] = {};
-#elif QS_COOP_STATE
     DroneWords<Q, LOAD_WORDS> dw;
     load_words_q(kp, b, g, q, dw, kp.stats ? LOAD_WORDS : DRONE_WORDS);
-#if QS_LOADS_FIRST
     __builtin_amdgcn_sched_barrier(0);
-#endif
     float stw[STAT_WORDS];
     unpack_words_q(dw, d, stw);
-#else
-    load_drone(kp, b, g, d);
-    float stw[STAT_WORDS];
-    for (int k = 0; k < STAT_WORDS; ++k) stw[k] = kp.stats ? b.st[(QS_F_DRING + k) * kp.I + g] : 0.f;
-#endif
     float a[4] = {av.x, av.y, av.z, av.w};
     const Rng rng = env_rng(seed, tick0, episode);
     const int tick = tick0 + 1;
@@ -1001,11 +807,7 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
 #pragma unroll
         for (int t = 0; t < 4 / Q; ++t) {
             const int k = q + Q * t;
-#ifdef QS_DIAG_NOPHILOX
-            for (int i = 0; i < 4; ++i) zr[t][i] = 0.001f * (float)(i + k);
-#else
             if (k == 0 || kp.sense) normals4(rng, gid, k == 0 ? S_OU : S_SENSOR, k == 0 ? 0u : (uint32_t)(k - 1), zr[t]);
-#endif
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -1020,33 +822,20 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     // ---- per-drone control + physics (QuadrotorSingle._step), replicated on the sub-lanes ----
     float rw = 0.f;
     bool floor_now = false;   // drone 0's on the env's flags: its rew_crash feeds the replay wrapper
+    float rc_dist, rc_effort, rc_orient, rc_spin;   // compute_reward_weighted's raw terms (per-step infos)
     {
 #pragma unroll
         for (int k = 0; k < 4; ++k) d.ou[k] = d.ou[k] + (kp.ou_theta * (kp.ou_mu - d.ou[k]) + kp.ou_sigma * zou[k]);
         float cmds[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) cmds[k] = 0.5f * (clampf(a[k], -1.f, 1.f) + 1.f);
-#if defined(QS_DIAG_NOPHYS)
-        for (int i = 0; i < 3; ++i) d.pos[i] += 0.01f * d.vel[i] + 0.001f * cmds[i];
-#elif QS_DEAL_PHYS
-        if constexpr (Q > 1) physics_q<Q>(kp, d, cmds, q, rng, gid);
-        else for (int s = 0; s < kp.sim_steps; ++s) substep(kp, d, cmds, d.ou, rng, gid, s);
-#else
         for (int s = 0; s < kp.sim_steps; ++s) substep(kp, d, cmds, d.ou, rng, gid, s);
-#endif
-#if 0
-        for (int i = 0; i < 3; ++i) d.pos[i] += 0.01f * d.vel[i] + 0.001f * cmds[i];
-#endif
         // compute_reward_weighted (quadrotor_single.py:34-66)
         const float gx = d.goal[0] - d.pos[0], gy = d.goal[1] - d.pos[1], gz = d.goal[2] - d.pos[2];
         const bool on_floor = d.flags & QS_FL_ON_FLOOR;
         floor_now = on_floor;
         const float dist = fsqrt(gx * gx + gy * gy + gz * gz);
-#ifdef QS_DIAG_NOST_RING   // diagnostic builds only (QS_JIT_OPTS)
-        if (false) {
-#else
         if (kp.stats && active) {   // distance_to_goal[i].append(-rewraw_pos) and reached_goal (:651-655)
-#endif
             // every sub-lane (the flags stay identical); the words reach HBM with the state's store burst
             const float v = kp.dt * dist;
             const int slot = tick % 5;
@@ -1068,10 +857,12 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
                 if (m / 5.f / kp.dt < 0.5f) d.flags |= QS_FL_REACHED;   // approch_goal_metric
             }
         }
-        const float cost = kpm.rew_pos * dist +
-                           kpm.rew_effort * fsqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2] + a[3] * a[3]) +
-                           kpm.rew_crash * (on_floor ? 1.f : 0.f) + kpm.rew_orient * (on_floor ? 1.f : -d.rot[8]) +
-                           kpm.rew_spin * fsqrt(d.om[0] * d.om[0] + d.om[1] * d.om[1] + d.om[2] * d.om[2]);
+        rc_dist = dist;
+        rc_effort = fsqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2] + a[3] * a[3]);
+        rc_orient = on_floor ? 1.f : -d.rot[8];
+        rc_spin = fsqrt(d.om[0] * d.om[0] + d.om[1] * d.om[1] + d.om[2] * d.om[2]);
+        const float cost = kpm.rew_pos * dist + kpm.rew_effort * rc_effort + kpm.rew_crash * (on_floor ? 1.f : 0.f) +
+                           kpm.rew_orient * rc_orient + kpm.rew_spin * rc_spin;
         rw = -kp.dt * cost;
     }
 
@@ -1081,11 +872,7 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     float pen = 0.f;
     if (q == 0) xch_put(xch, dbase + di, d.pos, d.vel);
     lds_sync();
-#ifndef QS_DIAG_NOCOLL
     if (kp.N > 1) {
-#else
-    if (false) {
-#endif
         // sub-lane q tests the partners j = q + Q t (LDS reads issued back to back, branch-free
         // tests), then the drone's collision row and proximity sum are reduced over the sub-lanes
         constexpr int PJ = (NPAD + Q - 1) / Q;
@@ -1128,22 +915,14 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     int ohit = -1;
     bool onew = false;
     if (OBST) {
-#if QS_SDF_DEAL
         ohit = (Q == 2 || Q == 4) ? obst_detect_q<Q>(og, myob, d.pos[0], d.pos[1], q) : obst_detect(og, myob, d.pos[0], d.pos[1]);
-#else
-        ohit = obst_detect(og, myob, d.pos[0], d.pos[1]);
-#endif
         onew = active && ohit >= 0 && !(d.flags & QS_FL_PREV_OBST);
         rw += kpm.quadcol_obst * (onew ? -1.f : 0.f);
         d.flags = (d.flags & ~(uint32_t)QS_FL_PREV_OBST) | (ohit >= 0 ? (uint32_t)QS_FL_PREV_OBST : 0u);
     }
     bool any_onew = false;   // curr_quad_col non-empty (quadrotor_multi.py:576)
     if (OBST) any_onew = ((__ballot(onew && q == 0) >> lbase) & lmask) != 0;
-#ifdef QS_DIAG_NOST_COUNT
-    if (false) {
-#else
     if (kp.stats) {   // episode_extra_stats counters (quadrotor_multi.py:555-566, 575-589, 599-606, 631-635)
-#endif
         auto env_count = [&](bool x) { return __popcll((__ballot(x && q == 0) >> lbase) & lmask); };
         const bool settle = tick >= kp.st_settle;
         const bool cfloor = active && (d.flags & QS_FL_CRASH_FLOOR);
@@ -1152,9 +931,7 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
         // every count below is zero unless one of these events happened somewhere in the wave (a new
         // collision, a first floor contact, a new wall / ceiling / room crash, a new pillar hit): one
         // wave-uniform test skips the per-env counting in the common step
-#if QS_CNT_GUARD
         if (__ballot(q == 0 && (uniq || cfloor || (active && (wall_new || ceil_new)) || room_new || (OBST && onew))))
-#endif
         {
         const int col = env_count(uniq) / 2;   // len(last_step_unique_collisions) // 2
         if (col > 0 && settle && uniq) d.flags |= QS_FL_HIT_AGENT;
@@ -1191,17 +968,9 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
                             k == 3 ? (settle ? nw : 0) : k == 4 ? (settle ? nc : 0) :
                             k == 5 ? (settle ? col : 0) : k == 6 ? (fin5 ? col : 0) : k == 7 ? oc :
                             k == 8 ? (os ? oc : 0) : k == 9 ? (os ? o35 : 0) : k == 10 ? (os ? o5 : 0) : 0;
-#ifdef QS_DIAG_NOST_CSTORE
-            if (false) {
-#else
             if (envok && k < NCNT && inc != 0) {
-#endif
                 cnt[t] += inc;
-#if QS_CNT_DEFER
                 cdirty[t] = true;
-#else
-                *cnt_at(k) = cnt[t];
-#endif
             }
         }
         }
@@ -1212,23 +981,11 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     bool vchanged = false;
     if (kp.downwash && kp.N > 1)   // perform_downwash (aerodynamics/downwash.py:4-51)
         vchanged = downwash_env<NPAD, Q>(kp, d, rng, gid, env, lbase, di, q, active,
-                                         (QS_DW_LDS && kp.obs_dim >= 8) ? reinterpret_cast<float4*>(lds) : nullptr, dbase);
-#ifndef QS_DIAG_NOIMPULSE
+                                         kp.obs_dim >= 8 ? reinterpret_cast<float4*>(lds) : nullptr, dbase);
     if (kp.collide) {
-#else
-    if (false) {
-#endif
         // drone-drone impulses, pairs in (i, j) order; a wave-uniform loop over pending events.
         // Ballots read sub-lane 0 of each drone (bit lbase + i * Q).
-#if defined(QS_DIAG_NOPAIR)
-        uint64_t pend = 0ull;
-#elif defined(QS_DIAG_PAIRNEVER)   // the loop stays in the code, no event ever runs it
-        uint32_t zero_ = 0u;
-        asm volatile("" : "+v"(zero_));
-        uint64_t pend = active ? (newpairs & ~((2ull << di) - 1ull)) & (uint64_t)zero_ : 0ull;
-#else
         uint64_t pend = active ? (newpairs & ~((2ull << di) - 1ull)) : 0ull;
-#endif
         for (;;) {
             const uint64_t bal = __ballot(pend != 0ull && q == 0);
             if (bal == 0ull) break;
@@ -1294,11 +1051,7 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
             collide_obstacle(kp, og, d, myob[ohit].x, myob[ohit].y, z, u);
             vchanged = true;
         }
-#ifdef QS_DIAG_NOWALL
-        if (false) {
-#else
         if (active && (wall_new || ceil_new)) {
-#endif
             float u[12];
             if (wall_new) {
                 qdraws<Q, 0, 3>(rng, gid, S_WALL, S_WALL, q, nullptr, u);
@@ -1340,27 +1093,23 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
 
     // The drone state is final here (unless its env resets below, which stores it again): storing it now
     // lets its write-through bytes drain while the observations are computed.
-#if defined(QS_DIAG_NOSTORE)
-#elif QS_COOP_STATE
-#ifdef QS_DIAG_NOST_RSTORE
-    stmask = 0u;
-#endif
-#if QS_STORE_CHANGED && !defined(QS_DIAG_NOLOAD)
-    const uint32_t* old_words = dw.r;
-#else
-    const uint32_t* old_words = nullptr;
-#endif
-    if (kp.stats) store_drone_q<Q, true>(kp, b, g, q, active, d, stw, stmask, old_words);
-    else store_drone_q<Q>(kp, b, g, q, active, d, nullptr, 0u, old_words);
-#else
-    if (lead) store_drone(kp, b, g, d);
-    if (lead)
-        for (int k = 0; k < STAT_WORDS; ++k)
-            if ((stmask >> k) & 1u) b.st[(QS_F_DRING + k) * kp.I + g] = stw[k];
-#endif
+    if (kp.stats) store_drone_q<Q, true>(kp, b, g, q, active, d, stw, stmask);
+    else store_drone_q<Q>(kp, b, g, q, active, d);
     if (lead) {
         b.rew[g] = rw;
         b.done[g] = done ? 1 : 0;
+    }
+    if (kp.rcomp && active) {   // per-step infos: the reward components (QS_RI_*), fields dealt over the sub-lanes
+        const float rc[QS_NRI] = {rc_dist, rc_effort, floor_now ? 1.f : 0.f, rc_orient, rc_spin,
+                                  (any_uniq && uniq) ? -1.f : 0.f, -(kp.cdt * pen), onew ? -1.f : 0.f};
+#pragma unroll
+        for (int t = 0; t < (QS_NRI + Q - 1) / Q; ++t) {
+            float v = rc[t * Q];
+#pragma unroll
+            for (int k = 1; k < Q; ++k)
+                if (q == k && t * Q + k < QS_NRI) v = rc[t * Q + k];
+            if (t * Q + q < QS_NRI) b.rcomp[(size_t)(t * Q + q) * kp.I + g] = v;
+        }
     }
     QS_STAMP(4);
     // ---- observations (post-impulse state; quadrotor_multi.py:704-720) ----
@@ -1371,11 +1120,7 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
         lds_sync();
     }
     QS_STAMP(5);
-#ifndef QS_DIAG_NOSELFOBS
     if (lead) {
-#else
-    if (false) {
-#endif
         if (SCEN) {   // the self obs measure against the goal the reference's observation saw
             Drone dv = d;
             for (int k = 0; k < 3; ++k) dv.goal[k] = obs_goal[k];
@@ -1385,23 +1130,13 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
         }
     }
     QS_STAMP(6);
-#ifndef QS_DIAG_NONBR
     if (nbr) neighbor_obs<NPAD, Q>(kp, xch, dbase, di, q, d.pos, d.vel, active, row);
-#endif
-#if QS_SDF_DEAL
     if (OBST && active) sdf_obs_q<Q>(kp, og, myob, d.pos[0], d.pos[1], row + kp.obs_dim - 9, q);   // MultiObstacles.step
-#else
-    if (OBST && lead) sdf_obs(kp, og, myob, d.pos[0], d.pos[1], row + kp.obs_dim - 9);   // MultiObstacles.step
-#endif
     QS_STAMP(7);
     // non-finite guard of the stepped drone and its reward (before a fused reset replaces the drone)
     const bool state_bad = lead && drone_nonfinite(d), rew_bad = lead && !(rw * 0.f == 0.f);
 
-#ifdef QS_DIAG_NODONE
-    const uint64_t dball = 0;
-#else
     const uint64_t dball = __ballot(active && done);
-#endif
     if (dball) {  // rare: some env of this block finished -> terminal obs + fused auto-reset (:739-838)
         lds_sync();
         // terminal obs: the finished envs' rows (contiguous in the tile and in HBM), all lanes of the wave;
@@ -1448,12 +1183,8 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
             for (int t = 0; t < CT; ++t) {
                 const int k = li + LPE * t;
                 if (envok && done && k < NCNT) {
-#if QS_CNT_DEFER
                     cnt[t] = 0;
                     cdirty[t] = true;
-#else
-                    b.env[(QS_E_ST_COL + k) * kp.E + env] = 0;
-#endif
                 }
             }
         }
@@ -1501,20 +1232,12 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
             self_obs(kp, d, rng, gid, S_RESET_SENSOR, row);
         }
         // the reset drones' state (the stepped state was stored before the obs phase)
-#if QS_COOP_STATE
         if (kp.stats) {
             const float zero[STAT_WORDS] = {};
             store_drone_q<Q, true>(kp, b, g, q, active && done, d, zero, (1u << STAT_WORDS) - 1u);
         } else {
             store_drone_q<Q>(kp, b, g, q, active && done, d);
         }
-#else
-        if (lead && done) {
-            store_drone(kp, b, g, d);
-            if (kp.stats)
-                for (int k = 0; k < STAT_WORDS; ++k) b.st[(QS_F_DRING + k) * kp.I + g] = 0.f;
-        }
-#endif
         if (nbr) {
             if (q == 0) xch_put(xch, dbase + di, d.pos, sv);
             lds_sync();
@@ -1528,22 +1251,14 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     }
     lds_sync();
     QS_STAMP(8);
-#ifndef QS_DIAG_NOOBSSTORE
     const int obs_bad = tile_store(lds, b.obs + (size_t)env0 * kp.N * kp.obs_dim, rows * kp.obs_dim, lane);
-#else
-    const int obs_bad = 0;
-#endif
     QS_STAMP(9);
 
     if (lead) {
         if (di == 0) {
             b.env[QS_E_TICK * kp.E + env] = done ? 0 : tick;
             if (done) b.env[QS_E_EPISODE * kp.E + env] = episode + 1;
-#ifdef QS_DIAG_LATE_EF
-            const int32_t ef = b.env[QS_E_FLAGS * kp.E + env];
-#else
             const int32_t ef = ef0;
-#endif
             int32_t nf = done ? (ef | QS_EF_STALE) : (ef & ~QS_EF_STALE);
             // what the replay wrapper reads of this step (quad_experience_replay.py:161-163, quadrotor_multi.py:725)
             nf = (nf & ~(QS_EF_NEWCOL | QS_EF_FLOOR0)) | ((any_uniq || any_onew) ? QS_EF_NEWCOL : 0) |
@@ -1551,7 +1266,6 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
             if (nf != ef) b.env[QS_E_FLAGS * kp.E + env] = nf;
         }
     }
-#if QS_CNT_DEFER
     // the env's episode counters that changed this step (a finished env's zeroed ones included), after every
     // other global access of the step: a store issued mid-step made the step's later memory waits wait for it
     if (kp.stats) {
@@ -1561,10 +1275,7 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
             if (envok && k < NCNT && cdirty[t]) *cnt_at(k) = cnt[t];
         }
     }
-#endif
-#ifndef QS_DIAG_NOGUARD
     guard_count(b, obs_bad, rew_bad, state_bad);
-#endif
     QS_STAMP(10);
     if (r.ri != nullptr) {   // experience replay on (uniform): ExperienceReplayWrapper.step of every env (:124-180)
         // the step's global stores above are read back by other lanes of the wave: workgroup-scope

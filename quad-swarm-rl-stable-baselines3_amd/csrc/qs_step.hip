@@ -170,8 +170,11 @@ static int validate(const qs_config* c) {
     if (c->neighbor_obs != QS_NEIGHBOR_NONE && (c->k_neighbors < 1 || c->k_neighbors > c->num_agents - 1))
         return fail(QS_E_INVALID, "k_neighbors must be in [1, num_agents-1]");
     if (c->sim_steps < 1 || c->svd_every < 1 || c->ep_len < 0) return fail(QS_E_INVALID, "bad sim_steps/svd_every/ep_len");
-    // SoA offsets are 32-bit byte offsets (buffer stores): 64 fields x 4 B x I must stay below 4 GB
-    if ((long long)c->num_envs * c->num_agents > (1ll << 32) / 256) return fail(QS_E_INVALID, "too many drones");
+    // The drone state is addressed by 32-bit byte offsets from the state buffer, and the step's state stores go
+    // through a buffer descriptor of 0x7fffffff records (qs_rsrc): the last istate word, at most
+    // 4 (QS_NF + QS_NI) I + 255 bytes from the state base, must stay inside it (I <= 7 895 160 drones).
+    if (4ll * (QS_NF + QS_NI) * ((long long)c->num_envs * c->num_agents) + 256 > 0x7fffffffll)
+        return fail(QS_E_INVALID, "too many drones: 4 (QS_NF + QS_NI) num_envs num_agents + 256 must stay below 2^31");
     return QS_OK;
 }
 
@@ -212,6 +215,7 @@ static qs_layout make_layout(const qs_config* c) {
     L.reset_info = o; o = al(o + E);
     L.stats = o; o = al(o + sizeof(uint64_t) * QS_NSTAT);
     L.estats = o; o = al(o + sizeof(float) * QS_NES * (c->episode_stats ? I : 0));
+    L.rew_info = o; o = al(o + sizeof(float) * QS_NRI * (c->step_infos ? I : 0));
     L.total_bytes = o;
     L.obs_dim = od;
     L.num_drones = (int32_t)I;
@@ -350,6 +354,7 @@ static qs::KP make_kp(const qs_config* c, const qs_layout& L) {
     if (!c->use_obstacles && c->scenario >= QS_SCEN_MIX && c->scenario <= QS_SCEN_RUN_AWAY)
         k.scen_b = c->scenario == QS_SCEN_MIX ? 10 : c->scenario - QS_SCEN_MIX;
     if (c->flavor == QS_FLAVOR_A) make_kp_a(c, k);
+    k.rcomp = c->step_infos ? 1 : 0;
     if (c->episode_stats) {   // quadrotor_multi.py:156-161, 651-655, 761-774; quadrotor_multi_rewards.py:131-136
         double freq = 1.0 / (double)c->control_dt;   // control_freq (100 for the reference's 0.01 s)
         if (fabs(freq - (double)llround(freq)) < 1e-4) freq = (double)llround(freq);
@@ -581,6 +586,7 @@ static qs::Bufs bufs_of(qs_handle* h) {
     b.mask = nullptr;
     b.stats = (unsigned long long*)(w + h->lay.stats);
     b.estats = (float*)(w + h->lay.estats);
+    b.rcomp = (float*)(w + h->lay.rew_info);
     return b;
 }
 
@@ -591,6 +597,7 @@ extern "C" int qs_buffers_get(qs_handle* h, qs_buffers* o) {
     o->obs = b.obs; o->term_obs = b.term; o->rew = b.rew; o->done = b.done; o->reset_info = b.rinfo;
     o->stats = (uint64_t*)b.stats;
     o->estats = h->cfg.episode_stats ? b.estats : nullptr;
+    o->rew_info = h->cfg.step_infos ? b.rcomp : nullptr;
     return QS_OK;
 }
 
@@ -1106,7 +1113,7 @@ extern "C" int qs_specialize(qs_handle* h, int enable) {
     int qb, qa;
     jit_lanes(&qb, &qa);
     if (shm_bytes(h->cfg, h->lay.obs_dim, h->npad, true, qb, qa) > QS_LDS_MAX)
-        return fail(QS_E_UNSUPPORTED, "QS_QB / QS_QA geometry exceeds 64 KB of LDS per workgroup");
+        return fail(QS_E_UNSUPPORTED, "QS_QB / QS_QA geometry exceeds the 160 KB of LDS of a workgroup");
     std::string rn;
     const std::string key = std::to_string(h->device) + "|" + kernel_names(&h->cfg, h->kp, h->npad, &rn) + "|" +
                             std::to_string(qb) + "," + std::to_string(qa) + "|" +

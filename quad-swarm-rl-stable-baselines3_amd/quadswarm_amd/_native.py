@@ -9,7 +9,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("QUADSWARM_LIB", os.path.join(HERE, "lib", "libquadswarm.so"))
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 MAX_AGENTS = 64
 MAX_DR_CHOICES = 8
 F, I32, U32, U64, SZ = ctypes.c_float, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_size_t
@@ -73,6 +73,7 @@ class QsConfig(ctypes.Structure):
         ("dr_num_counts", I32), ("dr_counts", I32 * MAX_DR_CHOICES), ("dr_num_sizes", I32),
         ("dr_sizes", F * MAX_DR_CHOICES),
         ("episode_stats", I32),
+        ("step_infos", I32),
     ]
 
 
@@ -80,15 +81,19 @@ class QsLayout(ctypes.Structure):
     _fields_ = [("params", SZ), ("state", SZ), ("istate", SZ), ("env", SZ), ("env_f", SZ), ("obst", SZ), ("stale_vel", SZ),
                 ("obs", SZ),
                 ("term_obs", SZ), ("rew", SZ), ("done", SZ), ("reset_info", SZ), ("stats", SZ), ("estats", SZ),
-                ("total_bytes", SZ),
+                ("rew_info", SZ), ("total_bytes", SZ),
                 ("obs_dim", I32),
                 ("num_drones", I32)]
 
 
 class QsBuffers(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in ("state", "istate", "env", "env_f", "obst", "stale_vel", "obs", "term_obs",
-                                               "rew", "done", "reset_info", "stats", "estats")]
+                                               "rew", "done", "reset_info", "stats", "estats", "rew_info")]
 
+
+# per-step reward components, rows of buffers.rew_info (qs_rinfo)
+RI_DIST, RI_EFFORT, RI_CRASH, RI_ORIENT, RI_SPIN, RI_QUADCOL, RI_PROX, RI_OBST, NRI = range(9)
+RI_GOAL_DIST = 0   # flavor A
 
 # non-finite guard counters (qs_stat / qs_stats)
 ST_OBS, ST_REW, ST_STATE, NSTAT = 0, 1, 2, 4

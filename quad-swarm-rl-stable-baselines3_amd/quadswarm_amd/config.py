@@ -73,6 +73,11 @@ class QuadSwarmConfig:
     # ---- episode_extra_stats (flavor B, quadrotor_multi.py:739-831): the reference always keeps them; the
     # step kernels do so when on (infos of finished envs, GpuQuadVecEnv) ----
     episode_stats: bool = True
+    # ---- per-step infos (quadrotor_single.py:79-105, quadrotor_multi.py:642-651; flavor A
+    # quadrotor_single_rewards.py:457): the step writes each drone's reward components (buffers.rew_info), from
+    # which GpuQuadVecEnv builds infos[i]["rewards"] / infos[i]["goal_dist"].  Off for the raw env (the bench's
+    # step does not pay for it); GpuQuadVecEnv turns it on (infos=True) ----
+    step_infos: bool = False
 
     @classmethod
     def c4(cls, num_envs=4096, num_agents=8, **over):
@@ -341,4 +346,5 @@ class QuadSwarmConfig:
                 for i, v in enumerate(sizes):
                     c.dr_sizes[i] = float(v)
         c.episode_stats = 1 if self.episode_stats else 0
+        c.step_infos = 1 if self.step_infos else 0
         return c

@@ -70,8 +70,16 @@ class QuadSwarmEnv:
         from .stats import NES
         # episode_extra_stats rows [I, QS_NES] (written for the drones of envs that finished in a step)
         self.estats = view(lay.estats, 4 * NES * I, torch.float32, (I, NES)) if self.qcfg.episode_stats else None
+        # the last step's reward components [QS_NRI, I] (config step_infos; quadswarm_amd.infos builds the dicts)
+        self.rew_info = view(lay.rew_info, 4 * N.NRI * I, torch.float32, (N.NRI, I)) if self.qcfg.step_infos else None
         self.act_dim = cfg.act_dim
         self._align = 8 if cfg.flavor == "A" else 16
+        # the reward coefficients the kernels use, as the host set them (float64: what the reference's rew_coeff
+        # holds; infos[i]["rewards"] is built with them)
+        r = cfg.rew_coeff
+        self._coeff = {"pos": r.get("pos", 1.0), "effort": r.get("effort", 0.05), "crash": r.get("crash", 1.0),
+                       "orient": r.get("orient", 1.0), "spin": r.get("spin", 0.1),
+                       "quadcol_bin": float(cfg.collision_reward), "quadcol_bin_obst": float(cfg.obst_collision_reward)}
         self._torch = torch
         self.replay = None
         if cfg.replay_buffer_sample_prob > 0:
@@ -178,8 +186,17 @@ class QuadSwarmEnv:
         return bool(N.lib().qs_is_specialized(self._h))
 
     # ------------------------------------------------------------------------------------------
+    _COEFF_PARAMS = {"rew_pos": "pos", "rew_effort": "effort", "rew_crash": "crash", "rew_orient": "orient",
+                     "rew_spin": "spin", "quadcol_bin": "quadcol_bin", "quadcol_bin_obst": "quadcol_bin_obst"}
+
     def set_param(self, key, value):
         N.check(N.lib().qs_set_param(self._h, key.encode(), float(value)), "qs_set_param")
+        if key in self._COEFF_PARAMS:
+            self._coeff[self._COEFF_PARAMS[key]] = float(value)
+
+    def reward_coefficients(self):
+        """The reward coefficients of the next step (rew_coeff + quadcol_bin / quadcol_bin_obst), float64."""
+        return dict(self._coeff)
 
     def get_param(self, key):
         v = ctypes.c_double()

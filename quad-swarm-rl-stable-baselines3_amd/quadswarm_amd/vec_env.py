@@ -56,17 +56,42 @@ _EMPTY = types.MappingProxyType({})
 
 
 class StepInfos(Sequence):
-    """infos of one step, len == num_envs (agent rows).  Rows of finished envs get a fresh dict with
-    terminal_observation (and episode_extra_stats, quadrotor_multi.py:739-831, when the env keeps them); every
-    other row is a shared read-only empty mapping, so a 32k-agent step does not build 32k dicts."""
+    """infos of one step, len == num_envs (agent rows).  Rows of finished envs get terminal_observation (and
+    episode_extra_stats, quadrotor_multi.py:739-831, when the env keeps them).  With per-step infos on, every row
+    carries the reference's per-agent entries: flavor B {"rewards": {...}} (quadrotor_single.py:79-105, 371;
+    quadrotor_multi.py:642-651), flavor A {"rewards": {}, "goal_dist": ...} (quadrotor_single_rewards.py:457);
+    their dicts are built when a row is read, so a 32k-agent step does not build 32k dicts.  Without them a row
+    that did not finish is a shared read-only empty mapping.
 
-    def __init__(self, n, done_rows=(), term=None, extra=None):
+    Native mode builds it lazily: nothing is copied to the host until a row (or the done rows) is read, which
+    must happen before the next step_wait (the device buffers it reads are the step's)."""
+
+    def __init__(self, n, done_rows=(), term=None, extra=None, rewards=None, goal_dist=None, resolve=None):
         self._n = n
+        self._resolve = resolve
+        self._d = None
+        if resolve is None:
+            self._build(done_rows, term, extra, rewards, goal_dist)
+
+    def _build(self, done_rows, term, extra, rewards, goal_dist):
+        self._rows = np.asarray(done_rows, dtype=np.int64)
+        self._rewards, self._gd = rewards, goal_dist
         self._d = {}
-        for k, r in enumerate(done_rows):
-            self._d[int(r)] = {"terminal_observation": term[int(r)], "TimeLimit.truncated": False}
+        for k, r in enumerate(self._rows.tolist()):
+            self._d[r] = {"terminal_observation": term[r], "TimeLimit.truncated": False}
             if extra is not None:
-                self._d[int(r)]["episode_extra_stats"] = extra[k]
+                self._d[r]["episode_extra_stats"] = extra[k]
+
+    def _ready(self):
+        if self._d is None:
+            self._build(*self._resolve())
+            self._resolve = None
+
+    @property
+    def done_rows(self):
+        """Agent rows of the envs that finished in this step (host int64 array)."""
+        self._ready()
+        return self._rows
 
     def __len__(self):
         return self._n
@@ -78,17 +103,35 @@ class StepInfos(Sequence):
             i += self._n
         if not 0 <= i < self._n:
             raise IndexError(i)
-        return self._d.get(i, _EMPTY)
+        self._ready()
+        base = self._d.get(i)
+        if self._rewards is None and self._gd is None:
+            return _EMPTY if base is None else base
+        row = {} if base is None else dict(base)
+        if self._rewards is not None:
+            from .infos import rewards_dict
+            row["rewards"] = rewards_dict(self._rewards, i)
+        else:
+            row["rewards"] = {}
+            row["goal_dist"] = float(self._gd[i])
+        return row
 
 
 class GpuQuadVecEnv:
     """raise_on_nan: like QuadrotorSingle's reward check (quadrotor_single.py:87-90), raise ValueError when a
-    step produced a non-finite reward (the kernels' qs_counters guard, read with the step's done rows)."""
+    step produced a non-finite reward (the kernels' qs_counters guard).  Compat mode checks every step when it
+    reads the step's results; native mode never waits for the device: it polls a stream-ordered copy of the
+    counter and raises at the first step_wait that finds it increased (at most a few steps late).
+    infos: per-step infos (config step_infos): infos[i]["rewards"] (flavor B) / infos[i]["goal_dist"] (flavor A)
+    on every agent row, like the reference's step."""
 
-    def __init__(self, cfg: QuadSwarmConfig = None, as_torch=False, device=None, raise_on_nan=True, **cfg_over):
+    def __init__(self, cfg: QuadSwarmConfig = None, as_torch=False, device=None, raise_on_nan=True, infos=True,
+                 **cfg_over):
         cfg = cfg or QuadSwarmConfig()
         for k, v in cfg_over.items():
             setattr(cfg, k, v)
+        if infos:
+            cfg.step_infos = True
         self.cfg = cfg
         self.env = QuadSwarmEnv(cfg, device=device)
         self.agents_per_env = cfg.num_agents
@@ -101,45 +144,107 @@ class GpuQuadVecEnv:
         self.batch = 0
         self.waiting = False
         self.closed = False
-        self.reset_infos = tuple(None for _ in range(cfg.num_envs))
+        self._reset_infos = tuple(None for _ in range(cfg.num_envs))
+        self._last_infos = None
         self._actions = None
         self.render_mode = None
         self.raise_on_nan = raise_on_nan
-        self._nan_seen = 0
+        self._nan_last = 0      # the non-finite reward counter as last read
+        self._gen = 0           # step counter: lazy infos of an older step refuse to resolve
+        self._nan_host = self._nan_ev = None
+        if as_torch:            # a pinned slot + event for the stream-ordered counter copy (native mode)
+            import torch
+            self._nan_host = torch.zeros(1, dtype=torch.int64, pin_memory=True)
+            self._nan_ev = torch.cuda.Event()
+            self._nan_pending = False
 
     # ---- VecEnv API ----
     def reset(self):
         obs = self.env.reset()
         if self.cfg.flavor == "A":
             ri = self.env.reset_info.cpu().numpy()
-            self.reset_infos = tuple({"success": bool(v == 2)} for v in ri)
+            self._reset_infos = tuple({"success": bool(v == 2)} for v in ri)
         else:
-            self.reset_infos = tuple({} for _ in range(self.cfg.num_envs))
+            self._reset_infos = tuple({} for _ in range(self.cfg.num_envs))
+        self._last_infos = None
         return obs if self.as_torch else obs.cpu().numpy()
+
+    @property
+    def reset_infos(self):
+        """Per env: {"success": bool} (flavor A) / {} (flavor B) when the env was reset by the last call, else None
+        (SubprocVecEnvCustom.reset_infos, subproc_vec_env_custom.py:152, 162).  Native mode computes it on first
+        read after a step."""
+        if self._last_infos is not None:
+            self._reset_infos = self._reset_infos_of(self._last_infos.done_rows)
+            self._last_infos = None
+        return self._reset_infos
+
+    @reset_infos.setter
+    def reset_infos(self, v):
+        self._reset_infos, self._last_infos = v, None
 
     def step_async(self, actions):
         self._actions = actions
         self.waiting = True
 
+    def _check_nan(self, value):
+        """Raise on any increase of the non-finite reward counter since the last read; a drop means it was
+        reset (qs_counters_reset through any path): resynchronise."""
+        v = int(value)
+        last, self._nan_last = self._nan_last, v
+        if self.raise_on_nan and v > last:
+            raise ValueError("QuadEnv: reward is Nan")
+
     def step_wait(self):
         import torch
 
+        if self.as_torch and self._nan_pending and self._nan_ev.query():   # the previous copy has landed
+            self._nan_pending = False
+            self._check_nan(self._nan_host[0])
         obs, rew, done, term = self.env.step(self._actions)
         self.waiting = False
         self.batch += 1
+        self._gen += 1
         d = done.bool()
-        # one small D2H sync (like the pipes' recv): the finished rows and the non-finite reward counter
-        h = torch.cat([torch.nonzero(d).flatten(), self.env.stats[N.ST_REW:N.ST_REW + 1]]).cpu().numpy()
-        rows, nan_rew = h[:-1], int(h[-1])
-        if self.raise_on_nan and nan_rew > self._nan_seen:
-            self._nan_seen = nan_rew
-            raise ValueError("QuadEnv: reward is Nan")
-        self._set_reset_infos(rows)
-        extra = self._episode_extra_stats(rows) if len(rows) else None
         if self.as_torch:
-            return obs, rew, d, StepInfos(self.num_envs, rows, term, extra)
+            # nothing leaves the device here: the counter is copied stream-ordered into pinned memory, the
+            # infos resolve on first read
+            if not self._nan_pending:
+                self._nan_host.copy_(self.env.stats[N.ST_REW:N.ST_REW + 1], non_blocking=True)
+                self._nan_ev.record()
+                self._nan_pending = True
+            gen = self._gen
+            comp = self.env.rew_info.clone() if self.env.rew_info is not None else None
+
+            def resolve():
+                if gen != self._gen:
+                    raise RuntimeError("GpuQuadVecEnv infos of an older step: read them before the next step_wait")
+                rows = torch.nonzero(d).flatten().cpu().numpy()
+                return (rows, term, self._episode_extra_stats(rows) if len(rows) else None) + \
+                    self._step_info_columns(comp)
+            infos = StepInfos(self.num_envs, resolve=resolve)
+            self._last_infos = infos
+            return obs, rew, d, infos
+        # compat: one small D2H read (like the pipes' recv): the finished rows and the non-finite reward counter
+        h = torch.cat([torch.nonzero(d).flatten(), self.env.stats[N.ST_REW:N.ST_REW + 1]]).cpu().numpy()
+        rows = h[:-1]
+        self._check_nan(h[-1])
+        self._reset_infos, self._last_infos = self._reset_infos_of(rows), None
+        extra = self._episode_extra_stats(rows) if len(rows) else None
         term_np = term.cpu().numpy() if len(rows) else None
-        return obs.cpu().numpy(), rew.cpu().numpy(), d.cpu().numpy(), StepInfos(self.num_envs, rows, term_np, extra)
+        cols = self._step_info_columns(self.env.rew_info)
+        return obs.cpu().numpy(), rew.cpu().numpy(), d.cpu().numpy(), StepInfos(self.num_envs, rows, term_np, extra,
+                                                                               *cols)
+
+    def _step_info_columns(self, comp):
+        """(flavor-B reward columns, flavor-A goal distances) of a step's reward components (None when off)."""
+        if comp is None:
+            return None, None
+        c = comp.cpu().numpy()
+        if self.cfg.flavor == "A":
+            return None, c[N.RI_GOAL_DIST]
+        from .infos import reward_columns_b
+        return reward_columns_b(c, self.env.reward_coefficients(), float(self.cfg.dt), self.cfg.use_obstacles), None
 
     def _episode_extra_stats(self, rows):
         """infos[i]["episode_extra_stats"] of the finished rows: the env's counters (quadrotor_multi.py:739-831)
@@ -181,16 +286,15 @@ class GpuQuadVecEnv:
 
     def reset_counters(self):
         self.env.reset_counters()
-        self._nan_seen = 0
+        self._nan_last = 0
 
     def step(self, actions):
         self.step_async(actions)
         return self.step_wait()
 
-    def _set_reset_infos(self, done_rows):
+    def _reset_infos_of(self, done_rows):
         if len(done_rows) == 0:
-            self.reset_infos = (None,) * self.cfg.num_envs
-            return
+            return (None,) * self.cfg.num_envs
         envs = sorted(set(int(r) // self.agents_per_env for r in np.asarray(done_rows).tolist()))
         ri = [None] * self.cfg.num_envs
         if self.cfg.flavor == "A":
@@ -200,7 +304,7 @@ class GpuQuadVecEnv:
         else:
             for e in envs:
                 ri[e] = {}
-        self.reset_infos = tuple(ri)
+        return tuple(ri)
 
     def close(self):
         if not self.closed:

@@ -257,33 +257,104 @@ def crowd(oenv, rng, frac_pairs=0.5, walls=True):
             oenv.envs[e].tick = oenv.p.ep_len   # finishes on the next step
 
 
-def assert_obs_match(gpu_obs, want_obs, oenv, so_dim, K, atol=2e-4, rtol=1e-4, key_tol=1e-4):
-    """Compare observations; a neighbour block may legitimately differ from the oracle's when the
-    K-th and (K+1)-th sort keys tie within fp32 rounding.  Such rows are accepted if every GPU slot
-    is the (clipped) relative vector of a real neighbour whose oracle key is within key_tol of the
-    K-th smallest, and the self part matches."""
-    bad = ~np.isclose(gpu_obs, want_obs, atol=atol, rtol=rtol)
+# flavor-B neighbour slots accepted only through a sort-key tie (assert_obs_match), counted per kind
+EXCUSES_B = {"slot_order_tie": 0, "selection_tie": 0, "rows": 0}
+
+
+def _one_to_one(cands):
+    """A perfect matching slot -> candidate (augmenting paths; K <= 63 slots), or None."""
+    owner = {}
+
+    def take(a, seen):
+        for j in cands[a]:
+            if j in seen:
+                continue
+            seen.add(j)
+            if j not in owner or take(owner[j], seen):
+                owner[j] = a
+                return True
+        return False
+    for a in range(len(cands)):
+        if not take(a, set()):
+            return None
+    m = [None] * len(cands)
+    for j, a in owner.items():
+        m[a] = j
+    return m
+
+
+def neighbor_slots_b(oenv, e, i, K):
+    """(keys, clipped relative vectors, the oracle's slot order) of drone i of env e: the sort key of
+    neighborhood_indices (quadrotor_multi.py:344-375, |[rel_pos, rel_vel]| clamped at 0.01, the drone itself
+    excluded), the clipped [rel_pos, rel_vel] of extend_obs_space (:328-342), and the neighbours in slot order
+    (index order when K = N - 1, else ascending key; among EXACTLY equal keys the oracle keeps index order --
+    numpy's own argsort order among equal keys is its sort implementation's)."""
+    N = oenv.N
+    ev = oenv.envs[e]
+    P = np.array([ev.obs_pos[j][:] for j in range(N)], dtype=np.float64)
+    V = np.array([ev.obs_vel[j][:] for j in range(N)], dtype=np.float64)
+    rel = np.concatenate([P - P[i], V - V[i]], 1)
+    keys = np.maximum(np.linalg.norm(rel, axis=1), 0.01)
+    keys[i] = np.inf
+    rr = oenv.p.room_hi[0] - oenv.p.room_lo[0]
+    relc = np.concatenate([np.clip(rel[:, :3], -rr, rr), np.clip(rel[:, 3:], -6.0, 6.0)], 1)
+    if K == N - 1:
+        order = [j for j in range(N) if j != i]
+    else:
+        order = [int(j) for j in np.argsort(keys, kind="stable")[:K]]
+    return keys, relc, order
+
+
+def assert_obs_match(gpu_obs, want_obs, oenv, so_dim, K, atol=2e-4, rtol=1e-4, key_tol=1e-4, max_excused=None):
+    """Compare flavor-B observations row by row.  The self part must match.  A neighbour block that differs
+    from the oracle's is accepted only through a one-to-one mapping of its K slots to distinct neighbours of
+    the drone (each GPU slot is the clipped [rel_pos, rel_vel] of exactly one neighbour, no neighbour twice)
+    in which every slot whose neighbour is not the oracle's holds one whose sort key ties, within fp32
+    rounding (key_tol relative + 1e-5), with the key of the oracle's neighbour for that slot: two selected
+    neighbours with tied keys swapped ("slot_order_tie"), or the K-th / (K+1)-th tie picked the other way
+    ("selection_tie").  So slot order, distinctness and the selected set are all checked; a wrong sort order
+    or a duplicated neighbour fails.  Excused rows are counted in EXCUSES_B and may be at most max_excused
+    (default: 1 % of the rows, at least 2)."""
+    got_all = np.asarray(gpu_obs, dtype=np.float64)
+    want_all = np.asarray(want_obs, dtype=np.float64)
+    bad = ~np.isclose(got_all, want_all, atol=atol, rtol=rtol)
     rows = np.flatnonzero(bad.any(1))
     N = oenv.N
+    excused = 0
     for r in rows:
-        np.testing.assert_allclose(gpu_obs[r, :so_dim], want_obs[r, :so_dim], atol=atol, rtol=rtol,
+        np.testing.assert_allclose(got_all[r, :so_dim], want_all[r, :so_dim], atol=atol, rtol=rtol,
                                    err_msg=f"row {r} self obs")
         e, i = divmod(int(r), N)
-        ev = oenv.envs[e]
-        P = np.array([ev.obs_pos[j][:] for j in range(N)])
-        V = np.array([ev.obs_vel[j][:] for j in range(N)])
-        rel = np.concatenate([P - P[i], V - V[i]], 1)
-        keys = np.maximum(np.linalg.norm(rel, axis=1), 0.01)
-        keys[i] = np.inf
-        kth = np.sort(keys)[K - 1]
-        rr = oenv.p.room_hi[0] - oenv.p.room_lo[0]
-        relc = np.concatenate([np.clip(rel[:, :3], -rr, rr), np.clip(rel[:, 3:], -6.0, 6.0)], 1)
-        got = gpu_obs[r, so_dim:].reshape(K, 6)
+        keys, relc, order = neighbor_slots_b(oenv, e, i, K)
+        want = want_all[r, so_dim:so_dim + 6 * K].reshape(K, 6)
+        assert np.allclose(relc[order], want, rtol=1e-9, atol=1e-9), \
+            f"row {r}: the oracle's neighbour block is not the restated selection"
+        got = got_all[r, so_dim:so_dim + 6 * K].reshape(K, 6)
+        cands = []
         for s in range(K):
-            d = np.abs(relc - got[s]).max(1)
-            j = int(np.argmin(d))
-            assert d[j] <= atol + rtol * np.abs(got[s]).max(), f"row {r} slot {s}: no neighbour matches"
-            assert keys[j] <= kth * (1 + key_tol) + key_tol, f"row {r} slot {s}: neighbour {j} is not among the K nearest"
+            tol = atol + rtol * np.abs(got[s])
+            ok = [j for j in range(N) if j != i and np.all(np.abs(relc[j] - got[s]) <= tol)]
+            assert ok, f"row {r} slot {s}: no neighbour of drone {i} matches {got[s]}"
+            cands.append(ok)
+        m = _one_to_one(cands)
+        assert m is not None, f"row {r}: the slots do not hold {K} distinct neighbours ({cands})"
+        kinds = []
+        for s in range(K):
+            j, w = m[s], order[s]
+            if j == w:
+                continue
+            tie = abs(keys[j] - keys[w]) <= key_tol * max(keys[j], keys[w]) + 1e-5
+            assert tie, (f"row {r} slot {s}: neighbour {j} (key {keys[j]:.7g}) where the reference's sort puts "
+                         f"{w} (key {keys[w]:.7g})")
+            kinds.append("slot_order_tie" if j in order else "selection_tie")
+        if kinds:
+            excused += 1
+            for k in kinds:
+                EXCUSES_B[k] += 1
+    EXCUSES_B["rows"] += excused
+    limit = max(2, len(got_all) // 100) if max_excused is None else max_excused
+    assert excused <= limit, f"{excused} rows excused by sort-key ties (limit {limit})"
+    return excused
 
 
 # ---------------------------------------------------------------------------------------------

@@ -81,6 +81,19 @@ def test_validation_errors_are_reported():
     bad = N.QsConfig.from_buffer_copy(c)
     bad.num_agents = 65
     assert L.qs_layout_query(bad, lay) == -2
+    # the state / istate byte offsets (32-bit, 2 GB buffer descriptor) bound the drone count: the largest
+    # accepted shard still addresses its last istate word inside the descriptor, one more drone is refused
+    limit = (0x7fffffff - 256) // (4 * (N.NF + N.NI))
+    big = N.QsConfig.from_buffer_copy(QuadSwarmConfig(num_envs=limit, num_agents=1, neighbor_obs_type="none",
+                                                      neighbor_visible_num=0).to_qs_config())
+    assert L.qs_layout_query(big, lay) == 0
+    assert 4 * (N.NF + N.NI) * lay.num_drones + 255 < 0x7fffffff
+    assert lay.istate - lay.state + 4 * N.NI * lay.num_drones <= 0x7fffffff
+    big.num_envs = limit + 1
+    assert L.qs_layout_query(big, lay) == -1 and b"too many drones" in L.qs_last_error()
+    big.num_envs, big.num_agents = limit // 8 + 1, 8
+    big.neighbor_obs, big.k_neighbors = c.neighbor_obs, c.k_neighbors
+    assert L.qs_layout_query(big, lay) == -1
     bad = N.QsConfig.from_buffer_copy(c)
     bad.abi_version = 99
     assert L.qs_layout_query(bad, lay) == -1

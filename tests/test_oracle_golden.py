@@ -269,3 +269,40 @@ def test_episode_extra_stats_tape_replay(golden):
             assert sorted(a) == sorted(b)
             for key in b:
                 assert a[key] == pytest.approx(b[key], rel=1e-9, abs=1e-12), (eg["step"], i, key)
+
+
+def oracle_coeff(p):
+    return {"pos": p.rew_pos, "effort": p.rew_effort, "crash": p.rew_crash, "orient": p.rew_orient,
+            "spin": p.rew_spin, "quadcol_bin": p.rew_quadcol_bin, "quadcol_bin_obst": p.rew_quadcol_bin_obst}
+
+
+def test_step_infos_tape_replay(golden):
+    """Per-step infos[i]["rewards"] (quadrotor_single.py:79-105, 371; quadrotor_multi.py:642-651): the oracle's
+    reward components, replayed on the reference's draws through a crowded run with collisions, proximity,
+    floor / wall contacts and an auto-reset, turned into dicts by the product's quadswarm_amd.infos, are the
+    reference's own dicts -- the same keys and values."""
+    import json
+    from quadswarm_amd.infos import REWARD_KEYS_B, reward_columns_b
+
+    keys = json.load(open(os.path.join(GOLDEN, "traj_n8info_infokeys.json")))["rewards_keys"]
+    assert sorted(keys) == sorted(REWARD_KEYS_B)
+    g, p, drones, envs = load_traj_env(golden, "n8info")
+    n = p.num_agents
+    od = O.lib().or_obs_dim(ctypes.byref(p))
+    tape = O.TapeRng(g["tape"], g["spawn"])
+    ref = g["info_rewards"]
+    nonzero = {k: 0 for k in keys}
+    for t in range(len(g["actions"])):
+        a = np.ascontiguousarray(g["actions"][t], dtype=np.float64)
+        obs, term, rew = np.zeros((n, od)), np.zeros((n, od)), np.zeros(n)
+        done = np.zeros(n, dtype=np.uint8)
+        O.lib().or_env_step(ctypes.byref(p), drones, envs, 0, O.dptr(a), tape.ref, O.dptr(obs), O.dptr(rew),
+                            done.ctypes.data_as(ctypes.POINTER(ctypes.c_ubyte)), O.dptr(term))
+        comp = np.array([list(drones[i].rinfo) for i in range(n)]).T
+        cols = reward_columns_b(comp, oracle_coeff(p), p.dt)
+        for c, k in enumerate(keys):
+            np.testing.assert_allclose(cols[k], ref[t, :, c], rtol=1e-9, atol=1e-12, err_msg=f"step {t} {k}")
+            nonzero[k] += int((ref[t, :, c] != 0).sum())
+    assert tape.r.tape_pos == len(g["tape"])
+    # the run exercises every term (collisions, proximity, floor contact)
+    assert all(v > 0 for v in nonzero.values()), nonzero

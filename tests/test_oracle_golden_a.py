@@ -292,3 +292,28 @@ def test_episode_extra_stats_a_tape_replay(golden):
     # the run exercised collisions after settle, the final-5 s window and the room lists
     r0 = ref[0]["agents"][0]
     assert r0["num_collisions_after_settle"] > 0 and r0["num_collisions_with_room"] > 0
+
+
+def test_step_infos_goal_dist_a(golden):
+    """Flavor A's per-step infos[i] = {"rewards": {}, "goal_dist": |pos - goal|} of the last executed tick
+    (quadrotor_single_rewards.py:457), through captures and timeouts: the oracle's OR_RI_GOAL_DIST vs the
+    reference's values."""
+    g, p, drones, envs = load_traj_a(golden, "n4info")
+    n = p.num_agents
+    od = O.lib().or_obs_dim_a(ctypes.byref(p))
+    tape = O.TapeRng(g["tape"], g["gtape"])
+    U8 = ctypes.POINTER(ctypes.c_ubyte)
+    dones = 0
+    for t in range(len(g["actions"])):
+        envs[0].capture_radius = float(g["capture"][t])
+        a = np.ascontiguousarray(g["actions"][t], dtype=np.float64)
+        obs, term, rew = np.zeros((n, od)), np.zeros((n, od)), np.zeros(n)
+        done = np.zeros(n, dtype=np.uint8)
+        ri = np.zeros(1, dtype=np.uint8)
+        O.lib().or_env_step_a(ctypes.byref(p), drones, envs, 0, O.dptr(a), tape.ref, O.dptr(obs), O.dptr(rew),
+                              done.ctypes.data_as(U8), O.dptr(term), ri.ctypes.data_as(U8))
+        gd = np.array([drones[i].rinfo[O.RI_GOAL_DIST] for i in range(n)])
+        close(gd, g["info_goal_dist"][t], 1e-9, 1e-12, f"goal_dist step {t}")
+        dones += int(done[0])
+    assert tape.r.tape_pos == len(g["tape"])
+    assert dones >= 2   # goal_dist of a finished step is the pre-reset one

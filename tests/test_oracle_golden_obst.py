@@ -6,11 +6,13 @@ np.random tape (incl. np.random.choice) and the Generator tape (spawn jitter, mi
 CPU-only.
 """
 import ctypes
+import os
 
 import numpy as np
 import pytest
 
 import oracle as O
+from conftest import GOLDEN
 
 RTOL_TRAJ, ATOL_TRAJ = 1e-7, 1e-8
 
@@ -200,3 +202,33 @@ def test_domain_random_tables(golden):
         np.testing.assert_array_equal(sizes, t["sizes_%d" % i])
         want = [c if d != 0.0 else -1 for c, d in zip(t["counts_%d" % i], t["densities_%d" % i])]
         assert counts == want
+
+
+def test_step_infos_with_obstacles(golden):
+    """infos[i]["rewards"] with the obstacle terms rew_quadcol_obstacle / rewraw_quadcol_obstacle
+    (quadrotor_multi.py:642-651): oracle components through quadswarm_amd.infos vs the reference's dicts."""
+    import json
+    from quadswarm_amd.infos import REWARD_KEYS_B, REWARD_KEYS_OBST, reward_columns_b
+
+    keys = json.load(open(os.path.join(GOLDEN, "obst_traj_c4info_infokeys.json")))["rewards_keys"]
+    assert sorted(keys) == sorted(REWARD_KEYS_B + REWARD_KEYS_OBST)
+    g, p, drones, envs = load_traj_obst(golden, "c4info")
+    n = p.num_agents
+    od = O.lib().or_obs_dim(ctypes.byref(p))
+    tape = O.TapeRng(g["tape"], g["spawn"])
+    coeff = {"pos": p.rew_pos, "effort": p.rew_effort, "crash": p.rew_crash, "orient": p.rew_orient,
+             "spin": p.rew_spin, "quadcol_bin": p.rew_quadcol_bin, "quadcol_bin_obst": p.rew_quadcol_bin_obst}
+    hits = 0
+    for t in range(len(g["actions"])):
+        a = np.ascontiguousarray(g["actions"][t], dtype=np.float64)
+        obs, term, rew = np.zeros((n, od)), np.zeros((n, od)), np.zeros(n)
+        done = np.zeros(n, dtype=np.uint8)
+        O.lib().or_env_step(ctypes.byref(p), drones, envs, 0, O.dptr(a), tape.ref, O.dptr(obs), O.dptr(rew),
+                            done.ctypes.data_as(ctypes.POINTER(ctypes.c_ubyte)), O.dptr(term))
+        comp = np.array([list(drones[i].rinfo) for i in range(n)]).T
+        cols = reward_columns_b(comp, coeff, p.dt, use_obstacles=True)
+        for c, k in enumerate(keys):
+            close(cols[k], g["info_rewards"][t, :, c], 1e-9, 1e-12, f"step {t} {k}")
+        hits += int((g["info_rewards"][t, :, keys.index("rewraw_quadcol_obstacle")] != 0).sum())
+    assert tape.r.tape_pos == len(g["tape"])
+    assert hits >= 1

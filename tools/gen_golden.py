@@ -361,7 +361,7 @@ def snapshot(env):
         env_vel=env.vel.copy())
 
 
-def gen_traj(name, n, k, steps, ep_time, seed, setup=None, hover=False, stats=False, **kw):
+def gen_traj(name, n, k, steps, ep_time, seed, setup=None, hover=False, stats=False, infos=False, **kw):
     np.random.seed(seed)
     env = make_env_B(n, k, ep_time=ep_time, seed=seed, **kw)
     env.reset()
@@ -375,10 +375,14 @@ def gen_traj(name, n, k, steps, ep_time, seed, setup=None, hover=False, stats=Fa
     elif n > 1:  # climbing thrust so drones stay airborne and interact
         actions = np.clip(actions * 0.6 + 0.3, -1, 1)
     obs, rew, done = [], [], []
-    events = []
+    events, rinfo, rkeys = [], [], None
     begin()
     for t in range(steps):
         o, r, dn, info = env.step(actions[t])
+        if infos:   # every agent's infos[i]["rewards"] (quadrotor_single.py:79-105, quadrotor_multi.py:642-651)
+            rkeys = rkeys or sorted(info[0]["rewards"])
+            assert all(sorted(info[i]["rewards"]) == rkeys for i in range(n))
+            rinfo.append([[float(info[i]["rewards"][key]) for key in rkeys] for i in range(n)])
         obs.append(np.array(o, dtype=np.float64))
         rew.append(np.array(r, dtype=np.float64))
         done.append(np.array(dn, dtype=np.float64))
@@ -390,8 +394,14 @@ def gen_traj(name, n, k, steps, ep_time, seed, setup=None, hover=False, stats=Fa
         import json
         with open(os.path.join(OUT, f"traj_{name}_stats.json"), "w") as f:
             json.dump({"name": name, "events": events}, f, indent=0, sort_keys=True)
+    extra = {}
+    if infos:
+        import json
+        with open(os.path.join(OUT, f"traj_{name}_infokeys.json"), "w") as f:
+            json.dump({"name": name, "rewards_keys": rkeys, "rew_coeff": REW}, f, indent=0, sort_keys=True)
+        extra["info_rewards"] = np.array(rinfo, dtype=np.float64)
     final = snapshot(env)
-    np.savez_compressed(os.path.join(OUT, f"traj_{name}.npz"), actions=actions, obs=np.stack(obs),
+    np.savez_compressed(os.path.join(OUT, f"traj_{name}.npz"), actions=actions, obs=np.stack(obs), **extra,
                         rew=np.stack(rew), done=np.stack(done), tape=tv, spawn=sp, n=n, k=k,
                         ep_len=env.envs[0].ep_len, downwash=int(kw.get("downwash", False)),
                         sense=int(kw.get("sense", "default") == "default"),
@@ -472,7 +482,9 @@ def main_extra(which):
       wall   the xyz_vxyz_R_omega_wall self obs (get_state.py:270-292): a noisy 8-drone run with wall / ceiling
              contacts and a noise-free 4-drone hover the GPU replays
       stats  episode_extra_stats of every finished episode (quadrotor_multi.py:739-831) over 2-s episodes
-      n64    a 64-drone crowded trajectory and 64-drone neighbour selections (k = 6 and all 63 visible)"""
+      n64    a 64-drone crowded trajectory and 64-drone neighbour selections (k = 6 and all 63 visible)
+      info   every agent's per-step infos["rewards"] dict (quadrotor_single.py:79-105, quadrotor_multi.py:642-651)
+             over a crowded 8-drone run with an in-env auto-reset"""
     os.makedirs(OUT, exist_ok=True)
     if "wall" in which:
         gen_traj("n8wall", 8, 6, 120, ep_time=0.5, seed=17, setup=setup_crowd, obs_repr="xyz_vxyz_R_omega_wall")
@@ -480,6 +492,8 @@ def main_extra(which):
                  obs_repr="xyz_vxyz_R_omega_wall")
     if "stats" in which:
         gen_traj("n8stats", 8, 6, 420, ep_time=2.0, seed=19, setup=setup_crowd, stats=True)
+    if "info" in which:
+        gen_traj("n8info", 8, 6, 60, ep_time=0.3, seed=21, setup=setup_crowd, infos=True)
     if "n64" in which:   # 64-drone swarms: the first size past one drone per lane of a wave with Q > 1
         gen_traj("n64k6", 64, 6, 25, ep_time=0.2, seed=20, setup=setup_crowd)
         gen_neighbors_sizes("neighbors64.npz", [(64, 6), (64, 63)], seed=6, count=10)

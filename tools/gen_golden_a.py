@@ -261,7 +261,7 @@ def snapshot(env):
         capture=np.array(float(env.capture_radius)))
 
 
-def gen_traj(name, n, steps, seed, capture_schedule=None, act_scale=1.0, setup=None, stats=False, **kw):
+def gen_traj(name, n, steps, seed, capture_schedule=None, act_scale=1.0, setup=None, stats=False, infos=False, **kw):
     np.random.seed(seed)
     env = make_env_A(n, seed=seed, **kw)
     begin()
@@ -275,11 +275,14 @@ def gen_traj(name, n, steps, seed, capture_schedule=None, act_scale=1.0, setup=N
     caps = np.array([capture_schedule(t) for t in range(steps)]) if capture_schedule else \
         np.full(steps, env.capture_radius)
     obs, rew, done, term, rinfo = [], [], [], [], []
-    events = []
+    events, gdist = [], []
     begin()
     for t in range(steps):
         env.set_capture_radius(float(caps[t]))
         o, r, dn, info = env.step(actions[t])
+        if infos:   # infos[i] = {"rewards": {}, "goal_dist": ...} of the last tick (quadrotor_single_rewards.py:457)
+            assert all(info[i]["rewards"] == {} for i in range(n))
+            gdist.append([float(info[i]["goal_dist"]) for i in range(n)])
         if stats and any(dn):   # infos[i]["episode_extra_stats"] (quadrotor_multi_rewards.py:886-969)
             events.append({"step": t, "agents": [{k_: float(v) for k_, v in info[i]["episode_extra_stats"].items()}
                                                  for i in range(n)]})
@@ -299,13 +302,14 @@ def gen_traj(name, n, steps, seed, capture_schedule=None, act_scale=1.0, setup=N
             json.dump({"name": name, "events": events}, f, indent=0, sort_keys=True)
     final = snapshot(env)
     c = env.cfg
+    extra = {"info_goal_dist": np.array(gdist, dtype=np.float64)} if infos else {}
     np.savez_compressed(
         os.path.join(OUT, f"a_traj_{name}.npz"), actions=actions, capture=caps, obs0=np.array(obs0, dtype=np.float64),
         obs=np.stack(obs), term=np.stack(term), rew=np.stack(rew), done=np.stack(done), reset_info=np.array(rinfo),
         tape0=tv0, gtape0=gt0, tape=tv, gtape=gt, n=n, k=env.num_use_neighbor_obs, ep_len=env.envs[0].ep_len,
         obs_repr=REPRS.index(c.obs_repr), ntype=NTYPES.index(c.neighbor_obs_type), px_noise=c.pixel_noise_cam,
         sense=int(c.sense_noise == "default"), thrust_noise=env.envs[0].dynamics.thrust_noise_ratio,
-        room=np.array(c.room_dims, dtype=np.float64),
+        room=np.array(c.room_dims, dtype=np.float64), **extra,
         **{"init_" + a: b for a, b in init.items()}, **{"final_" + a: b for a, b in final.items()})
 
 
@@ -362,11 +366,15 @@ def setup_stats_a(env):
 def main_extra(which):
     """Fixtures added later, generated on their own (the ones above stay byte-identical):
       dw     use_downwash (quadrotor_multi_rewards.py:810-815) with stacked drone pairs, 8 drones
-      stats  episode_extra_stats of the episodes that end (quadrotor_multi_rewards.py:886-969)"""
+      stats  episode_extra_stats of the episodes that end (quadrotor_multi_rewards.py:886-969)
+      info   every agent's per-step infos["goal_dist"] (quadrotor_single_rewards.py:457), captures and timeouts"""
     os.makedirs(OUT, exist_ok=True)
     if "dw" in which:
         gen_traj("n8dw", 8, 40, seed=36, ntype="dist_angle", repr_="cdist_cdistdot_dist_distdot_angle_angledot",
                  capture_schedule=lambda t: 0.05, ep_time=30.0, downwash=True, setup=setup_stacks_a)
+    if "info" in which:
+        gen_traj("n4info", 4, 120, seed=38, capture_schedule=lambda t: 3.0 if t >= 100 else 0.3, ep_time=0.8,
+                 infos=True)
     if "stats" in which:
         gen_traj("n8stats", 8, 40, seed=37, ntype="dist_angle", repr_="cdist_cdistdot_dist_distdot_angle_angledot",
                  capture_schedule=lambda t: 0.01, ep_time=3.0, setup=setup_stats_a, stats=True)

@@ -185,7 +185,7 @@ def setup_obst(env, rng):
         ds[5].pos = ds[4].pos + np.array([0.05, 0.03, 0.0])
 
 
-def gen_traj(name, n, k, steps, seed, ep_time, setup=None, hover=False, reset_kw=None, **kw):
+def gen_traj(name, n, k, steps, seed, ep_time, setup=None, hover=False, reset_kw=None, infos=False, **kw):
     np.random.seed(seed)
     env = make_env_obst(n, k, seed=seed, ep_time=ep_time, **kw)
     G.begin()
@@ -199,15 +199,25 @@ def gen_traj(name, n, k, steps, seed, ep_time, setup=None, hover=False, reset_kw
     if hover:   # ~hover thrust with small perturbations: no contacts, no random impulses
         actions = 0.0526 + 0.1 * act_rng.uniform(-1.0, 1.0, (steps, n, 4))
     obs, rew, done = [], [], []
+    rinfo, rkeys = [], None
     G.begin()
     for t in range(steps):
-        o, r, dn, _ = env.step(actions[t])
+        o, r, dn, info = env.step(actions[t])
+        if infos:   # infos[i]["rewards"] incl. the obstacle terms (quadrotor_multi.py:642-651)
+            rkeys = rkeys or sorted(info[0]["rewards"])
+            rinfo.append([[float(info[i]["rewards"][key]) for key in rkeys] for i in range(n)])
         obs.append(np.array(o, dtype=np.float64))
         rew.append(np.array(r, dtype=np.float64))
         done.append(np.array(dn, dtype=np.float64))
     tv, sp = G.end()
+    extra = {}
+    if infos:
+        import json
+        with open(os.path.join(OUT, f"obst_traj_{name}_infokeys.json"), "w") as f:
+            json.dump({"name": name, "rewards_keys": rkeys}, f, indent=0, sort_keys=True)
+        extra["info_rewards"] = np.array(rinfo, dtype=np.float64)
     final = snapshot(env)
-    np.savez_compressed(os.path.join(OUT, f"obst_traj_{name}.npz"), actions=actions, obs=np.stack(obs),
+    np.savez_compressed(os.path.join(OUT, f"obst_traj_{name}.npz"), actions=actions, obs=np.stack(obs), **extra,
                         rew=np.stack(rew), done=np.stack(done), tape=tv, spawn=sp, tape0=tv0, spawn0=sp0,
                         obs0=np.array(obs0, dtype=np.float64), n=n, k=k, ep_len=env.envs[0].ep_len,
                         downwash=int(kw.get("downwash", True)), sense=int(kw.get("sense", "default") == "default"),
@@ -252,6 +262,9 @@ def main():
     os.makedirs(OUT, exist_ok=True)
     if len(sys.argv) > 1 and sys.argv[1] == "dr":
         gen_dr()
+        return
+    if len(sys.argv) > 1 and sys.argv[1] == "info":   # per-step infos["rewards"] with the obstacle terms
+        gen_traj("c4info", 8, 2, 40, seed=54, ep_time=0.3, setup=setup_obst, infos=True)
         return
     gen_sdf()
     gen_maps()

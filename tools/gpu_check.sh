@@ -119,6 +119,20 @@ for s in "$@"; do
       step profc4_sq 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INSTS_LDS -d gpurun_out/profc4_sq -o s --output-format csv -- python bench.py --config c4 --steps 100 --warmup 10 --no-cpu-baseline --graph 0 --e2e-iters 0
       rm -f gpurun_out/profc4_*/*kernel_trace.csv
       ;;
+    profcfg)   # CONFIG=<name>: kernel trace + FETCH / WRITE / SQ passes of one bench config
+      export TMPDIR=/tmp
+      C=${CONFIG:-c3}
+      step prof_${C}_kt 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${C}_kt -o kt --output-format csv -- python bench.py --config $C --steps 1000 --no-cpu-baseline --e2e-iters 0
+      step prof_${C}_fetch 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof_${C}_fetch -o f --output-format csv -- python bench.py --config $C --steps 100 --warmup 10 --no-cpu-baseline --graph 0 --e2e-iters 0
+      step prof_${C}_write 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof_${C}_write -o w --output-format csv -- python bench.py --config $C --steps 100 --warmup 10 --no-cpu-baseline --graph 0 --e2e-iters 0
+      step prof_${C}_sq 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INSTS_LDS -d gpurun_out/prof_${C}_sq -o s --output-format csv -- python bench.py --config $C --steps 100 --warmup 10 --no-cpu-baseline --graph 0 --e2e-iters 0
+      rm -f gpurun_out/prof_${C}_*/*kernel_trace.csv gpurun_out/prof_${C}_*/*/*kernel_trace.csv
+      ;;
+    sel2)      # QS_NBR_SELECT2 on 32-drone envs: bitwise digest A/B + timing A/B
+      step sel2_dig0 200 python tools/bitwise_ab.py c5 60
+      step sel2_dig1 200 env QS_JIT_OPTS=-DQS_NBR_SELECT2=1 python tools/bitwise_ab.py c5 60
+      CONFIG=c5 STEPS=2000 step sel2_ab 600 bash tools/ab_jit.sh base: sel2:-DQS_NBR_SELECT2=1 base2: sel2b:-DQS_NBR_SELECT2=1
+      ;;
     stamps) step stamps 300 python tools/phase_stamps.py ;;
     calib)
       export TMPDIR=/tmp
