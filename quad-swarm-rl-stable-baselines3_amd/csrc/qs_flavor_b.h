@@ -767,14 +767,38 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
         cnt[t] = (kp.stats && envok && k < NCNT) ? *cnt_at(k) : 0;
         cdirty[t] = false;
     }
+    int omi = 0, osi = 0;   // the env's domain-randomisation choice (QS_E_OBST_M / _SZ)
+    if (OBST && kp.dr) { omi = b.env[QS_E_OBST_M * kp.E + eidx]; osi = b.env[QS_E_OBST_SZ * kp.E + eidx]; }
     Drone d;   // every sub-lane holds the whole drone
     DroneWords<Q, LOAD_WORDS> dw;
     load_words_q(kp, b, g, q, dw, kp.stats ? LOAD_WORDS : DRONE_WORDS);
     __builtin_amdgcn_sched_barrier(0);
+    const Rng rng = env_rng(seed, tick0, episode);
+    // The step's regular draws: Philox block k of {OU 0, sensor 0, sensor 1, sensor 2} on sub-lane
+    // k % Q, slot k / Q -- one block per lane for Q = 4 -- then broadcast by DPP.  They need only the env's
+    // Philox counter {tick, episode}, the oldest of the step's loads: drawn while the drone's state words
+    // are still in flight (the unpack below is the first wait on them).
+    float zou[4], zs[12];
+    {
+        float zr[4 / Q][4];
+#pragma unroll
+        for (int t = 0; t < 4 / Q; ++t) {
+            const int k = q + Q * t;
+            if (k == 0 || kp.sense) normals4(rng, gid, k == 0 ? S_OU : S_SENSOR, k == 0 ? 0u : (uint32_t)(k - 1), zr[t]);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            zou[i] = qbc<Q, 0>(zr[0][i]);
+            zs[i] = qbc<Q, 1 % Q>(zr[1 / Q][i]);
+            zs[4 + i] = qbc<Q, 2 % Q>(zr[2 / Q][i]);
+            zs[8 + i] = qbc<Q, 3 % Q>(zr[3 / Q][i]);
+        }
+    }
+
+    __builtin_amdgcn_sched_barrier(0);
     float stw[STAT_WORDS];
     unpack_words_q(dw, d, stw);
     float a[4] = {av.x, av.y, av.z, av.w};
-    const Rng rng = env_rng(seed, tick0, episode);
     const int tick = tick0 + 1;
     const bool done = tick > kpm.ep_len;
     // episode_extra_stats (kp.stats): distance_to_goal's last entries and window sums of this drone (loaded
@@ -795,28 +819,7 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
         for (int k = 0; k < 3; ++k)
             if (in_win[k]) dsum[k] = stw[5 + k];
     }
-    int omi = 0, osi = 0;   // the env's domain-randomisation choice (QS_E_OBST_M / _SZ)
-    if (OBST && kp.dr) { omi = b.env[QS_E_OBST_M * kp.E + eidx]; osi = b.env[QS_E_OBST_SZ * kp.E + eidx]; }
     OGeo og = ogeo(kp, omi, osi);
-
-    // The step's regular draws: Philox block k of {OU 0, sensor 0, sensor 1, sensor 2} on sub-lane
-    // k % Q, slot k / Q -- one block per lane for Q = 4 -- then broadcast by DPP.
-    float zou[4], zs[12];
-    {
-        float zr[4 / Q][4];
-#pragma unroll
-        for (int t = 0; t < 4 / Q; ++t) {
-            const int k = q + Q * t;
-            if (k == 0 || kp.sense) normals4(rng, gid, k == 0 ? S_OU : S_SENSOR, k == 0 ? 0u : (uint32_t)(k - 1), zr[t]);
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            zou[i] = qbc<Q, 0>(zr[0][i]);
-            zs[i] = qbc<Q, 1 % Q>(zr[1 / Q][i]);
-            zs[4 + i] = qbc<Q, 2 % Q>(zr[2 / Q][i]);
-            zs[8 + i] = qbc<Q, 3 % Q>(zr[3 / Q][i]);
-        }
-    }
 
     QS_STAMP(1);
     // ---- per-drone control + physics (QuadrotorSingle._step), replicated on the sub-lanes ----

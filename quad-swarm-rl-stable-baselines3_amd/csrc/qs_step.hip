@@ -1055,8 +1055,25 @@ static int jit_compile(const qs_config* c, const qs::KP& kp, int npad, int qb, i
         "#define QS_JIT 1\n#define QS_QB " + std::to_string(qb) + "\n#define QS_QA " + std::to_string(qa) +
         "\n#define QS_KP_WORDS " + kp_words(kp) + "\n";
     src += c->flavor == QS_FLAVOR_A ? "#include \"qs_flavor_a.h\"\n" : "#include \"qs_flavor_b.h\"\n";
+    // the kernel sources embedded at build time, or (QS_JIT_SRC_DIR, kernel-variant A/B experiments) the same
+    // header names read from that directory
+    std::vector<std::string> dir_src;
+    std::vector<const char*> hsrc(kJitHeaderSources, kJitHeaderSources + kJitNumHeaders);
+    if (const char* dir = getenv("QS_JIT_SRC_DIR")) {
+        for (int i = 0; i < kJitNumHeaders; ++i) {
+            std::string path = std::string(dir) + "/" + kJitHeaderNames[i];
+            FILE* f = fopen(path.c_str(), "rb");
+            if (!f) return fail(QS_E_INVALID, "QS_JIT_SRC_DIR: cannot read " + path);
+            std::string txt;
+            char chunk[4096];
+            for (size_t n; (n = fread(chunk, 1, sizeof chunk, f)) > 0;) txt.append(chunk, n);
+            fclose(f);
+            dir_src.push_back(txt);
+        }
+        for (int i = 0; i < kJitNumHeaders; ++i) hsrc[i] = dir_src[i].c_str();
+    }
     hiprtcProgram prog;
-    if (hiprtcCreateProgram(&prog, src.c_str(), "qs_jit.hip", kJitNumHeaders, kJitHeaderSources, kJitHeaderNames) !=
+    if (hiprtcCreateProgram(&prog, src.c_str(), "qs_jit.hip", kJitNumHeaders, hsrc.data(), kJitHeaderNames) !=
         HIPRTC_SUCCESS)
         return fail(QS_E_HIP, "hiprtcCreateProgram failed");
     hiprtcAddNameExpression(prog, step_name.c_str());
@@ -1117,7 +1134,8 @@ extern "C" int qs_specialize(qs_handle* h, int enable) {
     std::string rn;
     const std::string key = std::to_string(h->device) + "|" + kernel_names(&h->cfg, h->kp, h->npad, &rn) + "|" +
                             std::to_string(qb) + "," + std::to_string(qa) + "|" +
-                            (getenv("QS_JIT_OPTS") ? getenv("QS_JIT_OPTS") : "") + "|" + kp_words(h->kp);
+                            (getenv("QS_JIT_OPTS") ? getenv("QS_JIT_OPTS") : "") + "|" +
+                            (getenv("QS_JIT_SRC_DIR") ? getenv("QS_JIT_SRC_DIR") : "") + "|" + kp_words(h->kp);
     std::lock_guard<std::mutex> lock(g_jit_mu);
     auto it = g_jit_cache.find(key);
     if (it == g_jit_cache.end()) {
