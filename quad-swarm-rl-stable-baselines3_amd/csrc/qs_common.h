@@ -145,7 +145,27 @@ __device__ uint64_t qs_dbg_stamps[65536 * 16];
             for (int k_ = 0; k_ < 16; ++k_) qs_dbg_stamps[blockIdx.x * 16 + k_] = stamps_[k_];        \
     } while (0)
 #define QS_STAMP_DECL uint64_t stamps_[16] = {0};
+// accumulating form (phases inside a loop, flavor A's tick loop): slot k += cycles since the previous mark
+#define QS_STAMP_ACC_DECL uint64_t stamp_last_ = 0;
+#define QS_STAMP_MARK()                                                                               \
+    do {                                                                                              \
+        __builtin_amdgcn_sched_barrier(0);                                                            \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(stamp_last_)::"memory");          \
+        __builtin_amdgcn_sched_barrier(0);                                                            \
+    } while (0)
+#define QS_STAMP_ACC(k)                                                                               \
+    do {                                                                                              \
+        uint64_t t_;                                                                                  \
+        __builtin_amdgcn_sched_barrier(0);                                                            \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                   \
+        __builtin_amdgcn_sched_barrier(0);                                                            \
+        stamps_[k] += t_ - stamp_last_;                                                               \
+        stamp_last_ = t_;                                                                             \
+    } while (0)
 #else
+#define QS_STAMP_ACC_DECL
+#define QS_STAMP_MARK() do {} while (0)
+#define QS_STAMP_ACC(k) do {} while (0)
 #define QS_STAMP(k) do {} while (0)
 #define QS_RTSTAMP(k) do {} while (0)
 #define QS_STAMP_FLUSH() do {} while (0)

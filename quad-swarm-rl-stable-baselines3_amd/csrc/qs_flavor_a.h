@@ -513,6 +513,13 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
     extern __shared__ __attribute__((aligned(16))) float lds[];
     QS_BIND_KP(kpp);
     const uint32_t seed = kpm.seed;
+    // phase stamps (QS_STAMPS builds only): slot 0 loads, then summed over the ticks 1 controller, 2 OU draw,
+    // 3 physics, 4 per-tick stats collisions, 5 capture / done, 6 downwash + target / scenario; after the loop
+    // 7 counters + final obs, 8 done path, 9 obs tile + stores; 12 / 13 realtime wave start / end
+    QS_STAMP_DECL
+    QS_STAMP_ACC_DECL
+    QS_RTSTAMP(12);
+    QS_STAMP_MARK();
     using G = StepGeoA<NPAD>;
     constexpr int Q = G::Q, LPE = G::LPE, EPB = G::EPB, SLOTS = G::SLOTS;
     const int lane = threadIdx.x;
@@ -561,6 +568,7 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
         cnt[t] = cnt0[t] = (kp.stats && envok && k < NCNT) ? b.env[(QS_E_ST_COL + k) * kp.E + env] : 0;
     }
 
+    QS_STAMP_ACC(0);
     bool fin = false, success = eflags & QS_EF_SUCCESS;
     float rw = 0.f, gox = d.goal[0], goy = d.goal[1];
     float gdist = 0.f;   // infos[i]["goal_dist"] of the last executed tick (per-step infos, kp.rcomp)
@@ -572,6 +580,7 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
         const Rng rng = env_rng(seed, tick, episode);
         float u[4];
         controller(kp, d, c, a0, d.goal[2], u);
+        QS_STAMP_ACC(1);
         float z[4];   // QuadrotorDynamics.step: one OU draw per tick (:216)
         if constexpr (Q == 1) {
             normals4(rng, gid, S_OU, 0, z);
@@ -589,7 +598,9 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
         }
 #pragma unroll
         for (int k = 0; k < 4; ++k) d.ou[k] = d.ou[k] + (kp.ou_theta * (kp.ou_mu - d.ou[k]) + kp.ou_sigma * z[k]);
-            for (int s = 0; s < kp.sim_steps; ++s) substep(kp, d, u, d.ou, rng, gid, s);
+        QS_STAMP_ACC(2);
+        for (int s = 0; s < kp.sim_steps; ++s) substep(kp, d, u, d.ou, rng, gid, s);
+        QS_STAMP_ACC(3);
         ++tick;
         if (kp.rcomp) {   // np.linalg.norm(self.dynamics.pos - self.goal) of this _step (quadrotor_single_rewards.py:457)
             const float gx = d.pos[0] - d.goal[0], gy = d.pos[1] - d.goal[1], gz = d.pos[2] - d.goal[2];
@@ -644,6 +655,7 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
                 }
             }
         }
+        QS_STAMP_ACC(4);
         gox = d.goal[0];
         goy = d.goal[1];
         // capture reward (:711-735) against env 0's goal; dones (:882-988)
@@ -658,6 +670,7 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
         dn = cap ? capi : (tick > kpm.ep_len);
         fin = seg_any<LPE>(active && dn, base);
         success = success || cap;
+        QS_STAMP_ACC(5);
         // perform_downwash once per tick with the control dt (:810-815); the reference then rebuilds the
         // tick's obs from the post-downwash state, which is what the final obs below read
         bool dwa = false;
@@ -686,6 +699,7 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
             gox = d.goal[0];
             goy = d.goal[1];
         }
+        QS_STAMP_ACC(6);
     }
 
     if (SCEN && active && di == 0 && q == 0 && !fin) scen_store(kp, b, env, sc);   // (a reset stores its own)
@@ -706,6 +720,7 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
         neighbor_obs_a<NPAD, Q>(kp, xch, sbase, di, d.pos, c.angle, c.angle, d.vel, rng_last, gid, false, active, row, q);
 
     const bool state_bad = lead && drone_nonfinite(d), rew_bad = lead && !(rw * 0.f == 0.f);
+    QS_STAMP_ACC(7);
     const uint64_t fball = __ballot(active && fin);
     if (fball) {  // some env finished: terminal obs + the worker's reset (subproc_vec_env_custom.py:42-46)
         lds_sync();
@@ -765,6 +780,7 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
         }
     }
     lds_sync();
+    QS_STAMP_ACC(8);
     const int obs_bad = tile_store(lds, b.obs + (size_t)env0 * kp.N * kp.obs_dim, rows * kp.obs_dim, lane);
     guard_count(b, obs_bad, rew_bad, state_bad);
 
@@ -786,6 +802,9 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
             b.rinfo[env] = fin ? (success ? 2 : 1) : 0;
         }
     }
+    QS_STAMP_ACC(9);
+    QS_RTSTAMP(13);
+    QS_STAMP_FLUSH();
 }
 
 // explicit reset of masked envs (quadrotor_multi_rewards.QuadrotorEnvMulti.reset)

@@ -52,6 +52,7 @@ struct qs_handle {
     int npad;
     hipFunction_t jit_step = nullptr;    // qs_specialize: kernels compiled for this handle's parameters
     hipFunction_t jit_reset = nullptr;
+    hipModule_t jit_mod = nullptr;       // their module
     int qb = QS_QB, qa = QS_QA;          // sub-lanes per drone of the step kernels in use (flavor B / A)
     // experience replay (qs_replay_enable): one device allocation holding every RBufs array
     void* rws = nullptr;
@@ -1122,6 +1123,7 @@ extern "C" int qs_specialize(qs_handle* h, int enable) {
     if (!h) return fail(QS_E_INVALID, "NULL handle");
     if (!enable) {
         h->jit_step = h->jit_reset = nullptr;
+        h->jit_mod = nullptr;
         h->qb = QS_QB;
         h->qa = QS_QA;
         return QS_OK;
@@ -1150,6 +1152,7 @@ extern "C" int qs_specialize(qs_handle* h, int enable) {
     }
     h->jit_step = it->second.step;
     h->jit_reset = it->second.reset;
+    h->jit_mod = it->second.mod;
     h->qb = qb;
     h->qa = qa;
     return QS_OK;
@@ -1176,3 +1179,19 @@ extern "C" long long qs_specialize_compile(const qs_config* c) {
 
 // 1 when the handle launches specialised kernels
 extern "C" int qs_is_specialized(const qs_handle* h) { return h && h->jit_step ? 1 : 0; }
+
+#ifdef QS_STAMPS
+// diagnostics build only: the phase stamps of the kernels this handle launches (tools/phase_stamps.py); a
+// specialised handle's kernels write the copy of qs_dbg_stamps in their own hipRTC module
+extern "C" int qs_debug_stamps_h(qs_handle* h, uint64_t* host, size_t n) {
+    if (!h || !host) return fail(QS_E_INVALID, "NULL argument");
+    QS_HIP(use_device(h));
+    QS_HIP(hipDeviceSynchronize());
+    if (!h->jit_mod) return qs_debug_stamps(host, n);
+    hipDeviceptr_t p = nullptr;
+    size_t bytes = 0;
+    QS_HIP(hipModuleGetGlobal(&p, &bytes, h->jit_mod, "_ZN2qs13qs_dbg_stampsE"));
+    QS_HIP(hipMemcpyDtoH(host, p, n * sizeof(uint64_t) < bytes ? n * sizeof(uint64_t) : bytes));
+    return QS_OK;
+}
+#endif

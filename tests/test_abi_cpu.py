@@ -266,8 +266,11 @@ def test_create_without_device_fails_loudly():
 
 @pytest.mark.parametrize("make", [lambda: QuadSwarmConfig(num_envs=64, num_agents=8, neighbor_visible_num=6),
                                   lambda: QuadSwarmConfig.c4(num_envs=64),
-                                  lambda: QuadSwarmConfig.sb_train(num_envs=64, num_agents=4)],
-                         ids=["c3", "c4", "a4"])
+                                  lambda: QuadSwarmConfig.sb_train(num_envs=64, num_agents=4),
+                                  lambda: QuadSwarmConfig(num_envs=64, num_agents=64, neighbor_visible_num=6),
+                                  lambda: QuadSwarmConfig(num_envs=64, num_agents=1, neighbor_obs_type="none",
+                                                          episode_stats=False)],
+                         ids=["c3", "c4", "a4", "n64", "c2-nostats"])
 def test_specialised_kernels_compile_on_the_host(make):
     """qs_specialize's hipRTC path (kernel source embedded in the .so, parameter block baked in)
     compiles for gfx950 without a device."""

@@ -12,7 +12,9 @@ for spec in "$@"; do
   tag=${spec%%:*}; dir=${spec#*:}
   if [ -n "$dir" ]; then export QS_JIT_SRC_DIR=$(realpath $dir); else unset QS_JIT_SRC_DIR; fi
   timeout -k 10 200 python tools/bitwise_ab.py $CONFIG 60 > gpurun_out/ab_src/${CONFIG}_${tag}_digest.txt 2>&1
-  rc=$?; echo "$CONFIG $tag digest rc=$rc $(tail -1 gpurun_out/ab_src/${CONFIG}_${tag}_digest.txt | awk '{print $NF}')"
+  rc=$?
+  if grep -q "qs_specialize failed" gpurun_out/ab_src/${CONFIG}_${tag}_digest.txt; then echo "$tag: not specialised"; exit 1; fi
+  echo "$CONFIG $tag digest rc=$rc $(tail -1 gpurun_out/ab_src/${CONFIG}_${tag}_digest.txt | awk '{print $NF}')"
   if [ $rc -ne 0 ]; then exit $rc; fi
 done
 for r in $(seq 1 $ROUNDS); do
