@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define QS_ABI_VERSION 8
+#define QS_ABI_VERSION 9
 #define QS_MAX_AGENTS 64            /* drones per env: one env lives inside one 64-lane wavefront */
 #define QS_MAX_DR_CHOICES 8         /* entries per obstacle domain-randomisation list */
 
@@ -427,6 +427,43 @@ int qs_replay_buffers_get(qs_handle* h, qs_replay_buffers* out);
 int qs_gae(const float* d_rewards, const float* d_values, const uint8_t* d_episode_starts,
            const float* d_last_values, const uint8_t* d_last_dones, float* d_advantages, float* d_returns,
            int32_t n_steps, int32_t n_cols, float gamma, float gae_lambda, void* stream);
+
+/* Fused no-grad forward of the rollout policy's attention neighbour encoder (replaces the torch evaluation of
+ * QuadNeighborhoodEncoderAttention, swarm_rl/models/quad_multi_model.py:44-101, inside
+ * ActorCriticPolicyCustomSeparateWeights.forward during SB3 collect_rollouts).  One tower = one encoder's
+ * weights and buffers; up to QS_ATTN_MAX_TOWERS towers (actor, critic) per launch.  H (hidden size) is 128
+ * or 256; K (neighbours per agent) 1..64; nd (features per neighbour) 1..16.  Every pointer is device
+ * memory, fp32, row-major.  The [H, Kd] weights are passed PACKED for the matrix cores: packed[ct][g][l][u]
+ * = W[32 ct + (l & 31)][(l >> 5) Kd/2 + 4 g + u] for ct < H/32, g < Kd/8, l < 64, u < 4
+ * (quadswarm_amd.policy_fused.pack_mfma_weight).  Stage 1 (qs_attn_embed) writes e2 and e_mean; the caller
+ * forms P = e_mean A_m^T + b_a1; stage 2 (qs_attn_pool) writes out.  Asynchronous on `stream`. */
+#define QS_ATTN_MAX_TOWERS 2
+typedef struct qs_attn_tower {
+    /* stage 1: embedding_mlp */
+    const float* w_e1p;    /* packed [H, 32]: [embedding_mlp[0].weight[:, so:] (nd) | [:, :so] (so) | 0] */
+    const float* b_e1;     /* [H] */
+    const float* w_e2p;    /* packed embedding_mlp[2].weight */
+    const float* b_e2;     /* [H] */
+    float* e2;             /* [B*K, H] out: embeddings e_i (row j = agent j / K, neighbour j % K) */
+    float* e_mean;         /* [B, H] out: mean over the agent's K rows */
+    /* stage 2: neighbor_value_mlp + attention_mlp + softmax pooling */
+    const float* P;        /* [B, H] e_mean @ W_a1[:, H:]^T + b_a1 */
+    const float* w_v1p;    /* packed neighbor_value_mlp[0].weight */
+    const float* b_v1;
+    const float* w_v2p;    /* packed neighbor_value_mlp[2].weight */
+    const float* b_v2;
+    const float* w_a1ep;   /* packed attention_mlp[0].weight[:, :H] */
+    const float* w_a2p;    /* packed attention_mlp[2].weight */
+    const float* b_a2;
+    const float* w_a3;     /* [H] attention_mlp[4].weight */
+    float b_a3;            /* attention_mlp[4].bias */
+    float* out;            /* [B, H] out: the attention-weighted value embedding per agent */
+} qs_attn_tower;
+/* obs: [B, obs_stride] rows; agent b's self features are obs[b * obs_stride + 0 .. self_dim), its neighbour
+ * block obs[b * obs_stride + nbr_off ...], K x nd; nd + self_dim <= 32. */
+int qs_attn_embed(const float* d_obs, int32_t obs_stride, int32_t self_dim, int32_t nbr_off, int32_t B, int32_t K,
+                  int32_t nd, int32_t H, const qs_attn_tower* towers, int32_t n_towers, void* stream);
+int qs_attn_pool(int32_t B, int32_t K, int32_t H, const qs_attn_tower* towers, int32_t n_towers, void* stream);
 
 #ifdef __cplusplus
 }

@@ -123,7 +123,8 @@ struct Bufs {
 // each block records s_memtime at phase boundaries; tools/phase_stamps.py reads them back.  A stamp waits
 // for nothing but its own counter read: a phase's time includes the memory waits its own code has.
 #ifdef QS_STAMPS
-__device__ uint64_t qs_dbg_stamps[65536 * 16];
+constexpr int QS_NSTAMP = 32;   // slots per block
+__device__ uint64_t qs_dbg_stamps[65536 * QS_NSTAMP];
 #define QS_STAMP(k)                                                                                   \
     do {                                                                                              \
         uint64_t t_;                                                                                  \
@@ -139,12 +140,20 @@ __device__ uint64_t qs_dbg_stamps[65536 * 16];
         asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                \
         stamps_[k] = t_;                                                                              \
     } while (0)
+// slots 14 / 15: the wave's HW_ID (wave slot, SIMD, CU, SH, SE) and XCC_ID registers (where it ran)
 #define QS_STAMP_FLUSH()                                                                              \
     do {                                                                                              \
+        uint32_t hw_, xcc_;                                                                           \
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_));                            \
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_));                          \
+        stamps_[14] = hw_;                                                                            \
+        stamps_[15] = xcc_;                                                                           \
         if (threadIdx.x == 0 && blockIdx.x < 65536)                                                   \
-            for (int k_ = 0; k_ < 16; ++k_) qs_dbg_stamps[blockIdx.x * 16 + k_] = stamps_[k_];        \
+            for (int k_ = 0; k_ < QS_NSTAMP; ++k_) qs_dbg_stamps[blockIdx.x * QS_NSTAMP + k_] = stamps_[k_]; \
     } while (0)
-#define QS_STAMP_DECL uint64_t stamps_[16] = {0};
+#define QS_STAMP_DECL uint64_t stamps_[QS_NSTAMP] = {0};
+// a wave-uniform value in slot k (16..31): what the wave's drones were doing
+#define QS_STAMP_NOTE(k, v) do { stamps_[k] = (uint64_t)(v); } while (0)
 // accumulating form (phases inside a loop, flavor A's tick loop): slot k += cycles since the previous mark
 #define QS_STAMP_ACC_DECL uint64_t stamp_last_ = 0;
 #define QS_STAMP_MARK()                                                                               \
@@ -164,6 +173,7 @@ __device__ uint64_t qs_dbg_stamps[65536 * 16];
     } while (0)
 #else
 #define QS_STAMP_ACC_DECL
+#define QS_STAMP_NOTE(k, v) do {} while (0)
 #define QS_STAMP_MARK() do {} while (0)
 #define QS_STAMP_ACC(k) do {} while (0)
 #define QS_STAMP(k) do {} while (0)
@@ -352,8 +362,9 @@ __device__ __forceinline__ void polar3(float* x) {
     }
 }
 
-// The substep in three pieces (motors -> torques, Rodrigues attitude update, the rest), so that the
-// flavor-B step kernel can deal the first two over a drone's sub-lanes (substep_q in qs_flavor_b.h).
+// The substep in three pieces (motors -> torques, Rodrigues attitude update, the rest).  Every sub-lane of a
+// drone runs all of it: dealing the motors and the Rodrigues rows over the sub-lanes measured slower (the DPP
+// exchanges cost more issue slots than the replicated arithmetic).
 struct Torque {
     float t0, t1, t2, sum;   // body torque, total thrust
 };

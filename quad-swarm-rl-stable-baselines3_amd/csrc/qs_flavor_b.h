@@ -1288,6 +1288,9 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
         if (env < kp.E) replay_env<true>(kp, kpm, b, r, rp, seed, env, lane % LPE, LPE);
     }
     QS_STAMP(11);
+    // slots 16 / 17: drones of the wave on the floor / in a drone collision this step
+    QS_STAMP_NOTE(16, __builtin_popcountll(__ballot(active && q == 0 && (d.flags & QS_FL_ON_FLOOR))));
+    QS_STAMP_NOTE(17, __builtin_popcountll(__ballot(active && q == 0 && cur != 0)));
     QS_RTSTAMP(13);
     QS_STAMP_FLUSH();
 }

@@ -1,0 +1,360 @@
+// qs_policy.h -- fused no-grad forward of the rollout policy's attention neighbour encoder.
+//
+// QuadNeighborhoodEncoderAttention (swarm_rl/models/quad_multi_model.py:44-101) as the rollout evaluates it
+// once per tower (actor, critic) and step: per neighbour row j of the [B*K, nd] neighbour block
+//   e1 = tanh([nbr_j | self_{j % B}] [W_n | W_s]^T + b_e1)   embedding_mlp[0] on the concatenated row
+//   e2 = tanh(e1 W_e2^T + b_e2)                               embedding_mlp[2]
+//   a1 = tanh(e2 A_e^T + P[j % B]),  P = mean_K(e2) A_m^T + b_a1  (attention_mlp[0], split: per agent)
+//   a2 = tanh(a1 A2^T + b_a2),  score = a2 . a3 + b_a3
+//   h  = tanh(tanh(e2 V1^T + c1) V2^T + c2)                   neighbor_value_mlp
+//   out[b] = sum_k softmax_k(score[bK + k]) h[bK + k]
+// (the row pairing j % B is the reference's Tensor.repeat tiling, ppo.py NeighborAttention).
+//
+// Two kernels, because P of agent j % B needs the mean embedding of agents another block computes:
+//   attn_embed_kernel : e1, e2 -> e2 rows and mean_K(e2) per agent to HBM
+//   attn_pool_kernel  : e2 rows -> a1, a2, score, softmax, then h weighted and pooled -> out [B, H]
+// (torch forms P between them: a [B, H] x [H, H] GEMM).
+//
+// A block owns 64 neighbour rows (AB = 64 / K whole agents, MU = AB K rows used) and keeps them in LDS as
+// ONE [64][H + 4] fp32 tile (67 KB at H = 256: two blocks per CU, so one block's epilogues, barriers and
+// loads overlap the other's matrix-core work); each layer's output stays in the accumulators until every
+// wave has read the tile, then overwrites it.  A layer is a 64 x H x Kd fp32 GEMM on the matrix cores,
+// v_mfma_f32_32x32x2f32, wave w owning output columns [w H/4, (w+1) H/4).  The contraction index is
+// permuted so that lane half hf covers k in [hf Kd/2, (hf+1) Kd/2): one ds_read_b128 of a row gives a lane
+// its A operand for 4 MFMA steps, and the weights are pre-packed (quadswarm.h qs_attn_tower, policy_fused.py
+// pack_mfma_weight) so that one global_load_dwordx4 per lane gives its B operand for 4 steps, 1 KB
+// contiguous per wave-instruction.  Activations never leave the CU between layers; bias + tanh are applied
+// to the accumulators as they are written back to LDS.  fp32 throughout (the reference trains in fp32);
+// tanh is 1 - 2 / (exp(2x) + 1) on the hardware exp2 / rcp (absolute error < 3e-7 against tanhf).
+// Roofline: the matrix cores (157 TF fp32 dense): 5 H^2 + 32 H MACs per neighbour row and tower.
+#pragma once
+#ifndef __HIPCC_RTC__
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#endif
+#include "quadswarm.h"
+
+namespace qs {
+namespace pol {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int MROWS = 64;            // neighbour rows per block
+constexpr int RT = MROWS / 32;       // 32-row MFMA tiles
+constexpr int NWAVE = 4;
+constexpr int NTHR = 64 * NWAVE;
+constexpr int MAX_ND = 16;           // neighbour features per row (the reference's largest is 6)
+constexpr int KD0 = 32;              // embedding layer 0's input: nd + so <= 32 (the reference's largest is 30)
+constexpr int LD0 = KD0 + 4;
+
+template <int H>
+struct Geo {
+    static_assert(H == 128 || H == 256, "hidden size 128 or 256");
+    static constexpr int LD = H + 4;             // LDS row stride in floats: ds_read_b128 of 32 rows conflict-free
+    static constexpr int CT = H / (32 * NWAVE);  // 32-column output tiles per wave
+    static constexpr int G = H / 8;              // float4 groups along k: 4 MFMA steps each
+};
+
+struct Towers {
+    qs_attn_tower t[QS_ATTN_MAX_TOWERS];
+};
+
+// tanh x = 1 - 2 / (exp(2x) + 1): +-1 at the extremes (exp2 -> inf / 0), NaN in -> NaN out
+__device__ __forceinline__ float tanh_fast(float x) {
+    const float e = __builtin_amdgcn_exp2f(x * 2.8853900817779268f);   // 2 log2(e)
+    return 1.f - 2.f * __builtin_amdgcn_rcpf(e + 1.f);
+}
+
+__device__ __forceinline__ float f4at(const float4& v, int u) {
+    return u == 0 ? v.x : (u == 1 ? v.y : (u == 2 ? v.z : v.w));
+}
+
+// acc = X W^T for the block's 64 rows (X: LDS [64][LD]); W packed: float4 index ((ct G + g) 64 + lane) holds
+// W[ct 32 + (lane & 31)][(lane >> 5) H/2 + 4g .. + 3].
+struct ZeroInit {
+    __device__ float operator()(int, int) const { return 0.f; }
+};
+// (init(i, n): the accumulators' starting value, e.g. a per-row bias; 0 by default)
+// KD: the contraction size (the layer's input width; the tile X has row stride KD + 4).  ZERO: start the
+// accumulators at 0 (else they keep what the caller put there, e.g. a per-row bias loaded early)
+template <int H, int KD = H, bool ZERO = true>
+__device__ __forceinline__ void mfma_layer(const float* X, const float4* __restrict__ Wp, f32x16 (&acc)[RT][Geo<H>::CT],
+                                           int wave, int lane) {
+    static_assert(KD % 16 == 0, "contraction in float4 groups per lane half");
+    constexpr int CT = Geo<H>::CT, G = KD / 8, LD = KD + 4;
+    if constexpr (ZERO) {
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int c = 0; c < CT; ++c)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[rt][c][r] = 0.f;
+    }
+    const float* xa = X + (lane & 31) * LD + (lane >> 5) * (KD / 2);
+    const float4* wb = Wp + (size_t)(wave * CT) * G * 64 + lane;
+    float4 b0[CT], b1[CT];
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+        b0[c] = wb[(size_t)(c * G + 0) * 64];
+        b1[c] = G > 1 ? wb[(size_t)(c * G + 1) * 64] : b0[c];
+    }
+    float4 an[RT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) an[rt] = *reinterpret_cast<const float4*>(xa + rt * 32 * LD);
+    for (int g = 0; g < G; ++g) {
+        float4 b[CT], a[RT];
+#pragma unroll
+        for (int c = 0; c < CT; ++c) {   // weights: two groups in flight ahead of the MFMAs
+            b[c] = b0[c];
+            b0[c] = b1[c];
+            if (g + 2 < G) b1[c] = wb[(size_t)(c * G + g + 2) * 64];
+        }
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {   // activations: one group ahead
+            a[rt] = an[rt];
+            if (g + 1 < G) an[rt] = *reinterpret_cast<const float4*>(xa + rt * 32 * LD + 4 * (g + 1));
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+                for (int c = 0; c < CT; ++c)
+                    acc[rt][c] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4at(a[rt], u), f4at(b[c], u), acc[rt][c], 0, 0, 0);
+    }
+}
+
+// the accumulator element r of tile (rt, c) on this lane: row and column of the block's output
+__device__ __forceinline__ int acc_row(int rt, int r, int lane) { return rt * 32 + 8 * (r >> 2) + 4 * (lane >> 5) + (r & 3); }
+template <int H>
+__device__ __forceinline__ int acc_col(int wave, int c, int lane) { return (wave * Geo<H>::CT + c) * 32 + (lane & 31); }
+
+// Y[i][n] = tanh(acc + bias(i, n)) into LDS
+template <int H, typename Bias>
+__device__ __forceinline__ void store_tanh(float* Y, const f32x16 (&acc)[RT][Geo<H>::CT], int wave, int lane, Bias bias) {
+    constexpr int CT = Geo<H>::CT, LD = Geo<H>::LD;
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int c = 0; c < CT; ++c) {
+            const int n = acc_col<H>(wave, c, lane);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int i = acc_row(rt, r, lane);
+                Y[i * LD + n] = tanh_fast(acc[rt][c][r] + bias(i, n));
+            }
+        }
+}
+
+template <int H>
+constexpr size_t embed_lds_bytes() { return (size_t)(MROWS * Geo<H>::LD + MROWS * LD0 + 2 * H) * 4; }
+template <int H>
+constexpr size_t pool_lds_bytes() { return (size_t)(MROWS * Geo<H>::LD + 3 * MROWS + 4 * H) * 4; }
+
+// e1 -> e2 for the block's rows (both layers on the matrix cores); e2 rows and the per-agent mean of e2 to HBM
+template <int H>
+__global__ __launch_bounds__(NTHR, 2) void attn_embed_kernel(const float* __restrict__ obs, int stride, int so,
+                                                            int off, int B, int K, int nd, Towers tw) {
+    constexpr int LD = Geo<H>::LD, CT = Geo<H>::CT;
+    extern __shared__ float4 smem4[];
+    float* X = reinterpret_cast<float*>(smem4);
+    float* X0 = X + MROWS * LD;   // layer 0's input rows
+    float* BI = X0 + MROWS * LD0;  // b_e1, b_e2
+    const qs_attn_tower& t = tw.t[blockIdx.y];
+    const int AB = MROWS / K, MU = AB * K;
+    const long R = (long)B * K, row0 = (long)blockIdx.x * MU;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    QS_STAMP_DECL
+    QS_RTSTAMP(12);
+    QS_STAMP(0);
+    for (int n = tid; n < H; n += NTHR) {
+        BI[n] = t.b_e1[n];
+        BI[H + n] = t.b_e2[n];
+    }
+    // layer 0's input rows [nbr_j (nd) | self_{j % B} (so) | 0 ...] (KD0 wide): row j = agent j / K, slot j % K;
+    // its self half comes from agent j % B (the reference's row pairing)
+    for (int e = tid; e < MROWS * KD0; e += NTHR) {   // (row indices < 2^31: qs_attn_embed checks B K H)
+        const int r = e / KD0, c = e - r * KD0;
+        const int j = (int)row0 + r;
+        float v = 0.f;
+        if (r < MU && j < R) {
+            if (c < nd) v = obs[(size_t)(j / K) * stride + off + (j % K) * nd + c];
+            else if (c < nd + so) v = obs[(size_t)(j % B) * stride + (c - nd)];
+        }
+        X0[r * LD0 + c] = v;
+    }
+    __syncthreads();
+    QS_STAMP(1);
+    f32x16 acc[RT][CT];
+    {   // e1 = tanh([nbr | self] [W_n | W_s]^T + b_e1): a KD0-deep layer on the matrix cores
+        mfma_layer<H, KD0>(X0, reinterpret_cast<const float4*>(t.w_e1p), acc, wave, lane);
+        store_tanh<H>(X, acc, wave, lane, [&](int i, int n) { return (i < MU && row0 + i < R) ? BI[n] : 0.f; });
+    }
+    __syncthreads();
+    QS_STAMP(2);
+    mfma_layer<H>(X, reinterpret_cast<const float4*>(t.w_e2p), acc, wave, lane);
+    QS_STAMP(3);
+    __syncthreads();   // every wave has read the tile
+    store_tanh<H>(X, acc, wave, lane, [&](int, int n) { return BI[H + n]; });
+    __syncthreads();
+    QS_STAMP(4);
+    for (int e = tid; e < MROWS * (H / 4); e += NTHR) {
+        const int r = e / (H / 4), c4 = e - r * (H / 4);
+        const long j = row0 + r;
+        if (r < MU && j < R)
+            reinterpret_cast<float4*>(t.e2 + j * H)[c4] = *reinterpret_cast<const float4*>(X + r * LD + 4 * c4);
+    }
+    const float inv = 1.f / (float)K;   // torch's mean: the sum times 1 / K
+    for (int e = tid; e < AB * H; e += NTHR) {
+        const int a = e / H, n = e - a * H;
+        const long agent = row0 / K + a;
+        if (agent < B) {
+            float s = 0.f;
+            for (int k = 0; k < K; ++k) s += X[(a * K + k) * LD + n];
+            t.e_mean[agent * H + n] = s * inv;
+        }
+    }
+    QS_STAMP(5);
+    QS_RTSTAMP(13);
+    QS_STAMP_FLUSH();
+}
+
+// the block's e2 rows into the tile (zero rows past the data)
+template <int H>
+__device__ __forceinline__ void load_rows(float* X, const float* __restrict__ src, long row0, int MU, long R, int tid) {
+    constexpr int LD = Geo<H>::LD, NV = MROWS * (H / 4) / NTHR;   // float4 per thread, all loads in flight
+    float4 v[NV];
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+        const int e = tid + u * NTHR, r = e / (H / 4), c4 = e - r * (H / 4);
+        const long j = row0 + r;
+        v[u] = (r < MU && j < R) ? reinterpret_cast<const float4*>(src + j * H)[c4] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+        const int e = tid + u * NTHR, r = e / (H / 4), c4 = e - r * (H / 4);
+        *reinterpret_cast<float4*>(X + r * LD + 4 * c4) = v[u];
+    }
+}
+
+// e2 rows -> attention path (a1, a2, score, softmax over each agent's K rows), then the value path h, whose
+// accumulators are weighted and summed straight into out = sum_k w_k h_k (no second accumulator set live)
+template <int H>
+__global__ __launch_bounds__(NTHR, 2) void attn_pool_kernel(int B, int K, Towers tw) {
+    constexpr int LD = Geo<H>::LD, CT = Geo<H>::CT;
+    extern __shared__ float4 smem4[];
+    float* X = reinterpret_cast<float*>(smem4);
+    float* SC = X + MROWS * LD;
+    float* WT = SC + MROWS;
+    float* A3 = WT + 2 * MROWS;                      // attention_mlp[4].weight, then b_a2, b_v1, b_v2
+    const qs_attn_tower& t = tw.t[blockIdx.y];
+    const int AB = MROWS / K, MU = AB * K;
+    const long R = (long)B * K, row0 = (long)blockIdx.x * MU;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    QS_STAMP_DECL
+    QS_RTSTAMP(12);
+    QS_STAMP(0);
+    for (int n = tid; n < H; n += NTHR) {
+        A3[n] = t.w_a3[n];
+        A3[H + n] = t.b_a2[n];
+        A3[2 * H + n] = t.b_v1[n];
+        A3[3 * H + n] = t.b_v2[n];
+    }
+    // attention_mlp: a1 = tanh(e2 A_e^T + P[j % B]); the per-agent half (with its bias) is the accumulators'
+    // start, loaded with the block's e2 rows so that both latencies overlap
+    f32x16 acc[RT][CT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int c = 0; c < CT; ++c) {
+            const int n = acc_col<H>(wave, c, lane);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int i = acc_row(rt, r, lane);
+                const int j = (int)row0 + i;
+                acc[rt][c][r] = (i < MU && j < R) ? t.P[(size_t)(j % B) * H + n] : 0.f;
+            }
+        }
+    load_rows<H>(X, t.e2, row0, MU, R, tid);
+    __syncthreads();
+    QS_STAMP(1);
+    mfma_layer<H, H, false>(X, reinterpret_cast<const float4*>(t.w_a1ep), acc, wave, lane);
+    QS_STAMP(2);
+    __syncthreads();
+    store_tanh<H>(X, acc, wave, lane, ZeroInit());
+    __syncthreads();
+    QS_STAMP(3);
+    mfma_layer<H>(X, reinterpret_cast<const float4*>(t.w_a2p), acc, wave, lane);
+    QS_STAMP(4);
+    __syncthreads();
+    store_tanh<H>(X, acc, wave, lane, [&](int, int n) { return A3[H + n]; });
+    __syncthreads();
+    QS_STAMP(5);
+    {   // score = a2 . a3 + b_a3: 4 lanes per row
+        const int r = tid >> 2, qq = tid & 3;   // the row's 4 lanes read interleaved columns: no bank conflict
+        float pp[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+        for (int m = 0; m < H / 4; ++m) {
+            const int n = 4 * m + qq;
+            pp[m & 3] = fmaf(X[r * LD + n], A3[n], pp[m & 3]);
+        }
+        float p = (pp[0] + pp[1]) + (pp[2] + pp[3]);
+        p += __shfl_xor(p, 1);
+        p += __shfl_xor(p, 2);
+        if (qq == 0) SC[r] = p + t.b_a3;
+    }
+    __syncthreads();
+    if (tid < AB) {   // softmax over the agent's K rows
+        const int base = tid * K;
+        float m = SC[base];
+        for (int k = 1; k < K; ++k) m = fmaxf(m, SC[base + k]);
+        float s = 0.f;
+        for (int k = 0; k < K; ++k) {
+            const float x = expf(SC[base + k] - m);
+            WT[base + k] = x;
+            s += x;
+        }
+        for (int k = 0; k < K; ++k) WT[base + k] = WT[base + k] / s;
+    }
+    // neighbor_value_mlp on the e2 rows again (L2 / Infinity Cache): h1 -> tile, h -> weighted into the tile
+    load_rows<H>(X, t.e2, row0, MU, R, tid);
+    __syncthreads();
+    QS_STAMP(6);
+    mfma_layer<H>(X, reinterpret_cast<const float4*>(t.w_v1p), acc, wave, lane);
+    QS_STAMP(7);
+    __syncthreads();
+    store_tanh<H>(X, acc, wave, lane, [&](int, int n) { return A3[2 * H + n]; });
+    __syncthreads();
+    QS_STAMP(8);
+    mfma_layer<H>(X, reinterpret_cast<const float4*>(t.w_v2p), acc, wave, lane);
+    QS_STAMP(9);
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+        const int n = acc_col<H>(wave, c, lane);
+        const float bn = A3[3 * H + n];
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int i = acc_row(rt, r, lane);
+                X[i * LD + n] = i < MU ? WT[i] * tanh_fast(acc[rt][c][r] + bn) : 0.f;
+            }
+    }
+    __syncthreads();
+    for (int e = tid; e < AB * H; e += NTHR) {
+        const int a = e / H, n = e - a * H;
+        const long agent = row0 / K + a;
+        if (agent < B) {
+            float s = 0.f;
+            for (int k = 0; k < K; ++k) s += X[(a * K + k) * LD + n];
+            t.out[agent * H + n] = s;
+        }
+    }
+    QS_STAMP(10);
+    QS_RTSTAMP(13);
+    QS_STAMP_FLUSH();
+}
+
+}  // namespace pol
+}  // namespace qs

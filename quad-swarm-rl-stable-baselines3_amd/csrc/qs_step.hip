@@ -37,6 +37,7 @@
 #include "qs_flavor_b.h"
 #include "qs_flavor_a.h"
 #include "qs_gae.h"
+#include "qs_policy.h"
 #include "qs_replay.h"
 
 // =============================================================================================
@@ -965,6 +966,72 @@ extern "C" int qs_gae(const float* rewards, const float* values, const uint8_t* 
                        last_values, last_dones, advantages, returns, n_steps, n_cols, gamma, gae_lambda);
     QS_HIP(hipGetLastError());
     return QS_OK;
+}
+
+// fused attention-encoder forward (qs_policy.h)
+static int attn_check(int32_t B, int32_t K, int32_t H, const qs_attn_tower* towers, int32_t n_towers) {
+    if (!towers) return fail(QS_E_INVALID, "NULL towers");
+    if (n_towers < 1 || n_towers > QS_ATTN_MAX_TOWERS) return fail(QS_E_INVALID, "n_towers must be 1 or 2");
+    if (H != 128 && H != 256) return fail(QS_E_INVALID, "attention hidden size must be 128 or 256");
+    if (K < 1 || K > qs::pol::MROWS) return fail(QS_E_INVALID, "neighbours per agent must be 1..64");
+    if (B < 1) return fail(QS_E_INVALID, "B must be >= 1");
+    if ((long long)B * K * H >= (1ll << 31)) return fail(QS_E_INVALID, "B * K * H must stay below 2^31");
+    return QS_OK;
+}
+template <int H>
+static int attn_launch(bool embed, const float* obs, int32_t stride, int32_t so, int32_t off, int32_t B, int32_t K,
+                       int32_t nd, const qs::pol::Towers& tw, int32_t n_towers, hipStream_t st) {
+    const int mu = (qs::pol::MROWS / K) * K;
+    const dim3 grid((unsigned)(((long long)B * K + mu - 1) / mu), (unsigned)n_towers), block(qs::pol::NTHR);
+    if (embed) {
+        const size_t lds = qs::pol::embed_lds_bytes<H>();
+        QS_HIP(hipFuncSetAttribute((const void*)qs::pol::attn_embed_kernel<H>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL(qs::pol::attn_embed_kernel<H>, grid, block, lds, st, obs, stride, so, off, B, K, nd, tw);
+    } else {
+        const size_t lds = qs::pol::pool_lds_bytes<H>();
+        QS_HIP(hipFuncSetAttribute((const void*)qs::pol::attn_pool_kernel<H>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL(qs::pol::attn_pool_kernel<H>, grid, block, lds, st, B, K, tw);
+    }
+    QS_HIP(hipGetLastError());
+    return QS_OK;
+}
+extern "C" int qs_attn_embed(const float* obs, int32_t obs_stride, int32_t self_dim, int32_t nbr_off, int32_t B,
+                             int32_t K, int32_t nd, int32_t H, const qs_attn_tower* towers, int32_t n_towers,
+                             void* stream) {
+    int rc = attn_check(B, K, H, towers, n_towers);
+    if (rc) return rc;
+    if (!obs) return fail(QS_E_INVALID, "NULL obs");
+    if (nd < 1 || nd > qs::pol::MAX_ND) return fail(QS_E_INVALID, "features per neighbour must be 1..16");
+    if (self_dim < 1 || self_dim > obs_stride) return fail(QS_E_INVALID, "self features must lie inside the obs row");
+    if (nd + self_dim > qs::pol::KD0) return fail(QS_E_INVALID, "self + neighbour features must be <= 32");
+    if (nbr_off < 0 || nbr_off + K * nd > obs_stride) return fail(QS_E_INVALID, "neighbour block outside the obs row");
+    qs::pol::Towers tw{};
+    for (int i = 0; i < n_towers; ++i) {
+        const qs_attn_tower& t = towers[i];
+        if (!t.w_e1p || !t.b_e1 || !t.w_e2p || !t.b_e2 || !t.e2 || !t.e_mean)
+            return fail(QS_E_INVALID, "NULL stage-1 tower pointer");
+        tw.t[i] = t;
+    }
+    hipStream_t st = (hipStream_t)stream;
+    return H == 256 ? attn_launch<256>(true, obs, obs_stride, self_dim, nbr_off, B, K, nd, tw, n_towers, st)
+                    : attn_launch<128>(true, obs, obs_stride, self_dim, nbr_off, B, K, nd, tw, n_towers, st);
+}
+extern "C" int qs_attn_pool(int32_t B, int32_t K, int32_t H, const qs_attn_tower* towers, int32_t n_towers,
+                            void* stream) {
+    int rc = attn_check(B, K, H, towers, n_towers);
+    if (rc) return rc;
+    qs::pol::Towers tw{};
+    for (int i = 0; i < n_towers; ++i) {
+        const qs_attn_tower& t = towers[i];
+        if (!t.e2 || !t.P || !t.w_v1p || !t.b_v1 || !t.w_v2p || !t.b_v2 || !t.w_a1ep || !t.w_a2p || !t.b_a2 ||
+            !t.w_a3 || !t.out)
+            return fail(QS_E_INVALID, "NULL stage-2 tower pointer");
+        tw.t[i] = t;
+    }
+    return H == 256 ? attn_launch<256>(false, nullptr, 0, 0, 0, B, K, 0, tw, n_towers, (hipStream_t)stream)
+                    : attn_launch<128>(false, nullptr, 0, 0, 0, B, K, 0, tw, n_towers, (hipStream_t)stream);
 }
 
 // the kernel parameter block a config produces (host only; runtime specialisation / diagnostics)

@@ -9,7 +9,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("QUADSWARM_LIB", os.path.join(HERE, "lib", "libquadswarm.so"))
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 MAX_AGENTS = 64
 MAX_DR_CHOICES = 8
 F, I32, U32, U64, SZ = ctypes.c_float, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_size_t
@@ -117,6 +117,16 @@ R_ACTIVE, R_SAVED, R_CK_N, R_CK_HEAD, R_BUF_N, R_BUF_IDX, R_LAST_ADD, R_EPISODES
 R_HIST_N, R_HIST_HEAD, R_RESTORED, R_PUSHED, NR = 10, 11, 12, 13, 14
 
 
+ATTN_MAX_TOWERS = 2
+
+
+class QsAttnTower(ctypes.Structure):
+    """qs_attn_tower (device pointers of one attention-encoder tower, quadswarm.h)."""
+    _fields_ = [(n, ctypes.c_void_p) for n in ("w_e1p", "b_e1", "w_e2p", "b_e2", "e2", "e_mean", "P", "w_v1p", "b_v1",
+                                                "w_v2p", "b_v2", "w_a1ep", "w_a2p", "b_a2", "w_a3")] + \
+               [("b_a3", F), ("out", ctypes.c_void_p)]
+
+
 class QuadSwarmError(RuntimeError):
     pass
 
@@ -128,7 +138,8 @@ EXPORTS = ["qs_abi_version", "qs_last_error", "qs_struct_sizes", "qs_config_defa
            "qs_set_param",
            "qs_get_param", "qs_state_bytes", "qs_get_state", "qs_set_state", "qs_gae",
            "qs_specialize", "qs_is_specialized", "qs_config_kp_words", "qs_specialize_compile",
-           "qs_replay_config_default", "qs_replay_workspace_bytes", "qs_replay_enable", "qs_replay_disable", "qs_replay_buffers_get"]
+           "qs_replay_config_default", "qs_replay_workspace_bytes", "qs_replay_enable", "qs_replay_disable", "qs_replay_buffers_get",
+           "qs_attn_embed", "qs_attn_pool"]
 
 _lib = None
 
@@ -163,6 +174,8 @@ def lib():
         "qs_replay_workspace_bytes": ([V, P(QsReplayConfig), P(SZ)], I32),
         "qs_replay_enable": ([V, P(QsReplayConfig), V], I32), "qs_replay_disable": ([V], I32),
         "qs_replay_buffers_get": ([V, P(QsReplayBuffers)], I32),
+        "qs_attn_embed": ([V, I32, I32, I32, I32, I32, I32, I32, P(QsAttnTower), I32, V], I32),
+        "qs_attn_pool": ([I32, I32, I32, P(QsAttnTower), I32, V], I32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

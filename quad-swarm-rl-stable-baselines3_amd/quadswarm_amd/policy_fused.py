@@ -1,0 +1,151 @@
+"""Fused rollout forward of the attention policy: the no-grad evaluation that SB3's
+collect_rollouts makes of ActorCriticPolicyCustomSeparateWeights (swarm_rl/models/ActorCriticPolicyCustom.py:
+515-536) once per step, with both towers' attention neighbour encoders (QuadNeighborhoodEncoderAttention,
+swarm_rl/models/quad_multi_model.py:44-101) run by the HIP kernels of csrc/qs_policy.h through the C ABI
+(qs_attn_embed / qs_attn_pool) instead of ~20 torch GEMM + tanh launches per tower.
+
+Per step, for the actor and the critic tower at once (one launch per stage):
+  HIP     e1 (self and neighbour halves of layer 0), e2 rows, mean_K(e2)   (qs_attn_embed)
+  torch   P = mean_K(e2) W_a1[:, H:]^T + b_a1                      [B, H]
+  HIP     value path, attention path, softmax over K, pooled out    (qs_attn_pool)
+  torch   self encoder, feed_forward, core, decoder, heads          (small per-agent GEMMs)
+The result is the same function as the torch module (fp32 throughout; only the summation order of the
+GEMMs differs: tests/test_gpu_policy_fused.py bounds it).  Training (the PPO update with autograd) keeps
+the torch module.
+"""
+import ctypes
+
+import torch
+
+from . import _native as NAT
+
+
+def pack_mfma_weight(w):
+    """[N, Kd] fp32 weight -> the matrix-core operand layout of qs_attn_tower (quadswarm.h):
+    packed[ct][g][l][u] = W[32 ct + (l & 31)][(l >> 5) Kd/2 + 4 g + u]."""
+    n, kd = w.shape
+    assert n % 32 == 0 and kd % 8 == 0, (n, kd)
+    return w.detach().float().contiguous().view(n // 32, 32, 2, kd // 8, 4).permute(0, 3, 2, 1, 4).contiguous()
+
+
+def supports(policy):
+    """Can the fused kernels evaluate this policy's encoders?"""
+    c = policy.cfg
+    return (c.neighbor_encoder_type == "attention" and c.num_use_neighbor_obs >= 1 and
+            c.neighbor_hidden_size in (128, 256) and 1 <= c.neighbor_obs_dim <= 16 and
+            c.num_use_neighbor_obs <= 64 and c.self_obs_dim + c.neighbor_obs_dim <= 32 and c.nonlinearity == "tanh")
+
+
+class FusedRolloutPolicy:
+    """forward(obs) / predict_values(obs) of a SwarmActorCritic with the fused neighbour encoders.
+    refresh() re-packs the weights: call it whenever the policy's parameters changed (PPOTrainer does,
+    once per rollout)."""
+
+    def __init__(self, policy):
+        if not supports(policy):
+            raise ValueError("fused rollout forward: needs the tanh attention encoder with hidden size 128 or 256")
+        self.policy = policy
+        self.cfg = policy.cfg
+        self.H = self.cfg.neighbor_hidden_size
+        self.K = self.cfg.num_use_neighbor_obs
+        self.nd = self.cfg.neighbor_obs_dim
+        self.so = self.cfg.self_obs_dim
+        self.encs = (policy.actor_encoder, policy.critic_encoder)
+        self.L = NAT.lib()
+        self.B = None
+        self.packed = None
+        self.towers = (NAT.QsAttnTower * NAT.ATTN_MAX_TOWERS)()
+
+    # ---- weights / buffers ----
+    def refresh(self):
+        H, so = self.H, self.so
+        packed = []
+        for enc in self.encs:
+            ne = enc.neighbor_encoder
+            emb, val, att = ne.embedding_mlp, ne.neighbor_value_mlp, ne.attention_mlp
+            w0 = emb[0].weight.detach()
+            w_e1 = torch.zeros(H, 32, dtype=torch.float32, device=w0.device)   # [neighbour | self | 0]
+            w_e1[:, :self.nd] = w0[:, so:]
+            w_e1[:, self.nd:self.nd + so] = w0[:, :so]
+            packed.append(dict(
+                w_e1p=pack_mfma_weight(w_e1), b_e1=emb[0].bias.detach(),
+                w_e2p=pack_mfma_weight(emb[2].weight), b_e2=emb[2].bias.detach(),
+                w_v1p=pack_mfma_weight(val[0].weight), b_v1=val[0].bias.detach(),
+                w_v2p=pack_mfma_weight(val[2].weight), b_v2=val[2].bias.detach(),
+                w_a1ep=pack_mfma_weight(att[0].weight[:, :H]), w_a1m=att[0].weight[:, H:].detach(),
+                b_a1=att[0].bias.detach(),
+                w_a2p=pack_mfma_weight(att[2].weight), b_a2=att[2].bias.detach(),
+                w_a3=att[4].weight.detach().reshape(-1).contiguous(), b_a3=float(att[4].bias.detach().item())))
+        self.packed = packed
+        self._bind()
+
+    def _alloc(self, B, dev):
+        H, K, T = self.H, self.K, len(self.encs)
+        z = lambda *s: torch.empty(*s, dtype=torch.float32, device=dev)  # noqa: E731
+        self.B = B
+        self.P = z(T, B, H)
+        self.e2, self.e_mean, self.out = z(T, B * K, H), z(T, B, H), z(T, B, H)
+        self._bind()
+
+    def _bind(self):
+        if self.packed is None or self.B is None:
+            return
+        p = lambda t: t.data_ptr()  # noqa: E731
+        for i, w in enumerate(self.packed):
+            t = self.towers[i]
+            t.w_e1p, t.b_e1 = p(w["w_e1p"]), p(w["b_e1"])
+            t.w_e2p, t.b_e2 = p(w["w_e2p"]), p(w["b_e2"])
+            t.e2, t.e_mean, t.P = p(self.e2[i]), p(self.e_mean[i]), p(self.P[i])
+            t.w_v1p, t.b_v1, t.w_v2p, t.b_v2 = p(w["w_v1p"]), p(w["b_v1"]), p(w["w_v2p"]), p(w["b_v2"])
+            t.w_a1ep, t.w_a2p, t.b_a2, t.w_a3 = p(w["w_a1ep"]), p(w["w_a2p"]), p(w["b_a2"]), p(w["w_a3"])
+            t.b_a3, t.out = w["b_a3"], p(self.out[i])
+
+    # ---- forward ----
+    @torch.no_grad()
+    def neighbor_encodings(self, obs):
+        """[T, B, H]: both towers' QuadNeighborhoodEncoderAttention outputs (the tensor is reused by the next call)."""
+        assert obs.is_cuda and obs.dtype == torch.float32 and obs.dim() == 2
+        obs = obs.contiguous()
+        B = obs.shape[0]
+        if self.packed is None:
+            self.refresh()
+        if self.B != B:
+            self._alloc(B, obs.device)
+        so, H, K = self.so, self.H, self.K
+        st = ctypes.c_void_p(torch.cuda.current_stream(obs.device).cuda_stream)
+        NAT.check(self.L.qs_attn_embed(ctypes.c_void_p(obs.data_ptr()), obs.shape[1], so, so, B, K, self.nd, H,
+                                       self.towers, len(self.encs), st), "qs_attn_embed")
+        for i, w in enumerate(self.packed):
+            torch.addmm(w["b_a1"], self.e_mean[i], w["w_a1m"].t(), out=self.P[i])
+        NAT.check(self.L.qs_attn_pool(B, K, H, self.towers, len(self.encs), st), "qs_attn_pool")
+        return self.out
+
+    def _encode(self, enc, obs, nbr_out):
+        so, na = self.so, enc.all_neighbor_obs_size
+        parts = [enc.self_encoder(obs[:, :so]), nbr_out]
+        if enc.obstacle_encoder is not None:
+            parts.append(enc.obstacle_encoder(obs[:, so + na:]))
+        return enc.feed_forward(torch.cat(parts, dim=1))
+
+    @torch.no_grad()
+    def forward(self, obs, deterministic=False):
+        """SwarmActorCritic.forward: (actions, values [B, 1], log_prob [B])."""
+        from .ppo import squashed_log_prob
+        pol = self.policy
+        nbr = self.neighbor_encodings(obs)
+        a_lat = pol.actor_decoder(pol.actor_core(self._encode(pol.actor_encoder, obs, nbr[0])))
+        mean = pol.action_net(a_lat)
+        values = pol.value_net(pol.critic_decoder(pol.critic_core(self._encode(pol.critic_encoder, obs, nbr[1]))))
+        if deterministic:
+            actions = torch.tanh(mean)
+        else:
+            actions = torch.tanh(mean + torch.randn_like(mean) * pol.log_std.exp())
+        return actions, values, squashed_log_prob(mean, pol.log_std, actions)
+
+    __call__ = forward
+
+    @torch.no_grad()
+    def predict_values(self, obs):
+        pol = self.policy
+        nbr = self.neighbor_encodings(obs)
+        return pol.value_net(pol.critic_decoder(pol.critic_core(self._encode(pol.critic_encoder, obs, nbr[1]))))

@@ -410,7 +410,7 @@ class PPOTrainer:
     the trainer on a CPU stand-in env; the default is the HIP kernel."""
 
     def __init__(self, env, policy: SwarmActorCritic, cfg: PPOConfig = None, device=None, seed=0,
-                 gae_fn=None, group=None):
+                 gae_fn=None, group=None, fused_rollout=True):
         import torch.distributed as dist
 
         self.env, self.policy, self.cfg = env, policy, cfg or PPOConfig()
@@ -430,6 +430,13 @@ class PPOTrainer:
         self.last_obs = None
         self.last_done = torch.zeros(env.I, dtype=torch.uint8, device=self.device)
         self.last_values = torch.zeros(env.I, dtype=torch.float32, device=self.device)
+        # the rollout's policy evaluations through the fused HIP attention encoders (policy_fused.py) where
+        # the policy has that encoder; the update keeps the torch module (autograd)
+        self.fused = None
+        if fused_rollout and self.device.type == "cuda":
+            from .policy_fused import FusedRolloutPolicy, supports
+            if supports(policy):
+                self.fused = FusedRolloutPolicy(policy)
 
     def reset(self):
         self.last_obs = self.env.reset()
@@ -441,9 +448,13 @@ class PPOTrainer:
             self.reset()
         st, pol = self.storage, self.policy
         pol.train(False)
+        fwd = pol
+        if self.fused is not None:
+            self.fused.refresh()      # the weights the last update left
+            fwd = self.fused
         for t in range(self.cfg.n_steps):
             st.obs[t].copy_(self.last_obs)
-            actions, values, logp = pol(st.obs[t])
+            actions, values, logp = fwd(st.obs[t])
             st.actions[t].copy_(actions)
             st.values[t].copy_(values.view(-1))
             st.log_probs[t].copy_(logp)
@@ -453,7 +464,7 @@ class PPOTrainer:
             self.last_done.copy_(done)
             self.last_obs = obs
         self.num_timesteps += self.cfg.n_steps * self.env.I
-        self.last_values.copy_(pol.predict_values(self.last_obs).view(-1))
+        self.last_values.copy_(fwd.predict_values(self.last_obs).view(-1))
         self.gae_fn(st.rewards, st.values, st.episode_starts, self.last_values, self.last_done,
                     self.cfg.gamma, self.cfg.gae_lambda, st.advantages, st.returns)
 

@@ -5,7 +5,7 @@
 
 The stamps library compiles the specialised (hipRTC) kernels with -DQS_STAMPS=1, i.e. the kernels the bench runs
 plus the stamps.  Flavor B stamps phase boundaries (slots 0-11); flavor A sums each phase of its 8-tick loop over
-the ticks (slots 0-9).  Slots 12 / 13 are the wave's s_memrealtime start / end (the launch timeline).  A stamp
+the ticks (slots 0-9).  Slots 12 / 13 are the wave's s_memrealtime start / end (the launch timeline), 14 / 15 its HW_ID / XCC_ID.  A stamp
 waits for its own counter read only (s_waitcnt lgkmcnt(0)): read the SHARES; the total runs a little long."""
 import ctypes
 import os
@@ -49,9 +49,10 @@ def main():
     q = qd if npad * qd <= 64 else 64 // npad
     epb = 64 // (npad * q)
     nb = min((cfg.num_envs + epb - 1) // epb, 65536)
-    buf = np.zeros(65536 * 16, np.uint64)
+    NS = 32   # slots per block (QS_NSTAMP)
+    buf = np.zeros(65536 * NS, np.uint64)
     assert L.qs_debug_stamps_h(env._h, buf.ctypes.data, buf.size) == 0, L.qs_last_error()
-    st = buf.reshape(65536, 16)[:nb].astype(np.int64)
+    st = buf.reshape(65536, NS)[:nb].astype(np.int64)
     rt = st[:, 12:14]
     t0 = rt[:, 0].min()
     s_, e_ = (rt[:, 0] - t0) * 10, (rt[:, 1] - t0) * 10   # ns (s_memrealtime = 100 MHz)
@@ -69,7 +70,25 @@ def main():
     print(f"wave cycles between the first and last stamp: median {np.median(tot):.0f}  p90 {np.percentile(tot, 90):.0f}")
     for k, name in enumerate(names):
         print(f"  {name:36s} {np.median(d[:, k]):8.0f} cycles  {100 * np.median(d[:, k]) / np.median(tot):5.1f} %")
-    slow = np.argsort(e_)[-max(1, nb // 100):]   # the last 1 % of waves to finish: what holds the launch open
+    # where the waves ran: HW_ID (gfx9 layout: wave slot 3:0, SIMD 5:4, CU 11:8, SH 12, SE 15:13) + XCC_ID
+    hw, xcc = st[:, 14], st[:, 15] & 0xF
+    simd_key = (xcc << 16) | (((hw >> 8) & 0xFF) << 2) | ((hw >> 4) & 3)
+    cu_key = simd_key >> 2
+    for name, key in (("SIMD", simd_key), ("CU", cu_key)):
+        u, inv, cnt = np.unique(key, return_inverse=True, return_counts=True)
+        per = cnt[inv]   # waves sharing this wave's SIMD / CU
+        line = ", ".join(f"{c} waves: {np.sum(cnt == c)} {name}s (wave end p50 {np.median(e_[per == c]):.0f} ns, "
+                         f"max {e_[per == c].max():.0f})" for c in np.unique(cnt))
+        print(f"waves per {name} ({len(u)} {name}s used): {line}")
+    print("wave end by XCD (ns): " + ", ".join(f"{x}: p50 {np.median(e_[xcc == x]):.0f} max {e_[xcc == x].max():.0f}"
+                                              for x in np.unique(xcc)))
+    slow = np.argsort(e_)[-max(1, nb // 100):]
+    if cfg.flavor == "B":   # slots 16 / 17: the wave's drones on the floor / in a drone collision
+        fl, co = st[:, 16], st[:, 17]
+        print(f"drones per wave on the floor: mean {fl.mean():.2f} (slowest 1%: {fl[slow].mean():.2f}); in a "
+              f"collision: mean {co.mean():.3f} (slowest 1%: {co[slow].mean():.3f})")
+        for c in np.unique(fl)[:8]:
+            print(f"  {c} on the floor: {np.sum(fl == c)} waves, end p50 {np.median(e_[fl == c]):.0f} ns")   # the last 1 % of waves to finish: what holds the launch open
     print(f"slowest 1% of waves (end >= {e_[slow].min():.0f} ns): cycles median {np.median(tot[slow]):.0f}, "
           f"start ns median {np.median(s_[slow]):.0f}")
     for k, name in enumerate(names):
