@@ -201,7 +201,7 @@ def update_flops_per_sample(pol, obs_dim, act_dim, dev, rows=256):
     return fc.get_total_flops() / rows
 
 
-def end_to_end(env, cfg, dev, world, iters, n_steps=None, log=None):
+def end_to_end(env, cfg, dev, world, iters, n_steps=None, log=None, fused=True):
     """Timed PPO iterations (rollout + GAE + update) on the bench's env shard."""
     import torch
     import torch.distributed as dist
@@ -215,7 +215,7 @@ def end_to_end(env, cfg, dev, world, iters, n_steps=None, log=None):
     pcfg.batch_size = -(-samples // n_mb)
     torch.manual_seed(0)
     pol = SwarmActorCritic(pc).to(dev)
-    tr = PPOTrainer(env, pol, pcfg, seed=0)
+    tr = PPOTrainer(env, pol, pcfg, seed=0, fused_rollout=fused)
     tr.reset()
 
     def sync():
@@ -263,7 +263,8 @@ def end_to_end(env, cfg, dev, world, iters, n_steps=None, log=None):
         "minibatches_per_epoch": n_mb, "policy_params": nparam,
         "policy": f"ActorCriticPolicyCustomSeparateWeights: {pc.neighbor_encoder_type} k={pc.num_use_neighbor_obs}, "
                   f"rnn {pc.rnn_size}, core {pc.rnn_type or 'identity'} x{pc.rnn_num_layers if pc.rnn_type else 0}, "
-                  f"fp32 (torch/hipBLASLt GEMMs)",
+                  f"fp32 (torch/hipBLASLt GEMMs" + (", rollout neighbour encoders: fused HIP MFMA kernels)"
+                                                    if tr.fused is not None else ")"),
         "gemm_table": tuned,
         "update_flop_per_sample": round(fps), "update_tflops": round(upd_tf, 2),
         "update_frac_fp32_mfma_peak": round(upd_tf / 157.3, 3),
@@ -401,6 +402,8 @@ def main():
     ap.add_argument("--cpu-worker", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--e2e-iters", type=int, default=2, help="timed PPO iterations for end_to_end (0 = skip)")
     ap.add_argument("--e2e-steps", type=int, default=0, help="override the PPO rollout length n_steps")
+    ap.add_argument("--e2e-unfused", action="store_true",
+                    help="A/B only: the rollout evaluates the torch policy module instead of the fused encoders")
     args = ap.parse_args()
     if args.cpu_worker:
         return cpu_worker(args.config, args.cpu_seconds)
@@ -521,7 +524,8 @@ def main():
     if args.e2e_iters > 0:
         log = (lambda m: print(m, file=sys.stderr, flush=True)) if rank == 0 else None
         try:
-            e2e = end_to_end(env, cfg, dev, world, args.e2e_iters, args.e2e_steps or None, log)
+            e2e = end_to_end(env, cfg, dev, world, args.e2e_iters, args.e2e_steps or None, log,
+                             fused=not args.e2e_unfused)
         except Exception as e:  # never let the PPO leg kill the env number
             if world > 1:
                 raise
