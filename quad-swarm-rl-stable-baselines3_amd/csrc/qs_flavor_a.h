@@ -54,11 +54,24 @@ __device__ __forceinline__ float sin_small(float x) {
     return x * (1.f + x2 * (-1.f / 6.f + x2 * (1.f / 120.f + x2 * (-1.f / 5040.f + x2 * (1.f / 362880.f + x2 * (-1.f / 39916800.f))))));
 }
 
-// (x + pi) % (2 pi) - pi with Python's modulo sign convention
+// (x + pi) % (2 pi) - pi with Python's modulo sign convention.  For r = x + pi in [-2 pi, 4 pi) -- every
+// angle the step wraps -- fmodf(r, 2 pi) is r itself below 2 pi and r - 2 pi above (exact by Sterbenz), so
+// the fast path gives fmodf's bits without its ~30-instruction loop; anything else (and NaN / inf) takes it.
 __device__ __forceinline__ float wrap_pi(float x) {
-    float r = fmodf(x + kPi, k2Pi);
+    float r = x + kPi;
+    if (!(r >= -k2Pi && r < 2.f * k2Pi)) r = fmodf(r, k2Pi);
+    else if (r >= k2Pi) r -= k2Pi;
     if (r < 0.f) r += k2Pi;
     return r - kPi;
+}
+
+// u[k] = sub-lane (k % Q)'s v[k / Q]
+template <int Q, int K = 0>
+__device__ __forceinline__ void ctl_share(const float (&v)[4 / Q], float* u) {
+    if constexpr (K < 4) {
+        u[K] = qbc<Q, K % Q>(v[K / Q]);
+        ctl_share<Q, K + 1>(v, u);
+    }
 }
 
 // _pid_update_numba (Controller/Pid.py:6-26)
@@ -76,7 +89,10 @@ __device__ __forceinline__ float pid_update(const KP& kp, int k, float e, float*
 // Controller.update_vel_height_dir (Controller.py:76-101) -> Mixer output -> _step's reorder/arctan
 // (quadrotor_single_rewards.py:436-437) -> CustomPidControl.step (quadrotor_control.py:90-94): the 4
 // normalised thrust commands for QuadrotorDynamics.step.
-__device__ __forceinline__ void controller(const KP& kp, const Drone& d, Ctl& c, float a0, float height, float* u) {
+// Q > 1: the drone's Q sub-lanes each take the atan of motors q, q + Q, ..., shared by DPP (bitwise the same)
+template <int Q = 1>
+__device__ __forceinline__ void controller(const KP& kp, const Drone& d, Ctl& c, float a0, float height, float* u,
+                                           int q = 0) {
     c.angvel = a0;
     c.angle = wrap_pi(c.angle + a0 * kp.hrate);
     float sa, ca;
@@ -141,8 +157,21 @@ __device__ __forceinline__ void controller(const KP& kp, const Drone& d, Ctl& c,
         }
     }
     const float re[4] = {m[0], m[3], m[1], m[2]};
+    if constexpr (Q == 1 || 4 % Q != 0) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) u[k] = 0.5f * (clampf(atanf(re[k] * 2.f - 1.f), -1.f, 1.f) + 1.f);
+        for (int k = 0; k < 4; ++k) u[k] = 0.5f * (clampf(atanf(re[k] * 2.f - 1.f), -1.f, 1.f) + 1.f);
+    } else {
+        float v[4 / Q];
+#pragma unroll
+        for (int t = 0; t < 4 / Q; ++t) {
+            float x = re[Q * t];
+#pragma unroll
+            for (int s = 1; s < Q; ++s)
+                if (q == s) x = re[Q * t + s];
+            v[t] = 0.5f * (clampf(atanf(x * 2.f - 1.f), -1.f, 1.f) + 1.f);
+        }
+        ctl_share<Q>(v, u);
+    }
 }
 
 // (|p + v dt| - |p|) / dt without the fp32 cancellation: (2 p.v + dt |v|^2) / (|p + v dt| + |p|)
@@ -160,7 +189,7 @@ __device__ __forceinline__ void camera(const KP& kp, float rx, float ry, float g
     float s, c;
     sincos_hw(-ga, &s, &c);
     const float rp0 = c * rx - s * ry, rp1 = s * rx + c * ry;
-    float m = fmodf(atan2f(rp1, rp0), k2Pi);
+    float m = atan2f(rp1, rp0);   // fmodf(m, 2 pi) is m itself: |atan2| <= pi
     if (m < 0.f) m += k2Pi;
     const float seg = k2Pi / (float)kp.n_cam;
     const int ci = ((int)rintf(m / seg)) % kp.n_cam;
@@ -322,6 +351,22 @@ __device__ __forceinline__ void neighbor_obs_a(const KP& kp, const float4* xch, 
         }
     }
     if (!write) return;
+    if constexpr (Q > 1) {
+        if (!sorted) {   // every neighbour in index order: sub-lane q takes j = q, q + Q, ... (the same code path)
+#pragma unroll
+            for (int t = 0; t < (NPAD + Q - 1) / Q; ++t) {
+                const int j = q + Q * t;
+                const int rank = j < di ? j : j - 1;
+                if (j != di && j < kp.N && rank < kp.K) {
+                    float* o = out + kp.so_dim + rank * F;
+                    rel_features(kp, xch[2 * (base + j)], xch[2 * (base + j) + 1], P, H, aw, V, rng, gid,
+                                 st_obs | ((uint32_t)j << 8),
+                                 [&](int k, float v) { o[k] = clampf(v, kp.nclip_lo[k], kp.nclip_hi[k]); });
+                }
+            }
+            return;
+        }
+    }
 #pragma unroll
     for (int j = 0; j < NPAD; ++j) {
         const bool valid = (j != di) && (j < kp.N);
@@ -579,7 +624,7 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
         if (fin) continue;   // the reference breaks out of its tick loop (:988); segment-uniform
         const Rng rng = env_rng(seed, tick, episode);
         float u[4];
-        controller(kp, d, c, a0, d.goal[2], u);
+        controller<Q>(kp, d, c, a0, d.goal[2], u, q);
         QS_STAMP_ACC(1);
         float z[4];   // QuadrotorDynamics.step: one OU draw per tick (:216)
         if constexpr (Q == 1) {
