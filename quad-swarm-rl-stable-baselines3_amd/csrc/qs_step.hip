@@ -1148,6 +1148,14 @@ static int jit_compile(const qs_config* c, const qs::KP& kp, int npad, int qb, i
     hiprtcAddNameExpression(prog, reset_name.c_str());
     std::vector<const char*> opts = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=on",
                                      "-munsafe-fp-atomics"};
+    // Code generation measured on MI355X (tools/opts_ab.sh, profiles/ab/r03_jit_opts_ab.txt; every variant
+    // bitwise identical): the ILP-first machine scheduler for both flavors, and for flavor B no SLP packing
+    // of fp32 math into v_pk_* (the packing's operand moves cost more issue slots than the pairs save at 2
+    // waves per SIMD; flavor A's single wave per SIMD keeps it).  C3 8.69 -> 8.19 us, C5 15.2 -> 13.4,
+    // C4 12.0 -> 11.2, C2 5.69 -> 5.55, a8 27.2 -> 26.3.
+    opts.push_back("-mllvm");
+    opts.push_back("-amdgpu-sched-strategy=max-ilp");
+    if (c->flavor != QS_FLAVOR_A) opts.push_back("-fno-slp-vectorize");
     // QS_JIT_OPTS: extra space-separated hipRTC options (kernel-variant experiments, e.g. -DQS_X=1)
     std::vector<std::string> extra = jit_extra_opts();
     for (const std::string& o : extra) opts.push_back(o.c_str());
