@@ -48,10 +48,13 @@ CONFIGS = {
     "a8": dict(flavor="A", num_envs=4096, num_agents=8, initial_capture_radius=0.5),
     # 64-drone swarms (the paper's scaling axis, paper/fps_compare.py:7): one env per wave, one lane per drone
     "n64": dict(num_envs=512, num_agents=64, neighbor_visible_num=6, neighbor_obs_type="pos_vel"),
+    # 128-drone swarms (the paper's largest, paper/fps_compare.py:7): one env per two-wave workgroup
+    "n128": dict(num_envs=256, num_agents=128, neighbor_visible_num=6, neighbor_obs_type="pos_vel"),
     "a4": dict(flavor="A", num_envs=8192, num_agents=4, initial_capture_radius=0.5),
 }
 WORKLOAD = {"c2": "single_quad x 16384 envs", "c3": "8-drone swarm static_same_goal x 4096 envs (pos_vel k=6)",
             "n64": "64-drone swarm static_same_goal x 512 envs (pos_vel k=6)",
+            "n128": "128-drone swarm static_same_goal x 256 envs (pos_vel k=6)",
             "c3mix": "8-drone swarm, quads_mode mix (the 9 goal scenarios of QUADS_MODE_LIST) x 4096 envs (pos_vel k=6)",
             "c3mixr": "8-drone swarm, quads_mode mix x 4096 envs (pos_vel k=6) + experience replay (p=0.75), the "
                       "reference's swarm run (runs/quad_multi_mix_baseline.py)",

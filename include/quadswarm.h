@@ -36,8 +36,9 @@
 extern "C" {
 #endif
 
-#define QS_ABI_VERSION 9
-#define QS_MAX_AGENTS 64            /* drones per env: one env lives inside one 64-lane wavefront */
+#define QS_ABI_VERSION 10
+#define QS_MAX_AGENTS 128           /* drones per env: up to 64 inside one 64-lane wavefront, 128 = a two-wave
+                                       workgroup per env (flavor B without obstacles; paper/fps_compare.py:7) */
 #define QS_MAX_DR_CHOICES 8         /* entries per obstacle domain-randomisation list */
 
 enum qs_status {
@@ -179,7 +180,10 @@ enum qs_state_field {
     QS_F_DRING = 56, QS_F_DSUM = 61,
     QS_NF = 64
 };
-enum qs_istate_field { QS_I_SVD = 0, QS_I_FLAGS = 1, QS_I_PREV_LO = 2, QS_I_PREV_HI = 3, QS_NI = 4 };
+/* QS_I_PREV_*: the drone's previous-collision row, bit j = partner j, 32 bits per word (PREV_2 / PREV_3 are
+ * used by 128-drone envs only) */
+enum qs_istate_field { QS_I_SVD = 0, QS_I_FLAGS = 1, QS_I_PREV_LO = 2, QS_I_PREV_HI = 3, QS_I_PREV_2 = 4, QS_I_PREV_3 = 5,
+                       QS_NI = 6 };
 enum qs_drone_flags {
     QS_FL_ON_FLOOR = 1, QS_FL_PREV_WALL = 2, QS_FL_PREV_CEIL = 4,
     QS_FL_CRASH_FLOOR = 8, QS_FL_CRASH_WALL = 16, QS_FL_CRASH_CEIL = 32,

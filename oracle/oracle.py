@@ -95,10 +95,13 @@ class OrDrone(ctypes.Structure):
     ]
 
 
+MAXN = 128   # OR_MAXN (quadswarm_oracle.h): drones per env
+
+
 class OrEnv(ctypes.Structure):
-    _fields_ = [("tick", I), ("episode", ctypes.c_uint32), ("prev_pair_bits", ctypes.c_ubyte * (64 * 64)),
-                ("obs_pos", (D * 3) * 64), ("obs_vel", (D * 3) * 64),
-                ("heading", D * 64), ("target", D * 2), ("capture_radius", D), ("success", I), ("has_pos", I),
+    _fields_ = [("tick", I), ("episode", ctypes.c_uint32), ("prev_pair_bits", ctypes.c_ubyte * (MAXN * MAXN)),
+                ("obs_pos", (D * 3) * MAXN), ("obs_vel", (D * 3) * MAXN),
+                ("heading", D * MAXN), ("target", D * 2), ("capture_radius", D), ("success", I), ("has_pos", I),
                 ("n_obst", I), ("obst", (D * 2) * 64), ("obst_mode", I), ("scen", OrScen),
                 ("last_col", I), ("last_floor0", I), ("obst_mi", I), ("obst_si", I),
                 ("st_col", I), ("st_room", I), ("st_floor", I), ("st_wall", I), ("st_ceil", I), ("st_col_settle", I),

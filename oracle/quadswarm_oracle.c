@@ -417,8 +417,8 @@ static void neighbor_obs(const or_params* p, const or_env* ev, double* obs, int 
         rv[i] = 2.0 * 3.0;          /* 2 * vxyz_max (quadrotor_single.py:296) */
     }
     for (int i = 0; i < N; ++i) {
-        int idx[64], ord[64];
-        double key[64], rel[64][6];
+        int idx[OR_MAXN], ord[OR_MAXN];
+        double key[OR_MAXN], rel[OR_MAXN][6];
         int m = 0;
         for (int j = 0; j < N; ++j) {
             if (j == i) continue;
@@ -574,7 +574,7 @@ void or_collide_ceiling(or_drone* d, or_rng* r, uint32_t gid) {
  * OR_S_DWPAIR | j<<8 uniforms 0-2 z-axis noise, 3-5 omega direction. */
 int or_downwash(const or_params* p, or_drone* dr, int N, uint32_t gbase, or_rng* r) {
     int applied = 0;
-    double P[64][3];
+    double P[OR_MAXN][3];
     for (int i = 0; i < N; ++i) for (int c = 0; c < 3; ++c) P[i][c] = dr[i].pos[c];
     for (int i = 0; i < N; ++i) {
         double z[3] = {dr[i].rot[2], dr[i].rot[5], dr[i].rot[8]};
@@ -769,8 +769,8 @@ static void obstacle_reset(const or_params* p, or_env* ev, uint32_t gbase, or_rn
     ev->obst_mode = mode;
     int fr[64 * 64], F = 0;
     for (int i = 0; i < n * n; ++i) if (!map[i]) fr[F++] = i;   /* np.where(map == 0): row-major */
-    int sp[64], gl[64];
-    double sz[64], gz[64], ez = 0.0;
+    int sp[OR_MAXN], gl[OR_MAXN];
+    double sz[OR_MAXN], gz[OR_MAXN], ez = 0.0;
     if (mode == 0) {   /* o_random */
         if (tape) {
             for (int k = 0; k < 2 * N; ++k) { (void)tape_next(r); (void)tape_next(r); }   /* generate_pos_obst_map x2N */
@@ -913,7 +913,7 @@ void or_env_reset(const or_params* p, or_drone* drones, or_env* envs, int e, or_
     or_env* ev = &envs[e];
     r->step = ((uint64_t)ev->episode << 32) | (uint32_t)ev->tick;   /* env Philox counter */
     const uint32_t gbase = p->id_offset + (uint32_t)((size_t)e * N);
-    double spawn[64][3], goal[64][3];
+    double spawn[OR_MAXN][3], goal[OR_MAXN][3];
     if (p->use_obstacles) {
         obstacle_reset(p, ev, gbase, r, spawn, goal);
     } else if (p->scenario_b != OR_SC_NONE) {   /* scenario.reset(); spawn points = goals (:459-472) */
@@ -986,7 +986,7 @@ void or_env_step(const or_params* p, or_drone* drones, or_env* envs, int e, cons
     double* rw = rew + (size_t)e * N;
     r->step = ((uint64_t)ev->episode << 32) | (uint32_t)ev->tick;   /* env Philox counter */
     const int time_remain = p->ep_len - ev->tick;                  /* QuadrotorSingle.time_remain (:361) */
-    double dist_goal[64];
+    double dist_goal[OR_MAXN];
 
     for (int i = 0; i < N; ++i) {
         or_drone* d = &dr[i];
@@ -1022,10 +1022,10 @@ void or_env_step(const or_params* p, or_drone* drones, or_env* envs, int e, cons
     int is_done = ev->tick > p->ep_len;
 
     /* 1) drone-drone collisions (quadrotor_multi.py:537-568, collisions/quadrotors.py:62-103) */
-    unsigned char cur[64][64];
+    unsigned char cur[OR_MAXN][OR_MAXN];
     memset(cur, 0, sizeof cur);
-    double dist[64][64];
-    int in_cur[64] = {0}, in_prev[64] = {0};
+    double dist[OR_MAXN][OR_MAXN];
+    int in_cur[OR_MAXN] = {0}, in_prev[OR_MAXN] = {0};
     for (int i = 0; i < N; ++i)
         for (int j = i + 1; j < N; ++j) {
             double dx = ev->obs_pos[i][0] - ev->obs_pos[j][0];
@@ -1033,12 +1033,12 @@ void or_env_step(const or_params* p, or_drone* drones, or_env* envs, int e, cons
             double dz = ev->obs_pos[i][2] - ev->obs_pos[j][2];
             dist[i][j] = pow(dx * dx + dy * dy + dz * dz, 0.5);
             if (dist[i][j] <= p->collision_threshold) { cur[i][j] = 1; in_cur[i] = in_cur[j] = 1; }
-            if (ev->prev_pair_bits[i * 64 + j]) { in_prev[i] = in_prev[j] = 1; }
+            if (ev->prev_pair_bits[i * OR_MAXN + j]) { in_prev[i] = in_prev[j] = 1; }
         }
     /* last_step_unique_collisions = setdiff1d(flat(cur), flat(prev)); penalty only if .any() */
     int any_nonzero = 0;
     for (int i = 0; i < N; ++i) if (in_cur[i] && !in_prev[i] && i != 0) any_nonzero = 1;
-    double pen[64] = {0};
+    double pen[OR_MAXN] = {0};
     int any_near = 0;
     double ratio = -p->rew_quadcol_smooth_max / p->collision_falloff_threshold;
     for (int i = 0; i < N; ++i)
@@ -1048,7 +1048,7 @@ void or_env_step(const or_params* p, or_drone* drones, or_env* envs, int e, cons
                 pen[i] += pe; pen[j] += pe; any_near = 1;
             }
     /* 3) room (quadrotor_multi.py:390-403, 600-606) */
-    int wall_new[64], ceil_new[64];
+    int wall_new[OR_MAXN], ceil_new[OR_MAXN];
     for (int i = 0; i < N; ++i) {
         wall_new[i] = dr[i].crashed_wall && !dr[i].prev_wall;
         ceil_new[i] = dr[i].crashed_ceiling && !dr[i].prev_ceiling;
@@ -1056,7 +1056,7 @@ void or_env_step(const or_params* p, or_drone* drones, or_env* envs, int e, cons
         dr[i].prev_ceiling = ceil_new[i];
     }
     /* 2) obstacles (quadrotor_multi.py:570-589): first obstacle hit per drone, new vs previous step */
-    int ocol[64], onew[64];
+    int ocol[OR_MAXN], onew[OR_MAXN];
     for (int i = 0; i < N; ++i) {
         ocol[i] = p->use_obstacles ? or_obst_detect(p, ev, ev->obs_pos[i]) : -1;
         onew[i] = ocol[i] >= 0 && !dr[i].prev_obst;
@@ -1080,7 +1080,7 @@ void or_env_step(const or_params* p, or_drone* drones, or_env* envs, int e, cons
     if (p->apply_collision_force) {
         for (int i = 0; i < N; ++i)
             for (int j = i + 1; j < N; ++j)
-                if (cur[i][j] && !ev->prev_pair_bits[i * 64 + j]) {
+                if (cur[i][j] && !ev->prev_pair_bits[i * OR_MAXN + j]) {
                     flag = 1;
                     or_collide_drones(dr[i].pos, dr[i].vel, dr[i].omega, dr[j].pos, dr[j].vel, dr[j].omega,
                                       r, gbase + (uint32_t)i, (uint32_t)j);
@@ -1095,7 +1095,7 @@ void or_env_step(const or_params* p, or_drone* drones, or_env* envs, int e, cons
         for (int i = 0; i < N; ++i) if (ceil_new[i]) { flag = 1; or_collide_ceiling(&dr[i], r, gbase + (uint32_t)i); }
     }
     for (int i = 0; i < N; ++i)
-        for (int j = i + 1; j < N; ++j) ev->prev_pair_bits[i * 64 + j] = cur[i][j];
+        for (int j = i + 1; j < N; ++j) ev->prev_pair_bits[i * OR_MAXN + j] = cur[i][j];
     for (int i = 0; i < N; ++i) dr[i].prev_obst = ocol[i] >= 0;
     /* 4. scenario.step() (:700-701): new goals; the observations above keep the old ones unless the
      * state-update flag makes the reference recompute them below */
@@ -1103,7 +1103,7 @@ void or_env_step(const or_params* p, or_drone* drones, or_env* envs, int e, cons
         or_sdraw sd;
         memset(&sd, 0, sizeof sd);
         sd.mode = OR_RNG_PHILOX; sd.seed = r->seed; sd.key = gbase; sd.stream = OR_S_SCN; sd.step = r->step;
-        double g[64][3];
+        double g[OR_MAXN][3];
         for (int i = 0; i < N; ++i) memcpy(g[i], dr[i].goal, sizeof g[i]);
         or_scen_step(p, &ev->scen, ev->tick, &sd, g);
         for (int i = 0; i < N; ++i) memcpy(dr[i].goal, g[i], sizeof g[i]);

@@ -16,6 +16,8 @@
  */
 #ifndef QUADSWARM_ORACLE_H
 #define QUADSWARM_ORACLE_H
+/* drones per env: the largest swarm the build steps (QS_MAX_AGENTS, the paper's 128 quads, paper/fps_compare.py:7) */
+#define OR_MAXN 128
 #include <stdint.h>
 
 /* OR_F32: the same sources as an fp32 twin (liboracle_f32.so, built with -fsingle-precision-constant),
@@ -220,10 +222,10 @@ enum { OR_ES_COL = 0, OR_ES_ROOM, OR_ES_FLOOR, OR_ES_WALL, OR_ES_CEIL, OR_ES_COL
 typedef struct {
     int tick;
     uint32_t episode;   /* resets so far; with tick it is the env's Philox counter {tick, episode} */
-    unsigned char prev_pair_bits[64 * 64];  /* [i*64+j], i<j: pair collided at the previous step */
-    double obs_pos[64][3], obs_vel[64][3];  /* QuadrotorEnvMulti.pos / .vel (neighbour obs) */
+    unsigned char prev_pair_bits[OR_MAXN * OR_MAXN];  /* [i*OR_MAXN+j], i<j: pair collided at the previous step */
+    double obs_pos[OR_MAXN][3], obs_vel[OR_MAXN][3];  /* QuadrotorEnvMulti.pos / .vel (neighbour obs) */
     /* flavor A */
-    double heading[64];                      /* QuadrotorEnvMulti.heading (stale across resets) */
+    double heading[OR_MAXN];                      /* QuadrotorEnvMulti.heading (stale across resets) */
     double target[2];                        /* Scenario_dynamic_repulsive.pos                  */
     double capture_radius;
     int success;                             /* episode_success                                 */

@@ -49,7 +49,7 @@ int or_sd_int(or_sdraw* s, int lo, int hi) {
  * Fisher-Yates from the top (i = n-1 .. 1, j = floor(u (i+1))), the order numpy's shuffle walks */
 void or_sd_shuffle(or_sdraw* s, double (*g)[3], int n) {
     if (s->mode == OR_RNG_TAPE) {
-        double tmp[64][3];
+        double tmp[OR_MAXN][3];
         memcpy(tmp, g, sizeof(double) * 3 * (size_t)n);
         for (int i = 0; i < n; ++i) {
             const int p = (int)sd_next(s);
@@ -202,7 +202,7 @@ static double z_value(int n, int per_layer, double box, int f, double size, or_s
 /* Scenario_swarm_vs_swarm.create_formations (swarm_vs_swarm.py:49-54) [+ the shuffles of update_goals
  * :66-71]: goals_1 (N // 2 around c1) then goals_2 (the rest around c2); surplus sphere points spill */
 static void vs_formations(const or_params* p, or_scen* sc, double (*g)[3], int shuffle, or_sdraw* s) {
-    double g1[64][3], g2[64][3];
+    double g1[OR_MAXN][3], g2[OR_MAXN][3];
     const int N = p->num_agents;
     const int n1 = or_generate_goals(sc->formation, N / 2, sc->per_layer, sc->size, sc->layer, sc->c1, g1);
     const int n2 = or_generate_goals(sc->formation, N - N / 2, sc->per_layer, sc->size, sc->layer, sc->c2, g2);
@@ -223,7 +223,7 @@ void or_scen_reset(const or_params* p, or_scen* sc, or_sdraw* s, double (*g)[3])
     memset(sc, 0, sizeof *sc);   /* a fresh Scenario_* object per reset (mix.py:88) */
     const double cf = 1.0 / p->control_dt;                 /* control_freq (quadrotor_single.py:160) */
     sc->mode = p->scenario_b == OR_SC_MIX ? or_sd_int(s, 0, N == 1 ? 5 : 9) : p->scenario_b;  /* mix.py:46-56, 82 */
-    double tmp[64][3];
+    double tmp[OR_MAXN][3];
     sc->period = (int)(5.0 * cf);                          /* __init__: duration_time = 5.0 */
     switch (sc->mode) {
         case OR_SC_DYNAMIC_FORMATIONS:                     /* dynamic_formations.py:9-16 (__init__), 42-48 */
@@ -290,7 +290,7 @@ static void bezier2(const double (*nd)[3], double s, double* out) {
 void or_scen_step(const or_params* p, or_scen* sc, int tick, or_sdraw* s, double (*g)[3]) {
     const int N = p->num_agents;
     const double box = p->spawn_box, cf = 1.0 / p->control_dt;
-    double tmp[64][3];
+    double tmp[OR_MAXN][3];
     switch (sc->mode) {
         case OR_SC_DYNAMIC_SAME_GOAL:                      /* dynamic_same_goal.py:16-29 (np.random) */
             if (tick % sc->period == 0 && tick > 0) {

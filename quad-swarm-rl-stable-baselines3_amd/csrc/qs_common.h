@@ -182,11 +182,34 @@ __device__ uint64_t qs_dbg_stamps[65536 * QS_NSTAMP];
 #define QS_STAMP_DECL
 #endif
 
+// Two waves share each SIMD (C3: 2048 one-wave workgroups), and VALU issue goes to the older one first: it
+// ends ~1.1 us before its partner (profiles/r03_stamps_c3_s2.txt, by wave slot), and the launch ends with the
+// younger waves.  The younger wave (wave slot != 0) takes the issue priority once the older one has drawn
+// its Philox blocks -- mark 11, between the draws and the first wait on the state loads -- so the pair
+// finishes together: C3 8.16 -> 7.77 us (profiles/ab/r03_prio_ab.txt; marks after the loads / physics
+// gain less, priority from the start loses).  -DQS_PRIO_AT=-1 turns it off for A/Bs.
+#ifndef QS_PRIO_AT
+#define QS_PRIO_AT 11
+#endif
+#if QS_PRIO_AT >= 0
+#define QS_PRIO(k)                                                                                    \
+    do {                                                                                              \
+        if ((k) == QS_PRIO_AT) {                                                                      \
+            uint32_t hw_;                                                                             \
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_));                        \
+            if (hw_ & 0xFu) __builtin_amdgcn_s_setprio(1);                                            \
+        }                                                                                             \
+    } while (0)
+#else
+#define QS_PRIO(k) do {} while (0)
+#endif
+
 struct Drone {
     float pos[3], vel[3], rot[9], om[3], rd[4], cd[4], ou[4], goal[3];
     int32_t svd;
     uint32_t flags;
-    uint64_t prev;
+    uint64_t prev;    // previous-collision row, partners 0..63 (bit j = partner j)
+    uint64_t prevx;   // partners 64..127 (128-drone envs only; zero otherwise)
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -235,6 +258,8 @@ __device__ __forceinline__ T ld_field(const T* base, int f, int I, uint32_t boff
     return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base + (size_t)f * (size_t)I) + boff);
 }
 
+// WIDE: the 128-drone envs' collision row (istate words QS_I_PREV_2 / _3 too)
+template <bool WIDE = false>
 __device__ __forceinline__ void load_drone(const KP& kp, const Bufs& b, int g, Drone& d) {
     const float* s = b.st;
     const int I = kp.I;
@@ -256,6 +281,9 @@ __device__ __forceinline__ void load_drone(const KP& kp, const Bufs& b, int g, D
     d.flags = (uint32_t)ld_field(is, QS_I_FLAGS, I, bo);
     d.prev = (uint64_t)(uint32_t)ld_field(is, QS_I_PREV_LO, I, bo) |
              ((uint64_t)(uint32_t)ld_field(is, QS_I_PREV_HI, I, bo) << 32);
+    d.prevx = WIDE ? (uint64_t)(uint32_t)ld_field(is, QS_I_PREV_2, I, bo) |
+                         ((uint64_t)(uint32_t)ld_field(is, QS_I_PREV_3, I, bo) << 32)
+                   : 0ull;
 }
 
 // Write-through (sc1) stores: the bytes leave the XCD's L2 during the kernel instead of being
@@ -295,6 +323,7 @@ __device__ __forceinline__ void st_field(T* base, int f, int I, uint32_t boff, T
     st_wt1(qs_rsrc(base), boff, (uint32_t)f * (uint32_t)I * 4u, w);
 }
 
+template <bool WIDE = false>
 __device__ __forceinline__ void store_drone(const KP& kp, const Bufs& b, int g, const Drone& d) {
     float* s = b.st;
     const int I = kp.I;
@@ -316,6 +345,10 @@ __device__ __forceinline__ void store_drone(const KP& kp, const Bufs& b, int g, 
     st_field(is, QS_I_FLAGS, I, bo, (int32_t)d.flags);
     st_field(is, QS_I_PREV_LO, I, bo, (int32_t)(uint32_t)d.prev);
     st_field(is, QS_I_PREV_HI, I, bo, (int32_t)(uint32_t)(d.prev >> 32));
+    if (WIDE) {
+        st_field(is, QS_I_PREV_2, I, bo, (int32_t)(uint32_t)d.prevx);
+        st_field(is, QS_I_PREV_3, I, bo, (int32_t)(uint32_t)(d.prevx >> 32));
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -654,7 +687,7 @@ __device__ __forceinline__ int xcd_block(int b, int nblocks) {
 // block-level obs staging: LDS tile [rows, obs_dim] -> contiguous global rows
 // ---------------------------------------------------------------------------------------------
 // Returns how many of the values this lane stored are non-finite (the obs guard of qs_counters).
-__device__ __forceinline__ int tile_store(const float* lds, float* dst, int nfloat, int lane) {
+__device__ __forceinline__ int tile_store(const float* lds, float* dst, int nfloat, int lane, int nthr = 64) {
     // dst = first row of the block; rows are contiguous in HBM.  obs is 256-B aligned and a block owns
     // 64/NPAD*N rows, so the start is 16-B aligned whenever rows*obs_dim*4 is: b128 in, dwordx4 out.
     int bad = 0;
@@ -662,7 +695,7 @@ __device__ __forceinline__ int tile_store(const float* lds, float* dst, int nflo
         const int nvec = nfloat >> 2;
         const float4* lv = reinterpret_cast<const float4*>(lds);
         const __amdgpu_buffer_rsrc_t r = qs_rsrc(dst);
-        for (int v = lane; v < nvec; v += 64) {
+        for (int v = lane; v < nvec; v += nthr) {
             const float4 x = lv[v];
             st_wt4(r, (uint32_t)v * 16u, x);
             if (!(fin_acc(fin_acc(fin_acc(x.x * 0.f, x.y), x.z), x.w) == 0.f))
@@ -674,7 +707,7 @@ __device__ __forceinline__ int tile_store(const float* lds, float* dst, int nflo
             bad += !(lds[t] * 0.f == 0.f);
         }
     } else {
-        for (int f = lane; f < nfloat; f += 64) {
+        for (int f = lane; f < nfloat; f += nthr) {
             dst[f] = lds[f];
             bad += !(lds[f] * 0.f == 0.f);
         }

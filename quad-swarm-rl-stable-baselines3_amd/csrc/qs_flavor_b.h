@@ -164,7 +164,9 @@ __device__ void neighbor_obs(const KP& kp, const float4* xch, int dbase, int di,
     const float vm = 2.f * kp.vxyz_max;
     const bool pairs = ((kp.so_dim | kp.obs_dim) & 1) == 0;   // 8-byte aligned slots: ds_write_b64
     if constexpr (Q == 1 && NPAD >= 64) {
-        if (sorted && kp.K <= 16) {
+        // 128-drone envs always take this path (k = N - 1 keys are all 0: the passes pick index order, as the
+        // ranking does); their 128 x 128 ranking is not compiled
+        if (NPAD > 64 || (sorted && kp.K <= 16)) {
             // one lane per drone, many candidates, few neighbours: K passes of a (key, index) minimum above
             // the previous pick instead of ranking every candidate against all the others -- the same
             // strict (key, index) order, so the same neighbours in the same slots
@@ -194,6 +196,7 @@ __device__ void neighbor_obs(const KP& kp, const float4* xch, int dbase, int di,
             return;
         }
     }
+    if constexpr (NPAD <= 64) {
 #pragma unroll
     for (int t = 0; t < PJ; ++t) {
         const int j = q + Q * t;
@@ -224,6 +227,7 @@ __device__ void neighbor_obs(const KP& kp, const float4* xch, int dbase, int di,
                 o[0] = o0; o[1] = o1; o[2] = o2; o[3] = o3; o[4] = o4; o[5] = o5;
             }
         }
+    }
     }
 }
 
@@ -359,6 +363,7 @@ __device__ __forceinline__ void reset_drone(const KP& kp, Drone& d, const Rng& r
     for (int k = 0; k < 4; ++k) { d.rd[k] = 0.f; d.cd[k] = 0.f; }
     d.flags = 0;
     d.prev = 0;
+    d.prevx = 0;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -591,18 +596,27 @@ constexpr int DRONE_WORDS = QS_F_GOAL + 3 + 4;
 constexpr int STAT_WORDS = 8;
 constexpr int LOAD_WORDS = DRONE_WORDS + STAT_WORDS;
 
-template <int Q, int W, int T>
+// 128-drone envs carry NIW = 6 istate words (the 128-bit collision row, QS_I_PREV_2 / _3): the drone's words
+// are then the 33 fp32 fields, 6 int fields and the stats words
+template <int NIW>
+struct WordsOf {
+    static constexpr int DW = QS_F_GOAL + 3 + NIW, LW = DW + STAT_WORDS;
+};
+
+template <int Q, int W, int T, int LW = LOAD_WORDS>
 __device__ __forceinline__ void qbc_words(const uint32_t (&r)[T], uint32_t* wv) {
-    if constexpr (W < LOAD_WORDS && W / Q < T) {
+    if constexpr (W < LW && W / Q < T) {
         wv[W] = (uint32_t)__float_as_int(qbc<Q, W % Q>(__int_as_float((int)r[W / Q])));
-        qbc_words<Q, W + 1, T>(r, wv);
+        qbc_words<Q, W + 1, T, LW>(r, wv);
     }
 }
 
+template <int NIW = 4>
 __device__ __forceinline__ uint32_t drone_word_off(const KP& kp, const Bufs& b, int w, uint32_t go) {
+    constexpr int DW = WordsOf<NIW>::DW;
     const uint32_t I4 = (uint32_t)kp.I * 4u;
     const uint32_t ist0 = (uint32_t)((const char*)b.ist - (const char*)b.st);
-    if (w >= DRONE_WORDS) return (uint32_t)(QS_F_DRING + w - DRONE_WORDS) * I4 + go;
+    if (w >= DW) return (uint32_t)(QS_F_DRING + w - DW) * I4 + go;
     return (w < QS_F_GOAL + 3 ? (uint32_t)w * I4 : ist0 + (uint32_t)(w - QS_F_GOAL - 3) * I4) + go;
 }
 
@@ -612,27 +626,27 @@ struct DroneWords {
     uint32_t r[T];
 };
 // issue the sub-lane's state-word loads (no wait): the first nw <= NW words
-template <int Q, int NW>
+template <int Q, int NW, int NIW = 4>
 __device__ __forceinline__ void load_words_q(const KP& kp, const Bufs& b, int g, int q, DroneWords<Q, NW>& dw,
                                              int nw = NW) {
     const uint32_t go = (uint32_t)g * 4u;
 #pragma unroll
     for (int t = 0; t < DroneWords<Q, NW>::T; ++t) {
         const int w = t * Q + q;
-        dw.r[t] = w < nw ? *reinterpret_cast<const uint32_t*>((const char*)b.st + drone_word_off(kp, b, w, go)) : 0u;
+        dw.r[t] = w < nw ? *reinterpret_cast<const uint32_t*>((const char*)b.st + drone_word_off<NIW>(kp, b, w, go)) : 0u;
     }
 }
 // the drone on every sub-lane; stw (if given) gets the STAT_WORDS words as floats
-template <int Q, int NW>
+template <int Q, int NW, int NIW = 4>
 __device__ __forceinline__ void unpack_words_q(const DroneWords<Q, NW>& dw, Drone& d, float* stw = nullptr) {
-    constexpr int T = DroneWords<Q, NW>::T;
+    constexpr int T = DroneWords<Q, NW>::T, DW = WordsOf<NIW>::DW;
     const uint32_t (&r)[T] = dw.r;
-    uint32_t wv[T * Q > DRONE_WORDS ? T * Q : DRONE_WORDS];
-    qbc_words<Q, 0, T>(r, wv);
-    if constexpr (NW > DRONE_WORDS) {
+    uint32_t wv[T * Q > DW ? T * Q : DW];
+    qbc_words<Q, 0, T, WordsOf<NIW>::LW>(r, wv);
+    if constexpr (NW > DW) {
         if (stw) {
 #pragma unroll
-            for (int k = 0; k < STAT_WORDS; ++k) stw[k] = __int_as_float((int)wv[DRONE_WORDS + k]);
+            for (int k = 0; k < STAT_WORDS; ++k) stw[k] = __int_as_float((int)wv[DW + k]);
         }
     }
 #pragma unroll
@@ -652,6 +666,7 @@ __device__ __forceinline__ void unpack_words_q(const DroneWords<Q, NW>& dw, Dron
     d.svd = (int32_t)wv[IW + QS_I_SVD];
     d.flags = wv[IW + QS_I_FLAGS];
     d.prev = (uint64_t)wv[IW + QS_I_PREV_LO] | ((uint64_t)wv[IW + QS_I_PREV_HI] << 32);
+    d.prevx = NIW > 4 ? (uint64_t)wv[IW + QS_I_PREV_2 % NIW] | ((uint64_t)wv[IW + QS_I_PREV_3 % NIW] << 32) : 0ull;
 }
 template <int Q>
 __device__ __forceinline__ void load_drone_q(const KP& kp, const Bufs& b, int g, int q, Drone& d) {
@@ -661,10 +676,10 @@ __device__ __forceinline__ void load_drone_q(const KP& kp, const Bufs& b, int g,
 }
 
 // ST: also the stats words DRONE_WORDS + k whose bit k of stmask is set (stw = their values).
-template <int Q, bool ST = false>
+template <int Q, bool ST = false, int NIW = 4>
 __device__ __forceinline__ void store_drone_q(const KP& kp, const Bufs& b, int g, int q, bool active, const Drone& d,
                                               const float* stw = nullptr, uint32_t stmask = 0u) {
-    constexpr int NW = ST ? LOAD_WORDS : DRONE_WORDS;
+    constexpr int DW = WordsOf<NIW>::DW, NW = ST ? WordsOf<NIW>::LW : DW;
     uint32_t wv[NW];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -684,9 +699,13 @@ __device__ __forceinline__ void store_drone_q(const KP& kp, const Bufs& b, int g
     wv[IW + QS_I_FLAGS] = d.flags;
     wv[IW + QS_I_PREV_LO] = (uint32_t)d.prev;
     wv[IW + QS_I_PREV_HI] = (uint32_t)(d.prev >> 32);
+    if constexpr (NIW > 4) {
+        wv[IW + QS_I_PREV_2 % NIW] = (uint32_t)d.prevx;
+        wv[IW + QS_I_PREV_3 % NIW] = (uint32_t)(d.prevx >> 32);
+    }
     if constexpr (ST) {
 #pragma unroll
-        for (int k = 0; k < STAT_WORDS; ++k) wv[DRONE_WORDS + k] = (uint32_t)__float_as_int(stw[k]);
+        for (int k = 0; k < STAT_WORDS; ++k) wv[DW + k] = (uint32_t)__float_as_int(stw[k]);
     }
     constexpr int T = (NW + Q - 1) / Q;
     const uint32_t go = (uint32_t)g * 4u;
@@ -698,8 +717,8 @@ __device__ __forceinline__ void store_drone_q(const KP& kp, const Bufs& b, int g
 #pragma unroll
         for (int k = 1; k < Q; ++k)
             if (q == k && t * Q + k < NW) v = wv[t * Q + k];
-        const bool wr = w < DRONE_WORDS || (w < NW && ((stmask >> (w - DRONE_WORDS)) & 1u));
-        if (active && wr) st_wt1(rs, drone_word_off(kp, b, w, go), 0u, v);
+        const bool wr = w < DW || (w < NW && ((stmask >> (w - DW)) & 1u));
+        if (active && wr) st_wt1(rs, drone_word_off<NIW>(kp, b, w, go), 0u, v);
     }
 }
 
@@ -709,15 +728,144 @@ __device__ __forceinline__ void store_drone_q(const KP& kp, const Bufs& b, int g
 #endif
 template <int NPAD>
 struct StepGeo {
-    static constexpr int Q = NPAD * QS_QB <= 64 ? QS_QB : 64 / NPAD;
-    static constexpr int LPE = NPAD * Q;        // lanes per env
-    static constexpr int EPB = 64 / LPE;        // envs per workgroup (one wave)
-    static constexpr int SLOTS = EPB * NPAD;    // drone slots per workgroup
+    static constexpr int Q = NPAD * QS_QB <= 64 ? QS_QB : (NPAD >= 64 ? 1 : 64 / NPAD);
+    static constexpr int LPE = NPAD * Q;           // lanes per env
+    static constexpr int WGS = LPE > 64 ? LPE : 64; // threads per workgroup: one wave, or the env's two waves
+    static constexpr int EPB = WGS / LPE;           // envs per workgroup
+    static constexpr int SLOTS = EPB * NPAD;        // drone slots per workgroup
+    static constexpr bool WIDE = NPAD > 64;         // the env spans the workgroup's waves (128-drone envs)
+    static constexpr int NIW = WIDE ? 6 : 4;        // istate words per drone (WordsOf)
+};
+
+// ---- collision rows: bit j = partner drone j; 64 bits, or two words for the 128-drone envs ----
+struct Row128 {
+    uint64_t lo, hi;
+};
+__device__ __forceinline__ Row128 operator|(Row128 a, Row128 b) { return Row128{a.lo | b.lo, a.hi | b.hi}; }
+__device__ __forceinline__ Row128 operator&(Row128 a, Row128 b) { return Row128{a.lo & b.lo, a.hi & b.hi}; }
+__device__ __forceinline__ Row128 operator~(Row128 a) { return Row128{~a.lo, ~a.hi}; }
+template <bool WIDE> struct RowOf { using T = uint64_t; };
+template <> struct RowOf<true> { using T = Row128; };
+__device__ __forceinline__ bool row_any(uint64_t r) { return r != 0ull; }
+__device__ __forceinline__ bool row_any(Row128 r) { return (r.lo | r.hi) != 0ull; }
+__device__ __forceinline__ int row_popc(uint64_t r) { return __popcll(r); }
+__device__ __forceinline__ int row_popc(Row128 r) { return __popcll(r.lo) + __popcll(r.hi); }
+__device__ __forceinline__ int row_ffs(uint64_t r) { return __ffsll((long long)r) - 1; }   // r != 0
+__device__ __forceinline__ int row_ffs(Row128 r) {
+    return r.lo ? __ffsll((long long)r.lo) - 1 : 64 + __ffsll((long long)r.hi) - 1;
+}
+__device__ __forceinline__ void row_set(uint64_t& r, int j, bool c) { r |= c ? (1ull << j) : 0ull; }
+__device__ __forceinline__ void row_set(Row128& r, int j, bool c) {
+    if (j < 64) r.lo |= c ? (1ull << j) : 0ull;
+    else r.hi |= c ? (1ull << (j - 64)) : 0ull;
+}
+__device__ __forceinline__ void row_clear(uint64_t& r, int j) { r &= ~(1ull << j); }
+__device__ __forceinline__ void row_clear(Row128& r, int j) {
+    if (j < 64) r.lo &= ~(1ull << j);
+    else r.hi &= ~(1ull << (j - 64));
+}
+// the partners above drone di (pairs (di, j > di))
+__device__ __forceinline__ uint64_t row_above(uint64_t r, int di) { return r & ~((2ull << di) - 1ull); }
+__device__ __forceinline__ Row128 row_above(Row128 r, int di) {
+    return di < 64 ? Row128{r.lo & ~((2ull << di) - 1ull), r.hi} : Row128{0ull, r.hi & ~((2ull << (di - 64)) - 1ull)};
+}
+__device__ __forceinline__ void row_of(const Drone& d, uint64_t& r) { r = d.prev; }
+__device__ __forceinline__ void row_of(const Drone& d, Row128& r) { r = Row128{d.prev, d.prevx}; }
+__device__ __forceinline__ void row_keep(Drone& d, uint64_t r) { d.prev = r; }
+__device__ __forceinline__ void row_keep(Drone& d, Row128 r) { d.prev = r.lo; d.prevx = r.hi; }
+
+// Env-level collectives of the step kernel over a predicate of the env's lanes (callers pass x && q == 0 to
+// count drones).  An env inside one wave: a ballot of the env's lane segment (drone i at bit i Q).  A 128-drone
+// env (WIDE, Q = 1): each wave's ballot through a 2-word LDS slot and a workgroup barrier; the slots alternate
+// so that one barrier per collective suffices.  Every lane of the workgroup must make the same calls.
+template <bool WIDE>
+struct EnvColl {
+    using Row = typename RowOf<WIDE>::T;
+    int lbase;
+    uint64_t lmask;
+    uint64_t* scr;   // WIDE: 4 words of LDS
+    int slot;
+    __device__ __forceinline__ Row bits(bool x) {
+        if constexpr (!WIDE) {
+            return (__ballot(x) >> lbase) & lmask;
+        } else {
+            const uint64_t bw = __ballot(x);
+            uint64_t* s = scr + 2 * slot;
+            slot ^= 1;
+            if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = bw;
+            lds_sync();
+            return Row128{s[0], s[1]};
+        }
+    }
+    __device__ __forceinline__ bool any(bool x) { return row_any(bits(x)); }
+    __device__ __forceinline__ int count(bool x) { return row_popc(bits(x)); }
+    // uniform over the launch's unit of lockstep (the wave, or the WIDE workgroup): guards work that has barriers
+    __device__ __forceinline__ bool wany(bool x) {
+        if constexpr (!WIDE) return __ballot(x) != 0ull;
+        else return any(x);
+    }
 };
 
 
+// Drone-drone impulses of a 128-drone env (its two waves): the new pairs in the reference's (i, j) order, one
+// event per round.  Every drone posts its pos / vel / omega and its first pending partner to LDS tables (in the
+// obs tile, unused until the obs phase), a collective finds the first drone i with a pending pair, lanes 0..8
+// draw the pair's 9 Philox blocks (7 normal, 2 uniform), and the pair's two lanes apply collide_pair --
+// the same draws and arithmetic as the one-wave loop of step_kernel.
+template <int NPAD>
+__device__ __forceinline__ void impulses_wide(const KP& kp, const Rng& rng, float* lds, EnvColl<true>& ec, Drone& d,
+                                              Row128 pend, int env, int di, int lane, bool& vchanged) {
+    float4* pscr = reinterpret_cast<float4*>(lds);       // the pair's 9 blocks
+    float4* tab = pscr + 16;                              // per drone: {pos}, {vel}, {omega}
+    int* jt = reinterpret_cast<int*>(tab + 3 * NPAD);     // per drone: first pending partner, -1 = none
+    for (;;) {
+        tab[3 * di] = make_float4(d.pos[0], d.pos[1], d.pos[2], 0.f);
+        tab[3 * di + 1] = make_float4(d.vel[0], d.vel[1], d.vel[2], 0.f);
+        tab[3 * di + 2] = make_float4(d.om[0], d.om[1], d.om[2], 0.f);
+        const bool has = row_any(pend);
+        jt[di] = has ? row_ffs(pend) : -1;
+        const Row128 bal = ec.bits(has);   // its barrier also orders the table writes
+        if (!row_any(bal)) break;
+        const int istar = row_ffs(bal), jstar = jt[istar];
+        const bool involved = di == istar || di == jstar;
+        const int partner = di == istar ? jstar : istar;
+        const float4 a = tab[3 * partner], bv = tab[3 * partner + 1], c = tab[3 * partner + 2];
+        const float pp[3] = {a.x, a.y, a.z};
+        float pv[3] = {bv.x, bv.y, bv.z}, pw[3] = {c.x, c.y, c.z};   // the partner's copy (collide_pair writes both)
+        const uint32_t gi = kp.id0 + (uint32_t)(env * kp.N + istar);
+        const uint32_t st = S_PAIR | ((uint32_t)jstar << 8);
+        if (lane < 9) {
+            const bool isn = lane < 7;
+            const W4 w = block(rng, gi, isn ? st : (st | UNIF_BIT), (uint32_t)(isn ? lane : lane - 7));
+            float v[4];
+            if (isn) {
+                box_muller(w.w[0], w.w[1], v[0], v[1]);
+                box_muller(w.w[2], w.w[3], v[2], v[3]);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) v[i] = u01(w.w[i]);
+            }
+            pscr[lane] = make_float4(v[0], v[1], v[2], v[3]);
+        }
+        lds_sync();
+        if (involved) {
+            float z[28], u[8];
+#pragma unroll
+            for (int k = 0; k < 9; ++k) {
+                const float4 x = pscr[k];
+                float* o = k < 7 ? z + 4 * k : u + 4 * (k - 7);
+                o[0] = x.x; o[1] = x.y; o[2] = x.z; o[3] = x.w;
+            }
+            if (di == istar) collide_pair(d.pos, d.vel, d.om, pp, pv, pw, z, u);
+            else collide_pair(pp, pv, pw, d.pos, d.vel, d.om, z, u);
+        }
+        vchanged |= involved;
+        if (di == istar) row_clear(pend, jstar);
+    }
+}
+
 template <int NPAD, bool OBST>
-__global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bufs b, RBufs r, RP rp) {
+__global__ __launch_bounds__(StepGeo<NPAD>::WGS) void step_kernel(const KP* __restrict__ kpp, Bufs b, RBufs r, RP rp) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     QS_BIND_KP(kpp);
     const uint32_t seed = kpm.seed;
@@ -725,7 +873,10 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     QS_RTSTAMP(12);
     QS_STAMP(0);
     using G = StepGeo<NPAD>;
-    constexpr int Q = G::Q, LPE = G::LPE, EPB = G::EPB, SLOTS = G::SLOTS;
+    constexpr int Q = G::Q, LPE = G::LPE, EPB = G::EPB, SLOTS = G::SLOTS, WGS = G::WGS, NIW = G::NIW;
+    constexpr bool WIDE = G::WIDE;
+    constexpr int LW = WordsOf<NIW>::LW, DW = WordsOf<NIW>::DW;
+    using Row = typename RowOf<WIDE>::T;
     const int lane = threadIdx.x;
     const int el = lane / LPE, di = (lane % LPE) / Q, q = lane % Q;
     const int env0 = xcd_block((int)blockIdx.x, (int)gridDim.x) * EPB;
@@ -740,11 +891,15 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     const int rows = nenv_blk * kp.N;
     float* row = lds + (size_t)(el * kp.N + di) * kp.obs_dim;
     float4* xch = reinterpret_cast<float4*>(lds + SLOTS * kp.obs_dim);
+    const uint64_t lmask = (LPE >= 64) ? ~0ull : ((1ull << LPE) - 1ull);
+    // env-level collectives; WIDE: their LDS slots and the env counters' exchange in the 64 words after xch
+    uint64_t* wscr = reinterpret_cast<uint64_t*>(lds + SLOTS * kp.obs_dim + SLOTS * 8);
+    EnvColl<WIDE> ec{lbase, lmask, wscr, 0};
     float2* otile = obst_tile(lds, kp, SLOTS);
     ObstScratch* oscr = reinterpret_cast<ObstScratch*>(otile + EPB * kp.M);
     const float2* myob = otile + el * kp.M;
     if (OBST)   // the block's obstacle lists -> LDS (ordered by the first lds_sync below)
-        for (int k = lane; k < nenv_blk * kp.M; k += 64) otile[k] = b.obst[(size_t)env0 * kp.M + k];
+        for (int k = lane; k < nenv_blk * kp.M; k += WGS) otile[k] = b.obst[(size_t)env0 * kp.M + k];
 
     // Every global load of the step is issued up front, back to back -- the action, the env's counters, the
     // drone's state words -- before anything waits: their HBM latencies overlap instead of adding up (the
@@ -770,8 +925,8 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     int omi = 0, osi = 0;   // the env's domain-randomisation choice (QS_E_OBST_M / _SZ)
     if (OBST && kp.dr) { omi = b.env[QS_E_OBST_M * kp.E + eidx]; osi = b.env[QS_E_OBST_SZ * kp.E + eidx]; }
     Drone d;   // every sub-lane holds the whole drone
-    DroneWords<Q, LOAD_WORDS> dw;
-    load_words_q(kp, b, g, q, dw, kp.stats ? LOAD_WORDS : DRONE_WORDS);
+    DroneWords<Q, LW> dw;
+    load_words_q<Q, LW, NIW>(kp, b, g, q, dw, kp.stats ? LW : DW);
     __builtin_amdgcn_sched_barrier(0);
     const Rng rng = env_rng(seed, tick0, episode);
     // The step's regular draws: Philox block k of {OU 0, sensor 0, sensor 1, sensor 2} on sub-lane
@@ -795,9 +950,10 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
         }
     }
 
+    QS_PRIO(11);
     __builtin_amdgcn_sched_barrier(0);
     float stw[STAT_WORDS];
-    unpack_words_q(dw, d, stw);
+    unpack_words_q<Q, LW, NIW>(dw, d, stw);
     float a[4] = {av.x, av.y, av.z, av.w};
     const int tick = tick0 + 1;
     const bool done = tick > kpm.ep_len;
@@ -871,7 +1027,7 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
 
     QS_STAMP(2);
     // ---- swarm phase: collisions + proximity (quadrotor_multi.py:537-568, 608-622) ----
-    uint64_t cur = 0;
+    Row cur{};
     float pen = 0.f;
     if (q == 0) xch_put(xch, dbase + di, d.pos, d.vel);
     lds_sync();
@@ -893,20 +1049,20 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
                 const float dx = d.pos[0] - pj[u].x, dy = d.pos[1] - pj[u].y, dz = d.pos[2] - pj[u].z;
                 const float dist = fsqrt(dx * dx + dy * dy + dz * dz);
                 const bool ok = j != di && j < kp.N;
-                cur |= (ok && dist <= kp.col_thr) ? (1ull << j) : 0ull;
+                row_set(cur, j, ok && dist <= kp.col_thr);
                 const float pterm = kpm.prox_ratio * dist + kpm.prox_max;
                 pen += (ok && dist <= kp.fall_thr) ? pterm : 0.f;   // pen >= 0: adding +0 is exact
             }
         }
-        cur = qor<Q>(cur);
+        if constexpr (Q > 1) cur = qor<Q>(cur);
         pen = qsum<Q>(pen);
     }
-    const uint64_t newpairs = cur & ~d.prev;
+    Row prow;
+    row_of(d, prow);
+    const Row newpairs = cur & ~prow;
     // setdiff1d(flat(cur), flat(prev)) and its ".any()" (drone 0 alone does not count)
-    const bool uniq = active && cur != 0 && d.prev == 0;
-    const uint64_t ub = __ballot(uniq && di != 0 && q == 0);
-    const uint64_t lmask = (LPE == 64) ? ~0ull : ((1ull << LPE) - 1ull);
-    const bool any_uniq = ((ub >> lbase) & lmask) != 0;
+    const bool uniq = active && row_any(cur) && !row_any(prow);
+    const bool any_uniq = ec.any(uniq && di != 0 && q == 0);
     rw += kpm.quadcol * ((any_uniq && uniq) ? -1.f : 0.f);
     rw += -(kp.cdt * pen);
     // room: new wall / ceiling crashes vs the previous NEW lists (:390-403, :604-605)
@@ -924,9 +1080,9 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
         d.flags = (d.flags & ~(uint32_t)QS_FL_PREV_OBST) | (ohit >= 0 ? (uint32_t)QS_FL_PREV_OBST : 0u);
     }
     bool any_onew = false;   // curr_quad_col non-empty (quadrotor_multi.py:576)
-    if (OBST) any_onew = ((__ballot(onew && q == 0) >> lbase) & lmask) != 0;
+    if (OBST) any_onew = ec.any(onew && q == 0);
     if (kp.stats) {   // episode_extra_stats counters (quadrotor_multi.py:555-566, 575-589, 599-606, 631-635)
-        auto env_count = [&](bool x) { return __popcll((__ballot(x && q == 0) >> lbase) & lmask); };
+        auto env_count = [&](bool x) { return ec.count(x && q == 0); };
         const bool settle = tick >= kp.st_settle;
         const bool cfloor = active && (d.flags & QS_FL_CRASH_FLOOR);
         const bool room_new = active && (cfloor || wall_new || ceil_new) && !(d.flags & QS_FL_PREV_ROOM);
@@ -934,7 +1090,7 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
         // every count below is zero unless one of these events happened somewhere in the wave (a new
         // collision, a first floor contact, a new wall / ceiling / room crash, a new pillar hit): one
         // wave-uniform test skips the per-env counting in the common step
-        if (__ballot(q == 0 && (uniq || cfloor || (active && (wall_new || ceil_new)) || room_new || (OBST && onew))))
+        if (ec.wany(q == 0 && (uniq || cfloor || (active && (wall_new || ceil_new)) || room_new || (OBST && onew))))
         {
         const int col = env_count(uniq) / 2;   // len(last_step_unique_collisions) // 2
         if (col > 0 && settle && uniq) d.flags |= QS_FL_HIT_AGENT;
@@ -988,7 +1144,10 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     if (kp.collide) {
         // drone-drone impulses, pairs in (i, j) order; a wave-uniform loop over pending events.
         // Ballots read sub-lane 0 of each drone (bit lbase + i * Q).
-        uint64_t pend = active ? (newpairs & ~((2ull << di) - 1ull)) : 0ull;
+        if constexpr (WIDE) {
+            impulses_wide<NPAD>(kp, rng, lds, ec, d, active ? row_above(newpairs, di) : Row{}, env, di, lane, vchanged);
+        } else {
+        uint64_t pend = active ? row_above(newpairs, di) : 0ull;
         for (;;) {
             const uint64_t bal = __ballot(pend != 0ull && q == 0);
             if (bal == 0ull) break;
@@ -1048,6 +1207,7 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
             }
             if (eb != 0 && di == istar) pend &= ~(1ull << jstar);
         }
+        }
         if (OBST && onew) {   // perform_collision_with_obstacle, drones in ascending order (:680-689)
             float z[20], u[8];
             qdraws<Q, 5, 2>(rng, gid, S_OBST, S_OBST, q, z, u);
@@ -1067,7 +1227,7 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
         }
         vchanged |= active && (wall_new || ceil_new);
     }
-    d.prev = cur;
+    row_keep(d, cur);
 
     // ---- scenario.step() (quadrotor_multi.py:700-701): new goals after the forces.  The reference's
     // observations keep the old goal unless the env's state-update flag (a downwash or impulse on any
@@ -1086,7 +1246,7 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
             scen_store(kp, b, env, sc);
         }
         lds_sync();
-        const bool upd = ((__ballot(active && vchanged) >> lbase) & lmask) != 0;
+        const bool upd = ec.any(active && vchanged);
         if (di < kp.N)
             for (int k = 0; k < 3; ++k) {
                 d.goal[k] = stab[4 * di + k];
@@ -1096,8 +1256,8 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
 
     // The drone state is final here (unless its env resets below, which stores it again): storing it now
     // lets its write-through bytes drain while the observations are computed.
-    if (kp.stats) store_drone_q<Q, true>(kp, b, g, q, active, d, stw, stmask);
-    else store_drone_q<Q>(kp, b, g, q, active, d);
+    if (kp.stats) store_drone_q<Q, true, NIW>(kp, b, g, q, active, d, stw, stmask);
+    else store_drone_q<Q, false, NIW>(kp, b, g, q, active, d);
     if (lead) {
         b.rew[g] = rw;
         b.done[g] = done ? 1 : 0;
@@ -1117,7 +1277,7 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     QS_STAMP(4);
     // ---- observations (post-impulse state; quadrotor_multi.py:704-720) ----
     const bool nbr = kp.neighbor == QS_NEIGHBOR_POS_VEL && kp.K > 0;
-    if (nbr && __ballot(vchanged)) {  // impulses changed velocities: refresh the tile
+    if (nbr && ec.wany(vchanged)) {  // impulses changed velocities: refresh the tile
         lds_sync();
         if (q == 0) xch_put(xch, dbase + di, d.pos, d.vel);
         lds_sync();
@@ -1139,7 +1299,8 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     // non-finite guard of the stepped drone and its reward (before a fused reset replaces the drone)
     const bool state_bad = lead && drone_nonfinite(d), rew_bad = lead && !(rw * 0.f == 0.f);
 
-    const uint64_t dball = __ballot(active && done);
+    // a WIDE workgroup holds one env: bit 0 = it finished
+    const uint64_t dball = WIDE ? (ec.wany(active && done) ? 1ull : 0ull) : __ballot(active && done);
     if (dball) {  // rare: some env of this block finished -> terminal obs + fused auto-reset (:739-838)
         lds_sync();
         // terminal obs: the finished envs' rows (contiguous in the tile and in HBM), all lanes of the wave;
@@ -1149,31 +1310,39 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
             if (!((dball >> (e * LPE)) & 1ull)) continue;
             float* dst = b.term + (size_t)(env0 + e) * nrow;
             const float* src = lds + (size_t)e * nrow;
-            for (int c = lane; c < nrow; c += 64) dst[c] = src[c];
+            for (int c = lane; c < nrow; c += WGS) dst[c] = src[c];
         }
         lds_sync();
         if (kp.stats) {   // the finished episode's episode_extra_stats rows (quadrotor_multi.py:739-831)
             // the env's counters from the lanes that hold them (every lane takes part in the permutes)
             float cv[NCNT];
+            if constexpr (WIDE) {   // counter k lives on lane k (the first wave): through LDS words 16.. of wscr
+                int* cx = reinterpret_cast<int*>(wscr + 8);
+                if (li < NCNT) cx[li] = cnt[0];
+                lds_sync();
 #pragma unroll
-            for (int k = 0; k < NCNT; ++k) cv[k] = (float)__shfl(cnt[k / LPE], lbase + k % LPE);
-            auto env_bits = [&](bool x) { return (__ballot(x && q == 0) >> lbase) & lmask; };
-            const uint64_t hit_a = env_bits(active && (d.flags & QS_FL_HIT_AGENT));
-            const uint64_t hit_o = env_bits(active && (d.flags & QS_FL_HIT_OBST));
-            const uint64_t reach = env_bits(active && (d.flags & QS_FL_REACHED));
-            const uint64_t all = env_bits(active);
+                for (int k = 0; k < NCNT; ++k) cv[k] = (float)cx[k];
+            } else {
+#pragma unroll
+                for (int k = 0; k < NCNT; ++k) cv[k] = (float)__shfl(cnt[k / LPE], lbase + k % LPE);
+            }
+            auto env_bits = [&](bool x) { return ec.bits(x && q == 0); };
+            const Row hit_a = env_bits(active && (d.flags & QS_FL_HIT_AGENT));
+            const Row hit_o = env_bits(active && (d.flags & QS_FL_HIT_OBST));
+            const Row reach = env_bits(active && (d.flags & QS_FL_REACHED));
+            const Row all = env_bits(active);
             if (active && done && q == 0) {
                 const float n = (float)kp.N;
-                const uint64_t ok = all & ~hit_a & ~hit_o;   // logical_and(agent_col_agent, agent_col_obst)
+                const Row ok = all & ~hit_a & ~hit_o;   // logical_and(agent_col_agent, agent_col_obst)
                 float* row = b.estats + (size_t)g * QS_NES;
                 const int E = kp.E;
 #pragma unroll
                 for (int k = 0; k < NCNT; ++k) row[QS_ES_COL + k] = cv[k];
-                row[QS_ES_SUCCESS] = (float)__popcll(ok & reach) / n;
-                row[QS_ES_DEADLOCK] = (float)__popcll(ok & ~reach) / n;
-                row[QS_ES_COLRATE] = 1.f - (float)__popcll(ok) / n;
-                row[QS_ES_NCOLRATE] = 1.f - (float)__popcll(all & ~hit_a) / n;
-                row[QS_ES_OCOLRATE] = 1.f - (float)__popcll(all & ~hit_o) / n;
+                row[QS_ES_SUCCESS] = (float)row_popc(ok & reach) / n;
+                row[QS_ES_DEADLOCK] = (float)row_popc(ok & ~reach) / n;
+                row[QS_ES_COLRATE] = 1.f - (float)row_popc(ok) / n;
+                row[QS_ES_NCOLRATE] = 1.f - (float)row_popc(all & ~hit_a) / n;
+                row[QS_ES_OCOLRATE] = 1.f - (float)row_popc(all & ~hit_o) / n;
                 row[QS_ES_SCEN] = (OBST || SCEN) ? (float)b.env[QS_E_SC_MODE * E + env] : 0.f;
                 const int T = kpm.ep_len + 1;
 #pragma unroll
@@ -1237,9 +1406,9 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
         // the reset drones' state (the stepped state was stored before the obs phase)
         if (kp.stats) {
             const float zero[STAT_WORDS] = {};
-            store_drone_q<Q, true>(kp, b, g, q, active && done, d, zero, (1u << STAT_WORDS) - 1u);
+            store_drone_q<Q, true, NIW>(kp, b, g, q, active && done, d, zero, (1u << STAT_WORDS) - 1u);
         } else {
-            store_drone_q<Q>(kp, b, g, q, active && done, d);
+            store_drone_q<Q, false, NIW>(kp, b, g, q, active && done, d);
         }
         if (nbr) {
             if (q == 0) xch_put(xch, dbase + di, d.pos, sv);
@@ -1254,7 +1423,7 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
     }
     lds_sync();
     QS_STAMP(8);
-    const int obs_bad = tile_store(lds, b.obs + (size_t)env0 * kp.N * kp.obs_dim, rows * kp.obs_dim, lane);
+    const int obs_bad = tile_store(lds, b.obs + (size_t)env0 * kp.N * kp.obs_dim, rows * kp.obs_dim, lane, WGS);
     QS_STAMP(9);
 
     if (lead) {
@@ -1284,6 +1453,7 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
         // the step's global stores above are read back by other lanes of the wave: workgroup-scope
         // release/acquire (one wave per workgroup, one L1)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (WIDE) lds_sync();   // the env's other wave has made its stores too
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         if (env < kp.E) replay_env<true>(kp, kpm, b, r, rp, seed, env, lane % LPE, LPE);
     }
@@ -1297,11 +1467,12 @@ __global__ __launch_bounds__(64) void step_kernel(const KP* __restrict__ kpp, Bu
 
 // explicit reset of masked envs (QuadrotorEnvMulti.reset quadrotor_multi.py:440-517)
 template <int NPAD, bool OBST>
-__global__ __launch_bounds__(64) void reset_kernel(const KP* __restrict__ kpp, Bufs b) {
+__global__ __launch_bounds__(NPAD > 64 ? NPAD : 64) void reset_kernel(const KP* __restrict__ kpp, Bufs b) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     QS_BIND_KP(kpp);
     const uint32_t seed = kpm.seed;
-    constexpr int EPB = 64 / NPAD;
+    constexpr int WGS = NPAD > 64 ? NPAD : 64, EPB = WGS / NPAD, SLOTS = EPB * NPAD;   // one lane per drone
+    constexpr bool WIDE = NPAD > 64;
     const int lane = threadIdx.x;
     const int el = lane / NPAD, di = lane % NPAD;
     const int env0 = blockIdx.x * EPB;
@@ -1315,13 +1486,13 @@ __global__ __launch_bounds__(64) void reset_kernel(const KP* __restrict__ kpp, B
     const Rng rng = env_rng(seed, b.env[QS_E_TICK * kp.E + eidx], episode);
     float* row = lds + (size_t)(el * kp.N + di) * kp.obs_dim;
     Drone d;
-    load_drone(kp, b, g, d);
+    load_drone<WIDE>(kp, b, g, d);
     // stale QuadrotorEnvMulti.vel: the state's vel unless a reset already happened since the last step
     const bool stale_valid = inr && (b.env[QS_E_FLAGS * kp.E + env] & 1);
     float sv[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) sv[c] = stale_valid ? b.stale[c * kp.I + g] : d.vel[c];
-    float2* otile = obst_tile(lds, kp, 64);
+    float2* otile = obst_tile(lds, kp, SLOTS);
     ObstScratch* oscr = reinterpret_cast<ObstScratch*>(otile + EPB * kp.M);
     if (OBST) {
         if (sel && di == 0) {
@@ -1336,7 +1507,7 @@ __global__ __launch_bounds__(64) void reset_kernel(const KP* __restrict__ kpp, B
         }
         lds_sync();
     }
-    float* stab = scen_tab(lds, kp, 64) + el * scen_stride<NPAD>();
+    float* stab = scen_tab(lds, kp, SLOTS) + el * scen_stride<NPAD>();
     const bool SCEN = !OBST && kp.scen_b >= 0;
     if (SCEN) {   // scenario.reset() (quadrotor_multi.py:449-459) by each selected env's lead lane
         if (sel && di == 0) {
@@ -1356,7 +1527,7 @@ __global__ __launch_bounds__(64) void reset_kernel(const KP* __restrict__ kpp, B
         self_obs(kp, d, rng, kp.id0 + (uint32_t)g, S_RESET_SENSOR, row);
     }
     if (kp.neighbor == QS_NEIGHBOR_POS_VEL && kp.K > 0) {
-        float4* xch = reinterpret_cast<float4*>(lds + 64 * kp.obs_dim);
+        float4* xch = reinterpret_cast<float4*>(lds + SLOTS * kp.obs_dim);
         xch_put(xch, lane, d.pos, sv);
         lds_sync();
         neighbor_obs<NPAD, 1>(kp, xch, base, di, 0, d.pos, sv, sel, row);
@@ -1372,11 +1543,11 @@ __global__ __launch_bounds__(64) void reset_kernel(const KP* __restrict__ kpp, B
     for (int r = 0; r < nenv_blk * kp.N; ++r) {
         const int e = env0 + r / kp.N;
         if (b.mask != nullptr && b.mask[e] == 0) continue;
-        for (int c = lane; c < kp.obs_dim; c += 64)
+        for (int c = lane; c < kp.obs_dim; c += WGS)
             b.obs[(size_t)(env0 * kp.N + r) * kp.obs_dim + c] = lds[(size_t)r * kp.obs_dim + c];
     }
     if (sel) {
-        store_drone(kp, b, g, d);
+        store_drone<WIDE>(kp, b, g, d);
 #pragma unroll
         for (int c = 0; c < 3; ++c) b.stale[c * kp.I + g] = sv[c];
         b.done[g] = 0;

@@ -131,6 +131,8 @@ static int validate(const qs_config* c) {
     if (c->num_agents < 1 || c->num_agents > QS_MAX_AGENTS)
         return fail(QS_E_UNSUPPORTED, "num_agents must be in [1, QS_MAX_AGENTS]");
     if (c->flavor != QS_FLAVOR_B && c->flavor != QS_FLAVOR_A) return fail(QS_E_INVALID, "unknown flavor");
+    if (c->num_agents > 64 && c->flavor != QS_FLAVOR_B)
+        return fail(QS_E_UNSUPPORTED, "envs of more than 64 drones (two-wave workgroups) are implemented for flavor B");
     if (c->neighbor_obs < 0 || c->neighbor_obs > QS_NEIGHBOR_NPOS) return fail(QS_E_INVALID, "unknown neighbor_obs");
     if (c->flavor == QS_FLAVOR_B) {
         if (c->obs_repr < 0 || c->obs_repr > 2) return fail(QS_E_INVALID, "obs_repr is not a flavor-B repr");
@@ -174,7 +176,7 @@ static int validate(const qs_config* c) {
     if (c->sim_steps < 1 || c->svd_every < 1 || c->ep_len < 0) return fail(QS_E_INVALID, "bad sim_steps/svd_every/ep_len");
     // The drone state is addressed by 32-bit byte offsets from the state buffer, and the step's state stores go
     // through a buffer descriptor of 0x7fffffff records (qs_rsrc): the last istate word, at most
-    // 4 (QS_NF + QS_NI) I + 255 bytes from the state base, must stay inside it (I <= 7 895 160 drones).
+    // 4 (QS_NF + QS_NI) I + 255 bytes from the state base, must stay inside it (I <= 7 669 584 drones).
     if (4ll * (QS_NF + QS_NI) * ((long long)c->num_envs * c->num_agents) + 256 > 0x7fffffffll)
         return fail(QS_E_INVALID, "too many drones: 4 (QS_NF + QS_NI) num_envs num_agents + 256 must stay below 2^31");
     return QS_OK;
@@ -484,12 +486,18 @@ extern "C" int qs_layout_query(const qs_config* c, qs_layout* out) {
 // Step launches give every drone Q lanes (qs::StepGeo for flavor B: QS_QB, qs::StepGeoA for A: QS_QA; fewer
 // when an env would not fit a wave); resets one lane.  Specialised kernels may be compiled with another Q
 // (qs_handle::qb / qa).
-static int step_lanes_per_drone(int npad, int q) { return npad * q <= 64 ? q : 64 / npad; }
-static_assert(qs::StepGeo<8>::Q == QS_QB && qs::StepGeo<32>::Q == 64 / 32 && qs::StepGeoA<8>::Q == QS_QA &&
-              qs::StepGeoA<32>::Q == 2, "step_lanes_per_drone");
+static int step_lanes_per_drone(int npad, int q) { return npad * q <= 64 ? q : (npad >= 64 ? 1 : 64 / npad); }
+static_assert(qs::StepGeo<8>::Q == QS_QB && qs::StepGeo<32>::Q == 64 / 32 && qs::StepGeo<128>::Q == 1 &&
+              qs::StepGeo<128>::WGS == 128 && qs::StepGeoA<8>::Q == QS_QA && qs::StepGeoA<32>::Q == 2,
+              "step_lanes_per_drone");
+// threads per workgroup: one wave, or (128-drone envs) the env's lanes
+static int block_threads(const qs_config& c, int npad, bool step, int qb = QS_QB, int qa = QS_QA) {
+    const int q = !step ? 1 : step_lanes_per_drone(npad, c.flavor == QS_FLAVOR_A ? qa : qb);
+    return npad * q > 64 ? npad * q : 64;
+}
 static int envs_per_block(const qs_config& c, int npad, bool step, int qb = QS_QB, int qa = QS_QA) {
     const int q = !step ? 1 : step_lanes_per_drone(npad, c.flavor == QS_FLAVOR_A ? qa : qb);
-    return 64 / (npad * q);
+    return block_threads(c, npad, step, qb, qa) / (npad * q);
 }
 
 // dynamic LDS of a launch with `slots` drone rows per workgroup: obs tile + neighbour exchange tile
@@ -609,7 +617,7 @@ static int launch(qs_handle* h, bool step, const float* act, const uint8_t* mask
     b.mask = mask;
     const qs::KP* kpd = (const qs::KP*)((char*)h->ws + h->lay.params);
     const int epb = envs_per_block(h->cfg, h->npad, step, h->qb, h->qa);
-    const dim3 grid((unsigned)((h->kp.E + epb - 1) / epb)), block(64);
+    const dim3 grid((unsigned)((h->kp.E + epb - 1) / epb)), block((unsigned)block_threads(h->cfg, h->npad, step, h->qb, h->qa));
     const size_t shm = shm_bytes(h->cfg, h->kp.obs_dim, h->npad, step, h->qb, h->qa);
     const bool a = h->cfg.flavor == QS_FLAVOR_A, ob = h->kp.obst != 0;
     // the flavor-B step kernel runs the replay wrapper in its tail (qs_replay.h); rb.ri == NULL: replay off
@@ -641,6 +649,10 @@ static int launch(qs_handle* h, bool step, const float* act, const uint8_t* mask
         QS_LAUNCH(16)
         QS_LAUNCH(32)
         QS_LAUNCH(64)
+        case 128:   // flavor B without obstacles only (validate)
+            if (step) hipLaunchKernelGGL((qs::step_kernel<128, false>), grid, block, shm, s, kpd, b, rb, rp);
+            else hipLaunchKernelGGL((qs::reset_kernel<128, false>), grid, block, shm, s, kpd, b);
+            break;
         default:
             return fail(QS_E_UNSUPPORTED, "num_agents not supported");
     }

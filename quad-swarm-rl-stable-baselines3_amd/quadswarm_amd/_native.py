@@ -9,8 +9,8 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("QUADSWARM_LIB", os.path.join(HERE, "lib", "libquadswarm.so"))
 
-ABI_VERSION = 9
-MAX_AGENTS = 64
+ABI_VERSION = 10
+MAX_AGENTS = 128
 MAX_DR_CHOICES = 8
 F, I32, U32, U64, SZ = ctypes.c_float, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_size_t
 
@@ -34,7 +34,7 @@ SCENARIO_B = {"static_same_goal": 0, "mix": 5, "static_diff_goal": 6, "ep_lissaj
 F_POS, F_VEL, F_ROT, F_OMEGA, F_ROT_DAMP, F_CMD_DAMP, F_OU, F_GOAL = 0, 3, 6, 15, 18, 22, 26, 30
 F_PID, F_ANGLE, F_ANGVEL, F_HEADING = 33, 53, 54, 55
 F_DRING, F_DSUM, NF = 56, 61, 64
-I_SVD, I_FLAGS, I_PREV_LO, I_PREV_HI, NI = 0, 1, 2, 3, 4
+I_SVD, I_FLAGS, I_PREV_LO, I_PREV_HI, I_PREV_2, I_PREV_3, NI = 0, 1, 2, 3, 4, 5, 6   # rows 4, 5: 128-drone envs
 FL_ON_FLOOR, FL_PREV_WALL, FL_PREV_CEIL, FL_CRASH_FLOOR, FL_CRASH_WALL, FL_CRASH_CEIL = 1, 2, 4, 8, 16, 32
 FL_PREV_OBST = 64
 FL_PREV_ROOM, FL_HIT_AGENT, FL_HIT_OBST, FL_REACHED = 128, 256, 512, 1024

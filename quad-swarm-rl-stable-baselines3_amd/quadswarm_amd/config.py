@@ -275,6 +275,8 @@ class QuadSwarmConfig:
             raise ValueError("replay_buffer_sample_prob must be in [0, 1]")
         if not 1 <= self.num_agents <= N.MAX_AGENTS:
             raise ValueError(f"num_agents must be in [1, {N.MAX_AGENTS}]")
+        if self.num_agents > 64 and self.flavor != "B":   # qs_step.hip validate: two-wave envs are flavor B
+            raise ValueError("envs of more than 64 drones are implemented for flavor B (quad_swarm_rl's env)")
         k = self.k_neighbors
         if self.neighbor_obs_type != "none" and self.num_agents > 1 and not 1 <= k <= self.num_agents - 1:
             raise ValueError("neighbor_visible_num out of range")

@@ -115,6 +115,10 @@ STAT_ENV_FIELDS = ["st_col", "st_room", "st_floor", "st_wall", "st_ceil", "st_co
                    "st_ocol_settle", "st_o35", "st_o5"]
 
 
+# istate words of a drone's previous-collision row (bit j = partner j), least significant first
+PREV_WORDS = (NAT.I_PREV_LO, NAT.I_PREV_HI, NAT.I_PREV_2, NAT.I_PREV_3)
+
+
 def gpu_to_oracle(env, oenv):
     """Copy the GPU env state (fp32 SoA) into the oracle's drones/envs (fp64)."""
     st = env.state.double().cpu().numpy()
@@ -156,10 +160,12 @@ def gpu_to_oracle(env, oenv):
         stale_valid = bool(es[NAT.E_FLAGS, e] & 1)
         for i in range(N):
             g = e * N + i
-            prev = int(np.uint32(ist[NAT.I_PREV_LO, g])) | (int(np.uint32(ist[NAT.I_PREV_HI, g])) << 32)
+            prev = 0
+            for w, f in enumerate(PREV_WORDS):
+                prev |= int(np.uint32(ist[f, g])) << (32 * w)
             for j in range(N):
                 if j > i:
-                    ev.prev_pair_bits[i * 64 + j] = (prev >> j) & 1
+                    ev.prev_pair_bits[i * O.MAXN + j] = (prev >> j) & 1
             for c in range(3):
                 ev.obs_vel[i][c] = stale[c, g] if stale_valid else st[3 + c, g]
                 ev.obs_pos[i][c] = st[c, g]
@@ -204,10 +210,10 @@ def oracle_to_gpu(oenv, env):
             prev = 0
             for j in range(N):
                 a, b = min(i, j), max(i, j)
-                if i != j and ev.prev_pair_bits[a * 64 + b]:
+                if i != j and ev.prev_pair_bits[a * O.MAXN + b]:
                     prev |= 1 << j
-            ist[NAT.I_PREV_LO, g] = np.int64(prev & 0xFFFFFFFF).astype(np.uint32).view(np.int32)
-            ist[NAT.I_PREV_HI, g] = np.int64(prev >> 32).astype(np.uint32).view(np.int32)
+            for w, f in enumerate(PREV_WORDS):   # the 64 (128-drone envs: 128) bits of the row, 32 per word
+                ist[f, g] = np.int64((prev >> (32 * w)) & 0xFFFFFFFF).astype(np.uint32).view(np.int32)
             stale[:, g] = ev.obs_vel[i][:]
     env.state.copy_(torch.from_numpy(st))
     env.istate.copy_(torch.from_numpy(ist.astype(np.uint32).view(np.int32)))

@@ -56,7 +56,8 @@ def test_config_default_matches_host_derivation():
 
 @pytest.mark.parametrize("N_,K,repr_,od", [(8, 6, "xyz_vxyz_R_omega", 54), (1, 0, "xyz_vxyz_R_omega", 18),
                                           (8, 2, "xyz_vxyz_R_omega_floor", 31), (32, 6, "xyz_vxyz_R_omega", 54),
-                                          (8, -1, "xyz_vxyz_R_omega_wall", 66)])
+                                          (8, -1, "xyz_vxyz_R_omega_wall", 66), (128, 6, "xyz_vxyz_R_omega", 54),
+                                          (128, 16, "xyz_vxyz_R_omega", 114)])
 def test_layout(N_, K, repr_, od):
     cfg = QuadSwarmConfig(num_envs=100, num_agents=N_, neighbor_visible_num=K, obs_repr=repr_,
                           neighbor_obs_type="pos_vel" if N_ > 1 else "none")
@@ -79,8 +80,16 @@ def test_validation_errors_are_reported():
     assert L.qs_layout_query(bad, lay) == -1
     assert b"k_neighbors" in L.qs_last_error()
     bad = N.QsConfig.from_buffer_copy(c)
-    bad.num_agents = 65
+    bad.num_agents = 129
     assert L.qs_layout_query(bad, lay) == -2
+    # envs of 65..128 drones (two-wave workgroups) are flavor B only; their obs tile must fit the LDS
+    a = N.QsConfig.from_buffer_copy(QuadSwarmConfig.sb_train(num_envs=4, num_agents=8).to_qs_config())
+    a.num_agents = 65
+    assert L.qs_layout_query(a, lay) == -2 and b"flavor B" in L.qs_last_error()
+    with pytest.raises(ValueError):
+        QuadSwarmConfig.sb_train(num_envs=2, num_agents=128).to_qs_config()
+    wide = N.QsConfig.from_buffer_copy(QuadSwarmConfig(num_envs=4, num_agents=128, neighbor_visible_num=127).to_qs_config())
+    assert L.qs_layout_query(wide, lay) == -2 and b"LDS" in L.qs_last_error()
     # the state / istate byte offsets (32-bit, 2 GB buffer descriptor) bound the drone count: the largest
     # accepted shard still addresses its last istate word inside the descriptor, one more drone is refused
     limit = (0x7fffffff - 256) // (4 * (N.NF + N.NI))

@@ -67,7 +67,7 @@ def eventful_rows(oenv, floor_before, done):
     N = oenv.N
     ev = np.array(done, bool).copy()
     for e in range(oenv.E):
-        bits = np.frombuffer(bytes(oenv.envs[e].prev_pair_bits), np.uint8).reshape(64, 64)[:N, :N]
+        bits = np.frombuffer(bytes(oenv.envs[e].prev_pair_bits), np.uint8).reshape(O.MAXN, O.MAXN)[:N, :N]
         hit = (bits | bits.T).any(1)
         for i in range(N):
             d = oenv.drones[e * N + i]

@@ -163,9 +163,9 @@ def test_collide_wall_ceiling(golden):
             close(np.concatenate([O.get_arr(d.vel), O.get_arr(d.omega)]), g[f"{kind}_out"][c], 1e-10, 1e-11)
 
 
-@pytest.mark.parametrize("n,k", [(8, 6), (8, 2), (8, 7), (32, 6), (64, 6), (64, 63)])
+@pytest.mark.parametrize("n,k", [(8, 6), (8, 2), (8, 7), (32, 6), (64, 6), (64, 63), (128, 6), (128, 16)])
 def test_neighbor_obs(golden, n, k):
-    g = golden("neighbors64" if n == 64 else "neighbors")
+    g = golden({64: "neighbors64", 128: "neighbors128"}.get(n, "neighbors"))
     p = O.default_params(num_agents=n, k_neighbors=k)
     od = 18 + 6 * k
     for c in range(len(g[f"n{n}k{k}_pos"])):
@@ -204,7 +204,7 @@ def load_traj_env(golden, name):
 
 
 @pytest.mark.parametrize("name", ["n8k6", "n8k7", "n1", "n8dw", "n32k6", "n8quiet", "n8wall", "n4wallquiet", "n8stats",
-                                  "n64k6"])
+                                  "n64k6", "n128k6"])
 def test_trajectory_tape_replay(golden, name):
     g, p, drones, envs = load_traj_env(golden, name)
     n = p.num_agents
@@ -228,7 +228,7 @@ def test_trajectory_tape_replay(golden, name):
     assert tape.r.tape_pos == len(g["tape"])
     assert tape.r.spawn_pos == len(g["spawn"])
     close(np.stack([O.get_arr(drones[i].pos) for i in range(n)]), g["final_pos"], RTOL_TRAJ, ATOL_TRAJ)
-    if name in ("n8k6", "n8k7", "n1", "n32k6", "n8wall", "n8stats", "n64k6"):
+    if name in ("n8k6", "n8k7", "n1", "n32k6", "n8wall", "n8stats", "n64k6", "n128k6"):
         assert n_done >= 1   # the auto-reset path was exercised
     if name == "n8wall":     # the wall features saw contacts: clipped at 0 and at 5
         w = g["obs"][:, :, 18:24]

@@ -483,6 +483,8 @@ def main_extra(which):
              contacts and a noise-free 4-drone hover the GPU replays
       stats  episode_extra_stats of every finished episode (quadrotor_multi.py:739-831) over 2-s episodes
       n64    a 64-drone crowded trajectory and 64-drone neighbour selections (k = 6 and all 63 visible)
+      n128   a 128-drone crowded trajectory with an in-env auto-reset and 128-drone neighbour selections (k = 6, 16;
+             the paper's largest swarm, paper/fps_compare.py:7)
       info   every agent's per-step infos["rewards"] dict (quadrotor_single.py:79-105, quadrotor_multi.py:642-651)
              over a crowded 8-drone run with an in-env auto-reset"""
     os.makedirs(OUT, exist_ok=True)
@@ -497,6 +499,9 @@ def main_extra(which):
     if "n64" in which:   # 64-drone swarms: the first size past one drone per lane of a wave with Q > 1
         gen_traj("n64k6", 64, 6, 25, ep_time=0.2, seed=20, setup=setup_crowd)
         gen_neighbors_sizes("neighbors64.npz", [(64, 6), (64, 63)], seed=6, count=10)
+    if "n128" in which:  # 128-drone swarms: an env spans two waves (a 128-lane workgroup)
+        gen_traj("n128k6", 128, 6, 14, ep_time=0.1, seed=22, setup=setup_crowd)
+        gen_neighbors_sizes("neighbors128.npz", [(128, 6), (128, 16)], seed=7, count=6)
 
 
 if __name__ == "__main__":

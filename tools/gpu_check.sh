@@ -134,6 +134,13 @@ for s in "$@"; do
       CONFIG=c5 STEPS=2000 step sel2_ab 600 bash tools/ab_jit.sh base: sel2:-DQS_NBR_SELECT2=1 base2: sel2b:-DQS_NBR_SELECT2=1
       ;;
     stamps) step stamps 300 python tools/phase_stamps.py ;;
+    n128) step gpu_tests_n128 900 python -u -m pytest tests/test_gpu_n128.py -x -v --timeout 300 --timeout-method thread ;;
+    benchn128) step bench_n128 300 python bench.py --config n128 --steps 500 --cpu-seconds 5 --e2e-iters 0 ;;
+    prioab)    # the younger-wave priority flip (QS_PRIO_AT, default 11) against off, per config
+      for c in c3 c4 c3mix c5 c2; do
+        CONFIG=$c STEPS=1000 step prioab_$c 300 bash tools/ab_jit.sh on: off:-DQS_PRIO_AT=-1 on2: off2:-DQS_PRIO_AT=-1
+      done
+      ;;
     calib)
       export TMPDIR=/tmp
       step calib_fetch 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/calib_fetch -o cf --output-format csv -- ./tools/calib/fetch_calib

@@ -80,6 +80,11 @@ def main():
         line = ", ".join(f"{c} waves: {np.sum(cnt == c)} {name}s (wave end p50 {np.median(e_[per == c]):.0f} ns, "
                          f"max {e_[per == c].max():.0f})" for c in np.unique(cnt))
         print(f"waves per {name} ({len(u)} {name}s used): {line}")
+    slot = hw & 0xF
+    print("wave end by wave slot (ns): " + ", ".join(
+        f"slot {s}: {np.sum(slot == s)} waves, start p50 {np.median(s_[slot == s]):.0f}, end p50 "
+        f"{np.median(e_[slot == s]):.0f} p99 {np.percentile(e_[slot == s], 99):.0f} max {e_[slot == s].max():.0f}"
+        for s in np.unique(slot)))
     print("wave end by XCD (ns): " + ", ".join(f"{x}: p50 {np.median(e_[xcc == x]):.0f} max {e_[xcc == x].max():.0f}"
                                               for x in np.unique(xcc)))
     slow = np.argsort(e_)[-max(1, nb // 100):]
