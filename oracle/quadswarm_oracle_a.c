@@ -649,16 +649,16 @@ void or_env_step_a(const or_params* p, or_drone* drones, or_env* envs, int e, co
          * False, :203), only the episode_extra_stats bookkeeping */
         {
             int in_cur[64] = {0}, in_prev[64] = {0}, wall_new[64], ceil_new[64];
-            unsigned char cur[64 * 64];
+            unsigned char cur[OR_MAXN * OR_MAXN];   /* the env's pair-bit layout (stride OR_MAXN) */
             memset(cur, 0, sizeof cur);
             for (int i = 0; i < N; ++i)
                 for (int j = i + 1; j < N; ++j) {
                     const double dx = dr[i].pos[0] - dr[j].pos[0], dy = dr[i].pos[1] - dr[j].pos[1];
                     const double dz = dr[i].pos[2] - dr[j].pos[2];
                     if (sqrt(dx * dx + dy * dy + dz * dz) <= p->collision_threshold) {
-                        cur[i * 64 + j] = 1; in_cur[i] = in_cur[j] = 1;
+                        cur[i * OR_MAXN + j] = 1; in_cur[i] = in_cur[j] = 1;
                     }
-                    if (ev->prev_pair_bits[i * 64 + j]) in_prev[i] = in_prev[j] = 1;
+                    if (ev->prev_pair_bits[i * OR_MAXN + j]) in_prev[i] = in_prev[j] = 1;
                 }
             memcpy(ev->prev_pair_bits, cur, sizeof cur);
             for (int i = 0; i < N; ++i) {   /* calculate_room_collision (:491-504): new wall / ceiling lists */
