@@ -1460,7 +1460,7 @@ __global__ __launch_bounds__(StepGeo<NPAD>::WGS) void step_kernel(const KP* __re
     QS_STAMP(11);
     // slots 16 / 17: drones of the wave on the floor / in a drone collision this step
     QS_STAMP_NOTE(16, __builtin_popcountll(__ballot(active && q == 0 && (d.flags & QS_FL_ON_FLOOR))));
-    QS_STAMP_NOTE(17, __builtin_popcountll(__ballot(active && q == 0 && cur != 0)));
+    QS_STAMP_NOTE(17, __builtin_popcountll(__ballot(active && q == 0 && row_any(cur))));
     QS_RTSTAMP(13);
     QS_STAMP_FLUSH();
 }
