@@ -145,11 +145,11 @@ __device__ void neighbor_obs(const KP& kp, const float4* xch, int dbase, int di,
             for (int c = 0; c < 6; ++c) rel[KEEP ? t : 0][c] = r[c];
         }
     }
-    float allk_[Q == 1 ? 1 : PJ * Q];   // key of candidate m = q' + Q t' (sub-lane q', slot t')
-    float* allk = Q == 1 ? key : allk_;
+    float allk_[Q == 1 || NPAD >= 64 ? 1 : PJ * Q];   // key of candidate m = q' + Q t' (sub-lane q', slot t')
+    float* allk = Q == 1 || NPAD >= 64 ? key : allk_;
 #pragma unroll
     for (int t = 0; t < PJ; ++t) {
-        if constexpr (Q == 1) {
+        if constexpr (Q == 1 || NPAD >= 64) {   // (the K-pass selection below needs no gathered keys)
         } else if constexpr (Q == 2) {
             allk[2 * t] = qbc<2, 0>(key[t]);
             allk[2 * t + 1] = qbc<2, 1>(key[t]);
@@ -163,13 +163,14 @@ __device__ void neighbor_obs(const KP& kp, const float4* xch, int dbase, int di,
     if (!write) return;
     const float vm = 2.f * kp.vxyz_max;
     const bool pairs = ((kp.so_dim | kp.obs_dim) & 1) == 0;   // 8-byte aligned slots: ds_write_b64
-    if constexpr (Q == 1 && NPAD >= 64) {
-        // 128-drone envs always take this path (k = N - 1 keys are all 0: the passes pick index order, as the
-        // ranking does); their 128 x 128 ranking is not compiled
-        if (NPAD > 64 || (sorted && kp.K <= 16)) {
-            // one lane per drone, many candidates, few neighbours: K passes of a (key, index) minimum above
-            // the previous pick instead of ranking every candidate against all the others -- the same
-            // strict (key, index) order, so the same neighbours in the same slots
+    if constexpr (NPAD >= 64) {
+        // 128-drone envs and the sub-lane (multi-wave) envs always take this path (k = N - 1 keys are all 0: the
+        // passes pick index order, as the ranking does); their ranking is not compiled
+        if (NPAD > 64 || Q > 1 || (sorted && kp.K <= 16)) {
+            // many candidates, few neighbours: K passes of a (key, index) minimum above the previous pick instead
+            // of ranking every candidate against all the others -- the same strict (key, index) order, so the
+            // same neighbours in the same slots.  With 2 sub-lanes each scans its candidates j = q + 2 m and the
+            // pair's two minima meet by one DPP swap.
             float pk = -1.f;
             int pjx = -1;
             for (int r = 0; r < kp.K; ++r) {
@@ -177,13 +178,20 @@ __device__ void neighbor_obs(const KP& kp, const float4* xch, int dbase, int di,
                 int bj = NPAD;
 #pragma unroll
                 for (int m = 0; m < PJ; ++m) {
-                    const bool above = key[m] > pk || (key[m] == pk && m > pjx);
-                    const bool below = key[m] < bk;   // m ascending: the first of equal keys wins
-                    if (above && below) { bk = key[m]; bj = m; }
+                    const int j = q + Q * m;
+                    const bool above = key[m] > pk || (key[m] == pk && j > pjx);
+                    const bool below = key[m] < bk;   // j ascending: the first of equal keys wins
+                    if (above && below) { bk = key[m]; bj = j; }
+                }
+                if constexpr (Q == 2) {
+                    const float ok = dpp_f<quad_perm(1, 0, 3, 2)>(bk);
+                    const int oj = dpp_i<quad_perm(1, 0, 3, 2)>(bj);
+                    if (ok < bk || (ok == bk && oj < bj)) { bk = ok; bj = oj; }
                 }
                 if (bk == __builtin_inff()) break;
                 pk = bk;
                 pjx = bj;
+                if (Q > 1 && q != 0) continue;   // the pair's first sub-lane writes the slot
                 const float4 pj = xch[2 * (dbase + bj)], vj = xch[2 * (dbase + bj) + 1];
                 const float o0 = clampf(pj.x - P[0], -kp.room_range[0], kp.room_range[0]);
                 const float o1 = clampf(pj.y - P[1], -kp.room_range[1], kp.room_range[1]);
@@ -196,7 +204,7 @@ __device__ void neighbor_obs(const KP& kp, const float4* xch, int dbase, int di,
             return;
         }
     }
-    if constexpr (NPAD <= 64) {
+    if constexpr (NPAD < 64 || (NPAD == 64 && Q == 1)) {
 #pragma unroll
     for (int t = 0; t < PJ; ++t) {
         const int j = q + Q * t;
@@ -726,15 +734,21 @@ __device__ __forceinline__ void store_drone_q(const KP& kp, const Bufs& b, int g
 #ifndef QS_QB
 #define QS_QB 4
 #endif
+// Sub-lanes per drone of an env that spans several waves (64- and 128-drone envs): with 2, a 512-env
+// 64-drone shard or a 256-env 128-drone shard is 1024 waves, one per SIMD.
+#ifndef QS_QW
+#define QS_QW 2
+#endif
 template <int NPAD>
 struct StepGeo {
-    static constexpr int Q = NPAD * QS_QB <= 64 ? QS_QB : (NPAD >= 64 ? 1 : 64 / NPAD);
-    static constexpr int LPE = NPAD * Q;           // lanes per env
-    static constexpr int WGS = LPE > 64 ? LPE : 64; // threads per workgroup: one wave, or the env's two waves
+    static constexpr int Q = NPAD * QS_QB <= 64 ? QS_QB : (NPAD >= 64 ? QS_QW : 64 / NPAD);
+    static constexpr int LPE = NPAD * Q;            // lanes per env
+    static constexpr int WGS = LPE > 64 ? LPE : 64; // threads per workgroup: one wave, or the env's waves
     static constexpr int EPB = WGS / LPE;           // envs per workgroup
     static constexpr int SLOTS = EPB * NPAD;        // drone slots per workgroup
-    static constexpr bool WIDE = NPAD > 64;         // the env spans the workgroup's waves (128-drone envs)
-    static constexpr int NIW = WIDE ? 6 : 4;        // istate words per drone (WordsOf)
+    static constexpr bool WIDE = LPE > 64;          // the env spans the workgroup's waves (64 / 128 drones)
+    static constexpr bool ROW2 = NPAD > 64;         // 128-bit collision rows (128-drone envs)
+    static constexpr int NIW = ROW2 ? 6 : 4;        // istate words per drone (WordsOf)
 };
 
 // ---- collision rows: bit j = partner drone j; 64 bits, or two words for the 128-drone envs ----
@@ -769,32 +783,51 @@ __device__ __forceinline__ uint64_t row_above(uint64_t r, int di) { return r & ~
 __device__ __forceinline__ Row128 row_above(Row128 r, int di) {
     return di < 64 ? Row128{r.lo & ~((2ull << di) - 1ull), r.hi} : Row128{0ull, r.hi & ~((2ull << (di - 64)) - 1ull)};
 }
+template <int Q>
+__device__ __forceinline__ Row128 qor(Row128 r) { return Row128{qor<Q>(r.lo), qor<Q>(r.hi)}; }
 __device__ __forceinline__ void row_of(const Drone& d, uint64_t& r) { r = d.prev; }
 __device__ __forceinline__ void row_of(const Drone& d, Row128& r) { r = Row128{d.prev, d.prevx}; }
 __device__ __forceinline__ void row_keep(Drone& d, uint64_t r) { d.prev = r; }
 __device__ __forceinline__ void row_keep(Drone& d, Row128 r) { d.prev = r.lo; d.prevx = r.hi; }
 
+// the drones' bits of a wave ballot with Q = 2 sub-lanes per drone: bit i = lane 2i or 2i + 1 (32 bits)
+__device__ __forceinline__ uint64_t compact_pairs(uint64_t b) {
+    uint64_t x = (b | (b >> 1)) & 0x5555555555555555ull;
+    x = (x | (x >> 1)) & 0x3333333333333333ull;
+    x = (x | (x >> 2)) & 0x0F0F0F0F0F0F0F0Full;
+    x = (x | (x >> 4)) & 0x00FF00FF00FF00FFull;
+    x = (x | (x >> 8)) & 0x0000FFFF0000FFFFull;
+    return (x | (x >> 16)) & 0x00000000FFFFFFFFull;
+}
+
 // Env-level collectives of the step kernel over a predicate of the env's lanes (callers pass x && q == 0 to
-// count drones).  An env inside one wave: a ballot of the env's lane segment (drone i at bit i Q).  A 128-drone
-// env (WIDE, Q = 1): each wave's ballot through a 2-word LDS slot and a workgroup barrier; the slots alternate
-// so that one barrier per collective suffices.  Every lane of the workgroup must make the same calls.
-template <bool WIDE>
+// count drones).  An env inside one wave: a ballot of the env's lane segment (drone i at bit i Q).  An env that
+// spans the workgroup's NW waves (WIDE: 64 drones x 2 sub-lanes, 128 drones x 1 or 2): each wave's ballot,
+// reduced to its drones (bit i = drone i of the env), through an LDS slot and a workgroup barrier; the slots
+// alternate so that one barrier per collective suffices.  Every lane of the workgroup must make the same calls.
+template <bool WIDE, bool ROW2 = false, int Q = 1, int NW = 1>
 struct EnvColl {
-    using Row = typename RowOf<WIDE>::T;
+    using Row = typename RowOf<ROW2>::T;
     int lbase;
     uint64_t lmask;
-    uint64_t* scr;   // WIDE: 4 words of LDS
+    uint64_t* scr;   // WIDE: 2 NW words of LDS
     int slot;
     __device__ __forceinline__ Row bits(bool x) {
         if constexpr (!WIDE) {
             return (__ballot(x) >> lbase) & lmask;
         } else {
-            const uint64_t bw = __ballot(x);
-            uint64_t* s = scr + 2 * slot;
+            static_assert(Q == 1 || Q == 2, "sub-lanes of a multi-wave env");
+            constexpr int DPW = 64 / Q;   // drones per wave
+            const uint64_t bw = Q == 2 ? compact_pairs(__ballot(x)) : __ballot(x);
+            uint64_t* s = scr + NW * slot;
             slot ^= 1;
             if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = bw;
             lds_sync();
-            return Row128{s[0], s[1]};
+            uint64_t w[2] = {0ull, 0ull};
+#pragma unroll
+            for (int k = 0; k < NW; ++k) w[(k * DPW) >> 6] |= s[k] << ((k * DPW) & 63);
+            if constexpr (ROW2) return Row128{w[0], w[1]};
+            else return w[0];
         }
     }
     __device__ __forceinline__ bool any(bool x) { return row_any(bits(x)); }
@@ -807,24 +840,26 @@ struct EnvColl {
 };
 
 
-// Drone-drone impulses of a 128-drone env (its two waves): the new pairs in the reference's (i, j) order, one
+// Drone-drone impulses of an env that spans several waves: the new pairs in the reference's (i, j) order, one
 // event per round.  Every drone posts its pos / vel / omega and its first pending partner to LDS tables (in the
 // obs tile, unused until the obs phase), a collective finds the first drone i with a pending pair, lanes 0..8
-// draw the pair's 9 Philox blocks (7 normal, 2 uniform), and the pair's two lanes apply collide_pair --
-// the same draws and arithmetic as the one-wave loop of step_kernel.
-template <int NPAD>
-__device__ __forceinline__ void impulses_wide(const KP& kp, const Rng& rng, float* lds, EnvColl<true>& ec, Drone& d,
-                                              Row128 pend, int env, int di, int lane, bool& vchanged) {
+// draw the pair's 9 Philox blocks (7 normal, 2 uniform), and the pair's lanes apply collide_pair -- the same
+// draws and arithmetic as the one-wave loop of step_kernel.
+template <int NPAD, class EC, class Row>
+__device__ __forceinline__ void impulses_wide(const KP& kp, const Rng& rng, float* lds, EC& ec, Drone& d,
+                                              Row pend, int env, int di, int q, int lane, bool& vchanged) {
     float4* pscr = reinterpret_cast<float4*>(lds);       // the pair's 9 blocks
     float4* tab = pscr + 16;                              // per drone: {pos}, {vel}, {omega}
     int* jt = reinterpret_cast<int*>(tab + 3 * NPAD);     // per drone: first pending partner, -1 = none
     for (;;) {
-        tab[3 * di] = make_float4(d.pos[0], d.pos[1], d.pos[2], 0.f);
-        tab[3 * di + 1] = make_float4(d.vel[0], d.vel[1], d.vel[2], 0.f);
-        tab[3 * di + 2] = make_float4(d.om[0], d.om[1], d.om[2], 0.f);
         const bool has = row_any(pend);
-        jt[di] = has ? row_ffs(pend) : -1;
-        const Row128 bal = ec.bits(has);   // its barrier also orders the table writes
+        if (q == 0) {
+            tab[3 * di] = make_float4(d.pos[0], d.pos[1], d.pos[2], 0.f);
+            tab[3 * di + 1] = make_float4(d.vel[0], d.vel[1], d.vel[2], 0.f);
+            tab[3 * di + 2] = make_float4(d.om[0], d.om[1], d.om[2], 0.f);
+            jt[di] = has ? row_ffs(pend) : -1;
+        }
+        const Row bal = ec.bits(has);   // its barrier also orders the table writes
         if (!row_any(bal)) break;
         const int istar = row_ffs(bal), jstar = jt[istar];
         const bool involved = di == istar || di == jstar;
@@ -876,7 +911,7 @@ __global__ __launch_bounds__(StepGeo<NPAD>::WGS) void step_kernel(const KP* __re
     constexpr int Q = G::Q, LPE = G::LPE, EPB = G::EPB, SLOTS = G::SLOTS, WGS = G::WGS, NIW = G::NIW;
     constexpr bool WIDE = G::WIDE;
     constexpr int LW = WordsOf<NIW>::LW, DW = WordsOf<NIW>::DW;
-    using Row = typename RowOf<WIDE>::T;
+    using Row = typename RowOf<G::ROW2>::T;
     const int lane = threadIdx.x;
     const int el = lane / LPE, di = (lane % LPE) / Q, q = lane % Q;
     const int env0 = xcd_block((int)blockIdx.x, (int)gridDim.x) * EPB;
@@ -894,7 +929,7 @@ __global__ __launch_bounds__(StepGeo<NPAD>::WGS) void step_kernel(const KP* __re
     const uint64_t lmask = (LPE >= 64) ? ~0ull : ((1ull << LPE) - 1ull);
     // env-level collectives; WIDE: their LDS slots and the env counters' exchange in the 64 words after xch
     uint64_t* wscr = reinterpret_cast<uint64_t*>(lds + SLOTS * kp.obs_dim + SLOTS * 8);
-    EnvColl<WIDE> ec{lbase, lmask, wscr, 0};
+    EnvColl<WIDE, G::ROW2, Q, WGS / 64> ec{lbase, lmask, wscr, 0};
     float2* otile = obst_tile(lds, kp, SLOTS);
     ObstScratch* oscr = reinterpret_cast<ObstScratch*>(otile + EPB * kp.M);
     const float2* myob = otile + el * kp.M;
@@ -1145,7 +1180,7 @@ __global__ __launch_bounds__(StepGeo<NPAD>::WGS) void step_kernel(const KP* __re
         // drone-drone impulses, pairs in (i, j) order; a wave-uniform loop over pending events.
         // Ballots read sub-lane 0 of each drone (bit lbase + i * Q).
         if constexpr (WIDE) {
-            impulses_wide<NPAD>(kp, rng, lds, ec, d, active ? row_above(newpairs, di) : Row{}, env, di, lane, vchanged);
+            impulses_wide<NPAD>(kp, rng, lds, ec, d, active ? row_above(newpairs, di) : Row{}, env, di, q, lane, vchanged);
         } else {
         uint64_t pend = active ? row_above(newpairs, di) : 0ull;
         for (;;) {

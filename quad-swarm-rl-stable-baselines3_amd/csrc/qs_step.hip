@@ -486,17 +486,21 @@ extern "C" int qs_layout_query(const qs_config* c, qs_layout* out) {
 // Step launches give every drone Q lanes (qs::StepGeo for flavor B: QS_QB, qs::StepGeoA for A: QS_QA; fewer
 // when an env would not fit a wave); resets one lane.  Specialised kernels may be compiled with another Q
 // (qs_handle::qb / qa).
-static int step_lanes_per_drone(int npad, int q) { return npad * q <= 64 ? q : (npad >= 64 ? 1 : 64 / npad); }
-static_assert(qs::StepGeo<8>::Q == QS_QB && qs::StepGeo<32>::Q == 64 / 32 && qs::StepGeo<128>::Q == 1 &&
-              qs::StepGeo<128>::WGS == 128 && qs::StepGeoA<8>::Q == QS_QA && qs::StepGeoA<32>::Q == 2,
-              "step_lanes_per_drone");
+// flavor B (qs::StepGeo): QS_QW sub-lanes for the multi-wave 64 / 128-drone envs; flavor A (qs::StepGeoA): an
+// env stays inside one wave
+static int step_lanes_per_drone(int npad, int q, bool flavor_a = false) {
+    return npad * q <= 64 ? q : (npad >= 64 && !flavor_a ? QS_QW : 64 / npad);
+}
+static_assert(qs::StepGeo<8>::Q == QS_QB && qs::StepGeo<32>::Q == 64 / 32 && qs::StepGeo<64>::Q == QS_QW &&
+              qs::StepGeo<128>::Q == QS_QW && qs::StepGeo<128>::WGS == 128 * QS_QW && qs::StepGeoA<8>::Q == QS_QA &&
+              qs::StepGeoA<32>::Q == 2 && qs::StepGeoA<64>::Q == 1, "step_lanes_per_drone");
 // threads per workgroup: one wave, or (128-drone envs) the env's lanes
 static int block_threads(const qs_config& c, int npad, bool step, int qb = QS_QB, int qa = QS_QA) {
-    const int q = !step ? 1 : step_lanes_per_drone(npad, c.flavor == QS_FLAVOR_A ? qa : qb);
+    const int q = !step ? 1 : step_lanes_per_drone(npad, c.flavor == QS_FLAVOR_A ? qa : qb, c.flavor == QS_FLAVOR_A);
     return npad * q > 64 ? npad * q : 64;
 }
 static int envs_per_block(const qs_config& c, int npad, bool step, int qb = QS_QB, int qa = QS_QA) {
-    const int q = !step ? 1 : step_lanes_per_drone(npad, c.flavor == QS_FLAVOR_A ? qa : qb);
+    const int q = !step ? 1 : step_lanes_per_drone(npad, c.flavor == QS_FLAVOR_A ? qa : qb, c.flavor == QS_FLAVOR_A);
     return block_threads(c, npad, step, qb, qa) / (npad * q);
 }
 

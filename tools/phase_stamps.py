@@ -46,8 +46,8 @@ def main():
     L.qs_debug_stamps_h.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
     npad = 1 << (cfg.num_agents - 1).bit_length()
     qd = 2 if cfg.flavor == "A" else 4
-    q = qd if npad * qd <= 64 else 64 // npad
-    epb = 64 // (npad * q)
+    q = qd if npad * qd <= 64 else (2 if npad >= 64 and cfg.flavor == "B" else 64 // npad)   # StepGeo / StepGeoA
+    epb = max(64, npad * q) // (npad * q)
     nb = min((cfg.num_envs + epb - 1) // epb, 65536)
     NS = 32   # slots per block (QS_NSTAMP)
     buf = np.zeros(65536 * NS, np.uint64)
