@@ -486,7 +486,9 @@ __device__ __forceinline__ void col_row16(const KP& kp, const Drone& d, int di, 
         const float dx = d.pos[0] - dpp_f<C>(d.pos[0]), dy = d.pos[1] - dpp_f<C>(d.pos[1]);
         const float dz = d.pos[2] - dpp_f<C>(d.pos[2]);
         const int j = dpp_i<C>(di);
-        if (j < kp.N && dx * dx + dy * dy + dz * dz <= thr2) cur |= 1ull << j;
+        // non-short-circuit: a select, not a branch per partner
+        const bool hit = (j < kp.N) & (dx * dx + dy * dy + dz * dz <= thr2);
+        cur |= hit ? (1ull << j) : 0ull;
         col_row16<Q, K + 1>(kp, d, di, thr2, cur);
     }
 }
@@ -501,7 +503,8 @@ __device__ __forceinline__ void col_row16_q2(const KP& kp, const Drone& d, int d
         const float dx = d.pos[0] - dpp_f<C>(d.pos[0]), dy = d.pos[1] - dpp_f<C>(d.pos[1]);
         const float dz = d.pos[2] - dpp_f<C>(d.pos[2]);
         const int j = dpp_i<C>(di);
-        if (j != di && j < kp.N && dx * dx + dy * dy + dz * dz <= thr2) cur |= 1ull << j;
+        const bool hit = (j != di) & (j < kp.N) & (dx * dx + dy * dy + dz * dz <= thr2);   // a select, not a branch
+        cur |= hit ? (1ull << j) : 0ull;
         col_row16_q2<K + 1>(kp, d, di, thr2, cur);
     }
 }
@@ -668,7 +671,8 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
                     const int j = q + Q * t;
                     const float4 pj = xch[2 * (sbase + (j < NPAD ? j : NPAD - 1))];
                     const float dx = d.pos[0] - pj.x, dy = d.pos[1] - pj.y, dz = d.pos[2] - pj.z;
-                    if (j != di && j < kp.N && dx * dx + dy * dy + dz * dz <= thr2) cur |= 1ull << j;
+                    const bool hit = (j != di) & (j < kp.N) & (dx * dx + dy * dy + dz * dz <= thr2);
+                    cur |= hit ? (1ull << j) : 0ull;
                 }
                 cur = qor<Q>(cur);
                 lds_sync();   // the tile is rewritten next tick
