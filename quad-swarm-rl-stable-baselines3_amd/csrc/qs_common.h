@@ -612,8 +612,15 @@ __device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\
 // exchanged through DPP quad permutes (a VALU modifier: no LDS round trip).  Every helper below
 // must be called with all Q lanes of the drone active (quad-uniform control flow).
 // ---------------------------------------------------------------------------------------------
+// QS_DPP_BC: bound_ctrl on (an out-of-range / disabled source lane reads 0 -- the same value as the old = 0
+// form, so bitwise the same results) lets the compiler fold the permute into its consumer (v_sub_f32_dpp ...)
+// more often: C3 7.74 -> 7.64 us; the specialised flavor-A kernels keep it off (a8 25.63 vs 25.74 us,
+// profiles/ab/r03_dpp_bc_ab.txt; qs_step.hip jit_compile)
+#ifndef QS_DPP_BC
+#define QS_DPP_BC 1
+#endif
 template <int CTRL>
-__device__ __forceinline__ int dpp_i(int x) { return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xF, 0xF, false); }
+__device__ __forceinline__ int dpp_i(int x) { return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xF, 0xF, QS_DPP_BC != 0); }
 template <int CTRL>
 __device__ __forceinline__ float dpp_f(float x) { return __int_as_float(dpp_i<CTRL>(__float_as_int(x))); }
 constexpr int quad_perm(int a, int b, int c, int d) { return a | (b << 2) | (c << 4) | (d << 6); }

@@ -1172,6 +1172,7 @@ static int jit_compile(const qs_config* c, const qs::KP& kp, int npad, int qb, i
     opts.push_back("-mllvm");
     opts.push_back("-amdgpu-sched-strategy=max-ilp");
     if (c->flavor != QS_FLAVOR_A) opts.push_back("-fno-slp-vectorize");
+    if (c->flavor == QS_FLAVOR_A) opts.push_back("-DQS_DPP_BC=0");   // qs_common.h dpp_i (measured per flavor)
     // QS_JIT_OPTS: extra space-separated hipRTC options (kernel-variant experiments, e.g. -DQS_X=1)
     std::vector<std::string> extra = jit_extra_opts();
     for (const std::string& o : extra) opts.push_back(o.c_str());
