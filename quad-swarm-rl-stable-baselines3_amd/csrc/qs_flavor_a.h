@@ -116,7 +116,8 @@ __device__ __forceinline__ void controller(const KP& kp, const Drone& d, Ctl& c,
     y0 *= iyn; y1 *= iyn; y2 *= iyn;
     const float* R = d.rot;
     const float tf = fmaxf(fd0 * R[2] + fd1 * R[5] + fd2 * R[8], 0.f);
-    const float thr = clampf((fsqrt(tf / kp.m_kf4) - kp.m_min_rpm) * kp.m_inv_rpm, 0.f, 1.f);
+    // tf / kf4 as a product with the (constant-folded) reciprocal: ~1 ulp, no IEEE division in the tick loop
+    const float thr = clampf((fsqrt(tf * frcp(kp.m_kf4)) - kp.m_min_rpm) * kp.m_inv_rpm, 0.f, 1.f);
     // AttitudeController (AttitudeController.py:60-82): e = vee(0.5 (Rd^T R - R^T Rd)); M = Rd^T R
     const float Rd0[3] = {x0, x1, x2}, Rd1[3] = {y0, y1, y2}, Rd2[3] = {n0, n1, n2};
     auto M = [&](const float* col, int j) { return col[0] * R[j] + col[1] * R[3 + j] + col[2] * R[6 + j]; };
@@ -417,15 +418,16 @@ __device__ __forceinline__ float seg_sum(float v) {
 // and the arena edge, speed <= v_max.  Every lane of the env computes the same update.
 template <int NPAD, int Q = 1>
 __device__ __forceinline__ void target_step(const KP& kp, float& tx, float& ty, const float* pos, bool contrib) {
+    // the quotients as products with hardware reciprocals (~1 ulp; five IEEE divisions per tick otherwise)
     const float r0 = tx - pos[0], r1 = ty - pos[1];
-    const float d2 = r0 * r0 + r1 * r1;
-    const float fx = seg_sum<NPAD, Q>(contrib ? r0 / d2 : 0.f);
-    const float fy = seg_sum<NPAD, Q>(contrib ? r1 / d2 : 0.f);
+    const float id2 = frcp(r0 * r0 + r1 * r1);
+    const float fx = seg_sum<NPAD, Q>(contrib ? r0 * id2 : 0.f);
+    const float fy = seg_sum<NPAD, Q>(contrib ? r1 * id2 : 0.f);
     const float de = fsqrt(tx * tx + ty * ty);
-    const float den = de * fmaxf(kp.arena - de, 0.1f);
-    const float vx = fx - tx / den, vy = fy - ty / den;
+    const float iden = frcp(de * fmaxf(kp.arena - de, 0.1f));
+    const float vx = fx - tx * iden, vy = fy - ty * iden;
     const float vs = fsqrt(vx * vx + vy * vy);
-    const float sc = fminf(vs, kp.tgt_vmax) / vs * kp.tgt_dt;
+    const float sc = fminf(vs, kp.tgt_vmax) * frcp(vs) * kp.tgt_dt;
     tx = tx + vx * sc;
     ty = ty + vy * sc;
 }
