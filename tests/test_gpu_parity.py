@@ -157,7 +157,12 @@ def test_free_run_matches_oracle():
 
 
 def test_reference_quiet_trajectory(golden):
-    """Noise-free reference trajectory (tests/golden/traj_n8quiet.npz, 300 steps) replayed on the GPU."""
+    """Noise-free reference trajectory (tests/golden/traj_n8quiet.npz, 300 steps) replayed on the GPU.
+
+    SURVEY §8c's long-horizon bound is position error <= 1e-3 m after 100 control ticks; the divergence curve
+    (tools/divergence_curve.py, profiles/r03_divergence_curve.txt) measures 8.0e-6 m at tick 100 and 2.2e-5 m at
+    most over the 178 airborne ticks, self obs 6.0e-5: the bounds below are 1e-4 m (and 2e-5 m up to tick 100),
+    3e-4 on the self obs."""
     g = golden("traj_n8quiet")
     n = int(g["n"])
     cfg = QuadSwarmConfig(num_envs=1, num_agents=n, neighbor_visible_num=int(g["k"]), sense_noise=None,
@@ -178,8 +183,8 @@ def test_reference_quiet_trajectory(golden):
         want = g["obs"][t]
         airborne &= (want[:, 2] + 2.0) > 0.3
         m = airborne
-        np.testing.assert_allclose(o[m, 0:3], want[m, 0:3], atol=2e-3, err_msg=f"step {t}")
-        np.testing.assert_allclose(o[m, :18], want[m, :18], atol=2e-2, err_msg=f"step {t}")
+        np.testing.assert_allclose(o[m, 0:3], want[m, 0:3], atol=2e-5 if t < 100 else 1e-4, err_msg=f"step {t}")
+        np.testing.assert_allclose(o[m, :18], want[m, :18], atol=3e-4, err_msg=f"step {t}")
         np.testing.assert_allclose(np_(rew)[m], g["rew"][t][m], atol=2e-4, err_msg=f"step {t}")
         if m.all():
             assert_neighbors_close(o[:, 18:], want[:, 18:], atol=2e-2)
@@ -207,9 +212,9 @@ def test_reference_wall_trajectory(golden):
         assert not done.any() and np.isfinite(o).all()
         want = g["obs"][t]
         airborne &= (want[:, 2] + 2.0) > 0.3
-        m = airborne
-        np.testing.assert_allclose(o[m, 0:3], want[m, 0:3], atol=2e-3, err_msg=f"step {t}")
-        np.testing.assert_allclose(o[m, :24], want[m, :24], atol=2e-2, err_msg=f"step {t}")
+        m = airborne   # divergence curve: 1.1e-5 m at most, self obs 3.6e-5 (profiles/r03_divergence_curve.txt)
+        np.testing.assert_allclose(o[m, 0:3], want[m, 0:3], atol=1e-4, err_msg=f"step {t}")
+        np.testing.assert_allclose(o[m, :24], want[m, :24], atol=3e-4, err_msg=f"step {t}")
         # the wall block is the room distances of the position, clipped to [0, 5] (get_state.py:282-287)
         np.testing.assert_allclose(o[m, 18:24], want[m, 18:24], atol=2e-3, err_msg=f"step {t} walls")
         np.testing.assert_allclose(np_(rew)[m], g["rew"][t][m], atol=2e-4, err_msg=f"step {t}")
