@@ -572,13 +572,13 @@ __device__ __forceinline__ void substep_tail(const KP& kp, Drone& d, const Torqu
             fl |= QS_FL_ON_FLOOR | QS_FL_CRASH_FLOOR;
 #pragma unroll
             for (int i = 0; i < 3; ++i) { d.vel[i] = 0.f; d.om[i] = 0.f; }
-            float theta = atan2f(R[3], R[0] + 1e-6f);
-            if (R[8] < 0.f) {
+            if (R[8] < 0.f) {   // upside down: a random yaw
                 uint32_t gid_ = gid;   // opaque: keeps the Philox key schedule out of the common path
                 asm volatile("" : "+v"(gid_));
-                theta = -3.14159265358979f + 6.28318530717959f * uniform1(rng, gid_, S_FLOOR | ((uint32_t)s << 8), 0);
+                yaw_rot(-3.14159265358979f + 6.28318530717959f * uniform1(rng, gid_, S_FLOOR | ((uint32_t)s << 8), 0), R);
+            } else {            // yaw_rot(arctan2(R10, R00 + EPS)) as normalised components, like the resting case
+                yaw_rot_xy(R[0] + 1e-6f, R[3], R);
             }
-            yaw_rot(theta, R);
 #pragma unroll
             for (int k = 0; k < 4; ++k) { d.cd[k] = 0.f; d.rd[k] = 0.f; }
         }
