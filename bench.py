@@ -346,10 +346,9 @@ class Blocks:
                 raise RuntimeError(f"hipGraphUpload failed ({rc})")
         self.torch.cuda.synchronize(self.dev)
 
-    def timed(self, n, stream):
-        """n steps bracketed by HIP events on `stream` (the blocks' streams join it on both sides; one
-        handle runs on `stream` itself, so no cross-stream waits sit in the timed region)"""
-        ev0, ev1 = self.torch.cuda.Event(enable_timing=True), self.torch.cuda.Event(enable_timing=True)
+    def timed(self, n, stream, ev0, ev1):
+        """n steps bracketed by HIP events (created by the caller) on `stream` (the blocks' streams join it on
+        both sides; one handle runs on `stream` itself, so no cross-stream waits sit in the timed region)"""
         joins = [st for _, _, st in self.entries if st is not stream]
         ev0.record(stream)
         for st in joins:
@@ -407,10 +406,15 @@ def main():
     ap.add_argument("--e2e-steps", type=int, default=0, help="override the PPO rollout length n_steps")
     ap.add_argument("--e2e-unfused", action="store_true",
                     help="A/B only: the rollout evaluates the torch policy module instead of the fused encoders")
+    ap.add_argument("--host-sync", choices=["spin", "auto"], default="auto",
+                    help="host wait of torch.cuda.synchronize(): spin (hipDeviceScheduleSpin) or HIP's default")
     args = ap.parse_args()
     if args.cpu_worker:
         return cpu_worker(args.config, args.cpu_seconds)
 
+    if args.host_sync == "spin":   # before anything creates the device's context
+        if ctypes.CDLL("libamdhip64.so").hipSetDeviceFlags(ctypes.c_uint(1)) != 0:   # hipDeviceScheduleSpin
+            raise RuntimeError("hipSetDeviceFlags(hipDeviceScheduleSpin) failed")
     import torch
     import torch.distributed as dist
 
@@ -474,7 +478,8 @@ def main():
         torch.cuda.synchronize(dev)
         times = {}
         for name, cand in (("one_handle", one), ("blocks", blocks)):
-            ev = cand.timed(2 * n_ab, stream)
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            cand.timed(2 * n_ab, stream, *ev)
             torch.cuda.synchronize(dev)
             times[name] = ev[0].elapsed_time(ev[1]) * 1e3 / (2 * n_ab)
         if world > 1:   # every rank takes the same decision (rank 0's measurement)
@@ -500,8 +505,9 @@ def main():
     # torch's current stream, or to the block streams that join it), bracketing the timed region: back to
     # back step kernels, so the average step time = span / K (rocprofv3 --kernel-trace, one handle, agrees)
     replays0, eager0 = run.replays, run.eager_steps
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    ev0, ev1 = run.timed(args.steps, stream)
+    run.timed(args.steps, stream, ev0, ev1)
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
     k_ms = ev0.elapsed_time(ev1) / args.steps
