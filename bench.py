@@ -346,9 +346,12 @@ class Blocks:
                 raise RuntimeError(f"hipGraphUpload failed ({rc})")
         self.torch.cuda.synchronize(self.dev)
 
-    def timed(self, n, stream, ev0, ev1):
-        """n steps bracketed by HIP events (created by the caller) on `stream` (the blocks' streams join it on
-        both sides; one handle runs on `stream` itself, so no cross-stream waits sit in the timed region)"""
+    def timed(self, n, stream, ev0=None, ev1=None):
+        """n steps bracketed by HIP events (best created by the caller, outside any timed region) on `stream`
+        (the blocks' streams join it on both sides; one handle runs on `stream` itself, so no cross-stream
+        waits sit in the timed region)"""
+        if ev0 is None:
+            ev0, ev1 = self.torch.cuda.Event(enable_timing=True), self.torch.cuda.Event(enable_timing=True)
         joins = [st for _, _, st in self.entries if st is not stream]
         ev0.record(stream)
         for st in joins:

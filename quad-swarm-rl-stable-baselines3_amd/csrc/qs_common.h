@@ -371,9 +371,9 @@ __device__ __forceinline__ void yaw_rot_xy(float x, float y, float* R) {
         const float r = __builtin_amdgcn_rsqf(h2);
         c = x * r;
         s = y * r;
-    } else {
-        c = __builtin_copysignf(1.f, x);
-        s = __builtin_copysignf(0.f, y);
+    } else {   // h2 == 0, or NaN: arctan2 of a NaN is NaN, and so are its cos / sin (the state stays non-finite)
+        c = h2 == 0.f ? __builtin_copysignf(1.f, x) : h2;
+        s = h2 == 0.f ? __builtin_copysignf(0.f, y) : h2;
     }
     R[0] = c; R[1] = -s; R[2] = 0.f;
     R[3] = s; R[4] = c; R[5] = 0.f;
