@@ -4,6 +4,9 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
 
+`python bench.py --gpus N` (N > 1) with no launcher around starts the second form itself as a child process
+(before any HIP call) and relays rank 0's line; under a launcher WORLD_SIZE must equal --gpus (else exit 1).
+
 A "step" = one QuadrotorEnvMulti.step of every env on the GPU (qs_step: physics x2 substeps,
 collisions, proximity, impulses, neighbour top-k, sensor noise, obs, rewards, fused auto-reset),
 actions read from a fixed device buffer of U(-1,1) draws (seed 1234), state resident in HBM.
@@ -21,6 +24,7 @@ import argparse
 import ctypes
 import json
 import os
+import socket
 import subprocess
 import sys
 import time
@@ -165,7 +169,7 @@ def npad(n):
 
 def pmc_traffic(config):
     """HBM bytes per launch measured by rocprofv3 --pmc (profiles/pmc_<config>.json, written by
-    tools/profile_pmc.py from separate FETCH_SIZE / WRITE_SIZE passes with the gfx950 correction)."""
+    tools/summarize_prof.py from separate FETCH_SIZE / WRITE_SIZE passes with the gfx950 correction)."""
     p = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
     if not os.path.exists(p):
         return None
@@ -388,7 +392,65 @@ def raw_streams(torch, dev, n, spare):
     return streams, destroy
 
 
-def main():
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launcher_argv(argv, gpus, port):
+    """The N-rank launch of this bench (one process per GPU, rendezvous on 127.0.0.1): what the driver runs for
+    N > 1, started by `python bench.py --gpus N` itself when no launcher is around.  Replaces the reference's
+    process-parallel envs (swarm_rl/env_wrappers/subproc_vec_env_custom.py:118-134) at GPU granularity."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def launch_ranks(argv, gpus):
+    """Run the N ranks as a child process (nothing here has touched the GPU yet, so no exec), relay rank 0's
+    JSON line as this process's last stdout line and return the child's exit code."""
+    r = subprocess.run(launcher_argv(argv, gpus, free_port()), stdout=subprocess.PIPE, text=True)
+    lines = r.stdout.splitlines()
+    js = [ln for ln in lines if ln.startswith("{")]
+    for ln in lines:
+        if ln not in js:
+            print(ln, file=sys.stderr, flush=True)
+    for ln in js:
+        print(ln, flush=True)
+    return r.returncode
+
+
+def launch_world(gpus, environ=None):
+    """World size the bench runs at, checked against --gpus: under a launcher WORLD_SIZE must equal --gpus
+    (a mismatch exits non-zero instead of reporting a line for a different GPU count)."""
+    environ = os.environ if environ is None else environ
+    if gpus < 1:
+        raise SystemExit(f"bench.py: --gpus must be >= 1 (got {gpus})")
+    world = int(environ.get("WORLD_SIZE", "1"))
+    if world != gpus:
+        raise SystemExit(f"bench.py: --gpus {gpus} but the launcher started {world} rank(s)")
+    return world
+
+
+def aggregate_ranks(agent_steps, seconds, world, device=None):
+    """Weak-scaling aggregate: (sum of every rank's agent-steps, max-over-ranks seconds, per-rank agent-steps/s).
+    One all_gather of two fp64 words per rank (RCCL on the GPU ranks, gloo in the CPU tests)."""
+    if world == 1:
+        return float(agent_steps), float(seconds), [float(agent_steps) / float(seconds)]
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([float(agent_steps), float(seconds)], dtype=torch.float64, device=device)
+    parts = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(parts, t)
+    rows = torch.stack(parts).cpu()
+    return (float(rows[:, 0].sum()), float(rows[:, 1].max()),
+            [float(a / s) for a, s in rows.tolist()])
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2000)
@@ -411,9 +473,13 @@ def main():
                     help="A/B only: the rollout evaluates the torch policy module instead of the fused encoders")
     ap.add_argument("--host-sync", choices=["spin", "auto"], default="auto",
                     help="host wait of torch.cuda.synchronize(): spin (hipDeviceScheduleSpin) or HIP's default")
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
     if args.cpu_worker:
         return cpu_worker(args.config, args.cpu_seconds)
+    # --gpus N without a launcher: start the N ranks as a child (before any HIP call in this process)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(launch_ranks(argv, args.gpus))
+    world = launch_world(args.gpus)
 
     if args.host_sync == "spin":   # before anything creates the device's context
         if ctypes.CDLL("libamdhip64.so").hipSetDeviceFlags(ctypes.c_uint(1)) != 0:   # hipDeviceScheduleSpin
@@ -421,13 +487,14 @@ def main():
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     use_dist = world > 1 or os.environ.get("QS_BENCH_DIST") == "1"   # QS_BENCH_DIST: RCCL path at N=1 (rehearsal)
     if use_dist:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but the process group has {dist.get_world_size()} ranks")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -517,9 +584,7 @@ def main():
     timed_replays, timed_eager = run.replays - replays0, run.eager_steps - eager0
     if world > 1:
         dist.barrier()
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    total_agent_steps, el, per_rank = aggregate_ranks(I * args.steps, el, world, dev)
 
     # secondary: one eager launch of the one handle bracketed by its own events (includes the host launch gap)
     nk = min(200, max(20, args.steps // 10))
@@ -544,7 +609,7 @@ def main():
             e2e = {"error": repr(e)}
 
     if rank == 0:
-        value = world * I * args.steps / el
+        value = total_agent_steps / el
         bpa = algorithmic_bytes_per_agent_step(cfg.obs_dim, cfg.num_agents, cfg.flavor,
                                                cfg.num_obstacles if cfg.use_obstacles else 0)
         achieved = bpa * I / (k_ms * 1e-3) / 1e9
@@ -563,6 +628,8 @@ def main():
             "value": round(value, 1),
             "unit": "agent-steps/s",
             "n_gpus": world,
+            "per_rank_agent_steps_per_s": [round(v, 1) for v in per_rank],
+            "rccl_world_size": dist.get_world_size() if use_dist else None,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(el * 1e3 / args.steps, 5),
@@ -614,4 +681,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -1,0 +1,100 @@
+"""bench.py's multi-GPU entry on CPU: `--gpus N` starts N ranks through torch.distributed.run (argv checked,
+the launch itself stubbed), a WORLD_SIZE / --gpus mismatch exits non-zero before touching a device, and the
+line's aggregate (sum of the ranks' agent-steps / max-over-ranks seconds) is right at world size 2 (gloo)."""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def test_launcher_argv():
+    argv = bench.launcher_argv(["--gpus", "8", "--steps", "20", "--warmup", "5"], 8, 29511)
+    assert argv[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nnodes=1" in argv and "--nproc-per-node=8" in argv
+    assert "--master-addr=127.0.0.1" in argv and "--master-port=29511" in argv
+    i = argv.index(os.path.join(ROOT, "bench.py"))
+    assert argv[i + 1:] == ["--gpus", "8", "--steps", "20", "--warmup", "5"]
+
+
+def test_gpus_n_without_launcher_starts_ranks(monkeypatch):
+    seen = {}
+
+    class R:
+        returncode = 3
+        stdout = 'rank noise\n{"metric": "m", "n_gpus": 4}\n'
+
+    def fake_run(cmd, **kw):
+        seen["cmd"] = cmd
+        return R()
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(bench.subprocess, "run", fake_run)
+    with pytest.raises(SystemExit) as ex:
+        bench.main(["--gpus", "4", "--steps", "7"])
+    assert ex.value.code == 3                       # the child's exit code
+    cmd = seen["cmd"]
+    assert "--nproc-per-node=4" in cmd and cmd[-4:] == ["--gpus", "4", "--steps", "7"]
+
+
+@pytest.mark.parametrize("world,gpus", [("2", "4"), ("4", "1"), ("1", "2")])
+def test_world_gpus_mismatch_exits_nonzero(world, gpus):
+    env = dict(os.environ, WORLD_SIZE=world, RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", gpus], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0
+    assert f"--gpus {gpus} but the launcher started {world} rank" in r.stderr
+    assert r.stdout.strip() == ""
+
+
+def test_launch_world_checks():
+    assert bench.launch_world(1, {}) == 1
+    assert bench.launch_world(8, {"WORLD_SIZE": "8"}) == 8
+    with pytest.raises(SystemExit):
+        bench.launch_world(0, {})
+    with pytest.raises(SystemExit):
+        bench.launch_world(2, {"WORLD_SIZE": "1"})
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _agg_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sys.path.insert(0, ROOT)
+    import bench as b
+    # rank r processed (r + 1) * 1000 agent-steps in (r + 2) seconds
+    out = b.aggregate_ranks((rank + 1) * 1000, float(rank + 2), world, device="cpu")
+    q.put((rank, out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_aggregate_sum_over_max():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_agg_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in (0, 1):
+        total, tmax, per_rank = got[r]
+        assert total == 3000.0 and tmax == 3.0      # every rank sees the same aggregate
+        assert per_rank == [500.0, 2000.0 / 3.0]
+    assert bench.aggregate_ranks(500, 2.0, 1) == (500.0, 2.0, [250.0])
