@@ -16,6 +16,7 @@
  *   - qs_set_param("capture_radius") replaces set_capture_radius         quadrotor_multi_rewards.py:212-213
  *   - qs_set_param replaces rew_coeff updates          swarm_rl/env_wrappers/reward_shaping.py:70-76,110-118
  *   - qs_get_state/qs_set_state: env snapshot/restore (no reference equivalent; checkpoint + parity)
+ *   - qs_curriculum_step replaces CurriculumCallback._on_step          swarm_rl/custom_callbacks.py:441-468
  * The Python mirror of the reference's VecEnv surface (quadswarm_amd.vec_env.GpuQuadVecEnv) calls
  * these through ctypes; INTEGRATION.md shows the binding.
  *
@@ -36,7 +37,7 @@
 extern "C" {
 #endif
 
-#define QS_ABI_VERSION 10
+#define QS_ABI_VERSION 11
 #define QS_MAX_AGENTS 128           /* drones per env: up to 64 inside one 64-lane wavefront, 128 = a two-wave
                                        workgroup per env (flavor B without obstacles; paper/fps_compare.py:7) */
 #define QS_MAX_DR_CHOICES 8         /* entries per obstacle domain-randomisation list */
@@ -468,6 +469,32 @@ typedef struct qs_attn_tower {
 int qs_attn_embed(const float* d_obs, int32_t obs_stride, int32_t self_dim, int32_t nbr_off, int32_t B, int32_t K,
                   int32_t nd, int32_t H, const qs_attn_tower* towers, int32_t n_towers, void* stream);
 int qs_attn_pool(int32_t B, int32_t K, int32_t H, const qs_attn_tower* towers, int32_t n_towers, void* stream);
+
+/* sb_train's capture-radius curriculum on the device (ABI 11; replaces CurriculumCallback._on_step,
+ * swarm_rl/custom_callbacks.py:441-468, which SB3 runs after every VecEnv step).  Flavor A.  The callback's state
+ * is a qs_curriculum in DEVICE memory; qs_curriculum_step, enqueued after a qs_step, records the outcome of every
+ * env that step reset (buffers.reset_info, env order) into the window, re-evaluates the success rate when any env
+ * was reset and, when it exceeds sr_threshold, multiplies the radius by decay, writes it to every env's
+ * env_f[QS_ENVF_CAPTURE] row (set_capture_radius) and clears the window.  Nothing is read back: the host copies
+ * the struct when it wants to log or checkpoint (n_shrinks / history name the reference's curriculum
+ * checkpoints).  fp64 arithmetic like the reference's numpy / Python floats. */
+#define QS_CUR_MAX_WINDOW 64
+#define QS_CUR_MAX_HIST 64
+typedef struct qs_curriculum {
+    double radius;                  /* current_capture_radius (initial_capture_radius at the start)      */
+    double success_rate;            /* sucess_rate: the window mean at the last step that reset an env    */
+    double sr_threshold;            /* cfg.capture_radius_sr                                              */
+    double decay;                   /* cfg.capture_radius_decay                                           */
+    int64_t window_i;               /* window_i: outcomes recorded so far                                 */
+    int32_t window;                 /* window_size (40 in the reference), 1..QS_CUR_MAX_WINDOW            */
+    int32_t n_shrinks;              /* radius reductions so far                                           */
+    double past[QS_CUR_MAX_WINDOW]; /* past_successes (first `window` entries)                            */
+    double history[QS_CUR_MAX_HIST];/* radius after reduction k, at k % QS_CUR_MAX_HIST                   */
+} qs_curriculum;
+/* Fill a host struct with the reference's initial values (window cleared); copy it to device memory yourself. */
+int qs_curriculum_init(qs_curriculum* host, double initial_radius, double sr_threshold, double decay, int32_t window);
+/* One curriculum update for the step just enqueued on `stream` (d_cur: device qs_curriculum). */
+int qs_curriculum_step(qs_handle* h, qs_curriculum* d_cur, void* stream);
 
 #ifdef __cplusplus
 }

@@ -37,6 +37,7 @@
 #include "qs_flavor_b.h"
 #include "qs_flavor_a.h"
 #include "qs_gae.h"
+#include "qs_curriculum.h"
 #include "qs_policy.h"
 #include "qs_replay.h"
 
@@ -984,6 +985,32 @@ extern "C" int qs_gae(const float* rewards, const float* values, const uint8_t* 
     return QS_OK;
 }
 
+// capture-radius curriculum (qs_curriculum.h)
+extern "C" int qs_curriculum_init(qs_curriculum* c, double initial_radius, double sr_threshold, double decay,
+                                  int32_t window) {
+    if (!c) return fail(QS_E_INVALID, "NULL argument");
+    if (window < 1 || window > QS_CUR_MAX_WINDOW) return fail(QS_E_INVALID, "curriculum window must be 1..64");
+    if (!(initial_radius > 0.0) || !(decay > 0.0)) return fail(QS_E_INVALID, "radius and decay must be > 0");
+    memset(c, 0, sizeof *c);
+    c->radius = initial_radius;
+    c->sr_threshold = sr_threshold;
+    c->decay = decay;
+    c->window = window;
+    return QS_OK;
+}
+
+extern "C" int qs_curriculum_step(qs_handle* h, qs_curriculum* d_cur, void* stream) {
+    if (!h || !d_cur) return fail(QS_E_INVALID, "NULL argument");
+    if (h->cfg.flavor != QS_FLAVOR_A) return fail(QS_E_INVALID, "the capture-radius curriculum is flavor A");
+    QS_HIP(use_device(h));
+    const uint8_t* ri = (const uint8_t*)((char*)h->ws + h->lay.reset_info);
+    float* cap = (float*)((char*)h->ws + h->lay.env_f) + (size_t)QS_ENVF_CAPTURE * (size_t)h->cfg.num_envs;
+    hipLaunchKernelGGL(qs::curriculum_kernel, dim3(1), dim3(qs::QS_CUR_THREADS), 0, (hipStream_t)stream, ri, cap,
+                       (int)h->cfg.num_envs, d_cur);
+    QS_HIP(hipGetLastError());
+    return QS_OK;
+}
+
 // fused attention-encoder forward (qs_policy.h)
 static int attn_check(int32_t B, int32_t K, int32_t H, const qs_attn_tower* towers, int32_t n_towers) {
     if (!towers) return fail(QS_E_INVALID, "NULL towers");
@@ -1137,7 +1164,7 @@ static int jit_compile(const qs_config* c, const qs::KP& kp, int npad, int qb, i
         "typedef __hip_internal::int64_t int64_t;\n"
         "typedef unsigned long uintptr_t;\n"
         "#define QS_JIT 1\n#define QS_QB " + std::to_string(qb) + "\n#define QS_QA " + std::to_string(qa) +
-        "\n#define QS_KP_WORDS " + kp_words(kp) + "\n";
+        "\n#define QS_QW " + std::to_string(QS_QW) + "\n#define QS_KP_WORDS " + kp_words(kp) + "\n";
     src += c->flavor == QS_FLAVOR_A ? "#include \"qs_flavor_a.h\"\n" : "#include \"qs_flavor_b.h\"\n";
     // the kernel sources embedded at build time, or (QS_JIT_SRC_DIR, kernel-variant A/B experiments) the same
     // header names read from that directory
@@ -1173,8 +1200,15 @@ static int jit_compile(const qs_config* c, const qs::KP& kp, int npad, int qb, i
     opts.push_back("-amdgpu-sched-strategy=max-ilp");
     if (c->flavor != QS_FLAVOR_A) opts.push_back("-fno-slp-vectorize");
     if (c->flavor == QS_FLAVOR_A) opts.push_back("-DQS_DPP_BC=0");   // qs_common.h dpp_i (measured per flavor)
-    // QS_JIT_OPTS: extra space-separated hipRTC options (kernel-variant experiments, e.g. -DQS_X=1)
+    // QS_JIT_OPTS: extra space-separated hipRTC options (kernel-variant experiments, e.g. -DQS_X=1).  The launch
+    // geometry (sub-lanes per drone) is the host's: block_threads / envs_per_block size the launch from it, so a
+    // kernel compiled with another QS_QB / QS_QA / QS_QW would index envs and LDS differently -- refused here.
     std::vector<std::string> extra = jit_extra_opts();
+    for (const std::string& o : extra)
+        for (const char* geo : {"QS_QB", "QS_QA", "QS_QW", "QS_JIT", "QS_KP_WORDS"})
+            if (o.find(geo) != std::string::npos)
+                return fail(QS_E_INVALID, std::string("QS_JIT_OPTS may not set ") + geo +
+                                              " (launch geometry comes from the host; use the QS_QB / QS_QA env vars)");
     for (const std::string& o : extra) opts.push_back(o.c_str());
     const hiprtcResult rc = hiprtcCompileProgram(prog, (int)opts.size(), opts.data());
     if (rc != HIPRTC_SUCCESS) {

@@ -9,7 +9,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("QUADSWARM_LIB", os.path.join(HERE, "lib", "libquadswarm.so"))
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 MAX_AGENTS = 128
 MAX_DR_CHOICES = 8
 F, I32, U32, U64, SZ = ctypes.c_float, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_size_t
@@ -127,6 +127,16 @@ class QsAttnTower(ctypes.Structure):
                [("b_a3", F), ("out", ctypes.c_void_p)]
 
 
+CUR_MAX_WINDOW = CUR_MAX_HIST = 64
+
+
+class QsCurriculum(ctypes.Structure):
+    """qs_curriculum (the device-side CurriculumCallback state, quadswarm.h)."""
+    _fields_ = [("radius", ctypes.c_double), ("success_rate", ctypes.c_double), ("sr_threshold", ctypes.c_double),
+                ("decay", ctypes.c_double), ("window_i", ctypes.c_int64), ("window", I32), ("n_shrinks", I32),
+                ("past", ctypes.c_double * CUR_MAX_WINDOW), ("history", ctypes.c_double * CUR_MAX_HIST)]
+
+
 class QuadSwarmError(RuntimeError):
     pass
 
@@ -139,7 +149,7 @@ EXPORTS = ["qs_abi_version", "qs_last_error", "qs_struct_sizes", "qs_config_defa
            "qs_get_param", "qs_state_bytes", "qs_get_state", "qs_set_state", "qs_gae",
            "qs_specialize", "qs_is_specialized", "qs_config_kp_words", "qs_specialize_compile",
            "qs_replay_config_default", "qs_replay_workspace_bytes", "qs_replay_enable", "qs_replay_disable", "qs_replay_buffers_get",
-           "qs_attn_embed", "qs_attn_pool"]
+           "qs_attn_embed", "qs_attn_pool", "qs_curriculum_init", "qs_curriculum_step"]
 
 _lib = None
 
@@ -176,6 +186,8 @@ def lib():
         "qs_replay_buffers_get": ([V, P(QsReplayBuffers)], I32),
         "qs_attn_embed": ([V, I32, I32, I32, I32, I32, I32, I32, P(QsAttnTower), I32, V], I32),
         "qs_attn_pool": ([I32, I32, I32, P(QsAttnTower), I32, V], I32),
+        "qs_curriculum_init": ([V, ctypes.c_double, ctypes.c_double, ctypes.c_double, I32], I32),
+        "qs_curriculum_step": ([V, V, V], I32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -260,6 +260,37 @@ class SwarmActorCritic(nn.Module):
     def predict(self, obs, deterministic=True):
         return torch.tanh(self.action_net(self.actor_latent(obs))) if deterministic else self.forward(obs)[0]
 
+    # ---- checkpoints interchangeable with the reference's policy ----
+    # The reference's module tree differs only in two wrapper levels: ModelCoreMLP keeps its layers in `.core`
+    # (ActorCriticPolicyCustom.py:260-276) and MlpDecoder in `.mlp` (sample_factory); every other parameter
+    # name (encoders, attention MLPs, feed_forward, action_net, log_std, value_net) is the same.
+    _REF_WRAP = (("actor_core.", "actor_core.core."), ("critic_core.", "critic_core.core."),
+                 ("actor_decoder.", "actor_decoder.mlp."), ("critic_decoder.", "critic_decoder.mlp."))
+
+    @classmethod
+    def reference_key(cls, key):
+        """This module's parameter name -> ActorCriticPolicyCustomSeparateWeights' name for it."""
+        for ours, ref in cls._REF_WRAP:
+            if key.startswith(ours):
+                return ref + key[len(ours):]
+        return key
+
+    @classmethod
+    def from_reference_key(cls, key):
+        for ours, ref in cls._REF_WRAP:
+            if key.startswith(ref):
+                return ours + key[len(ref):]
+        return key
+
+    def reference_state_dict(self):
+        """state_dict under the reference policy's names (loadable by ActorCriticPolicyCustomSeparateWeights)."""
+        return {self.reference_key(k): v for k, v in self.state_dict().items()}
+
+    def load_reference_state_dict(self, sd, strict=True):
+        """Load a state_dict of the reference's ActorCriticPolicyCustomSeparateWeights (e.g. the `policy` entry
+        of an SB3 checkpoint of sb_train) -- same architecture, same function."""
+        return self.load_state_dict({self.from_reference_key(k): v for k, v in sd.items()}, strict=strict)
+
 
 _LOG_SQRT_2PI = 0.5 * math.log(2 * math.pi)
 
@@ -427,6 +458,9 @@ class PPOTrainer:
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(seed)
         self.num_timesteps = 0
+        self.env_steps = 0          # VecEnv steps taken (SubprocVecEnvCustom.batch)
+        self.iterations = 0
+        self.callbacks = []
         self.last_obs = None
         self.last_done = torch.zeros(env.I, dtype=torch.uint8, device=self.device)
         self.last_values = torch.zeros(env.I, dtype=torch.float32, device=self.device)
@@ -443,7 +477,10 @@ class PPOTrainer:
         self.last_done.fill_(1)      # SB3: _last_episode_starts = ones after reset
 
     @torch.no_grad()
-    def collect_rollouts(self):
+    def collect_rollouts(self, callbacks=()):
+        """OnPolicyAlgorithm.collect_rollouts: n_steps env steps into the rollout buffer, then GAE.  After every env
+        step each callback's on_step(StepContext) runs (SB3 order: num_timesteps already advanced); one returning
+        False stops the rollout and the method returns False (no GAE), like SB3."""
         if self.last_obs is None:
             self.reset()
         st, pol = self.storage, self.policy
@@ -452,6 +489,9 @@ class PPOTrainer:
         if self.fused is not None:
             self.fused.refresh()      # the weights the last update left
             fwd = self.fused
+        from .callbacks import StepContext
+        for cb in callbacks:
+            cb.on_rollout_start(self)
         for t in range(self.cfg.n_steps):
             st.obs[t].copy_(self.last_obs)
             actions, values, logp = fwd(st.obs[t])
@@ -463,10 +503,21 @@ class PPOTrainer:
             st.rewards[t].copy_(rew)
             self.last_done.copy_(done)
             self.last_obs = obs
-        self.num_timesteps += self.cfg.n_steps * self.env.I
+            self.num_timesteps += self.env.I
+            self.env_steps += 1
+            if callbacks:
+                ctx = StepContext(self, t, obs, rew, done, st.actions[t])
+                go = True
+                for cb in callbacks:
+                    go = cb.on_step(ctx) is not False and go
+                if not go:
+                    return False
         self.last_values.copy_(fwd.predict_values(self.last_obs).view(-1))
         self.gae_fn(st.rewards, st.values, st.episode_starts, self.last_values, self.last_done,
                     self.cfg.gamma, self.cfg.gae_lambda, st.advantages, st.returns)
+        for cb in callbacks:
+            cb.on_rollout_end(self)
+        return True
 
     def train(self, max_updates=None):
         """PPO.train: n_epochs over shuffled minibatches of the flattened rollout (max_updates cuts the
@@ -517,4 +568,100 @@ class PPOTrainer:
 
     def learn_iteration(self):
         self.collect_rollouts()
-        return self.train()
+        stats = self.train()
+        self.iterations += 1
+        return stats
+
+    def learn(self, total_timesteps, callback=None):
+        """OnPolicyAlgorithm.learn as sb_train calls it (sb_train.py:93-98): rollouts + updates until
+        num_timesteps reaches total_timesteps, with the callbacks' hooks (quadswarm_amd.callbacks).  Returns the
+        last update's stats."""
+        cbs = [] if callback is None else (list(callback) if isinstance(callback, (list, tuple)) else [callback])
+        self.callbacks = cbs
+        for cb in cbs:
+            cb.on_training_start(self)
+        stats = {}
+        while self.num_timesteps < total_timesteps:
+            if not self.collect_rollouts(cbs):
+                break
+            stats = self.train()
+            self.iterations += 1
+            for cb in cbs:
+                cb.on_iteration_end(self)
+        for cb in cbs:
+            cb.on_training_end(self)
+        return stats
+
+    # ---- checkpoint / resume (sb_train: CheckpointCallback + model.save, sb_train.py:99-106) ----
+    CKPT_FORMAT = "quadswarm_amd.PPOTrainer/1"
+    ENV_PARAMS = ("seed", "ep_len", "rew_pos", "rew_effort", "rew_crash", "rew_orient", "rew_spin", "quadcol_bin",
+                  "quadcol_bin_smooth_max", "quadcol_bin_obst")
+
+    def save(self, path, callbacks=None):
+        """Everything the next iteration depends on: policy and Adam state, counters, the trainer's minibatch
+        generator and the device's default generator (rollout action noise), the env snapshot (qs_get_state: drone
+        and env state incl. the per-env Philox counters, capture radii, pillar maps), the current observation and
+        episode starts, the replay wrapper's device state, and the callbacks' state.  Loaded with
+        torch.load(weights_only=True).  Resuming reproduces the continuation bitwise (tests/test_gpu_trainer.py)."""
+        from dataclasses import asdict
+        callbacks = self.callbacks if callbacks is None else callbacks
+        env = self.env
+        u8 = lambda b: torch.frombuffer(bytearray(b), dtype=torch.uint8).clone()  # noqa: E731
+        ck = {"format": self.CKPT_FORMAT,
+              "policy": self.policy.state_dict(), "optimizer": self.optimizer.state_dict(),
+              "policy_cfg": asdict(self.policy.cfg), "ppo_cfg": asdict(self.cfg),
+              "num_timesteps": self.num_timesteps, "env_steps": self.env_steps, "iterations": self.iterations,
+              "gen": self.gen.get_state(), "device_rng": torch.cuda.get_rng_state(self.device)
+              if self.device.type == "cuda" else torch.get_rng_state(),
+              "last_obs": None if self.last_obs is None else self.last_obs.detach().cpu().clone(),
+              "last_done": self.last_done.cpu().clone(), "last_values": self.last_values.cpu().clone(),
+              "callbacks": [cb.state_dict() for cb in callbacks]}
+        if hasattr(env, "get_state"):
+            ck["env_state"] = u8(env.get_state())
+            # the runtime parameters qs_set_param may have changed (seed, reward annealing, episode length)
+            ck["env_params"] = {}
+            for k in self.ENV_PARAMS:
+                try:
+                    ck["env_params"][k] = env.get_param(k)
+                except NAT.QuadSwarmError:
+                    pass
+        if getattr(env, "replay", None) is not None:
+            ck["replay_ws"] = env._replay_ws.cpu().clone()
+        d = os.path.dirname(os.path.abspath(path))
+        os.makedirs(d, exist_ok=True)
+        torch.save(ck, path)
+        return path
+
+    def load(self, path, callbacks=()):
+        """Restore a save() checkpoint into this trainer (same policy / env configuration); `callbacks` (the same
+        kinds, in the order they were saved) get their state back for the next learn()."""
+        ck = torch.load(path, map_location="cpu", weights_only=True)
+        if ck.get("format") != self.CKPT_FORMAT:
+            raise ValueError(f"{path}: not a {self.CKPT_FORMAT} checkpoint")
+        self.policy.load_state_dict(ck["policy"])
+        self.optimizer.load_state_dict(ck["optimizer"])
+        self.num_timesteps, self.env_steps, self.iterations = (int(ck["num_timesteps"]), int(ck["env_steps"]),
+                                                                int(ck["iterations"]))
+        self.gen.set_state(ck["gen"])
+        if self.device.type == "cuda":
+            torch.cuda.set_rng_state(ck["device_rng"], self.device)
+        else:
+            torch.set_rng_state(ck["device_rng"])
+        env = self.env
+        if "env_state" in ck:
+            for k, v in ck.get("env_params", {}).items():
+                env.set_param(k, v)
+            env.set_state(bytes(ck["env_state"].numpy().tobytes()))
+        if "replay_ws" in ck:
+            env._replay_ws.copy_(ck["replay_ws"].to(env._replay_ws.device))
+        if ck["last_obs"] is not None:
+            obs = env.obs if hasattr(env, "obs") else torch.empty_like(ck["last_obs"], device=self.device)
+            obs.copy_(ck["last_obs"].to(self.device))
+            self.last_obs = obs
+        self.last_done.copy_(ck["last_done"].to(self.device))
+        self.last_values.copy_(ck["last_values"].to(self.device))
+        for cb, sd in zip(callbacks, ck["callbacks"]):
+            cb.load_state_dict(sd)
+        if self.fused is not None:
+            self.fused.refresh()
+        return ck

@@ -14,9 +14,9 @@ swapped for `GpuQuadVecEnv(cfg)`:
 Two modes:
   * compat (default): numpy in/out, exactly the reference's types (obs float32 instead of float64;
     the policy casts to float32 anyway, ActorCriticPolicyCustom.py:463);
-  * native (as_torch=True): torch device tensors in/out, nothing crosses PCIe.
+  * native (as_torch=True): torch device tensors in/out, nothing crosses PCIe.  Its infos are lazy (a
+    contract change, see StepInfos): read them before the next step_wait.
 """
-import types
 from collections.abc import Sequence
 
 import numpy as np
@@ -52,33 +52,35 @@ def make_box(low, high):
     return Box(low, high)
 
 
-_EMPTY = types.MappingProxyType({})
-
-
 class StepInfos(Sequence):
     """infos of one step, len == num_envs (agent rows).  Rows of finished envs get terminal_observation (and
     episode_extra_stats, quadrotor_multi.py:739-831, when the env keeps them).  With per-step infos on, every row
     carries the reference's per-agent entries: flavor B {"rewards": {...}} (quadrotor_single.py:79-105, 371;
     quadrotor_multi.py:642-651), flavor A {"rewards": {}, "goal_dist": ...} (quadrotor_single_rewards.py:457);
-    their dicts are built when a row is read, so a 32k-agent step does not build 32k dicts.  Without them a row
-    that did not finish is a shared read-only empty mapping.
+    their dicts are built when a row is read, so a 32k-agent step does not build 32k dicts.  A row's dict is built
+    once and kept: infos[i] returns the same mutable dict every time, so in-place writes (SB3's VecNormalize
+    rewriting terminal_observation, a wrapper adding episode_extra_stats) stick, as with the reference's list.
 
-    Native mode builds it lazily: nothing is copied to the host until a row (or the done rows) is read, which
-    must happen before the next step_wait (the device buffers it reads are the step's)."""
+    Native mode builds it lazily -- a contract change against the reference's eager list: nothing is copied to the
+    host until a row (or the done rows) is read, and that first read must happen before the next step_wait (the
+    device buffers it reads are the step's; a later first read raises RuntimeError).  Rows read in time stay
+    valid: their terminal_observation is a copy of the finished agents' rows, not a view of the env's buffer."""
 
     def __init__(self, n, done_rows=(), term=None, extra=None, rewards=None, goal_dist=None, resolve=None):
         self._n = n
         self._resolve = resolve
         self._d = None
+        self._m = {}       # row -> the dict handed out for it (memoised)
         if resolve is None:
             self._build(done_rows, term, extra, rewards, goal_dist)
 
     def _build(self, done_rows, term, extra, rewards, goal_dist):
+        """term: the terminal observations of the finished rows, in done_rows order."""
         self._rows = np.asarray(done_rows, dtype=np.int64)
         self._rewards, self._gd = rewards, goal_dist
         self._d = {}
         for k, r in enumerate(self._rows.tolist()):
-            self._d[r] = {"terminal_observation": term[r], "TimeLimit.truncated": False}
+            self._d[r] = {"terminal_observation": term[k], "TimeLimit.truncated": False}
             if extra is not None:
                 self._d[r]["episode_extra_stats"] = extra[k]
 
@@ -103,17 +105,20 @@ class StepInfos(Sequence):
             i += self._n
         if not 0 <= i < self._n:
             raise IndexError(i)
+        row = self._m.get(i)
+        if row is not None:
+            return row
         self._ready()
-        base = self._d.get(i)
-        if self._rewards is None and self._gd is None:
-            return _EMPTY if base is None else base
-        row = {} if base is None else dict(base)
+        row = self._d.get(i)
+        if row is None:
+            row = {}
         if self._rewards is not None:
             from .infos import rewards_dict
             row["rewards"] = rewards_dict(self._rewards, i)
-        else:
+        elif self._gd is not None:
             row["rewards"] = {}
             row["goal_dist"] = float(self._gd[i])
+        self._m[i] = row
         return row
 
 
@@ -219,8 +224,9 @@ class GpuQuadVecEnv:
             def resolve():
                 if gen != self._gen:
                     raise RuntimeError("GpuQuadVecEnv infos of an older step: read them before the next step_wait")
-                rows = torch.nonzero(d).flatten().cpu().numpy()
-                return (rows, term, self._episode_extra_stats(rows) if len(rows) else None) + \
+                rows_t = torch.nonzero(d).flatten()
+                rows = rows_t.cpu().numpy()
+                return (rows, term[rows_t].clone(), self._episode_extra_stats(rows) if len(rows) else None) + \
                     self._step_info_columns(comp)
             infos = StepInfos(self.num_envs, resolve=resolve)
             self._last_infos = infos
@@ -231,7 +237,7 @@ class GpuQuadVecEnv:
         self._check_nan(h[-1])
         self._reset_infos, self._last_infos = self._reset_infos_of(rows), None
         extra = self._episode_extra_stats(rows) if len(rows) else None
-        term_np = term.cpu().numpy() if len(rows) else None
+        term_np = term[torch.as_tensor(rows, device=term.device)].cpu().numpy() if len(rows) else None
         cols = self._step_info_columns(self.env.rew_info)
         return obs.cpu().numpy(), rew.cpu().numpy(), d.cpu().numpy(), StepInfos(self.num_envs, rows, term_np, extra,
                                                                                *cols)
@@ -285,6 +291,9 @@ class GpuQuadVecEnv:
         return self.env.counters()
 
     def reset_counters(self):
+        if self.as_torch and self._nan_pending:   # a copy still in flight carries the count from before the reset
+            self._nan_ev.synchronize()
+            self._nan_pending = False
         self.env.reset_counters()
         self._nan_last = 0
 

@@ -337,3 +337,29 @@ def test_flavor_a_replay_refused_like_the_reference():
     assert c.replay_buffer_sample_prob == 0.5
     with pytest.raises(KeyError, match="rew_crash"):
         c.to_qs_config()
+
+
+def test_jit_opts_may_not_change_launch_geometry(monkeypatch):
+    """The host sizes step launches from its own QS_QB / QS_QA / QS_QW (block_threads, envs_per_block); a hipRTC
+    option that redefines them would compile kernels indexing envs and LDS for another geometry: refused."""
+    L = N.lib()
+    qc = QuadSwarmConfig(num_envs=64, num_agents=64, neighbor_visible_num=6).to_qs_config()
+    for opt in ("-DQS_QW=1", "-DQS_QB=2", "-DQS_QA=4"):
+        monkeypatch.setenv("QS_JIT_OPTS", "-DQS_FOO=1 " + opt)
+        assert L.qs_specialize_compile(qc) == -1          # QS_E_INVALID
+        assert opt[2:7] in L.qs_last_error().decode()
+
+
+def test_curriculum_init_fills_the_struct_mirror():
+    """qs_curriculum_init (host only) writes exactly the mirrored struct: the reference's starting state of
+    CurriculumCallback (custom_callbacks.py:442-451), a cleared window."""
+    L = N.lib()
+    n = ctypes.sizeof(N.QsCurriculum)
+    raw = (ctypes.c_uint8 * (n + 64))(*([0xAB] * (n + 64)))
+    assert L.qs_curriculum_init(raw, 0.5, 0.8, 0.9, 40) == 0
+    assert bytes(raw[n:]) == b"\xab" * 64             # nothing written past the mirror's size
+    c = N.QsCurriculum.from_buffer_copy(bytes(raw[:n]))
+    assert (c.radius, c.sr_threshold, c.decay, c.window) == (0.5, 0.8, 0.9, 40)
+    assert c.window_i == 0 and c.n_shrinks == 0 and c.success_rate == 0.0 and not any(c.past)
+    assert L.qs_curriculum_init(raw, 0.5, 0.8, 0.9, 65) == -1
+    assert L.qs_curriculum_init(raw, 0.0, 0.8, 0.9, 40) == -1

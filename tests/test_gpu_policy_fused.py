@@ -116,3 +116,48 @@ def test_trainer_rollout_uses_fused_forward():
             assert (v - tr.storage.values[t]).abs().max().item() < 2e-4
     stats = tr.train()
     assert np.isfinite(stats["loss"])
+
+
+@pytest.mark.parametrize("case", ["c3", "a8"])
+def test_fused_rollout_log_probs_match_evaluate_actions(case):
+    """The rollout stores the fused path's log-probs; PPO's first epoch divides the torch module's
+    evaluate_actions log-probs of the same (obs, actions) by them.  At a small std (exp(log_std) = 0.05, a late
+    training stage) the log-prob amplifies a mean difference by z / std, so this bounds the ratio PPO sees
+    before any update: |exp(lp_torch - lp_fused) - 1| (the clip range is 0.2)."""
+    import math
+    pol = make_policy(case, seed=5)
+    with torch.no_grad():
+        pol.log_std.fill_(math.log(0.05))
+    fp = FusedRolloutPolicy(pol)
+    obs = obs_for(pol.cfg, 4096, seed=6)
+    torch.manual_seed(7)
+    a_f, v_f, lp_f = fp(obs)
+    with torch.no_grad():
+        v_t, lp_t, _ = pol.evaluate_actions(obs, a_f)
+    dev = (torch.exp(lp_t - lp_f) - 1).abs()
+    print(f"{case}: ratio deviation max {dev.max().item():.3e} mean {dev.mean().item():.3e}")
+    assert dev.max().item() < 2e-3 and dev.mean().item() < 2e-4
+    assert (v_t.view(-1) - v_f.view(-1)).abs().max().item() < 2e-4
+
+
+@pytest.mark.parametrize("case", ["c3", "a8", "c4"])
+def test_fused_policy_matches_reference_fixture(case):
+    """The fused rollout forward against the reference's own policy module: tests/golden/policy_<case> (written by
+    tools/gen_golden_policy.py from swarm_rl/models/ActorCriticPolicyCustom.py + quad_multi_model.py), weights
+    loaded under the reference's parameter names."""
+    from test_policy_reference import load_case, reference_weights
+    meta, data, pc = load_case(case)
+    pol = SwarmActorCritic(pc).cuda().eval()
+    pol.load_reference_state_dict(reference_weights(meta, torch.float32))
+    assert supports(pol)
+    fp = FusedRolloutPolicy(pol)
+    obs = torch.from_numpy(data["obs"].astype(np.float32)).cuda()
+    nbr = fp.neighbor_encodings(obs)
+    for i, tw in enumerate(("actor", "critic")):
+        err = np.abs(nbr[i].cpu().numpy() - data[f"{tw}_nbr64"]).max()
+        assert err < ATOL, (case, tw, err)
+    a, v, lp = fp(obs, deterministic=True)
+    np.testing.assert_allclose(a.cpu().numpy(), data["det_actions32"], rtol=0, atol=2e-4)
+    np.testing.assert_allclose(v.cpu().numpy(), data["det_values32"], rtol=1e-4, atol=2e-4)
+    np.testing.assert_allclose(lp.cpu().numpy(), data["det_log_prob32"], rtol=1e-4, atol=2e-3)
+    np.testing.assert_allclose(fp.predict_values(obs).cpu().numpy(), data["pv_values32"], rtol=1e-4, atol=2e-4)
