@@ -633,15 +633,29 @@ struct DroneWords {
     static constexpr int T = (NW + Q - 1) / Q;
     uint32_t r[T];
 };
-// issue the sub-lane's state-word loads (no wait): the first nw <= NW words
+// Words of a drone that can hold something other than 0, i.e. that a step must move: the previous-collision
+// row's words no partner can set (N = 1: both; N <= 32: bits 32..63) always hold 0 and are neither loaded nor
+// stored, and the episode-stats window sums (words DW + 5 + k) are loaded only while window k is open (wsum bit
+// k; outside it the step neither reads nor writes them).  With the specialised kernels kp.N is a constant, so
+// the row words' tests fold away.
+template <int NIW = 4>
+__device__ __forceinline__ bool word_live(const KP& kp, int w, uint32_t wsum) {
+    constexpr int IW = QS_F_GOAL + 3, DW = WordsOf<NIW>::DW;
+    if (w == IW + QS_I_PREV_LO) return kp.N > 1;
+    if (w == IW + QS_I_PREV_HI) return kp.N > 32;
+    if (w >= DW + 5) return (wsum >> (w - DW - 5)) & 1u;
+    return true;
+}
+// issue the sub-lane's state-word loads (no wait): the first nw <= NW words (live ones only; the others read 0)
 template <int Q, int NW, int NIW = 4>
 __device__ __forceinline__ void load_words_q(const KP& kp, const Bufs& b, int g, int q, DroneWords<Q, NW>& dw,
-                                             int nw = NW) {
+                                             int nw = NW, uint32_t wsum = 7u) {
     const uint32_t go = (uint32_t)g * 4u;
 #pragma unroll
     for (int t = 0; t < DroneWords<Q, NW>::T; ++t) {
         const int w = t * Q + q;
-        dw.r[t] = w < nw ? *reinterpret_cast<const uint32_t*>((const char*)b.st + drone_word_off<NIW>(kp, b, w, go)) : 0u;
+        dw.r[t] = (w < nw && word_live<NIW>(kp, w, wsum))
+                      ? *reinterpret_cast<const uint32_t*>((const char*)b.st + drone_word_off<NIW>(kp, b, w, go)) : 0u;
     }
 }
 // the drone on every sub-lane; stw (if given) gets the STAT_WORDS words as floats
@@ -725,7 +739,7 @@ __device__ __forceinline__ void store_drone_q(const KP& kp, const Bufs& b, int g
 #pragma unroll
         for (int k = 1; k < Q; ++k)
             if (q == k && t * Q + k < NW) v = wv[t * Q + k];
-        const bool wr = w < DW || (w < NW && ((stmask >> (w - DW)) & 1u));
+        const bool wr = (w < DW && word_live<NIW>(kp, w, 7u)) || (w >= DW && w < NW && ((stmask >> (w - DW)) & 1u));
         if (active && wr) st_wt1(rs, drone_word_off<NIW>(kp, b, w, go), 0u, v);
     }
 }
@@ -951,17 +965,26 @@ __global__ __launch_bounds__(StepGeo<NPAD>::WGS) void step_kernel(const KP* __re
     int cnt[CT];
     bool cdirty[CT];   // the counter changed this step: stored once, at the end of the step
     auto cnt_at = [&](int k) -> int32_t* { return b.env + (QS_E_ST_COL + k) * kp.E + env; };
+    // a counter that no event of this configuration can increment stays 0: not loaded (drone-drone collisions
+    // need a partner, the obstacle counters obstacles; with the specialised kernels these tests are constants)
+    auto cnt_live = [&](int k) { return (k == 0 || k == 5 || k == 6) ? kp.N > 1 : (k >= 7 ? OBST : true); };
 #pragma unroll
     for (int t = 0; t < CT; ++t) {
         const int k = li + LPE * t;
-        cnt[t] = (kp.stats && envok && k < NCNT) ? *cnt_at(k) : 0;
+        cnt[t] = (kp.stats && envok && k < NCNT && cnt_live(k)) ? *cnt_at(k) : 0;
         cdirty[t] = false;
     }
     int omi = 0, osi = 0;   // the env's domain-randomisation choice (QS_E_OBST_M / _SZ)
     if (OBST && kp.dr) { omi = b.env[QS_E_OBST_M * kp.E + eidx]; osi = b.env[QS_E_OBST_SZ * kp.E + eidx]; }
     Drone d;   // every sub-lane holds the whole drone
     DroneWords<Q, LW> dw;
-    load_words_q<Q, LW, NIW>(kp, b, g, q, dw, kp.stats ? LW : DW);
+    // the episode-stats window sums open in this step (tick0 + 1 > ep_len + 1 - window; the test below repeats it)
+    uint32_t wsum = 0u;
+    if (kp.stats) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) wsum |= (tick0 + 1 > kpm.ep_len + 1 - kp.st_win[k]) ? 1u << k : 0u;
+    }
+    load_words_q<Q, LW, NIW>(kp, b, g, q, dw, kp.stats ? LW : DW, wsum);
     __builtin_amdgcn_sched_barrier(0);
     const Rng rng = env_rng(seed, tick0, episode);
     // The step's regular draws: Philox block k of {OU 0, sensor 0, sensor 1, sensor 2} on sub-lane
@@ -1391,7 +1414,7 @@ __global__ __launch_bounds__(StepGeo<NPAD>::WGS) void step_kernel(const KP* __re
 #pragma unroll
             for (int t = 0; t < CT; ++t) {
                 const int k = li + LPE * t;
-                if (envok && done && k < NCNT) {
+                if (envok && done && k < NCNT && cnt_live(k)) {
                     cnt[t] = 0;
                     cdirty[t] = true;
                 }

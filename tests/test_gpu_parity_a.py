@@ -159,7 +159,7 @@ def test_one_step_from_identical_state(name):
     assert stats["cap"] > 0
 
 
-def load_golden_into_gpu(golden, name, E=1):
+def load_golden_into_gpu(golden, name, E=1, with_oracle=False):
     g = golden("a_traj_" + name)
     n = int(g["n"])
     ntypes = ["dist_angle", "dist_sangle", "ndist_nsangle", "dist_angle_heading", "dist_sangle_sheading",
@@ -191,7 +191,7 @@ def load_golden_into_gpu(golden, name, E=1):
         ev.capture_radius = float(g["init_capture"])
         ev.has_pos = 1
     oracle_to_gpu_a(oenv, env)
-    return g, cfg, env
+    return (g, cfg, env, oenv) if with_oracle else (g, cfg, env)
 
 
 def test_reference_quiet_trajectory(golden):
