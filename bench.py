@@ -97,6 +97,28 @@ def algorithmic_bytes_per_agent_step(obs_dim, n_agents, flavor="B", n_obst=0):
     return 4 * (33 + 30 + 4 + obs_dim + 1) + 1 + 8.0 * n_obst / n_agents
 
 
+def state_bytes_per_agent_step(cfg):
+    """Bytes a step moves per agent once the state the reference's step also carries is counted (§8d's formula leaves
+    it out): per drone the istate words (SVD counter, flags, the collision-row words a swarm of N can set: 0 / 1 / 2 / 4
+    for N = 1 / <= 32 / <= 64 / 128) read and written, and with episode_extra_stats on (the reference's default) the
+    distance ring + window sums read (8 words) and one ring slot written; per env (divided by N) tick, episode and flags
+    read, tick and flags written, and the episode counters no configuration leaves at 0 read (room 4, drone-drone 3
+    when N > 1, obstacle 4 with obstacles).  Flavor B only (flavor A's §8d count already includes its env words).
+    Returns (bytes per agent-step, read bytes per agent-step)."""
+    n = cfg.num_agents
+    npad = 1 << (n - 1).bit_length()
+    niw = 2 if npad == 1 else (3 if npad <= 32 else (4 if npad <= 64 else 6))
+    obst = cfg.num_obstacles if cfg.use_obstacles else 0
+    base = algorithmic_bytes_per_agent_step(cfg.obs_dim, n, cfg.flavor, obst)
+    base_read = 4 * (33 + 4) + 8.0 * obst / n
+    stats = bool(cfg.episode_stats)
+    ncnt = (4 + (3 if n > 1 else 0) + (4 if cfg.use_obstacles else 0)) if stats else 0
+    drone_r = 4 * niw + (4 * 8 if stats else 0)
+    drone_w = 4 * niw + (4 if stats else 0)
+    env_r, env_w = 4 * (3 + ncnt), 4 * 2
+    return base + drone_r + drone_w + (env_r + env_w) / n, base_read + drone_r + env_r / n
+
+
 def cpu_worker(config, seconds):
     """One cpu_baseline leg, run as a child process (bench.py --cpu-worker): the C oracle on this host's cores,
     fp64 (liboracle.so) or its fp32 twin (liboracle_f32.so, QS_ORACLE_F32=1), OpenMP over envs with
@@ -169,14 +191,19 @@ def npad(n):
 
 def pmc_traffic(config):
     """HBM bytes per launch measured by rocprofv3 --pmc (profiles/pmc_<config>.json, written by
-    tools/summarize_prof.py from separate FETCH_SIZE / WRITE_SIZE passes with the gfx950 correction)."""
+    tools/summarize_prof.py from separate FETCH_SIZE / WRITE_SIZE passes with the gfx950 correction), and where
+    they come from (file, the tree they were taken on, reads / writes)."""
     p = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
     if not os.path.exists(p):
-        return None
+        return None, None
     try:
-        return json.load(open(p)).get("hbm_bytes_per_launch")
+        d = json.load(open(p))
+        src = {"file": os.path.relpath(p, ROOT), "tree": d.get("tree"),
+               "read_bytes": d.get("hbm_read_bytes_per_launch"), "write_bytes": d.get("hbm_write_bytes_per_launch"),
+               "passes": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate runs, FETCH x2 (gfx950)"}
+        return d.get("hbm_bytes_per_launch"), src
     except Exception:
-        return None
+        return None, None
 
 
 # end-to-end PPO leg per workload family: policy / PPO settings of the reference run that trains it
@@ -208,7 +235,7 @@ def update_flops_per_sample(pol, obs_dim, act_dim, dev, rows=256):
     return fc.get_total_flops() / rows
 
 
-def end_to_end(env, cfg, dev, world, iters, n_steps=None, log=None, fused=True):
+def end_to_end(env, cfg, dev, world, iters, n_steps=None, log=None, fused=True, precision="fp32"):
     """Timed PPO iterations (rollout + GAE + update) on the bench's env shard."""
     import torch
     import torch.distributed as dist
@@ -222,7 +249,7 @@ def end_to_end(env, cfg, dev, world, iters, n_steps=None, log=None, fused=True):
     pcfg.batch_size = -(-samples // n_mb)
     torch.manual_seed(0)
     pol = SwarmActorCritic(pc).to(dev)
-    tr = PPOTrainer(env, pol, pcfg, seed=0, fused_rollout=fused)
+    tr = PPOTrainer(env, pol, pcfg, seed=0, fused_rollout=fused, rollout_precision=precision)
     tr.reset()
 
     def sync():
@@ -270,8 +297,9 @@ def end_to_end(env, cfg, dev, world, iters, n_steps=None, log=None, fused=True):
         "minibatches_per_epoch": n_mb, "policy_params": nparam,
         "policy": f"ActorCriticPolicyCustomSeparateWeights: {pc.neighbor_encoder_type} k={pc.num_use_neighbor_obs}, "
                   f"rnn {pc.rnn_size}, core {pc.rnn_type or 'identity'} x{pc.rnn_num_layers if pc.rnn_type else 0}, "
-                  f"fp32 (torch/hipBLASLt GEMMs" + (", rollout neighbour encoders: fused HIP MFMA kernels)"
+                  f"fp32 (torch/hipBLASLt GEMMs" + (f", rollout neighbour encoders: fused HIP MFMA kernels, {precision})"
                                                     if tr.fused is not None else ")"),
+        "rollout_precision": precision if tr.fused is not None else "torch fp32",
         "gemm_table": tuned,
         "update_flop_per_sample": round(fps), "update_tflops": round(upd_tf, 2),
         "update_frac_fp32_mfma_peak": round(upd_tf / 157.3, 3),
@@ -471,6 +499,8 @@ def main(argv=None):
     ap.add_argument("--e2e-steps", type=int, default=0, help="override the PPO rollout length n_steps")
     ap.add_argument("--e2e-unfused", action="store_true",
                     help="A/B only: the rollout evaluates the torch policy module instead of the fused encoders")
+    ap.add_argument("--e2e-precision", choices=["fp32", "x3"], default="fp32",
+                    help="fused rollout encoders: fp32 matrix cores, or each fp32 product as 3 f16 products (x3)")
     ap.add_argument("--host-sync", choices=["spin", "auto"], default="auto",
                     help="host wait of torch.cuda.synchronize(): spin (hipDeviceScheduleSpin) or HIP's default")
     args = ap.parse_args(argv)
@@ -602,7 +632,7 @@ def main(argv=None):
         log = (lambda m: print(m, file=sys.stderr, flush=True)) if rank == 0 else None
         try:
             e2e = end_to_end(env, cfg, dev, world, args.e2e_iters, args.e2e_steps or None, log,
-                             fused=not args.e2e_unfused)
+                             fused=not args.e2e_unfused, precision=args.e2e_precision)
         except Exception as e:  # never let the PPO leg kill the env number
             if world > 1:
                 raise
@@ -613,7 +643,7 @@ def main(argv=None):
         bpa = algorithmic_bytes_per_agent_step(cfg.obs_dim, cfg.num_agents, cfg.flavor,
                                                cfg.num_obstacles if cfg.use_obstacles else 0)
         achieved = bpa * I / (k_ms * 1e-3) / 1e9
-        traffic = pmc_traffic(args.config)
+        traffic, traffic_src = pmc_traffic(args.config)
         if chunk:
             launch = f"{timed_replays} hipGraph replays ({timed_replays * len(run.entries)} graphs) for {args.steps} timed steps"
         else:
@@ -650,6 +680,7 @@ def main(argv=None):
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
                          "traffic_scope": "HBM bytes of one whole-shard step (PMC, one handle)",
+                         "traffic_source": traffic_src,
                          "kernel": (f"qs::step_kernel_a<{npad(cfg.num_agents)}>" if cfg.flavor == "A" else
                                     f"qs::step_kernel<{npad(cfg.num_agents)}, {'true' if cfg.use_obstacles else 'false'}>"),
                          "kernel_us": round(k_ms * 1e3, 3),
@@ -659,6 +690,8 @@ def main(argv=None):
                          "launches_per_step": S,
                          "kernel_us_eager_single": round(k_eager_ms * 1e3, 3),
                          "bytes_per_agent_step": round(bpa, 1),
+                         "bytes_per_agent_step_state_complete": (round(state_bytes_per_agent_step(cfg)[0], 1)
+                                                                 if cfg.flavor == "B" else None),
                          "bytes_per_launch": round(bpa * I / S)},
             "nonfinite_guard": guard,
             "cpu_baseline": None,

@@ -469,6 +469,15 @@ typedef struct qs_attn_tower {
 int qs_attn_embed(const float* d_obs, int32_t obs_stride, int32_t self_dim, int32_t nbr_off, int32_t B, int32_t K,
                   int32_t nd, int32_t H, const qs_attn_tower* towers, int32_t n_towers, void* stream);
 int qs_attn_pool(int32_t B, int32_t K, int32_t H, const qs_attn_tower* towers, int32_t n_towers, void* stream);
+/* The same two stages with every fp32 product of the contractions split over the f16 matrix cores (ABI 11):
+ * x = (hi + lo) / s with hi = f16(s x), lo = f16(s x - hi), and x w = (hi_x hi_w + hi_x lo_w + lo_x hi_w) / (s_x s_w)
+ * accumulated in fp32 (per-product error ~7e-7 relative; biases, tanh, softmax, pooling fp32).  The towers' w_*p then
+ * point to weights packed for v_mfma_f32_32x32x16_f16 (quadswarm_amd.policy_fused.pack_mfma_weight_x3): per
+ * 32-column tile ct, 16-deep step s and lane l, 8 f16 of hi(256 W[32 ct + (l & 31)][16 s + 8 (l >> 5) + j]) then
+ * the 8 matching lo halves; every other pointer as above. */
+int qs_attn_embed_x3(const float* d_obs, int32_t obs_stride, int32_t self_dim, int32_t nbr_off, int32_t B, int32_t K,
+                     int32_t nd, int32_t H, const qs_attn_tower* towers, int32_t n_towers, void* stream);
+int qs_attn_pool_x3(int32_t B, int32_t K, int32_t H, const qs_attn_tower* towers, int32_t n_towers, void* stream);
 
 /* sb_train's capture-radius curriculum on the device (ABI 11; replaces CurriculumCallback._on_step,
  * swarm_rl/custom_callbacks.py:441-468, which SB3 runs after every VecEnv step).  Flavor A.  The callback's state

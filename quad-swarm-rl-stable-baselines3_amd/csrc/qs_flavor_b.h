@@ -591,8 +591,9 @@ __device__ __forceinline__ float2* obst_tile(float* lds, const KP& kp, int slots
 }
 
 // Geometry of the flavor-B step kernel: Q lanes per drone (Q * NPAD <= 64), EPB envs per wave.
-// Cooperative state load / store of the Q sub-lanes of a drone (flavor-B step).  The drone's 37 state
-// words (33 fp32 fields QS_F_POS .. QS_F_GOAL, then 4 int fields QS_I_*) are dealt over the sub-lanes:
+// Cooperative state load / store of the Q sub-lanes of a drone (flavor-B step).  The drone's state words
+// (33 fp32 fields QS_F_POS .. QS_F_GOAL, then the NIW int fields QS_I_* a swarm of its size uses: 2 for
+// single drones, 3 up to 32, 4 up to 64, 6 at 128 -- StepGeo::NIW) are dealt over the sub-lanes:
 // instruction t moves word t*Q + q on sub-lane q, so a wave instruction covers Q fields x its drones and
 // the drone needs ceil(37 / Q) load / store instructions instead of 37.  Loaded words are broadcast to
 // every sub-lane by DPP (every sub-lane holds the whole drone).  Addresses are b.st (SGPRs) + a 32-bit
@@ -633,29 +634,15 @@ struct DroneWords {
     static constexpr int T = (NW + Q - 1) / Q;
     uint32_t r[T];
 };
-// Words of a drone that can hold something other than 0, i.e. that a step must move: the previous-collision
-// row's words no partner can set (N = 1: both; N <= 32: bits 32..63) always hold 0 and are neither loaded nor
-// stored, and the episode-stats window sums (words DW + 5 + k) are loaded only while window k is open (wsum bit
-// k; outside it the step neither reads nor writes them).  With the specialised kernels kp.N is a constant, so
-// the row words' tests fold away.
-template <int NIW = 4>
-__device__ __forceinline__ bool word_live(const KP& kp, int w, uint32_t wsum) {
-    constexpr int IW = QS_F_GOAL + 3, DW = WordsOf<NIW>::DW;
-    if (w == IW + QS_I_PREV_LO) return kp.N > 1;
-    if (w == IW + QS_I_PREV_HI) return kp.N > 32;
-    if (w >= DW + 5) return (wsum >> (w - DW - 5)) & 1u;
-    return true;
-}
-// issue the sub-lane's state-word loads (no wait): the first nw <= NW words (live ones only; the others read 0)
+// issue the sub-lane's state-word loads (no wait): the first nw <= NW words
 template <int Q, int NW, int NIW = 4>
 __device__ __forceinline__ void load_words_q(const KP& kp, const Bufs& b, int g, int q, DroneWords<Q, NW>& dw,
-                                             int nw = NW, uint32_t wsum = 7u) {
+                                             int nw = NW) {
     const uint32_t go = (uint32_t)g * 4u;
 #pragma unroll
     for (int t = 0; t < DroneWords<Q, NW>::T; ++t) {
         const int w = t * Q + q;
-        dw.r[t] = (w < nw && word_live<NIW>(kp, w, wsum))
-                      ? *reinterpret_cast<const uint32_t*>((const char*)b.st + drone_word_off<NIW>(kp, b, w, go)) : 0u;
+        dw.r[t] = w < nw ? *reinterpret_cast<const uint32_t*>((const char*)b.st + drone_word_off<NIW>(kp, b, w, go)) : 0u;
     }
 }
 // the drone on every sub-lane; stw (if given) gets the STAT_WORDS words as floats
@@ -687,8 +674,11 @@ __device__ __forceinline__ void unpack_words_q(const DroneWords<Q, NW>& dw, Dron
     constexpr int IW = QS_F_GOAL + 3;
     d.svd = (int32_t)wv[IW + QS_I_SVD];
     d.flags = wv[IW + QS_I_FLAGS];
-    d.prev = (uint64_t)wv[IW + QS_I_PREV_LO] | ((uint64_t)wv[IW + QS_I_PREV_HI] << 32);
-    d.prevx = NIW > 4 ? (uint64_t)wv[IW + QS_I_PREV_2 % NIW] | ((uint64_t)wv[IW + QS_I_PREV_3 % NIW] << 32) : 0ull;
+    d.prev = 0ull;
+    d.prevx = 0ull;
+    if constexpr (NIW > QS_I_PREV_LO) d.prev = (uint64_t)wv[IW + QS_I_PREV_LO];
+    if constexpr (NIW > QS_I_PREV_HI) d.prev |= (uint64_t)wv[IW + QS_I_PREV_HI] << 32;
+    if constexpr (NIW > QS_I_PREV_3) d.prevx = (uint64_t)wv[IW + QS_I_PREV_2] | ((uint64_t)wv[IW + QS_I_PREV_3] << 32);
 }
 template <int Q>
 __device__ __forceinline__ void load_drone_q(const KP& kp, const Bufs& b, int g, int q, Drone& d) {
@@ -719,11 +709,11 @@ __device__ __forceinline__ void store_drone_q(const KP& kp, const Bufs& b, int g
     constexpr int IW = QS_F_GOAL + 3;
     wv[IW + QS_I_SVD] = (uint32_t)d.svd;
     wv[IW + QS_I_FLAGS] = d.flags;
-    wv[IW + QS_I_PREV_LO] = (uint32_t)d.prev;
-    wv[IW + QS_I_PREV_HI] = (uint32_t)(d.prev >> 32);
-    if constexpr (NIW > 4) {
-        wv[IW + QS_I_PREV_2 % NIW] = (uint32_t)d.prevx;
-        wv[IW + QS_I_PREV_3 % NIW] = (uint32_t)(d.prevx >> 32);
+    if constexpr (NIW > QS_I_PREV_LO) wv[IW + QS_I_PREV_LO] = (uint32_t)d.prev;
+    if constexpr (NIW > QS_I_PREV_HI) wv[IW + QS_I_PREV_HI] = (uint32_t)(d.prev >> 32);
+    if constexpr (NIW > QS_I_PREV_3) {
+        wv[IW + QS_I_PREV_2] = (uint32_t)d.prevx;
+        wv[IW + QS_I_PREV_3] = (uint32_t)(d.prevx >> 32);
     }
     if constexpr (ST) {
 #pragma unroll
@@ -739,7 +729,7 @@ __device__ __forceinline__ void store_drone_q(const KP& kp, const Bufs& b, int g
 #pragma unroll
         for (int k = 1; k < Q; ++k)
             if (q == k && t * Q + k < NW) v = wv[t * Q + k];
-        const bool wr = (w < DW && word_live<NIW>(kp, w, 7u)) || (w >= DW && w < NW && ((stmask >> (w - DW)) & 1u));
+        const bool wr = w < DW || (w < NW && ((stmask >> (w - DW)) & 1u));
         if (active && wr) st_wt1(rs, drone_word_off<NIW>(kp, b, w, go), 0u, v);
     }
 }
@@ -762,7 +752,10 @@ struct StepGeo {
     static constexpr int SLOTS = EPB * NPAD;        // drone slots per workgroup
     static constexpr bool WIDE = LPE > 64;          // the env spans the workgroup's waves (64 / 128 drones)
     static constexpr bool ROW2 = NPAD > 64;         // 128-bit collision rows (128-drone envs)
-    static constexpr int NIW = ROW2 ? 6 : 4;        // istate words per drone (WordsOf)
+    // istate words a step moves per drone (WordsOf): SVD counter, flags, then the previous-collision row's
+    // words that a partner can set -- none for single-drone envs, the low word up to 32 drones, both up to 64,
+    // four for the 128-bit rows.  The words beyond stay 0 in memory (zeroed at creation) and are never moved.
+    static constexpr int NIW = NPAD == 1 ? 2 : (NPAD <= 32 ? 3 : (ROW2 ? 6 : 4));
 };
 
 // ---- collision rows: bit j = partner drone j; 64 bits, or two words for the 128-drone envs ----
@@ -967,7 +960,9 @@ __global__ __launch_bounds__(StepGeo<NPAD>::WGS) void step_kernel(const KP* __re
     auto cnt_at = [&](int k) -> int32_t* { return b.env + (QS_E_ST_COL + k) * kp.E + env; };
     // a counter that no event of this configuration can increment stays 0: not loaded (drone-drone collisions
     // need a partner, the obstacle counters obstacles; with the specialised kernels these tests are constants)
-    auto cnt_live = [&](int k) { return (k == 0 || k == 5 || k == 6) ? kp.N > 1 : (k >= 7 ? OBST : true); };
+    // (counters 0, 5, 6: drone-drone; 1-4: room; 7-10: obstacles -> the live ones are [cnt_lo, cnt_hi))
+    const int cnt_lo = kp.N > 1 ? 0 : 1, cnt_hi = OBST ? NCNT : (kp.N > 1 ? 7 : 5);
+    auto cnt_live = [&](int k) { return k >= cnt_lo && k < cnt_hi; };
 #pragma unroll
     for (int t = 0; t < CT; ++t) {
         const int k = li + LPE * t;
@@ -978,13 +973,7 @@ __global__ __launch_bounds__(StepGeo<NPAD>::WGS) void step_kernel(const KP* __re
     if (OBST && kp.dr) { omi = b.env[QS_E_OBST_M * kp.E + eidx]; osi = b.env[QS_E_OBST_SZ * kp.E + eidx]; }
     Drone d;   // every sub-lane holds the whole drone
     DroneWords<Q, LW> dw;
-    // the episode-stats window sums open in this step (tick0 + 1 > ep_len + 1 - window; the test below repeats it)
-    uint32_t wsum = 0u;
-    if (kp.stats) {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) wsum |= (tick0 + 1 > kpm.ep_len + 1 - kp.st_win[k]) ? 1u << k : 0u;
-    }
-    load_words_q<Q, LW, NIW>(kp, b, g, q, dw, kp.stats ? LW : DW, wsum);
+    load_words_q<Q, LW, NIW>(kp, b, g, q, dw, kp.stats ? LW : DW);
     __builtin_amdgcn_sched_barrier(0);
     const Rng rng = env_rng(seed, tick0, episode);
     // The step's regular draws: Philox block k of {OU 0, sensor 0, sensor 1, sensor 2} on sub-lane

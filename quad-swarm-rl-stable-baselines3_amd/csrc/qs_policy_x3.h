@@ -1,0 +1,325 @@
+// qs_policy_x3.h -- the fused attention-encoder forward of qs_policy.h with every fp32 product split over the
+// f16 matrix cores (precision QS_ATTN_X3).
+//
+// Same function, same two kernels, same block structure (64 neighbour rows per block, 4 waves, wave w owning
+// output columns [w H/4, (w+1) H/4)); what changes is the contraction.  Each fp32 operand x is carried as two
+// f16 values, hi = f16(s x) and lo = f16(s x - hi) with a power-of-two scale s (activations 2^8, raw obs 2^4,
+// weights 2^8: both halves stay normal f16 numbers), so x = (hi + lo) / s to 2^-22 relative, and
+//   x . w = (hi_x hi_w + hi_x lo_w + lo_x hi_w) / (s_x s_w)   (+ the dropped lo_x lo_w, < 2^-22 relative)
+// with every f16 x f16 product exact in the fp32 accumulator (11 + 11 bits).  Three v_mfma_f32_32x32x16_f16 per
+// 32 x 32 x 16 step replace eight v_mfma_f32_32x32x2f32 (32 vs 64 cycles each): 5.3x the fp32 matrix rate at a
+// per-product error of ~7e-7 relative (fp32's own rounding: 6e-8), i.e. the fp32 GEMM emulated on the f16 matrix
+// cores the way split-precision ("3 x f16") GEMMs do.  Accumulation, biases, tanh, softmax and pooling stay fp32.
+//
+// LDS: the block's activation tile as two f16 tiles (hi, lo) [64][H + 8] -- the same 67 KB as the fp32 tile, so
+// two blocks still share a CU; the A operand of a 16-deep step is one ds_read_b128 per tile and 32-row half.
+// Weights: packed per (32-column tile ct, 16-deep step s, lane l): 8 hi halves then 8 lo halves of
+// W[32 ct + (l & 31)][16 s + 8 (l >> 5) .. + 7] * 2^8 -- two global_load_dwordx4 per lane and step, 2 KB
+// contiguous per wave (policy_fused.pack_mfma_weight_x3).
+#pragma once
+#include "qs_policy.h"
+
+namespace qs {
+namespace pol {
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+constexpr float X3_SX = 256.f;        // activation scale (tanh outputs, e2 rows)
+constexpr float X3_SIN = 16.f;        // raw observation scale (layer 0 inputs)
+constexpr float X3_SW = 256.f;        // weight scale (policy_fused.pack_mfma_weight_x3)
+
+template <int KD>
+struct GeoX3 {
+    static constexpr int LDH = KD + 8;   // f16 row stride: 16-B rotation per row, ds_read_b128 of 16 rows conflict-free
+    static constexpr int S = KD / 16;    // 16-deep steps
+};
+
+// one tile pair: element (i, n) -> hi / lo halves
+struct TileX3 {
+    _Float16* h;
+    _Float16* l;
+    int ld;
+    __device__ __forceinline__ void put(int i, int n, float ys) const {   // ys = s x (already scaled)
+        const _Float16 a = (_Float16)ys;
+        h[i * ld + n] = a;
+        l[i * ld + n] = (_Float16)(ys - (float)a);
+    }
+    __device__ __forceinline__ float get(int i, int n) const {   // s x
+        return (float)h[i * ld + n] + (float)l[i * ld + n];
+    }
+};
+
+// acc = (Xh + Xl)(Wh + Wl)^T for the block's 64 rows (dropping Xl Wl), scaled by s_x s_w
+template <int H, int KD = H, bool ZERO = true>
+__device__ __forceinline__ void mfma_layer_x3(const TileX3& X, const uint4* __restrict__ Wp, f32x16 (&acc)[RT][Geo<H>::CT],
+                                              int wave, int lane) {
+    constexpr int CT = Geo<H>::CT, S = GeoX3<KD>::S;
+    if constexpr (ZERO) {
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int c = 0; c < CT; ++c)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[rt][c][r] = 0.f;
+    }
+    const int aoff = (lane & 31) * X.ld + (lane >> 5) * 8;
+    // lane's 32 B of (ct, s): uint4 index ((ct S + s) 64 + lane) 2 + {0: hi, 1: lo}
+    const uint4* wb = Wp + ((size_t)(wave * CT) * S * 64 + lane) * 2;
+    auto wld = [&](int c, int s, int part) { return wb[((size_t)(c * S + s) * 64) * 2 + part]; };
+    uint4 bh0[CT], bl0[CT], bh1[CT], bl1[CT];
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+        bh0[c] = wld(c, 0, 0);
+        bl0[c] = wld(c, 0, 1);
+        bh1[c] = S > 1 ? wld(c, 1, 0) : bh0[c];
+        bl1[c] = S > 1 ? wld(c, 1, 1) : bl0[c];
+    }
+    for (int s = 0; s < S; ++s) {
+        f16x8 ah[RT], al[RT], bh[CT], bl[CT];
+#pragma unroll
+        for (int c = 0; c < CT; ++c) {   // weights: two steps in flight ahead of the MFMAs
+            bh[c] = __builtin_bit_cast(f16x8, bh0[c]);
+            bl[c] = __builtin_bit_cast(f16x8, bl0[c]);
+            bh0[c] = bh1[c];
+            bl0[c] = bl1[c];
+            if (s + 2 < S) {
+                bh1[c] = wld(c, s + 2, 0);
+                bl1[c] = wld(c, s + 2, 1);
+            }
+        }
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+            ah[rt] = *reinterpret_cast<const f16x8*>(X.h + aoff + rt * 32 * X.ld + 16 * s);
+            al[rt] = *reinterpret_cast<const f16x8*>(X.l + aoff + rt * 32 * X.ld + 16 * s);
+        }
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int c = 0; c < CT; ++c) {
+                acc[rt][c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[rt], bh[c], acc[rt][c], 0, 0, 0);
+                acc[rt][c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[rt], bl[c], acc[rt][c], 0, 0, 0);
+                acc[rt][c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[rt], bh[c], acc[rt][c], 0, 0, 0);
+            }
+    }
+}
+
+// Y = tanh(acc / (s_x s_w) + bias(i, n)), stored scaled by X3_SX as hi / lo
+template <int H, typename Bias>
+__device__ __forceinline__ void store_tanh_x3(const TileX3& Y, const f32x16 (&acc)[RT][Geo<H>::CT], float inv, int wave,
+                                              int lane, Bias bias) {
+    constexpr int CT = Geo<H>::CT;
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int c = 0; c < CT; ++c) {
+            const int n = acc_col<H>(wave, c, lane);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int i = acc_row(rt, r, lane);
+                Y.put(i, n, X3_SX * tanh_fast(fmaf(acc[rt][c][r], inv, bias(i, n))));
+            }
+        }
+}
+
+template <int H>
+constexpr size_t embed_x3_lds_bytes() {
+    return (size_t)(2 * MROWS * GeoX3<H>::LDH + 2 * MROWS * GeoX3<KD0>::LDH) * 2 + (size_t)2 * H * 4;
+}
+template <int H>
+constexpr size_t pool_x3_lds_bytes() {
+    return (size_t)(2 * MROWS * GeoX3<H>::LDH) * 2 + (size_t)(3 * MROWS + 4 * H) * 4;
+}
+
+// attn_embed_kernel with the split-f16 contraction (same inputs, same outputs: e2 rows and means in fp32)
+template <int H>
+__global__ __launch_bounds__(NTHR, 2) void attn_embed_x3_kernel(const float* __restrict__ obs, int stride, int so,
+                                                               int off, int B, int K, int nd, Towers tw) {
+    constexpr int LDH = GeoX3<H>::LDH, LD0 = GeoX3<KD0>::LDH, CT = Geo<H>::CT;
+    extern __shared__ float4 smem4[];
+    _Float16* xh = reinterpret_cast<_Float16*>(smem4);
+    const TileX3 X{xh, xh + MROWS * LDH, LDH};
+    const TileX3 X0{xh + 2 * MROWS * LDH, xh + 2 * MROWS * LDH + MROWS * LD0, LD0};
+    float* BI = reinterpret_cast<float*>(xh + 2 * MROWS * LDH + 2 * MROWS * LD0);   // b_e1, b_e2
+    const qs_attn_tower& t = tw.t[blockIdx.y];
+    const int AB = MROWS / K, MU = AB * K;
+    const long R = (long)B * K, row0 = (long)blockIdx.x * MU;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    for (int n = tid; n < H; n += NTHR) {
+        BI[n] = t.b_e1[n];
+        BI[H + n] = t.b_e2[n];
+    }
+    // layer 0's input rows [nbr_j (nd) | self_{j % B} (so) | 0 ...], row j = agent j / K, slot j % K; self half from
+    // agent j % B (the reference's row pairing)
+    for (int e = tid; e < MROWS * KD0; e += NTHR) {
+        const int r = e / KD0, c = e - r * KD0;
+        const int j = (int)row0 + r;
+        float v = 0.f;
+        if (r < MU && j < R) {
+            if (c < nd) v = obs[(size_t)(j / K) * stride + off + (j % K) * nd + c];
+            else if (c < nd + so) v = obs[(size_t)(j % B) * stride + (c - nd)];
+        }
+        X0.put(r, c, X3_SIN * v);
+    }
+    __syncthreads();
+    f32x16 acc[RT][CT];
+    mfma_layer_x3<H, KD0>(X0, reinterpret_cast<const uint4*>(t.w_e1p), acc, wave, lane);
+    store_tanh_x3<H>(X, acc, 1.f / (X3_SIN * X3_SW), wave, lane,
+                     [&](int i, int n) { return (i < MU && row0 + i < R) ? BI[n] : 0.f; });
+    __syncthreads();
+    mfma_layer_x3<H>(X, reinterpret_cast<const uint4*>(t.w_e2p), acc, wave, lane);
+    __syncthreads();   // every wave has read the tile
+    store_tanh_x3<H>(X, acc, 1.f / (X3_SX * X3_SW), wave, lane, [&](int, int n) { return BI[H + n]; });
+    __syncthreads();
+    constexpr float isx = 1.f / X3_SX;
+    for (int e = tid; e < MROWS * (H / 4); e += NTHR) {
+        const int r = e / (H / 4), c4 = e - r * (H / 4);
+        const long j = row0 + r;
+        if (r < MU && j < R)
+            reinterpret_cast<float4*>(t.e2 + j * H)[c4] =
+                make_float4(X.get(r, 4 * c4) * isx, X.get(r, 4 * c4 + 1) * isx, X.get(r, 4 * c4 + 2) * isx,
+                            X.get(r, 4 * c4 + 3) * isx);
+    }
+    const float inv = 1.f / (float)K;   // torch's mean: the sum times 1 / K
+    for (int e = tid; e < AB * H; e += NTHR) {
+        const int a = e / H, n = e - a * H;
+        const long agent = row0 / K + a;
+        if (agent < B) {
+            float s = 0.f;
+            for (int k = 0; k < K; ++k) s += X.get(a * K + k, n) * isx;
+            t.e_mean[agent * H + n] = s * inv;
+        }
+    }
+}
+
+// the block's e2 rows (fp32, HBM) into the split tile (zero rows past the data)
+template <int H>
+__device__ __forceinline__ void load_rows_x3(const TileX3& X, const float* __restrict__ src, long row0, int MU, long R,
+                                             int tid) {
+    constexpr int NV = MROWS * (H / 4) / NTHR;
+    float4 v[NV];
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+        const int e = tid + u * NTHR, r = e / (H / 4), c4 = e - r * (H / 4);
+        const long j = row0 + r;
+        v[u] = (r < MU && j < R) ? reinterpret_cast<const float4*>(src + j * H)[c4] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+        const int e = tid + u * NTHR, r = e / (H / 4), c4 = e - r * (H / 4);
+        X.put(r, 4 * c4, X3_SX * v[u].x);
+        X.put(r, 4 * c4 + 1, X3_SX * v[u].y);
+        X.put(r, 4 * c4 + 2, X3_SX * v[u].z);
+        X.put(r, 4 * c4 + 3, X3_SX * v[u].w);
+    }
+}
+
+// attn_pool_kernel with the split-f16 contraction
+template <int H>
+__global__ __launch_bounds__(NTHR, 2) void attn_pool_x3_kernel(int B, int K, Towers tw) {
+    constexpr int LDH = GeoX3<H>::LDH, CT = Geo<H>::CT;
+    extern __shared__ float4 smem4[];
+    _Float16* xh = reinterpret_cast<_Float16*>(smem4);
+    const TileX3 X{xh, xh + MROWS * LDH, LDH};
+    float* SC = reinterpret_cast<float*>(xh + 2 * MROWS * LDH);
+    float* WT = SC + MROWS;
+    float* A3 = WT + 2 * MROWS;                      // attention_mlp[4].weight, then b_a2, b_v1, b_v2
+    const qs_attn_tower& t = tw.t[blockIdx.y];
+    const int AB = MROWS / K, MU = AB * K;
+    const long R = (long)B * K, row0 = (long)blockIdx.x * MU;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    constexpr float SS = X3_SX * X3_SW, iSS = 1.f / SS, isx = 1.f / X3_SX;
+    for (int n = tid; n < H; n += NTHR) {
+        A3[n] = t.w_a3[n];
+        A3[H + n] = t.b_a2[n];
+        A3[2 * H + n] = t.b_v1[n];
+        A3[3 * H + n] = t.b_v2[n];
+    }
+    // attention_mlp: a1 = tanh(e2 A_e^T + P[j % B]): the accumulators start at P (scaled like the products)
+    f32x16 acc[RT][CT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int c = 0; c < CT; ++c) {
+            const int n = acc_col<H>(wave, c, lane);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int i = acc_row(rt, r, lane);
+                const int j = (int)row0 + i;
+                acc[rt][c][r] = (i < MU && j < R) ? SS * t.P[(size_t)(j % B) * H + n] : 0.f;
+            }
+        }
+    load_rows_x3<H>(X, t.e2, row0, MU, R, tid);
+    __syncthreads();
+    mfma_layer_x3<H, H, false>(X, reinterpret_cast<const uint4*>(t.w_a1ep), acc, wave, lane);
+    __syncthreads();
+    store_tanh_x3<H>(X, acc, iSS, wave, lane, [&](int, int) { return 0.f; });
+    __syncthreads();
+    mfma_layer_x3<H>(X, reinterpret_cast<const uint4*>(t.w_a2p), acc, wave, lane);
+    __syncthreads();
+    store_tanh_x3<H>(X, acc, iSS, wave, lane, [&](int, int n) { return A3[H + n]; });
+    __syncthreads();
+    {   // score = a2 . a3 + b_a3: 4 lanes per row
+        const int r = tid >> 2, qq = tid & 3;
+        float pp[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+        for (int m = 0; m < H / 4; ++m) {
+            const int n = 4 * m + qq;
+            pp[m & 3] = fmaf(X.get(r, n) * isx, A3[n], pp[m & 3]);
+        }
+        float p = (pp[0] + pp[1]) + (pp[2] + pp[3]);
+        p += __shfl_xor(p, 1);
+        p += __shfl_xor(p, 2);
+        if (qq == 0) SC[r] = p + t.b_a3;
+    }
+    __syncthreads();
+    if (tid < AB) {   // softmax over the agent's K rows
+        const int base = tid * K;
+        float m = SC[base];
+        for (int k = 1; k < K; ++k) m = fmaxf(m, SC[base + k]);
+        float s = 0.f;
+        for (int k = 0; k < K; ++k) {
+            const float x = expf(SC[base + k] - m);
+            WT[base + k] = x;
+            s += x;
+        }
+        for (int k = 0; k < K; ++k) WT[base + k] = WT[base + k] / s;
+    }
+    // neighbor_value_mlp on the e2 rows again (L2 / Infinity Cache)
+    load_rows_x3<H>(X, t.e2, row0, MU, R, tid);
+    __syncthreads();
+    mfma_layer_x3<H>(X, reinterpret_cast<const uint4*>(t.w_v1p), acc, wave, lane);
+    __syncthreads();
+    store_tanh_x3<H>(X, acc, iSS, wave, lane, [&](int, int n) { return A3[2 * H + n]; });
+    __syncthreads();
+    mfma_layer_x3<H>(X, reinterpret_cast<const uint4*>(t.w_v2p), acc, wave, lane);
+    __syncthreads();
+    // the weighted h rows into a plain fp32 tile over the same LDS (the split tile is no longer read)
+    float* Y = reinterpret_cast<float*>(smem4);
+    constexpr int LDY = H + 4;
+    static_assert(MROWS * (H + 4) * 4 <= 2 * MROWS * GeoX3<H>::LDH * 2, "fp32 tile fits the split tile's bytes");
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+        const int n = acc_col<H>(wave, c, lane);
+        const float bn = A3[3 * H + n];
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int i = acc_row(rt, r, lane);
+                Y[i * LDY + n] = i < MU ? WT[i] * tanh_fast(fmaf(acc[rt][c][r], iSS, bn)) : 0.f;
+            }
+    }
+    __syncthreads();
+    for (int e = tid; e < AB * H; e += NTHR) {
+        const int a = e / H, n = e - a * H;
+        const long agent = row0 / K + a;
+        if (agent < B) {
+            float s = 0.f;
+            for (int k = 0; k < K; ++k) s += Y[(a * K + k) * LDY + n];
+            t.out[agent * H + n] = s;
+        }
+    }
+}
+
+}  // namespace pol
+}  // namespace qs

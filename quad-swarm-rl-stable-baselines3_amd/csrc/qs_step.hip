@@ -39,6 +39,7 @@
 #include "qs_gae.h"
 #include "qs_curriculum.h"
 #include "qs_policy.h"
+#include "qs_policy_x3.h"
 #include "qs_replay.h"
 
 // =============================================================================================
@@ -1023,9 +1024,24 @@ static int attn_check(int32_t B, int32_t K, int32_t H, const qs_attn_tower* towe
 }
 template <int H>
 static int attn_launch(bool embed, const float* obs, int32_t stride, int32_t so, int32_t off, int32_t B, int32_t K,
-                       int32_t nd, const qs::pol::Towers& tw, int32_t n_towers, hipStream_t st) {
+                       int32_t nd, const qs::pol::Towers& tw, int32_t n_towers, hipStream_t st, bool x3 = false) {
     const int mu = (qs::pol::MROWS / K) * K;
     const dim3 grid((unsigned)(((long long)B * K + mu - 1) / mu), (unsigned)n_towers), block(qs::pol::NTHR);
+    if (x3) {   // the split-f16 contraction (qs_policy_x3.h)
+        if (embed) {
+            const size_t lds = qs::pol::embed_x3_lds_bytes<H>();
+            QS_HIP(hipFuncSetAttribute((const void*)qs::pol::attn_embed_x3_kernel<H>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            hipLaunchKernelGGL(qs::pol::attn_embed_x3_kernel<H>, grid, block, lds, st, obs, stride, so, off, B, K, nd, tw);
+        } else {
+            const size_t lds = qs::pol::pool_x3_lds_bytes<H>();
+            QS_HIP(hipFuncSetAttribute((const void*)qs::pol::attn_pool_x3_kernel<H>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            hipLaunchKernelGGL(qs::pol::attn_pool_x3_kernel<H>, grid, block, lds, st, B, K, tw);
+        }
+        QS_HIP(hipGetLastError());
+        return QS_OK;
+    }
     if (embed) {
         const size_t lds = qs::pol::embed_lds_bytes<H>();
         QS_HIP(hipFuncSetAttribute((const void*)qs::pol::attn_embed_kernel<H>,
@@ -1040,9 +1056,9 @@ static int attn_launch(bool embed, const float* obs, int32_t stride, int32_t so,
     QS_HIP(hipGetLastError());
     return QS_OK;
 }
-extern "C" int qs_attn_embed(const float* obs, int32_t obs_stride, int32_t self_dim, int32_t nbr_off, int32_t B,
-                             int32_t K, int32_t nd, int32_t H, const qs_attn_tower* towers, int32_t n_towers,
-                             void* stream) {
+static int attn_embed_impl(const float* obs, int32_t obs_stride, int32_t self_dim, int32_t nbr_off, int32_t B,
+                           int32_t K, int32_t nd, int32_t H, const qs_attn_tower* towers, int32_t n_towers,
+                           void* stream, bool x3) {
     int rc = attn_check(B, K, H, towers, n_towers);
     if (rc) return rc;
     if (!obs) return fail(QS_E_INVALID, "NULL obs");
@@ -1058,11 +1074,21 @@ extern "C" int qs_attn_embed(const float* obs, int32_t obs_stride, int32_t self_
         tw.t[i] = t;
     }
     hipStream_t st = (hipStream_t)stream;
-    return H == 256 ? attn_launch<256>(true, obs, obs_stride, self_dim, nbr_off, B, K, nd, tw, n_towers, st)
-                    : attn_launch<128>(true, obs, obs_stride, self_dim, nbr_off, B, K, nd, tw, n_towers, st);
+    return H == 256 ? attn_launch<256>(true, obs, obs_stride, self_dim, nbr_off, B, K, nd, tw, n_towers, st, x3)
+                    : attn_launch<128>(true, obs, obs_stride, self_dim, nbr_off, B, K, nd, tw, n_towers, st, x3);
 }
-extern "C" int qs_attn_pool(int32_t B, int32_t K, int32_t H, const qs_attn_tower* towers, int32_t n_towers,
-                            void* stream) {
+extern "C" int qs_attn_embed(const float* obs, int32_t obs_stride, int32_t self_dim, int32_t nbr_off, int32_t B,
+                             int32_t K, int32_t nd, int32_t H, const qs_attn_tower* towers, int32_t n_towers,
+                             void* stream) {
+    return attn_embed_impl(obs, obs_stride, self_dim, nbr_off, B, K, nd, H, towers, n_towers, stream, false);
+}
+extern "C" int qs_attn_embed_x3(const float* obs, int32_t obs_stride, int32_t self_dim, int32_t nbr_off, int32_t B,
+                                int32_t K, int32_t nd, int32_t H, const qs_attn_tower* towers, int32_t n_towers,
+                                void* stream) {
+    return attn_embed_impl(obs, obs_stride, self_dim, nbr_off, B, K, nd, H, towers, n_towers, stream, true);
+}
+static int attn_pool_impl(int32_t B, int32_t K, int32_t H, const qs_attn_tower* towers, int32_t n_towers,
+                          void* stream, bool x3) {
     int rc = attn_check(B, K, H, towers, n_towers);
     if (rc) return rc;
     qs::pol::Towers tw{};
@@ -1073,8 +1099,16 @@ extern "C" int qs_attn_pool(int32_t B, int32_t K, int32_t H, const qs_attn_tower
             return fail(QS_E_INVALID, "NULL stage-2 tower pointer");
         tw.t[i] = t;
     }
-    return H == 256 ? attn_launch<256>(false, nullptr, 0, 0, 0, B, K, 0, tw, n_towers, (hipStream_t)stream)
-                    : attn_launch<128>(false, nullptr, 0, 0, 0, B, K, 0, tw, n_towers, (hipStream_t)stream);
+    return H == 256 ? attn_launch<256>(false, nullptr, 0, 0, 0, B, K, 0, tw, n_towers, (hipStream_t)stream, x3)
+                    : attn_launch<128>(false, nullptr, 0, 0, 0, B, K, 0, tw, n_towers, (hipStream_t)stream, x3);
+}
+extern "C" int qs_attn_pool(int32_t B, int32_t K, int32_t H, const qs_attn_tower* towers, int32_t n_towers,
+                            void* stream) {
+    return attn_pool_impl(B, K, H, towers, n_towers, stream, false);
+}
+extern "C" int qs_attn_pool_x3(int32_t B, int32_t K, int32_t H, const qs_attn_tower* towers, int32_t n_towers,
+                               void* stream) {
+    return attn_pool_impl(B, K, H, towers, n_towers, stream, true);
 }
 
 // the kernel parameter block a config produces (host only; runtime specialisation / diagnostics)

@@ -149,7 +149,8 @@ EXPORTS = ["qs_abi_version", "qs_last_error", "qs_struct_sizes", "qs_config_defa
            "qs_get_param", "qs_state_bytes", "qs_get_state", "qs_set_state", "qs_gae",
            "qs_specialize", "qs_is_specialized", "qs_config_kp_words", "qs_specialize_compile",
            "qs_replay_config_default", "qs_replay_workspace_bytes", "qs_replay_enable", "qs_replay_disable", "qs_replay_buffers_get",
-           "qs_attn_embed", "qs_attn_pool", "qs_curriculum_init", "qs_curriculum_step"]
+           "qs_attn_embed", "qs_attn_pool", "qs_attn_embed_x3", "qs_attn_pool_x3", "qs_curriculum_init",
+           "qs_curriculum_step"]
 
 _lib = None
 
@@ -186,6 +187,8 @@ def lib():
         "qs_replay_buffers_get": ([V, P(QsReplayBuffers)], I32),
         "qs_attn_embed": ([V, I32, I32, I32, I32, I32, I32, I32, P(QsAttnTower), I32, V], I32),
         "qs_attn_pool": ([I32, I32, I32, P(QsAttnTower), I32, V], I32),
+        "qs_attn_embed_x3": ([V, I32, I32, I32, I32, I32, I32, I32, P(QsAttnTower), I32, V], I32),
+        "qs_attn_pool_x3": ([I32, I32, I32, P(QsAttnTower), I32, V], I32),
         "qs_curriculum_init": ([V, ctypes.c_double, ctypes.c_double, ctypes.c_double, I32], I32),
         "qs_curriculum_step": ([V, V, V], I32),
     }

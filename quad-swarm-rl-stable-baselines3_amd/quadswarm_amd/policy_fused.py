@@ -28,6 +28,24 @@ def pack_mfma_weight(w):
     return w.detach().float().contiguous().view(n // 32, 32, 2, kd // 8, 4).permute(0, 3, 2, 1, 4).contiguous()
 
 
+X3_SW = 256.0   # weight scale of the split-f16 packing (csrc/qs_policy_x3.h X3_SW)
+
+
+def pack_mfma_weight_x3(w):
+    """[N, Kd] fp32 weight -> the split-f16 operand layout of qs_attn_embed_x3 / qs_attn_pool_x3 (quadswarm.h):
+    packed[ct][s][l] = 8 halves of hi(256 W[32 ct + (l & 31)][16 s + 8 (l >> 5) + j]), then the 8 lo halves,
+    hi = f16(256 w), lo = f16(256 w - hi).  Returned as an int16 tensor [N/32, Kd/16, 64, 2, 8]."""
+    n, kd = w.shape
+    assert n % 32 == 0 and kd % 16 == 0, (n, kd)
+    ws = w.detach().float() * X3_SW
+    hi = ws.half()
+    lo = (ws - hi.float()).half()
+
+    def lay(x):   # [n, kd] -> [ct, s, h, r, j] -> [ct, s, l = 32 h + r, j]
+        return x.contiguous().view(n // 32, 32, kd // 16, 2, 8).permute(0, 2, 3, 1, 4).reshape(n // 32, kd // 16, 64, 8)
+    return torch.stack((lay(hi), lay(lo)), dim=3).contiguous().view(torch.int16)
+
+
 def supports(policy):
     """Can the fused kernels evaluate this policy's encoders?"""
     c = policy.cfg
@@ -41,7 +59,15 @@ class FusedRolloutPolicy:
     refresh() re-packs the weights: call it whenever the policy's parameters changed (PPOTrainer does,
     once per rollout)."""
 
-    def __init__(self, policy):
+    PRECISIONS = ("fp32", "x3")
+
+    def __init__(self, policy, precision="fp32"):
+        """precision "fp32": fp32 operands on the fp32 matrix cores (v_mfma_f32_32x32x2f32); "x3": every fp32 product
+        as three f16 products (hi/lo split, fp32 accumulation, ~7e-7 relative per product) on the f16 matrix cores
+        (csrc/qs_policy_x3.h), 5.3x the contraction rate."""
+        if precision not in self.PRECISIONS:
+            raise ValueError(f"precision must be one of {self.PRECISIONS}")
+        self.precision = precision
         if not supports(policy):
             raise ValueError("fused rollout forward: needs the tanh attention encoder with hidden size 128 or 256")
         self.policy = policy
@@ -59,6 +85,7 @@ class FusedRolloutPolicy:
     # ---- weights / buffers ----
     def refresh(self):
         H, so = self.H, self.so
+        pack = pack_mfma_weight_x3 if self.precision == "x3" else pack_mfma_weight
         packed = []
         for enc in self.encs:
             ne = enc.neighbor_encoder
@@ -68,13 +95,13 @@ class FusedRolloutPolicy:
             w_e1[:, :self.nd] = w0[:, so:]
             w_e1[:, self.nd:self.nd + so] = w0[:, :so]
             packed.append(dict(
-                w_e1p=pack_mfma_weight(w_e1), b_e1=emb[0].bias.detach(),
-                w_e2p=pack_mfma_weight(emb[2].weight), b_e2=emb[2].bias.detach(),
-                w_v1p=pack_mfma_weight(val[0].weight), b_v1=val[0].bias.detach(),
-                w_v2p=pack_mfma_weight(val[2].weight), b_v2=val[2].bias.detach(),
-                w_a1ep=pack_mfma_weight(att[0].weight[:, :H]), w_a1m=att[0].weight[:, H:].detach(),
+                w_e1p=pack(w_e1), b_e1=emb[0].bias.detach(),
+                w_e2p=pack(emb[2].weight), b_e2=emb[2].bias.detach(),
+                w_v1p=pack(val[0].weight), b_v1=val[0].bias.detach(),
+                w_v2p=pack(val[2].weight), b_v2=val[2].bias.detach(),
+                w_a1ep=pack(att[0].weight[:, :H]), w_a1m=att[0].weight[:, H:].detach(),
                 b_a1=att[0].bias.detach(),
-                w_a2p=pack_mfma_weight(att[2].weight), b_a2=att[2].bias.detach(),
+                w_a2p=pack(att[2].weight), b_a2=att[2].bias.detach(),
                 w_a3=att[4].weight.detach().reshape(-1).contiguous(), b_a3=float(att[4].bias.detach().item())))
         self.packed = packed
         self._bind()
@@ -113,11 +140,13 @@ class FusedRolloutPolicy:
             self._alloc(B, obs.device)
         so, H, K = self.so, self.H, self.K
         st = ctypes.c_void_p(torch.cuda.current_stream(obs.device).cuda_stream)
-        NAT.check(self.L.qs_attn_embed(ctypes.c_void_p(obs.data_ptr()), obs.shape[1], so, so, B, K, self.nd, H,
-                                       self.towers, len(self.encs), st), "qs_attn_embed")
+        x3 = self.precision == "x3"
+        embed, pool = (self.L.qs_attn_embed_x3, self.L.qs_attn_pool_x3) if x3 else (self.L.qs_attn_embed, self.L.qs_attn_pool)
+        NAT.check(embed(ctypes.c_void_p(obs.data_ptr()), obs.shape[1], so, so, B, K, self.nd, H,
+                        self.towers, len(self.encs), st), "qs_attn_embed")
         for i, w in enumerate(self.packed):
             torch.addmm(w["b_a1"], self.e_mean[i], w["w_a1m"].t(), out=self.P[i])
-        NAT.check(self.L.qs_attn_pool(B, K, H, self.towers, len(self.encs), st), "qs_attn_pool")
+        NAT.check(pool(B, K, H, self.towers, len(self.encs), st), "qs_attn_pool")
         return self.out
 
     def _encode(self, enc, obs, nbr_out):

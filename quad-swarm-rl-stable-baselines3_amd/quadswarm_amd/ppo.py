@@ -441,7 +441,7 @@ class PPOTrainer:
     the trainer on a CPU stand-in env; the default is the HIP kernel."""
 
     def __init__(self, env, policy: SwarmActorCritic, cfg: PPOConfig = None, device=None, seed=0,
-                 gae_fn=None, group=None, fused_rollout=True):
+                 gae_fn=None, group=None, fused_rollout=True, rollout_precision="fp32"):
         import torch.distributed as dist
 
         self.env, self.policy, self.cfg = env, policy, cfg or PPOConfig()
@@ -470,7 +470,7 @@ class PPOTrainer:
         if fused_rollout and self.device.type == "cuda":
             from .policy_fused import FusedRolloutPolicy, supports
             if supports(policy):
-                self.fused = FusedRolloutPolicy(policy)
+                self.fused = FusedRolloutPolicy(policy, precision=rollout_precision)
 
     def reset(self):
         self.last_obs = self.env.reset()

@@ -56,12 +56,17 @@ def obs_for(pc, B, seed=1):
     return torch.randn(B, od, device="cuda", generator=g) * 2.0
 
 
+PRECISIONS = ["fp32", "x3"]
+
+
+@pytest.mark.parametrize("precision", PRECISIONS)
 @pytest.mark.parametrize("case,B", [("c3", 4096), ("c3", 1003), ("a8", 2050), ("k1", 777), ("k64", 130),
                                     ("k31obst", 257)])
-def test_neighbor_encodings_match_torch(case, B):
+def test_neighbor_encodings_match_torch(case, B, precision):
+    """x3 (split f16 products, csrc/qs_policy_x3.h) is held to the same bound as the fp32 matrix cores."""
     pol = make_policy(case)
     assert supports(pol)
-    fp = FusedRolloutPolicy(pol)
+    fp = FusedRolloutPolicy(pol, precision=precision)
     obs = obs_for(pol.cfg, B)
     got = fp.neighbor_encodings(obs).clone()
     so, K = pol.cfg.self_obs_dim, pol.cfg.num_use_neighbor_obs
@@ -74,10 +79,11 @@ def test_neighbor_encodings_match_torch(case, B):
             assert want.abs().max().item() > 0.05   # a non-trivial output
 
 
+@pytest.mark.parametrize("precision", PRECISIONS)
 @pytest.mark.parametrize("case", ["c3", "a8", "k31obst"])
-def test_fused_forward_matches_policy(case):
+def test_fused_forward_matches_policy(case, precision):
     pol = make_policy(case, seed=3)
-    fp = FusedRolloutPolicy(pol)
+    fp = FusedRolloutPolicy(pol, precision=precision)
     obs = obs_for(pol.cfg, 3000, seed=4)
     a_f, v_f, lp_f = fp(obs, deterministic=True)
     with torch.no_grad():
@@ -118,8 +124,9 @@ def test_trainer_rollout_uses_fused_forward():
     assert np.isfinite(stats["loss"])
 
 
+@pytest.mark.parametrize("precision", PRECISIONS)
 @pytest.mark.parametrize("case", ["c3", "a8"])
-def test_fused_rollout_log_probs_match_evaluate_actions(case):
+def test_fused_rollout_log_probs_match_evaluate_actions(case, precision):
     """The rollout stores the fused path's log-probs; PPO's first epoch divides the torch module's
     evaluate_actions log-probs of the same (obs, actions) by them.  At a small std (exp(log_std) = 0.05, a late
     training stage) the log-prob amplifies a mean difference by z / std, so this bounds the ratio PPO sees
@@ -128,20 +135,21 @@ def test_fused_rollout_log_probs_match_evaluate_actions(case):
     pol = make_policy(case, seed=5)
     with torch.no_grad():
         pol.log_std.fill_(math.log(0.05))
-    fp = FusedRolloutPolicy(pol)
+    fp = FusedRolloutPolicy(pol, precision=precision)
     obs = obs_for(pol.cfg, 4096, seed=6)
     torch.manual_seed(7)
     a_f, v_f, lp_f = fp(obs)
     with torch.no_grad():
         v_t, lp_t, _ = pol.evaluate_actions(obs, a_f)
     dev = (torch.exp(lp_t - lp_f) - 1).abs()
-    print(f"{case}: ratio deviation max {dev.max().item():.3e} mean {dev.mean().item():.3e}")
+    print(f"{case} {precision}: ratio deviation max {dev.max().item():.3e} mean {dev.mean().item():.3e}")
     assert dev.max().item() < 2e-3 and dev.mean().item() < 2e-4
     assert (v_t.view(-1) - v_f.view(-1)).abs().max().item() < 2e-4
 
 
+@pytest.mark.parametrize("precision", PRECISIONS)
 @pytest.mark.parametrize("case", ["c3", "a8", "c4"])
-def test_fused_policy_matches_reference_fixture(case):
+def test_fused_policy_matches_reference_fixture(case, precision):
     """The fused rollout forward against the reference's own policy module: tests/golden/policy_<case> (written by
     tools/gen_golden_policy.py from swarm_rl/models/ActorCriticPolicyCustom.py + quad_multi_model.py), weights
     loaded under the reference's parameter names."""
@@ -150,11 +158,12 @@ def test_fused_policy_matches_reference_fixture(case):
     pol = SwarmActorCritic(pc).cuda().eval()
     pol.load_reference_state_dict(reference_weights(meta, torch.float32))
     assert supports(pol)
-    fp = FusedRolloutPolicy(pol)
+    fp = FusedRolloutPolicy(pol, precision=precision)
     obs = torch.from_numpy(data["obs"].astype(np.float32)).cuda()
     nbr = fp.neighbor_encodings(obs)
     for i, tw in enumerate(("actor", "critic")):
         err = np.abs(nbr[i].cpu().numpy() - data[f"{tw}_nbr64"]).max()
+        print(f"{case} {precision} {tw}: max |encoder - reference fp64| {err:.2e}")
         assert err < ATOL, (case, tw, err)
     a, v, lp = fp(obs, deterministic=True)
     np.testing.assert_allclose(a.cpu().numpy(), data["det_actions32"], rtol=0, atol=2e-4)

@@ -49,3 +49,24 @@ def test_abi_argument_checks():
     assert b"self features" in L.qs_last_error()
     assert L.qs_attn_embed(ctypes.c_void_p(16), 54, 30, 18, 4096, 6, 6, 256, towers, 1, None) == -1
     assert b"<= 32" in L.qs_last_error()
+
+
+def test_pack_x3_layout_and_split_accuracy():
+    """pack_mfma_weight_x3: lane l of (column tile ct, step s) holds hi / lo halves of
+    256 W[32 ct + (l & 31)][16 s + 8 (l >> 5) + j]; (hi + lo) / 256 reproduces W to 2^-22 relative."""
+    import torch
+    from quadswarm_amd.policy_fused import pack_mfma_weight_x3
+    g = torch.Generator().manual_seed(3)
+    w = (torch.rand(64, 48, generator=g) * 2 - 1) * 0.2
+    w[0, 0], w[1, 1] = 1e-6, -3.5          # tiny and large entries
+    p = pack_mfma_weight_x3(w).view(torch.float16).float()   # [ct, s, l, part, j]
+    assert p.shape == (2, 3, 64, 2, 8)
+    for ct in range(2):
+        for s in range(3):
+            for lane in (0, 5, 31, 32, 63):
+                n, k0 = 32 * ct + (lane & 31), 16 * s + 8 * (lane >> 5)
+                rec = (p[ct, s, lane, 0] + p[ct, s, lane, 1]) / 256.0
+                want = w[n, k0:k0 + 8]
+                # (lo below the f16 normal range: an absolute floor of half its subnormal spacing 2^-24, / 256)
+                assert torch.all((rec - want).abs() <= 2.0 ** -21 * want.abs() + 2.0 ** -25 / 256), (ct, s, lane)
+                assert torch.equal(p[ct, s, lane, 0], (want * 256.0).half().float())

@@ -134,6 +134,12 @@ for s in "$@"; do
       CONFIG=c5 STEPS=2000 step sel2_ab 600 bash tools/ab_jit.sh base: sel2:-DQS_NBR_SELECT2=1 base2: sel2b:-DQS_NBR_SELECT2=1
       ;;
     stamps) step stamps 300 python tools/phase_stamps.py ;;
+    profpol)   # the rollout policy's kernels (C3): kernel trace + one PMC pass of MFMA counters on the fused encoders
+      export TMPDIR=/tmp
+      step profpol_kt 300 rocprofv3 --kernel-trace --stats -d gpurun_out/profpol_kt -o kt --output-format csv -- python tools/rollout_prof.py c3
+      step profpol_pmc 200 timeout -s KILL 180 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE --kernel-include-regex attn -d gpurun_out/profpol_pmc -o p --output-format csv -- python tools/rollout_prof.py c3
+      rm -f gpurun_out/profpol_*/*kernel_trace.csv gpurun_out/profpol_*/*/*kernel_trace.csv
+      ;;
     n128) step gpu_tests_n128 900 python -u -m pytest tests/test_gpu_n128.py -x -v --timeout 300 --timeout-method thread ;;
     benchn128) step bench_n128 300 python bench.py --config n128 --steps 500 --cpu-seconds 5 --e2e-iters 0 ;;
     prioab)    # the younger-wave priority flip (QS_PRIO_AT, default 11) against off, per config

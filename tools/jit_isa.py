@@ -42,7 +42,8 @@ def main():
         f = os.path.join(d, "jit.hip")
         open(f, "w").write(src)
         subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=on",
-                        "-munsafe-fp-atomics", "--cuda-device-only", "-S", "-I", os.path.join(PKG, "csrc"), "-I",
+                        "-munsafe-fp-atomics", "--cuda-device-only", "-S", "-I",
+                        os.environ.get("QS_JIT_SRC_DIR", os.path.join(PKG, "csrc")), "-I",
                         os.path.join(ROOT, "include"), f, "-o", out], check=True)
     text = open(out).read()
     body = text[text.index(".text"):]

@@ -50,8 +50,15 @@ def main():
         from quadswarm_amd.policy_fused import FusedRolloutPolicy
         fp = FusedRolloutPolicy(pol)
         fp.refresh()
+        fx = FusedRolloutPolicy(pol, precision="x3")
+        fx.refresh()
         rows += [("fused policy forward (actor+critic)", lambda: fp(obs)),
-                 ("  fused neighbour encoders (both towers)", lambda: fp.neighbor_encodings(obs))]
+                 ("  fused neighbour encoders (both towers)", lambda: fp.neighbor_encodings(obs)),
+                 ("fused policy forward, x3 (split f16)", lambda: fx(obs)),
+                 ("  fused neighbour encoders, x3", lambda: fx.neighbor_encodings(obs))]
+        e32 = fp.neighbor_encodings(obs).clone()
+        ex3 = fx.neighbor_encodings(obs).clone()
+        print(f"max |x3 - fp32| encoder outputs: {(e32 - ex3).abs().max().item():.3e}")
         for name, fn in rows:
             print(f"{name:42s} {timed(fn):8.3f} ms")
 

@@ -65,7 +65,14 @@ def main():
             if cname == kind:
                 calib[f"{short}:{kind}"] = (sorted(v)[len(v) // 2] * 1024.0) / CALIB_BYTES
 
-    res = {"kernel": stats.get("name"), "config": args.config, "kernel_trace": stats, "calibration_ratio": calib}
+    import subprocess
+    try:   # the tree the profiles were taken on (gpurun snapshots the working tree: dirty = uncommitted edits)
+        head = subprocess.run(["git", "-C", ROOT, "describe", "--always", "--dirty"], capture_output=True,
+                              text=True).stdout.strip()
+    except OSError:
+        head = None
+    res = {"kernel": stats.get("name"), "config": args.config, "tree": head, "kernel_trace": stats,
+           "calibration_ratio": calib}
     for pat in ("_fetch/*counter_collection.csv", "_write/*counter_collection.csv", "_sq/*counter_collection.csv"):
         for (kname, cname), v in counters(args.prefix + pat, args.kernel).items():
             if not (args.kernel + "<" in kname or args.kernel + "I" in kname):
