@@ -137,7 +137,7 @@ for s in "$@"; do
     profpol)   # the rollout policy's kernels (C3): kernel trace + one PMC pass of MFMA counters on the fused encoders
       export TMPDIR=/tmp
       step profpol_kt 300 rocprofv3 --kernel-trace --stats -d gpurun_out/profpol_kt -o kt --output-format csv -- python tools/rollout_prof.py c3
-      step profpol_pmc 200 timeout -s KILL 180 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE --kernel-include-regex attn -d gpurun_out/profpol_pmc -o p --output-format csv -- python tools/rollout_prof.py c3
+      step profpol_pmc 200 timeout -s KILL 180 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE --kernel-include-regex attn -d gpurun_out/profpol_pmc -o p --output-format csv -- python tools/rollout_prof.py c3
       rm -f gpurun_out/profpol_*/*kernel_trace.csv gpurun_out/profpol_*/*/*kernel_trace.csv
       ;;
     n128) step gpu_tests_n128 900 python -u -m pytest tests/test_gpu_n128.py -x -v --timeout 300 --timeout-method thread ;;
