@@ -98,3 +98,15 @@ def test_two_rank_aggregate_sum_over_max():
         assert total == 3000.0 and tmax == 3.0      # every rank sees the same aggregate
         assert per_rank == [500.0, 2000.0 / 3.0]
     assert bench.aggregate_ranks(500, 2.0, 1) == (500.0, 2.0, [250.0])
+
+
+def test_state_complete_bytes():
+    """The state-complete count adds to §8d's bytes what the reference's step also carries (istate words sized per
+    swarm, the episode-stats words, the env words per drone): C2 / C3 / C5 / 128-drone values."""
+    want = {"c2": (433.0, 216.0), "c3": (555.0, 197.0), "c5": (550.5, 193.25), "n128": (573.375, 204.3125)}
+    for c, (b, r) in want.items():
+        cfg = bench.make_cfg(bench.CONFIGS[c])
+        got = bench.state_bytes_per_agent_step(cfg)
+        assert abs(got[0] - b) < 1e-6 and abs(got[1] - r) < 1e-6, (c, got)
+        base = bench.algorithmic_bytes_per_agent_step(cfg.obs_dim, cfg.num_agents, cfg.flavor)
+        assert got[0] > base
