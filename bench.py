@@ -499,8 +499,9 @@ def main(argv=None):
     ap.add_argument("--e2e-steps", type=int, default=0, help="override the PPO rollout length n_steps")
     ap.add_argument("--e2e-unfused", action="store_true",
                     help="A/B only: the rollout evaluates the torch policy module instead of the fused encoders")
-    ap.add_argument("--e2e-precision", choices=["fp32", "x3"], default="fp32",
-                    help="fused rollout encoders: fp32 matrix cores, or each fp32 product as 3 f16 products (x3)")
+    ap.add_argument("--e2e-precision", choices=["fp32", "x3"], default="x3",
+                    help="fused rollout encoders: fp32 matrix cores, or each fp32 product as 3 f16 products with fp32 "
+                         "accumulation (x3, the default: within 2e-7 of fp32 on the encoder outputs, DESIGN.md §4.6)")
     ap.add_argument("--host-sync", choices=["spin", "auto"], default="auto",
                     help="host wait of torch.cuda.synchronize(): spin (hipDeviceScheduleSpin) or HIP's default")
     args = ap.parse_args(argv)

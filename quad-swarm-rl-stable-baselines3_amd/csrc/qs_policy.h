@@ -72,7 +72,7 @@ __device__ __forceinline__ float f4at(const float4& v, int u) {
 // acc = X W^T for the block's 64 rows (X: LDS [64][LD]); W packed: float4 index ((ct G + g) 64 + lane) holds
 // W[ct 32 + (lane & 31)][(lane >> 5) H/2 + 4g .. + 3].
 struct ZeroInit {
-    __device__ float operator()(int, int) const { return 0.f; }
+    __device__ float4 operator()(int, int) const { return make_float4(0.f, 0.f, 0.f, 0.f); }
 };
 // (init(i, n): the accumulators' starting value, e.g. a per-row bias; 0 by default)
 // KD: the contraction size (the layer's input width; the tile X has row stride KD + 4).  ZERO: start the
@@ -114,42 +114,80 @@ __device__ __forceinline__ void mfma_layer(const float* X, const float4* __restr
             a[rt] = an[rt];
             if (g + 1 < G) an[rt] = *reinterpret_cast<const float4*>(xa + rt * 32 * LD + 4 * (g + 1));
         }
+        __builtin_amdgcn_sched_barrier(0);   // keep the loads ahead of the MFMAs (qs_policy_x3.h mfma_layer_x3)
 #pragma unroll
         for (int u = 0; u < 4; ++u)
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
                 for (int c = 0; c < CT; ++c)
-                    acc[rt][c] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4at(a[rt], u), f4at(b[c], u), acc[rt][c], 0, 0, 0);
+                    acc[rt][c] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4at(b[c], u), f4at(a[rt], u), acc[rt][c], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
     }
 }
 
-// the accumulator element r of tile (rt, c) on this lane: row and column of the block's output
-__device__ __forceinline__ int acc_row(int rt, int r, int lane) { return rt * 32 + 8 * (r >> 2) + 4 * (lane >> 5) + (r & 3); }
+// The weights are the MFMA's A operand and the activations its B operand, so a 32 x 32 result tile is
+// [output column][row]: the block row i is on the lane, and registers 4g .. 4g + 3 of tile (rt, c) hold four
+// consecutive output columns n0 .. n0 + 3 -- an epilogue writes them as one float4 (or four packed halves).
+__device__ __forceinline__ int acc_i(int rt, int lane) { return rt * 32 + (lane & 31); }
 template <int H>
-__device__ __forceinline__ int acc_col(int wave, int c, int lane) { return (wave * Geo<H>::CT + c) * 32 + (lane & 31); }
+__device__ __forceinline__ int acc_n0(int wave, int c, int g, int lane) {
+    return (wave * Geo<H>::CT + c) * 32 + 8 * g + 4 * (lane >> 5);
+}
+__device__ __forceinline__ float4 f4_add(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
+__device__ __forceinline__ float4 f4_tanh(float4 a) {
+    return make_float4(tanh_fast(a.x), tanh_fast(a.y), tanh_fast(a.z), tanh_fast(a.w));
+}
+__device__ __forceinline__ float4 acc4(const f32x16& a, int g) { return make_float4(a[4 * g], a[4 * g + 1], a[4 * g + 2], a[4 * g + 3]); }
 
-// Y[i][n] = tanh(acc + bias(i, n)) into LDS
-template <int H, typename Bias>
-__device__ __forceinline__ void store_tanh(float* Y, const f32x16 (&acc)[RT][Geo<H>::CT], int wave, int lane, Bias bias) {
+// Y[i][n0 .. n0 + 3] = tanh(acc + bias4(i, n0)) into LDS
+template <int H, typename Bias4>
+__device__ __forceinline__ void store_tanh(float* Y, const f32x16 (&acc)[RT][Geo<H>::CT], int wave, int lane, Bias4 bias4) {
     constexpr int CT = Geo<H>::CT, LD = Geo<H>::LD;
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt)
+    for (int rt = 0; rt < RT; ++rt) {
+        const int i = acc_i(rt, lane);
 #pragma unroll
-        for (int c = 0; c < CT; ++c) {
-            const int n = acc_col<H>(wave, c, lane);
+        for (int c = 0; c < CT; ++c)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int i = acc_row(rt, r, lane);
-                Y[i * LD + n] = tanh_fast(acc[rt][c][r] + bias(i, n));
+            for (int g = 0; g < 4; ++g) {
+                const int n0 = acc_n0<H>(wave, c, g, lane);
+                *reinterpret_cast<float4*>(Y + i * LD + n0) = f4_tanh(f4_add(acc4(acc[rt][c], g), bias4(i, n0)));
             }
-        }
+    }
+}
+__device__ __forceinline__ float4 lds4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+// score = tanh(acc * inv + b_a2) . a3 straight from the a2 layer's accumulators (a2 itself is never stored): this
+// lane's part of row i's dot, summed with the other lane half (same row, other columns); SCP[wave][i] = the wave's
+// column range.  The caller adds the 4 waves' parts after a barrier.
+template <int H>
+__device__ __forceinline__ void score_partials(const f32x16 (&acc)[RT][Geo<H>::CT], float inv, const float* a3,
+                                               const float* ba2, float* SCP, int wave, int lane) {
+    constexpr int CT = Geo<H>::CT;
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+        float p = 0.f;
+#pragma unroll
+        for (int c = 0; c < CT; ++c)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int n0 = acc_n0<H>(wave, c, g, lane);
+                const float4 b = lds4(ba2 + n0), w = lds4(a3 + n0);
+                p = fmaf(tanh_fast(fmaf(acc[rt][c][4 * g], inv, b.x)), w.x, p);
+                p = fmaf(tanh_fast(fmaf(acc[rt][c][4 * g + 1], inv, b.y)), w.y, p);
+                p = fmaf(tanh_fast(fmaf(acc[rt][c][4 * g + 2], inv, b.z)), w.z, p);
+                p = fmaf(tanh_fast(fmaf(acc[rt][c][4 * g + 3], inv, b.w)), w.w, p);
+            }
+        p += __shfl_xor(p, 32);
+        if (lane < 32) SCP[wave * MROWS + acc_i(rt, lane)] = p;
+    }
 }
 
 template <int H>
 constexpr size_t embed_lds_bytes() { return (size_t)(MROWS * Geo<H>::LD + MROWS * LD0 + 2 * H) * 4; }
 template <int H>
-constexpr size_t pool_lds_bytes() { return (size_t)(MROWS * Geo<H>::LD + 3 * MROWS + 4 * H) * 4; }
+constexpr size_t pool_lds_bytes() { return (size_t)(MROWS * Geo<H>::LD + 3 * MROWS + 4 * H + NWAVE * MROWS) * 4; }
 
 // e1 -> e2 for the block's rows (both layers on the matrix cores); e2 rows and the per-agent mean of e2 to HBM
 template <int H>
@@ -188,14 +226,16 @@ __global__ __launch_bounds__(NTHR, 2) void attn_embed_kernel(const float* __rest
     f32x16 acc[RT][CT];
     {   // e1 = tanh([nbr | self] [W_n | W_s]^T + b_e1): a KD0-deep layer on the matrix cores
         mfma_layer<H, KD0>(X0, reinterpret_cast<const float4*>(t.w_e1p), acc, wave, lane);
-        store_tanh<H>(X, acc, wave, lane, [&](int i, int n) { return (i < MU && row0 + i < R) ? BI[n] : 0.f; });
+        store_tanh<H>(X, acc, wave, lane, [&](int i, int n0) {
+            return (i < MU && row0 + i < R) ? lds4(BI + n0) : make_float4(0.f, 0.f, 0.f, 0.f);
+        });
     }
     __syncthreads();
     QS_STAMP(2);
     mfma_layer<H>(X, reinterpret_cast<const float4*>(t.w_e2p), acc, wave, lane);
     QS_STAMP(3);
     __syncthreads();   // every wave has read the tile
-    store_tanh<H>(X, acc, wave, lane, [&](int, int n) { return BI[H + n]; });
+    store_tanh<H>(X, acc, wave, lane, [&](int, int n0) { return lds4(BI + H + n0); });
     __syncthreads();
     QS_STAMP(4);
     for (int e = tid; e < MROWS * (H / 4); e += NTHR) {
@@ -228,7 +268,10 @@ __device__ __forceinline__ void load_rows(float* X, const float* __restrict__ sr
     for (int u = 0; u < NV; ++u) {
         const int e = tid + u * NTHR, r = e / (H / 4), c4 = e - r * (H / 4);
         const long j = row0 + r;
-        v[u] = (r < MU && j < R) ? reinterpret_cast<const float4*>(src + j * H)[c4] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const bool ok = r < MU && j < R;
+        const float okf = ok ? 1.f : 0.f;
+        v[u] = reinterpret_cast<const float4*>(src + (ok ? j : 0) * H)[c4];   // unconditional (see the P loads)
+        v[u] = make_float4(v[u].x * okf, v[u].y * okf, v[u].z * okf, v[u].w * okf);
     }
 #pragma unroll
     for (int u = 0; u < NV; ++u) {
@@ -264,17 +307,25 @@ __global__ __launch_bounds__(NTHR, 2) void attn_pool_kernel(int B, int K, Towers
     // start, loaded with the block's e2 rows so that both latencies overlap
     f32x16 acc[RT][CT];
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt)
+    for (int rt = 0; rt < RT; ++rt) {
+        const int i = acc_i(rt, lane);
+        const int j = (int)row0 + i;
+        const bool ok = i < MU && j < R;
+        const float okf = ok ? 1.f : 0.f;
+        const float* pr = t.P + (size_t)(ok ? j % B : 0) * H;
 #pragma unroll
-        for (int c = 0; c < CT; ++c) {
-            const int n = acc_col<H>(wave, c, lane);
+        for (int c = 0; c < CT; ++c)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int i = acc_row(rt, r, lane);
-                const int j = (int)row0 + i;
-                acc[rt][c][r] = (i < MU && j < R) ? t.P[(size_t)(j % B) * H + n] : 0.f;
+            for (int g = 0; g < 4; ++g) {
+                // loaded unconditionally (row 0 stands in for an unused row) and zeroed by a product: a
+                // conditional load (or a select the compiler sinks back into a branch) costs a branch + a full
+                // wait per load, 16 serial HBM latencies
+                float4 v = *reinterpret_cast<const float4*>(pr + acc_n0<H>(wave, c, g, lane));
+                v = make_float4(v.x * okf, v.y * okf, v.z * okf, v.w * okf);
+                acc[rt][c][4 * g] = v.x; acc[rt][c][4 * g + 1] = v.y;
+                acc[rt][c][4 * g + 2] = v.z; acc[rt][c][4 * g + 3] = v.w;
             }
-        }
+    }
     load_rows<H>(X, t.e2, row0, MU, R, tid);
     __syncthreads();
     QS_STAMP(1);
@@ -286,23 +337,12 @@ __global__ __launch_bounds__(NTHR, 2) void attn_pool_kernel(int B, int K, Towers
     QS_STAMP(3);
     mfma_layer<H>(X, reinterpret_cast<const float4*>(t.w_a2p), acc, wave, lane);
     QS_STAMP(4);
-    __syncthreads();
-    store_tanh<H>(X, acc, wave, lane, [&](int, int n) { return A3[H + n]; });
+    // score = a2 . a3 + b_a3 from the accumulators (a2 is not stored)
+    float* SCP = A3 + 4 * H;
+    score_partials<H>(acc, 1.f, A3, A3 + H, SCP, wave, lane);
     __syncthreads();
     QS_STAMP(5);
-    {   // score = a2 . a3 + b_a3: 4 lanes per row
-        const int r = tid >> 2, qq = tid & 3;   // the row's 4 lanes read interleaved columns: no bank conflict
-        float pp[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 8
-        for (int m = 0; m < H / 4; ++m) {
-            const int n = 4 * m + qq;
-            pp[m & 3] = fmaf(X[r * LD + n], A3[n], pp[m & 3]);
-        }
-        float p = (pp[0] + pp[1]) + (pp[2] + pp[3]);
-        p += __shfl_xor(p, 1);
-        p += __shfl_xor(p, 2);
-        if (qq == 0) SC[r] = p + t.b_a3;
-    }
+    if (tid < MROWS) SC[tid] = ((SCP[tid] + SCP[MROWS + tid]) + (SCP[2 * MROWS + tid] + SCP[3 * MROWS + tid])) + t.b_a3;
     __syncthreads();
     if (tid < AB) {   // softmax over the agent's K rows
         const int base = tid * K;
@@ -323,22 +363,23 @@ __global__ __launch_bounds__(NTHR, 2) void attn_pool_kernel(int B, int K, Towers
     mfma_layer<H>(X, reinterpret_cast<const float4*>(t.w_v1p), acc, wave, lane);
     QS_STAMP(7);
     __syncthreads();
-    store_tanh<H>(X, acc, wave, lane, [&](int, int n) { return A3[2 * H + n]; });
+    store_tanh<H>(X, acc, wave, lane, [&](int, int n0) { return lds4(A3 + 2 * H + n0); });
     __syncthreads();
     QS_STAMP(8);
     mfma_layer<H>(X, reinterpret_cast<const float4*>(t.w_v2p), acc, wave, lane);
     QS_STAMP(9);
     __syncthreads();
 #pragma unroll
-    for (int c = 0; c < CT; ++c) {
-        const int n = acc_col<H>(wave, c, lane);
-        const float bn = A3[3 * H + n];
+    for (int rt = 0; rt < RT; ++rt) {
+        const int i = acc_i(rt, lane);
+        const float wi = i < MU ? WT[i] : 0.f;
 #pragma unroll
-        for (int rt = 0; rt < RT; ++rt)
+        for (int c = 0; c < CT; ++c)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int i = acc_row(rt, r, lane);
-                X[i * LD + n] = i < MU ? WT[i] * tanh_fast(acc[rt][c][r] + bn) : 0.f;
+            for (int g = 0; g < 4; ++g) {
+                const int n0 = acc_n0<H>(wave, c, g, lane);
+                const float4 h = f4_tanh(f4_add(acc4(acc[rt][c], g), lds4(A3 + 3 * H + n0)));
+                *reinterpret_cast<float4*>(X + i * LD + n0) = make_float4(wi * h.x, wi * h.y, wi * h.z, wi * h.w);
             }
     }
     __syncthreads();

@@ -47,10 +47,20 @@ struct TileX3 {
     __device__ __forceinline__ float get(int i, int n) const {   // s x
         return (float)h[i * ld + n] + (float)l[i * ld + n];
     }
+    // four consecutive elements (n0 % 4 == 0): one 8-byte LDS store per half
+    __device__ __forceinline__ void put4(int i, int n0, float4 ys) const {
+        typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+        const f16x4 a = {(_Float16)ys.x, (_Float16)ys.y, (_Float16)ys.z, (_Float16)ys.w};
+        const f16x4 b = {(_Float16)(ys.x - (float)a[0]), (_Float16)(ys.y - (float)a[1]), (_Float16)(ys.z - (float)a[2]),
+                         (_Float16)(ys.w - (float)a[3])};
+        *reinterpret_cast<f16x4*>(h + i * ld + n0) = a;
+        *reinterpret_cast<f16x4*>(l + i * ld + n0) = b;
+    }
 };
 
 // acc = (Xh + Xl)(Wh + Wl)^T for the block's 64 rows (dropping Xl Wl), scaled by s_x s_w
-template <int H, int KD = H, bool ZERO = true>
+// PIN: fence the MFMA block of each step with scheduling barriers (below); measured per kernel
+template <int H, int KD = H, bool ZERO = true, bool PIN = true>
 __device__ __forceinline__ void mfma_layer_x3(const TileX3& X, const uint4* __restrict__ Wp, f32x16 (&acc)[RT][Geo<H>::CT],
                                               int wave, int lane) {
     constexpr int CT = Geo<H>::CT, S = GeoX3<KD>::S;
@@ -66,6 +76,9 @@ __device__ __forceinline__ void mfma_layer_x3(const TileX3& X, const uint4* __re
     // lane's 32 B of (ct, s): uint4 index ((ct S + s) 64 + lane) 2 + {0: hi, 1: lo}
     const uint4* wb = Wp + ((size_t)(wave * CT) * S * 64 + lane) * 2;
     auto wld = [&](int c, int s, int part) { return wb[((size_t)(c * S + s) * 64) * 2 + part]; };
+    auto ald = [&](const _Float16* t, int rt, int s) {
+        return *reinterpret_cast<const f16x8*>(t + aoff + rt * 32 * X.ld + 16 * s);
+    };
     uint4 bh0[CT], bl0[CT], bh1[CT], bl1[CT];
 #pragma unroll
     for (int c = 0; c < CT; ++c) {
@@ -73,6 +86,12 @@ __device__ __forceinline__ void mfma_layer_x3(const TileX3& X, const uint4* __re
         bl0[c] = wld(c, 0, 1);
         bh1[c] = S > 1 ? wld(c, 1, 0) : bh0[c];
         bl1[c] = S > 1 ? wld(c, 1, 1) : bl0[c];
+    }
+    f16x8 ahn[RT], aln[RT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+        ahn[rt] = ald(X.h, rt, 0);
+        aln[rt] = ald(X.l, rt, 0);
     }
     for (int s = 0; s < S; ++s) {
         f16x8 ah[RT], al[RT], bh[CT], bl[CT];
@@ -88,37 +107,50 @@ __device__ __forceinline__ void mfma_layer_x3(const TileX3& X, const uint4* __re
             }
         }
 #pragma unroll
-        for (int rt = 0; rt < RT; ++rt) {
-            ah[rt] = *reinterpret_cast<const f16x8*>(X.h + aoff + rt * 32 * X.ld + 16 * s);
-            al[rt] = *reinterpret_cast<const f16x8*>(X.l + aoff + rt * 32 * X.ld + 16 * s);
+        for (int rt = 0; rt < RT; ++rt) {   // activations: one step ahead (the LDS latency off the MFMA chain)
+            ah[rt] = ahn[rt];
+            al[rt] = aln[rt];
+            if (s + 1 < S) {
+                ahn[rt] = ald(X.h, rt, s + 1);
+                aln[rt] = ald(X.l, rt, s + 1);
+            }
         }
+        // keep the queue where it is written: left alone, the scheduler sinks each load next to its first MFMA
+        // (and reuses one register for every LDS read), which waits out the full latency at each step
+        if constexpr (PIN) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
             for (int c = 0; c < CT; ++c) {
-                acc[rt][c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[rt], bh[c], acc[rt][c], 0, 0, 0);
-                acc[rt][c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[rt], bl[c], acc[rt][c], 0, 0, 0);
-                acc[rt][c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[rt], bh[c], acc[rt][c], 0, 0, 0);
+                // weights as A, activations as B: the result tile is [output column][row] (qs_policy.h acc_i / acc_n0)
+                acc[rt][c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bh[c], ah[rt], acc[rt][c], 0, 0, 0);
+                acc[rt][c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bl[c], ah[rt], acc[rt][c], 0, 0, 0);
+                acc[rt][c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bh[c], al[rt], acc[rt][c], 0, 0, 0);
             }
+        if constexpr (PIN) __builtin_amdgcn_sched_barrier(0);
     }
 }
 
-// Y = tanh(acc / (s_x s_w) + bias(i, n)), stored scaled by X3_SX as hi / lo
-template <int H, typename Bias>
+// Y = tanh(acc / (s_x s_w) + bias4(i, n0)), stored scaled by X3_SX as hi / lo
+template <int H, typename Bias4>
 __device__ __forceinline__ void store_tanh_x3(const TileX3& Y, const f32x16 (&acc)[RT][Geo<H>::CT], float inv, int wave,
-                                              int lane, Bias bias) {
+                                              int lane, Bias4 bias4) {
     constexpr int CT = Geo<H>::CT;
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt)
+    for (int rt = 0; rt < RT; ++rt) {
+        const int i = acc_i(rt, lane);
 #pragma unroll
-        for (int c = 0; c < CT; ++c) {
-            const int n = acc_col<H>(wave, c, lane);
+        for (int c = 0; c < CT; ++c)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int i = acc_row(rt, r, lane);
-                Y.put(i, n, X3_SX * tanh_fast(fmaf(acc[rt][c][r], inv, bias(i, n))));
+            for (int g = 0; g < 4; ++g) {
+                const int n0 = acc_n0<H>(wave, c, g, lane);
+                const float4 b = bias4(i, n0);
+                Y.put4(i, n0, make_float4(X3_SX * tanh_fast(fmaf(acc[rt][c][4 * g], inv, b.x)),
+                                          X3_SX * tanh_fast(fmaf(acc[rt][c][4 * g + 1], inv, b.y)),
+                                          X3_SX * tanh_fast(fmaf(acc[rt][c][4 * g + 2], inv, b.z)),
+                                          X3_SX * tanh_fast(fmaf(acc[rt][c][4 * g + 3], inv, b.w))));
             }
-        }
+    }
 }
 
 template <int H>
@@ -127,12 +159,12 @@ constexpr size_t embed_x3_lds_bytes() {
 }
 template <int H>
 constexpr size_t pool_x3_lds_bytes() {
-    return (size_t)(2 * MROWS * GeoX3<H>::LDH) * 2 + (size_t)(3 * MROWS + 4 * H) * 4;
+    return (size_t)(2 * MROWS * GeoX3<H>::LDH) * 2 + (size_t)(3 * MROWS + 4 * H + NWAVE * MROWS) * 4;
 }
 
 // attn_embed_kernel with the split-f16 contraction (same inputs, same outputs: e2 rows and means in fp32)
 template <int H>
-__global__ __launch_bounds__(NTHR, 2) void attn_embed_x3_kernel(const float* __restrict__ obs, int stride, int so,
+__global__ __launch_bounds__(NTHR, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void attn_embed_x3_kernel(const float* __restrict__ obs, int stride, int so,
                                                                int off, int B, int K, int nd, Towers tw) {
     constexpr int LDH = GeoX3<H>::LDH, LD0 = GeoX3<KD0>::LDH, CT = Geo<H>::CT;
     extern __shared__ float4 smem4[];
@@ -162,13 +194,14 @@ __global__ __launch_bounds__(NTHR, 2) void attn_embed_x3_kernel(const float* __r
     }
     __syncthreads();
     f32x16 acc[RT][CT];
-    mfma_layer_x3<H, KD0>(X0, reinterpret_cast<const uint4*>(t.w_e1p), acc, wave, lane);
-    store_tanh_x3<H>(X, acc, 1.f / (X3_SIN * X3_SW), wave, lane,
-                     [&](int i, int n) { return (i < MU && row0 + i < R) ? BI[n] : 0.f; });
+    mfma_layer_x3<H, KD0, true, false>(X0, reinterpret_cast<const uint4*>(t.w_e1p), acc, wave, lane);
+    store_tanh_x3<H>(X, acc, 1.f / (X3_SIN * X3_SW), wave, lane, [&](int i, int n0) {
+        return (i < MU && row0 + i < R) ? lds4(BI + n0) : make_float4(0.f, 0.f, 0.f, 0.f);
+    });
     __syncthreads();
-    mfma_layer_x3<H>(X, reinterpret_cast<const uint4*>(t.w_e2p), acc, wave, lane);
+    mfma_layer_x3<H, H, true, false>(X, reinterpret_cast<const uint4*>(t.w_e2p), acc, wave, lane);
     __syncthreads();   // every wave has read the tile
-    store_tanh_x3<H>(X, acc, 1.f / (X3_SX * X3_SW), wave, lane, [&](int, int n) { return BI[H + n]; });
+    store_tanh_x3<H>(X, acc, 1.f / (X3_SX * X3_SW), wave, lane, [&](int, int n0) { return lds4(BI + H + n0); });
     __syncthreads();
     constexpr float isx = 1.f / X3_SX;
     for (int e = tid; e < MROWS * (H / 4); e += NTHR) {
@@ -201,21 +234,21 @@ __device__ __forceinline__ void load_rows_x3(const TileX3& X, const float* __res
     for (int u = 0; u < NV; ++u) {
         const int e = tid + u * NTHR, r = e / (H / 4), c4 = e - r * (H / 4);
         const long j = row0 + r;
-        v[u] = (r < MU && j < R) ? reinterpret_cast<const float4*>(src + j * H)[c4] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const bool ok = r < MU && j < R;
+        const float okf = ok ? 1.f : 0.f;
+        v[u] = reinterpret_cast<const float4*>(src + (ok ? j : 0) * H)[c4];   // unconditional (see the P loads)
+        v[u] = make_float4(v[u].x * okf, v[u].y * okf, v[u].z * okf, v[u].w * okf);
     }
 #pragma unroll
     for (int u = 0; u < NV; ++u) {
         const int e = tid + u * NTHR, r = e / (H / 4), c4 = e - r * (H / 4);
-        X.put(r, 4 * c4, X3_SX * v[u].x);
-        X.put(r, 4 * c4 + 1, X3_SX * v[u].y);
-        X.put(r, 4 * c4 + 2, X3_SX * v[u].z);
-        X.put(r, 4 * c4 + 3, X3_SX * v[u].w);
+        X.put4(r, 4 * c4, make_float4(X3_SX * v[u].x, X3_SX * v[u].y, X3_SX * v[u].z, X3_SX * v[u].w));
     }
 }
 
 // attn_pool_kernel with the split-f16 contraction
 template <int H>
-__global__ __launch_bounds__(NTHR, 2) void attn_pool_x3_kernel(int B, int K, Towers tw) {
+__global__ __launch_bounds__(NTHR, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void attn_pool_x3_kernel(int B, int K, Towers tw) {
     constexpr int LDH = GeoX3<H>::LDH, CT = Geo<H>::CT;
     extern __shared__ float4 smem4[];
     _Float16* xh = reinterpret_cast<_Float16*>(smem4);
@@ -227,7 +260,7 @@ __global__ __launch_bounds__(NTHR, 2) void attn_pool_x3_kernel(int B, int K, Tow
     const int AB = MROWS / K, MU = AB * K;
     const long R = (long)B * K, row0 = (long)blockIdx.x * MU;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    constexpr float SS = X3_SX * X3_SW, iSS = 1.f / SS, isx = 1.f / X3_SX;
+    constexpr float SS = X3_SX * X3_SW, iSS = 1.f / SS;
     for (int n = tid; n < H; n += NTHR) {
         A3[n] = t.w_a3[n];
         A3[H + n] = t.b_a2[n];
@@ -237,40 +270,37 @@ __global__ __launch_bounds__(NTHR, 2) void attn_pool_x3_kernel(int B, int K, Tow
     // attention_mlp: a1 = tanh(e2 A_e^T + P[j % B]): the accumulators start at P (scaled like the products)
     f32x16 acc[RT][CT];
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt)
+    for (int rt = 0; rt < RT; ++rt) {
+        const int i = acc_i(rt, lane);
+        const int j = (int)row0 + i;
+        const bool ok = i < MU && j < R;
+        const float okf = ok ? 1.f : 0.f;
+        const float* pr = t.P + (size_t)(ok ? j % B : 0) * H;
 #pragma unroll
-        for (int c = 0; c < CT; ++c) {
-            const int n = acc_col<H>(wave, c, lane);
+        for (int c = 0; c < CT; ++c)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int i = acc_row(rt, r, lane);
-                const int j = (int)row0 + i;
-                acc[rt][c][r] = (i < MU && j < R) ? SS * t.P[(size_t)(j % B) * H + n] : 0.f;
+            for (int g = 0; g < 4; ++g) {
+                // loaded unconditionally (row 0 stands in for an unused row) and zeroed by a product: a
+                // conditional load (or a select the compiler sinks back into a branch) costs a branch + a full
+                // wait per load, 16 serial HBM latencies
+                float4 v = *reinterpret_cast<const float4*>(pr + acc_n0<H>(wave, c, g, lane));
+                v = make_float4(v.x * okf, v.y * okf, v.z * okf, v.w * okf);
+                acc[rt][c][4 * g] = SS * v.x; acc[rt][c][4 * g + 1] = SS * v.y;
+                acc[rt][c][4 * g + 2] = SS * v.z; acc[rt][c][4 * g + 3] = SS * v.w;
             }
-        }
+    }
     load_rows_x3<H>(X, t.e2, row0, MU, R, tid);
     __syncthreads();
     mfma_layer_x3<H, H, false>(X, reinterpret_cast<const uint4*>(t.w_a1ep), acc, wave, lane);
     __syncthreads();
-    store_tanh_x3<H>(X, acc, iSS, wave, lane, [&](int, int) { return 0.f; });
+    store_tanh_x3<H>(X, acc, iSS, wave, lane, ZeroInit());
     __syncthreads();
     mfma_layer_x3<H>(X, reinterpret_cast<const uint4*>(t.w_a2p), acc, wave, lane);
+    // score = a2 . a3 + b_a3 from the accumulators (a2 is not stored)
+    float* SCP = A3 + 4 * H;
+    score_partials<H>(acc, iSS, A3, A3 + H, SCP, wave, lane);
     __syncthreads();
-    store_tanh_x3<H>(X, acc, iSS, wave, lane, [&](int, int n) { return A3[H + n]; });
-    __syncthreads();
-    {   // score = a2 . a3 + b_a3: 4 lanes per row
-        const int r = tid >> 2, qq = tid & 3;
-        float pp[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 8
-        for (int m = 0; m < H / 4; ++m) {
-            const int n = 4 * m + qq;
-            pp[m & 3] = fmaf(X.get(r, n) * isx, A3[n], pp[m & 3]);
-        }
-        float p = (pp[0] + pp[1]) + (pp[2] + pp[3]);
-        p += __shfl_xor(p, 1);
-        p += __shfl_xor(p, 2);
-        if (qq == 0) SC[r] = p + t.b_a3;
-    }
+    if (tid < MROWS) SC[tid] = ((SCP[tid] + SCP[MROWS + tid]) + (SCP[2 * MROWS + tid] + SCP[3 * MROWS + tid])) + t.b_a3;
     __syncthreads();
     if (tid < AB) {   // softmax over the agent's K rows
         const int base = tid * K;
@@ -289,7 +319,7 @@ __global__ __launch_bounds__(NTHR, 2) void attn_pool_x3_kernel(int B, int K, Tow
     __syncthreads();
     mfma_layer_x3<H>(X, reinterpret_cast<const uint4*>(t.w_v1p), acc, wave, lane);
     __syncthreads();
-    store_tanh_x3<H>(X, acc, iSS, wave, lane, [&](int, int n) { return A3[2 * H + n]; });
+    store_tanh_x3<H>(X, acc, iSS, wave, lane, [&](int, int n0) { return lds4(A3 + 2 * H + n0); });
     __syncthreads();
     mfma_layer_x3<H>(X, reinterpret_cast<const uint4*>(t.w_v2p), acc, wave, lane);
     __syncthreads();
@@ -298,15 +328,20 @@ __global__ __launch_bounds__(NTHR, 2) void attn_pool_x3_kernel(int B, int K, Tow
     constexpr int LDY = H + 4;
     static_assert(MROWS * (H + 4) * 4 <= 2 * MROWS * GeoX3<H>::LDH * 2, "fp32 tile fits the split tile's bytes");
 #pragma unroll
-    for (int c = 0; c < CT; ++c) {
-        const int n = acc_col<H>(wave, c, lane);
-        const float bn = A3[3 * H + n];
+    for (int rt = 0; rt < RT; ++rt) {
+        const int i = acc_i(rt, lane);
+        const float wi = i < MU ? WT[i] : 0.f;
 #pragma unroll
-        for (int rt = 0; rt < RT; ++rt)
+        for (int c = 0; c < CT; ++c)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int i = acc_row(rt, r, lane);
-                Y[i * LDY + n] = i < MU ? WT[i] * tanh_fast(fmaf(acc[rt][c][r], iSS, bn)) : 0.f;
+            for (int g = 0; g < 4; ++g) {
+                const int n0 = acc_n0<H>(wave, c, g, lane);
+                const float4 b = lds4(A3 + 3 * H + n0);
+                *reinterpret_cast<float4*>(Y + i * LDY + n0) =
+                    make_float4(wi * tanh_fast(fmaf(acc[rt][c][4 * g], iSS, b.x)),
+                                wi * tanh_fast(fmaf(acc[rt][c][4 * g + 1], iSS, b.y)),
+                                wi * tanh_fast(fmaf(acc[rt][c][4 * g + 2], iSS, b.z)),
+                                wi * tanh_fast(fmaf(acc[rt][c][4 * g + 3], iSS, b.w)));
             }
     }
     __syncthreads();

@@ -53,6 +53,11 @@ for s in "$@"; do
     bench) step bench 600 python bench.py ;;
     ppotests) step ppo_tests 600 python -m pytest tests/test_gpu_ppo.py -q -x ;;
     e2ea) step e2e_a8 600 python bench.py --config a8 --steps 500 --no-cpu-baseline --e2e-iters 1 --e2e-steps 64 ;;
+    e2ec3p)    # C3 end to end, the rollout encoders in fp32 and split-f16 (x3)
+      step e2e_c3_fp32 600 python bench.py --config c3 --steps 500 --no-cpu-baseline --e2e-iters 2 --e2e-precision fp32
+      step e2e_c3_x3 600 python bench.py --config c3 --steps 500 --no-cpu-baseline --e2e-iters 2 --e2e-precision x3
+      ;;
+    polt) step pol_tests 600 python -u -m pytest tests/test_gpu_policy_fused.py tests/test_gpu_ppo.py tests/test_gpu_trainer.py -x -v --timeout 200 --timeout-method thread ;;
     e2ec3) step e2e_c3 600 python bench.py --config c3 --steps 500 --no-cpu-baseline --e2e-iters 1 ;;
     e2ea512) step e2e_a8_512 900 python bench.py --config a8 --steps 500 --no-cpu-baseline --e2e-iters 2 ;;
     benchgen) step bench_generic 300 python bench.py --generic --steps 2000 --e2e-iters 0 --no-cpu-baseline ;;
