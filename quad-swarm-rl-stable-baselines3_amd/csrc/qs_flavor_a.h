@@ -54,15 +54,20 @@ __device__ __forceinline__ float sin_small(float x) {
     return x * (1.f + x2 * (-1.f / 6.f + x2 * (1.f / 120.f + x2 * (-1.f / 5040.f + x2 * (1.f / 362880.f + x2 * (-1.f / 39916800.f))))));
 }
 
+#ifndef QS_CAM_RCP
+#define QS_CAM_RCP 1
+#endif
+
 // (x + pi) % (2 pi) - pi with Python's modulo sign convention.  For r = x + pi in [-2 pi, 4 pi) -- every
 // angle the step wraps -- fmodf(r, 2 pi) is r itself below 2 pi and r - 2 pi above (exact by Sterbenz), so
 // the fast path gives fmodf's bits without its ~30-instruction loop; anything else (and NaN / inf) takes it.
+// The common range as selects, the fmodf fallback as the only branch (rare, skipped by whole waves).
 __device__ __forceinline__ float wrap_pi(float x) {
-    float r = x + kPi;
-    if (!(r >= -k2Pi && r < 2.f * k2Pi)) r = fmodf(r, k2Pi);
-    else if (r >= k2Pi) r -= k2Pi;
-    if (r < 0.f) r += k2Pi;
-    return r - kPi;
+    const float r = x + kPi;
+    float w = r >= k2Pi ? r - k2Pi : r;
+    if (__builtin_expect(!(r >= -k2Pi && r < 2.f * k2Pi), 0)) w = fmodf(r, k2Pi);
+    w = w < 0.f ? w + k2Pi : w;
+    return w - kPi;
 }
 
 // u[k] = sub-lane (k % Q)'s v[k / Q]
@@ -199,6 +204,24 @@ __device__ __forceinline__ void camera(const KP& kp, float rx, float ry, float g
     const float c0 = c * rp0 - s * rp1, c1 = s * rp0 + c * rp1;
     const float cn2 = c0 * c0 + c1 * c1, cn = fsqrt(cn2);
     const float r = kp.cam_r, r2 = r * r;
+    const float pxs = kp.cam_w / (kp.cam_res * kp.cam_f);  // pixel -> tan(angle)
+#if QS_CAM_RCP
+    // the quotients as products with hardware reciprocals (~1 ulp each, like target_step): 1 / |c| once for
+    // a, mf and the perpendicular; the camera index (m / seg above) keeps its IEEE division, since a rounding
+    // flip there would move the segment.  0 / inf / NaN cases as the divisions give them (x * rcp(0) = +-inf,
+    // 0 * rcp(0) = NaN)
+    const float icn = frcp(cn);
+    const float a = r2 * icn;
+    const float h = sqrtf(r2 - a * a);                   // NaN when the target is inside the marker
+    const float mf = 1.f - r2 * (icn * icn);
+    const float mid0 = c0 * mf, mid1 = c1 * mf;
+    const float pe0 = c1 * icn, pe1 = -c0 * icn;
+    const float x10 = mid0 + h * pe0, x11 = mid1 + h * pe1;
+    const float x20 = mid0 - h * pe0, x21 = mid1 - h * pe1;
+    const float at1 = atanf(x11 * frcp(x10) + n1 * pxs), at2 = atanf(x21 * frcp(x20) + n2 * pxs);
+    const float alpha = fabsf(at1 - at2);
+    const float l = r * frcp(sin_small(0.5f * alpha));
+#else
     const float a = r2 / cn;
     const float h = sqrtf(r2 - a * a);                   // NaN when the target is inside the marker
     const float mf = 1.f - r2 / cn2;
@@ -206,10 +229,10 @@ __device__ __forceinline__ void camera(const KP& kp, float rx, float ry, float g
     const float pe0 = c1 / cn, pe1 = -c0 / cn;
     const float x10 = mid0 + h * pe0, x11 = mid1 + h * pe1;
     const float x20 = mid0 - h * pe0, x21 = mid1 - h * pe1;
-    const float pxs = kp.cam_w / (kp.cam_res * kp.cam_f);  // pixel -> tan(angle)
     const float at1 = atanf(x11 / x10 + n1 * pxs), at2 = atanf(x21 / x20 + n2 * pxs);
     const float alpha = fabsf(at1 - at2);
     const float l = r / sin_small(0.5f * alpha);
+#endif
     const float ar = wrap_pi(0.5f * (at1 + at2) + cam);
     dist = (l != l) ? 0.f : l;
     ang = (ar != ar) ? 0.f : ar;
@@ -482,7 +505,7 @@ __device__ __forceinline__ void reset_env_a(const KP& kp, Drone& d, Ctl& c, floa
 // di + k (mod 8) -- its position and its index -- to this lane, no LDS round trip.  Squared distances
 // against the squared threshold (the same order as |r| <= thr up to the last bit).
 template <int Q, int K>
-__device__ __forceinline__ void col_row16(const KP& kp, const Drone& d, int di, float thr2, uint64_t& cur) {
+__device__ __forceinline__ void col_row16(const KP& kp, const Drone& d, int di, float thr2, uint32_t& cur) {
     if constexpr (K * Q < 16) {
         constexpr int C = 0x120 + K * Q;   // DPP row_ror:K*Q
         const float dx = d.pos[0] - dpp_f<C>(d.pos[0]), dy = d.pos[1] - dpp_f<C>(d.pos[1]);
@@ -490,7 +513,7 @@ __device__ __forceinline__ void col_row16(const KP& kp, const Drone& d, int di, 
         const int j = dpp_i<C>(di);
         // non-short-circuit: a select, not a branch per partner
         const bool hit = (j < kp.N) & (dx * dx + dy * dy + dz * dz <= thr2);
-        cur |= hit ? (1ull << j) : 0ull;
+        cur |= hit ? (1u << j) : 0u;   // j < 16: the row's low word
         col_row16<Q, K + 1>(kp, d, di, thr2, cur);
     }
 }
@@ -499,14 +522,14 @@ __device__ __forceinline__ void col_row16(const KP& kp, const Drone& d, int di, 
 // di + 2k (its sub-lane 1) to sub-lane 0 and drone di + 2k + 1 (its sub-lane 0) to sub-lane 1, so 4
 // rotations cover the 7 partners (and the drone itself once, skipped); the two halves are OR-ed by DPP.
 template <int K>
-__device__ __forceinline__ void col_row16_q2(const KP& kp, const Drone& d, int di, float thr2, uint64_t& cur) {
+__device__ __forceinline__ void col_row16_q2(const KP& kp, const Drone& d, int di, float thr2, uint32_t& cur) {
     if constexpr (K < 4) {
         constexpr int C = 0x120 + 4 * K + 1;   // DPP row_ror:4K+1
         const float dx = d.pos[0] - dpp_f<C>(d.pos[0]), dy = d.pos[1] - dpp_f<C>(d.pos[1]);
         const float dz = d.pos[2] - dpp_f<C>(d.pos[2]);
         const int j = dpp_i<C>(di);
         const bool hit = (j != di) & (j < kp.N) & (dx * dx + dy * dy + dz * dz <= thr2);   // a select, not a branch
-        cur |= hit ? (1ull << j) : 0ull;
+        cur |= hit ? (1u << j) : 0u;   // j < 8: the row's low word
         col_row16_q2<K + 1>(kp, d, di, thr2, cur);
     }
 }
@@ -659,12 +682,14 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
         if (kp.stats) {   // collisions between drones and with the room (:649-720): bookkeeping only
             uint64_t cur = 0;
             const float thr2 = kp.col_thr * kp.col_thr;
-            if constexpr (LPE == 16 && NPAD * Q == 16) {
+            if constexpr (LPE == 16 && NPAD * Q == 16) {   // (32-bit row words: the env's drones are < 16)
+                uint32_t c32 = 0;
                 if constexpr (Q == 2) {
-                    col_row16_q2<0>(kp, d, di, thr2, cur);
-                    cur = qor<Q>(cur);
+                    col_row16_q2<0>(kp, d, di, thr2, c32);
+                    c32 |= (uint32_t)dpp_i<quad_perm(1, 0, 3, 2)>((int)c32);   // qor<2> of the low word
                 } else
-                    col_row16<Q, 1>(kp, d, di, thr2, cur);
+                    col_row16<Q, 1>(kp, d, di, thr2, c32);
+                cur = c32;
             } else {
                 if (active && q == 0) xch[2 * (sbase + di)] = make_float4(d.pos[0], d.pos[1], d.pos[2], 0.f);
                 lds_sync();

@@ -2,7 +2,7 @@
 """Diagnostic: the ISA of a config's specialised step kernel (what qs_specialize compiles with hipRTC), built
 offline with hipcc from the same sources and parameter words, plus instruction counts.
 
-    python tools/jit_isa.py a8 [out.s]        (bench.py config names)"""
+    python tools/jit_isa.py a8 [out.s]        (bench.py config names; QS_JIT_OPTS as for qs_specialize)"""
 import os
 import re
 import subprocess
@@ -44,7 +44,8 @@ def main():
         subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=on",
                         "-munsafe-fp-atomics", "--cuda-device-only", "-S", "-I",
                         os.environ.get("QS_JIT_SRC_DIR", os.path.join(PKG, "csrc")), "-I",
-                        os.path.join(ROOT, "include"), f, "-o", out], check=True)
+                        os.path.join(ROOT, "include"), f, "-o", out] + os.environ.get("QS_JIT_OPTS", "").split(),
+                       check=True)
     text = open(out).read()
     body = text[text.index(".text"):]
     ins = [ln.split()[0] for ln in body.splitlines() if ln.startswith("\t") and not ln.startswith("\t.")
