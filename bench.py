@@ -55,6 +55,8 @@ CONFIGS = {
     # 128-drone swarms (the paper's largest, paper/fps_compare.py:7): one env per two-wave workgroup
     "n128": dict(num_envs=256, num_agents=128, neighbor_visible_num=6, neighbor_obs_type="pos_vel"),
     "a4": dict(flavor="A", num_envs=8192, num_agents=4, initial_capture_radius=0.5),
+    # flavor A at the paper's largest swarm (paper/fps_compare.py:7): one env per 4-wave workgroup, k = 7
+    "a128": dict(flavor="A", num_envs=256, num_agents=128, neighbor_visible_num=7, initial_capture_radius=0.5),
 }
 WORKLOAD = {"c2": "single_quad x 16384 envs", "c3": "8-drone swarm static_same_goal x 4096 envs (pos_vel k=6)",
             "n64": "64-drone swarm static_same_goal x 512 envs (pos_vel k=6)",
@@ -69,7 +71,8 @@ WORKLOAD = {"c2": "single_quad x 16384 envs", "c3": "8-drone swarm static_same_g
             "c5": "32-drone swarm x 1024 envs per GPU (pos_vel k=6)",
             "a8": "flavor A (sb_train env: PID pre-controller x 8 ticks, dynamic_repulsive target, ndist_nsangle "
                   "camera neighbours k=7) 8 drones x 4096 envs, capture radius 0.5",
-            "a4": "flavor A sb_train default 4 drones x 8192 envs (k=3), capture radius 0.5"}
+            "a4": "flavor A sb_train default 4 drones x 8192 envs (k=3), capture radius 0.5",
+            "a128": "flavor A (sb_train env) 128 drones x 256 envs, camera neighbours k=7, capture radius 0.5"}
 
 
 def make_cfg(kw, **extra):

@@ -408,8 +408,8 @@ class OracleEnvA:
         # quadswarm_oracle_a.c): trace["step"|"reset"][g, slot] = (j, pixel noise 1, 2, pr[3], vr[3], aw, h_i, h_j),
         # keys["step"|"reset"][g, j] = selection key (K < N-1); NaN where the call ran no such pass
         on = FT == np.float64
-        self.trace = {k: np.full((n, 64, NB_TRACE_W), np.nan) for k in ("step", "reset")} if on else None
-        self.keys = {k: np.full((n, 64), np.nan) for k in ("step", "reset")} if on else None
+        self.trace = {k: np.full((n, MAXN, NB_TRACE_W), np.nan) for k in ("step", "reset")} if on else None
+        self.keys = {k: np.full((n, MAXN), np.nan) for k in ("step", "reset")} if on else None
 
     def _traced(self, fn):
         if self.trace is None:

@@ -357,8 +357,8 @@ void or_self_obs_a(const or_params* p, const or_drone* d, or_rng* r, uint32_t gi
 /* ------------------------------------------------------------------------------------------ */
 /* Test hooks (tests/parity_utils.py, per-feature conditioning of the GPU-vs-oracle comparison): when set,
  * the obs pass of or_neighbor_obs_a records the inputs of every (drone, slot) feature block in
- * or_nb_trace[(gid * 64 + slot) * OR_NB_TRACE_W] = {j, n1, n2, pr[3], vr[3], aw, h_i, h_j}, and the selection
- * pass the sort key of every candidate j in or_key_trace[gid * 64 + j]; the *_reset pair gets the passes of
+ * or_nb_trace[(gid * OR_MAXN + slot) * OR_NB_TRACE_W] = {j, n1, n2, pr[3], vr[3], aw, h_i, h_j}, and the
+ * selection pass the sort key of every candidate j in or_key_trace[gid * OR_MAXN + j]; the *_reset pair gets the passes of
  * the resets (the obs a finished env returns), the other pair those of the step (its terminal obs). */
 double* or_nb_trace = NULL;
 double* or_key_trace = NULL;
@@ -417,18 +417,18 @@ void or_neighbor_obs_a(const or_params* p, const or_env* ev, const or_drone* dr,
     double* nbt = reset ? or_nb_trace_reset : or_nb_trace;
     double* kt = reset ? or_key_trace_reset : or_key_trace;
     const uint32_t st_obs = reset ? OR_S_RESET_CAM : OR_S_CAM, st_sel = reset ? OR_S_RESET_CAM_SEL : OR_S_CAM_SEL;
-    int sel[64][64];
+    int sel[OR_MAXN][OR_MAXN];
     for (int i = 0; i < N; ++i) {
         int c = 0;
         for (int j = 0; j < N; ++j) if (j != i) sel[i][c++] = j;
     }
     if (K < N - 1) {
         for (int i = 0; i < N; ++i) {
-            double n1[64] = {0}, n2[64] = {0}, key[64];
+            double n1[OR_MAXN] = {0}, n2[OR_MAXN] = {0}, key[OR_MAXN];
             if (cam) {
                 for (int c = 0; c < N - 1; ++c) cam_noise(p, r, gbase + (uint32_t)i, st_sel | ((uint32_t)sel[i][c] << 8), &n1[c], &n2[c]);
                 if (r->mode == OR_RNG_TAPE) {   /* tape: n1 of all pairs, then n2 of all pairs */
-                    double t[128];
+                    double t[2 * OR_MAXN];
                     for (int c = 0; c < N - 1; ++c) { t[2 * c] = n1[c]; t[2 * c + 1] = n2[c]; }
                     for (int c = 0; c < N - 1; ++c) { n1[c] = t[c]; n2[c] = t[N - 1 + c]; }
                 }
@@ -440,10 +440,10 @@ void or_neighbor_obs_a(const or_params* p, const or_env* ev, const or_drone* dr,
                 for (int q = 0; q < nf; ++q) s += f[q] * f[q];
                 double k = sqrt(s);
                 key[c] = k > 0.01 ? k : (k == k ? 0.01 : k);
-                if (kt) kt[(size_t)(gbase + (uint32_t)i) * 64 + sel[i][c]] = key[c];
+                if (kt) kt[(size_t)(gbase + (uint32_t)i) * OR_MAXN + sel[i][c]] = key[c];
             }
-            /* argsort (insertion sort for <= 16 keys: stable; NaN sorts last) */
-            int order[64];
+            /* argsort (insertion sort: stable; NaN sorts last) */
+            int order[OR_MAXN];
             for (int c = 0; c < N - 1; ++c) order[c] = c;
             for (int a = 1; a < N - 1; ++a) {
                 int v = order[a], b = a - 1;
@@ -453,17 +453,17 @@ void or_neighbor_obs_a(const or_params* p, const or_env* ev, const or_drone* dr,
                 }
                 order[b + 1] = v;
             }
-            int tmp[64];
+            int tmp[OR_MAXN];
             for (int c = 0; c < K; ++c) tmp[c] = sel[i][order[c]];
             for (int c = 0; c < K; ++c) sel[i][c] = tmp[c];
         }
     }
     for (int i = 0; i < N; ++i) {
-        double n1[64] = {0}, n2[64] = {0};
+        double n1[OR_MAXN] = {0}, n2[OR_MAXN] = {0};
         if (cam) {
             for (int c = 0; c < K; ++c) cam_noise(p, r, gbase + (uint32_t)i, st_obs | ((uint32_t)sel[i][c] << 8), &n1[c], &n2[c]);
             if (r->mode == OR_RNG_TAPE) {
-                double t[128];
+                double t[2 * OR_MAXN];
                 for (int c = 0; c < K; ++c) { t[2 * c] = n1[c]; t[2 * c + 1] = n2[c]; }
                 for (int c = 0; c < K; ++c) { n1[c] = t[c]; n2[c] = t[K + c]; }
             }
@@ -473,7 +473,7 @@ void or_neighbor_obs_a(const or_params* p, const or_env* ev, const or_drone* dr,
             double f[8];
             if (nbt) {
                 const int j = sel[i][c];
-                double* t = nbt + ((size_t)(gbase + (uint32_t)i) * 64 + c) * OR_NB_TRACE_W;
+                double* t = nbt + ((size_t)(gbase + (uint32_t)i) * OR_MAXN + c) * OR_NB_TRACE_W;
                 t[0] = j; t[1] = n1[c]; t[2] = n2[c];
                 for (int q = 0; q < 3; ++q) {
                     t[3 + q] = ev->obs_pos[j][q] - ev->obs_pos[i][q];
@@ -527,7 +527,7 @@ void or_env_reset_a(const or_params* p, or_drone* drones, or_env* envs, int e, o
     r->step = ((uint64_t)ev->episode << 32) | (uint32_t)ev->tick;
     const int tape = r->mode == OR_RNG_TAPE;
     if (p->scenario_a == 1) {
-        double dirs[64][2], rad, t0, t1, tr;
+        double dirs[OR_MAXN][2], rad, t0, t1, tr;
         if (tape) {
             for (int k = 0; k < 4; ++k) (void)or_gnext(r);   /* duration, formation, size, layer dist */
             for (int i = 0; i < N; ++i) { dirs[i][0] = or_gnext(r); dirs[i][1] = or_gnext(r); }
@@ -542,7 +542,7 @@ void or_env_reset_a(const or_params* p, or_drone* drones, or_env* envs, int e, o
             t1 = or_ru(r, gbase, OR_S_SCEN, 2, 0.0, 1.0);
             tr = or_ru(r, gbase, OR_S_SCEN, 3, 0.0, 1.0);
         }
-        double sp[64][2];   /* spawn_points[:, :2] */
+        double sp[OR_MAXN][2];   /* spawn_points[:, :2] */
         for (int i = 0; i < N; ++i) {
             double a = dirs[i][0] - 0.5, b = dirs[i][1] - 0.5, n = sqrt(a * a + b * b);
             sp[i][0] = (a / n) * (rad * 0.5);
@@ -555,7 +555,7 @@ void or_env_reset_a(const or_params* p, or_drone* drones, or_env* envs, int e, o
         or_target_step(p, ev, dr);
         for (int i = 0; i < N; ++i) { dr[i].pos[0] = sp[i][0]; dr[i].pos[1] = sp[i][1]; }
     } else {   /* static_same_goal: goals at the formation centre (size 0), spawn_points None -> spawn at the goal */
-        double goal[64][3];
+        double goal[OR_MAXN][3];
         if (p->scenario_b != OR_SC_NONE) {   /* any other create_scenario goal scenario (:123, :560) */
             or_sdraw sd;
             memset(&sd, 0, sizeof sd);
@@ -648,7 +648,7 @@ void or_env_step_a(const or_params* p, or_drone* drones, or_env* envs, int e, co
         /* 1. collisions between drones and with the room (:649-720) -- no forces (apply_collision_force is
          * False, :203), only the episode_extra_stats bookkeeping */
         {
-            int in_cur[64] = {0}, in_prev[64] = {0}, wall_new[64], ceil_new[64];
+            int in_cur[OR_MAXN] = {0}, in_prev[OR_MAXN] = {0}, wall_new[OR_MAXN], ceil_new[OR_MAXN];
             unsigned char cur[OR_MAXN * OR_MAXN];   /* the env's pair-bit layout (stride OR_MAXN) */
             memset(cur, 0, sizeof cur);
             for (int i = 0; i < N; ++i)
@@ -670,7 +670,7 @@ void or_env_step_a(const or_params* p, or_drone* drones, or_env* envs, int e, co
             or_episode_stats_step(p, ev, dr, N, in_cur, in_prev, NULL, wall_new, ceil_new, NULL, NULL, od, time_remain);
         }
         /* capture reward (:711-735): xy distance of every drone to env 0's goal */
-        double rel[64];
+        double rel[OR_MAXN];
         int cap = 0;
         for (int i = 0; i < N; ++i) {
             double a = dr[0].goal[0] - dr[i].pos[0], b = dr[0].goal[1] - dr[i].pos[1];
@@ -700,7 +700,7 @@ void or_env_step_a(const or_params* p, or_drone* drones, or_env* envs, int e, co
             or_sdraw sd;
             memset(&sd, 0, sizeof sd);
             sd.mode = OR_RNG_PHILOX; sd.seed = r->seed; sd.key = gbase; sd.stream = OR_S_SCN; sd.step = r->step;
-            double g[64][3];
+            double g[OR_MAXN][3];
             for (int i = 0; i < N; ++i) memcpy(g[i], dr[i].goal, sizeof g[i]);
             or_scen_step(p, &ev->scen, ev->tick, &sd, g);
             for (int i = 0; i < N; ++i) memcpy(dr[i].goal, g[i], sizeof g[i]);

@@ -690,6 +690,100 @@ __device__ __forceinline__ int xcd_block(int b, int nblocks) {
     return (nblocks & 7) ? b : (b & 7) * (nblocks >> 3) + (b >> 3);
 }
 
+// Sub-lanes per drone of an env that spans several waves (64- and 128-drone envs): with 2, a 512-env
+// 64-drone shard or a 256-env 128-drone shard is 1024 waves, one per SIMD.
+#ifndef QS_QW
+#define QS_QW 2
+#endif
+
+// ---- collision rows: bit j = partner drone j; 64 bits, or two words for the 128-drone envs ----
+struct Row128 {
+    uint64_t lo, hi;
+};
+__device__ __forceinline__ Row128 operator|(Row128 a, Row128 b) { return Row128{a.lo | b.lo, a.hi | b.hi}; }
+__device__ __forceinline__ Row128 operator&(Row128 a, Row128 b) { return Row128{a.lo & b.lo, a.hi & b.hi}; }
+__device__ __forceinline__ Row128 operator~(Row128 a) { return Row128{~a.lo, ~a.hi}; }
+template <bool WIDE> struct RowOf { using T = uint64_t; };
+template <> struct RowOf<true> { using T = Row128; };
+__device__ __forceinline__ bool row_any(uint64_t r) { return r != 0ull; }
+__device__ __forceinline__ bool row_any(Row128 r) { return (r.lo | r.hi) != 0ull; }
+__device__ __forceinline__ int row_popc(uint64_t r) { return __popcll(r); }
+__device__ __forceinline__ int row_popc(Row128 r) { return __popcll(r.lo) + __popcll(r.hi); }
+__device__ __forceinline__ int row_ffs(uint64_t r) { return __ffsll((long long)r) - 1; }   // r != 0
+__device__ __forceinline__ int row_ffs(Row128 r) {
+    return r.lo ? __ffsll((long long)r.lo) - 1 : 64 + __ffsll((long long)r.hi) - 1;
+}
+__device__ __forceinline__ void row_set(uint64_t& r, int j, bool c) { r |= c ? (1ull << j) : 0ull; }
+__device__ __forceinline__ void row_set(Row128& r, int j, bool c) {
+    if (j < 64) r.lo |= c ? (1ull << j) : 0ull;
+    else r.hi |= c ? (1ull << (j - 64)) : 0ull;
+}
+__device__ __forceinline__ void row_clear(uint64_t& r, int j) { r &= ~(1ull << j); }
+__device__ __forceinline__ void row_clear(Row128& r, int j) {
+    if (j < 64) r.lo &= ~(1ull << j);
+    else r.hi &= ~(1ull << (j - 64));
+}
+// the partners above drone di (pairs (di, j > di))
+__device__ __forceinline__ uint64_t row_above(uint64_t r, int di) { return r & ~((2ull << di) - 1ull); }
+__device__ __forceinline__ Row128 row_above(Row128 r, int di) {
+    return di < 64 ? Row128{r.lo & ~((2ull << di) - 1ull), r.hi} : Row128{0ull, r.hi & ~((2ull << (di - 64)) - 1ull)};
+}
+template <int Q>
+__device__ __forceinline__ Row128 qor(Row128 r) { return Row128{qor<Q>(r.lo), qor<Q>(r.hi)}; }
+__device__ __forceinline__ void row_of(const Drone& d, uint64_t& r) { r = d.prev; }
+__device__ __forceinline__ void row_of(const Drone& d, Row128& r) { r = Row128{d.prev, d.prevx}; }
+__device__ __forceinline__ void row_keep(Drone& d, uint64_t r) { d.prev = r; }
+__device__ __forceinline__ void row_keep(Drone& d, Row128 r) { d.prev = r.lo; d.prevx = r.hi; }
+
+// the drones' bits of a wave ballot with Q = 2 sub-lanes per drone: bit i = lane 2i or 2i + 1 (32 bits)
+__device__ __forceinline__ uint64_t compact_pairs(uint64_t b) {
+    uint64_t x = (b | (b >> 1)) & 0x5555555555555555ull;
+    x = (x | (x >> 1)) & 0x3333333333333333ull;
+    x = (x | (x >> 2)) & 0x0F0F0F0F0F0F0F0Full;
+    x = (x | (x >> 4)) & 0x00FF00FF00FF00FFull;
+    x = (x | (x >> 8)) & 0x0000FFFF0000FFFFull;
+    return (x | (x >> 16)) & 0x00000000FFFFFFFFull;
+}
+
+// Env-level collectives of the step kernel over a predicate of the env's lanes (callers pass x && q == 0 to
+// count drones).  An env inside one wave: a ballot of the env's lane segment (drone i at bit i Q).  An env that
+// spans the workgroup's NW waves (WIDE: 64 drones x 2 sub-lanes, 128 drones x 1 or 2): each wave's ballot,
+// reduced to its drones (bit i = drone i of the env), through an LDS slot and a workgroup barrier; the slots
+// alternate so that one barrier per collective suffices.  Every lane of the workgroup must make the same calls.
+template <bool WIDE, bool ROW2 = false, int Q = 1, int NW = 1>
+struct EnvColl {
+    using Row = typename RowOf<ROW2>::T;
+    int lbase;
+    uint64_t lmask;
+    uint64_t* scr;   // WIDE: 2 NW words of LDS
+    int slot;
+    __device__ __forceinline__ Row bits(bool x) {
+        if constexpr (!WIDE) {
+            return (__ballot(x) >> lbase) & lmask;
+        } else {
+            static_assert(Q == 1 || Q == 2, "sub-lanes of a multi-wave env");
+            constexpr int DPW = 64 / Q;   // drones per wave
+            const uint64_t bw = Q == 2 ? compact_pairs(__ballot(x)) : __ballot(x);
+            uint64_t* s = scr + NW * slot;
+            slot ^= 1;
+            if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = bw;
+            lds_sync();
+            uint64_t w[2] = {0ull, 0ull};
+#pragma unroll
+            for (int k = 0; k < NW; ++k) w[(k * DPW) >> 6] |= s[k] << ((k * DPW) & 63);
+            if constexpr (ROW2) return Row128{w[0], w[1]};
+            else return w[0];
+        }
+    }
+    __device__ __forceinline__ bool any(bool x) { return row_any(bits(x)); }
+    __device__ __forceinline__ int count(bool x) { return row_popc(bits(x)); }
+    // uniform over the launch's unit of lockstep (the wave, or the WIDE workgroup): guards work that has barriers
+    __device__ __forceinline__ bool wany(bool x) {
+        if constexpr (!WIDE) return __ballot(x) != 0ull;
+        else return any(x);
+    }
+};
+
 // ---------------------------------------------------------------------------------------------
 // block-level obs staging: LDS tile [rows, obs_dim] -> contiguous global rows
 // ---------------------------------------------------------------------------------------------

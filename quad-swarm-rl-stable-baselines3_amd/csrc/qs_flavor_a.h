@@ -411,6 +411,77 @@ __device__ __forceinline__ void neighbor_obs_a(const KP& kp, const float4* xch, 
     }
 }
 
+// neighbor_obs_a for the envs of more than 64 drones (k < N - 1 always selects there), without the NPAD-entry key
+// array: sub-lane q evaluates the candidates j = q, q + Q, ... once each (camera with the selection noise) and keeps
+// the k smallest (key, j) in a sorted register list by insertion; the Q lists are merged over DPP, so every
+// sub-lane holds the env's k nearest in the order the rank formula of neighbor_obs_a gives (key, then index).
+// Sub-lane q then writes slots q, q + Q, ... with the obs-pass noise.  k <= QS_A_KMAX (qs_step.hip validate).
+#ifndef QS_A_KMAX
+#define QS_A_KMAX 16
+#endif
+template <int NPAD, int Q = 1>
+__device__ __forceinline__ void neighbor_obs_wide(const KP& kp, const float4* xch, int base, int di, const float* P, float H,
+                                                  float aw, const float* V, const Rng& rng, uint32_t gid, bool reset,
+                                                  bool write, float* out, int q = 0) {
+    constexpr int KM = QS_A_KMAX;
+    const uint32_t st_obs = reset ? S_RESET_CAM : S_CAM, st_sel = reset ? S_RESET_CAM_SEL : S_CAM_SEL;
+    const int F = kp.nfd;
+    float lk[KM];
+    int lj[KM];
+#pragma unroll
+    for (int s = 0; s < KM; ++s) { lk[s] = __builtin_inff(); lj[s] = NPAD; }
+    auto insert = [&](float ck, int cj) {
+#pragma unroll
+        for (int s = 0; s < KM; ++s) {
+            if (s < kp.K) {   // a constant in specialised builds
+                const bool lt = ck < lk[s] || (ck == lk[s] && cj < lj[s]);
+                const float tk = lk[s];
+                const int tj = lj[s];
+                lk[s] = lt ? ck : tk;
+                lj[s] = lt ? cj : tj;
+                ck = lt ? tk : ck;
+                cj = lt ? tj : cj;
+            }
+        }
+    };
+#pragma unroll 1
+    for (int t = 0; t < NPAD / Q; ++t) {
+        const int j = q + Q * t;
+        const bool valid = (j != di) && (j < kp.N);
+        float sq = 0.f;
+        rel_features(kp, xch[2 * (base + j)], xch[2 * (base + j) + 1], P, H, aw, V, rng, gid, st_sel | ((uint32_t)j << 8),
+                     [&](int, float v) { sq += v * v; });
+        insert(valid ? ((sq != sq) ? 3.0e38f : fmaxf(sq, 1e-4f)) : __builtin_inff(), j);
+    }
+    if constexpr (Q == 2) {   // the pair's lists: each the k smallest of its half, merged into the union's k smallest
+        float pk[KM];
+        int pj[KM];
+#pragma unroll
+        for (int s = 0; s < KM; ++s) {
+            pk[s] = dpp_f<quad_perm(1, 0, 3, 2)>(lk[s]);
+            pj[s] = dpp_i<quad_perm(1, 0, 3, 2)>(lj[s]);
+        }
+#pragma unroll
+        for (int s = 0; s < KM; ++s)
+            if (s < kp.K) insert(pk[s], pj[s]);
+    } else {
+        static_assert(Q == 1, "one or two sub-lanes per drone");
+    }
+    if (!write) return;
+#pragma unroll 1
+    for (int t = 0; t * Q < kp.K; ++t) {
+        const int slot = q + Q * t;
+        int j = lj[0];
+#pragma unroll
+        for (int s = 1; s < KM; ++s) j = slot == s ? lj[s] : j;
+        if (slot < kp.K && j < kp.N) {
+            float* o = out + kp.so_dim + slot * F;
+            rel_features(kp, xch[2 * (base + j)], xch[2 * (base + j) + 1], P, H, aw, V, rng, gid, st_obs | ((uint32_t)j << 8),
+                         [&](int k, float v) { o[k] = clampf(v, kp.nclip_lo[k], kp.nclip_hi[k]); });
+        }
+    }
+}
+
 // segment (= env) helpers over the LPE = NPAD * Q lanes of an env (Q sub-lanes per drone)
 template <int LPE>
 __device__ __forceinline__ bool seg_any(bool x, int base) {
@@ -437,15 +508,66 @@ __device__ __forceinline__ float seg_sum(float v) {
     return v;
 }
 
+// Env collectives of flavor A.  An env inside one wave: segment ballots and the butterfly above.  An env that
+// spans the workgroup's NW waves (WIDE: 128-drone envs): the drone ballots of EnvColl (qs_common.h) and float
+// sums as a butterfly over each wave's drones whose NW partials meet in LDS and are added in wave order on every
+// lane (the same bits everywhere; two alternating slots, so one barrier per collective).  Every lane of the
+// workgroup makes the same calls.  Counts take x && q == 0 (one bit per drone in either form).
+template <int NPAD, int Q>
+struct EnvA {
+    static constexpr int LPE = NPAD * Q;
+    static constexpr bool WIDE = LPE > 64;
+    static constexpr int NW = WIDE ? LPE / 64 : 1;
+    EnvColl<WIDE, (NPAD > 64), Q, NW> ec;
+    float* fscr;   // WIDE: 4 NW floats
+    int fslot;
+    __device__ __forceinline__ EnvA(int base, uint64_t* bscr, float* fs) : fscr(fs), fslot(0) {
+        ec.lbase = base;
+        ec.lmask = (LPE >= 64) ? ~0ull : ((1ull << LPE) - 1ull);
+        ec.scr = bscr;
+        ec.slot = 0;
+    }
+    __device__ __forceinline__ bool any(bool x) { return ec.any(x); }
+    __device__ __forceinline__ int count(bool x) { return ec.count(x); }
+    __device__ __forceinline__ bool wany(bool x) { return ec.wany(x); }
+    __device__ __forceinline__ void sum2(float& a, float& b) {
+        if constexpr (!WIDE) {
+            a = seg_sum<NPAD, Q>(a);
+            b = seg_sum<NPAD, Q>(b);
+        } else {
+#pragma unroll
+            for (int m = Q; m < 64; m <<= 1) {
+                a += __shfl_xor(a, m);
+                b += __shfl_xor(b, m);
+            }
+            float* sc = fscr + 2 * NW * fslot;
+            fslot ^= 1;
+            const int w = threadIdx.x >> 6;
+            if ((threadIdx.x & 63) == 0) {
+                sc[w] = a;
+                sc[NW + w] = b;
+            }
+            lds_sync();
+            a = sc[0];
+            b = sc[NW];
+#pragma unroll
+            for (int k = 1; k < NW; ++k) {
+                a += sc[k];
+                b += sc[NW + k];
+            }
+        }
+    }
+};
+
 // Scenario_dynamic_repulsive.step (dynamic_repulsive.py:37-62): target flees the chasers (1/d each)
 // and the arena edge, speed <= v_max.  Every lane of the env computes the same update.
-template <int NPAD, int Q = 1>
-__device__ __forceinline__ void target_step(const KP& kp, float& tx, float& ty, const float* pos, bool contrib) {
+template <class Env>
+__device__ __forceinline__ void target_step(const KP& kp, float& tx, float& ty, const float* pos, bool contrib, Env& ev) {
     // the quotients as products with hardware reciprocals (~1 ulp; five IEEE divisions per tick otherwise)
     const float r0 = tx - pos[0], r1 = ty - pos[1];
     const float id2 = frcp(r0 * r0 + r1 * r1);
-    const float fx = seg_sum<NPAD, Q>(contrib ? r0 * id2 : 0.f);
-    const float fy = seg_sum<NPAD, Q>(contrib ? r1 * id2 : 0.f);
+    float fx = contrib ? r0 * id2 : 0.f, fy = contrib ? r1 * id2 : 0.f;
+    ev.sum2(fx, fy);
     const float de = fsqrt(tx * tx + ty * ty);
     const float iden = frcp(de * fmaxf(kp.arena - de, 0.1f));
     const float vx = fx - tx * iden, vy = fy - ty * iden;
@@ -459,16 +581,16 @@ __device__ __forceinline__ void target_step(const KP& kp, float& tx, float& ty, 
 // Scenario_dynamic_repulsive.reset (dynamic_repulsive.py:64-74, its step() sees the pre-reset chaser
 // positions) and QuadrotorSingle._reset (quadrotor_single_rewards.py:480-549).  All lanes of the
 // segment must call it (the target update is a segment reduction); `sel` lanes take the new state.
-template <int NPAD, int Q = 1>
+template <class Env>
 __device__ __forceinline__ void reset_env_a(const KP& kp, Drone& d, Ctl& c, float& tx, float& ty, bool has_pos, bool active,
-                            bool sel, const Rng& rng, uint32_t gid, uint32_t genv) {
+                            bool sel, const Rng& rng, uint32_t gid, uint32_t genv, Env& ev) {
     float ru[4], ue[4];
     uniforms4(rng, gid, S_RESET_A, 0, ru);
     if (kp.scenario == QS_SCEN_DYNAMIC_REPULSIVE) {
         uniforms4(rng, genv, S_SCEN, 0, ue);
         const float a = ue[1] - 0.5f, b = ue[2] - 0.5f, in = rsqrtf(a * a + b * b), tr = ue[3] * 3.f + 2.f;
         float ntx = a * in * tr, nty = b * in * tr;
-        target_step<NPAD, Q>(kp, ntx, nty, d.pos, active && has_pos);
+        target_step(kp, ntx, nty, d.pos, active && has_pos, ev);
         if (sel) {
             tx = ntx;
             ty = nty;
@@ -575,14 +697,28 @@ __device__ __forceinline__ void qbc_ticks(const float (&zr)[4], float (&z)[4], f
 }
 template <int NPAD>
 struct StepGeoA {
-    static constexpr int Q = NPAD * QS_QA <= 64 ? QS_QA : 64 / NPAD;
+    // 128-drone envs: QS_QW sub-lanes, the env is a workgroup of 4 waves (one per SIMD at 256 envs)
+    static constexpr int Q = NPAD * QS_QA <= 64 ? QS_QA : (NPAD > 64 ? QS_QW : 64 / NPAD);
     static constexpr int LPE = NPAD * Q;        // lanes per env
-    static constexpr int EPB = 64 / LPE;        // envs per workgroup (one wave)
+    static constexpr int WGS = LPE > 64 ? LPE : 64;   // threads per workgroup: one wave, or the env's waves
+    static constexpr int EPB = WGS / LPE;       // envs per workgroup
     static constexpr int SLOTS = EPB * NPAD;    // drone slots (LDS rows) per workgroup
+    static constexpr bool WIDE = LPE > 64;      // the env spans the workgroup's waves
 };
+// the explicit reset kernel: one lane per drone
+template <int NPAD>
+struct ResetGeoA {
+    static constexpr int WGS = NPAD > 64 ? NPAD : 64;
+    static constexpr int EPB = WGS / NPAD;
+    static constexpr int SLOTS = EPB * NPAD;
+};
+// LDS words after the exchange tile (64 words before the scenario tables, qs_scen.h scen_tab): the env-finished
+// flags (one per env of the workgroup), then for the multi-wave envs the collectives' scratch (EnvColl ballots at
+// words 16-31, float sums at 32-47), the episode counters (48-58) and env drone 0's goal (60-62)
+constexpr int QS_A_SCR_BITS = 16, QS_A_SCR_SUM = 32, QS_A_SCR_CNT = 48, QS_A_SCR_GOAL0 = 60;
 
 template <int NPAD>
-__global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, Bufs b) {
+__global__ __launch_bounds__(StepGeoA<NPAD>::WGS) void step_kernel_a(const KP* __restrict__ kpp, Bufs b) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     QS_BIND_KP(kpp);
     const uint32_t seed = kpm.seed;
@@ -594,7 +730,8 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
     QS_RTSTAMP(12);
     QS_STAMP_MARK();
     using G = StepGeoA<NPAD>;
-    constexpr int Q = G::Q, LPE = G::LPE, EPB = G::EPB, SLOTS = G::SLOTS;
+    constexpr int Q = G::Q, LPE = G::LPE, EPB = G::EPB, SLOTS = G::SLOTS, WGS = G::WGS;
+    constexpr bool WIDE = G::WIDE;
     const int lane = threadIdx.x;
     const int el = lane / LPE, di = (lane % LPE) / Q, q = lane % Q;
     const int env0 = blockIdx.x * EPB;
@@ -610,9 +747,11 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
     float* row = lds + (size_t)(el * kp.N + di) * kp.obs_dim;
     float4* xch = reinterpret_cast<float4*>(lds + SLOTS * kp.obs_dim);
     int* efin = reinterpret_cast<int*>(lds + SLOTS * kp.obs_dim + SLOTS * 8);
+    EnvA<NPAD, Q> ev(base, reinterpret_cast<uint64_t*>(efin + QS_A_SCR_BITS), reinterpret_cast<float*>(efin + QS_A_SCR_SUM));
+    using Row = typename RowOf<(NPAD > 64)>::T;
 
     Drone d;
-    load_drone(kp, b, g, d);
+    load_drone<(NPAD > 64)>(kp, b, g, d);
     Ctl c;
     load_ctl(kp, b, g, c);
     const float a0 = reinterpret_cast<const float2*>(b.act)[g].x;
@@ -633,7 +772,6 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
     constexpr int NCNT = 11, CT = (NCNT + LPE - 1) / LPE;
     const int li = lane - base;
     const bool envok = env < kp.E;
-    const uint64_t lmask = (LPE == 64) ? ~0ull : ((1ull << LPE) - 1ull);
     int cnt[CT], cnt0[CT];
 #pragma unroll
     for (int t = 0; t < CT; ++t) {
@@ -680,7 +818,7 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
             gdist = fsqrt(gx * gx + gy * gy + gz * gz);
         }
         if (kp.stats) {   // collisions between drones and with the room (:649-720): bookkeeping only
-            uint64_t cur = 0;
+            Row cur{};
             const float thr2 = kp.col_thr * kp.col_thr;
             if constexpr (LPE == 16 && NPAD * Q == 16) {   // (32-bit row words: the env's drones are < 16)
                 uint32_t c32 = 0;
@@ -699,18 +837,19 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
                     const float4 pj = xch[2 * (sbase + (j < NPAD ? j : NPAD - 1))];
                     const float dx = d.pos[0] - pj.x, dy = d.pos[1] - pj.y, dz = d.pos[2] - pj.z;
                     const bool hit = (j != di) & (j < kp.N) & (dx * dx + dy * dy + dz * dz <= thr2);
-                    cur |= hit ? (1ull << j) : 0ull;
+                    row_set(cur, j, hit);
                 }
                 cur = qor<Q>(cur);
                 lds_sync();   // the tile is rewritten next tick
             }
-            const bool uniq = active && cur != 0 && d.prev == 0;   // setdiff1d(flat(cur), flat(prev))
-            d.prev = cur;
-            auto env_count = [&](bool x) { return __popcll((__ballot(x && q == 0) >> base) & lmask); };
+            Row prevrow;
+            row_of(d, prevrow);
+            const bool uniq = active && row_any(cur) && !row_any(prevrow);   // setdiff1d(flat(cur), flat(prev))
+            row_keep(d, cur);
+            auto env_count = [&](bool x) { return ev.count(x && q == 0); };
             const bool settle = tick >= kp.st_settle;
             const bool fin5 = kpm.ep_len - (tick - 1) <= kp.st_final;   // time_remain (before tick += 1)
-            const uint64_t ub = __ballot(uniq && q == 0);
-            const int col = ub ? (int)__popcll((ub >> base) & lmask) / 2 : 0;   // wave-uniform skip
+            const int col = env_count(uniq) / 2;
             if (col > 0 && settle && uniq) d.flags |= QS_FL_HIT_AGENT;
             const bool wall_new = (d.flags & QS_FL_CRASH_WALL) && !(d.flags & QS_FL_PREV_WALL);
             const bool ceil_new = (d.flags & QS_FL_CRASH_CEIL) && !(d.flags & QS_FL_PREV_CEIL);
@@ -719,7 +858,7 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
             d.flags = (d.flags & ~(uint32_t)(QS_FL_PREV_WALL | QS_FL_PREV_CEIL | QS_FL_PREV_ROOM)) |
                       (wall_new ? QS_FL_PREV_WALL : 0u) | (ceil_new ? QS_FL_PREV_CEIL : 0u) |
                       (room_new ? (uint32_t)QS_FL_PREV_ROOM : 0u);
-            if (__ballot(cfloor || wall_new || ceil_new || room_new || col > 0)) {   // rare: something to count
+            if (ev.wany(cfloor || wall_new || ceil_new || room_new || col > 0)) {   // rare: something to count
                 const int nfl = env_count(cfloor), nw = env_count(active && wall_new);
                 const int nc = env_count(active && ceil_new), nr = env_count(room_new);
 #pragma unroll
@@ -735,16 +874,31 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
         gox = d.goal[0];
         goy = d.goal[1];
         // capture reward (:711-735) against env 0's goal; dones (:882-988)
-        const float g0x = repulsive ? tx : __shfl(d.goal[0], base), g0y = repulsive ? ty : __shfl(d.goal[1], base);
+        float g0x = tx, g0y = ty;
+        if (!repulsive) {
+            if constexpr (WIDE) {   // env drone 0's goal through LDS (read before the next collective's barrier)
+                float* g0 = reinterpret_cast<float*>(efin + QS_A_SCR_GOAL0);
+                if (threadIdx.x == 0) {
+                    g0[0] = d.goal[0];
+                    g0[1] = d.goal[1];
+                }
+                lds_sync();
+                g0x = g0[0];
+                g0y = g0[1];
+            } else {
+                g0x = __shfl(d.goal[0], base);
+                g0y = __shfl(d.goal[1], base);
+            }
+        }
         const float dx = g0x - d.pos[0], dy = g0y - d.pos[1];
         const float rel = fsqrt(dx * dx + dy * dy);
         const bool capi = capr > rel;
-        const bool cap = seg_any<LPE>(active && capi, base);
+        const bool cap = ev.any(active && capi);
         const float captor = cap && capi ? kp.w_captor : 0.f;
         const float helper = cap && capr < rel ? kp.w_helper : 0.f;
         rw = ((0.f + captor) + helper) + kp.existence;
         dn = cap ? capi : (tick > kpm.ep_len);
-        fin = seg_any<LPE>(active && dn, base);
+        fin = ev.any(active && dn);
         success = success || cap;
         QS_STAMP_ACC(5);
         // perform_downwash once per tick with the control dt (:810-815); the reference then rebuilds the
@@ -752,9 +906,9 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
         bool dwa = false;
         if (kp.downwash && kp.N > 1)
             dwa = downwash_env<NPAD, Q>(kp, d, rng, gid, env, base, di, q, active,
-                                        kp.obs_dim >= 8 ? reinterpret_cast<float4*>(lds) : nullptr, sbase);
+                                        kp.obs_dim >= 8 ? reinterpret_cast<float4*>(lds) : (WIDE ? xch : nullptr), sbase);
         if (repulsive) {   // scenario.step() (:797)
-            target_step<NPAD, Q>(kp, tx, ty, d.pos, active);
+            target_step(kp, tx, ty, d.pos, active, ev);
             d.goal[0] = tx;
             d.goal[1] = ty;
         } else if (SCEN) {   // scenario.step() of a goal scenario (:848): the env's goal table in LDS
@@ -771,7 +925,7 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
         }
         // downwash anywhere in the env: the tick's obs are rebuilt after scenario.step (:848-859), i.e. they
         // see the moved goal
-        if (kp.downwash && kp.N > 1 && seg_any<LPE>(active && dwa, base)) {
+        if (kp.downwash && kp.N > 1 && ev.any(active && dwa)) {
             gox = d.goal[0];
             goy = d.goal[1];
         }
@@ -792,37 +946,48 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
     lds_sync();
     if (fin && di == 0 && q == 0) efin[el] = 1;
     if (lead) self_obs_a(kp, d, c, gox, goy, rng_last, gid, S_SENSOR, S_SELF_CAM, row);
-    if (kp.K > 0)
-        neighbor_obs_a<NPAD, Q>(kp, xch, sbase, di, d.pos, c.angle, c.angle, d.vel, rng_last, gid, false, active, row, q);
+    if (kp.K > 0) {
+        if constexpr (WIDE)
+            neighbor_obs_wide<NPAD, Q>(kp, xch, sbase, di, d.pos, c.angle, c.angle, d.vel, rng_last, gid, false, active, row, q);
+        else
+            neighbor_obs_a<NPAD, Q>(kp, xch, sbase, di, d.pos, c.angle, c.angle, d.vel, rng_last, gid, false, active, row, q);
+    }
 
     const bool state_bad = lead && drone_nonfinite(d), rew_bad = lead && !(rw * 0.f == 0.f);
     QS_STAMP_ACC(7);
-    const uint64_t fball = __ballot(active && fin);
-    if (fball) {  // some env finished: terminal obs + the worker's reset (subproc_vec_env_custom.py:42-46)
+    if (ev.wany(active && fin)) {  // some env finished: terminal obs + the worker's reset (subproc_vec_env_custom.py:42-46)
         lds_sync();
         for (int r = 0; r < rows; ++r) {
             if (!efin[r / kp.N]) continue;
-            for (int q = lane; q < kp.obs_dim; q += 64)
+            for (int q = lane; q < kp.obs_dim; q += WGS)
                 b.term[(size_t)(env0 * kp.N + r) * kp.obs_dim + q] = lds[(size_t)r * kp.obs_dim + q];
         }
         lds_sync();
         if (kp.stats) {   // the finished episodes' episode_extra_stats rows (:886-969)
             float cv[NCNT];
+            if constexpr (WIDE) {   // the counters live on lanes 0..10 of wave 0: through LDS
+                int* cs = efin + QS_A_SCR_CNT;
+                if (li < NCNT) cs[li] = cnt[0];
+                lds_sync();
 #pragma unroll
-            for (int k = 0; k < NCNT; ++k) cv[k] = (float)__shfl(cnt[k / LPE], base + k % LPE);
-            auto env_bits = [&](bool x) { return (__ballot(x && q == 0) >> base) & lmask; };
-            const uint64_t hit_a = env_bits(active && (d.flags & QS_FL_HIT_AGENT));
-            const uint64_t all = env_bits(active);
+                for (int k = 0; k < NCNT; ++k) cv[k] = (float)cs[k];
+            } else {
+#pragma unroll
+                for (int k = 0; k < NCNT; ++k) cv[k] = (float)__shfl(cnt[k / LPE], base + k % LPE);
+            }
+            auto env_bits = [&](bool x) { return ev.ec.bits(x && q == 0); };
+            const Row hit_a = env_bits(active && (d.flags & QS_FL_HIT_AGENT));
+            const Row all = env_bits(active);
             if (active && fin && q == 0) {
                 const float n = (float)kp.N;
-                const uint64_t ok = all & ~hit_a;   // agent_col_obst stays 1 (no obstacles in flavor A)
+                const Row ok = all & ~hit_a;   // agent_col_obst stays 1 (no obstacles in flavor A)
                 float* er = b.estats + (size_t)g * QS_NES;
 #pragma unroll
                 for (int k = 0; k < NCNT; ++k) er[QS_ES_COL + k] = cv[k];
                 er[QS_ES_SUCCESS] = 0.f;                           // reached_goal is never set (:797-802)
-                er[QS_ES_DEADLOCK] = (float)__popcll(ok) / n;
-                er[QS_ES_COLRATE] = 1.f - (float)__popcll(ok) / n;
-                er[QS_ES_NCOLRATE] = 1.f - (float)__popcll(all & ~hit_a) / n;
+                er[QS_ES_DEADLOCK] = (float)row_popc(ok) / n;
+                er[QS_ES_COLRATE] = 1.f - (float)row_popc(ok) / n;
+                er[QS_ES_NCOLRATE] = 1.f - (float)row_popc(all & ~hit_a) / n;
                 er[QS_ES_OCOLRATE] = 0.f;
                 er[QS_ES_SCEN] = repulsive ? 18.f : (SCEN ? (float)b.env[QS_E_SC_MODE * kp.E + env] : 0.f);
                 const float nan = __builtin_nanf("");                  // np.mean of the empty distance list
@@ -834,14 +999,14 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
                 const int k = li + LPE * t;
                 if (envok && fin && k < NCNT) b.env[(QS_E_ST_COL + k) * kp.E + env] = 0;
             }
-            if (fin) d.prev = 0;
+            if (fin) row_keep(d, Row{});
         }
         const float sh = c.angle, sv[3] = {d.vel[0], d.vel[1], d.vel[2]};  // QuadrotorEnvMulti.heading / .vel
         const Rng rr = env_rng(seed, tick, episode);
         if (SCEN)
             scen_reset_a<NPAD>(kp, b, stab, env, di, active && fin && di == 0 && q == 0, active && fin, rr,
                                kp.id0 + (uint32_t)(env * kp.N), d);
-        reset_env_a<NPAD, Q>(kp, d, c, tx, ty, true, active, active && fin, rr, gid, kp.id0 + (uint32_t)(env * kp.N));
+        reset_env_a(kp, d, c, tx, ty, true, active, active && fin, rr, gid, kp.id0 + (uint32_t)(env * kp.N), ev);
         if (lead && fin) {
             self_obs_a(kp, d, c, d.goal[0], d.goal[1], rr, gid, S_RESET_SENSOR, S_RESET_SELF_CAM, row);
             b.stale[0 * kp.I + g] = sv[0];
@@ -852,16 +1017,19 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
         if (kp.K > 0) {
             if (q == 0) xch_put_a(xch, sbase + di, d.pos, sh, sv);
             lds_sync();
-            neighbor_obs_a<NPAD, Q>(kp, xch, sbase, di, d.pos, sh, c.angle, sv, rr, gid, true, active && fin, row, q);
+            if constexpr (WIDE)
+                neighbor_obs_wide<NPAD, Q>(kp, xch, sbase, di, d.pos, sh, c.angle, sv, rr, gid, true, active && fin, row, q);
+            else
+                neighbor_obs_a<NPAD, Q>(kp, xch, sbase, di, d.pos, sh, c.angle, sv, rr, gid, true, active && fin, row, q);
         }
     }
     lds_sync();
     QS_STAMP_ACC(8);
-    const int obs_bad = tile_store(lds, b.obs + (size_t)env0 * kp.N * kp.obs_dim, rows * kp.obs_dim, lane);
+    const int obs_bad = tile_store(lds, b.obs + (size_t)env0 * kp.N * kp.obs_dim, rows * kp.obs_dim, lane, WGS);
     guard_count(b, obs_bad, rew_bad, state_bad);
 
     if (lead) {
-        store_drone(kp, b, g, d);
+        store_drone<(NPAD > 64)>(kp, b, g, d);
         store_ctl(kp, b, g, c);
         b.rew[g] = rw;
         b.done[g] = fin ? 1 : 0;
@@ -885,11 +1053,12 @@ __global__ __launch_bounds__(64) void step_kernel_a(const KP* __restrict__ kpp, 
 
 // explicit reset of masked envs (quadrotor_multi_rewards.QuadrotorEnvMulti.reset)
 template <int NPAD>
-__global__ __launch_bounds__(64) void reset_kernel_a(const KP* __restrict__ kpp, Bufs b) {
+__global__ __launch_bounds__(ResetGeoA<NPAD>::WGS) void reset_kernel_a(const KP* __restrict__ kpp, Bufs b) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     QS_BIND_KP(kpp);
     const uint32_t seed = kpm.seed;
-    constexpr int EPB = 64 / NPAD;
+    using G = ResetGeoA<NPAD>;
+    constexpr int EPB = G::EPB, SLOTS = G::SLOTS, WGS = G::WGS;
     const int lane = threadIdx.x;
     const int el = lane / NPAD, di = lane % NPAD;
     const int env0 = blockIdx.x * EPB;
@@ -905,8 +1074,10 @@ __global__ __launch_bounds__(64) void reset_kernel_a(const KP* __restrict__ kpp,
     const int eflags = b.env[QS_E_FLAGS * kp.E + eidx];
     const Rng rng = env_rng(seed, b.env[QS_E_TICK * kp.E + eidx], episode);
     float* row = lds + (size_t)(el * kp.N + di) * kp.obs_dim;
+    int* escr = reinterpret_cast<int*>(lds + SLOTS * kp.obs_dim + SLOTS * 8);
+    EnvA<NPAD, 1> ev(base, reinterpret_cast<uint64_t*>(escr + QS_A_SCR_BITS), reinterpret_cast<float*>(escr + QS_A_SCR_SUM));
     Drone d;
-    load_drone(kp, b, g, d);
+    load_drone<(NPAD > 64)>(kp, b, g, d);
     Ctl c;
     load_ctl(kp, b, g, c);
     float tx = b.envf[QS_ENVF_TARGET_X * kp.E + eidx], ty = b.envf[QS_ENVF_TARGET_Y * kp.E + eidx];
@@ -917,27 +1088,30 @@ __global__ __launch_bounds__(64) void reset_kernel_a(const KP* __restrict__ kpp,
     for (int q = 0; q < 3; ++q) sv[q] = stale_valid ? b.stale[q * kp.I + g] : d.vel[q];
     const bool success = eflags & QS_EF_SUCCESS;
     if (kp.scen_b >= 0)
-        scen_reset_a<NPAD>(kp, b, scen_tab(lds, kp, 64) + el * scen_stride<NPAD>(), env, di, sel && di == 0, sel, rng,
+        scen_reset_a<NPAD>(kp, b, scen_tab(lds, kp, SLOTS) + el * scen_stride<NPAD>(), env, di, sel && di == 0, sel, rng,
                            kp.id0 + (uint32_t)(env * kp.N), d);
-    reset_env_a<NPAD>(kp, d, c, tx, ty, eflags & QS_EF_HAS_POS, inr, sel, rng, gid, kp.id0 + (uint32_t)(env * kp.N));
+    reset_env_a(kp, d, c, tx, ty, eflags & QS_EF_HAS_POS, inr, sel, rng, gid, kp.id0 + (uint32_t)(env * kp.N), ev);
     if (sel) self_obs_a(kp, d, c, d.goal[0], d.goal[1], rng, gid, S_RESET_SENSOR, S_RESET_SELF_CAM, row);
     if (kp.K > 0) {
-        float4* xch = reinterpret_cast<float4*>(lds + 64 * kp.obs_dim);
+        float4* xch = reinterpret_cast<float4*>(lds + SLOTS * kp.obs_dim);
         xch_put_a(xch, lane, d.pos, sh, sv);
         lds_sync();
-        neighbor_obs_a<NPAD>(kp, xch, base, di, d.pos, sh, c.angle, sv, rng, gid, true, sel, row);
+        if constexpr (NPAD > 64)
+            neighbor_obs_wide<NPAD>(kp, xch, base, di, d.pos, sh, c.angle, sv, rng, gid, true, sel, row);
+        else
+            neighbor_obs_a<NPAD>(kp, xch, base, di, d.pos, sh, c.angle, sv, rng, gid, true, sel, row);
     }
     lds_sync();
     const int nenv_blk = min(EPB, kp.E - env0);
     for (int r = 0; r < nenv_blk * kp.N; ++r) {
         const int e = env0 + r / kp.N;
         if (b.mask != nullptr && b.mask[e] == 0) continue;
-        for (int q = lane; q < kp.obs_dim; q += 64)
+        for (int q = lane; q < kp.obs_dim; q += WGS)
             b.obs[(size_t)(env0 * kp.N + r) * kp.obs_dim + q] = lds[(size_t)r * kp.obs_dim + q];
     }
     if (env < kp.E && di == 0) b.rinfo[env] = envsel ? (success ? 2 : 1) : 0;
     if (sel) {
-        store_drone(kp, b, g, d);
+        store_drone<(NPAD > 64)>(kp, b, g, d);
         store_ctl(kp, b, g, c);
 #pragma unroll
         for (int q = 0; q < 3; ++q) b.stale[q * kp.I + g] = sv[q];

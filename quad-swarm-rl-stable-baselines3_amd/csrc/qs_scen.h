@@ -167,8 +167,9 @@ __device__ int sc_generate(int f, int n, int per_layer, float size, float layer,
         return m;
     }
     if (f == F_CUBE) {
-        // int(np.power(n, 1/3)) as float64 rounds it for n <= 32: 27 ** (1/3) = 2.9999999999999996 -> 2
-        const int fd = n < 8 ? 1 : (n <= 27 ? 2 : 3);
+        // int(np.power(n, 1/3)) as float64 rounds it: 27 ** (1/3) = 2.9999999999999996 -> 2, 64 ** (1/3) -> 3,
+        // 125 ** (1/3) = 4.999999999999999 -> 4 (the steps over n <= 128, QS_MAX_AGENTS)
+        const int fd = n < 8 ? 1 : (n < 28 ? 2 : (n < 65 ? 3 : (n < 126 ? 4 : 5)));
         for (int i = 0; i < n; ++i) {
             float* gi = g + 4 * i;
             gi[0] = c[2] + size * (float)(i / (fd * fd));

@@ -133,8 +133,6 @@ static int validate(const qs_config* c) {
     if (c->num_agents < 1 || c->num_agents > QS_MAX_AGENTS)
         return fail(QS_E_UNSUPPORTED, "num_agents must be in [1, QS_MAX_AGENTS]");
     if (c->flavor != QS_FLAVOR_B && c->flavor != QS_FLAVOR_A) return fail(QS_E_INVALID, "unknown flavor");
-    if (c->num_agents > 64 && c->flavor != QS_FLAVOR_B)
-        return fail(QS_E_UNSUPPORTED, "envs of more than 64 drones (two-wave workgroups) are implemented for flavor B");
     if (c->neighbor_obs < 0 || c->neighbor_obs > QS_NEIGHBOR_NPOS) return fail(QS_E_INVALID, "unknown neighbor_obs");
     if (c->flavor == QS_FLAVOR_B) {
         if (c->obs_repr < 0 || c->obs_repr > 2) return fail(QS_E_INVALID, "obs_repr is not a flavor-B repr");
@@ -172,6 +170,10 @@ static int validate(const qs_config* c) {
             return fail(QS_E_INVALID, "run_away needs at least 2 drones (run_away.py:16-27)");
         if (c->ticks_per_step < 1) return fail(QS_E_INVALID, "ticks_per_step must be >= 1");
         if (c->n_cameras < 1) return fail(QS_E_INVALID, "n_cameras must be >= 1");
+        // envs of more than 64 drones (multi-wave workgroups) select their neighbours by register insertion
+        // (qs_flavor_a.h neighbor_obs_wide)
+        if (c->num_agents > 64 && c->neighbor_obs != QS_NEIGHBOR_NONE && c->k_neighbors > QS_A_KMAX)
+            return fail(QS_E_UNSUPPORTED, "flavor A with more than 64 drones: k_neighbors must be <= QS_A_KMAX (16)");
     }
     if (c->neighbor_obs != QS_NEIGHBOR_NONE && (c->k_neighbors < 1 || c->k_neighbors > c->num_agents - 1))
         return fail(QS_E_INVALID, "k_neighbors must be in [1, num_agents-1]");
@@ -489,13 +491,15 @@ extern "C" int qs_layout_query(const qs_config* c, qs_layout* out) {
 // when an env would not fit a wave); resets one lane.  Specialised kernels may be compiled with another Q
 // (qs_handle::qb / qa).
 // flavor B (qs::StepGeo): QS_QW sub-lanes for the multi-wave 64 / 128-drone envs; flavor A (qs::StepGeoA): an
-// env stays inside one wave
+// env of up to 64 drones stays inside one wave, a 128-drone env takes QS_QW sub-lanes over 4 waves
 static int step_lanes_per_drone(int npad, int q, bool flavor_a = false) {
-    return npad * q <= 64 ? q : (npad >= 64 && !flavor_a ? QS_QW : 64 / npad);
+    return npad * q <= 64 ? q : ((npad >= 64 && !flavor_a) || npad > 64 ? QS_QW : 64 / npad);
 }
 static_assert(qs::StepGeo<8>::Q == QS_QB && qs::StepGeo<32>::Q == 64 / 32 && qs::StepGeo<64>::Q == QS_QW &&
               qs::StepGeo<128>::Q == QS_QW && qs::StepGeo<128>::WGS == 128 * QS_QW && qs::StepGeoA<8>::Q == QS_QA &&
-              qs::StepGeoA<32>::Q == 2 && qs::StepGeoA<64>::Q == 1, "step_lanes_per_drone");
+              qs::StepGeoA<32>::Q == 2 && qs::StepGeoA<64>::Q == 1 && qs::StepGeoA<128>::Q == QS_QW &&
+              qs::StepGeoA<128>::WGS == 128 * QS_QW && qs::ResetGeoA<128>::WGS == 128 && qs::ResetGeoA<8>::EPB == 8,
+              "step_lanes_per_drone");
 // threads per workgroup: one wave, or (128-drone envs) the env's lanes
 static int block_threads(const qs_config& c, int npad, bool step, int qb = QS_QB, int qa = QS_QA) {
     const int q = !step ? 1 : step_lanes_per_drone(npad, c.flavor == QS_FLAVOR_A ? qa : qb, c.flavor == QS_FLAVOR_A);
@@ -655,9 +659,14 @@ static int launch(qs_handle* h, bool step, const float* act, const uint8_t* mask
         QS_LAUNCH(16)
         QS_LAUNCH(32)
         QS_LAUNCH(64)
-        case 128:   // flavor B without obstacles only (validate)
-            if (step) hipLaunchKernelGGL((qs::step_kernel<128, false>), grid, block, shm, s, kpd, b, rb, rp);
-            else hipLaunchKernelGGL((qs::reset_kernel<128, false>), grid, block, shm, s, kpd, b);
+        case 128:   // flavor A, or flavor B without obstacles (validate)
+            if (a) {
+                if (step) hipLaunchKernelGGL(qs::step_kernel_a<128>, grid, block, shm, s, kpd, b);
+                else hipLaunchKernelGGL(qs::reset_kernel_a<128>, grid, block, shm, s, kpd, b);
+            } else {
+                if (step) hipLaunchKernelGGL((qs::step_kernel<128, false>), grid, block, shm, s, kpd, b, rb, rp);
+                else hipLaunchKernelGGL((qs::reset_kernel<128, false>), grid, block, shm, s, kpd, b);
+            }
             break;
         default:
             return fail(QS_E_UNSUPPORTED, "num_agents not supported");

@@ -275,11 +275,12 @@ class QuadSwarmConfig:
             raise ValueError("replay_buffer_sample_prob must be in [0, 1]")
         if not 1 <= self.num_agents <= N.MAX_AGENTS:
             raise ValueError(f"num_agents must be in [1, {N.MAX_AGENTS}]")
-        if self.num_agents > 64 and self.flavor != "B":   # qs_step.hip validate: two-wave envs are flavor B
-            raise ValueError("envs of more than 64 drones are implemented for flavor B (quad_swarm_rl's env)")
         k = self.k_neighbors
         if self.neighbor_obs_type != "none" and self.num_agents > 1 and not 1 <= k <= self.num_agents - 1:
             raise ValueError("neighbor_visible_num out of range")
+        # qs_step.hip validate: flavor-A envs of more than 64 drones keep their k nearest in registers
+        if self.flavor == "A" and self.num_agents > 64 and self.neighbor_obs_type != "none" and k > N.A_KMAX:
+            raise ValueError(f"flavor A with more than 64 drones: neighbor_visible_num must be <= {N.A_KMAX}")
 
     def to_qs_config(self):
         self.validate()

@@ -82,12 +82,16 @@ def test_validation_errors_are_reported():
     bad = N.QsConfig.from_buffer_copy(c)
     bad.num_agents = 129
     assert L.qs_layout_query(bad, lay) == -2
-    # envs of 65..128 drones (two-wave workgroups) are flavor B only; their obs tile must fit the LDS
+    # envs of 65..128 drones (multi-wave workgroups): flavor A keeps its k nearest in registers (k <= 16); the
+    # obs tile must fit the LDS
     a = N.QsConfig.from_buffer_copy(QuadSwarmConfig.sb_train(num_envs=4, num_agents=8).to_qs_config())
     a.num_agents = 65
-    assert L.qs_layout_query(a, lay) == -2 and b"flavor B" in L.qs_last_error()
+    assert L.qs_layout_query(a, lay) == 0
+    a.k_neighbors = N.A_KMAX + 1
+    assert L.qs_layout_query(a, lay) == -2 and b"QS_A_KMAX" in L.qs_last_error()
     with pytest.raises(ValueError):
-        QuadSwarmConfig.sb_train(num_envs=2, num_agents=128).to_qs_config()
+        QuadSwarmConfig.sb_train(num_envs=2, num_agents=128).to_qs_config()   # all 127 neighbours visible
+    QuadSwarmConfig.sb_train(num_envs=2, num_agents=128, neighbor_visible_num=7).to_qs_config()
     wide = N.QsConfig.from_buffer_copy(QuadSwarmConfig(num_envs=4, num_agents=128, neighbor_visible_num=127).to_qs_config())
     assert L.qs_layout_query(wide, lay) == -2 and b"LDS" in L.qs_last_error()
     # the state / istate byte offsets (32-bit, 2 GB buffer descriptor) bound the drone count: the largest

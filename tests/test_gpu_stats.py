@@ -155,14 +155,15 @@ def test_vec_env_raises_on_nan_reward():
     venv.close()
 
 
-def test_flavor_a_episode_stats_match_oracle():
+@pytest.mark.parametrize("E,N", [(128, 8), (8, 128)])
+def test_flavor_a_episode_stats_match_oracle(E, N):
     """Flavor A (quadrotor_multi_rewards.py:649-720 per tick, :886-969 at done): the A kernel's per-tick collision
     and room bookkeeping against the oracle's (pinned to the reference's dicts by a_traj_n8stats), from identical
-    states every step; pairs 5 cm apart and drones driven into the ceiling / floor keep every counter busy."""
+    states every step; pairs 5 cm apart and drones driven into the ceiling / floor keep every counter busy.
+    N = 128: the env spans a 4-wave workgroup (128-bit collision rows, the counters' LDS collectives)."""
     from parity_utils import gpu_to_oracle_a, oracle_params_a, oracle_to_gpu_a
-    E, N = 128, 8
     cfg = QuadSwarmConfig.sb_train(num_envs=E, num_agents=N, neighbor_obs_type="dist_angle", seed=4,
-                                   episode_duration=3.0)
+                                   episode_duration=3.0, neighbor_visible_num=7 if N > 8 else -1)
     env = QuadSwarmEnv(cfg)
     assert env.estats is not None
     oenv = O.OracleEnvA(oracle_params_a(cfg), seed=4)

@@ -160,7 +160,7 @@ def load_traj_a(golden, name, which="init"):
     return g, p, drones, envs
 
 
-TRAJ = ["n4", "n8", "n8k3cam", "n1", "n4quiet", "n8dw", "n8stats"]
+TRAJ = ["n4", "n8", "n8k3cam", "n1", "n4quiet", "n8dw", "n8stats", "n128k7"]
 
 
 @pytest.mark.parametrize("name", [t for t in TRAJ if t not in ("n8dw", "n8stats")])   # edited after the reset

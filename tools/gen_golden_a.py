@@ -19,6 +19,7 @@ Fixtures (plain arrays, np.load(allow_pickle=False)):
   a_obs.npz        state_* of every flavor-A obs repr with recorded sensor noise
   a_neighbors.npz  QuadrotorEnvMulti.add_neighborhood_obs for every flavor-A neighbour type
   a_traj_*.npz     whole-env trajectories (step + the SB3 worker's reset on done) with both tapes
+                   (a_traj_n128k7: `python tools/gen_golden_a.py n128`, see main_extra)
 """
 import os
 import sys
@@ -367,7 +368,9 @@ def main_extra(which):
     """Fixtures added later, generated on their own (the ones above stay byte-identical):
       dw     use_downwash (quadrotor_multi_rewards.py:810-815) with stacked drone pairs, 8 drones
       stats  episode_extra_stats of the episodes that end (quadrotor_multi_rewards.py:886-969)
-      info   every agent's per-step infos["goal_dist"] (quadrotor_single_rewards.py:457), captures and timeouts"""
+      info   every agent's per-step infos["goal_dist"] (quadrotor_single_rewards.py:457), captures and timeouts
+      n128   the paper's largest swarm (paper/fps_compare.py:7): 128 drones, the 7 nearest by the camera key (k < N - 1:
+             the selection pass over every pair, then the obs pass), five steps"""
     os.makedirs(OUT, exist_ok=True)
     if "dw" in which:
         gen_traj("n8dw", 8, 40, seed=36, ntype="dist_angle", repr_="cdist_cdistdot_dist_distdot_angle_angledot",
@@ -375,6 +378,8 @@ def main_extra(which):
     if "info" in which:
         gen_traj("n4info", 4, 120, seed=38, capture_schedule=lambda t: 3.0 if t >= 100 else 0.3, ep_time=0.8,
                  infos=True)
+    if "n128" in which:
+        gen_traj("n128k7", 128, 5, seed=39, k=7, capture_schedule=lambda t: 0.5, ep_time=30.0)
     if "stats" in which:
         gen_traj("n8stats", 8, 40, seed=37, ntype="dist_angle", repr_="cdist_cdistdot_dist_distdot_angle_angledot",
                  capture_schedule=lambda t: 0.01, ep_time=3.0, setup=setup_stats_a, stats=True)
