@@ -57,6 +57,12 @@ __device__ __forceinline__ float sin_small(float x) {
 #ifndef QS_CAM_RCP
 #define QS_CAM_RCP 1
 #endif
+#ifndef QS_CAM_SECTOR
+#define QS_CAM_SECTOR 1
+#endif
+#ifndef QS_A_DEAL_SENSE
+#define QS_A_DEAL_SENSE 1
+#endif
 
 // (x + pi) % (2 pi) - pi with Python's modulo sign convention.  For r = x + pi in [-2 pi, 4 pi) -- every
 // angle the step wraps -- fmodf(r, 2 pi) is r itself below 2 pi and r - 2 pi above (exact by Sterbenz), so
@@ -195,12 +201,32 @@ __device__ __forceinline__ void camera(const KP& kp, float rx, float ry, float g
     float s, c;
     sincos_hw(-ga, &s, &c);
     const float rp0 = c * rx - s * ry, rp1 = s * rx + c * ry;
+#if QS_CAM_SECTOR
+    // get_camera_angle (get_state.py:128-137) without the atan2: the camera whose axis k seg is nearest the
+    // bearing is the one with the largest projection rp . (cos k seg, sin k seg) (the first on an exact tie; the
+    // reference's round() differs only on the sector boundaries, where the features are ill-conditioned anyway).
+    // The axes are compile-time constants in the specialised kernels (libm cosf / sinf of constants fold).
+    const float seg = k2Pi / (float)kp.n_cam;
+    float best = rp0, ca = 1.f, sa = 0.f, cam = 0.f;
+    for (int k = 1; k < kp.n_cam; ++k) {
+        const float ck = cosf((float)k * seg), sk = sinf((float)k * seg);
+        const float pk = rp0 * ck + rp1 * sk;
+        const bool gt = pk > best;
+        best = gt ? pk : best;
+        ca = gt ? ck : ca;
+        sa = gt ? sk : sa;
+        cam = gt ? (float)k * seg : cam;
+    }
+    s = -sa;   // sincos(-cam)
+    c = ca;
+#else
     float m = atan2f(rp1, rp0);   // fmodf(m, 2 pi) is m itself: |atan2| <= pi
     if (m < 0.f) m += k2Pi;
     const float seg = k2Pi / (float)kp.n_cam;
     const int ci = ((int)rintf(m / seg)) % kp.n_cam;
     const float cam = (float)ci * seg;
     sincos_hw(-cam, &s, &c);
+#endif
     const float c0 = c * rp0 - s * rp1, c1 = s * rp0 + c * rp1;
     const float cn2 = c0 * c0 + c1 * c1, cn = fsqrt(cn2);
     const float r = kp.cam_r, r2 = r * r;
@@ -240,14 +266,20 @@ __device__ __forceinline__ void camera(const KP& kp, float rx, float ry, float g
 
 // pos / vel sensor noise (sensor_noise.py:234-261, draws 0-5 of the 27; the rest do not reach a
 // flavor-A observation)
+// zpre: the 8 normals already drawn (the step kernel deals the two blocks over the drone's sub-lanes), or null
 __device__ __forceinline__ void noisy_pos_vel(const KP& kp, const Drone& d, const Rng& rng, uint32_t gid,
-                                              uint32_t st, float* np_, float* nv) {
+                                              uint32_t st, float* np_, float* nv, const float* zpre = nullptr) {
 #pragma unroll
     for (int i = 0; i < 3; ++i) { np_[i] = d.pos[i]; nv[i] = d.vel[i]; }
     if (!kp.sense) return;
     float z[8];
-    normals4(rng, gid, st, 0, z);
-    normals4(rng, gid, st, 1, z + 4);
+    if (zpre) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) z[i] = zpre[i];
+    } else {
+        normals4(rng, gid, st, 0, z);
+        normals4(rng, gid, st, 1, z + 4);
+    }
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         np_[i] += kp.pos_std * z[i];
@@ -267,9 +299,9 @@ __device__ __forceinline__ void noisy_pos_vel(const KP& kp, const Drone& d, cons
 
 // flavor-A self observation (get_state.py:7-223)
 __device__ __forceinline__ void self_obs_a(const KP& kp, const Drone& d, const Ctl& c, float gx, float gy, const Rng& rng,
-                           uint32_t gid, uint32_t st_sensor, uint32_t st_cam, float* out) {
+                           uint32_t gid, uint32_t st_sensor, uint32_t st_cam, float* out, const float* zsense = nullptr) {
     float np_[3], nv[3];
-    noisy_pos_vel(kp, d, rng, gid, st_sensor, np_, nv);
+    noisy_pos_vel(kp, d, rng, gid, st_sensor, np_, nv, zsense);
     const float dt = kp.dt;
     const float rp0 = gx - np_[0], rp1 = gy - np_[1];
     const float rd = fsqrt(rp0 * rp0 + rp1 * rp1);
@@ -945,6 +977,13 @@ __global__ __launch_bounds__(StepGeoA<NPAD>::WGS) void step_kernel_a(const KP* _
     if (lane < EPB) efin[lane] = 0;
     lds_sync();
     if (fin && di == 0 && q == 0) efin[el] = 1;
+#if QS_A_DEAL_SENSE
+    if constexpr (Q == 2) {   // the sensor noise's two Philox blocks, one per sub-lane (bitwise the lead's draws)
+        float zs[8];
+        if (kp.sense) qdraws<Q, 2, 0>(rng_last, gid, S_SENSOR, 0, q, zs, nullptr);
+        if (lead) self_obs_a(kp, d, c, gox, goy, rng_last, gid, S_SENSOR, S_SELF_CAM, row, zs);
+    } else
+#endif
     if (lead) self_obs_a(kp, d, c, gox, goy, rng_last, gid, S_SENSOR, S_SELF_CAM, row);
     if (kp.K > 0) {
         if constexpr (WIDE)
