@@ -45,6 +45,7 @@ CONFIGS = {
     # (pos features: the formations stack drones vertically, where the horizontal bearing of dist_angle is the
     # atan2 of a ~0 vector and the k-nearest selection would rank such a neighbour by an ill-conditioned key)
     "mix128": dict(num_agents=128, neighbor_visible_num=4, neighbor_obs_type="pos", quads_mode="mix"),
+    "dw128": dict(num_agents=128, neighbor_visible_num=6, neighbor_obs_type="dist_angle", use_downwash=True),
     # use_downwash (quadrotor_multi_rewards.py:810-815): _perturb stacks the drones in vertical pairs
     "dw8": dict(num_agents=8, neighbor_obs_type="dist_angle", use_downwash=True),
     # goal scenarios through create_scenario (quadrotor_multi_rewards.py:123): mix draws one per env and reset
@@ -102,7 +103,8 @@ def _perturb(oenv, cfg, rng, step):
                 lo, hi = oenv.drones[e * oenv.N + i], oenv.drones[e * oenv.N + i + 1]
                 # pairs 0.8 m apart (no accidental cones between pairs: drones at one height sit on the
                 # cone's rz = 0 edge, where fp32 and fp64 may decide differently)
-                lo.pos[0], lo.pos[1] = -1.2 + 0.8 * (i // 2), 0.3
+                # (pairs on a row of 8, further rows 0.8 m apart for the 128-drone envs)
+                lo.pos[0], lo.pos[1] = -1.2 + 0.8 * ((i // 2) % 8), 0.3 + 0.8 * ((i // 2) // 8)
                 gap = rng.uniform(0.2, 0.5)
                 # 4-8 cm sideways: inside the 0.1 m cone, yet far enough that the pair's angle feature stays
                 # well conditioned after 8 fp32 ticks (atan2 of a mm-scale offset would not be)

@@ -83,7 +83,7 @@ for s in "$@"; do
       rm -f gpurun_out/prof_*/*kernel_trace.csv
       ;;
     sweep)
-      for c in c2 c3 c3mix c3mixr c4 c4dr c5 a8 n64 n128; do
+      for c in c2 c3 c3mix c3mixr c4 c4dr c5 a8 a128 n64 n128; do
         step sweep_$c 200 python bench.py --config $c --steps 1000 --no-cpu-baseline --e2e-iters 0
       done
       ;;
