@@ -131,10 +131,14 @@ __device__ __forceinline__ void mfma_layer_x3(const TileX3& X, const uint4* __re
     }
 }
 
-// Y = tanh(acc / (s_x s_w) + bias4(i, n0)), stored scaled by X3_SX as hi / lo
-template <int H, typename Bias4>
+// Y = tanh(acc / (s_x s_w) + bias4(i, n0)), stored scaled by X3_SX as hi / lo; out(i, n0, y4) also receives the
+// fp32 values (four consecutive columns of row i)
+struct NoOut {
+    __device__ void operator()(int, int, float4) const {}
+};
+template <int H, typename Bias4, typename Out = NoOut>
 __device__ __forceinline__ void store_tanh_x3(const TileX3& Y, const f32x16 (&acc)[RT][Geo<H>::CT], float inv, int wave,
-                                              int lane, Bias4 bias4) {
+                                              int lane, Bias4 bias4, Out out = NoOut()) {
     constexpr int CT = Geo<H>::CT;
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
@@ -145,10 +149,12 @@ __device__ __forceinline__ void store_tanh_x3(const TileX3& Y, const f32x16 (&ac
             for (int g = 0; g < 4; ++g) {
                 const int n0 = acc_n0<H>(wave, c, g, lane);
                 const float4 b = bias4(i, n0);
-                Y.put4(i, n0, make_float4(X3_SX * tanh_fast(fmaf(acc[rt][c][4 * g], inv, b.x)),
-                                          X3_SX * tanh_fast(fmaf(acc[rt][c][4 * g + 1], inv, b.y)),
-                                          X3_SX * tanh_fast(fmaf(acc[rt][c][4 * g + 2], inv, b.z)),
-                                          X3_SX * tanh_fast(fmaf(acc[rt][c][4 * g + 3], inv, b.w))));
+                const float4 y = make_float4(tanh_fast(fmaf(acc[rt][c][4 * g], inv, b.x)),
+                                             tanh_fast(fmaf(acc[rt][c][4 * g + 1], inv, b.y)),
+                                             tanh_fast(fmaf(acc[rt][c][4 * g + 2], inv, b.z)),
+                                             tanh_fast(fmaf(acc[rt][c][4 * g + 3], inv, b.w)));
+                out(i, n0, y);
+                Y.put4(i, n0, make_float4(X3_SX * y.x, X3_SX * y.y, X3_SX * y.z, X3_SX * y.w));   // (exact: 2^8)
             }
     }
 }
@@ -201,17 +207,14 @@ __global__ __launch_bounds__(NTHR, 2) __attribute__((amdgpu_waves_per_eu(2, 2)))
     __syncthreads();
     mfma_layer_x3<H, H, true, false>(X, reinterpret_cast<const uint4*>(t.w_e2p), acc, wave, lane);
     __syncthreads();   // every wave has read the tile
-    store_tanh_x3<H>(X, acc, 1.f / (X3_SX * X3_SW), wave, lane, [&](int, int n0) { return lds4(BI + H + n0); });
+    // e2 to HBM straight from the epilogue (fp32 tanh values; the pool's split of them is the tile's hi / lo, so
+    // its products are the same) -- no read-back of the split tile
+    store_tanh_x3<H>(X, acc, 1.f / (X3_SX * X3_SW), wave, lane, [&](int, int n0) { return lds4(BI + H + n0); },
+                     [&](int i, int n0, float4 y) {
+                         if (i < MU && row0 + i < R) *reinterpret_cast<float4*>(t.e2 + (row0 + i) * H + n0) = y;
+                     });
     __syncthreads();
     constexpr float isx = 1.f / X3_SX;
-    for (int e = tid; e < MROWS * (H / 4); e += NTHR) {
-        const int r = e / (H / 4), c4 = e - r * (H / 4);
-        const long j = row0 + r;
-        if (r < MU && j < R)
-            reinterpret_cast<float4*>(t.e2 + j * H)[c4] =
-                make_float4(X.get(r, 4 * c4) * isx, X.get(r, 4 * c4 + 1) * isx, X.get(r, 4 * c4 + 2) * isx,
-                            X.get(r, 4 * c4 + 3) * isx);
-    }
     const float inv = 1.f / (float)K;   // torch's mean: the sum times 1 / K
     for (int e = tid; e < AB * H; e += NTHR) {
         const int a = e / H, n = e - a * H;

@@ -145,6 +145,10 @@ for s in "$@"; do
       step profpol_pmc 200 timeout -s KILL 180 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE --kernel-include-regex attn -d gpurun_out/profpol_pmc -o p --output-format csv -- python tools/rollout_prof.py c3
       rm -f gpurun_out/profpol_*/*kernel_trace.csv gpurun_out/profpol_*/*/*kernel_trace.csv
       ;;
+    profpol2)  # the fused encoders' instruction mix (one PMC pass)
+      export TMPDIR=/tmp
+      step profpol2_pmc 200 timeout -s KILL 180 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_WAVES SQ_WAVE_CYCLES --kernel-include-regex attn -d gpurun_out/profpol2_pmc -o p --output-format csv -- python tools/rollout_prof.py c3
+      ;;
     n128) step gpu_tests_n128 900 python -u -m pytest tests/test_gpu_n128.py -x -v --timeout 300 --timeout-method thread ;;
     benchn128) step bench_n128 300 python bench.py --config n128 --steps 500 --cpu-seconds 5 --e2e-iters 0 ;;
     prioab)    # the younger-wave priority flip (QS_PRIO_AT, default 11) against off, per config
