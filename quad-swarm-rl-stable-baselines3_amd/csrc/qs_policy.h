@@ -126,6 +126,34 @@ __device__ __forceinline__ void mfma_layer(const float* X, const float4* __restr
     }
 }
 
+// Layer 0's input rows of a block (MROWS x KD0): [nbr_j (nd) | self_{j % B} (so) | 0 ...], row j = agent j / K, slot
+// j % K (the reference's row pairing), through put(r, c, v).  Every lane's loads are issued unconditionally, back to
+// back: a predicated load compiles to a branch and a full wait per element (8 serial HBM latencies per lane).  The
+// padding columns read the row's own self word and are zeroed by a product (finite unless the row itself is not);
+// rows past the data read obs[0] and are never used.  (row indices < 2^31: qs_attn_embed checks B K H)
+template <typename Put>
+__device__ __forceinline__ void gather_rows0(const float* __restrict__ obs, int stride, int so, int off, int B, int K,
+                                             int nd, long row0, int MU, long R, int tid, Put put) {
+    constexpr int NV = MROWS * KD0 / NTHR;
+    float v[NV];
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+        const int e = tid + u * NTHR, r = e / KD0, c = e - r * KD0;
+        const int j = (int)row0 + r;
+        const bool okr = r < MU && j < R;
+        const int a = j / K;
+        const size_t self = (size_t)(j % B) * stride;
+        const size_t idx = c < nd ? (size_t)a * stride + off + (size_t)(j - a * K) * nd + c
+                                  : self + (c < nd + so ? c - nd : 0);
+        v[u] = obs[okr ? idx : 0] * (c < nd + so ? 1.f : 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+        const int e = tid + u * NTHR;
+        put(e / KD0, e % KD0, v[u]);
+    }
+}
+
 // The weights are the MFMA's A operand and the activations its B operand, so a 32 x 32 result tile is
 // [output column][row]: the block row i is on the lane, and registers 4g .. 4g + 3 of tile (rt, c) hold four
 // consecutive output columns n0 .. n0 + 3 -- an epilogue writes them as one float4 (or four packed halves).
@@ -211,16 +239,7 @@ __global__ __launch_bounds__(NTHR, 2) void attn_embed_kernel(const float* __rest
     }
     // layer 0's input rows [nbr_j (nd) | self_{j % B} (so) | 0 ...] (KD0 wide): row j = agent j / K, slot j % K;
     // its self half comes from agent j % B (the reference's row pairing)
-    for (int e = tid; e < MROWS * KD0; e += NTHR) {   // (row indices < 2^31: qs_attn_embed checks B K H)
-        const int r = e / KD0, c = e - r * KD0;
-        const int j = (int)row0 + r;
-        float v = 0.f;
-        if (r < MU && j < R) {
-            if (c < nd) v = obs[(size_t)(j / K) * stride + off + (j % K) * nd + c];
-            else if (c < nd + so) v = obs[(size_t)(j % B) * stride + (c - nd)];
-        }
-        X0[r * LD0 + c] = v;
-    }
+    gather_rows0(obs, stride, so, off, B, K, nd, row0, MU, R, tid, [&](int r, int c, float v) { X0[r * LD0 + c] = v; });
     __syncthreads();
     QS_STAMP(1);
     f32x16 acc[RT][CT];

@@ -188,16 +188,7 @@ __global__ __launch_bounds__(NTHR, 2) __attribute__((amdgpu_waves_per_eu(2, 2)))
     }
     // layer 0's input rows [nbr_j (nd) | self_{j % B} (so) | 0 ...], row j = agent j / K, slot j % K; self half from
     // agent j % B (the reference's row pairing)
-    for (int e = tid; e < MROWS * KD0; e += NTHR) {
-        const int r = e / KD0, c = e - r * KD0;
-        const int j = (int)row0 + r;
-        float v = 0.f;
-        if (r < MU && j < R) {
-            if (c < nd) v = obs[(size_t)(j / K) * stride + off + (j % K) * nd + c];
-            else if (c < nd + so) v = obs[(size_t)(j % B) * stride + (c - nd)];
-        }
-        X0.put(r, c, X3_SIN * v);
-    }
+    gather_rows0(obs, stride, so, off, B, K, nd, row0, MU, R, tid, [&](int r, int c, float v) { X0.put(r, c, X3_SIN * v); });
     __syncthreads();
     f32x16 acc[RT][CT];
     mfma_layer_x3<H, KD0, true, false>(X0, reinterpret_cast<const uint4*>(t.w_e1p), acc, wave, lane);
