@@ -258,39 +258,44 @@ def test_full_size_sb_train_properties():
     assert np.all(np.hypot(tgt[0], tgt[1]) < 8.0)
 
 
-def test_deterministic_and_shard_invariant():
-    cfg = QuadSwarmConfig.sb_train(num_envs=64, num_agents=8, seed=9, pixel_noise_cam=3.0)
+@pytest.mark.parametrize("E,N,k", [(64, 8, -1), (8, 128, 7)])
+def test_deterministic_and_shard_invariant(E, N, k):
+    """Two runs bitwise equal, and two half shards (drone id offsets) bitwise the whole; N = 128: the multi-wave
+    envs (their LDS float sums are added in a fixed wave order, so they are deterministic too)."""
+    kw = dict(num_agents=N, seed=9, pixel_noise_cam=3.0, neighbor_visible_num=k)
+    cfg = QuadSwarmConfig.sb_train(num_envs=E, **kw)
     a = [QuadSwarmEnv(cfg) for _ in range(2)]
     shards = []
+    h = E // 2
     for r in range(2):
-        c = QuadSwarmConfig.sb_train(num_envs=32, num_agents=8, seed=9, pixel_noise_cam=3.0,
-                                     drone_id_offset=r * 32 * 8)
+        c = QuadSwarmConfig.sb_train(num_envs=h, drone_id_offset=r * h * N, **kw)
         shards.append(QuadSwarmEnv(c))
     outs = [[e.reset().clone()] for e in a]
     so = [[s.reset().clone()] for s in shards]
     rng = np.random.default_rng(0)
     for t in range(6):
-        act = torch.from_numpy(rng.uniform(-1, 1, (64 * 8, 2)).astype(np.float32)).cuda()
+        act = torch.from_numpy(rng.uniform(-1, 1, (E * N, 2)).astype(np.float32)).cuda()
         for e, o in zip(a, outs):
             o.append(e.step(act)[0].clone())
         for r, (s, o) in enumerate(zip(shards, so)):
-            o.append(s.step(act[r * 256:(r + 1) * 256].contiguous())[0].clone())
+            o.append(s.step(act[r * h * N:(r + 1) * h * N].contiguous())[0].clone())
     for x, y in zip(outs[0], outs[1]):
         assert torch.equal(x, y)
     for t in range(len(outs[0])):
         assert torch.equal(outs[0][t], torch.cat([so[0][t], so[1][t]]))
 
 
-def test_partial_reset_and_snapshot():
-    cfg, env, oenv = make_pair("sb8", E=64)
+@pytest.mark.parametrize("name,E", [("sb8", 64), ("n128k6", 8)])
+def test_partial_reset_and_snapshot(name, E):
+    cfg, env, oenv = make_pair(name, E=E)
     env.reset()
     oenv.reset()
-    mask = np.zeros(64, dtype=np.uint8)
+    mask = np.zeros(E, dtype=np.uint8)
     mask[::3] = 1
     blob = env.get_state()
     obs = np_(env.reset(mask))
     want, ri = oenv.reset(mask)
-    sel = np.repeat(mask.astype(bool), 8)
+    sel = np.repeat(mask.astype(bool), cfg.num_agents)
     bad_ok = np.zeros(len(obs), bool)
     bad_ok[sel] = True
     got_all = np.where(bad_ok[:, None], obs, want)
