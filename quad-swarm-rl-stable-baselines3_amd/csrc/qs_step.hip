@@ -1237,11 +1237,12 @@ static int jit_compile(const qs_config* c, const qs::KP& kp, int npad, int qb, i
     // Code generation measured on MI355X (tools/opts_ab.sh, profiles/ab/r03_jit_opts_ab.txt; every variant
     // bitwise identical): the ILP-first machine scheduler for both flavors, and for flavor B no SLP packing
     // of fp32 math into v_pk_* (the packing's operand moves cost more issue slots than the pairs save at 2
-    // waves per SIMD; flavor A's single wave per SIMD keeps it).  C3 8.69 -> 8.19 us, C5 15.2 -> 13.4,
-    // C4 12.0 -> 11.2, C2 5.69 -> 5.55, a8 27.2 -> 26.3.
+    // waves per SIMD).  C3 8.69 -> 8.19 us, C5 15.2 -> 13.4, C4 12.0 -> 11.2, C2 5.69 -> 5.55, a8 27.2 -> 26.3.
+    // Flavor A kept the packing in round 3; on the round-4 kernel it loses there too (a8 23.82 -> 23.60,
+    // 23.69 -> 23.49 us, profiles/ab/r04_a8_noslp_ab.txt), so no flavor packs.
     opts.push_back("-mllvm");
     opts.push_back("-amdgpu-sched-strategy=max-ilp");
-    if (c->flavor != QS_FLAVOR_A) opts.push_back("-fno-slp-vectorize");
+    opts.push_back("-fno-slp-vectorize");
     if (c->flavor == QS_FLAVOR_A) opts.push_back("-DQS_DPP_BC=0");   // qs_common.h dpp_i (measured per flavor)
     // QS_JIT_OPTS: extra space-separated hipRTC options (kernel-variant experiments, e.g. -DQS_X=1).  The launch
     // geometry (sub-lanes per drone) is the host's: block_threads / envs_per_block size the launch from it, so a
