@@ -614,8 +614,8 @@ __device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\
 // ---------------------------------------------------------------------------------------------
 // QS_DPP_BC: bound_ctrl on (an out-of-range / disabled source lane reads 0 -- the same value as the old = 0
 // form, so bitwise the same results) lets the compiler fold the permute into its consumer (v_sub_f32_dpp ...)
-// more often: C3 7.74 -> 7.64 us; the specialised flavor-A kernels keep it off (a8 25.63 vs 25.74 us,
-// profiles/ab/r03_dpp_bc_ab.txt; qs_step.hip jit_compile)
+// more often: C3 7.74 -> 7.64 us (profiles/ab/r03_dpp_bc_ab.txt); flavor A kept it off in round 3 and takes it
+// since round 4 (a8 23.54 -> 23.37 us, profiles/ab/r04_a8_dpp_bc_ab.txt)
 #ifndef QS_DPP_BC
 #define QS_DPP_BC 1
 #endif

@@ -1243,7 +1243,8 @@ static int jit_compile(const qs_config* c, const qs::KP& kp, int npad, int qb, i
     opts.push_back("-mllvm");
     opts.push_back("-amdgpu-sched-strategy=max-ilp");
     opts.push_back("-fno-slp-vectorize");
-    if (c->flavor == QS_FLAVOR_A) opts.push_back("-DQS_DPP_BC=0");   // qs_common.h dpp_i (measured per flavor)
+    // (flavor A kept DPP permutes without bound_ctrl in round 3; on the round-4 kernel bound_ctrl is as good or
+    // better there too, a8 23.54 -> 23.37, 23.48 -> 23.41 us, profiles/ab/r04_a8_dpp_bc_ab.txt: one form for both)
     // QS_JIT_OPTS: extra space-separated hipRTC options (kernel-variant experiments, e.g. -DQS_X=1).  The launch
     // geometry (sub-lanes per drone) is the host's: block_threads / envs_per_block size the launch from it, so a
     // kernel compiled with another QS_QB / QS_QA / QS_QW would index envs and LDS differently -- refused here.
