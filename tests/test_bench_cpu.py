@@ -110,3 +110,15 @@ def test_state_complete_bytes():
         assert abs(got[0] - b) < 1e-6 and abs(got[1] - r) < 1e-6, (c, got)
         base = bench.algorithmic_bytes_per_agent_step(cfg.obs_dim, cfg.num_agents, cfg.flavor)
         assert got[0] > base
+
+
+def test_every_bench_config_is_valid():
+    """Every --config builds a configuration the C ABI accepts (layout query, no device): the sweep's configs,
+    including the 128-drone flavor-A env (k = 7 <= QS_A_KMAX) and the obstacle / replay / mix variants."""
+    from quadswarm_amd import _native as N
+    L = N.lib()
+    for name, kw in bench.CONFIGS.items():
+        cfg = bench.make_cfg(kw)
+        lay = N.QsLayout()
+        assert L.qs_layout_query(cfg.to_qs_config(), lay) == 0, (name, L.qs_last_error())
+        assert lay.obs_dim == cfg.obs_dim and lay.num_drones == cfg.num_envs * cfg.num_agents, name
