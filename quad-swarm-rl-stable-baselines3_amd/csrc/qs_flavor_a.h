@@ -60,6 +60,9 @@ __device__ __forceinline__ float sin_small(float x) {
 #ifndef QS_CAM_SECTOR
 #define QS_CAM_SECTOR 1
 #endif
+#ifndef QS_PID_MED3
+#define QS_PID_MED3 1
+#endif
 #ifndef QS_A_DEAL_SENSE
 #define QS_A_DEAL_SENSE 1
 #endif
@@ -91,7 +94,16 @@ __device__ __forceinline__ float pid_update(const KP& kp, int k, float e, float*
     st[0] = e;
     float out = kp.pkp[k] * e + kp.pkd[k] * diff + kp.pki[k] * st[1];
     const float sat = kp.psat[k];
+#if QS_PID_MED3
+    // the clamp as one v_med3_f32 (the same value for every non-NaN out, -0 and +-inf included); NaN passes through
+    // as in the reference's if / elif
+    if (sat > 0.f) {
+        const float c = __builtin_amdgcn_fmed3f(out, -sat, sat);
+        out = out != out ? out : c;
+    }
+#else
     if (sat > 0.f) out = out >= sat ? sat : (out <= -sat ? -sat : out);
+#endif
     const float aw = kp.paw[k];
     if (aw > 0.f && -aw < out && out < aw) st[1] += e * kp.dt;
     return out;
