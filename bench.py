@@ -495,6 +495,7 @@ def main(argv=None):
     ap.add_argument("--generic", action="store_true", help="generic kernels instead of qs_specialize (hipRTC)")
     ap.add_argument("--no-episode-stats", action="store_true",
                     help="A/B only: skip the episode_extra_stats accumulators the reference's step keeps")
+    ap.add_argument("--quads-mode", default=None, help="A/B only: override the config's quads_mode (goal scenario)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="seconds per cpu_baseline leg (3 legs)")
     ap.add_argument("--cpu-worker", action="store_true", help=argparse.SUPPRESS)
@@ -537,6 +538,8 @@ def main(argv=None):
     kw = CONFIGS[args.config]
     if args.no_episode_stats:
         kw = dict(kw, episode_stats=False)
+    if args.quads_mode:
+        kw = dict(kw, quads_mode=args.quads_mode)
     cfg = make_cfg(kw, seed=0, specialize=not args.generic)
     I = cfg.num_envs * cfg.num_agents
     cfg.drone_id_offset = rank * I

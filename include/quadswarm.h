@@ -17,6 +17,7 @@
  *   - qs_set_param replaces rew_coeff updates          swarm_rl/env_wrappers/reward_shaping.py:70-76,110-118
  *   - qs_get_state/qs_set_state: env snapshot/restore (no reference equivalent; checkpoint + parity)
  *   - qs_curriculum_step replaces CurriculumCallback._on_step          swarm_rl/custom_callbacks.py:441-468
+ *   - qs_curriculum_step_all: the same over every data-parallel rank's envs   custom_callbacks.py:452-462
  * The Python mirror of the reference's VecEnv surface (quadswarm_amd.vec_env.GpuQuadVecEnv) calls
  * these through ctypes; INTEGRATION.md shows the binding.
  *
@@ -37,7 +38,7 @@
 extern "C" {
 #endif
 
-#define QS_ABI_VERSION 11
+#define QS_ABI_VERSION 12
 #define QS_MAX_AGENTS 128           /* drones per env: up to 64 inside one 64-lane wavefront, 128 = a two-wave
                                        workgroup per env (flavor B without obstacles; paper/fps_compare.py:7) */
 #define QS_MAX_DR_CHOICES 8         /* entries per obstacle domain-randomisation list */
@@ -504,6 +505,12 @@ typedef struct qs_curriculum {
 int qs_curriculum_init(qs_curriculum* host, double initial_radius, double sr_threshold, double decay, int32_t window);
 /* One curriculum update for the step just enqueued on `stream` (d_cur: device qs_curriculum). */
 int qs_curriculum_step(qs_handle* h, qs_curriculum* d_cur, void* stream);
+/* The same update over the reset outcomes of ALL data-parallel ranks (ABI 12; SURVEY §8e, custom_callbacks.py:452-462
+ * iterating the whole VecEnv's reset_infos): d_reset_all holds n_all = world * num_envs reset_info bytes in global env
+ * order (rank r's handle owns envs [r * num_envs, (r + 1) * num_envs), e.g. an all-gather of every rank's
+ * buffers.reset_info); every rank runs it with the same bytes, so every rank's d_cur evolves identically, and the
+ * new radius is written to THIS handle's envs. */
+int qs_curriculum_step_all(qs_handle* h, const uint8_t* d_reset_all, int64_t n_all, qs_curriculum* d_cur, void* stream);
 
 #ifdef __cplusplus
 }

@@ -14,6 +14,11 @@
 // scanned across the workgroup (LDS), so each reset env knows its rank r among the step's c resets; only the
 // last `window` of them survive sequential writes (r >= c - window), and their slots (window_i + r) % window
 // are distinct, so they are written in parallel without a race.
+//
+// Data-parallel training: the reference runs ONE callback over all envs of its VecEnv.  With one rank
+// per GPU, each rank's handle owns a contiguous block of the global envs; the ranks all-gather their reset_info rows
+// (rank-major = global env order) and every rank runs this kernel over the concatenation (n_read = world * E), so
+// every rank computes the same window and radius, and writes it into its own n_write envs.
 #pragma once
 #ifndef __HIPCC_RTC__
 #include <hip/hip_runtime.h>
@@ -27,7 +32,7 @@ constexpr int QS_CUR_THREADS = 256;
 
 __global__ __launch_bounds__(QS_CUR_THREADS) void curriculum_kernel(const uint8_t* __restrict__ reset_info,
                                                                      float* __restrict__ capture, int E,
-                                                                     qs_curriculum* __restrict__ cur) {
+                                                                     int n_write, qs_curriculum* __restrict__ cur) {
     // the window and every value passed between lanes stay in LDS for the launch; the device struct is read at
     // the start and written back at the end
     __shared__ int scan[QS_CUR_THREADS];
@@ -82,7 +87,7 @@ __global__ __launch_bounds__(QS_CUR_THREADS) void curriculum_kernel(const uint8_
     __syncthreads();
     if (t < W) cur->past[t] = shrink ? 0.0 : win[t];
     if (shrink)
-        for (int e = t; e < E; e += QS_CUR_THREADS) capture[e] = rad;
+        for (int e = t; e < n_write; e += QS_CUR_THREADS) capture[e] = rad;
 }
 
 }  // namespace qs

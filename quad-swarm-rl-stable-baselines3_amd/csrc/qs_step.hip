@@ -517,7 +517,7 @@ static size_t shm_bytes(const qs_config& c, int obs_dim, int npad, bool step, in
     size_t b = sizeof(float) * slots * (size_t)obs_dim + sizeof(float) * slots * 8 + sizeof(float) * 64;
     if (c.use_obstacles) b += epb * (sizeof(float) * 2 * (size_t)obst_slots(&c) + (size_t)qs::QS_OBST_SCRATCH);
     else if (c.scenario >= QS_SCEN_MIX && c.scenario <= QS_SCEN_RUN_AWAY)   // goal tables (qs::scen_stride)
-        b += epb * sizeof(float) * 2 * ((size_t)npad + 4) * 4;
+        b += epb * sizeof(float) * (2 * ((size_t)npad + 4) * 4 + 32);
     return b;
 }
 
@@ -1016,7 +1016,21 @@ extern "C" int qs_curriculum_step(qs_handle* h, qs_curriculum* d_cur, void* stre
     const uint8_t* ri = (const uint8_t*)((char*)h->ws + h->lay.reset_info);
     float* cap = (float*)((char*)h->ws + h->lay.env_f) + (size_t)QS_ENVF_CAPTURE * (size_t)h->cfg.num_envs;
     hipLaunchKernelGGL(qs::curriculum_kernel, dim3(1), dim3(qs::QS_CUR_THREADS), 0, (hipStream_t)stream, ri, cap,
-                       (int)h->cfg.num_envs, d_cur);
+                       (int)h->cfg.num_envs, (int)h->cfg.num_envs, d_cur);
+    QS_HIP(hipGetLastError());
+    return QS_OK;
+}
+
+extern "C" int qs_curriculum_step_all(qs_handle* h, const uint8_t* d_reset_all, int64_t n_all, qs_curriculum* d_cur,
+                                      void* stream) {
+    if (!h || !d_cur || !d_reset_all) return fail(QS_E_INVALID, "NULL argument");
+    if (h->cfg.flavor != QS_FLAVOR_A) return fail(QS_E_INVALID, "the capture-radius curriculum is flavor A");
+    if (n_all < (int64_t)h->cfg.num_envs || n_all > (int64_t)INT32_MAX)
+        return fail(QS_E_INVALID, "n_all must cover at least the handle's envs (world * num_envs)");
+    QS_HIP(use_device(h));
+    float* cap = (float*)((char*)h->ws + h->lay.env_f) + (size_t)QS_ENVF_CAPTURE * (size_t)h->cfg.num_envs;
+    hipLaunchKernelGGL(qs::curriculum_kernel, dim3(1), dim3(qs::QS_CUR_THREADS), 0, (hipStream_t)stream, d_reset_all,
+                       cap, (int)n_all, (int)h->cfg.num_envs, d_cur);
     QS_HIP(hipGetLastError());
     return QS_OK;
 }

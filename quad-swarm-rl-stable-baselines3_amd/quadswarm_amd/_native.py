@@ -9,7 +9,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("QUADSWARM_LIB", os.path.join(HERE, "lib", "libquadswarm.so"))
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 MAX_AGENTS = 128
 A_KMAX = 16   # flavor A, more than 64 drones: visible neighbours (qs_flavor_a.h QS_A_KMAX)
 MAX_DR_CHOICES = 8
@@ -151,7 +151,7 @@ EXPORTS = ["qs_abi_version", "qs_last_error", "qs_struct_sizes", "qs_config_defa
            "qs_specialize", "qs_is_specialized", "qs_config_kp_words", "qs_specialize_compile",
            "qs_replay_config_default", "qs_replay_workspace_bytes", "qs_replay_enable", "qs_replay_disable", "qs_replay_buffers_get",
            "qs_attn_embed", "qs_attn_pool", "qs_attn_embed_x3", "qs_attn_pool_x3", "qs_curriculum_init",
-           "qs_curriculum_step"]
+           "qs_curriculum_step", "qs_curriculum_step_all"]
 
 _lib = None
 
@@ -192,6 +192,7 @@ def lib():
         "qs_attn_pool_x3": ([I32, I32, I32, P(QsAttnTower), I32, V], I32),
         "qs_curriculum_init": ([V, ctypes.c_double, ctypes.c_double, ctypes.c_double, I32], I32),
         "qs_curriculum_step": ([V, V, V], I32),
+        "qs_curriculum_step_all": ([V, V, ctypes.c_int64, V, V], I32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -448,6 +448,10 @@ class PPOTrainer:
         self.device = torch.device(device) if device is not None else next(policy.parameters()).device
         self.group = group
         self.distributed = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+        # data parallel: rank r steps its own env shard; num_timesteps counts every rank's agents (the reference's
+        # one VecEnv over all envs), so total_timesteps / save_freq / eval_freq keep their global meaning
+        self.world_size = dist.get_world_size(group) if self.distributed else 1
+        self.rank = dist.get_rank(group) if self.distributed else 0
         if self.distributed:
             for p in policy.parameters():   # identical weights on every rank
                 dist.broadcast(p.data, src=0, group=group)
@@ -503,7 +507,7 @@ class PPOTrainer:
             st.rewards[t].copy_(rew)
             self.last_done.copy_(done)
             self.last_obs = obs
-            self.num_timesteps += self.env.I
+            self.num_timesteps += self.env.I * self.world_size
             self.env_steps += 1
             if callbacks:
                 ctx = StepContext(self, t, obs, rew, done, st.actions[t])
@@ -593,73 +597,120 @@ class PPOTrainer:
         return stats
 
     # ---- checkpoint / resume (sb_train: CheckpointCallback + model.save, sb_train.py:99-106) ----
-    CKPT_FORMAT = "quadswarm_amd.PPOTrainer/1"
+    CKPT_FORMAT = "quadswarm_amd.PPOTrainer/2"
     ENV_PARAMS = ("seed", "ep_len", "rew_pos", "rew_effort", "rew_crash", "rew_orient", "rew_spin", "quadcol_bin",
                   "quadcol_bin_smooth_max", "quadcol_bin_obst")
 
-    def save(self, path, callbacks=None):
-        """Everything the next iteration depends on: policy and Adam state, counters, the trainer's minibatch
-        generator and the device's default generator (rollout action noise), the env snapshot (qs_get_state: drone
-        and env state incl. the per-env Philox counters, capture radii, pillar maps), the current observation and
-        episode starts, the replay wrapper's device state, and the callbacks' state.  Loaded with
-        torch.load(weights_only=True).  Resuming reproduces the continuation bitwise (tests/test_gpu_trainer.py)."""
-        from dataclasses import asdict
-        callbacks = self.callbacks if callbacks is None else callbacks
+    def _shard_state(self):
+        """This rank's part of a checkpoint: its env snapshot (qs_get_state: drone and env state incl. the per-env
+        Philox counters, capture radii, pillar maps) and runtime env parameters, the current observation / episode
+        starts / bootstrap values, the replay wrapper's device state, and its random generators."""
         env = self.env
         u8 = lambda b: torch.frombuffer(bytearray(b), dtype=torch.uint8).clone()  # noqa: E731
-        ck = {"format": self.CKPT_FORMAT,
-              "policy": self.policy.state_dict(), "optimizer": self.optimizer.state_dict(),
-              "policy_cfg": asdict(self.policy.cfg), "ppo_cfg": asdict(self.cfg),
-              "num_timesteps": self.num_timesteps, "env_steps": self.env_steps, "iterations": self.iterations,
+        sh = {"rank": self.rank,
               "gen": self.gen.get_state(), "device_rng": torch.cuda.get_rng_state(self.device)
               if self.device.type == "cuda" else torch.get_rng_state(),
               "last_obs": None if self.last_obs is None else self.last_obs.detach().cpu().clone(),
-              "last_done": self.last_done.cpu().clone(), "last_values": self.last_values.cpu().clone(),
-              "callbacks": [cb.state_dict() for cb in callbacks]}
+              "last_done": self.last_done.cpu().clone(), "last_values": self.last_values.cpu().clone()}
         if hasattr(env, "get_state"):
-            ck["env_state"] = u8(env.get_state())
+            sh["env_state"] = u8(env.get_state())
             # the runtime parameters qs_set_param may have changed (seed, reward annealing, episode length)
-            ck["env_params"] = {}
+            sh["env_params"] = {}
             for k in self.ENV_PARAMS:
                 try:
-                    ck["env_params"][k] = env.get_param(k)
+                    sh["env_params"][k] = env.get_param(k)
                 except NAT.QuadSwarmError:
                     pass
         if getattr(env, "replay", None) is not None:
-            ck["replay_ws"] = env._replay_ws.cpu().clone()
-        d = os.path.dirname(os.path.abspath(path))
-        os.makedirs(d, exist_ok=True)
-        torch.save(ck, path)
+            sh["replay_ws"] = env._replay_ws.cpu().clone()
+        return sh
+
+    def _gather_shards(self, shard):
+        """Every rank's shard on rank 0 (None elsewhere): each serialised with torch.save, the byte strings padded to
+        the longest and all-gathered (one length exchange + one all_gather), read back with weights_only=True."""
+        if not self.distributed:
+            return [shard]
+        import io
+        import torch.distributed as dist
+        bio = io.BytesIO()
+        torch.save(shard, bio)
+        raw = torch.frombuffer(bytearray(bio.getvalue()), dtype=torch.uint8)
+        cdev = self.device if dist.get_backend(self.group) == "nccl" else torch.device("cpu")
+        n = torch.tensor([raw.numel()], dtype=torch.int64, device=cdev)
+        ns = torch.empty(self.world_size, dtype=torch.int64, device=cdev)
+        dist.all_gather_into_tensor(ns, n, group=self.group)
+        ns = ns.cpu().tolist()
+        pad = torch.zeros(max(ns), dtype=torch.uint8)
+        pad[:raw.numel()] = raw
+        allb = torch.empty(self.world_size * max(ns), dtype=torch.uint8, device=cdev)
+        dist.all_gather_into_tensor(allb, pad.to(cdev), group=self.group)
+        if self.rank != 0:
+            return None
+        allb = allb.cpu().view(self.world_size, max(ns))
+        return [torch.load(io.BytesIO(allb[r, :ns[r]].numpy().tobytes()), map_location="cpu", weights_only=True)
+                for r in range(self.world_size)]
+
+    def save(self, path, callbacks=None):
+        """Everything the next iteration depends on: policy and Adam state, counters, the callbacks' state, and every
+        rank's shard (_shard_state).  Collective under data parallelism: every rank calls it with the same path, rank
+        0 writes ONE file holding all shards (in rank order, with the world size).  Loaded with
+        torch.load(weights_only=True).  Resuming reproduces the continuation bitwise (tests/test_gpu_trainer.py,
+        tests/test_trainer_distributed_cpu.py)."""
+        from dataclasses import asdict
+        callbacks = self.callbacks if callbacks is None else callbacks
+        shards = self._gather_shards(self._shard_state())
+        cbs = [cb.state_dict() for cb in callbacks]
+        if self.rank == 0:
+            ck = {"format": self.CKPT_FORMAT, "world_size": self.world_size,
+                  "policy": self.policy.state_dict(), "optimizer": self.optimizer.state_dict(),
+                  "policy_cfg": asdict(self.policy.cfg), "ppo_cfg": asdict(self.cfg),
+                  "num_timesteps": self.num_timesteps, "env_steps": self.env_steps, "iterations": self.iterations,
+                  "callbacks": cbs, "shards": shards}
+            d = os.path.dirname(os.path.abspath(path))
+            os.makedirs(d, exist_ok=True)
+            tmp = path + ".tmp"
+            torch.save(ck, tmp)
+            os.replace(tmp, path)
+        if self.distributed:   # the file exists for every rank when save() returns
+            import torch.distributed as dist
+            dist.barrier(group=self.group)
         return path
 
     def load(self, path, callbacks=()):
-        """Restore a save() checkpoint into this trainer (same policy / env configuration); `callbacks` (the same
-        kinds, in the order they were saved) get their state back for the next learn()."""
+        """Restore a save() checkpoint into this trainer (same policy / env configuration and the same world size;
+        each rank takes its own shard); `callbacks` (the same kinds, in the order they were saved) get their state
+        back for the next learn()."""
         ck = torch.load(path, map_location="cpu", weights_only=True)
         if ck.get("format") != self.CKPT_FORMAT:
             raise ValueError(f"{path}: not a {self.CKPT_FORMAT} checkpoint")
+        if int(ck["world_size"]) != self.world_size:
+            raise ValueError(f"{path}: written by {ck['world_size']} ranks, this run has {self.world_size} "
+                             "(the env shards are per rank)")
+        sh = ck["shards"][self.rank]
         self.policy.load_state_dict(ck["policy"])
         self.optimizer.load_state_dict(ck["optimizer"])
         self.num_timesteps, self.env_steps, self.iterations = (int(ck["num_timesteps"]), int(ck["env_steps"]),
                                                                 int(ck["iterations"]))
-        self.gen.set_state(ck["gen"])
+        self.gen.set_state(sh["gen"])
         if self.device.type == "cuda":
-            torch.cuda.set_rng_state(ck["device_rng"], self.device)
+            torch.cuda.set_rng_state(sh["device_rng"], self.device)
         else:
-            torch.set_rng_state(ck["device_rng"])
+            torch.set_rng_state(sh["device_rng"])
         env = self.env
-        if "env_state" in ck:
-            for k, v in ck.get("env_params", {}).items():
+        if "env_state" in sh:
+            for k, v in sh.get("env_params", {}).items():
                 env.set_param(k, v)
-            env.set_state(bytes(ck["env_state"].numpy().tobytes()))
-        if "replay_ws" in ck:
-            env._replay_ws.copy_(ck["replay_ws"].to(env._replay_ws.device))
-        if ck["last_obs"] is not None:
-            obs = env.obs if hasattr(env, "obs") else torch.empty_like(ck["last_obs"], device=self.device)
-            obs.copy_(ck["last_obs"].to(self.device))
+            env.set_state(bytes(sh["env_state"].numpy().tobytes()))
+        if "replay_ws" in sh:
+            env._replay_ws.copy_(sh["replay_ws"].to(env._replay_ws.device))
+        if sh["last_obs"] is not None:
+            obs = getattr(env, "obs", None)
+            if obs is None:
+                obs = torch.empty_like(sh["last_obs"], device=self.device)
+            obs.copy_(sh["last_obs"].to(self.device))
             self.last_obs = obs
-        self.last_done.copy_(ck["last_done"].to(self.device))
-        self.last_values.copy_(ck["last_values"].to(self.device))
+        self.last_done.copy_(sh["last_done"].to(self.device))
+        self.last_values.copy_(sh["last_values"].to(self.device))
         for cb, sd in zip(callbacks, ck["callbacks"]):
             cb.load_state_dict(sd)
         if self.fused is not None:

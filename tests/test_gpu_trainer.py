@@ -5,9 +5,15 @@ save / load):
   CurriculumCallback._on_step (swarm_rl/custom_callbacks.py:441-468) fed with the same per-step reset_infos: the
   window, window_i, success rate, radius and number of reductions agree exactly (fp64), and every env's capture
   radius on the device is the reduced one;
+* qs_curriculum_step_all (the data-parallel form: every rank runs it over all ranks' gathered reset_info rows) over
+  this handle's rows concatenated with a second, synthetic rank's: the same host restatement over the concatenation,
+  and the radius lands in this handle's envs only;
 * a checkpoint written by CheckpointCallback after one iteration, loaded into a fresh trainer (different weights
   and env seed), reproduces the following iteration bitwise: weights, Adam state, env snapshot, rollout buffer
-  and the curriculum's device state."""
+  and the curriculum's device state;
+* EvalCallback: the evaluation statistics equal SB3's evaluate_policy / EvalCallback._on_step restated over the eval
+  env's recorded per-step rewards and dones (episode rewards and lengths, mean reward, best-model checkpoint on
+  improvement only), the curriculum's radius reaches the eval env, and the evaluation episodes are deterministic."""
 import os
 
 import numpy as np
@@ -37,22 +43,14 @@ class RecordResets(TrainerCallback):
 
 
 def reference_curriculum(steps, r0, sr_thr, decay, W=40):
-    """CurriculumCallback._on_step (custom_callbacks.py:449-468) restated on the host, minus logging / eval env."""
-    past, wi, sr, r, n = np.zeros(W), 0, 0.0, r0, 0
+    """CurriculumCallback._on_step (custom_callbacks.py:449-468) restated on the host (oracle/curriculum_oracle.py),
+    minus logging / eval env."""
+    from curriculum_oracle import CurriculumOracle
+    o = CurriculumOracle(r0, sr_thr, decay, W)
     for resets in steps:
-        change = False
-        for e in resets:
-            if e is not None:
-                past[wi % W] = e["success"]
-                wi += 1
-                change = True
-        if change:
-            sr = np.sum(past) / W
-            if sr > sr_thr:
-                r = decay * r
-                n += 1
-                past = np.zeros(W)
-    return dict(past=past, window_i=wi, success_rate=sr, radius=r, n_shrinks=n)
+        o.step(resets)
+    return dict(past=o.past, window_i=o.window_i, success_rate=o.success_rate, radius=o.radius,
+                n_shrinks=len(o.history))
 
 
 def make(seed=0, E=64, n_steps=32, radius=3.0):
@@ -82,6 +80,46 @@ def test_device_curriculum_matches_reference_callback():
     caps = env.env_f[NAT.ENVF_CAPTURE].cpu().numpy()
     assert (caps == np.float32(want["radius"])).all()
     assert cur.records["curriculum/capture_radius"] == want["radius"]
+
+
+def test_curriculum_step_all_over_gathered_rows():
+    """The kernel over [this handle's reset_info | a synthetic second rank's row] (what the all-gather hands it)."""
+    import ctypes
+    from curriculum_oracle import CurriculumOracle
+    cfg = QuadSwarmConfig.sb_train(num_envs=64, num_agents=4, initial_capture_radius=3.0, seed=5)
+    env = QuadSwarmEnv(cfg)
+    env.reset()
+    env.set_capture_radius(3.0)
+    c = NAT.QsCurriculum()
+    NAT.check(NAT.lib().qs_curriculum_init(ctypes.byref(c), 3.0, 0.45, 0.9, 40), "init")
+    dev = torch.frombuffer(bytearray(bytes(c)), dtype=torch.uint8).cuda()
+    o = CurriculumOracle(3.0, 0.45, 0.9, 40)
+    g = torch.Generator(device="cuda").manual_seed(2)
+    other_g = np.random.default_rng(7)
+    allr = torch.empty(2 * env.E, dtype=torch.uint8, device="cuda")
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    resets = 0
+    for t in range(300):
+        a = (torch.rand(env.I, 2, device="cuda", generator=g) * 2 - 1).contiguous()
+        env.step(a)
+        other = other_g.choice([0, 0, 0, 0, 0, 1, 2, 2], size=env.E).astype(np.uint8)   # rank 1: mostly successes
+        allr[:env.E].copy_(env.reset_info)
+        allr[env.E:].copy_(torch.from_numpy(other))
+        NAT.check(NAT.lib().qs_curriculum_step_all(env._h, ctypes.c_void_p(allr.data_ptr()), 2 * env.E,
+                                                   ctypes.c_void_p(dev.data_ptr()), st), "step_all")
+        row = allr.cpu().numpy()
+        resets += int((row != 0).sum())
+        o.step(row.tolist())
+    got = NAT.QsCurriculum.from_buffer_copy(bytes(dev.cpu().numpy().tobytes()))
+    assert resets > 200 and len(o.history) >= 2
+    assert got.n_shrinks == len(o.history) and got.window_i == o.window_i
+    assert got.radius == o.radius and got.success_rate == o.success_rate
+    assert list(got.past)[:40] == list(o.past)
+    assert (env.env_f[NAT.ENVF_CAPTURE].cpu().numpy() == np.float32(o.radius)).all()
+    with pytest.raises(NAT.QuadSwarmError):      # fewer rows than the handle's own envs
+        NAT.check(NAT.lib().qs_curriculum_step_all(env._h, ctypes.c_void_p(allr.data_ptr()), env.E - 1,
+                                                   ctypes.c_void_p(dev.data_ptr()), st), "step_all")
+    env.close()
 
 
 def test_resume_from_checkpoint_reproduces_next_iteration_bitwise(tmp_path):
@@ -114,3 +152,99 @@ def test_resume_from_checkpoint_reproduces_next_iteration_bitwise(tmp_path):
     assert bytes(cur2.read()) == want_cur
     env.close()
     env2.close()
+
+
+class RecordingEnv:
+    """The eval env with every step's rewards, dones and reset_info recorded (host copies)."""
+
+    def __init__(self, env):
+        self.env, self.rec = env, []
+        self.I, self.N, self.E, self.cfg = env.I, env.N, env.E, env.cfg
+
+    @property
+    def reset_info(self):
+        return self.env.reset_info
+
+    def set_capture_radius(self, v):
+        self.env.set_capture_radius(v)
+
+    def reset(self):
+        self.rec.append("reset")
+        return self.env.reset()
+
+    def step(self, a):
+        out = self.env.step(a)
+        self.rec.append((out[1].double().cpu().numpy(), out[2].cpu().numpy().astype(bool),
+                         self.env.reset_info.cpu().numpy().copy()))
+        return out
+
+
+def reference_evaluate(rec, n_rows, n_eval_episodes):
+    """stable_baselines3 evaluate_policy(return_episode_rewards=True) restated over a recorded run (one evaluation:
+    the steps after its reset), per its published algorithm."""
+    targets = np.array([(n_eval_episodes + i) // n_rows for i in range(n_rows)])
+    counts = np.zeros(n_rows, dtype=int)
+    cr, cl = np.zeros(n_rows), np.zeros(n_rows, dtype=int)
+    er, el = [], []
+    for r, d, _ in rec:
+        cr += r
+        cl += 1
+        for i in range(n_rows):
+            if counts[i] < targets[i] and d[i]:
+                er.append(cr[i])
+                el.append(cl[i])
+                counts[i] += 1
+                cr[i] = 0
+                cl[i] = 0
+        if not (counts < targets).any():
+            break
+    return er, el
+
+
+def test_eval_callback_matches_sb3_evaluate_policy(tmp_path):
+    from quadswarm_amd.callbacks import EvalCallback
+    cfg, env, pol, tr = make(seed=4, E=64, n_steps=16, radius=3.0)
+    ecfg = QuadSwarmConfig.sb_train(num_envs=1, num_agents=4, initial_capture_radius=3.0, seed=99)
+    eenv = RecordingEnv(QuadSwarmEnv(ecfg))
+    cur = DeviceCurriculum(0.5, 0.9, 3.0, verbose=0, eval_env=eenv, eval_freq=0)   # pushes its radius only
+    ev = EvalCallback(eenv, n_eval_episodes=6, eval_freq=16, log_path=str(tmp_path / "eval"),
+                      best_model_save_path=str(tmp_path / "best"), verbose=0)
+    bests = []
+
+    class Watch(TrainerCallback):
+        def on_iteration_end(self, trainer):
+            bests.append((ev.last_mean_reward, ev.best_mean_reward, len(ev.best_saved)))
+    tr.learn(3 * 16 * env.I, callback=[cur, ev, Watch()])
+    # three evaluations, each: a reset, then steps until every row met its target
+    runs, curr = [], None
+    for x in eenv.rec:
+        if isinstance(x, str):
+            curr = []
+            runs.append(curr)
+        else:
+            curr.append(x)
+    assert len(runs) == 3
+    res = np.load(str(tmp_path / "eval" / "evaluations.npz"))
+    assert list(res["timesteps"]) == [16 * env.I * k for k in (1, 2, 3)]
+    best, nbest = -np.inf, 0
+    for k, run in enumerate(runs):
+        er, el = reference_evaluate(run, eenv.I, 6)
+        assert len(er) == 6                      # targets (6 + i) // 4 = [1, 1, 2, 2]
+        assert list(res["results"][k]) == er and list(res["ep_lengths"][k]) == el
+        m = float(np.mean(er))
+        assert bests[k][0] == m
+        if m > best:
+            best, nbest = m, nbest + 1
+        assert bests[k][1] == best and bests[k][2] == nbest
+    assert nbest >= 1 and os.path.exists(str(tmp_path / "best" / "best_model.pt"))
+    # the curriculum's radius (shrunk or not) is the eval env's
+    assert (eenv.env.env_f[NAT.ENVF_CAPTURE].cpu().numpy() == np.float32(cur.capture_radius)).all()
+    # deterministic policy: re-running an evaluation from the same env state gives the same episodes
+    from quadswarm_amd.callbacks import evaluate_policy
+    s0 = eenv.env.get_state()
+    a = evaluate_policy(tr.policy, eenv, 6)
+    eenv.env.set_state(s0)
+    b = evaluate_policy(tr.policy, eenv, 6)
+    assert a == b
+    env.close()
+    eenv.env.close()

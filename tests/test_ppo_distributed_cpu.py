@@ -66,7 +66,7 @@ def test_two_rank_ppo_update_stays_in_lockstep():
         assert p.exitcode == 0
     assert mean_err < 1e-7
     assert wdiff == 0.0
-    assert steps == 8 * 16
+    assert steps == 8 * 16 * 2          # global num_timesteps: both ranks' agents
 
 
 def test_bucket_without_process_group_is_identity():
