@@ -209,6 +209,43 @@ def pmc_traffic(config):
         return None, None
 
 
+VALU_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md chip table: FP32 vector (v_pk_fma_f32, 64 FLOP/clk/SIMD)
+
+
+def valu_roofline(config, agents_per_launch, kernel_ms):
+    """The VALU side of a flavor-A step (flavor A is near the fp32-vector ridge), from the committed PMC
+    summary profiles/pmc_<config>.json (tools/summarize_prof.py):
+      issue_frac   VALU instructions issued per wave / the wave's lifetime in quad-cycles (SQ_INSTS_VALU /
+                   SQ_WAVE_CYCLES per wave; one wave per SIMD, so the SIMD's VALU issue share)
+      flop         executed fp32 FLOP per launch = 64 lanes x (2 FMA + ADD + MUL + TRANS) instructions
+                   (SQ_INSTS_VALU_{FMA,ADD,MUL,TRANS}_F32, the derived-counter formula of rocprofiler's
+                   TOTAL_32_OPS without the integer and MFMA terms), per agent-step, and the rate at this
+                   line's kernel time against the 157.3 TF fp32 vector peak (frac).  Executed, not algorithmic: the
+                   chain replicated on a drone's sub-lanes counts once per sub-lane."""
+    p = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        d = json.load(open(p))
+        pw, c = d.get("per_wave", {}), d.get("counters_per_launch", {})
+        out = {"source": {"file": os.path.relpath(p, ROOT), "tree": d.get("tree")}}
+        if "SQ_INSTS_VALU" in pw and "SQ_WAVE_CYCLES" in pw:
+            out.update(valu_insts_per_wave=round(pw["SQ_INSTS_VALU"], 1),
+                       wave_quad_cycles=round(pw["SQ_WAVE_CYCLES"], 1),
+                       issue_frac=round(pw["SQ_INSTS_VALU"] / pw["SQ_WAVE_CYCLES"], 4))
+        keys = ("SQ_INSTS_VALU_FMA_F32", "SQ_INSTS_VALU_ADD_F32", "SQ_INSTS_VALU_MUL_F32", "SQ_INSTS_VALU_TRANS_F32")
+        if all(k in c for k in keys):
+            flop = 64.0 * (2 * c[keys[0]] + c[keys[1]] + c[keys[2]] + c[keys[3]])
+            tf = flop / (kernel_ms * 1e-3) / 1e12
+            out.update(flop_per_launch=round(flop), flop_per_agent_step=round(flop / agents_per_launch, 1),
+                       achieved_tflops=round(tf, 2), peak_tflops=VALU_PEAK_TFLOPS, frac=round(tf / VALU_PEAK_TFLOPS, 4))
+            if "SQ_INSTS_VALU_FLOPS_FP32" in c:
+                out["sq_insts_valu_flops_fp32_per_launch"] = round(c["SQ_INSTS_VALU_FLOPS_FP32"])
+        return out
+    except Exception:
+        return None
+
+
 # end-to-end PPO leg per workload family: policy / PPO settings of the reference run that trains it
 #   flavor A: swarm_rl/sb_train.py parameter_sweep (SB3 PPO, global_cfg.py:21-29): n_steps 512, 10 epochs,
 #             gamma 0.99, lambda 0.95, clip 0.2, max_grad_norm 0.5, lr 1e-4; attention encoder, 6x128 MLP core.
@@ -238,8 +275,10 @@ def update_flops_per_sample(pol, obs_dim, act_dim, dev, rows=256):
     return fc.get_total_flops() / rows
 
 
-def end_to_end(env, cfg, dev, world, iters, n_steps=None, log=None, fused=True, precision="fp32"):
-    """Timed PPO iterations (rollout + GAE + update) on the bench's env shard."""
+def end_to_end(env, cfg, dev, world, iters, n_steps=None, log=None, fused=True, precision="fp32",
+               update_precision="fp32"):
+    """Timed PPO iterations (rollout + GAE + update) on the bench's env shard.  update_precision "x3": the update's
+    attention encoders through the fused forward / backward kernels (encoder_train.py), else torch autograd."""
     import torch
     import torch.distributed as dist
     from quadswarm_amd.ppo import PPOTrainer, SwarmActorCritic, use_gemm_table
@@ -252,7 +291,9 @@ def end_to_end(env, cfg, dev, world, iters, n_steps=None, log=None, fused=True, 
     pcfg.batch_size = -(-samples // n_mb)
     torch.manual_seed(0)
     pol = SwarmActorCritic(pc).to(dev)
-    tr = PPOTrainer(env, pol, pcfg, seed=0, fused_rollout=fused, rollout_precision=precision)
+    from quadswarm_amd.policy_fused import supports
+    upd = update_precision if (fused and supports(pol)) else "fp32"
+    tr = PPOTrainer(env, pol, pcfg, seed=0, fused_rollout=fused, rollout_precision=precision, update_precision=upd)
     tr.reset()
 
     def sync():
@@ -303,6 +344,8 @@ def end_to_end(env, cfg, dev, world, iters, n_steps=None, log=None, fused=True, 
                   f"fp32 (torch/hipBLASLt GEMMs" + (f", rollout neighbour encoders: fused HIP MFMA kernels, {precision})"
                                                     if tr.fused is not None else ")"),
         "rollout_precision": precision if tr.fused is not None else "torch fp32",
+        "update_precision": ("x3: fused HIP attention-encoder forward + backward (encoder_train.py), dW on hipBLASLt"
+                             if upd == "x3" else "torch fp32 autograd (hipBLASLt)"),
         "gemm_table": tuned,
         "update_flop_per_sample": round(fps), "update_tflops": round(upd_tf, 2),
         "update_frac_fp32_mfma_peak": round(upd_tf / 157.3, 3),
@@ -506,6 +549,9 @@ def main(argv=None):
     ap.add_argument("--e2e-precision", choices=["fp32", "x3"], default="x3",
                     help="fused rollout encoders: fp32 matrix cores, or each fp32 product as 3 f16 products with fp32 "
                          "accumulation (x3, the default: within 2e-7 of fp32 on the encoder outputs, DESIGN.md §4.6)")
+    ap.add_argument("--e2e-update-precision", choices=["fp32", "x3"], default=None,
+                    help="the update's attention encoders: torch fp32 autograd or the fused x3 forward / backward "
+                         "kernels (default: --e2e-precision)")
     ap.add_argument("--host-sync", choices=["spin", "auto"], default="auto",
                     help="host wait of torch.cuda.synchronize(): spin (hipDeviceScheduleSpin) or HIP's default")
     args = ap.parse_args(argv)
@@ -639,7 +685,8 @@ def main(argv=None):
         log = (lambda m: print(m, file=sys.stderr, flush=True)) if rank == 0 else None
         try:
             e2e = end_to_end(env, cfg, dev, world, args.e2e_iters, args.e2e_steps or None, log,
-                             fused=not args.e2e_unfused, precision=args.e2e_precision)
+                             fused=not args.e2e_unfused, precision=args.e2e_precision,
+                             update_precision=args.e2e_update_precision or args.e2e_precision)
         except Exception as e:  # never let the PPO leg kill the env number
             if world > 1:
                 raise
@@ -699,7 +746,8 @@ def main(argv=None):
                          "bytes_per_agent_step": round(bpa, 1),
                          "bytes_per_agent_step_state_complete": (round(state_bytes_per_agent_step(cfg)[0], 1)
                                                                  if cfg.flavor == "B" else None),
-                         "bytes_per_launch": round(bpa * I / S)},
+                         "bytes_per_launch": round(bpa * I / S),
+                         "valu": valu_roofline(args.config, I, k_ms) if cfg.flavor == "A" else None},
             "nonfinite_guard": guard,
             "cpu_baseline": None,
             "end_to_end": e2e,

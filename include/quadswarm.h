@@ -18,6 +18,9 @@
  *   - qs_get_state/qs_set_state: env snapshot/restore (no reference equivalent; checkpoint + parity)
  *   - qs_curriculum_step replaces CurriculumCallback._on_step          swarm_rl/custom_callbacks.py:441-468
  *   - qs_curriculum_step_all: the same over every data-parallel rank's envs   custom_callbacks.py:452-462
+ *   - qs_attn_*_train_x3 / qs_attn_bwd{1,2}_x3: the PPO update's attention encoder forward + backward
+ *                                              (QuadNeighborhoodEncoderAttention, quad_multi_model.py:44-101,
+ *                                              under PPO.train's loss.backward)
  * The Python mirror of the reference's VecEnv surface (quadswarm_amd.vec_env.GpuQuadVecEnv) calls
  * these through ctypes; INTEGRATION.md shows the binding.
  *
@@ -479,6 +482,38 @@ int qs_attn_pool(int32_t B, int32_t K, int32_t H, const qs_attn_tower* towers, i
 int qs_attn_embed_x3(const float* d_obs, int32_t obs_stride, int32_t self_dim, int32_t nbr_off, int32_t B, int32_t K,
                      int32_t nd, int32_t H, const qs_attn_tower* towers, int32_t n_towers, void* stream);
 int qs_attn_pool_x3(int32_t B, int32_t K, int32_t H, const qs_attn_tower* towers, int32_t n_towers, void* stream);
+
+/* The PPO update's attention encoder (ABI 12; SURVEY §8 f4, the update side; qs_policy_train.h): the x3 forward with
+ * the activations the backward needs saved, and the backward's two row-block chains.  Per tower, next to its
+ * qs_attn_tower (x3-packed weights, e2 / e_mean / P / out as for qs_attn_embed_x3 / qs_attn_pool_x3), fp32 [B*K, H]
+ * unless noted (row j = agent j / K, neighbour j % K). */
+typedef struct qs_attn_train {
+    float* e1; float* a1; float* a2; float* v1; float* h;   /* forward: the tanh outputs (embedding 0, attention 0/2,
+                                                               value 0/2) */
+    float* w;              /* forward: [B*K] the softmax weights */
+    const float* dout;     /* backward 1: [B, H] dL/d out */
+    const float* dem;      /* backward 2: [B, H] dL/d e_mean = (sum over rows j % B = b of da1_pre_j) A_m */
+    const void* w_v2tp; const void* w_v1tp; const void* w_a2tp; const void* w_a1etp; const void* w_e2tp;
+                           /* x3-packed TRANSPOSED weights: W_v2^T, W_v1^T, W_a2^T, attention_mlp[0].weight[:, :H]^T, W_e2^T */
+    float* dh_pre; float* dv1_pre; float* da2_pre; float* da1_pre;   /* backward 1 outputs: pre-activation gradients */
+    float* dscore;         /* backward 1: [B*K] dL/d score */
+    float* de2p;           /* backward 1: dL/d e2 without the e_mean term */
+    float* de2_pre; float* de1_pre;                                  /* backward 2 outputs */
+} qs_attn_train;
+int qs_attn_embed_train_x3(const float* d_obs, int32_t obs_stride, int32_t self_dim, int32_t nbr_off, int32_t B, int32_t K,
+                           int32_t nd, int32_t H, const qs_attn_tower* towers, const qs_attn_train* trains,
+                           int32_t n_towers, void* stream);
+int qs_attn_pool_train_x3(int32_t B, int32_t K, int32_t H, const qs_attn_tower* towers, const qs_attn_train* trains,
+                          int32_t n_towers, void* stream);
+int qs_attn_bwd1_x3(int32_t B, int32_t K, int32_t H, const qs_attn_tower* towers, const qs_attn_train* trains,
+                    int32_t n_towers, void* stream);
+int qs_attn_bwd2_x3(int32_t B, int32_t K, int32_t H, const qs_attn_tower* towers, const qs_attn_train* trains,
+                    int32_t n_towers, void* stream);
+/* A weight gradient G^T A over R rows on the split-f16 matrix cores, split over n_parts row ranges:
+ * part[p] = G[rows of p]^T A[rows of p] ([n_parts, H, H] fp32; dW = the sum over p).  G [R, H] (pre-activation
+ * gradients) with a power-of-two scale per column, col_scale[n] |G[:, n]| < 2^14; A [R, H] with |A| <= 1 (tanh). */
+int qs_attn_dw_x3(const float* G, const float* A, const float* col_scale, int64_t R, int32_t H, float* part,
+                  int32_t n_parts, void* stream);
 
 /* sb_train's capture-radius curriculum on the device (ABI 11; replaces CurriculumCallback._on_step,
  * swarm_rl/custom_callbacks.py:441-468, which SB3 runs after every VecEnv step).  Flavor A.  The callback's state

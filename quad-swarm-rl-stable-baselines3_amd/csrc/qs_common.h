@@ -36,6 +36,7 @@ struct KP {
     // ---- flavor A (quadrotor_multi_rewards + Controller/), host-derived in make_kp ----
     int flavor, scenario, ticks, nfeat, nfd, n_cam;
     float cam_r, cam_f, cam_px, cam_w, cam_res;      // marker radius, focal, pixel sigma, sensor width, px
+    float cam_cos[8], cam_sin[8];                     // camera k's axis (cos, sin of k 2 pi / n_cam), host-computed
     float hrate;                                      // dt * MAX_ANGULAR_RATE (Controller.py:29,81)
     float speed, inv_dt;
     float pkp[10], pkd[10], pki[10], psat[10], paw[10];

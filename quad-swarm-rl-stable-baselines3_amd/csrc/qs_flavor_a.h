@@ -217,11 +217,12 @@ __device__ __forceinline__ void camera(const KP& kp, float rx, float ry, float g
     // get_camera_angle (get_state.py:128-137) without the atan2: the camera whose axis k seg is nearest the
     // bearing is the one with the largest projection rp . (cos k seg, sin k seg) (the first on an exact tie; the
     // reference's round() differs only on the sector boundaries, where the features are ill-conditioned anyway).
-    // The axes are compile-time constants in the specialised kernels (libm cosf / sinf of constants fold).
+    // The axes are computed once on the host (KP cam_cos / cam_sin): constants in the specialised kernels, loads
+    // in the generic ones (no libm call in the candidate loop).
     const float seg = k2Pi / (float)kp.n_cam;
     float best = rp0, ca = 1.f, sa = 0.f, cam = 0.f;
     for (int k = 1; k < kp.n_cam; ++k) {
-        const float ck = cosf((float)k * seg), sk = sinf((float)k * seg);
+        const float ck = kp.cam_cos[k], sk = kp.cam_sin[k];
         const float pk = rp0 * ck + rp1 * sk;
         const bool gt = pk > best;
         best = gt ? pk : best;

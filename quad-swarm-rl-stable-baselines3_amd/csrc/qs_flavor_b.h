@@ -5,6 +5,10 @@
 #include "qs_scen.h"
 #include "qs_replay.h"
 
+#ifndef QS_PAIR_ROUNDS
+#define QS_PAIR_ROUNDS 1   // drone-pair impulses in rounds of disjoint pairs (else one pair per iteration)
+#endif
+
 namespace qs {
 
 // ---------------------------------------------------------------------------------------------
@@ -877,6 +881,16 @@ __global__ __launch_bounds__(StepGeo<NPAD>::WGS) void step_kernel(const KP* __re
     }
     int omi = 0, osi = 0;   // the env's domain-randomisation choice (QS_E_OBST_M / _SZ)
     if (OBST && kp.dr) { omi = b.env[QS_E_OBST_M * kp.E + eidx]; osi = b.env[QS_E_OBST_SZ * kp.E + eidx]; }
+    // goal scenario: the env's scenario record (SC_WORDS words) dealt over its lanes -- word li + LPE t on lane li
+    // -- loaded with the step's other loads and staged in LDS for scenario.step() after the forces
+    const bool SCEN = !OBST && kp.scen_b >= 0;
+    constexpr int SRW = (SC_WORDS + LPE - 1) / LPE;
+    uint32_t scw[SRW];
+#pragma unroll
+    for (int t = 0; t < SRW; ++t) {
+        const int w = li + LPE * t;
+        scw[t] = (SCEN && envok && w < SC_WORDS) ? scen_word(kp, b, env, w) : 0u;
+    }
     Drone d;   // every sub-lane holds the whole drone
     DroneWords<Q, LW> dw;
     load_words_q<Q, LW, NIW>(kp, b, g, q, dw, kp.stats ? LW : DW);
@@ -1103,6 +1117,86 @@ __global__ __launch_bounds__(StepGeo<NPAD>::WGS) void step_kernel(const KP* __re
             impulses_wide<NPAD>(kp, rng, lds, ec, d, active ? row_above(newpairs, di) : Row{}, env, di, q, lane, vchanged);
         } else {
         uint64_t pend = active ? row_above(newpairs, di) : 0ull;
+#if QS_PAIR_ROUNDS
+        // Rounds of disjoint pairs (round 5).  The reference applies the new pairs one by one in (i, j) order
+        // (quadrotor_multi.py:671-676); a pair only reads and writes its two drones, so what matters is that every
+        // pair sees its drones after all their earlier pairs.  A round takes every pending pair that is the earliest
+        // pending pair of both its drones -- disjoint pairs, each already preceded by all of its drones' earlier
+        // pairs -- and applies them at once: the same draws and arithmetic per pair as the one-pair loop below
+        // (bitwise the same states), in as many rounds as the longest chain of pairs sharing drones instead of one
+        // iteration per pair.  Per round: the env's pending rows and their columns through LDS (the obs tile is
+        // free until the obs phase), the ready pairs' 9 Philox blocks drawn by the env's lanes (lane le: block
+        // le % 9 of pair le / 9), up to LPE / 9 pairs (more wait a round).
+        constexpr int PMAX = LPE / 9, TBL4 = (2 * NPAD + 3) / 4, STR4 = PMAX * 9 + TBL4;
+        if (PMAX > 0 && NPAD <= 32 && EPB * STR4 * 4 <= SLOTS * kp.obs_dim) {
+            float4* pscr = reinterpret_cast<float4*>(lds) + el * STR4;
+            uint32_t* pt = reinterpret_cast<uint32_t*>(pscr + PMAX * 9);   // [NPAD] the drones' pending rows
+            uint32_t* ct = pt + NPAD;                                     // [NPAD] their columns (earlier owners)
+            const int le = lane - lbase, pb = le / 9, kb = le - 9 * pb;
+            for (;;) {
+                const uint64_t bal = __ballot(pend != 0ull && q == 0);
+                if (bal == 0ull) break;
+                if (q == 0) pt[di] = (uint32_t)pend;
+                lds_sync();
+                uint32_t col = 0u;
+#pragma unroll
+                for (int i = 0; i < NPAD; ++i) col |= ((pt[i] >> di) & 1u) << i;
+                if (q == 0) ct[di] = col;
+                lds_sync();
+                const int jf = pend ? (__ffsll((long long)pend) - 1) : 0;
+                const int i0 = col ? (__ffs((int)col) - 1) : 0;
+                // owner of a ready pair: nothing earlier of this drone pending, and (di, jf) is jf's earliest
+                const bool own = pend != 0ull && col == 0u && (__ffs((int)ct[jf]) - 1) == di;
+                // partner in a ready pair: its earliest pair is (i0, di) and i0 has nothing earlier pending
+                const bool part = col != 0u && ct[i0] == 0u && (__ffs((int)pt[i0]) - 1) == di;
+                const uint64_t re = (__ballot(own && q == 0) >> lbase) & lmask;   // ready owners (bit owner * Q)
+                const int ow = own ? di : (part ? i0 : 0);
+                const int rank = __popcll(re & ((1ull << (ow * Q)) - 1ull));
+                const bool go = (own || part) && rank < PMAX;
+                const int partner = own ? jf : (part ? i0 : di);
+                float pp[3], pv[3], pw[3];
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    pp[c] = __shfl(d.pos[c], lbase + partner * Q + q);
+                    pv[c] = __shfl(d.vel[c], lbase + partner * Q + q);
+                    pw[c] = __shfl(d.om[c], lbase + partner * Q + q);
+                }
+                if (pb < PMAX && pb < __popcll(re)) {   // block kb of the round's pb-th pair
+                    uint64_t m = re;
+                    for (int k = 0; k < pb; ++k) m &= m - 1ull;
+                    const int ob = (__ffsll((long long)m) - 1) / Q, oj = __ffs((int)pt[ob]) - 1;
+                    const bool isn = kb < 7;
+                    const uint32_t st = S_PAIR | ((uint32_t)oj << 8);
+                    const W4 w = block(rng, kp.id0 + (uint32_t)(env * kp.N + ob), isn ? st : (st | UNIF_BIT),
+                                       (uint32_t)(isn ? kb : kb - 7));
+                    float v[4];
+                    if (isn) {
+                        box_muller(w.w[0], w.w[1], v[0], v[1]);
+                        box_muller(w.w[2], w.w[3], v[2], v[3]);
+                    } else {
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) v[i] = u01(w.w[i]);
+                    }
+                    pscr[le] = make_float4(v[0], v[1], v[2], v[3]);
+                }
+                lds_sync();
+                if (go) {
+                    float z[28], u[8];
+#pragma unroll
+                    for (int k = 0; k < 9; ++k) {
+                        const float4 x = pscr[rank * 9 + k];
+                        float* o = k < 7 ? z + 4 * k : u + 4 * (k - 7);
+                        o[0] = x.x; o[1] = x.y; o[2] = x.z; o[3] = x.w;
+                    }
+                    if (own) collide_pair(d.pos, d.vel, d.om, pp, pv, pw, z, u);
+                    else collide_pair(pp, pv, pw, d.pos, d.vel, d.om, z, u);
+                    vchanged = true;
+                }
+                lds_sync();   // the scratch and the tables are rewritten by the next round
+                if (go && own) pend &= ~(1ull << jf);
+            }
+        }
+#endif
         for (;;) {
             const uint64_t bal = __ballot(pend != 0ull && q == 0);
             if (bal == 0ull) break;
@@ -1187,26 +1281,42 @@ __global__ __launch_bounds__(StepGeo<NPAD>::WGS) void step_kernel(const KP* __re
     // ---- scenario.step() (quadrotor_multi.py:700-701): new goals after the forces.  The reference's
     // observations keep the old goal unless the env's state-update flag (a downwash or impulse on any
     // drone, :659-698) makes it recompute them after the scenario step (:711-712). ----
-    const bool SCEN = !OBST && kp.scen_b >= 0;
+    // Every lane of an env runs scenario.step() for its own drone (scen_step_lane: the same draws and scalars on
+    // every lane, the drone's own goal row); envs whose scenario does nothing at this tick skip it, and the
+    // scenario record is stored only where it changed.
     float obs_goal[3] = {d.goal[0], d.goal[1], d.goal[2]};
     float* stab = scen_tab(lds, kp, SLOTS) + el * scen_stride<NPAD>();
     if (SCEN) {
+        uint32_t* srec = reinterpret_cast<uint32_t*>(stab + 2 * (NPAD + 4) * 4);
         if (q == 0 && di < kp.N) { stab[4 * di] = d.goal[0]; stab[4 * di + 1] = d.goal[1]; stab[4 * di + 2] = d.goal[2]; }
-        lds_sync();
-        if (active && di == 0 && q == 0) {
-            Scen sc;
-            scen_load(kp, b, env, sc);
-            SDraw sd = sdraw(rng, gid, S_SCN);
-            scen_step(kp, sc, tick, sd, stab, stab + 4 * (NPAD + 4));
-            scen_store(kp, b, env, sc);
+#pragma unroll
+        for (int t = 0; t < SRW; ++t) {
+            const int w = li + LPE * t;
+            if (envok && w < SC_WORDS) srec[w] = scw[t];
         }
         lds_sync();
-        const bool upd = ec.any(active && vchanged);
-        if (di < kp.N)
-            for (int k = 0; k < 3; ++k) {
-                d.goal[k] = stab[4 * di + k];
-                if (upd) obs_goal[k] = d.goal[k];
+        const bool sact = active && scen_acts(kp, (int)srec[0], (int)srec[2], tick);
+        if (ec.wany(sact)) {
+            bool via = false;
+            if (sact) {
+                Scen sc;
+                scen_from_words(srec, sc);
+                SDraw sd = sdraw(rng, kp.id0 + (uint32_t)(env * kp.N), S_SCN);
+                const int ch = scen_step_lane(kp, sc, tick, sd, di, stab, stab + 4 * (NPAD + 4), d.goal, via);
+                if (di == 0 && q == 0) {
+                    if (ch == 2) scen_store(kp, b, env, sc);
+                    else if (ch == 1) scen_store_size(kp, b, env, sc);
+                }
             }
+            if (ec.wany(via)) {   // the shuffled goals: table B's row of the drone
+                lds_sync();
+                if (via)
+                    for (int k = 0; k < 3; ++k) d.goal[k] = stab[4 * (NPAD + 4) + 4 * di + k];
+            }
+        }
+        const bool upd = ec.any(active && vchanged);
+        if (upd)
+            for (int k = 0; k < 3; ++k) obs_goal[k] = d.goal[k];
     }
 
     // The drone state is final here (unless its env resets below, which stores it again): storing it now

@@ -1,0 +1,600 @@
+// qs_policy_train.h -- the PPO update's attention neighbour encoder on the split-f16 matrix cores: the forward with
+// the activations the backward needs saved, and the backward's two row-block chains (the update side).
+//
+// QuadNeighborhoodEncoderAttention (swarm_rl/models/quad_multi_model.py:44-101) as qs_policy.h writes it, per
+// neighbour row j (row j = agent j / K, neighbour j % K; self / e_mean of agent j % B -- the reference's pairing):
+//   e1 = tanh(x0_j W_e1^T + b_e1)        x0_j = [nbr_j | self_{j % B}]
+//   e2 = tanh(e1 W_e2^T + b_e2)          e_mean[a] = mean_k e2[a K + k]
+//   a1 = tanh(e2 A_e^T + P[j % B])       P = e_mean A_m^T + b_a1
+//   a2 = tanh(a1 W_a2^T + b_a2)          score = a2 . w3 + b3,  w = softmax over the agent's K rows
+//   v1 = tanh(e2 W_v1^T + b_v1),  h = tanh(v1 W_v2^T + b_v2),  out[a] = sum_k w h
+// Backward, with dout = dL/d out [B, H] (t' = 1 - t^2 the tanh derivative at the saved output t):
+//   dh_pre  = w_j dout[a] h'                        dw_j = h_j . dout[a]
+//   dv1_pre = (dh_pre W_v2) v1'                     dscore_j = w_j (dw_j - sum_k w_k dw_k)
+//   da2_pre = dscore_j w3 a2'                       da1_pre = (da2_pre W_a2) a1'
+//   de2p    = dv1_pre W_v1 + da1_pre A_e            (kernel 1: attn_bwd1_x3_kernel)
+//   dP[b]   = sum_{j % B = b} da1_pre_j,  dem = dP A_m                       (torch, [B, H])
+//   de2_pre = (de2p + dem[j / K] / K) e2'           de1_pre = (de2_pre W_e2) e1'   (kernel 2: attn_bwd2_x3_kernel)
+// and the weight gradients as GEMMs over the rows of the saved pairs (dW_v2 = dh_pre^T v1, ...; torch / hipBLASLt).
+//
+// Every contraction is mfma_layer_x3 (qs_policy_x3.h: x = (hi + lo) / s, three f16 products per fp32 product, fp32
+// accumulation).  The backward's tiles hold gradients, whose magnitudes are not bounded like tanh outputs: each
+// row gets its own power-of-two scale s_i (its max |x| into [2^13, 2^14) -- exact, the products come back divided by
+// s_i), the row maxima reduced over the wave (rows staged from HBM: a row is one wave's 64 lanes) or over the four
+// waves through LDS (rows staged from the accumulators, in the barrier every layer has anyway).  The weights' range
+// is checked by the packer (policy_fused.pack_mfma_weight_x3).  Block geometry, row pairing and packing as in
+// qs_policy.h / qs_policy_x3.h; the W^T operands of the backward GEMMs are packed like any weight (of W^T).
+#pragma once
+#include "qs_policy_x3.h"
+
+namespace qs {
+namespace pol {
+
+struct Trains {
+    qs_attn_train t[QS_ATTN_MAX_TOWERS];
+};
+
+// power-of-two scale of a row with max |x| = mx: s mx in [2^13, 2^14) (1 for an all-zero or non-finite row)
+__device__ __forceinline__ float row_scale(float mx) {
+    if (!(mx > 0.f) || !(mx <= 3.0e38f)) return 1.f;
+    return __builtin_amdgcn_ldexpf(1.f, 14 - __builtin_amdgcn_frexp_expf(mx));
+}
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v = fmaxf(v, __shfl_xor(v, m));
+    return v;
+}
+__device__ __forceinline__ float4 ld4g(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void st4g(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+__device__ __forceinline__ float absmax4(float4 v) { return fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))); }
+__device__ __forceinline__ float4 f4_scale(float4 v, float s) { return make_float4(s * v.x, s * v.y, s * v.z, s * v.w); }
+__device__ __forceinline__ float4 f4_dtanh(float4 g, float4 t) {   // g (1 - t^2)
+    return make_float4(g.x * (1.f - t.x * t.x), g.y * (1.f - t.y * t.y), g.z * (1.f - t.z * t.z), g.w * (1.f - t.w * t.w));
+}
+
+// Rows staged from HBM: wave w takes rows w, w + 4, ...; lane l < H/4 the row's columns 4l .. 4l+3.
+// val(r, c4, on) -> the row's float4 (0 for unused rows), called by every lane of the wave (it may reduce over the
+// wave) with on = the lane holds columns (c4 is clamped for the others, whose value is dropped); sink(r, c4, v) sees
+// the lane's value (e.g. stores it); the tile gets s_r v and RS[r] = 1 / s_r.
+template <int H, typename Val, typename Sink>
+__device__ __forceinline__ void stage_rows_scaled(const TileX3& X, float* RS, int wave, int lane, Val val, Sink sink) {
+    constexpr int L4 = H / 4;
+    const bool on = lane < L4;
+    const int c4 = on ? lane : 0;
+    for (int r = wave; r < MROWS; r += NWAVE) {
+        float4 v = val(r, c4, on);
+        if (!on) v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (on) sink(r, lane, v);
+        const float s = row_scale(wave_max(absmax4(v)));
+        if (on) X.put4(r, 4 * lane, f4_scale(v, s));
+        if (lane == 0) RS[r] = 1.f / s;
+    }
+}
+
+// Rows staged from a layer's accumulators (acc -> y in place by f(i, n0, acc4) -> float4): per-row max over the
+// four waves through RMX, then the scaled tile.  Contains the barrier between the layer's last tile read and the
+// tile's overwrite.  RS[i] (read by f) is replaced by the new row's 1 / s.
+template <int H, typename F>
+__device__ __forceinline__ void stage_acc_scaled(const TileX3& X, f32x16 (&acc)[RT][Geo<H>::CT], float* RS, float* RMX,
+                                                 int wave, int lane, F f) {
+    constexpr int CT = Geo<H>::CT;
+    float mx[RT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+        const int i = acc_i(rt, lane);
+        float m = 0.f;
+#pragma unroll
+        for (int c = 0; c < CT; ++c)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const float4 y = f(i, acc_n0<H>(wave, c, g, lane), acc4(acc[rt][c], g));
+                acc[rt][c][4 * g] = y.x; acc[rt][c][4 * g + 1] = y.y;
+                acc[rt][c][4 * g + 2] = y.z; acc[rt][c][4 * g + 3] = y.w;
+                m = fmaxf(m, absmax4(y));
+            }
+        mx[rt] = fmaxf(m, __shfl_xor(m, 32));
+    }
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+        if (lane < 32) RMX[wave * MROWS + acc_i(rt, lane)] = mx[rt];
+    __syncthreads();   // every wave has read the tile (and RS), RMX complete
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+        const int i = acc_i(rt, lane);
+        const float m = fmaxf(fmaxf(RMX[i], RMX[MROWS + i]), fmaxf(RMX[2 * MROWS + i], RMX[3 * MROWS + i]));
+        const float s = row_scale(m);
+#pragma unroll
+        for (int c = 0; c < CT; ++c)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) X.put4(i, acc_n0<H>(wave, c, g, lane), f4_scale(acc4(acc[rt][c], g), s));
+        if (wave == 0 && lane < 32) RS[i] = 1.f / s;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------------------------
+// forward with saves: attn_embed_x3_kernel + e1; attn_pool_x3_kernel + a1, a2, v1, h, w (qs_policy_x3.h, same math)
+// ------------------------------------------------------------------------------------------------------------------
+template <int H>
+__global__ __launch_bounds__(NTHR, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void attn_embed_train_x3_kernel(
+    const float* __restrict__ obs, int stride, int so, int off, int B, int K, int nd, Towers tw, Trains trs) {
+    constexpr int LDH = GeoX3<H>::LDH, LD0 = GeoX3<KD0>::LDH, CT = Geo<H>::CT;
+    extern __shared__ float4 smem4[];
+    _Float16* xh = reinterpret_cast<_Float16*>(smem4);
+    const TileX3 X{xh, xh + MROWS * LDH, LDH};
+    const TileX3 X0{xh + 2 * MROWS * LDH, xh + 2 * MROWS * LDH + MROWS * LD0, LD0};
+    float* BI = reinterpret_cast<float*>(xh + 2 * MROWS * LDH + 2 * MROWS * LD0);
+    const qs_attn_tower& t = tw.t[blockIdx.y];
+    const qs_attn_train& tr = trs.t[blockIdx.y];
+    const int AB = MROWS / K, MU = AB * K;
+    const long R = (long)B * K, row0 = (long)blockIdx.x * MU;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    for (int n = tid; n < H; n += NTHR) {
+        BI[n] = t.b_e1[n];
+        BI[H + n] = t.b_e2[n];
+    }
+    gather_rows0(obs, stride, so, off, B, K, nd, row0, MU, R, tid, [&](int r, int c, float v) { X0.put(r, c, X3_SIN * v); });
+    __syncthreads();
+    f32x16 acc[RT][CT];
+    mfma_layer_x3<H, KD0, true, false>(X0, reinterpret_cast<const uint4*>(t.w_e1p), acc, wave, lane);
+    store_tanh_x3<H>(X, acc, 1.f / (X3_SIN * X3_SW), wave, lane,
+                     [&](int i, int n0) {
+                         return (i < MU && row0 + i < R) ? lds4(BI + n0) : make_float4(0.f, 0.f, 0.f, 0.f);
+                     },
+                     [&](int i, int n0, float4 y) {
+                         if (i < MU && row0 + i < R) st4g(tr.e1 + (row0 + i) * H + n0, y);
+                     });
+    __syncthreads();
+    mfma_layer_x3<H, H, true, false>(X, reinterpret_cast<const uint4*>(t.w_e2p), acc, wave, lane);
+    __syncthreads();
+    store_tanh_x3<H>(X, acc, 1.f / (X3_SX * X3_SW), wave, lane, [&](int, int n0) { return lds4(BI + H + n0); },
+                     [&](int i, int n0, float4 y) {
+                         if (i < MU && row0 + i < R) st4g(t.e2 + (row0 + i) * H + n0, y);
+                     });
+    __syncthreads();
+    constexpr float isx = 1.f / X3_SX;
+    const float inv = 1.f / (float)K;
+    for (int e = tid; e < AB * H; e += NTHR) {
+        const int a = e / H, n = e - a * H;
+        const long agent = row0 / K + a;
+        if (agent < B) {
+            float s = 0.f;
+            for (int k = 0; k < K; ++k) s += X.get(a * K + k, n) * isx;
+            t.e_mean[agent * H + n] = s * inv;
+        }
+    }
+}
+
+template <int H>
+__global__ __launch_bounds__(NTHR, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void attn_pool_train_x3_kernel(
+    int B, int K, Towers tw, Trains trs) {
+    constexpr int LDH = GeoX3<H>::LDH, CT = Geo<H>::CT;
+    extern __shared__ float4 smem4[];
+    _Float16* xh = reinterpret_cast<_Float16*>(smem4);
+    const TileX3 X{xh, xh + MROWS * LDH, LDH};
+    float* SC = reinterpret_cast<float*>(xh + 2 * MROWS * LDH);
+    float* WT = SC + MROWS;
+    float* A3 = WT + 2 * MROWS;
+    const qs_attn_tower& t = tw.t[blockIdx.y];
+    const qs_attn_train& tr = trs.t[blockIdx.y];
+    const int AB = MROWS / K, MU = AB * K;
+    const long R = (long)B * K, row0 = (long)blockIdx.x * MU;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    constexpr float SS = X3_SX * X3_SW, iSS = 1.f / SS;
+    for (int n = tid; n < H; n += NTHR) {
+        A3[n] = t.w_a3[n];
+        A3[H + n] = t.b_a2[n];
+        A3[2 * H + n] = t.b_v1[n];
+        A3[3 * H + n] = t.b_v2[n];
+    }
+    auto okrow = [&](int i) { return i < MU && row0 + i < R; };
+    f32x16 acc[RT][CT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+        const int i = acc_i(rt, lane);
+        const int j = (int)row0 + i;
+        const float okf = okrow(i) ? 1.f : 0.f;
+        const float* pr = t.P + (size_t)(okrow(i) ? j % B : 0) * H;
+#pragma unroll
+        for (int c = 0; c < CT; ++c)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                float4 v = *reinterpret_cast<const float4*>(pr + acc_n0<H>(wave, c, g, lane));
+                v = make_float4(v.x * okf, v.y * okf, v.z * okf, v.w * okf);
+                acc[rt][c][4 * g] = SS * v.x; acc[rt][c][4 * g + 1] = SS * v.y;
+                acc[rt][c][4 * g + 2] = SS * v.z; acc[rt][c][4 * g + 3] = SS * v.w;
+            }
+    }
+    load_rows_x3<H>(X, t.e2, row0, MU, R, tid);
+    __syncthreads();
+    mfma_layer_x3<H, H, false>(X, reinterpret_cast<const uint4*>(t.w_a1ep), acc, wave, lane);
+    __syncthreads();
+    store_tanh_x3<H>(X, acc, iSS, wave, lane, ZeroInit(), [&](int i, int n0, float4 y) {
+        if (okrow(i)) st4g(tr.a1 + (row0 + i) * H + n0, y);
+    });
+    __syncthreads();
+    mfma_layer_x3<H>(X, reinterpret_cast<const uint4*>(t.w_a2p), acc, wave, lane);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {   // a2 (the rollout kernel keeps it in the score's registers only)
+        const int i = acc_i(rt, lane);
+        if (!okrow(i)) continue;
+#pragma unroll
+        for (int c = 0; c < CT; ++c)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int n0 = acc_n0<H>(wave, c, g, lane);
+                const float4 b = lds4(A3 + H + n0);
+                st4g(tr.a2 + (row0 + i) * H + n0,
+                     make_float4(tanh_fast(fmaf(acc[rt][c][4 * g], iSS, b.x)), tanh_fast(fmaf(acc[rt][c][4 * g + 1], iSS, b.y)),
+                                 tanh_fast(fmaf(acc[rt][c][4 * g + 2], iSS, b.z)), tanh_fast(fmaf(acc[rt][c][4 * g + 3], iSS, b.w))));
+            }
+    }
+    float* SCP = A3 + 4 * H;
+    score_partials<H>(acc, iSS, A3, A3 + H, SCP, wave, lane);
+    __syncthreads();
+    if (tid < MROWS) SC[tid] = ((SCP[tid] + SCP[MROWS + tid]) + (SCP[2 * MROWS + tid] + SCP[3 * MROWS + tid])) + t.b_a3;
+    __syncthreads();
+    if (tid < AB) {
+        const int base = tid * K;
+        float m = SC[base];
+        for (int k = 1; k < K; ++k) m = fmaxf(m, SC[base + k]);
+        float s = 0.f;
+        for (int k = 0; k < K; ++k) {
+            const float x = expf(SC[base + k] - m);
+            WT[base + k] = x;
+            s += x;
+        }
+        for (int k = 0; k < K; ++k) WT[base + k] = WT[base + k] / s;
+    }
+    load_rows_x3<H>(X, t.e2, row0, MU, R, tid);
+    __syncthreads();
+    if (tid < MU && row0 + tid < R) tr.w[row0 + tid] = WT[tid];
+    mfma_layer_x3<H>(X, reinterpret_cast<const uint4*>(t.w_v1p), acc, wave, lane);
+    __syncthreads();
+    store_tanh_x3<H>(X, acc, iSS, wave, lane, [&](int, int n0) { return lds4(A3 + 2 * H + n0); },
+                     [&](int i, int n0, float4 y) {
+                         if (okrow(i)) st4g(tr.v1 + (row0 + i) * H + n0, y);
+                     });
+    __syncthreads();
+    mfma_layer_x3<H>(X, reinterpret_cast<const uint4*>(t.w_v2p), acc, wave, lane);
+    __syncthreads();
+    float* Y = reinterpret_cast<float*>(smem4);
+    constexpr int LDY = H + 4;
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+        const int i = acc_i(rt, lane);
+        const float wi = i < MU ? WT[i] : 0.f;
+#pragma unroll
+        for (int c = 0; c < CT; ++c)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int n0 = acc_n0<H>(wave, c, g, lane);
+                const float4 b = lds4(A3 + 3 * H + n0);
+                const float4 h = make_float4(tanh_fast(fmaf(acc[rt][c][4 * g], iSS, b.x)), tanh_fast(fmaf(acc[rt][c][4 * g + 1], iSS, b.y)),
+                                             tanh_fast(fmaf(acc[rt][c][4 * g + 2], iSS, b.z)), tanh_fast(fmaf(acc[rt][c][4 * g + 3], iSS, b.w)));
+                if (okrow(i)) st4g(tr.h + (row0 + i) * H + n0, h);
+                *reinterpret_cast<float4*>(Y + i * LDY + n0) = make_float4(wi * h.x, wi * h.y, wi * h.z, wi * h.w);
+            }
+    }
+    __syncthreads();
+    for (int e = tid; e < AB * H; e += NTHR) {
+        const int a = e / H, n = e - a * H;
+        const long agent = row0 / K + a;
+        if (agent < B) {
+            float s = 0.f;
+            for (int k = 0; k < K; ++k) s += Y[(a * K + k) * LDY + n];
+            t.out[agent * H + n] = s;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------------------------
+// backward
+// ------------------------------------------------------------------------------------------------------------------
+template <int H>
+constexpr size_t bwd_fixed_lds_bytes() {   // split tile + WT, DW, SC, RS (MROWS each) + RMX (4 MROWS) + w3 (H)
+    return (size_t)(2 * MROWS * GeoX3<H>::LDH) * 2 + (size_t)(8 * MROWS + H) * 4;
+}
+
+// kernel 1: value chain (dh_pre -> dv1_pre -> de2 part) and attention chain (dscore -> da2_pre -> da1_pre -> de2 part);
+// dynamic LDS: bwd_fixed_lds_bytes<H>() + (MROWS / K) H floats for the block's dout rows
+template <int H>
+__global__ __launch_bounds__(NTHR, 2) void attn_bwd1_x3_kernel(int B, int K, Towers tw, Trains trs) {
+    constexpr int LDH = GeoX3<H>::LDH, CT = Geo<H>::CT, L4 = H / 4;
+    extern __shared__ float4 smem4[];
+    _Float16* xh = reinterpret_cast<_Float16*>(smem4);
+    const TileX3 X{xh, xh + MROWS * LDH, LDH};
+    float* WT = reinterpret_cast<float*>(xh + 2 * MROWS * LDH);
+    float* DW = WT + MROWS;
+    float* SC = DW + MROWS;
+    float* RS = SC + MROWS;
+    float* RMX = RS + MROWS;
+    float* W3 = RMX + NWAVE * MROWS;
+    float* DO = W3 + H;
+    const qs_attn_tower& t = tw.t[blockIdx.y];
+    const qs_attn_train& tr = trs.t[blockIdx.y];
+    const int AB = MROWS / K, MU = AB * K;
+    const long R = (long)B * K, row0 = (long)blockIdx.x * MU, a0 = row0 / K;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    auto okrow = [&](int i) { return i < MU && row0 + i < R; };
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int e = tid; e < AB * L4; e += NTHR) {
+        const int a = e / L4, c4 = e - a * L4;
+        reinterpret_cast<float4*>(DO)[e] = (a0 + a < B) ? ld4g(tr.dout + (a0 + a) * H + 4 * c4) : z4;
+    }
+    for (int n = tid; n < H; n += NTHR) W3[n] = t.w_a3[n];
+    if (tid < MROWS) WT[tid] = okrow(tid) ? tr.w[row0 + tid] : 0.f;
+    __syncthreads();
+    // dw_j = h_j . dout[a] and dh_pre = w_j dout[a] (1 - h^2): wave-owned rows
+    stage_rows_scaled<H>(X, RS, wave, lane,
+                         [&](int r, int c4, bool on) {
+                             if (!okrow(r)) return z4;
+                             const float4 h = ld4g(tr.h + (row0 + r) * H + 4 * c4);
+                             const float4 d = lds4(DO + (r / K) * H + 4 * c4);
+                             const float dw = wave_sum(on ? h.x * d.x + h.y * d.y + h.z * d.z + h.w * d.w : 0.f);
+                             if (lane == 0) DW[r] = dw;
+                             return f4_dtanh(f4_scale(d, WT[r]), h);
+                         },
+                         [&](int r, int c4, float4 v) {
+                             if (okrow(r)) st4g(tr.dh_pre + (row0 + r) * H + 4 * c4, v);
+                         });
+    __syncthreads();
+    f32x16 acc[RT][CT];
+    constexpr float iSW = 1.f / X3_SW;
+    // dv1_pre = (dh_pre W_v2) (1 - v1^2)
+    mfma_layer_x3<H>(X, reinterpret_cast<const uint4*>(tr.w_v2tp), acc, wave, lane);
+    stage_acc_scaled<H>(X, acc, RS, RMX, wave, lane, [&](int i, int n0, float4 a) {
+        if (!okrow(i)) return z4;
+        const float4 y = f4_dtanh(f4_scale(a, RS[i] * iSW), ld4g(tr.v1 + (row0 + i) * H + n0));
+        st4g(tr.dv1_pre + (row0 + i) * H + n0, y);
+        return y;
+    });
+    __syncthreads();
+    // de2p = dv1_pre W_v1 (the attention chain's part is added below)
+    mfma_layer_x3<H>(X, reinterpret_cast<const uint4*>(tr.w_v1tp), acc, wave, lane);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+        const int i = acc_i(rt, lane);
+        if (!okrow(i)) continue;
+        const float sc = RS[i] * iSW;
+#pragma unroll
+        for (int c = 0; c < CT; ++c)
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+                st4g(tr.de2p + (row0 + i) * H + acc_n0<H>(wave, c, g, lane), f4_scale(acc4(acc[rt][c], g), sc));
+    }
+    // dscore_j = w_j (dw_j - sum_k w_k dw_k) over the agent's K rows
+    if (tid < MROWS) {
+        float s = 0.f;
+        if (tid < MU) {
+            const int base = (tid / K) * K;
+            for (int k = 0; k < K; ++k) s += WT[base + k] * DW[base + k];
+        }
+        const float ds = okrow(tid) ? WT[tid] * (DW[tid] - s) : 0.f;
+        SC[tid] = ds;
+        if (okrow(tid)) tr.dscore[row0 + tid] = ds;
+    }
+    __syncthreads();   // SC complete; every wave has read the tile and RS
+    // da2_pre = dscore_j w3 (1 - a2^2)
+    stage_rows_scaled<H>(X, RS, wave, lane,
+                         [&](int r, int c4, bool) {
+                             if (!okrow(r)) return z4;
+                             const float4 a2 = ld4g(tr.a2 + (row0 + r) * H + 4 * c4);
+                             return f4_dtanh(f4_scale(lds4(W3 + 4 * c4), SC[r]), a2);
+                         },
+                         [&](int r, int c4, float4 v) {
+                             if (okrow(r)) st4g(tr.da2_pre + (row0 + r) * H + 4 * c4, v);
+                         });
+    __syncthreads();
+    // da1_pre = (da2_pre W_a2) (1 - a1^2)
+    mfma_layer_x3<H>(X, reinterpret_cast<const uint4*>(tr.w_a2tp), acc, wave, lane);
+    stage_acc_scaled<H>(X, acc, RS, RMX, wave, lane, [&](int i, int n0, float4 a) {
+        if (!okrow(i)) return z4;
+        const float4 y = f4_dtanh(f4_scale(a, RS[i] * iSW), ld4g(tr.a1 + (row0 + i) * H + n0));
+        st4g(tr.da1_pre + (row0 + i) * H + n0, y);
+        return y;
+    });
+    __syncthreads();
+    // de2p += da1_pre A_e
+    mfma_layer_x3<H>(X, reinterpret_cast<const uint4*>(tr.w_a1etp), acc, wave, lane);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+        const int i = acc_i(rt, lane);
+        if (!okrow(i)) continue;
+        const float sc = RS[i] * iSW;
+#pragma unroll
+        for (int c = 0; c < CT; ++c)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                float* p = tr.de2p + (row0 + i) * H + acc_n0<H>(wave, c, g, lane);
+                st4g(p, f4_add(ld4g(p), f4_scale(acc4(acc[rt][c], g), sc)));   // this lane stored it above
+            }
+    }
+}
+
+// kernel 2: de2_pre = (de2p + dem[j / K] / K) (1 - e2^2) -> de1_pre = (de2_pre W_e2) (1 - e1^2)
+template <int H>
+__global__ __launch_bounds__(NTHR, 2) void attn_bwd2_x3_kernel(int B, int K, Towers tw, Trains trs) {
+    constexpr int LDH = GeoX3<H>::LDH, CT = Geo<H>::CT;
+    extern __shared__ float4 smem4[];
+    _Float16* xh = reinterpret_cast<_Float16*>(smem4);
+    const TileX3 X{xh, xh + MROWS * LDH, LDH};
+    float* RS = reinterpret_cast<float*>(xh + 2 * MROWS * LDH);
+    float* RMX = RS + MROWS;
+    const qs_attn_tower& t = tw.t[blockIdx.y];
+    const qs_attn_train& tr = trs.t[blockIdx.y];
+    const int AB = MROWS / K, MU = AB * K;
+    const long R = (long)B * K, row0 = (long)blockIdx.x * MU;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    auto okrow = [&](int i) { return i < MU && row0 + i < R; };
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float invK = 1.f / (float)K;
+    stage_rows_scaled<H>(X, RS, wave, lane,
+                         [&](int r, int c4, bool) {
+                             if (!okrow(r)) return z4;
+                             const long j = row0 + r;
+                             const float4 g = f4_add(ld4g(tr.de2p + j * H + 4 * c4),
+                                                     f4_scale(ld4g(tr.dem + (j / K) * H + 4 * c4), invK));
+                             return f4_dtanh(g, ld4g(t.e2 + j * H + 4 * c4));
+                         },
+                         [&](int r, int c4, float4 v) {
+                             if (okrow(r)) st4g(tr.de2_pre + (row0 + r) * H + 4 * c4, v);
+                         });
+    __syncthreads();
+    f32x16 acc[RT][CT];
+    constexpr float iSW = 1.f / X3_SW;
+    mfma_layer_x3<H>(X, reinterpret_cast<const uint4*>(tr.w_e2tp), acc, wave, lane);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+        const int i = acc_i(rt, lane);
+        if (!okrow(i)) continue;
+        const float sc = RS[i] * iSW;
+#pragma unroll
+        for (int c = 0; c < CT; ++c)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int n0 = acc_n0<H>(wave, c, g, lane);
+                st4g(tr.de1_pre + (row0 + i) * H + n0,
+                     f4_dtanh(f4_scale(acc4(acc[rt][c], g), sc), ld4g(tr.e1 + (row0 + i) * H + n0)));
+            }
+    }
+    (void)RMX;
+}
+
+}  // namespace pol
+}  // namespace qs
+
+namespace qs {
+namespace pol {
+
+// ------------------------------------------------------------------------------------------------------------------
+// weight gradients: part[b] = G[rows of b]^T A[rows of b] (split-K over the B K rows; torch sums the parts)
+// G: [R, H] pre-activation gradients with a power-of-two scale per column (gs[n], |G[:, n]| gs[n] < 2^14: the
+// column's scale factors out of dW[n, :]); A: [R, H] tanh outputs (|a| <= 1, scale X3_SX).  Both split into f16
+// hi / lo, three MFMAs per product as mfma_layer_x3.  A block's 16-row step: the 16 x H tiles of G and A staged
+// TRANSPOSED in LDS ([n][r] / [k][r], 16 r + 8 padding halves per row), so that a lane's MFMA operand -- 8 consecutive
+// rows r of one column -- is one ds_read_b128; wave w owns output rows n in [w H/4, (w+1) H/4), all H columns k.
+// The next step's rows are loaded into registers while the current step's MFMAs run (double-buffered tiles).
+// ------------------------------------------------------------------------------------------------------------------
+constexpr int DW_STEP = 16, DW_LDR = DW_STEP + 8;   // rows per step; LDS row stride in halves (48 B)
+
+template <int H>
+constexpr size_t dw_lds_bytes() { return (size_t)2 * 4 * H * DW_LDR * 2; }   // 2 buffers x {Gh, Gl, Ah, Al}
+
+template <int H>
+__global__ __launch_bounds__(NTHR, 1) void dw_x3_kernel(const float* __restrict__ G, const float* __restrict__ A,
+                                                        const float* __restrict__ gs, long R, int steps_per_block,
+                                                        float* __restrict__ part) {
+    constexpr int NT = H / 128, KT = H / 32, L4 = H / 4, NITEM = L4 * (DW_STEP / 4);
+    constexpr int IPT = (NITEM + NTHR - 1) / NTHR;   // staging items per thread: (column quad, row quad)
+    extern __shared__ float4 smem4[];
+    _Float16* lds = reinterpret_cast<_Float16*>(smem4);
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const long r_begin = (long)blockIdx.x * steps_per_block * DW_STEP;
+    auto buf = [&](int b, int which) { return lds + ((size_t)b * 4 + which) * H * DW_LDR; };   // 0 Gh 1 Gl 2 Ah 3 Al
+    float4 gv[IPT][4], av[IPT][4];
+    auto load = [&](int s) {
+#pragma unroll
+        for (int it = 0; it < IPT; ++it) {
+            const int e = tid + it * NTHR;
+            const int n4 = e % L4, rq = e / L4;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const long r = r_begin + (long)s * DW_STEP + 4 * rq + u;
+                const bool ok = e < NITEM && r < R && s < steps_per_block;
+                const long rr = ok ? r : 0;
+                const float okf = ok ? 1.f : 0.f;
+                const float4 g = *reinterpret_cast<const float4*>(G + rr * H + 4 * n4);
+                const float4 a = *reinterpret_cast<const float4*>(A + rr * H + 4 * n4);
+                gv[it][u] = make_float4(g.x * okf, g.y * okf, g.z * okf, g.w * okf);
+                av[it][u] = make_float4(a.x * okf, a.y * okf, a.z * okf, a.w * okf);
+            }
+        }
+    };
+    typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+    auto stage = [&](int b) {
+#pragma unroll
+        for (int it = 0; it < IPT; ++it) {
+            const int e = tid + it * NTHR;
+            if (e >= NITEM) continue;
+            const int n4 = e % L4, rq = e / L4;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {   // column 4 n4 + c: its 4 rows as one 8-byte write per half
+                const int n = 4 * n4 + c;
+                const float sg = gs[n];
+                float g4[4], a4[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) { g4[u] = sg * f4at(gv[it][u], c); a4[u] = X3_SX * f4at(av[it][u], c); }
+                const f16x4 gh = {(_Float16)g4[0], (_Float16)g4[1], (_Float16)g4[2], (_Float16)g4[3]};
+                const f16x4 gl = {(_Float16)(g4[0] - (float)gh[0]), (_Float16)(g4[1] - (float)gh[1]),
+                                  (_Float16)(g4[2] - (float)gh[2]), (_Float16)(g4[3] - (float)gh[3])};
+                const f16x4 ah = {(_Float16)a4[0], (_Float16)a4[1], (_Float16)a4[2], (_Float16)a4[3]};
+                const f16x4 al = {(_Float16)(a4[0] - (float)ah[0]), (_Float16)(a4[1] - (float)ah[1]),
+                                  (_Float16)(a4[2] - (float)ah[2]), (_Float16)(a4[3] - (float)ah[3])};
+                const int off = n * DW_LDR + 4 * rq;
+                *reinterpret_cast<f16x4*>(buf(b, 0) + off) = gh;
+                *reinterpret_cast<f16x4*>(buf(b, 1) + off) = gl;
+                *reinterpret_cast<f16x4*>(buf(b, 2) + off) = ah;
+                *reinterpret_cast<f16x4*>(buf(b, 3) + off) = al;
+            }
+        }
+    };
+    f32x16 acc[NT][KT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int k = 0; k < KT; ++k)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[t][k][r] = 0.f;
+    const int aoff = (lane & 31) * DW_LDR + (lane >> 5) * 8;
+    load(0);
+    stage(0);
+    __syncthreads();
+    for (int s = 0; s < steps_per_block; ++s) {
+        const int b = s & 1;
+        if (s + 1 < steps_per_block) load(s + 1);   // next rows in flight during this step's MFMAs
+        f16x8 gh[NT], gl[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const int n0 = (wave * NT + t) * 32;
+            gh[t] = *reinterpret_cast<const f16x8*>(buf(b, 0) + n0 * DW_LDR + aoff);
+            gl[t] = *reinterpret_cast<const f16x8*>(buf(b, 1) + n0 * DW_LDR + aoff);
+        }
+#pragma unroll
+        for (int k = 0; k < KT; ++k) {
+            const f16x8 ah = *reinterpret_cast<const f16x8*>(buf(b, 2) + k * 32 * DW_LDR + aoff);
+            const f16x8 al = *reinterpret_cast<const f16x8*>(buf(b, 3) + k * 32 * DW_LDR + aoff);
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                acc[t][k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(gh[t], ah, acc[t][k], 0, 0, 0);
+                acc[t][k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(gl[t], ah, acc[t][k], 0, 0, 0);
+                acc[t][k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(gh[t], al, acc[t][k], 0, 0, 0);
+            }
+        }
+        if (s + 1 < steps_per_block) stage(b ^ 1);   // the other buffer: last read two steps ago (barrier below)
+        __syncthreads();
+    }
+    // acc[t][k] register 4g + j: output row n = (wave NT + t) 32 + (lane & 31), column k 32 + 8 g + 4 (lane >> 5) + j
+    float* out = part + (size_t)blockIdx.x * H * H;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const int n = (wave * NT + t) * 32 + (lane & 31);
+        const float inv = 1.f / (gs[n] * X3_SX);
+#pragma unroll
+        for (int k = 0; k < KT; ++k)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int col = k * 32 + 8 * g + 4 * (lane >> 5);
+                *reinterpret_cast<float4*>(out + (size_t)n * H + col) =
+                    make_float4(acc[t][k][4 * g] * inv, acc[t][k][4 * g + 1] * inv, acc[t][k][4 * g + 2] * inv,
+                                acc[t][k][4 * g + 3] * inv);
+            }
+    }
+}
+
+}  // namespace pol
+}  // namespace qs

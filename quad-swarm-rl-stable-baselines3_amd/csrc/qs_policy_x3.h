@@ -4,7 +4,9 @@
 // Same function, same two kernels, same block structure (64 neighbour rows per block, 4 waves, wave w owning
 // output columns [w H/4, (w+1) H/4)); what changes is the contraction.  Each fp32 operand x is carried as two
 // f16 values, hi = f16(s x) and lo = f16(s x - hi) with a power-of-two scale s (activations 2^8, raw obs 2^4,
-// weights 2^8: both halves stay normal f16 numbers), so x = (hi + lo) / s to 2^-22 relative, and
+// weights 2^8: the scale keeps hi normal for the values that matter; lo goes subnormal only where x itself is so
+// small that its lo half is below f16's normal range, i.e. where the dropped bits are below fp32's own rounding of
+// the products), so x = (hi + lo) / s to 2^-22 relative, and
 //   x . w = (hi_x hi_w + hi_x lo_w + lo_x hi_w) / (s_x s_w)   (+ the dropped lo_x lo_w, < 2^-22 relative)
 // with every f16 x f16 product exact in the fp32 accumulator (11 + 11 bits).  Three v_mfma_f32_32x32x16_f16 per
 // 32 x 32 x 16 step replace eight v_mfma_f32_32x32x2f32 (32 vs 64 cycles each): 5.3x the fp32 matrix rate at a
@@ -27,6 +29,9 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 constexpr float X3_SX = 256.f;        // activation scale (tanh outputs, e2 rows)
 constexpr float X3_SIN = 16.f;        // raw observation scale (layer 0 inputs)
 constexpr float X3_SW = 256.f;        // weight scale (policy_fused.pack_mfma_weight_x3)
+// range: f16 overflows at 65504, i.e. |w| >= 65504 / X3_SW = 255.9 or |obs| >= 65504 / X3_SIN = 4094 would become
+// +-inf.  tanh outputs are < 1; policy_fused checks the weights at every refresh (and packs fp32 if any is out of
+// range) and the observations it was given once per rollout (FusedRolloutPolicy.check_inputs).
 
 template <int KD>
 struct GeoX3 {

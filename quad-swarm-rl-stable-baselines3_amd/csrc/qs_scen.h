@@ -387,9 +387,282 @@ __device__ void scen_step(const KP& kp, Scen& s, int tick, SDraw& sd, float* g, 
     }
 }
 
-// LDS goal tables of the env (2 x (NPAD + 4) rows of 4 floats), after the obs / exchange tiles
+// ---------------------------------------------------------------------------------------------
+// scenario.step() on every lane of the env at once (flavor-B step kernel).  scen_step above runs the
+// reference's loops over the env's drones on the env's lead lane while the env's other lanes wait; here every
+// lane runs the same scalar code (the same Philox words, the same formation scalars) and computes only its
+// own drone's goal: generate_goals' row of the drone (sc_row), the cube / grid centring by a running sum over
+// the rows (the same rows in the same order, the sums bitwise the lead lane's), and a Generator.shuffle as the
+// drone's row tracked through the swaps (sd_track) instead of swapping a table.  Bitwise the same goals and
+// scenario state as scen_step (and so oracle/quadswarm_oracle_scen.c draw for draw).
+// ---------------------------------------------------------------------------------------------
+
+// generate_goals' row i before the cube / grid centring (circle and sphere rows are final) -- sc_generate's
+// per-row expressions
+__device__ __forceinline__ void sc_row(int f, int n, int per_layer, float size, float layer, const float* c, int i,
+                                       float* gi) {
+    if (f <= F_CIRCLE_YZ) {
+        const int whole = n / per_layer, rest = n % per_layer;
+        const int cur = n <= per_layer ? n : ((i / per_layer) < whole ? per_layer : rest);
+        const float rev = (float)(i % cur) / (float)cur;
+        sc_by_formation(f, size * __builtin_amdgcn_cosf(rev), size * __builtin_amdgcn_sinf(rev),
+                        (float)(i / per_layer) * layer, gi);
+        gi[0] += c[0]; gi[1] += c[1]; gi[2] += c[2];
+    } else if (f == F_SPHERE) {
+        const int m = n < 3 ? 3 : n;
+        const float x = 0.1f + 1.2f * (float)m;
+        const float start = -1.f + 1.f / ((float)m - 1.f), inc = (2.f - 2.f / ((float)m - 1.f)) / ((float)m - 1.f);
+        const float s = start + (float)i * inc;
+        const float sg = s > 0.f ? 1.f : (s < 0.f ? -1.f : 0.f);
+        const float a = s * x, bb = 1.5707963267948966f * sg * (1.f - fsqrt(1.f - fabsf(s)));
+        const float cb = cos_any(bb);
+        gi[0] = size * (cos_any(a) * cb) + c[0];
+        gi[1] = size * (sin_any(a) * cb) + c[1];
+        gi[2] = size * sin_any(bb) + c[2];
+    } else if (f == F_CUBE) {
+        const int fd = n < 8 ? 1 : (n < 28 ? 2 : (n < 65 ? 3 : (n < 126 ? 4 : 5)));
+        gi[0] = c[2] + size * (float)(i / (fd * fd));
+        gi[1] = size * (float)((i / fd) % fd);
+        gi[2] = size * (float)(i % fd);
+    } else {
+        int d1, d2, r1 = 1, r2 = 1;
+        sc_grid_dims(n <= per_layer ? n : per_layer, d1, d2);
+        if (n > per_layer && n % per_layer) sc_grid_dims(n % per_layer, r1, r2);
+        const int whole = n / per_layer, L = i / per_layer;
+        const bool full = n <= per_layer || L < whole;
+        const int a = full ? d1 : r1, b2 = full ? d2 : r2;
+        sc_by_formation(f, size * (float)(i % b2), size * (float)((i / b2) % a), (float)L * layer, gi);
+    }
+}
+// sc_generate's row count (a sphere has at least 3 points)
+__device__ __forceinline__ int sc_count(int f, int n) { return (f == F_SPHERE && n < 3) ? 3 : n; }
+
+// the centring of cube / grid formations (sc_generate's mean): rows 0..n-1 summed in order, each row from
+// running counters (the divisions of sc_row only where a grid's last, partial layer starts)
+__device__ __forceinline__ void sc_center(int f, int n, int per_layer, float size, float layer, const float* c,
+                                          float* gi) {
+    if (f <= F_CIRCLE_YZ || f == F_SPHERE) return;
+    float mean[3] = {0.f, 0.f, 0.f};
+    if (f == F_CUBE) {
+        const int fd = n < 8 ? 1 : (n < 28 ? 2 : (n < 65 ? 3 : (n < 126 ? 4 : 5)));
+        int u = 0, v = 0, w = 0;   // j % fd, (j / fd) % fd, j / fd^2
+        for (int j = 0; j < n; ++j) {
+            float gj[3];   // sc_row's cube row j, one statement per coordinate as there (same contraction)
+            gj[0] = c[2] + size * (float)w;
+            gj[1] = size * (float)v;
+            gj[2] = size * (float)u;
+            mean[0] += gj[0]; mean[1] += gj[1]; mean[2] += gj[2];
+            if (++u == fd) { u = 0; if (++v == fd) { v = 0; ++w; } }
+        }
+    } else {
+        int d1, d2, r1 = 1, r2 = 1;
+        sc_grid_dims(n <= per_layer ? n : per_layer, d1, d2);
+        if (n > per_layer && n % per_layer) sc_grid_dims(n % per_layer, r1, r2);
+        const int whole = n / per_layer;
+        int L = 0, jl = 0, a = d1, b2 = d2, u = 0, v = 0;   // layer, index in layer, j % b2, (j / b2) % a
+        for (int j = 0; j < n; ++j) {
+            if (jl == per_layer) {
+                ++L;
+                jl = 0;
+                const bool full = n <= per_layer || L < whole;
+                a = full ? d1 : r1;
+                b2 = full ? d2 : r2;
+                u = j % b2;
+                v = (j / b2) % a;
+            }
+            float gj[3];
+            sc_by_formation(f, size * (float)u, size * (float)v, (float)L * layer, gj);
+            mean[0] += gj[0]; mean[1] += gj[1]; mean[2] += gj[2];
+            ++jl;
+            if (++u == b2) { u = 0; if (++v == a) v = 0; }
+        }
+    }
+    for (int k = 0; k < 3; ++k) mean[k] /= (float)n;
+    for (int k = 0; k < 3; ++k) gi[k] = gi[k] - mean[k] + c[k];
+}
+
+// where row `pos` of an n-row table ends after sd_shuffle (Fisher-Yates from the top), consuming the same words
+__device__ __forceinline__ int sd_track(SDraw& s, int pos, int n) {
+    for (int i = n - 1; i >= 1; --i) {
+        const int j = sd_int(s, 0, i + 1);
+        pos = pos == i ? j : (pos == j ? i : pos);
+    }
+    return pos;
+}
+
+// does scenario.step() change anything at this tick (scen_step's branches)
+__device__ __forceinline__ bool scen_acts(const KP& kp, int mode, int period, int tick) {
+    const bool ev = period > 0 && tick % period == 0 && tick > 0;
+    switch (mode) {
+        case SC_DYNAMIC_SAME_GOAL: case SC_DYNAMIC_DIFF_GOAL: case SC_SWAP_GOALS: case SC_SWARM_VS_SWARM: return ev;
+        case SC_RUN_AWAY: return tick % (int)(1.f * (1.f / kp.cdt)) == 0 && tick > 0 && kp.N >= 2;
+        case SC_EP_LISSAJOUS3D: case SC_EP_RAND_BEZIER: case SC_DYNAMIC_FORMATIONS: return true;
+        default: return false;
+    }
+}
+
+// the scenario record of an env as 27 words (scen_load's fields): 0-3 mode, form, period, inc (env rows
+// QS_E_SC_MODE..); 4-26 the env_f rows QS_ENVF_SC_SIZE.. (size lo hi layer speed c[3] bz[9] c1[3] c2[3])
+constexpr int SC_WORDS = 27;
+__device__ __forceinline__ uint32_t scen_word(const KP& kp, const Bufs& b, int env, int w) {
+    return w < 4 ? (uint32_t)b.env[(QS_E_SC_MODE + w) * kp.E + env]
+                 : __float_as_uint(b.envf[(QS_ENVF_SC_SIZE + w - 4) * kp.E + env]);
+}
+__device__ __forceinline__ void scen_from_words(const uint32_t* r, Scen& s) {
+    s.mode = (int)r[0]; s.form = (int)r[1]; s.period = (int)r[2]; s.inc = (int)r[3];
+    s.size = __uint_as_float(r[4]); s.lo = __uint_as_float(r[5]); s.hi = __uint_as_float(r[6]);
+    s.layer = __uint_as_float(r[7]); s.speed = __uint_as_float(r[8]);
+    for (int i = 0; i < 3; ++i) {
+        s.c[i] = __uint_as_float(r[9 + i]);
+        s.c1[i] = __uint_as_float(r[21 + i]);
+        s.c2[i] = __uint_as_float(r[24 + i]);
+    }
+    for (int i = 0; i < 9; ++i) s.bz[i] = __uint_as_float(r[12 + i]);
+}
+
+// scen_step for drone di's lane.  ta: the env's goals (rows of 4 floats) as the step left them (read by the modes
+// that use other drones' goals); tb: the shuffled goals (the shuffling modes write their drones' rows there and
+// set via_tab: the new goal is tb's row di after a barrier).  goal: in, the drone's goal; out, its new goal.
+// Returns what of the scenario record changed: 0 nothing, 1 size / inc / speed, 2 more (the whole record).
+__device__ __forceinline__ int scen_step_lane(const KP& kp, Scen& s, int tick, SDraw& sd, int di, const float* ta,
+                                              float* tb, float* goal, bool& via_tab) {
+    const int N = sc_num(kp);
+    const float box = kp.spawn_box, cf = 1.f / kp.cdt;
+    const int pl = sc_per_layer(s.form);
+    const bool ev = s.period > 0 && tick % s.period == 0 && tick > 0;
+    via_tab = false;
+    if (s.mode == SC_DYNAMIC_SAME_GOAL) {   // dynamic_same_goal.py:16-29
+        if (!ev) return 0;
+        const float x = sd_uniform(sd, -box, box), y = sd_uniform(sd, -box, box);
+        const float z = fmaxf(sd_uniform(sd, -0.5f * box, 0.5f * box) + 2.f, 0.25f);
+        s.c[0] = x; s.c[1] = y; s.c[2] = z;
+        sc_row(s.form, N, pl, s.size, 0.f, s.c, di, goal);
+        sc_center(s.form, N, pl, s.size, 0.f, s.c, goal);
+        return 2;
+    } else if (s.mode == SC_DYNAMIC_DIFF_GOAL) {   // dynamic_diff_goal.py:13-40
+        if (!ev) return 0;
+        const float x = sd_uniform(sd, -box, box), y = sd_uniform(sd, -box, box);
+        const float z = sc_z_value(kp, s, sd);
+        s.c[0] = x; s.c[1] = y; s.c[2] = z;
+        sc_update_formation(kp, s, sd);
+        const int f = s.form, pl2 = sc_per_layer(f), m = sc_count(f, N);
+        const SDraw s0 = sd;   // the shuffle's words, for every row of the generated table
+        for (int r = di; r < m; r += N) {
+            float gr[3];
+            sc_row(f, N, pl2, s.size, s.layer, s.c, r, gr);
+            sc_center(f, N, pl2, s.size, s.layer, s.c, gr);
+            SDraw t = s0;
+            const int p = sd_track(t, r, m);
+            if (p < N) { tb[4 * p] = gr[0]; tb[4 * p + 1] = gr[1]; tb[4 * p + 2] = gr[2]; }
+        }
+        via_tab = true;
+        return 2;
+    } else if (s.mode == SC_SWAP_GOALS) {   // swap_goals.py:12-25
+        if (!ev) return 0;
+        const int p = sd_track(sd, di, N);
+        tb[4 * p] = goal[0]; tb[4 * p + 1] = goal[1]; tb[4 * p + 2] = goal[2];
+        via_tab = true;
+        return 0;
+    } else if (s.mode == SC_DYNAMIC_FORMATIONS) {   // dynamic_formations.py:18-40
+        if (s.size <= -s.hi) {
+            s.inc = 1;
+            s.speed = sd_uniform(sd, 1.f, 3.f);
+        } else if (s.size >= s.hi) {
+            s.inc = 0;
+            s.speed = sd_uniform(sd, 1.f, 3.f);
+        }
+        s.size += (s.inc ? 0.001f : -0.001f) * s.speed;
+        sc_row(s.form, N, pl, s.size, s.layer, s.c, di, goal);
+        sc_center(s.form, N, pl, s.size, s.layer, s.c, goal);
+        return 1;
+    } else if (s.mode == SC_EP_LISSAJOUS3D) {   // ep_lissajous3D.py:8-26 (accumulates on goals[0])
+        const float t = (float)tick / cf;
+        const float nx = 0.03f * sin_any(t) + ta[0], ny = 0.01f * sin_any(2.f * t + 90.f) + ta[1],
+                    nz = 0.01f * cos_any(2.f * t + 90.f) + ta[2];
+        goal[0] = nx; goal[1] = ny; goal[2] = nz;
+        return 0;
+    } else if (s.mode == SC_EP_RAND_BEZIER) {   // ep_rand_bezier.py:6-47
+        const int steps = (int)(5.f * cf);
+        const int t = tick % steps;
+        float rd[3], hi[3], lo[3];
+        for (int k = 0; k < 3; ++k) rd[k] = kp.room_hi[k] - kp.room_lo[k] - s.size;
+        const float mx = fminf(fmaxf(fmaxf(rd[0], rd[1]), rd[2]), 30.f);
+        hi[0] = rd[0] * 0.5f; hi[1] = rd[1] * 0.5f; hi[2] = rd[2];
+        lo[0] = -hi[0]; lo[1] = -hi[1]; lo[2] = 0.f;
+        int ch = 0;
+        if (t == 0 || tick == 1) {
+            float np_[3][2];
+            for (int tries = 0;; ++tries) {   // uniform(size=(2, 3)).reshape(3, 2): [c][j] = flat 2c + j
+                float u[6];
+                for (int k = 0; k < 6; ++k) u[k] = sd_uniform(sd, -hi[k % 3], hi[k % 3]);
+                const float mag = (float)sd_int(sd, (int)ceilf(mx * 0.5f), (int)floorf(mx) + 1);
+                bool ok = true;
+                for (int j = 0; j < 2; ++j) {
+                    const float v0 = u[j], v1 = u[2 + j], v2 = u[4 + j];
+                    const float sc = mag / fsqrt(v0 * v0 + v1 * v1 + v2 * v2);
+                    np_[0][j] = v0 * sc + ta[0]; np_[1][j] = v1 * sc + ta[1]; np_[2][j] = v2 * sc + ta[2];
+                    for (int k = 0; k < 3; ++k) ok = ok && np_[k][j] > lo[k] + 0.5f && np_[k][j] < hi[k] - 0.5f;
+                }
+                if (ok || tries >= 1023) break;   // the reference loops without a bound
+            }
+            for (int k = 0; k < 3; ++k) {
+                s.bz[k] = ta[k];
+                s.bz[3 + k] = np_[k][0];
+                s.bz[6 + k] = np_[k][1];
+            }
+            ch = 2;
+        }
+        if (t != 0 && tick > 1) {   // interp[:, t] of the degree-2 Bezier (bezier's Bernstein evaluation)
+            const float sp = t == steps - 1 ? 1.f : (float)t * (1.f / (float)(steps - 1));
+            const float l1 = 1.f - sp;
+            for (int k = 0; k < 3; ++k) goal[k] = (l1 * s.bz[k] + 2.f * sp * s.bz[3 + k]) * l1 + sp * sp * s.bz[6 + k];
+        }
+        return ch;
+    } else if (s.mode == SC_SWARM_VS_SWARM) {   // swarm_vs_swarm.py:56-76 (sc_vs_formations with the shuffles)
+        if (!ev) return 0;
+        for (int k = 0; k < 3; ++k) {
+            const float t3 = s.c1[k];
+            s.c1[k] = s.c2[k];
+            s.c2[k] = t3;
+        }
+        sc_update_formation(kp, s, sd);
+        const int f = s.form, pl2 = sc_per_layer(f);
+        const int h1 = N / 2, h2 = N - N / 2, m1 = sc_count(f, h1), m2 = sc_count(f, h2);
+        for (int rr = di; rr < m1 + m2; rr += N) {   // group 1's rows, then group 2's
+            const bool g2 = rr >= m1;
+            const int r = g2 ? rr - m1 : rr, n = g2 ? h2 : h1;
+            const float* cc = g2 ? s.c2 : s.c1;
+            float gr[3];
+            sc_row(f, n, pl2, s.size, s.layer, cc, r, gr);
+            sc_center(f, n, pl2, s.size, s.layer, cc, gr);
+            SDraw t = sd;
+            if (g2) t.k += (uint32_t)(m1 - 1);   // group 1's shuffle words come first
+            const int p = sd_track(t, r, g2 ? m2 : m1);
+            const int slot = g2 ? m1 + p : p;
+            if (slot < N) { tb[4 * slot] = gr[0]; tb[4 * slot + 1] = gr[1]; tb[4 * slot + 2] = gr[2]; }
+        }
+        via_tab = true;
+        return 2;
+    } else if (s.mode == SC_RUN_AWAY) {   // run_away.py:16-27
+        if (tick % (int)(1.f * cf) == 0 && tick > 0 && N >= 2) {
+            const int a = sd_int(sd, 1, N), b2 = sd_int(sd, 1, N);
+            const int src = di == 0 ? a : b2;
+            if (di < 2) { goal[0] = ta[4 * src]; goal[1] = ta[4 * src + 1]; goal[2] = ta[4 * src + 2]; }
+        }
+        return 0;
+    }
+    return 0;
+}
+__device__ __forceinline__ void scen_store_size(const KP& kp, const Bufs& b, int env, const Scen& s) {
+    b.env[QS_E_SC_INC * kp.E + env] = s.inc;
+    b.envf[QS_ENVF_SC_SIZE * kp.E + env] = s.size;
+    b.envf[QS_ENVF_SC_SPEED * kp.E + env] = s.speed;
+}
+
+// LDS goal tables of the env (2 x (NPAD + 4) rows of 4 floats), after the obs / exchange tiles, then the env's
+// scenario record (SC_WORDS words, padded to 32; the flavor-B step kernel's copy for scen_step_lane)
 template <int NPAD>
-constexpr int scen_stride() { return 2 * (NPAD + 4) * 4; }
+constexpr int scen_stride() { return 2 * (NPAD + 4) * 4 + 32; }
 __device__ __forceinline__ float* scen_tab(float* lds, const KP& kp, int slots) {
     return lds + slots * kp.obs_dim + slots * 8 + 64;
 }

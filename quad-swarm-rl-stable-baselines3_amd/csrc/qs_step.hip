@@ -38,6 +38,7 @@
 #include "qs_flavor_a.h"
 #include "qs_gae.h"
 #include "qs_curriculum.h"
+#include "qs_policy_train.h"
 #include "qs_policy.h"
 #include "qs_policy_x3.h"
 #include "qs_replay.h"
@@ -169,7 +170,7 @@ static int validate(const qs_config* c) {
         if (c->scenario == QS_SCEN_RUN_AWAY && c->num_agents < 2)
             return fail(QS_E_INVALID, "run_away needs at least 2 drones (run_away.py:16-27)");
         if (c->ticks_per_step < 1) return fail(QS_E_INVALID, "ticks_per_step must be >= 1");
-        if (c->n_cameras < 1) return fail(QS_E_INVALID, "n_cameras must be >= 1");
+        if (c->n_cameras < 1 || c->n_cameras > 8) return fail(QS_E_INVALID, "n_cameras must be 1..8");
         // envs of more than 64 drones (multi-wave workgroups) select their neighbours by register insertion
         // (qs_flavor_a.h neighbor_obs_wide)
         if (c->num_agents > 64 && c->neighbor_obs != QS_NEIGHBOR_NONE && c->k_neighbors > QS_A_KMAX)
@@ -261,6 +262,13 @@ static void make_kp_a(const qs_config* c, qs::KP& k) {
     k.nfeat = neighbor_feats(c->neighbor_obs); k.nfd = neighbor_dim(c->neighbor_obs);
     k.n_cam = c->n_cameras;
     k.cam_r = 0.5f * c->cam_size; k.cam_f = c->cam_focal; k.cam_px = c->cam_px_noise; k.cam_res = c->cam_res;
+    {   // the camera axes of qs::camera's sector pick, in the kernel's float arithmetic (seg = 2 pi / n in fp32)
+        const float seg = 6.28318530717959f / (float)k.n_cam;
+        for (int i = 0; i < 8; ++i) {
+            k.cam_cos[i] = i < k.n_cam ? cosf((float)i * seg) : 1.f;
+            k.cam_sin[i] = i < k.n_cam ? sinf((float)i * seg) : 0.f;
+        }
+    }
     k.cam_w = (float)(2.0 * tan((c->cam_fov_deg / 2.0) * PI / 180.0) * c->cam_focal);
     k.hrate = (float)((double)c->dt * (PI * 80.0 / 180.0));
     k.speed = 0.2f;
@@ -1132,6 +1140,113 @@ extern "C" int qs_attn_pool(int32_t B, int32_t K, int32_t H, const qs_attn_tower
 extern "C" int qs_attn_pool_x3(int32_t B, int32_t K, int32_t H, const qs_attn_tower* towers, int32_t n_towers,
                                void* stream) {
     return attn_pool_impl(B, K, H, towers, n_towers, stream, true);
+}
+
+// the PPO update's attention encoder (qs_policy_train.h)
+enum { TR_EMBED, TR_POOL, TR_BWD1, TR_BWD2 };
+template <int H>
+static int attn_train_launch(int what, const float* obs, int32_t stride, int32_t so, int32_t off, int32_t B, int32_t K,
+                             int32_t nd, const qs::pol::Towers& tw, const qs::pol::Trains& trs, int32_t n_towers,
+                             hipStream_t st) {
+    namespace P = qs::pol;
+    const int mu = (P::MROWS / K) * K;
+    const dim3 grid((unsigned)(((long long)B * K + mu - 1) / mu), (unsigned)n_towers), block(P::NTHR);
+    size_t lds = 0;
+    const void* fn = nullptr;
+    switch (what) {
+        case TR_EMBED: lds = P::embed_x3_lds_bytes<H>(); fn = (const void*)P::attn_embed_train_x3_kernel<H>; break;
+        case TR_POOL: lds = P::pool_x3_lds_bytes<H>(); fn = (const void*)P::attn_pool_train_x3_kernel<H>; break;
+        case TR_BWD1: lds = P::bwd_fixed_lds_bytes<H>() + (size_t)(P::MROWS / K) * H * 4; fn = (const void*)P::attn_bwd1_x3_kernel<H>; break;
+        default: lds = P::bwd_fixed_lds_bytes<H>(); fn = (const void*)P::attn_bwd2_x3_kernel<H>; break;
+    }
+    QS_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    switch (what) {
+        case TR_EMBED:
+            hipLaunchKernelGGL(P::attn_embed_train_x3_kernel<H>, grid, block, lds, st, obs, stride, so, off, B, K, nd, tw, trs);
+            break;
+        case TR_POOL: hipLaunchKernelGGL(P::attn_pool_train_x3_kernel<H>, grid, block, lds, st, B, K, tw, trs); break;
+        case TR_BWD1: hipLaunchKernelGGL(P::attn_bwd1_x3_kernel<H>, grid, block, lds, st, B, K, tw, trs); break;
+        default: hipLaunchKernelGGL(P::attn_bwd2_x3_kernel<H>, grid, block, lds, st, B, K, tw, trs); break;
+    }
+    QS_HIP(hipGetLastError());
+    return QS_OK;
+}
+static int attn_train_impl(int what, const float* obs, int32_t stride, int32_t so, int32_t off, int32_t B, int32_t K,
+                           int32_t nd, int32_t H, const qs_attn_tower* towers, const qs_attn_train* trains,
+                           int32_t n_towers, void* stream) {
+    int rc = attn_check(B, K, H, towers, n_towers);
+    if (rc) return rc;
+    if (!trains) return fail(QS_E_INVALID, "NULL trains");
+    if (what == TR_EMBED) {
+        if (!obs) return fail(QS_E_INVALID, "NULL obs");
+        if (nd < 1 || nd > qs::pol::MAX_ND) return fail(QS_E_INVALID, "features per neighbour must be 1..16");
+        if (so < 1 || so > stride) return fail(QS_E_INVALID, "self features must lie inside the obs row");
+        if (nd + so > qs::pol::KD0) return fail(QS_E_INVALID, "self + neighbour features must be <= 32");
+        if (off < 0 || off + K * nd > stride) return fail(QS_E_INVALID, "neighbour block outside the obs row");
+    }
+    qs::pol::Towers tw{};
+    qs::pol::Trains trs{};
+    for (int i = 0; i < n_towers; ++i) {
+        const qs_attn_tower& t = towers[i];
+        const qs_attn_train& r = trains[i];
+        bool ok = true;
+        switch (what) {
+            case TR_EMBED: ok = t.w_e1p && t.b_e1 && t.w_e2p && t.b_e2 && t.e2 && t.e_mean && r.e1; break;
+            case TR_POOL:
+                ok = t.e2 && t.P && t.w_v1p && t.b_v1 && t.w_v2p && t.b_v2 && t.w_a1ep && t.w_a2p && t.b_a2 && t.w_a3 &&
+                     t.out && r.a1 && r.a2 && r.v1 && r.h && r.w;
+                break;
+            case TR_BWD1:
+                ok = t.w_a3 && r.w && r.h && r.v1 && r.a1 && r.a2 && r.dout && r.w_v2tp && r.w_v1tp && r.w_a2tp &&
+                     r.w_a1etp && r.dh_pre && r.dv1_pre && r.da2_pre && r.da1_pre && r.dscore && r.de2p;
+                break;
+            default: ok = t.e2 && r.e1 && r.de2p && r.dem && r.w_e2tp && r.de2_pre && r.de1_pre; break;
+        }
+        if (!ok) return fail(QS_E_INVALID, "NULL tower / train pointer for this stage");
+        tw.t[i] = t;
+        trs.t[i] = r;
+    }
+    hipStream_t st = (hipStream_t)stream;
+    return H == 256 ? attn_train_launch<256>(what, obs, stride, so, off, B, K, nd, tw, trs, n_towers, st)
+                    : attn_train_launch<128>(what, obs, stride, so, off, B, K, nd, tw, trs, n_towers, st);
+}
+extern "C" int qs_attn_embed_train_x3(const float* obs, int32_t obs_stride, int32_t self_dim, int32_t nbr_off, int32_t B,
+                                      int32_t K, int32_t nd, int32_t H, const qs_attn_tower* towers,
+                                      const qs_attn_train* trains, int32_t n_towers, void* stream) {
+    return attn_train_impl(TR_EMBED, obs, obs_stride, self_dim, nbr_off, B, K, nd, H, towers, trains, n_towers, stream);
+}
+extern "C" int qs_attn_pool_train_x3(int32_t B, int32_t K, int32_t H, const qs_attn_tower* towers,
+                                     const qs_attn_train* trains, int32_t n_towers, void* stream) {
+    return attn_train_impl(TR_POOL, nullptr, 0, 0, 0, B, K, 0, H, towers, trains, n_towers, stream);
+}
+extern "C" int qs_attn_bwd1_x3(int32_t B, int32_t K, int32_t H, const qs_attn_tower* towers,
+                               const qs_attn_train* trains, int32_t n_towers, void* stream) {
+    return attn_train_impl(TR_BWD1, nullptr, 0, 0, 0, B, K, 0, H, towers, trains, n_towers, stream);
+}
+template <int H>
+static int dw_launch(const float* G, const float* A, const float* gs, int64_t R, float* part, int32_t n_parts,
+                     hipStream_t st) {
+    namespace P = qs::pol;
+    const long long rows_per = (R + n_parts - 1) / n_parts;
+    const int steps = (int)((rows_per + P::DW_STEP - 1) / P::DW_STEP);
+    const size_t lds = P::dw_lds_bytes<H>();
+    QS_HIP(hipFuncSetAttribute((const void*)P::dw_x3_kernel<H>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(P::dw_x3_kernel<H>, dim3((unsigned)n_parts), dim3(P::NTHR), lds, st, G, A, gs, (long)R, steps, part);
+    QS_HIP(hipGetLastError());
+    return QS_OK;
+}
+extern "C" int qs_attn_dw_x3(const float* G, const float* A, const float* col_scale, int64_t R, int32_t H, float* part,
+                             int32_t n_parts, void* stream) {
+    if (!G || !A || !col_scale || !part) return fail(QS_E_INVALID, "NULL argument");
+    if (H != 128 && H != 256) return fail(QS_E_INVALID, "hidden size must be 128 or 256");
+    if (R < 1 || n_parts < 1 || n_parts > 65535 || R * (int64_t)H >= (1ll << 40))
+        return fail(QS_E_INVALID, "R >= 1, 1 <= n_parts <= 65535");
+    hipStream_t st = (hipStream_t)stream;
+    return H == 256 ? dw_launch<256>(G, A, col_scale, R, part, n_parts, st) : dw_launch<128>(G, A, col_scale, R, part, n_parts, st);
+}
+extern "C" int qs_attn_bwd2_x3(int32_t B, int32_t K, int32_t H, const qs_attn_tower* towers,
+                               const qs_attn_train* trains, int32_t n_towers, void* stream) {
+    return attn_train_impl(TR_BWD2, nullptr, 0, 0, 0, B, K, 0, H, towers, trains, n_towers, stream);
 }
 
 // the kernel parameter block a config produces (host only; runtime specialisation / diagnostics)

@@ -128,6 +128,13 @@ class QsAttnTower(ctypes.Structure):
                [("b_a3", F), ("out", ctypes.c_void_p)]
 
 
+class QsAttnTrain(ctypes.Structure):
+    """qs_attn_train (the PPO update's saved activations and gradients of one tower, quadswarm.h)."""
+    _fields_ = [(n, ctypes.c_void_p) for n in ("e1", "a1", "a2", "v1", "h", "w", "dout", "dem", "w_v2tp", "w_v1tp",
+                                                "w_a2tp", "w_a1etp", "w_e2tp", "dh_pre", "dv1_pre", "da2_pre", "da1_pre",
+                                                "dscore", "de2p", "de2_pre", "de1_pre")]
+
+
 CUR_MAX_WINDOW = CUR_MAX_HIST = 64
 
 
@@ -151,7 +158,8 @@ EXPORTS = ["qs_abi_version", "qs_last_error", "qs_struct_sizes", "qs_config_defa
            "qs_specialize", "qs_is_specialized", "qs_config_kp_words", "qs_specialize_compile",
            "qs_replay_config_default", "qs_replay_workspace_bytes", "qs_replay_enable", "qs_replay_disable", "qs_replay_buffers_get",
            "qs_attn_embed", "qs_attn_pool", "qs_attn_embed_x3", "qs_attn_pool_x3", "qs_curriculum_init",
-           "qs_curriculum_step", "qs_curriculum_step_all"]
+           "qs_curriculum_step", "qs_curriculum_step_all", "qs_attn_embed_train_x3", "qs_attn_pool_train_x3",
+           "qs_attn_bwd1_x3", "qs_attn_bwd2_x3", "qs_attn_dw_x3"]
 
 _lib = None
 
@@ -193,6 +201,11 @@ def lib():
         "qs_curriculum_init": ([V, ctypes.c_double, ctypes.c_double, ctypes.c_double, I32], I32),
         "qs_curriculum_step": ([V, V, V], I32),
         "qs_curriculum_step_all": ([V, V, ctypes.c_int64, V, V], I32),
+        "qs_attn_embed_train_x3": ([V, I32, I32, I32, I32, I32, I32, I32, P(QsAttnTower), P(QsAttnTrain), I32, V], I32),
+        "qs_attn_pool_train_x3": ([I32, I32, I32, P(QsAttnTower), P(QsAttnTrain), I32, V], I32),
+        "qs_attn_bwd1_x3": ([I32, I32, I32, P(QsAttnTower), P(QsAttnTrain), I32, V], I32),
+        "qs_attn_bwd2_x3": ([I32, I32, I32, P(QsAttnTower), P(QsAttnTrain), I32, V], I32),
+        "qs_attn_dw_x3": ([V, V, V, ctypes.c_int64, I32, V, I32, V], I32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

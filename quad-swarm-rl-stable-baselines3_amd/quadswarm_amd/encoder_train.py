@@ -1,0 +1,218 @@
+"""The PPO update's attention neighbour encoders on the split-f16 matrix cores (the update side).
+
+PPO.train (as PPOTrainer.train restates it) evaluates ActorCriticPolicyCustomSeparateWeights on every minibatch with
+autograd (swarm_rl/models/ActorCriticPolicyCustom.py:538-566); 89 % of a C3 update is the two towers'
+QuadNeighborhoodEncoderAttention (swarm_rl/models/quad_multi_model.py:44-101): per neighbour row five H x H layers
+with tanh, forward and backward, ~20 hipBLASLt GEMMs and as many elementwise tanh / tanh-backward passes per tower.
+Here both towers' encoders are one autograd node (FusedAttentionTrain), whose forward and backward are the HIP
+kernels of csrc/qs_policy_train.h through the C ABI:
+
+  forward   qs_attn_embed_train_x3 (e1, e2, mean_K e2), torch P = mean A_m^T + b_a1, qs_attn_pool_train_x3 (a1, a2,
+            softmax, v1, h, pooled out) -- the rollout's x3 kernels plus the saved activations
+  backward  qs_attn_bwd1_x3: the value chain (dh_pre -> dv1_pre -> dL/de2) and the attention chain (dscore ->
+            da2_pre -> da1_pre -> dL/de2) of every 64-row block on the matrix cores, tanh derivatives in the epilogues;
+            torch: dP, dL/d e_mean (the grid-wide per-agent terms, [B, H]);
+            qs_attn_bwd2_x3: dL/de2 -> de2_pre -> de1_pre;
+            the weight gradients dW = grad^T act over the B K rows on the same split-f16 matrix cores (qs_attn_dw_x3:
+            split over row ranges, per-column power-of-two scales of the gradient, the parts summed by torch), the
+            biases as column sums, the small [B]-row terms (dA_m, the self half of layer 0) as torch GEMMs.
+Every contraction of the kernels is an fp32 product carried as three f16 products (hi/lo split, fp32 accumulation,
+~7e-7 relative per product; the backward's rows with their own power-of-two scales), i.e. fp32-equivalent; the
+gradients match the torch module's fp32 autograd within fp32 reassociation (tests/test_gpu_encoder_train.py).
+"""
+import ctypes
+
+import torch
+
+from . import _native as NAT
+from .policy_fused import pack_mfma_weight_x3, supports
+
+_PARAMS = ("e1_w", "e1_b", "e2_w", "e2_b", "v1_w", "v1_b", "v2_w", "v2_b", "a1_w", "a1_b", "a2_w", "a2_b", "a3_w", "a3_b")
+
+
+def tower_params(enc):
+    """The 14 parameters of one tower's NeighborAttention, in _PARAMS order."""
+    ne = enc.neighbor_encoder
+    emb, val, att = ne.embedding_mlp, ne.neighbor_value_mlp, ne.attention_mlp
+    return [emb[0].weight, emb[0].bias, emb[2].weight, emb[2].bias, val[0].weight, val[0].bias, val[2].weight,
+            val[2].bias, att[0].weight, att[0].bias, att[2].weight, att[2].bias, att[4].weight, att[4].bias]
+
+
+def col_scales(G):
+    """Per-column power-of-two scales of a gradient [R, H] for qs_attn_dw_x3: s_n |G[:, n]| in [2^13, 2^14) (1 for an
+    all-zero or non-finite column)."""
+    m = G.abs().amax(0)
+    _, e = torch.frexp(m)
+    s = torch.ldexp(torch.ones_like(m), (14 - e).to(torch.int32))
+    return torch.where((m > 0) & torch.isfinite(m), s, torch.ones_like(m)).contiguous()
+
+
+def dw_x3(G, A, parts=256, out=None):
+    """G^T A ([H, H]) over the rows of G, A [R, H] (|A| <= 1) on the split-f16 matrix cores (qs_attn_dw_x3), the row
+    range split over `parts` blocks and the parts summed here."""
+    R, H = G.shape
+    parts = max(1, min(parts, (R + 15) // 16))
+    buf = torch.empty(parts, H, H, dtype=torch.float32, device=G.device)
+    gs = col_scales(G)
+    st = ctypes.c_void_p(torch.cuda.current_stream(G.device).cuda_stream)
+    NAT.check(NAT.lib().qs_attn_dw_x3(ctypes.c_void_p(G.data_ptr()), ctypes.c_void_p(A.data_ptr()),
+                                      ctypes.c_void_p(gs.data_ptr()), R, H, ctypes.c_void_p(buf.data_ptr()), parts, st),
+              "qs_attn_dw_x3")
+    return torch.sum(buf, dim=0, out=out)
+
+
+class _Runner:
+    """Buffers and launches for one policy's towers (reused across minibatches of the same size)."""
+
+    def __init__(self, policy):
+        c = policy.cfg
+        self.H, self.K, self.nd, self.so = c.neighbor_hidden_size, c.num_use_neighbor_obs, c.neighbor_obs_dim, c.self_obs_dim
+        self.encs = (policy.actor_encoder, policy.critic_encoder)
+        self.T = len(self.encs)
+        self.L = NAT.lib()
+        self.B = None
+        self.towers = (NAT.QsAttnTower * NAT.ATTN_MAX_TOWERS)()
+        self.trains = (NAT.QsAttnTrain * NAT.ATTN_MAX_TOWERS)()
+        self.pending = False
+        self.dw_x3 = True   # the weight gradients on the split-f16 matrix cores (else torch fp32 GEMMs)
+
+    def dw(self, G, A):
+        """dW = G^T A over the B K rows (A: tanh outputs)."""
+        return dw_x3(G, A) if self.dw_x3 else G.t().mm(A)
+
+    def _alloc(self, B, dev):
+        H, T, R = self.H, self.T, B * self.K
+        z = lambda *s: torch.empty(*s, dtype=torch.float32, device=dev)  # noqa: E731
+        self.B = B
+        self.buf = [dict(e1=z(R, H), e2=z(R, H), a1=z(R, H), a2=z(R, H), v1=z(R, H), h=z(R, H), w=z(R),
+                         e_mean=z(B, H), P=z(B, H), out=z(B, H), dh_pre=z(R, H), dv1_pre=z(R, H), da2_pre=z(R, H),
+                         da1_pre=z(R, H), de2p=z(R, H), dscore=z(R), dem=z(B, H)) for _ in range(T)]
+
+    def _pack(self, params):
+        """x3-pack the towers' weights (forward operands and the backward's transposes), bind every pointer."""
+        H, so, nd = self.H, self.so, self.nd
+        p = lambda t: t.data_ptr()  # noqa: E731
+        self.keep = []
+        for i in range(self.T):
+            w = dict(zip(_PARAMS, params[14 * i:14 * i + 14]))
+            b = self.buf[i]
+            w_e1 = torch.zeros(H, 32, dtype=torch.float32, device=w["e1_w"].device)   # [neighbour | self | 0]
+            w_e1[:, :nd] = w["e1_w"][:, so:]
+            w_e1[:, nd:nd + so] = w["e1_w"][:, :so]
+            k = dict(w_e1p=pack_mfma_weight_x3(w_e1), w_e2p=pack_mfma_weight_x3(w["e2_w"]),
+                     w_v1p=pack_mfma_weight_x3(w["v1_w"]), w_v2p=pack_mfma_weight_x3(w["v2_w"]),
+                     w_a1ep=pack_mfma_weight_x3(w["a1_w"][:, :H]), w_a2p=pack_mfma_weight_x3(w["a2_w"]),
+                     w_v2tp=pack_mfma_weight_x3(w["v2_w"].t()), w_v1tp=pack_mfma_weight_x3(w["v1_w"].t()),
+                     w_a2tp=pack_mfma_weight_x3(w["a2_w"].t()), w_a1etp=pack_mfma_weight_x3(w["a1_w"][:, :H].t()),
+                     w_e2tp=pack_mfma_weight_x3(w["e2_w"].t()),
+                     b_e1=w["e1_b"].detach().contiguous(), b_e2=w["e2_b"].detach().contiguous(),
+                     b_v1=w["v1_b"].detach().contiguous(), b_v2=w["v2_b"].detach().contiguous(),
+                     b_a2=w["a2_b"].detach().contiguous(), w_a3=w["a3_w"].detach().reshape(-1).contiguous())
+            self.keep.append(k)
+            t = self.towers[i]
+            t.w_e1p, t.b_e1, t.w_e2p, t.b_e2 = p(k["w_e1p"]), p(k["b_e1"]), p(k["w_e2p"]), p(k["b_e2"])
+            t.e2, t.e_mean, t.P, t.out = p(b["e2"]), p(b["e_mean"]), p(b["P"]), p(b["out"])
+            t.w_v1p, t.b_v1, t.w_v2p, t.b_v2 = p(k["w_v1p"]), p(k["b_v1"]), p(k["w_v2p"]), p(k["b_v2"])
+            t.w_a1ep, t.w_a2p, t.b_a2, t.w_a3 = p(k["w_a1ep"]), p(k["w_a2p"]), p(k["b_a2"]), p(k["w_a3"])
+            t.b_a3 = float(w["a3_b"].detach().item())
+            r = self.trains[i]
+            for n in ("e1", "a1", "a2", "v1", "h", "w", "dh_pre", "dv1_pre", "da2_pre", "da1_pre", "dscore", "de2p", "dem"):
+                setattr(r, n, p(b[n]))
+            r.de2_pre = p(b["de2p"])      # in place: bwd2 reads de2p[j] and writes de2_pre[j] on the same lane
+            r.de1_pre = p(b["dh_pre"])    # dh_pre's last reader (dW_v2) runs before bwd2
+            for n in ("w_v2tp", "w_v1tp", "w_a2tp", "w_a1etp", "w_e2tp"):
+                setattr(r, n, p(k[n]))
+
+    def stream(self, dev):
+        return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+    @torch.no_grad()
+    def forward(self, obs, params):
+        B = obs.shape[0]
+        if self.B != B:
+            self._alloc(B, obs.device)
+        self._pack(params)
+        self.obs = obs
+        self.params = params
+        H, K, so, st = self.H, self.K, self.so, self.stream(obs.device)
+        NAT.check(self.L.qs_attn_embed_train_x3(ctypes.c_void_p(obs.data_ptr()), obs.shape[1], so, so, B, K, self.nd, H,
+                                                self.towers, self.trains, self.T, st), "qs_attn_embed_train_x3")
+        for i in range(self.T):
+            a1_w, a1_b = params[14 * i + 8], params[14 * i + 9]
+            torch.addmm(a1_b, self.buf[i]["e_mean"], a1_w[:, H:].t(), out=self.buf[i]["P"])
+        NAT.check(self.L.qs_attn_pool_train_x3(B, K, H, self.towers, self.trains, self.T, st), "qs_attn_pool_train_x3")
+        self.pending = True
+        return [self.buf[i]["out"].clone() for i in range(self.T)]
+
+    @torch.no_grad()
+    def backward(self, douts):
+        if not self.pending:
+            raise RuntimeError("FusedAttentionTrain: backward without a pending forward (buffers reused)")
+        B, H, K, so, nd = self.B, self.H, self.K, self.so, self.nd
+        obs, params = self.obs, self.params
+        st = self.stream(obs.device)
+        d = []
+        for i in range(self.T):
+            g = douts[i]
+            d.append(torch.zeros(B, H, device=obs.device) if g is None else g.contiguous())
+            self.trains[i].dout = d[i].data_ptr()
+        NAT.check(self.L.qs_attn_bwd1_x3(B, K, H, self.towers, self.trains, self.T, st), "qs_attn_bwd1_x3")
+        grads = [None] * (14 * self.T)
+        for i in range(self.T):
+            b, w0 = self.buf[i], 14 * i
+            gi = {}
+            gi["v2_w"], gi["v2_b"] = self.dw(b["dh_pre"], b["v1"]), b["dh_pre"].sum(0)
+            gi["v1_w"], gi["v1_b"] = self.dw(b["dv1_pre"], b["e2"]), b["dv1_pre"].sum(0)
+            gi["a2_w"], gi["a2_b"] = self.dw(b["da2_pre"], b["a1"]), b["da2_pre"].sum(0)
+            gi["a3_w"], gi["a3_b"] = b["dscore"].view(1, -1).mm(b["a2"]), b["dscore"].sum().view(1)
+            dP = b["da1_pre"].view(K, B, H).sum(0)                     # rows j with j % B == b (the repeat tiling)
+            a1_w = params[w0 + 8]
+            gi["a1_w"] = torch.cat((self.dw(b["da1_pre"], b["e2"]), dP.t().mm(b["e_mean"])), dim=1)
+            gi["a1_b"] = dP.sum(0)
+            torch.mm(dP, a1_w[:, H:], out=b["dem"])                    # dL/d e_mean
+            for n in gi:
+                grads[w0 + _PARAMS.index(n)] = gi[n]
+        NAT.check(self.L.qs_attn_bwd2_x3(B, K, H, self.towers, self.trains, self.T, st), "qs_attn_bwd2_x3")
+        self_obs = obs[:, :so]
+        nbr_rows = obs[:, so:so + K * nd].reshape(B * K, nd)
+        for i in range(self.T):
+            b, w0 = self.buf[i], 14 * i
+            de2_pre, de1_pre = b["de2p"], b["dh_pre"]
+            grads[w0 + 2], grads[w0 + 3] = self.dw(de2_pre, b["e1"]), de2_pre.sum(0)
+            # embedding_mlp[0] on cat(self_{j % B}, nbr_j): the self half summed over the K tiles first
+            g_self = de1_pre.view(K, B, H).sum(0).t().mm(self_obs)
+            grads[w0] = torch.cat((g_self, de1_pre.t().mm(nbr_rows)), dim=1)
+            grads[w0 + 1] = de1_pre.sum(0)
+        self.pending = False
+        self.obs = self.params = None
+        return grads
+
+
+class _AttnTrainFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, runner, obs, *params):
+        ctx.runner = runner
+        return tuple(runner.forward(obs, params))
+
+    @staticmethod
+    def backward(ctx, *douts):
+        return (None, None) + tuple(ctx.runner.backward(douts))
+
+
+class FusedAttentionTrain:
+    """Both towers' neighbour-encoder outputs for the PPO update as one autograd node on the HIP kernels:
+    encodings(obs) -> [actor [B, H], critic [B, H]] (SwarmActorCritic.evaluate_actions(obs, actions, nbr=...)).  One
+    backward per forward (the activations live in reused buffers)."""
+
+    def __init__(self, policy):
+        if not supports(policy):
+            raise ValueError("fused update: needs the tanh attention encoder with hidden size 128 or 256")
+        self.policy = policy
+        self.runner = _Runner(policy)
+
+    def params(self):
+        return [p for enc in self.runner.encs for p in tower_params(enc)]
+
+    def encodings(self, obs):
+        assert obs.is_cuda and obs.dtype == torch.float32 and obs.dim() == 2
+        return list(_AttnTrainFn.apply(self.runner, obs.contiguous(), *self.params()))

@@ -29,15 +29,21 @@ def pack_mfma_weight(w):
 
 
 X3_SW = 256.0   # weight scale of the split-f16 packing (csrc/qs_policy_x3.h X3_SW)
+X3_SIN = 16.0   # raw-observation scale of the x3 layer-0 inputs (csrc/qs_policy_x3.h X3_SIN)
+F16_MAX = 65504.0
 
 
 def pack_mfma_weight_x3(w):
     """[N, Kd] fp32 weight -> the split-f16 operand layout of qs_attn_embed_x3 / qs_attn_pool_x3 (quadswarm.h):
     packed[ct][s][l] = 8 halves of hi(256 W[32 ct + (l & 31)][16 s + 8 (l >> 5) + j]), then the 8 lo halves,
-    hi = f16(256 w), lo = f16(256 w - hi).  Returned as an int16 tensor [N/32, Kd/16, 64, 2, 8]."""
+    hi = f16(256 w), lo = f16(256 w - hi).  Returned as an int16 tensor [N/32, Kd/16, 64, 2, 8].
+    Raises ValueError for a weight with |256 w| beyond the f16 range (it would pack as +-inf)."""
     n, kd = w.shape
     assert n % 32 == 0 and kd % 16 == 0, (n, kd)
     ws = w.detach().float() * X3_SW
+    if not bool(ws.abs().amax() < F16_MAX):   # NaN fails too
+        raise ValueError(f"x3 packing: max |w| = {float(w.detach().abs().amax()):.4g} is outside the split-f16 range "
+                         f"(< {F16_MAX / X3_SW:.4g})")
     hi = ws.half()
     lo = (ws - hi.float()).half()
 
@@ -68,6 +74,8 @@ class FusedRolloutPolicy:
         if precision not in self.PRECISIONS:
             raise ValueError(f"precision must be one of {self.PRECISIONS}")
         self.precision = precision
+        self.packed_precision = None   # what refresh() packed: precision, or fp32 when x3 weights are out of range
+        self._obs_absmax = None        # running max |obs| the x3 layer 0 has seen since the last check_inputs()
         if not supports(policy):
             raise ValueError("fused rollout forward: needs the tanh attention encoder with hidden size 128 or 256")
         self.policy = policy
@@ -84,8 +92,37 @@ class FusedRolloutPolicy:
 
     # ---- weights / buffers ----
     def refresh(self):
+        """Re-pack the weights.  x3: a weight outside the split-f16 range (|w| >= 255.9) would become +-inf; the
+        towers are then packed (and evaluated) in fp32 until a later refresh finds every weight in range again."""
+        prec = self.precision
+        if prec == "x3":
+            lim = F16_MAX / X3_SW
+            big = max(float(m.weight.detach().abs().amax()) for enc in self.encs
+                      for m in (enc.neighbor_encoder.embedding_mlp[0], enc.neighbor_encoder.embedding_mlp[2],
+                                enc.neighbor_encoder.neighbor_value_mlp[0], enc.neighbor_encoder.neighbor_value_mlp[2],
+                                enc.neighbor_encoder.attention_mlp[0], enc.neighbor_encoder.attention_mlp[2]))
+            if not big < lim:
+                import warnings
+                warnings.warn(f"x3 rollout encoders: max |w| = {big:.4g} >= {lim:.4g} (f16 range); packing fp32")
+                prec = "fp32"
+        self.packed_precision = prec
+        self._pack(prec)
+
+    def check_inputs(self):
+        """x3 only: raise if an observation given to the encoders since the last call was beyond the split-f16 range
+        of layer 0 (|obs| >= 4094 packs as +-inf), i.e. the outputs of those calls are not the fp32 function.
+        Non-finite observations are left to the env's non-finite guard.  One host sync (PPOTrainer: per rollout)."""
+        m, self._obs_absmax = self._obs_absmax, None
+        if m is None:
+            return
+        v = float(m)
+        if v == v and v != float("inf") and v * X3_SIN >= F16_MAX:
+            raise ValueError(f"x3 rollout encoders: an observation reached |obs| = {v:.4g} >= {F16_MAX / X3_SIN:.4g}, "
+                             "beyond the split-f16 range of layer 0; use rollout_precision='fp32'")
+
+    def _pack(self, prec):
         H, so = self.H, self.so
-        pack = pack_mfma_weight_x3 if self.precision == "x3" else pack_mfma_weight
+        pack = pack_mfma_weight_x3 if prec == "x3" else pack_mfma_weight
         packed = []
         for enc in self.encs:
             ne = enc.neighbor_encoder
@@ -140,7 +177,10 @@ class FusedRolloutPolicy:
             self._alloc(B, obs.device)
         so, H, K = self.so, self.H, self.K
         st = ctypes.c_void_p(torch.cuda.current_stream(obs.device).cuda_stream)
-        x3 = self.precision == "x3"
+        x3 = self.packed_precision == "x3"
+        if x3:   # the range check of the layer-0 inputs, on the device (read by check_inputs)
+            m = obs.abs().amax()
+            self._obs_absmax = m if self._obs_absmax is None else torch.maximum(self._obs_absmax, m)
         embed, pool = (self.L.qs_attn_embed_x3, self.L.qs_attn_pool_x3) if x3 else (self.L.qs_attn_embed, self.L.qs_attn_pool)
         NAT.check(embed(ctypes.c_void_p(obs.data_ptr()), obs.shape[1], so, so, B, K, self.nd, H,
                         self.towers, len(self.encs), st), "qs_attn_embed")

@@ -193,11 +193,14 @@ class QuadMultiEncoder(nn.Module):
         self.feed_forward = nn.Sequential(nn.Linear(out, 2 * R), nn.Tanh())
         self.out_size = 2 * R
 
-    def forward(self, obs):
+    def forward(self, obs, nbr_out=None):
+        """nbr_out: the neighbour encoder's output computed elsewhere (the fused update, encoder_train.py)."""
         so, na = self.cfg.self_obs_dim, self.all_neighbor_obs_size
         self_obs = obs[:, :so]
         parts = [self.self_encoder(self_obs)]
-        if self.neighbor_encoder is not None:
+        if nbr_out is not None:
+            parts.append(nbr_out)
+        elif self.neighbor_encoder is not None:
             nbr = obs[:, so:so + na].reshape(obs.shape[0], self.cfg.num_use_neighbor_obs, -1)
             parts.append(self.neighbor_encoder(self_obs, nbr))
         if self.obstacle_encoder is not None:
@@ -252,10 +255,15 @@ class SwarmActorCritic(nn.Module):
             actions = torch.tanh(mean + torch.randn_like(mean) * self.log_std.exp())
         return actions, values, squashed_log_prob(mean, self.log_std, actions)
 
-    def evaluate_actions(self, obs, actions):
-        """(values, log_prob, entropy=None) -- ActorCriticPolicyCustom.py:538-566."""
-        mean = self.action_net(self.actor_latent(obs))
-        return self.predict_values(obs), squashed_log_prob(mean, self.log_std, actions), None
+    def evaluate_actions(self, obs, actions, nbr=None):
+        """(values, log_prob, entropy=None) -- ActorCriticPolicyCustom.py:538-566.  nbr: (actor, critic) neighbour
+        encoder outputs from the fused update (encoder_train.FusedAttentionTrain), else the torch encoders run."""
+        if nbr is None:
+            mean = self.action_net(self.actor_latent(obs))
+            return self.predict_values(obs), squashed_log_prob(mean, self.log_std, actions), None
+        mean = self.action_net(self.actor_decoder(self.actor_core(self.actor_encoder(obs, nbr[0]))))
+        values = self.value_net(self.critic_decoder(self.critic_core(self.critic_encoder(obs, nbr[1]))))
+        return values, squashed_log_prob(mean, self.log_std, actions), None
 
     def predict(self, obs, deterministic=True):
         return torch.tanh(self.action_net(self.actor_latent(obs))) if deterministic else self.forward(obs)[0]
@@ -441,7 +449,7 @@ class PPOTrainer:
     the trainer on a CPU stand-in env; the default is the HIP kernel."""
 
     def __init__(self, env, policy: SwarmActorCritic, cfg: PPOConfig = None, device=None, seed=0,
-                 gae_fn=None, group=None, fused_rollout=True, rollout_precision="fp32"):
+                 gae_fn=None, group=None, fused_rollout=True, rollout_precision="fp32", update_precision="fp32"):
         import torch.distributed as dist
 
         self.env, self.policy, self.cfg = env, policy, cfg or PPOConfig()
@@ -475,6 +483,17 @@ class PPOTrainer:
             from .policy_fused import FusedRolloutPolicy, supports
             if supports(policy):
                 self.fused = FusedRolloutPolicy(policy, precision=rollout_precision)
+        # the update's neighbour encoders: torch autograd ("fp32") or the fused split-f16 kernels ("x3",
+        # encoder_train.py: forward + backward on the matrix cores, fp32-equivalent products)
+        if update_precision not in ("fp32", "x3"):
+            raise ValueError("update_precision must be 'fp32' or 'x3'")
+        self.update_precision = update_precision
+        self.fused_update = None
+        if update_precision == "x3":
+            if self.device.type != "cuda":
+                raise NAT.QuadSwarmError("update_precision='x3' needs a HIP device")
+            from .encoder_train import FusedAttentionTrain
+            self.fused_update = FusedAttentionTrain(policy)
 
     def reset(self):
         self.last_obs = self.env.reset()
@@ -517,6 +536,8 @@ class PPOTrainer:
                 if not go:
                     return False
         self.last_values.copy_(fwd.predict_values(self.last_obs).view(-1))
+        if self.fused is not None:
+            self.fused.check_inputs()   # x3: the rollout's observations stayed inside the split-f16 range
         self.gae_fn(st.rewards, st.values, st.episode_starts, self.last_values, self.last_done,
                     self.cfg.gamma, self.cfg.gae_lambda, st.advantages, st.returns)
         for cb in callbacks:
@@ -537,7 +558,9 @@ class PPOTrainer:
             perm = torch.randperm(n, device=self.device, generator=self.gen)
             for s in range(0, n, c.batch_size):
                 idx = perm[s:s + c.batch_size]
-                values, logp, entropy = pol.evaluate_actions(obs[idx], act[idx])
+                ob = obs[idx]
+                nbr = self.fused_update.encodings(ob) if self.fused_update is not None else None
+                values, logp, entropy = pol.evaluate_actions(ob, act[idx], nbr=nbr)
                 values = values.flatten()
                 adv = adv_all[idx]
                 if c.normalize_advantage and idx.numel() > 1:

@@ -1,0 +1,167 @@
+"""The PPO update's fused attention encoders (quadswarm_amd/encoder_train.py, csrc/qs_policy_train.h) against the torch
+module's autograd: forward outputs, the gradients of every encoder parameter for a random upstream gradient, and the
+whole PPO loss / gradient bucket of a minibatch.
+
+Weights: the reference-pinned fixtures' (tests/golden/policy_c3 / policy_a8: the reference's own
+ActorCriticPolicyCustomSeparateWeights built by tools/gen_golden_policy.py; every tanh in its nonlinear range) and a
+widened random policy for K = 1 / partial blocks.  Reference: the same module in fp64.  The fused path's products are
+fp32-equivalent (three f16 products, ~7e-7 relative); torch's fp32 autograd is the yardstick: the fused gradients'
+error against fp64 (max |g - g64| / max |g64| per tensor) must stay within 1e-4 and within 8x of torch fp32's own
+error (+1e-6), the outputs within 5e-5 (the rollout kernels' bound)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("no HIP device", allow_module_level=True)
+
+from quadswarm_amd.encoder_train import FusedAttentionTrain, dw_x3, tower_params  # noqa: E402
+from quadswarm_amd.ppo import PolicyConfig, SwarmActorCritic  # noqa: E402
+
+
+def fixture_policy(case):
+    from test_policy_reference import load_case, reference_weights
+    meta, data, pc = load_case(case)
+    pol = SwarmActorCritic(pc).cuda()
+    pol.load_reference_state_dict(reference_weights(meta, torch.float32))
+    return pol
+
+
+def random_policy(K, H=256, seed=0):
+    torch.manual_seed(seed)
+    pol = SwarmActorCritic(PolicyConfig(self_obs_dim=18, neighbor_obs_dim=6, num_use_neighbor_obs=K, rnn_size=H,
+                                        neighbor_hidden_size=H, act_dim=4)).cuda()
+    with torch.no_grad():
+        for enc in (pol.actor_encoder, pol.critic_encoder):
+            for m in enc.neighbor_encoder.modules():
+                if isinstance(m, torch.nn.Linear):
+                    m.weight.mul_(3.0)
+                    m.bias.uniform_(-0.5, 0.5)
+    return pol
+
+
+def obs_for(pc, B, seed=1):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    od = pc.self_obs_dim + pc.neighbor_obs_dim * pc.num_use_neighbor_obs + pc.obstacle_obs_dim
+    return torch.randn(B, od, device="cuda", generator=g) * 2.0
+
+
+def torch_encodings(pol, obs):
+    so, K = pol.cfg.self_obs_dim, pol.cfg.num_use_neighbor_obs
+    nbr = obs[:, so:so + K * pol.cfg.neighbor_obs_dim].reshape(obs.shape[0], K, -1)
+    return [enc.neighbor_encoder(obs[:, :so], nbr) for enc in (pol.actor_encoder, pol.critic_encoder)]
+
+
+def rel_err(a, b):
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+@pytest.mark.parametrize("case,B", [("c3", 3000), ("a8", 2050), ("k1", 777), ("k6", 131)])
+def test_encoder_gradients_match_torch(case, B):
+    pol = fixture_policy(case) if case in ("c3", "a8") else random_policy(int(case[1:]), H=256 if case == "k6" else 128)
+    obs = obs_for(pol.cfg, B, seed=3)
+    H = pol.cfg.neighbor_hidden_size
+    g = torch.Generator(device="cuda").manual_seed(9)
+    G = [torch.randn(B, H, device="cuda", generator=g) * 1e-3 for _ in range(2)]   # dL/d out, a PPO-like scale
+    params = [p for enc in (pol.actor_encoder, pol.critic_encoder) for p in tower_params(enc)]
+
+    def grads_of(outs):
+        loss = sum((o * gi).sum() for o, gi in zip(outs, G))
+        return torch.autograd.grad(loss, params)
+
+    fused = FusedAttentionTrain(pol)
+    out_f = fused.encodings(obs)
+    g_f = grads_of(out_f)
+    out_t = torch_encodings(pol, obs)
+    g_t = grads_of(out_t)
+    pol64 = SwarmActorCritic(pol.cfg).cuda().double()
+    pol64.load_state_dict(pol.state_dict())
+    params64 = [p for enc in (pol64.actor_encoder, pol64.critic_encoder) for p in tower_params(enc)]
+    out64 = torch_encodings(pol64, obs.double())
+    g64 = torch.autograd.grad(sum((o * gi.double()).sum() for o, gi in zip(out64, G)), params64)
+    for i in range(2):
+        err = (out_f[i].double() - out64[i]).abs().max().item()
+        assert err < 5e-5, (case, "out", i, err)
+    names = ["e1_w", "e1_b", "e2_w", "e2_b", "v1_w", "v1_b", "v2_w", "v2_b", "a1_w", "a1_b", "a2_w", "a2_b", "a3_w",
+             "a3_b"] * 2
+    worst = 0.0
+    for n, a, b, c in zip(names, g_f, g_t, g64):
+        ef, et = rel_err(a.double(), c), rel_err(b.double(), c)
+        worst = max(worst, ef)
+        assert ef < 1e-4 and ef < 8 * et + 1e-6, (case, n, ef, et)
+    print(f"{case} B={B}: worst relative gradient error fused {worst:.2e}")
+
+
+@pytest.mark.parametrize("case", ["c3", "a8"])
+def test_ppo_loss_gradient_bucket_matches_torch(case):
+    """The whole PPO minibatch step as PPOTrainer.train runs it: evaluate_actions with the fused encoders (nbr=...)
+    vs the torch module -- values, log-probs and every parameter's gradient."""
+    pol = fixture_policy(case)
+    B = 2048
+    obs = obs_for(pol.cfg, B, seed=5)
+    g = torch.Generator(device="cuda").manual_seed(6)
+    act = torch.rand(B, pol.cfg.act_dim, device="cuda", generator=g) * 1.6 - 0.8
+    adv = torch.randn(B, device="cuda", generator=g)
+
+    def loss_of(v, lp):
+        return -(adv * torch.exp(lp - lp.detach())).mean() + 0.5 * (v.view(-1) ** 2).mean()
+
+    fused = FusedAttentionTrain(pol)
+    v_f, lp_f, _ = pol.evaluate_actions(obs, act, nbr=fused.encodings(obs))
+    gf = torch.autograd.grad(loss_of(v_f, lp_f), list(pol.parameters()), allow_unused=True)
+    v_t, lp_t, _ = pol.evaluate_actions(obs, act)
+    gt = torch.autograd.grad(loss_of(v_t, lp_t), list(pol.parameters()), allow_unused=True)
+    assert (v_f - v_t).abs().max().item() < 2e-4
+    assert (lp_f - lp_t).abs().max().item() < 2e-3
+    flat_f = torch.cat([(a if a is not None else torch.zeros_like(p)).flatten() for a, p in zip(gf, pol.parameters())])
+    flat_t = torch.cat([(a if a is not None else torch.zeros_like(p)).flatten() for a, p in zip(gt, pol.parameters())])
+    rel = ((flat_f - flat_t).norm() / flat_t.norm()).item()
+    print(f"{case}: |g_fused - g_torch| / |g_torch| = {rel:.2e}")
+    assert rel < 1e-4
+
+
+def test_trainer_update_x3_runs_and_tracks_fp32():
+    """PPOTrainer(update_precision='x3') on a device env: the same iteration from the same state as the fp32 update
+    ends at nearly the same weights."""
+    from quadswarm_amd import QuadSwarmConfig
+    from quadswarm_amd.env import QuadSwarmEnv
+    from quadswarm_amd.ppo import PPOConfig, PPOTrainer
+    cfg = QuadSwarmConfig(num_envs=64, num_agents=8, seed=2)
+    res, w0 = [], None
+    for prec in ("fp32", "x3"):
+        env = QuadSwarmEnv(cfg)
+        torch.manual_seed(0)
+        pol = SwarmActorCritic(PolicyConfig.for_env(cfg, rnn_size=256, neighbor_hidden_size=256)).cuda()
+        tr = PPOTrainer(env, pol, PPOConfig(n_steps=16, batch_size=1024, n_epochs=1), seed=0, update_precision=prec)
+        w0 = torch.cat([p.detach().flatten() for p in pol.parameters()])
+        tr.collect_rollouts()
+        stats = tr.train()
+        assert np.isfinite(stats["loss"])
+        res.append(torch.cat([p.detach().flatten() for p in pol.parameters()]))
+        env.close()
+    # Adam's first steps are ~lr sign(g): a gradient element near 0 may flip between the two, so the bound is on the
+    # mean change and on 2.5 lr for the maximum
+    d = (res[0] - res[1]).abs()
+    step = (res[0] - w0).abs().mean().item()
+    print(f"|w_fp32 - w_x3| after one update: max {d.max().item():.2e} mean {d.mean().item():.2e} (mean step {step:.2e})")
+    assert d.max().item() <= 2.5e-4 and d.mean().item() < 0.02 * step
+
+
+@pytest.mark.parametrize("H,R", [(256, 100003), (128, 777), (256, 16)])
+def test_dw_x3_matches_fp64(H, R):
+    """qs_attn_dw_x3: G^T A over R rows (a tail that is not a multiple of the 16-row step, column scales spanning
+    2^-20 .. 2^4) against fp64 and torch's fp32 GEMM."""
+    g = torch.Generator(device="cuda").manual_seed(R)
+    G = torch.randn(R, H, device="cuda", generator=g) * torch.exp2(torch.linspace(-20, 4, H, device="cuda"))
+    A = torch.tanh(torch.randn(R, H, device="cuda", generator=g) * 2)
+    want = G.double().t().mm(A.double())
+    got = dw_x3(G, A)
+    t32 = G.t().mm(A)
+    # per output row n (column n of G has its own scale): relative to the row's magnitude
+    scale = want.abs().amax(1, keepdim=True).clamp_min(1e-300)
+    e_x3 = ((got.double() - want).abs() / scale).max().item()
+    e_32 = ((t32.double() - want).abs() / scale).max().item()
+    print(f"H={H} R={R}: dW relative error x3 {e_x3:.2e}, torch fp32 {e_32:.2e}")
+    assert e_x3 < 1e-5 and e_x3 < 8 * e_32 + 1e-6

@@ -131,6 +131,7 @@ for s in "$@"; do
       step prof_${C}_fetch 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof_${C}_fetch -o f --output-format csv -- python bench.py --config $C --steps 100 --warmup 10 --no-cpu-baseline --graph 0 --e2e-iters 0
       step prof_${C}_write 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof_${C}_write -o w --output-format csv -- python bench.py --config $C --steps 100 --warmup 10 --no-cpu-baseline --graph 0 --e2e-iters 0
       step prof_${C}_sq 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INSTS_LDS -d gpurun_out/prof_${C}_sq -o s --output-format csv -- python bench.py --config $C --steps 100 --warmup 10 --no-cpu-baseline --graph 0 --e2e-iters 0
+      step prof_${C}_flops 300 timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_FLOPS_FP32 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_CVT SQ_WAVES -d gpurun_out/prof_${C}_flops -o fl --output-format csv -- python bench.py --config $C --steps 100 --warmup 10 --no-cpu-baseline --graph 0 --e2e-iters 0
       rm -f gpurun_out/prof_${C}_*/*kernel_trace.csv gpurun_out/prof_${C}_*/*/*kernel_trace.csv
       ;;
     sel2)      # QS_NBR_SELECT2 on 32-drone envs: bitwise digest A/B + timing A/B

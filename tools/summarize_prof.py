@@ -8,6 +8,7 @@ Inputs (written on the GPU box by tools/gpu_check.sh):
   gpurun_out/prof_fetch/*counter_collection   --pmc FETCH_SIZE pass
   gpurun_out/prof_write/*counter_collection   --pmc WRITE_SIZE pass (separate: TCC slots)
   gpurun_out/prof_sq/*counter_collection      --pmc SQ_* pass
+  gpurun_out/prof_flops/*counter_collection   --pmc SQ_INSTS_VALU_{FMA,ADD,MUL,TRANS}_F32 ... pass (optional)
   gpurun_out/calib_{fetch,write}/...           tools/calib/fetch_calib (known byte counts)
 Outputs:
   profiles/r<NN>_<config>_kernel_stats.csv   (verbatim copy)
@@ -73,7 +74,8 @@ def main():
         head = None
     res = {"kernel": stats.get("name"), "config": args.config, "tree": head, "kernel_trace": stats,
            "calibration_ratio": calib}
-    for pat in ("_fetch/*counter_collection.csv", "_write/*counter_collection.csv", "_sq/*counter_collection.csv"):
+    for pat in ("_fetch/*counter_collection.csv", "_write/*counter_collection.csv", "_sq/*counter_collection.csv",
+                "_flops/*counter_collection.csv"):
         for (kname, cname), v in counters(args.prefix + pat, args.kernel).items():
             if not (args.kernel + "<" in kname or args.kernel + "I" in kname):
                 continue
