@@ -344,7 +344,7 @@ def end_to_end(env, cfg, dev, world, iters, n_steps=None, log=None, fused=True, 
                   f"fp32 (torch/hipBLASLt GEMMs" + (f", rollout neighbour encoders: fused HIP MFMA kernels, {precision})"
                                                     if tr.fused is not None else ")"),
         "rollout_precision": precision if tr.fused is not None else "torch fp32",
-        "update_precision": ("x3: fused HIP attention-encoder forward + backward (encoder_train.py), dW on hipBLASLt"
+        "update_precision": ("x3: fused HIP attention-encoder forward + backward (encoder_train.py), dW on split-f16 MFMA (qs_attn_dw_x3)"
                              if upd == "x3" else "torch fp32 autograd (hipBLASLt)"),
         "gemm_table": tuned,
         "update_flop_per_sample": round(fps), "update_tflops": round(upd_tf, 2),

@@ -17,7 +17,7 @@ namespace qs {
 // sensor noise (add_noise_numba sensor_noise.py:172-218) + state_xyz_vxyz_R_omega[_floor|_wall]
 // (get_state.py:226-292), written to an LDS row.
 // z = the 12 normals of the stream's blocks 0..2 (drawn by the caller, possibly on other sub-lanes)
-__device__ void self_obs_z(const KP& kp, const Drone& d, const float* z, const Rng& rng, uint32_t gid, uint32_t stream,
+__device__ __forceinline__ void self_obs_z(const KP& kp, const Drone& d, const float* z, const Rng& rng, uint32_t gid, uint32_t stream,
                            float* out) {
     float np_[3], nv[3], no[3], nr[9];
     if (kp.sense) {
@@ -128,7 +128,7 @@ __device__ __forceinline__ void xch_put(float4* xch, int lane, const float* P, c
 // the candidates j = q + Q t: it builds their keys, gathers the other sub-lanes' keys by DPP, ranks
 // its own candidates and writes those that land among the K nearest.  Only write == true stores.
 template <int NPAD, int Q>
-__device__ void neighbor_obs(const KP& kp, const float4* xch, int dbase, int di, int q, const float* P, const float* V,
+__device__ __forceinline__ void neighbor_obs(const KP& kp, const float4* xch, int dbase, int di, int q, const float* P, const float* V,
                              bool write, float* out) {
     constexpr int PJ = (NPAD + Q - 1) / Q;   // candidates per sub-lane
     constexpr bool KEEP = PJ <= 8;           // keep the relative vectors in VGPRs between passes
@@ -260,7 +260,7 @@ __device__ __forceinline__ void new_vel(float maxv, float* v, const float* sh, f
 // perform_collision_between_drones (collisions/quadrotors.py:23-59) for the pair (1 = lower id).
 // Both drones of the pair evaluate it with identical inputs and draws (key = lower drone, stream j):
 // z = normals 0..27 (blocks 0..6: the 3 rejection tries use normals t*9 .. t*9+8), u = uniforms 0..7.
-__device__ void collide_pair(const float* p1, float* v1, float* w1, const float* p2, float* v2, float* w2,
+__device__ __forceinline__ void collide_pair(const float* p1, float* v1, float* w1, const float* p2, float* v2, float* w2,
                              const float* z, const float* u) {
     float n[3] = {p1[0] - p2[0], p1[1] - p2[1], p1[2] - p2[2]};
     const float m = fsqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
@@ -304,7 +304,7 @@ __device__ void collide_pair(const float* p1, float* v1, float* w1, const float*
 
 // perform_collision_with_wall (collisions/room.py:6-44) / _with_ceiling (:91-113); u = uniforms 0..11
 // of stream S_WALL / S_CEIL
-__device__ void collide_room(const KP& kp, Drone& d, const float* u, bool wall) {
+__device__ __forceinline__ void collide_room(const KP& kp, Drone& d, const float* u, bool wall) {
     const float sp = fsqrt(d.vel[0] * d.vel[0] + d.vel[1] * d.vel[1] + d.vel[2] * d.vel[2]);
     const float real = clampf(0.2f * sp + (0.8f * sp - 0.2f * sp) * u[0], 0.1f, 6.0f);
     float dir[3] = {-1.f + 2.f * u[1], -1.f + 2.f * u[2], -1.f + 2.f * u[3]};
@@ -884,12 +884,13 @@ __global__ __launch_bounds__(StepGeo<NPAD>::WGS) void step_kernel(const KP* __re
     // goal scenario: the env's scenario record (SC_WORDS words) dealt over its lanes -- word li + LPE t on lane li
     // -- loaded with the step's other loads and staged in LDS for scenario.step() after the forces
     const bool SCEN = !OBST && kp.scen_b >= 0;
+    const bool SCEN_STEP = SCEN && kp.scen_b != SC_STATIC_DIFF_GOAL;   // static_diff_goal's step() does nothing
     constexpr int SRW = (SC_WORDS + LPE - 1) / LPE;
     uint32_t scw[SRW];
 #pragma unroll
     for (int t = 0; t < SRW; ++t) {
         const int w = li + LPE * t;
-        scw[t] = (SCEN && envok && w < SC_WORDS) ? scen_word(kp, b, env, w) : 0u;
+        scw[t] = (SCEN_STEP && envok && w < SC_WORDS) ? scen_word(kp, b, env, w) : 0u;
     }
     Drone d;   // every sub-lane holds the whole drone
     DroneWords<Q, LW> dw;
@@ -1128,7 +1129,10 @@ __global__ __launch_bounds__(StepGeo<NPAD>::WGS) void step_kernel(const KP* __re
         // free until the obs phase), the ready pairs' 9 Philox blocks drawn by the env's lanes (lane le: block
         // le % 9 of pair le / 9), up to LPE / 9 pairs (more wait a round).
         constexpr int PMAX = LPE / 9, TBL4 = (2 * NPAD + 3) / 4, STR4 = PMAX * 9 + TBL4;
-        if (PMAX > 0 && NPAD <= 32 && EPB * STR4 * 4 <= SLOTS * kp.obs_dim) {
+        // only when some env of the wave has two or more pairs pending (else the one-pair loop takes one iteration)
+        const uint64_t pbal = __ballot(pend != 0ull && q == 0);
+        const bool multi = q == 0 && (__popcll(pend) >= 2 || __popcll((pbal >> lbase) & lmask) >= 2);
+        if (PMAX > 0 && NPAD <= 32 && EPB * STR4 * 4 <= SLOTS * kp.obs_dim && __ballot(multi) != 0ull) {
             float4* pscr = reinterpret_cast<float4*>(lds) + el * STR4;
             uint32_t* pt = reinterpret_cast<uint32_t*>(pscr + PMAX * 9);   // [NPAD] the drones' pending rows
             uint32_t* ct = pt + NPAD;                                     // [NPAD] their columns (earlier owners)
@@ -1286,7 +1290,7 @@ __global__ __launch_bounds__(StepGeo<NPAD>::WGS) void step_kernel(const KP* __re
     // scenario record is stored only where it changed.
     float obs_goal[3] = {d.goal[0], d.goal[1], d.goal[2]};
     float* stab = scen_tab(lds, kp, SLOTS) + el * scen_stride<NPAD>();
-    if (SCEN) {
+    if (SCEN_STEP) {
         uint32_t* srec = reinterpret_cast<uint32_t*>(stab + 2 * (NPAD + 4) * 4);
         if (q == 0 && di < kp.N) { stab[4 * di] = d.goal[0]; stab[4 * di + 1] = d.goal[1]; stab[4 * di + 2] = d.goal[2]; }
 #pragma unroll
@@ -1349,13 +1353,9 @@ __global__ __launch_bounds__(StepGeo<NPAD>::WGS) void step_kernel(const KP* __re
     }
     QS_STAMP(5);
     if (lead) {
-        if (SCEN) {   // the self obs measure against the goal the reference's observation saw
-            Drone dv = d;
-            for (int k = 0; k < 3; ++k) dv.goal[k] = obs_goal[k];
-            self_obs_z(kp, dv, zs, rng, gid, S_SENSOR, row);
-        } else {
-            self_obs_z(kp, d, zs, rng, gid, S_SENSOR, row);
-        }
+        Drone dv = d;   // the self obs measure against the goal the reference's observation saw
+        for (int k = 0; k < 3; ++k) dv.goal[k] = obs_goal[k];
+        self_obs_z(kp, dv, zs, rng, gid, S_SENSOR, row);
     }
     QS_STAMP(6);
     if (nbr) neighbor_obs<NPAD, Q>(kp, xch, dbase, di, q, d.pos, d.vel, active, row);

@@ -570,9 +570,11 @@ __global__ __launch_bounds__(NTHR, 1) void dw_x3_kernel(const float* __restrict_
             const f16x8 al = *reinterpret_cast<const f16x8*>(buf(b, 3) + k * 32 * DW_LDR + aoff);
 #pragma unroll
             for (int t = 0; t < NT; ++t) {
-                acc[t][k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(gh[t], ah, acc[t][k], 0, 0, 0);
-                acc[t][k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(gl[t], ah, acc[t][k], 0, 0, 0);
-                acc[t][k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(gh[t], al, acc[t][k], 0, 0, 0);
+                // A's columns as the first operand, G's as the second: the result tile is [k][n], i.e. a lane
+                // holds output row n = lane & 31 (the layout of the store below; qs_policy.h acc_i / acc_n0)
+                acc[t][k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, gh[t], acc[t][k], 0, 0, 0);
+                acc[t][k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, gl[t], acc[t][k], 0, 0, 0);
+                acc[t][k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, gh[t], acc[t][k], 0, 0, 0);
             }
         }
         if (s + 1 < steps_per_block) stage(b ^ 1);   // the other buffer: last read two steps ago (barrier below)

@@ -490,8 +490,13 @@ __device__ __forceinline__ int sd_track(SDraw& s, int pos, int n) {
     return pos;
 }
 
+// the env's scenario: the record's mode under quads_mode=mix, else the config's (a constant of the specialised
+// kernel, so that its step code is the only one compiled in)
+__device__ __forceinline__ int sc_mode(const KP& kp, int rec_mode) { return kp.scen_b == SC_MIX ? rec_mode : kp.scen_b; }
+
 // does scenario.step() change anything at this tick (scen_step's branches)
 __device__ __forceinline__ bool scen_acts(const KP& kp, int mode, int period, int tick) {
+    mode = sc_mode(kp, mode);
     const bool ev = period > 0 && tick % period == 0 && tick > 0;
     switch (mode) {
         case SC_DYNAMIC_SAME_GOAL: case SC_DYNAMIC_DIFF_GOAL: case SC_SWAP_GOALS: case SC_SWARM_VS_SWARM: return ev;
@@ -531,7 +536,8 @@ __device__ __forceinline__ int scen_step_lane(const KP& kp, Scen& s, int tick, S
     const int pl = sc_per_layer(s.form);
     const bool ev = s.period > 0 && tick % s.period == 0 && tick > 0;
     via_tab = false;
-    if (s.mode == SC_DYNAMIC_SAME_GOAL) {   // dynamic_same_goal.py:16-29
+    const int mode = sc_mode(kp, s.mode);
+    if (mode == SC_DYNAMIC_SAME_GOAL) {   // dynamic_same_goal.py:16-29
         if (!ev) return 0;
         const float x = sd_uniform(sd, -box, box), y = sd_uniform(sd, -box, box);
         const float z = fmaxf(sd_uniform(sd, -0.5f * box, 0.5f * box) + 2.f, 0.25f);
@@ -539,7 +545,7 @@ __device__ __forceinline__ int scen_step_lane(const KP& kp, Scen& s, int tick, S
         sc_row(s.form, N, pl, s.size, 0.f, s.c, di, goal);
         sc_center(s.form, N, pl, s.size, 0.f, s.c, goal);
         return 2;
-    } else if (s.mode == SC_DYNAMIC_DIFF_GOAL) {   // dynamic_diff_goal.py:13-40
+    } else if (mode == SC_DYNAMIC_DIFF_GOAL) {   // dynamic_diff_goal.py:13-40
         if (!ev) return 0;
         const float x = sd_uniform(sd, -box, box), y = sd_uniform(sd, -box, box);
         const float z = sc_z_value(kp, s, sd);
@@ -557,13 +563,13 @@ __device__ __forceinline__ int scen_step_lane(const KP& kp, Scen& s, int tick, S
         }
         via_tab = true;
         return 2;
-    } else if (s.mode == SC_SWAP_GOALS) {   // swap_goals.py:12-25
+    } else if (mode == SC_SWAP_GOALS) {   // swap_goals.py:12-25
         if (!ev) return 0;
         const int p = sd_track(sd, di, N);
         tb[4 * p] = goal[0]; tb[4 * p + 1] = goal[1]; tb[4 * p + 2] = goal[2];
         via_tab = true;
         return 0;
-    } else if (s.mode == SC_DYNAMIC_FORMATIONS) {   // dynamic_formations.py:18-40
+    } else if (mode == SC_DYNAMIC_FORMATIONS) {   // dynamic_formations.py:18-40
         if (s.size <= -s.hi) {
             s.inc = 1;
             s.speed = sd_uniform(sd, 1.f, 3.f);
@@ -575,13 +581,13 @@ __device__ __forceinline__ int scen_step_lane(const KP& kp, Scen& s, int tick, S
         sc_row(s.form, N, pl, s.size, s.layer, s.c, di, goal);
         sc_center(s.form, N, pl, s.size, s.layer, s.c, goal);
         return 1;
-    } else if (s.mode == SC_EP_LISSAJOUS3D) {   // ep_lissajous3D.py:8-26 (accumulates on goals[0])
+    } else if (mode == SC_EP_LISSAJOUS3D) {   // ep_lissajous3D.py:8-26 (accumulates on goals[0])
         const float t = (float)tick / cf;
         const float nx = 0.03f * sin_any(t) + ta[0], ny = 0.01f * sin_any(2.f * t + 90.f) + ta[1],
                     nz = 0.01f * cos_any(2.f * t + 90.f) + ta[2];
         goal[0] = nx; goal[1] = ny; goal[2] = nz;
         return 0;
-    } else if (s.mode == SC_EP_RAND_BEZIER) {   // ep_rand_bezier.py:6-47
+    } else if (mode == SC_EP_RAND_BEZIER) {   // ep_rand_bezier.py:6-47
         const int steps = (int)(5.f * cf);
         const int t = tick % steps;
         float rd[3], hi[3], lo[3];
@@ -618,7 +624,7 @@ __device__ __forceinline__ int scen_step_lane(const KP& kp, Scen& s, int tick, S
             for (int k = 0; k < 3; ++k) goal[k] = (l1 * s.bz[k] + 2.f * sp * s.bz[3 + k]) * l1 + sp * sp * s.bz[6 + k];
         }
         return ch;
-    } else if (s.mode == SC_SWARM_VS_SWARM) {   // swarm_vs_swarm.py:56-76 (sc_vs_formations with the shuffles)
+    } else if (mode == SC_SWARM_VS_SWARM) {   // swarm_vs_swarm.py:56-76 (sc_vs_formations with the shuffles)
         if (!ev) return 0;
         for (int k = 0; k < 3; ++k) {
             const float t3 = s.c1[k];
@@ -643,7 +649,7 @@ __device__ __forceinline__ int scen_step_lane(const KP& kp, Scen& s, int tick, S
         }
         via_tab = true;
         return 2;
-    } else if (s.mode == SC_RUN_AWAY) {   // run_away.py:16-27
+    } else if (mode == SC_RUN_AWAY) {   // run_away.py:16-27
         if (tick % (int)(1.f * cf) == 0 && tick > 0 && N >= 2) {
             const int a = sd_int(sd, 1, N), b2 = sd_int(sd, 1, N);
             const int src = di == 0 ? a : b2;

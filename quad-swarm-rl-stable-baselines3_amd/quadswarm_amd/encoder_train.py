@@ -40,10 +40,13 @@ def tower_params(enc):
 
 def col_scales(G):
     """Per-column power-of-two scales of a gradient [R, H] for qs_attn_dw_x3: s_n |G[:, n]| in [2^13, 2^14) (1 for an
-    all-zero or non-finite column)."""
+    all-zero or non-finite column).  The scales are built from their exponent bits: they must be exact powers of two
+    (torch.ldexp goes through pow on the device and is not), else the kernel's f16 hi / lo split of s G is taken from
+    a rounded product and near-tie elements lose an ulp of the hi half."""
     m = G.abs().amax(0)
     _, e = torch.frexp(m)
-    s = torch.ldexp(torch.ones_like(m), (14 - e).to(torch.int32))
+    k = (14 - e.to(torch.int32)).clamp(-126, 127)
+    s = ((k + 127) << 23).view(torch.float32)
     return torch.where((m > 0) & torch.isfinite(m), s, torch.ones_like(m)).contiguous()
 
 

@@ -88,6 +88,10 @@ def test_encoder_gradients_match_torch(case, B):
              "a3_b"] * 2
     worst = 0.0
     for n, a, b, c in zip(names, g_f, g_t, g64):
+        if n == "a3_b":   # the softmax is shift-invariant: the score bias' gradient is 0 (rounding noise in fp64 too)
+            ref = max(x.abs().max().item() for x in g64)
+            assert a.abs().max().item() < 1e-6 * ref and b.abs().max().item() < 1e-6 * ref, (case, n)
+            continue
         ef, et = rel_err(a.double(), c), rel_err(b.double(), c)
         worst = max(worst, ef)
         assert ef < 1e-4 and ef < 8 * et + 1e-6, (case, n, ef, et)

@@ -2,7 +2,7 @@
 """Diagnostic: the ISA of a config's specialised step kernel (what qs_specialize compiles with hipRTC), built
 offline with hipcc from the same sources and parameter words, plus instruction counts.
 
-    python tools/jit_isa.py a8 [out.s]        (bench.py config names; QS_JIT_OPTS as for qs_specialize)"""
+    python tools/jit_isa.py a8 [out.s]        (bench.py config names; QS_JIT_OPTS as for qs_specialize; QS_MODE=<quads_mode>)"""
 import os
 import re
 import subprocess
@@ -21,7 +21,10 @@ def main():
     from quadswarm_amd import _native as N
     config = sys.argv[1] if len(sys.argv) > 1 else "c3"
     out = sys.argv[2] if len(sys.argv) > 2 else f"/tmp/{config}_step.s"
-    cfg = bench.make_cfg(bench.CONFIGS[config], seed=0, specialize=True)
+    over = dict(bench.CONFIGS[config])
+    if os.environ.get("QS_MODE"):   # a goal scenario for the swarm configs (bench.py --quads-mode)
+        over["quads_mode"] = os.environ["QS_MODE"]
+    cfg = bench.make_cfg(over, seed=0, specialize=True)
     qc = cfg.to_qs_config()
     L = N.lib()
     buf = (ctypes.c_uint32 * 8192)()

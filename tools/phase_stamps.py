@@ -1,7 +1,7 @@
 #!/usr/bin/env python
 """Diagnostic: per-phase cycle budget of a step kernel from s_memtime stamps (QS_STAMPS build).
 
-    make -C quad-swarm-rl-stable-baselines3_amd stamps && python tools/phase_stamps.py [config]
+    make -C quad-swarm-rl-stable-baselines3_amd stamps && python tools/phase_stamps.py [config [quads_mode]]
 
 The stamps library compiles the specialised (hipRTC) kernels with -DQS_STAMPS=1, i.e. the kernels the bench runs
 plus the stamps.  Flavor B stamps phase boundaries (slots 0-11); flavor A sums each phase of its 8-tick loop over
@@ -34,7 +34,10 @@ def main():
     from quadswarm_amd.env import QuadSwarmEnv
 
     config = sys.argv[1] if len(sys.argv) > 1 else "c3"
-    cfg = bench.make_cfg(bench.CONFIGS[config], seed=0, specialize=True)
+    over = dict(bench.CONFIGS[config])
+    if len(sys.argv) > 2:   # a goal scenario for the swarm configs (bench.py --quads-mode)
+        over["quads_mode"] = sys.argv[2]
+    cfg = bench.make_cfg(over, seed=0, specialize=True)
     env = QuadSwarmEnv(cfg)
     assert env.specialized, "the stamps run on the specialised kernels"
     env.reset()
