@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define QS_ABI_VERSION 12
+#define QS_ABI_VERSION 13
 #define QS_MAX_AGENTS 128           /* drones per env: up to 64 inside one 64-lane wavefront, 128 = a two-wave
                                        workgroup per env (flavor B without obstacles; paper/fps_compare.py:7) */
 #define QS_MAX_DR_CHOICES 8         /* entries per obstacle domain-randomisation list */
@@ -257,6 +257,11 @@ enum qs_env_ffield {
     QS_ENVF_SC_CENTER = 8, QS_ENVF_SC_BEZIER = 11, QS_ENVF_SC_C1 = 20, QS_ENVF_SC_C2 = 23,
     QS_NENVF = 26
 };
+/* The scenario floats (rows QS_ENVF_SC_SIZE .. QS_ENVF_SC_C2 + 2, QS_SC_NF of them) are stored ENV-MAJOR inside
+ * their block (ABI 13): field k = row - QS_ENVF_SC_SIZE of env e at env_f[QS_ENVF_SC_SIZE * E + QS_SC_NF * e + k],
+ * so that an env's record is one 92-byte run (the step kernel loads it with one instruction over the env's lanes:
+ * 2-3 cache lines per wave instead of one per field).  The other env_f rows stay [row][E]. */
+#define QS_SC_NF 23
 
 typedef struct qs_layout {          /* byte offsets inside one workspace allocation */
     size_t params;                  /* kernel parameter block (device copy of the config + runtime params) */
@@ -514,6 +519,19 @@ int qs_attn_bwd2_x3(int32_t B, int32_t K, int32_t H, const qs_attn_tower* towers
  * gradients) with a power-of-two scale per column, col_scale[n] |G[:, n]| < 2^14; A [R, H] with |A| <= 1 (tanh). */
 int qs_attn_dw_x3(const float* G, const float* A, const float* col_scale, int64_t R, int32_t H, float* part,
                   int32_t n_parts, void* stream);
+/* Column reductions of a gradient G [R, H] in one pass over its rows (ABI 13; the update's bias gradients, the dW
+ * column scales and layer 0's weight gradient, in place of torch's abs / amax / sum / skinny-GEMM passes), split
+ * over n_parts row ranges, per part p and column n:
+ *   part_max[p, n] = max |G[r, n]| (NaN / inf propagate), part_sum[p, n] = sum G[r, n],
+ *   part_x[p, c, n] = sum G[r, n] X(r, c) for c < nx (nx <= QS_COLSTATS_MAX_X; part_x may be NULL when nx = 0) with
+ *   the layer-0 input of row r = k B + b of the attention encoder's repeat tiling (quad_multi_model.py:44-101):
+ *   X(r, c) = obs[(r / K) * obs_stride + nbr_off + (r % K) * nd + c] for c < nd (neighbour k of row r / K, the
+ *   reshape of the neighbour block), obs[(r % B) * obs_stride + c - nd] for nd <= c < nx (self.repeat(K, 1)).
+ * H is 128 or 256. */
+#define QS_COLSTATS_MAX_X 32
+int qs_colstats(const float* G, int64_t R, int32_t H, const float* d_obs, int32_t obs_stride, int32_t nbr_off,
+                int32_t B, int32_t K, int32_t nd, int32_t nx, float* part_max, float* part_sum, float* part_x,
+                int32_t n_parts, void* stream);
 
 /* sb_train's capture-radius curriculum on the device (ABI 11; replaces CurriculumCallback._on_step,
  * swarm_rl/custom_callbacks.py:441-468, which SB3 runs after every VecEnv step).  Flavor A.  The callback's state

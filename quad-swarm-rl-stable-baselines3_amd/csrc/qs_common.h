@@ -120,6 +120,39 @@ struct Bufs {
     float* rcomp;                // [QS_NRI, I] the step's reward components (kp.rcomp)
 };
 
+// The buffer pointers as VGPR values (QS_VPTR): a step kernel's uniform state outgrows the 102 SGPRs, and the
+// compiler then loads the kernel's pointer arguments in small batches, each waited for and spilled to VGPR lanes
+// before the next (five kernarg round trips at the start of the flavor-B mix kernel).  Moving them to VGPRs at
+// entry issues every argument load at once, waits once, and keeps them out of the SGPR budget (2 VGPRs each; the
+// per-lane addresses are VGPR arithmetic anyway).
+#ifndef QS_VPTR
+#define QS_VPTR 0   // measured slower on every flavor-B config (round 5: C3 8.00 vs 7.47 us); kept for A/B
+#endif
+template <class T, bool ON = true>
+__device__ __forceinline__ void vptr(T*& p) {
+#if QS_VPTR
+    if constexpr (!ON) return;
+    uint64_t x = reinterpret_cast<uint64_t>(p);
+    asm volatile("" : "+v"(x));
+    // back through a global (address space 1) pointer: the accesses stay global_* (a plain cast would make them
+    // generic -> flat_*)
+    typedef __attribute__((address_space(1))) T GT;
+    p = (T*)(reinterpret_cast<GT*>(x));
+#else
+    (void)p;
+#endif
+}
+// ON: the kernels whose VGPR budget has the room (flavor B up to 16 drone slots: 181 -> 226 VGPRs at C3, still two
+// waves per SIMD; the 32-slot kernel would cross 256 and lose its second wave)
+template <bool ON>
+__device__ __forceinline__ void vptr_bufs(Bufs& b) {
+    vptr<float, ON>(b.st); vptr<int32_t, ON>(b.ist); vptr<int32_t, ON>(b.env); vptr<float, ON>(b.envf);
+    vptr<float2, ON>(b.obst); vptr<float, ON>(b.stale); vptr<float, ON>(b.obs); vptr<float, ON>(b.term);
+    vptr<float, ON>(b.rew); vptr<uint8_t, ON>(b.done); vptr<uint8_t, ON>(b.rinfo); vptr<const float, ON>(b.act);
+    vptr<const uint8_t, ON>(b.mask); vptr<unsigned long long, ON>(b.stats); vptr<float, ON>(b.estats);
+    vptr<float, ON>(b.rcomp);
+}
+
 // Diagnostic phase stamps (build with -DQS_STAMPS=1 only; never in the shipped library): lane 0 of
 // each block records s_memtime at phase boundaries; tools/phase_stamps.py reads them back.  A stamp waits
 // for nothing but its own counter read: a phase's time includes the memory waits its own code has.

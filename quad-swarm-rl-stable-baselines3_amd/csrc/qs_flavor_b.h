@@ -5,6 +5,12 @@
 #include "qs_scen.h"
 #include "qs_replay.h"
 
+#ifndef QS_SCW_LATE
+#define QS_SCW_LATE 0   // A/B: the scenario record's loads after the drone state's (default: before)
+#endif
+#ifndef QS_SCW_SKIP
+#define QS_SCW_SKIP 0   // diagnostic only (wrong results): no scenario-record loads, every env reads as static
+#endif
 #ifndef QS_PAIR_ROUNDS
 #define QS_PAIR_ROUNDS 1   // drone-pair impulses in rounds of disjoint pairs (else one pair per iteration)
 #endif
@@ -817,9 +823,10 @@ __device__ __forceinline__ void impulses_wide(const KP& kp, const Rng& rng, floa
 }
 
 template <int NPAD, bool OBST>
-__global__ __launch_bounds__(StepGeo<NPAD>::WGS) void step_kernel(const KP* __restrict__ kpp, Bufs b, RBufs r, RP rp) {
+__global__ __launch_bounds__(StepGeo<NPAD>::WGS) void step_kernel(const KP* __restrict__ kpp, Bufs b, const RArgs* __restrict__ rargs) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     QS_BIND_KP(kpp);
+    vptr_bufs<(NPAD <= 16)>(b);
     const uint32_t seed = kpm.seed;
     QS_STAMP_DECL
     QS_RTSTAMP(12);
@@ -887,14 +894,23 @@ __global__ __launch_bounds__(StepGeo<NPAD>::WGS) void step_kernel(const KP* __re
     const bool SCEN_STEP = SCEN && kp.scen_b != SC_STATIC_DIFF_GOAL;   // static_diff_goal's step() does nothing
     constexpr int SRW = (SC_WORDS + LPE - 1) / LPE;
     uint32_t scw[SRW];
+    auto load_scw = [&]() {
 #pragma unroll
-    for (int t = 0; t < SRW; ++t) {
-        const int w = li + LPE * t;
-        scw[t] = (SCEN_STEP && envok && w < SC_WORDS) ? scen_word(kp, b, env, w) : 0u;
-    }
+        for (int t = 0; t < SRW; ++t) {
+            const int w = li + LPE * t;
+            scw[t] = (SCEN_STEP && !QS_SCW_SKIP && envok && w < SC_WORDS) ? scen_word(kp, b, env, w) : 0u;
+        }
+    };
+#if !QS_SCW_LATE
+    load_scw();
+#endif
     Drone d;   // every sub-lane holds the whole drone
     DroneWords<Q, LW> dw;
     load_words_q<Q, LW, NIW>(kp, b, g, q, dw, kp.stats ? LW : DW);
+#if QS_SCW_LATE
+    // after the state words: the unpack's wait (in-order vmcnt) then does not include the record's 27 rows
+    load_scw();
+#endif
     __builtin_amdgcn_sched_barrier(0);
     const Rng rng = env_rng(seed, tick0, episode);
     // The step's regular draws: Philox block k of {OU 0, sensor 0, sensor 1, sensor 2} on sub-lane
@@ -1290,6 +1306,7 @@ __global__ __launch_bounds__(StepGeo<NPAD>::WGS) void step_kernel(const KP* __re
     // scenario record is stored only where it changed.
     float obs_goal[3] = {d.goal[0], d.goal[1], d.goal[2]};
     float* stab = scen_tab(lds, kp, SLOTS) + el * scen_stride<NPAD>();
+    QS_STAMP(18);   // sub-phases of "impulses+scenario+state store" (slots 18-21)
     if (SCEN_STEP) {
         uint32_t* srec = reinterpret_cast<uint32_t*>(stab + 2 * (NPAD + 4) * 4);
         if (q == 0 && di < kp.N) { stab[4 * di] = d.goal[0]; stab[4 * di + 1] = d.goal[1]; stab[4 * di + 2] = d.goal[2]; }
@@ -1299,6 +1316,7 @@ __global__ __launch_bounds__(StepGeo<NPAD>::WGS) void step_kernel(const KP* __re
             if (envok && w < SC_WORDS) srec[w] = scw[t];
         }
         lds_sync();
+        QS_STAMP(19);
         const bool sact = active && scen_acts(kp, (int)srec[0], (int)srec[2], tick);
         if (ec.wany(sact)) {
             bool via = false;
@@ -1312,6 +1330,7 @@ __global__ __launch_bounds__(StepGeo<NPAD>::WGS) void step_kernel(const KP* __re
                     else if (ch == 1) scen_store_size(kp, b, env, sc);
                 }
             }
+            QS_STAMP(20);
             if (ec.wany(via)) {   // the shuffled goals: table B's row of the drone
                 lds_sync();
                 if (via)
@@ -1322,6 +1341,7 @@ __global__ __launch_bounds__(StepGeo<NPAD>::WGS) void step_kernel(const KP* __re
         if (upd)
             for (int k = 0; k < 3; ++k) obs_goal[k] = d.goal[k];
     }
+    QS_STAMP(21);
 
     // The drone state is final here (unless its env resets below, which stores it again): storing it now
     // lets its write-through bytes drain while the observations are computed.
@@ -1412,7 +1432,8 @@ __global__ __launch_bounds__(StepGeo<NPAD>::WGS) void step_kernel(const KP* __re
                 const int T = kpm.ep_len + 1;
 #pragma unroll
                 for (int k = 0; k < 3; ++k) row[QS_ES_D1 + k] = dsum[k] / (float)min(kp.st_win[k], T) / kp.dt;
-                row[QS_ES_REPLAY] = (r.ri != nullptr && r.ri[QS_R_SAVED * E + env]) ? 1.f : 0.f;
+                const int32_t* rri = gptr<int32_t>(rargs->ri);
+                row[QS_ES_REPLAY] = (rri != nullptr && rri[QS_R_SAVED * E + env]) ? 1.f : 0.f;
             }
             // QuadrotorEnvMulti.reset zeroes the statistics (:487-509): the drone's entries go out with the reset
             // drone's state store below, the env's counters from the lanes that hold them
@@ -1514,12 +1535,14 @@ __global__ __launch_bounds__(StepGeo<NPAD>::WGS) void step_kernel(const KP* __re
     }
     guard_count(b, obs_bad, rew_bad, state_bad);
     QS_STAMP(10);
+    const RBufs r = load_rbufs(rargs);
     if (r.ri != nullptr) {   // experience replay on (uniform): ExperienceReplayWrapper.step of every env (:124-180)
         // the step's global stores above are read back by other lanes of the wave: workgroup-scope
         // release/acquire (one wave per workgroup, one L1)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         if (WIDE) lds_sync();   // the env's other wave has made its stores too
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const RP rp = rargs->p;
         if (env < kp.E) replay_env<true>(kp, kpm, b, r, rp, seed, env, lane % LPE, LPE);
     }
     QS_STAMP(11);

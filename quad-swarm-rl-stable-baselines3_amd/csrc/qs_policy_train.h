@@ -478,7 +478,10 @@ namespace pol {
 // hi / lo, three MFMAs per product as mfma_layer_x3.  A block's 16-row step: the 16 x H tiles of G and A staged
 // TRANSPOSED in LDS ([n][r] / [k][r], 16 r + 8 padding halves per row), so that a lane's MFMA operand -- 8 consecutive
 // rows r of one column -- is one ds_read_b128; wave w owns output rows n in [w H/4, (w+1) H/4), all H columns k.
-// The next step's rows are loaded into registers while the current step's MFMAs run (double-buffered tiles).
+// Staging: thread t owns column t % H and rows (t / H) RPT .. of the step (coalesced 4-byte row loads; its column's
+// rows leave as ds_write_b128 at a 48-byte column stride, conflict-free); the next step's rows are loaded into
+// registers while the current step's MFMAs run (double-buffered tiles), which are issued product by product over
+// all 16 (H = 256) output tiles (no back-to-back dependent MFMAs).
 // ------------------------------------------------------------------------------------------------------------------
 constexpr int DW_STEP = 16, DW_LDR = DW_STEP + 8;   // rows per step; LDS row stride in halves (48 B)
 
@@ -489,58 +492,44 @@ template <int H>
 __global__ __launch_bounds__(NTHR, 1) void dw_x3_kernel(const float* __restrict__ G, const float* __restrict__ A,
                                                         const float* __restrict__ gs, long R, int steps_per_block,
                                                         float* __restrict__ part) {
-    constexpr int NT = H / 128, KT = H / 32, L4 = H / 4, NITEM = L4 * (DW_STEP / 4);
-    constexpr int IPT = (NITEM + NTHR - 1) / NTHR;   // staging items per thread: (column quad, row quad)
+    constexpr int NT = H / 128, KT = H / 32, TPC = NTHR / H, RPT = DW_STEP / TPC;   // threads per column, rows each
+    static_assert(RPT % 8 == 0, "a thread's rows leave as whole 8-row (16-byte) groups");
     extern __shared__ float4 smem4[];
     _Float16* lds = reinterpret_cast<_Float16*>(smem4);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int sc = tid % H, sr = (tid / H) * RPT;   // staging: column, first row of the step
     const long r_begin = (long)blockIdx.x * steps_per_block * DW_STEP;
     auto buf = [&](int b, int which) { return lds + ((size_t)b * 4 + which) * H * DW_LDR; };   // 0 Gh 1 Gl 2 Ah 3 Al
-    float4 gv[IPT][4], av[IPT][4];
+    const float sg = gs[sc];
+    float gv[RPT], av[RPT];
     auto load = [&](int s) {
 #pragma unroll
-        for (int it = 0; it < IPT; ++it) {
-            const int e = tid + it * NTHR;
-            const int n4 = e % L4, rq = e / L4;
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const long r = r_begin + (long)s * DW_STEP + 4 * rq + u;
-                const bool ok = e < NITEM && r < R && s < steps_per_block;
-                const long rr = ok ? r : 0;
-                const float okf = ok ? 1.f : 0.f;
-                const float4 g = *reinterpret_cast<const float4*>(G + rr * H + 4 * n4);
-                const float4 a = *reinterpret_cast<const float4*>(A + rr * H + 4 * n4);
-                gv[it][u] = make_float4(g.x * okf, g.y * okf, g.z * okf, g.w * okf);
-                av[it][u] = make_float4(a.x * okf, a.y * okf, a.z * okf, a.w * okf);
-            }
+        for (int u = 0; u < RPT; ++u) {
+            const long r = r_begin + (long)s * DW_STEP + sr + u;
+            const bool ok = r < R && s < steps_per_block;
+            const long rr = ok ? r : 0;
+            const float okf = ok ? 1.f : 0.f;
+            gv[u] = G[rr * H + sc] * okf;
+            av[u] = A[rr * H + sc] * okf;
         }
     };
-    typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
     auto stage = [&](int b) {
 #pragma unroll
-        for (int it = 0; it < IPT; ++it) {
-            const int e = tid + it * NTHR;
-            if (e >= NITEM) continue;
-            const int n4 = e % L4, rq = e / L4;
+        for (int o = 0; o < RPT; o += 8) {
+            f16x8 gh, gl, ah, al;
 #pragma unroll
-            for (int c = 0; c < 4; ++c) {   // column 4 n4 + c: its 4 rows as one 8-byte write per half
-                const int n = 4 * n4 + c;
-                const float sg = gs[n];
-                float g4[4], a4[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) { g4[u] = sg * f4at(gv[it][u], c); a4[u] = X3_SX * f4at(av[it][u], c); }
-                const f16x4 gh = {(_Float16)g4[0], (_Float16)g4[1], (_Float16)g4[2], (_Float16)g4[3]};
-                const f16x4 gl = {(_Float16)(g4[0] - (float)gh[0]), (_Float16)(g4[1] - (float)gh[1]),
-                                  (_Float16)(g4[2] - (float)gh[2]), (_Float16)(g4[3] - (float)gh[3])};
-                const f16x4 ah = {(_Float16)a4[0], (_Float16)a4[1], (_Float16)a4[2], (_Float16)a4[3]};
-                const f16x4 al = {(_Float16)(a4[0] - (float)ah[0]), (_Float16)(a4[1] - (float)ah[1]),
-                                  (_Float16)(a4[2] - (float)ah[2]), (_Float16)(a4[3] - (float)ah[3])};
-                const int off = n * DW_LDR + 4 * rq;
-                *reinterpret_cast<f16x4*>(buf(b, 0) + off) = gh;
-                *reinterpret_cast<f16x4*>(buf(b, 1) + off) = gl;
-                *reinterpret_cast<f16x4*>(buf(b, 2) + off) = ah;
-                *reinterpret_cast<f16x4*>(buf(b, 3) + off) = al;
+            for (int u = 0; u < 8; ++u) {
+                const float g = sg * gv[o + u], a = X3_SX * av[o + u];
+                gh[u] = (_Float16)g;
+                gl[u] = (_Float16)(g - (float)gh[u]);
+                ah[u] = (_Float16)a;
+                al[u] = (_Float16)(a - (float)ah[u]);
             }
+            const int off = sc * DW_LDR + sr + o;
+            *reinterpret_cast<f16x8*>(buf(b, 0) + off) = gh;
+            *reinterpret_cast<f16x8*>(buf(b, 1) + off) = gl;
+            *reinterpret_cast<f16x8*>(buf(b, 2) + off) = ah;
+            *reinterpret_cast<f16x8*>(buf(b, 3) + off) = al;
         }
     };
     f32x16 acc[NT][KT];
@@ -557,7 +546,7 @@ __global__ __launch_bounds__(NTHR, 1) void dw_x3_kernel(const float* __restrict_
     for (int s = 0; s < steps_per_block; ++s) {
         const int b = s & 1;
         if (s + 1 < steps_per_block) load(s + 1);   // next rows in flight during this step's MFMAs
-        f16x8 gh[NT], gl[NT];
+        f16x8 gh[NT], gl[NT], ah[KT], al[KT];
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
             const int n0 = (wave * NT + t) * 32;
@@ -566,17 +555,23 @@ __global__ __launch_bounds__(NTHR, 1) void dw_x3_kernel(const float* __restrict_
         }
 #pragma unroll
         for (int k = 0; k < KT; ++k) {
-            const f16x8 ah = *reinterpret_cast<const f16x8*>(buf(b, 2) + k * 32 * DW_LDR + aoff);
-            const f16x8 al = *reinterpret_cast<const f16x8*>(buf(b, 3) + k * 32 * DW_LDR + aoff);
-#pragma unroll
-            for (int t = 0; t < NT; ++t) {
-                // A's columns as the first operand, G's as the second: the result tile is [k][n], i.e. a lane
-                // holds output row n = lane & 31 (the layout of the store below; qs_policy.h acc_i / acc_n0)
-                acc[t][k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, gh[t], acc[t][k], 0, 0, 0);
-                acc[t][k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, gl[t], acc[t][k], 0, 0, 0);
-                acc[t][k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, gh[t], acc[t][k], 0, 0, 0);
-            }
+            ah[k] = *reinterpret_cast<const f16x8*>(buf(b, 2) + k * 32 * DW_LDR + aoff);
+            al[k] = *reinterpret_cast<const f16x8*>(buf(b, 3) + k * 32 * DW_LDR + aoff);
         }
+        // A's columns as the first operand, G's as the second: the result tile is [k][n], i.e. a lane holds output
+        // row n = lane & 31 (the layout of the store below; qs_policy.h acc_i / acc_n0)
+#pragma unroll
+        for (int k = 0; k < KT; ++k)
+#pragma unroll
+            for (int t = 0; t < NT; ++t) acc[t][k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[k], gh[t], acc[t][k], 0, 0, 0);
+#pragma unroll
+        for (int k = 0; k < KT; ++k)
+#pragma unroll
+            for (int t = 0; t < NT; ++t) acc[t][k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[k], gl[t], acc[t][k], 0, 0, 0);
+#pragma unroll
+        for (int k = 0; k < KT; ++k)
+#pragma unroll
+            for (int t = 0; t < NT; ++t) acc[t][k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[k], gh[t], acc[t][k], 0, 0, 0);
         if (s + 1 < steps_per_block) stage(b ^ 1);   // the other buffer: last read two steps ago (barrier below)
         __syncthreads();
     }
@@ -595,6 +590,52 @@ __global__ __launch_bounds__(NTHR, 1) void dw_x3_kernel(const float* __restrict_
                     make_float4(acc[t][k][4 * g] * inv, acc[t][k][4 * g + 1] * inv, acc[t][k][4 * g + 2] * inv,
                                 acc[t][k][4 * g + 3] * inv);
             }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------------------------
+// column reductions of a gradient G [R, H] (qs_colstats): block p walks rows [p rows_per, (p+1) rows_per), thread n
+// owns column n (blockDim = H): a coalesced row of H floats per step, max |g|, sum g and, with NX > 0, sum g X(r, c)
+// with the layer-0 input X of row r = q K + m (neighbour m of agent q; self row r % B) -- wave-uniform addresses,
+// scalar loads.  The bias gradients, the dW column scales and the layer-0 weight gradient in one pass; an empty
+// trailing part writes the identities.
+// ------------------------------------------------------------------------------------------------------------------
+template <int NX>
+__global__ __launch_bounds__(256) void colstats_kernel(const float* __restrict__ G, long R, int H, long rows_per,
+                                                       const float* __restrict__ obs, int stride, int nbr_off, int B,
+                                                       int K, int nd, int nx, float* __restrict__ pmx,
+                                                       float* __restrict__ psm, float* __restrict__ px) {
+    const int n = threadIdx.x;
+    const long r0 = (long)blockIdx.x * rows_per, r1 = r0 + rows_per < R ? r0 + rows_per : R;
+    float mx = 0.f, sm = 0.f, xs[NX > 0 ? NX : 1];
+#pragma unroll
+    for (int c = 0; c < (NX > 0 ? NX : 1); ++c) xs[c] = 0.f;
+    bool bad = false;
+    long q = r0 / K, rb = r0 % B;
+    int m = (int)(r0 - q * K);
+#pragma unroll 8
+    for (long r = r0; r < r1; ++r) {
+        const float g = G[r * H + n];
+        const float a = fabsf(g);
+        mx = fmaxf(mx, a);
+        bad |= !(a <= 3.4028235e38f);
+        sm += g;
+        if constexpr (NX > 0) {
+            const float* xn = obs + q * stride + nbr_off + (long)m * nd;
+            const float* xf = obs + rb * stride - nd;
+#pragma unroll
+            for (int c = 0; c < NX; ++c)
+                if (c < nx) xs[c] = fmaf(g, c < nd ? xn[c] : xf[c], xs[c]);
+        }
+        if (++m == K) { m = 0; ++q; }
+        if (++rb == B) rb = 0;
+    }
+    pmx[(long)blockIdx.x * H + n] = bad ? __builtin_inff() : mx;
+    psm[(long)blockIdx.x * H + n] = sm;
+    if constexpr (NX > 0) {
+#pragma unroll
+        for (int c = 0; c < NX; ++c)
+            if (c < nx) px[((long)blockIdx.x * nx + c) * H + n] = xs[c];
     }
 }
 

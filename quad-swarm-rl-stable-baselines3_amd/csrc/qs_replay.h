@@ -35,6 +35,27 @@ struct RBufs {
     uint32_t* store;   // [E, keep + bufsz, W]
 };
 
+// the flavor-B step kernel's replay arguments, in device memory after the KP block (rargs_of): read at the two
+// places that use them (the done path's stats row, the replay tail) instead of occupying 23 SGPRs (or, spilled,
+// serialising the kernel's argument loads) for the whole step
+struct RArgs {
+    uint64_t ri, crash, hist, perm, nrep, store;   // the RBufs pointers as integers (ri == 0: replay off)
+    RP p;
+};
+// an integer address -> a global (address space 1) pointer: the accesses through it stay global_* (a pointer loaded
+// from memory would be generic -> flat_*)
+template <class T>
+__device__ __forceinline__ T* gptr(uint64_t x) {
+    typedef __attribute__((address_space(1))) T GT;
+    return (T*)(reinterpret_cast<GT*>(x));
+}
+__device__ __forceinline__ RBufs load_rbufs(const RArgs* a) {
+    RBufs r;
+    r.ri = gptr<int32_t>(a->ri); r.crash = gptr<double>(a->crash); r.hist = gptr<double>(a->hist);
+    r.perm = gptr<int32_t>(a->perm); r.nrep = gptr<int32_t>(a->nrep); r.store = gptr<uint32_t>(a->store);
+    return r;
+}
+
 // Word w of env e's snapshot -> its live location (layout in quadswarm.h qs_replay_buffers.snap_words).
 // *episode is set for the env's episode counter, which a restore leaves alone.
 __device__ __forceinline__ uint32_t* snap_word(const KP& kp, const Bufs& b, int e, int w, bool* episode) {
@@ -51,7 +72,12 @@ __device__ __forceinline__ uint32_t* snap_word(const KP& kp, const Bufs& b, int 
     w -= n;
     if (w < QS_NE) { *episode = w == QS_E_EPISODE; return reinterpret_cast<uint32_t*>(b.env + (size_t)w * kp.E + e); }
     w -= QS_NE;
-    if (w < QS_NENVF) return reinterpret_cast<uint32_t*>(b.envf + (size_t)w * kp.E + e);
+    if (w < QS_NENVF) {   // the scenario floats are env-major inside their block (quadswarm.h QS_SC_NF)
+        if (w >= QS_ENVF_SC_SIZE && w < QS_ENVF_SC_SIZE + QS_SC_NF)
+            return reinterpret_cast<uint32_t*>(b.envf + (size_t)QS_ENVF_SC_SIZE * kp.E + (size_t)QS_SC_NF * e +
+                                               (w - QS_ENVF_SC_SIZE));
+        return reinterpret_cast<uint32_t*>(b.envf + (size_t)w * kp.E + e);
+    }
     w -= QS_NENVF;
     n = kp.obst ? 2 * kp.M : 0;
     if (w < n) return reinterpret_cast<uint32_t*>(b.obst) + (size_t)e * n + w;

@@ -30,33 +30,36 @@ struct Scen {
     float size, lo, hi, layer, speed, c[3], bz[9], c1[3], c2[3];
 };
 
+static_assert(QS_ENVF_SC_C2 + 3 - QS_ENVF_SC_SIZE == QS_SC_NF, "the scenario float block");
+// the env's scenario float k (row QS_ENVF_SC_SIZE + k) in the env-major block (quadswarm.h QS_SC_NF)
+__device__ __forceinline__ float* scf(float* f, int E, int env, int row) {
+    return f + (size_t)QS_ENVF_SC_SIZE * E + (size_t)QS_SC_NF * env + (row - QS_ENVF_SC_SIZE);
+}
 __device__ __forceinline__ void scen_load(const KP& kp, const Bufs& b, int env, Scen& s) {
     const int E = kp.E;
     s.mode = b.env[QS_E_SC_MODE * E + env]; s.form = b.env[QS_E_SC_FORM * E + env];
     s.period = b.env[QS_E_SC_PERIOD * E + env]; s.inc = b.env[QS_E_SC_INC * E + env];
-    const float* f = b.envf;
-    s.size = f[QS_ENVF_SC_SIZE * E + env]; s.lo = f[QS_ENVF_SC_LO * E + env]; s.hi = f[QS_ENVF_SC_HI * E + env];
-    s.layer = f[QS_ENVF_SC_LAYER * E + env]; s.speed = f[QS_ENVF_SC_SPEED * E + env];
+    const float* f = scf(b.envf, E, env, QS_ENVF_SC_SIZE);   // the env's 23 floats, row order
+    s.size = f[0]; s.lo = f[1]; s.hi = f[2]; s.layer = f[3]; s.speed = f[4];
     for (int i = 0; i < 3; ++i) {
-        s.c[i] = f[(QS_ENVF_SC_CENTER + i) * E + env];
-        s.c1[i] = f[(QS_ENVF_SC_C1 + i) * E + env];
-        s.c2[i] = f[(QS_ENVF_SC_C2 + i) * E + env];
+        s.c[i] = f[QS_ENVF_SC_CENTER - QS_ENVF_SC_SIZE + i];
+        s.c1[i] = f[QS_ENVF_SC_C1 - QS_ENVF_SC_SIZE + i];
+        s.c2[i] = f[QS_ENVF_SC_C2 - QS_ENVF_SC_SIZE + i];
     }
-    for (int i = 0; i < 9; ++i) s.bz[i] = f[(QS_ENVF_SC_BEZIER + i) * E + env];
+    for (int i = 0; i < 9; ++i) s.bz[i] = f[QS_ENVF_SC_BEZIER - QS_ENVF_SC_SIZE + i];
 }
 __device__ __forceinline__ void scen_store(const KP& kp, const Bufs& b, int env, const Scen& s) {
     const int E = kp.E;
     b.env[QS_E_SC_MODE * E + env] = s.mode; b.env[QS_E_SC_FORM * E + env] = s.form;
     b.env[QS_E_SC_PERIOD * E + env] = s.period; b.env[QS_E_SC_INC * E + env] = s.inc;
-    float* f = b.envf;
-    f[QS_ENVF_SC_SIZE * E + env] = s.size; f[QS_ENVF_SC_LO * E + env] = s.lo; f[QS_ENVF_SC_HI * E + env] = s.hi;
-    f[QS_ENVF_SC_LAYER * E + env] = s.layer; f[QS_ENVF_SC_SPEED * E + env] = s.speed;
+    float* f = scf(b.envf, E, env, QS_ENVF_SC_SIZE);
+    f[0] = s.size; f[1] = s.lo; f[2] = s.hi; f[3] = s.layer; f[4] = s.speed;
     for (int i = 0; i < 3; ++i) {
-        f[(QS_ENVF_SC_CENTER + i) * E + env] = s.c[i];
-        f[(QS_ENVF_SC_C1 + i) * E + env] = s.c1[i];
-        f[(QS_ENVF_SC_C2 + i) * E + env] = s.c2[i];
+        f[QS_ENVF_SC_CENTER - QS_ENVF_SC_SIZE + i] = s.c[i];
+        f[QS_ENVF_SC_C1 - QS_ENVF_SC_SIZE + i] = s.c1[i];
+        f[QS_ENVF_SC_C2 - QS_ENVF_SC_SIZE + i] = s.c2[i];
     }
-    for (int i = 0; i < 9; ++i) f[(QS_ENVF_SC_BEZIER + i) * E + env] = s.bz[i];
+    for (int i = 0; i < 9; ++i) f[QS_ENVF_SC_BEZIER - QS_ENVF_SC_SIZE + i] = s.bz[i];
 }
 
 // draw source: one Philox word per draw, the last block cached (draws are sequential)
@@ -401,15 +404,25 @@ __device__ void scen_step(const KP& kp, Scen& s, int tick, SDraw& sd, float* g, 
 // per-row expressions
 __device__ __forceinline__ void sc_row(int f, int n, int per_layer, float size, float layer, const float* c, int i,
                                        float* gi) {
+    // n: the row count as an integer constant of the specialised kernel where the JIT knows it (index arithmetic
+    // only: exact, folded); per_layer is sc_per_layer(f), a literal in each branch (8 circles, 50 grids); the
+    // sphere's float geometry takes n through an opaque copy (sc_num: no constant-folded transcendentals)
+    (void)per_layer;
     if (f <= F_CIRCLE_YZ) {
-        const int whole = n / per_layer, rest = n % per_layer;
-        const int cur = n <= per_layer ? n : ((i / per_layer) < whole ? per_layer : rest);
-        const float rev = (float)(i % cur) / (float)cur;
+        constexpr int PL = 8;
+        int idx = i, cur = n;   // n <= 8 (one layer): i % n = i
+        if (n > PL) {
+            const int whole = n / PL, rest = n % PL;
+            cur = (i / PL) < whole ? PL : rest;
+            idx = i % cur;
+        }
+        const float rev = (float)idx / (float)cur;
         sc_by_formation(f, size * __builtin_amdgcn_cosf(rev), size * __builtin_amdgcn_sinf(rev),
-                        (float)(i / per_layer) * layer, gi);
+                        (float)(i / PL) * layer, gi);
         gi[0] += c[0]; gi[1] += c[1]; gi[2] += c[2];
     } else if (f == F_SPHERE) {
-        const int m = n < 3 ? 3 : n;
+        int m = n < 3 ? 3 : n;
+        asm volatile("" : "+v"(m));
         const float x = 0.1f + 1.2f * (float)m;
         const float start = -1.f + 1.f / ((float)m - 1.f), inc = (2.f - 2.f / ((float)m - 1.f)) / ((float)m - 1.f);
         const float s = start + (float)i * inc;
@@ -425,11 +438,12 @@ __device__ __forceinline__ void sc_row(int f, int n, int per_layer, float size, 
         gi[1] = size * (float)((i / fd) % fd);
         gi[2] = size * (float)(i % fd);
     } else {
+        constexpr int PL = 50;
         int d1, d2, r1 = 1, r2 = 1;
-        sc_grid_dims(n <= per_layer ? n : per_layer, d1, d2);
-        if (n > per_layer && n % per_layer) sc_grid_dims(n % per_layer, r1, r2);
-        const int whole = n / per_layer, L = i / per_layer;
-        const bool full = n <= per_layer || L < whole;
+        sc_grid_dims(n <= PL ? n : PL, d1, d2);
+        if (n > PL && n % PL) sc_grid_dims(n % PL, r1, r2);
+        const int whole = n / PL, L = i / PL;
+        const bool full = n <= PL || L < whole;
         const int a = full ? d1 : r1, b2 = full ? d2 : r2;
         sc_by_formation(f, size * (float)(i % b2), size * (float)((i / b2) % a), (float)L * layer, gi);
     }
@@ -455,13 +469,15 @@ __device__ __forceinline__ void sc_center(int f, int n, int per_layer, float siz
             if (++u == fd) { u = 0; if (++v == fd) { v = 0; ++w; } }
         }
     } else {
+        (void)per_layer;
+        constexpr int PL = 50;   // sc_per_layer of the grids
         int d1, d2, r1 = 1, r2 = 1;
-        sc_grid_dims(n <= per_layer ? n : per_layer, d1, d2);
-        if (n > per_layer && n % per_layer) sc_grid_dims(n % per_layer, r1, r2);
-        const int whole = n / per_layer;
+        sc_grid_dims(n <= PL ? n : PL, d1, d2);
+        if (n > PL && n % PL) sc_grid_dims(n % PL, r1, r2);
+        const int whole = n / PL;
         int L = 0, jl = 0, a = d1, b2 = d2, u = 0, v = 0;   // layer, index in layer, j % b2, (j / b2) % a
         for (int j = 0; j < n; ++j) {
-            if (jl == per_layer) {
+            if (jl == PL) {
                 ++L;
                 jl = 0;
                 const bool full = n <= per_layer || L < whole;
@@ -507,11 +523,11 @@ __device__ __forceinline__ bool scen_acts(const KP& kp, int mode, int period, in
 }
 
 // the scenario record of an env as 27 words (scen_load's fields): 0-3 mode, form, period, inc (env rows
-// QS_E_SC_MODE..); 4-26 the env_f rows QS_ENVF_SC_SIZE.. (size lo hi layer speed c[3] bz[9] c1[3] c2[3])
+// QS_E_SC_MODE..); 4-26 the env's env-major env_f run QS_ENVF_SC_SIZE.. (size lo hi layer speed c[3] bz[9] c1[3] c2[3])
 constexpr int SC_WORDS = 27;
 __device__ __forceinline__ uint32_t scen_word(const KP& kp, const Bufs& b, int env, int w) {
     return w < 4 ? (uint32_t)b.env[(QS_E_SC_MODE + w) * kp.E + env]
-                 : __float_as_uint(b.envf[(QS_ENVF_SC_SIZE + w - 4) * kp.E + env]);
+                 : __float_as_uint(*scf(b.envf, kp.E, env, QS_ENVF_SC_SIZE + w - 4));
 }
 __device__ __forceinline__ void scen_from_words(const uint32_t* r, Scen& s) {
     s.mode = (int)r[0]; s.form = (int)r[1]; s.period = (int)r[2]; s.inc = (int)r[3];
@@ -531,7 +547,7 @@ __device__ __forceinline__ void scen_from_words(const uint32_t* r, Scen& s) {
 // Returns what of the scenario record changed: 0 nothing, 1 size / inc / speed, 2 more (the whole record).
 __device__ __forceinline__ int scen_step_lane(const KP& kp, Scen& s, int tick, SDraw& sd, int di, const float* ta,
                                               float* tb, float* goal, bool& via_tab) {
-    const int N = sc_num(kp);
+    const int N = kp.N;   // index arithmetic (a constant of the specialised kernel); float geometry: sc_row / sc_num
     const float box = kp.spawn_box, cf = 1.f / kp.cdt;
     const int pl = sc_per_layer(s.form);
     const bool ev = s.period > 0 && tick % s.period == 0 && tick > 0;
@@ -661,8 +677,8 @@ __device__ __forceinline__ int scen_step_lane(const KP& kp, Scen& s, int tick, S
 }
 __device__ __forceinline__ void scen_store_size(const KP& kp, const Bufs& b, int env, const Scen& s) {
     b.env[QS_E_SC_INC * kp.E + env] = s.inc;
-    b.envf[QS_ENVF_SC_SIZE * kp.E + env] = s.size;
-    b.envf[QS_ENVF_SC_SPEED * kp.E + env] = s.speed;
+    *scf(b.envf, kp.E, env, QS_ENVF_SC_SIZE) = s.size;
+    *scf(b.envf, kp.E, env, QS_ENVF_SC_SPEED) = s.speed;
 }
 
 // LDS goal tables of the env (2 x (NPAD + 4) rows of 4 floats), after the obs / exchange tiles, then the env's

@@ -210,7 +210,7 @@ static qs_layout make_layout(const qs_config* c) {
                    (c->use_obstacles ? 9 : 0);
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     size_t o = 0;
-    L.params = o; o = al(o + sizeof(qs::KP));
+    L.params = o; o = al(al(o + sizeof(qs::KP)) + sizeof(qs::RArgs));   // KP, then the replay arguments (rargs_of)
     L.state = o; o = al(o + sizeof(float) * QS_NF * I);
     L.istate = o; o = al(o + sizeof(int32_t) * QS_NI * I);
     L.env = o; o = al(o + sizeof(int32_t) * QS_NE * E);
@@ -577,10 +577,25 @@ extern "C" int qs_create(const qs_config* c, int dev, void* ws, qs_handle** out)
     return QS_OK;
 }
 
+// the step kernel's replay arguments in device memory, after the KP block (zeroed with the workspace: replay off)
+static qs::RArgs* rargs_of(qs_handle* h) {
+    return (qs::RArgs*)((char*)h->ws + h->lay.params + ((sizeof(qs::KP) + 255) & ~(size_t)255));
+}
+static hipError_t rargs_sync(qs_handle* h) {
+    qs::RArgs a{};
+    if (h->rws) {
+        a.ri = (uint64_t)h->rb.ri; a.crash = (uint64_t)h->rb.crash; a.hist = (uint64_t)h->rb.hist;
+        a.perm = (uint64_t)h->rb.perm; a.nrep = (uint64_t)h->rb.nrep; a.store = (uint64_t)h->rb.store;
+    }
+    a.p = h->rp;
+    return hipMemcpy(rargs_of(h), &a, sizeof a, hipMemcpyHostToDevice);
+}
+
 static void replay_free(qs_handle* h) {
     if (h->rws && h->rws_owned) (void)hipFree(h->rws);
     h->rws = nullptr;
     h->rb = qs::RBufs{};
+    if (h->ws) (void)rargs_sync(h);
 }
 
 extern "C" int qs_destroy(qs_handle* h) {
@@ -639,10 +654,9 @@ static int launch(qs_handle* h, bool step, const float* act, const uint8_t* mask
     const size_t shm = shm_bytes(h->cfg, h->kp.obs_dim, h->npad, step, h->qb, h->qa);
     const bool a = h->cfg.flavor == QS_FLAVOR_A, ob = h->kp.obst != 0;
     // the flavor-B step kernel runs the replay wrapper in its tail (qs_replay.h); rb.ri == NULL: replay off
-    qs::RBufs rb = h->rws ? h->rb : qs::RBufs{};
-    qs::RP rp = h->rp;
+    const qs::RArgs* ra = rargs_of(h);
     if (hipFunction_t f = step ? h->jit_step : h->jit_reset) {
-        void* args[] = {(void*)&kpd, (void*)&b, (void*)&rb, (void*)&rp};   // the last two: B step only
+        void* args[] = {(void*)&kpd, (void*)&b, (void*)&ra};   // the last one: B step only
         QS_HIP(hipModuleLaunchKernel(f, grid.x, 1, 1, block.x, 1, 1, (unsigned)shm, s, args, nullptr));
         return QS_OK;
     }
@@ -652,10 +666,10 @@ static int launch(qs_handle* h, bool step, const float* act, const uint8_t* mask
             if (step) hipLaunchKernelGGL(qs::step_kernel_a<NP>, grid, block, shm, s, kpd, b);                  \
             else hipLaunchKernelGGL(qs::reset_kernel_a<NP>, grid, block, shm, s, kpd, b);                      \
         } else if (ob) {                                                                                       \
-            if (step) hipLaunchKernelGGL((qs::step_kernel<NP, true>), grid, block, shm, s, kpd, b, rb, rp);    \
+            if (step) hipLaunchKernelGGL((qs::step_kernel<NP, true>), grid, block, shm, s, kpd, b, ra);        \
             else hipLaunchKernelGGL((qs::reset_kernel<NP, true>), grid, block, shm, s, kpd, b);                \
         } else {                                                                                               \
-            if (step) hipLaunchKernelGGL((qs::step_kernel<NP, false>), grid, block, shm, s, kpd, b, rb, rp);   \
+            if (step) hipLaunchKernelGGL((qs::step_kernel<NP, false>), grid, block, shm, s, kpd, b, ra);       \
             else hipLaunchKernelGGL((qs::reset_kernel<NP, false>), grid, block, shm, s, kpd, b);               \
         }                                                                                                      \
         break;
@@ -672,7 +686,7 @@ static int launch(qs_handle* h, bool step, const float* act, const uint8_t* mask
                 if (step) hipLaunchKernelGGL(qs::step_kernel_a<128>, grid, block, shm, s, kpd, b);
                 else hipLaunchKernelGGL(qs::reset_kernel_a<128>, grid, block, shm, s, kpd, b);
             } else {
-                if (step) hipLaunchKernelGGL((qs::step_kernel<128, false>), grid, block, shm, s, kpd, b, rb, rp);
+                if (step) hipLaunchKernelGGL((qs::step_kernel<128, false>), grid, block, shm, s, kpd, b, ra);
                 else hipLaunchKernelGGL((qs::reset_kernel<128, false>), grid, block, shm, s, kpd, b);
             }
             break;
@@ -804,6 +818,7 @@ extern "C" int qs_replay_enable(qs_handle* h, const qs_replay_config* rc, void* 
     e = hipMemset(h->rws, 0, total);
     if (e == hipSuccess) e = hipMemcpy(h->rb.ri, ri.data(), 4 * ri.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(h->rb.perm, perm.data(), 4 * perm.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = rargs_sync(h);            // the step kernel's replay arguments (replay on)
     if (e == hipSuccess) e = hipDeviceSynchronize();   // null-stream init complete before any caller stream
     if (e != hipSuccess) {
         replay_free(h);
@@ -1243,6 +1258,29 @@ extern "C" int qs_attn_dw_x3(const float* G, const float* A, const float* col_sc
         return fail(QS_E_INVALID, "R >= 1, 1 <= n_parts <= 65535");
     hipStream_t st = (hipStream_t)stream;
     return H == 256 ? dw_launch<256>(G, A, col_scale, R, part, n_parts, st) : dw_launch<128>(G, A, col_scale, R, part, n_parts, st);
+}
+extern "C" int qs_colstats(const float* G, int64_t R, int32_t H, const float* obs, int32_t stride, int32_t nbr_off,
+                           int32_t B, int32_t K, int32_t nd, int32_t nx, float* pmx, float* psm, float* px,
+                           int32_t n_parts, void* stream) {
+    namespace P = qs::pol;
+    if (!G || !pmx || !psm) return fail(QS_E_INVALID, "NULL argument");
+    if (H != 128 && H != 256) return fail(QS_E_INVALID, "hidden size must be 128 or 256");
+    if (R < 1 || n_parts < 1 || n_parts > (1 << 24) || R * (int64_t)H >= (1ll << 40))
+        return fail(QS_E_INVALID, "R >= 1, 1 <= n_parts <= 2^24");
+    if (nx < 0 || nx > QS_COLSTATS_MAX_X) return fail(QS_E_INVALID, "nx out of range");
+    if (nx > 0 && (!obs || !px || B < 1 || K < 1 || nd < 0 || nd > nx || (int64_t)B * K != R || stride < nx ||
+                   nbr_off < 0 || nbr_off + (int64_t)K * nd > stride))
+        return fail(QS_E_INVALID, "layer-0 input: obs, part_x, B K = R, nd <= nx, the neighbour block inside a row");
+    hipStream_t st = (hipStream_t)stream;
+    const long rows_per = (long)((R + n_parts - 1) / n_parts);
+    if (nx > 0)
+        hipLaunchKernelGGL(P::colstats_kernel<QS_COLSTATS_MAX_X>, dim3((unsigned)n_parts), dim3(H), 0, st, G, (long)R, H,
+                           rows_per, obs, stride, nbr_off, B, K, nd, nx, pmx, psm, px);
+    else
+        hipLaunchKernelGGL(P::colstats_kernel<0>, dim3((unsigned)n_parts), dim3(H), 0, st, G, (long)R, H, rows_per,
+                           obs, stride, nbr_off, B > 0 ? B : 1, K > 0 ? K : 1, nd, 0, pmx, psm, px);
+    QS_HIP(hipGetLastError());
+    return QS_OK;
 }
 extern "C" int qs_attn_bwd2_x3(int32_t B, int32_t K, int32_t H, const qs_attn_tower* towers,
                                const qs_attn_train* trains, int32_t n_towers, void* stream) {

@@ -9,7 +9,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("QUADSWARM_LIB", os.path.join(HERE, "lib", "libquadswarm.so"))
 
-ABI_VERSION = 12
+ABI_VERSION = 13
 MAX_AGENTS = 128
 A_KMAX = 16   # flavor A, more than 64 drones: visible neighbours (qs_flavor_a.h QS_A_KMAX)
 MAX_DR_CHOICES = 8
@@ -47,6 +47,24 @@ EF_STALE, EF_SUCCESS, EF_HAS_POS, EF_NEWCOL, EF_FLOOR0 = 1, 2, 4, 8, 16
 ENVF_TARGET_X, ENVF_TARGET_Y, ENVF_CAPTURE = 0, 1, 2
 ENVF_SC_SIZE, ENVF_SC_LO, ENVF_SC_HI, ENVF_SC_LAYER, ENVF_SC_SPEED = 3, 4, 5, 6, 7
 ENVF_SC_CENTER, ENVF_SC_BEZIER, ENVF_SC_C1, ENVF_SC_C2, NENVF = 8, 11, 20, 23, 26
+SC_NF = 23   # the scenario floats ENVF_SC_SIZE .. ENVF_SC_C2 + 2, stored env-major inside their block (QS_SC_NF)
+
+
+def env_f_rows(env_f):
+    """A numpy copy of an env_f array [NENVF, E] with the env-major scenario block as [row][E] rows like the others
+    (row ENVF_SC_SIZE + k = scenario float k of every env)."""
+    E = env_f.shape[1]
+    out = env_f.copy()
+    out[ENVF_SC_SIZE:ENVF_SC_SIZE + SC_NF] = env_f[ENVF_SC_SIZE:ENVF_SC_SIZE + SC_NF].reshape(E, SC_NF).T
+    return out
+
+
+def env_f_from_rows(rows):
+    """The inverse of env_f_rows: [row][E] scenario rows back into the device's env-major block (numpy)."""
+    E = rows.shape[1]
+    out = rows.copy()
+    out[ENVF_SC_SIZE:ENVF_SC_SIZE + SC_NF] = rows[ENVF_SC_SIZE:ENVF_SC_SIZE + SC_NF].T.reshape(SC_NF, E)
+    return out
 
 
 class QsConfig(ctypes.Structure):
@@ -159,7 +177,7 @@ EXPORTS = ["qs_abi_version", "qs_last_error", "qs_struct_sizes", "qs_config_defa
            "qs_replay_config_default", "qs_replay_workspace_bytes", "qs_replay_enable", "qs_replay_disable", "qs_replay_buffers_get",
            "qs_attn_embed", "qs_attn_pool", "qs_attn_embed_x3", "qs_attn_pool_x3", "qs_curriculum_init",
            "qs_curriculum_step", "qs_curriculum_step_all", "qs_attn_embed_train_x3", "qs_attn_pool_train_x3",
-           "qs_attn_bwd1_x3", "qs_attn_bwd2_x3", "qs_attn_dw_x3"]
+           "qs_attn_bwd1_x3", "qs_attn_bwd2_x3", "qs_attn_dw_x3", "qs_colstats"]
 
 _lib = None
 
@@ -206,6 +224,7 @@ def lib():
         "qs_attn_bwd1_x3": ([I32, I32, I32, P(QsAttnTower), P(QsAttnTrain), I32, V], I32),
         "qs_attn_bwd2_x3": ([I32, I32, I32, P(QsAttnTower), P(QsAttnTrain), I32, V], I32),
         "qs_attn_dw_x3": ([V, V, V, ctypes.c_int64, I32, V, I32, V], I32),
+        "qs_colstats": ([V, ctypes.c_int64, I32, V, I32, I32, I32, I32, I32, I32, V, V, V, I32, V], I32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -38,25 +38,49 @@ def tower_params(enc):
             val[2].bias, att[0].weight, att[0].bias, att[2].weight, att[2].bias, att[4].weight, att[4].bias]
 
 
-def col_scales(G):
-    """Per-column power-of-two scales of a gradient [R, H] for qs_attn_dw_x3: s_n |G[:, n]| in [2^13, 2^14) (1 for an
-    all-zero or non-finite column).  The scales are built from their exponent bits: they must be exact powers of two
-    (torch.ldexp goes through pow on the device and is not), else the kernel's f16 hi / lo split of s G is taken from
-    a rounded product and near-tie elements lose an ulp of the hi half."""
-    m = G.abs().amax(0)
+def _pow2_scales(m):
+    """Power-of-two scales s with s m in [2^13, 2^14) (1 where m is 0 or not finite), built from their exponent bits:
+    they must be exact powers of two (torch.ldexp goes through pow on the device and is not), else the kernel's f16
+    hi / lo split of s G is taken from a rounded product and near-tie elements lose an ulp of the hi half."""
     _, e = torch.frexp(m)
     k = (14 - e.to(torch.int32)).clamp(-126, 127)
     s = ((k + 127) << 23).view(torch.float32)
     return torch.where((m > 0) & torch.isfinite(m), s, torch.ones_like(m)).contiguous()
 
 
-def dw_x3(G, A, parts=256, out=None):
+def col_scales(G):
+    """Per-column power-of-two scales of a gradient [R, H] for qs_attn_dw_x3: s_n |G[:, n]| in [2^13, 2^14) (1 for an
+    all-zero or non-finite column)."""
+    return _pow2_scales(G.abs().amax(0))
+
+
+def col_stats(G, obs=None, B=0, K=0, nbr_off=0, nd=0, nx=0, parts=None):
+    """One pass over G [R, H] (qs_colstats): (the dW column scales, the column sums, and with obs the layer-0 weight
+    gradient sum_r G[r, :]^T X(r, :) as [nx, H] -- X the encoder's layer-0 input of row r, neighbour features first,
+    then the self features -- or None)."""
+    R, H = G.shape
+    parts = parts or max(1, min(2048, (R + 255) // 256))
+    z = lambda *sh: torch.empty(*sh, dtype=torch.float32, device=G.device)  # noqa: E731
+    pmx, psm = z(parts, H), z(parts, H)
+    px = z(parts, nx, H) if nx else None
+    st = ctypes.c_void_p(torch.cuda.current_stream(G.device).cuda_stream)
+    NAT.check(NAT.lib().qs_colstats(ctypes.c_void_p(G.data_ptr()), R, H,
+                                    ctypes.c_void_p(obs.data_ptr() if obs is not None else 0),
+                                    obs.shape[1] if obs is not None else 0, nbr_off, B, K, nd, nx,
+                                    ctypes.c_void_p(pmx.data_ptr()), ctypes.c_void_p(psm.data_ptr()),
+                                    ctypes.c_void_p(px.data_ptr() if px is not None else 0), parts, st),
+              "qs_colstats")
+    return _pow2_scales(pmx.amax(0)), psm.sum(0), (px.sum(0) if px is not None else None)
+
+
+def dw_x3(G, A, parts=256, out=None, gs=None):
     """G^T A ([H, H]) over the rows of G, A [R, H] (|A| <= 1) on the split-f16 matrix cores (qs_attn_dw_x3), the row
-    range split over `parts` blocks and the parts summed here."""
+    range split over `parts` blocks and the parts summed here.  gs: G's column scales (col_scales / col_stats)."""
     R, H = G.shape
     parts = max(1, min(parts, (R + 15) // 16))
     buf = torch.empty(parts, H, H, dtype=torch.float32, device=G.device)
-    gs = col_scales(G)
+    if gs is None:
+        gs = col_scales(G)
     st = ctypes.c_void_p(torch.cuda.current_stream(G.device).cuda_stream)
     NAT.check(NAT.lib().qs_attn_dw_x3(ctypes.c_void_p(G.data_ptr()), ctypes.c_void_p(A.data_ptr()),
                                       ctypes.c_void_p(gs.data_ptr()), R, H, ctypes.c_void_p(buf.data_ptr()), parts, st),
@@ -80,8 +104,11 @@ class _Runner:
         self.dw_x3 = True   # the weight gradients on the split-f16 matrix cores (else torch fp32 GEMMs)
 
     def dw(self, G, A):
-        """dW = G^T A over the B K rows (A: tanh outputs)."""
-        return dw_x3(G, A) if self.dw_x3 else G.t().mm(A)
+        """(dW = G^T A over the B K rows (A: tanh outputs), the bias gradient sum_r G[r, :])."""
+        if not self.dw_x3:
+            return G.t().mm(A), G.sum(0)
+        gs, sums, _ = col_stats(G)
+        return dw_x3(G, A, gs=gs), sums
 
     def _alloc(self, B, dev):
         H, T, R = self.H, self.T, B * self.K
@@ -164,14 +191,14 @@ class _Runner:
         for i in range(self.T):
             b, w0 = self.buf[i], 14 * i
             gi = {}
-            gi["v2_w"], gi["v2_b"] = self.dw(b["dh_pre"], b["v1"]), b["dh_pre"].sum(0)
-            gi["v1_w"], gi["v1_b"] = self.dw(b["dv1_pre"], b["e2"]), b["dv1_pre"].sum(0)
-            gi["a2_w"], gi["a2_b"] = self.dw(b["da2_pre"], b["a1"]), b["da2_pre"].sum(0)
+            gi["v2_w"], gi["v2_b"] = self.dw(b["dh_pre"], b["v1"])
+            gi["v1_w"], gi["v1_b"] = self.dw(b["dv1_pre"], b["e2"])
+            gi["a2_w"], gi["a2_b"] = self.dw(b["da2_pre"], b["a1"])
             gi["a3_w"], gi["a3_b"] = b["dscore"].view(1, -1).mm(b["a2"]), b["dscore"].sum().view(1)
             dP = b["da1_pre"].view(K, B, H).sum(0)                     # rows j with j % B == b (the repeat tiling)
             a1_w = params[w0 + 8]
-            gi["a1_w"] = torch.cat((self.dw(b["da1_pre"], b["e2"]), dP.t().mm(b["e_mean"])), dim=1)
-            gi["a1_b"] = dP.sum(0)
+            dA_e, gi["a1_b"] = self.dw(b["da1_pre"], b["e2"])          # a1_b = sum_j da1_pre_j = sum_b dP_b
+            gi["a1_w"] = torch.cat((dA_e, dP.t().mm(b["e_mean"])), dim=1)
             torch.mm(dP, a1_w[:, H:], out=b["dem"])                    # dL/d e_mean
             for n in gi:
                 grads[w0 + _PARAMS.index(n)] = gi[n]
@@ -181,11 +208,15 @@ class _Runner:
         for i in range(self.T):
             b, w0 = self.buf[i], 14 * i
             de2_pre, de1_pre = b["de2p"], b["dh_pre"]
-            grads[w0 + 2], grads[w0 + 3] = self.dw(de2_pre, b["e1"]), de2_pre.sum(0)
-            # embedding_mlp[0] on cat(self_{j % B}, nbr_j): the self half summed over the K tiles first
-            g_self = de1_pre.view(K, B, H).sum(0).t().mm(self_obs)
-            grads[w0] = torch.cat((g_self, de1_pre.t().mm(nbr_rows)), dim=1)
-            grads[w0 + 1] = de1_pre.sum(0)
+            grads[w0 + 2], grads[w0 + 3] = self.dw(de2_pre, b["e1"])
+            # embedding_mlp[0] on cat(self_{j % B}, nbr_j): sum_j de1_pre_j^T [nbr_j | self_{j % B}] in one pass
+            if self.dw_x3:
+                _, grads[w0 + 1], gx = col_stats(de1_pre, obs, B, K, so, nd, nd + so)
+                grads[w0] = torch.cat((gx[nd:].t(), gx[:nd].t()), dim=1)
+            else:
+                g_self = de1_pre.view(K, B, H).sum(0).t().mm(self_obs)
+                grads[w0] = torch.cat((g_self, de1_pre.t().mm(nbr_rows)), dim=1)
+                grads[w0 + 1] = de1_pre.sum(0)
         self.pending = False
         self.obs = self.params = None
         return grads

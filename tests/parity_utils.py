@@ -74,7 +74,7 @@ SC_F = ("size", "lo", "hi", "layer", "speed")
 def scen_gpu_to_oracle(env, oenv):
     """Scenario attributes (env rows QS_E_SC_*, QS_ENVF_SC_*) -> the oracle envs' or_scen."""
     es = env.env_state.cpu().numpy()
-    ef = env.env_f.double().cpu().numpy()
+    ef = NAT.env_f_rows(env.env_f.double().cpu().numpy())
     for e in range(env.E):
         sc = oenv.envs[e].scen
         for k, n in enumerate(SC_I):
@@ -93,7 +93,7 @@ def scen_gpu_to_oracle(env, oenv):
 def scen_oracle_to_gpu(oenv, env):
     import torch
     es = env.env_state.cpu().numpy().copy()
-    ef = env.env_f.cpu().numpy().copy()
+    ef = NAT.env_f_rows(env.env_f.cpu().numpy())
     for e in range(env.E):
         sc = oenv.envs[e].scen
         for k, n in enumerate(SC_I):
@@ -107,7 +107,7 @@ def scen_oracle_to_gpu(oenv, env):
             for j in range(3):
                 ef[NAT.ENVF_SC_BEZIER + 3 * j + c, e] = sc.bz[j][c]
     env.env_state.copy_(torch.from_numpy(es))
-    env.env_f.copy_(torch.from_numpy(ef))
+    env.env_f.copy_(torch.from_numpy(NAT.env_f_from_rows(ef)))
 
 
 # the oracle's episode_extra_stats counters in QS_E_ST_* order
@@ -438,7 +438,7 @@ def oracle_to_gpu_a(oenv, env):
     N, E, I = env.N, env.E, env.I
     st = env.state.cpu().numpy().copy()
     es = env.env_state.cpu().numpy().copy()
-    ef = env.env_f.cpu().numpy().copy()
+    ef = NAT.env_f_rows(env.env_f.cpu().numpy())
     for g in range(I):
         d = oenv.drones[g]
         st[NAT.F_PID:NAT.F_PID + 20, g] = d.pid[:]
@@ -452,7 +452,7 @@ def oracle_to_gpu_a(oenv, env):
             st[NAT.F_HEADING, e * N + i] = ev.heading[i]
     env.state.copy_(torch.from_numpy(st))
     env.env_state.copy_(torch.from_numpy(es))
-    env.env_f.copy_(torch.from_numpy(ef))
+    env.env_f.copy_(torch.from_numpy(NAT.env_f_from_rows(ef)))
 
 
 def angle_columns_a(cfg):

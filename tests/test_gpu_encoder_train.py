@@ -17,7 +17,7 @@ torch = pytest.importorskip("torch")
 if not torch.cuda.is_available():  # pragma: no cover
     pytest.skip("no HIP device", allow_module_level=True)
 
-from quadswarm_amd.encoder_train import FusedAttentionTrain, dw_x3, tower_params  # noqa: E402
+from quadswarm_amd.encoder_train import FusedAttentionTrain, col_scales, col_stats, dw_x3, tower_params  # noqa: E402
 from quadswarm_amd.ppo import PolicyConfig, SwarmActorCritic  # noqa: E402
 
 
@@ -169,3 +169,29 @@ def test_dw_x3_matches_fp64(H, R):
     e_32 = ((t32.double() - want).abs() / scale).max().item()
     print(f"H={H} R={R}: dW relative error x3 {e_x3:.2e}, torch fp32 {e_32:.2e}")
     assert e_x3 < 1e-5 and e_x3 < 8 * e_32 + 1e-6
+
+
+@pytest.mark.parametrize("H,B,K,parts", [(256, 4099, 6, None), (128, 777, 1, 5), (256, 300, 7, 4096)])
+def test_colstats_matches_torch(H, B, K, parts):
+    """qs_colstats: the column scales (bitwise those of col_scales), the column sums and the layer-0 weight gradient
+    sum_j G_j^T [nbr_j | self_{j % B}] against torch in fp64, on ragged part splits (empty trailing parts)."""
+    g = torch.Generator(device="cuda").manual_seed(B)
+    so, nd = 18, 6
+    R = B * K
+    G = torch.randn(R, H, device="cuda", generator=g) * torch.exp2(torch.linspace(-20, 4, H, device="cuda"))
+    obs = torch.randn(B, so + K * nd + 3, device="cuda", generator=g)
+    gs, sums, gx = col_stats(G, obs, B, K, so, nd, nd + so, parts=parts)
+    assert torch.equal(gs, col_scales(G))
+    G64 = G.double()
+    want_sum = G64.sum(0)
+    assert ((sums.double() - want_sum).abs() / G64.abs().sum(0)).max().item() < 1e-6
+    nbr = obs[:, so:so + K * nd].reshape(R, nd).double()
+    slf = obs[:, :so].double().repeat(K, 1)
+    X = torch.cat((nbr, slf), dim=1)
+    want_x = X.t().mm(G64)                      # [nd + so, H]
+    scale = (X.abs().t().mm(G64.abs())).clamp_min(1e-300)
+    assert ((gx.double() - want_x).abs() / scale).max().item() < 1e-6
+    # a non-finite column gets scale 1 (and the sums carry the NaN)
+    G[5, 3] = float("nan")
+    gs2, sums2, _ = col_stats(G)
+    assert gs2[3].item() == 1.0 and torch.isnan(sums2[3]) and torch.equal(gs2[4:], gs[4:])

@@ -43,7 +43,7 @@ def goals_of(oenv):
 
 
 def check_scen_state(env, oenv, atol=2e-5):
-    es, ef = env.env_state.cpu().numpy(), np_(env.env_f)
+    es, ef = env.env_state.cpu().numpy(), NAT.env_f_rows(np_(env.env_f))
     for e in range(env.E):
         sc = oenv.envs[e].scen
         got_i = es[NAT.E_SC_MODE:NAT.E_SC_MODE + 4, e]

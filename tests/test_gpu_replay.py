@@ -30,7 +30,7 @@ def host_views(env):
     """The live buffers a snapshot covers, on the host as 32-bit words."""
     v = dict(state=env.state.cpu().numpy().view(np.int32), istate=env.istate.cpu().numpy(),
              stale=env.stale_vel.cpu().numpy().view(np.int32), env=env.env_state.cpu().numpy(),
-             envf=env.env_f.cpu().numpy().view(np.int32), obs=env.obs.cpu().numpy().view(np.int32))
+             envf=N.env_f_rows(env.env_f.cpu().numpy()).view(np.int32), obs=env.obs.cpu().numpy().view(np.int32))
     v["obst"] = env.obstacles.cpu().numpy().view(np.int32) if env.obstacles is not None else None
     return v
 

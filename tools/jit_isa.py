@@ -36,7 +36,7 @@ def main():
     npad = 1 << (cfg.num_agents - 1).bit_length()
     flavor_a = cfg.flavor == "A"
     kern = f"qs::step_kernel_a<{npad}>" if flavor_a else f"qs::step_kernel<{npad}, {'true' if cfg.use_obstacles else 'false'}>"
-    sig = "(const qs::KP*, qs::Bufs)" if flavor_a else "(const qs::KP*, qs::Bufs, qs::RBufs, qs::RP)"
+    sig = "(const qs::KP*, qs::Bufs)" if flavor_a else "(const qs::KP*, qs::Bufs, const qs::RArgs*)"
     src = ("#define QS_JIT 1\n#define QS_QB 4\n#define QS_QA 2\n#define QS_KP_WORDS " +
            ",".join(f"0x{w:08x}u" for w in words) + "\n" +
            f'#include "{"qs_flavor_a.h" if flavor_a else "qs_flavor_b.h"}"\n' +

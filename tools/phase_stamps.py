@@ -70,9 +70,21 @@ def main():
         d = np.diff(st[:, :12], axis=1)
         names = NAMES_B[1:]
     tot = d.sum(1)
+    sub = None
+    if cfg.flavor == "B" and (st[:, 18] != 0).any():   # the scenario sub-phases (slots 18-21)
+        seq = np.stack([st[:, 3], st[:, 18], st[:, 19], st[:, 21], st[:, 4]], axis=1)
+        sub = np.diff(seq, axis=1)
+        s20 = np.where(st[:, 20] != 0, st[:, 20] - st[:, 19], 0)
+        sub = np.concatenate([sub, s20[:, None]], axis=1)
+        sub_names = ["  forces/impulses", "  scen: tables + sync", "  scen: step (+ via)", "  state store",
+                     "  (of which scen step proper)"]
     print(f"wave cycles between the first and last stamp: median {np.median(tot):.0f}  p90 {np.percentile(tot, 90):.0f}")
     for k, name in enumerate(names):
         print(f"  {name:36s} {np.median(d[:, k]):8.0f} cycles  {100 * np.median(d[:, k]) / np.median(tot):5.1f} %")
+    if sub is not None:
+        for k, name in enumerate(sub_names):
+            print(f"  {name:36s} median {np.median(sub[:, k]):8.0f}  p90 {np.percentile(sub[:, k], 90):8.0f}  max "
+                  f"{sub[:, k].max():8.0f} cycles")
     # where the waves ran: HW_ID (gfx9 layout: wave slot 3:0, SIMD 5:4, CU 11:8, SH 12, SE 15:13) + XCC_ID
     hw, xcc = st[:, 14], st[:, 15] & 0xF
     simd_key = (xcc << 16) | (((hw >> 8) & 0xFF) << 2) | ((hw >> 4) & 3)
@@ -101,6 +113,9 @@ def main():
           f"start ns median {np.median(s_[slow]):.0f}")
     for k, name in enumerate(names):
         print(f"  {name:36s} {np.median(d[slow, k]):8.0f} cycles (max {d[slow, k].max():.0f})")
+    if sub is not None:
+        for k, name in enumerate(sub_names):
+            print(f"  {name:36s} {np.median(sub[slow, k]):8.0f} cycles (max {sub[slow, k].max():.0f})")
 
 
 if __name__ == "__main__":

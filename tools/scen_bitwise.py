@@ -40,7 +40,13 @@ def digest(mode, n, steps, src):
         obs, rew, done, _ = env.step(acts)
         for t in (obs, rew, done):
             h.update(t.detach().cpu().numpy().tobytes())
-    h.update(env.get_state())
+    # the final state: drone state, env ints and env floats with the scenario block as [row][E] rows (the current
+    # kernels store it env-major, ABI 13; the round-4 base as rows)
+    from quadswarm_amd import _native as NAT
+    ef = env.env_f.cpu().numpy()
+    h.update(env.state.cpu().numpy().tobytes())
+    h.update(env.env_state.cpu().numpy().tobytes())
+    h.update((ef if src else NAT.env_f_rows(ef)).tobytes())
     env.close()
     return h.hexdigest()
 
