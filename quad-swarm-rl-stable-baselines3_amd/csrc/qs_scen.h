@@ -128,7 +128,10 @@ __device__ __forceinline__ void sc_mode_params(int mode, int& nform, float& low,
 }
 __device__ __forceinline__ int sc_per_layer(int f) { return (f == F_GRID_H || f == F_GRID_XZ || f == F_GRID_YZ) ? 50 : 8; }
 __device__ __forceinline__ void sc_grid_dims(int num, int& d1, int& d2) {   // get_grid_dim_number (utils.py:124-136)
-    int g = (int)floorf(fsqrt((float)num) + 1e-6f);
+    // floor(sqrt(num) + 1e-6) is the integer square root for every num this sees (a non-square's root is over 1e-6
+    // below the next integer up to num ~ 1e11): integer arithmetic, folded away when num is a JIT constant
+    int g = 0;
+    while ((g + 1) * (g + 1) <= num) ++g;
     while (g > 1 && num % g != 0) --g;
     d1 = g;
     d2 = num / g;
@@ -476,6 +479,7 @@ __device__ __forceinline__ void sc_center(int f, int n, int per_layer, float siz
         if (n > PL && n % PL) sc_grid_dims(n % PL, r1, r2);
         const int whole = n / PL;
         int L = 0, jl = 0, a = d1, b2 = d2, u = 0, v = 0;   // layer, index in layer, j % b2, (j / b2) % a
+        float s0 = 0.f, s1 = 0.f, sl = 0.f;
         for (int j = 0; j < n; ++j) {
             if (jl == PL) {
                 ++L;
@@ -486,12 +490,16 @@ __device__ __forceinline__ void sc_center(int f, int n, int per_layer, float siz
                 u = j % b2;
                 v = (j / b2) % a;
             }
-            float gj[3];
-            sc_by_formation(f, size * (float)u, size * (float)v, (float)L * layer, gj);
-            mean[0] += gj[0]; mean[1] += gj[1]; mean[2] += gj[2];
+            // the row's three terms summed per term and placed by the formation's axes after the loop: each
+            // coordinate's sum sees the same values in the same order as sc_generate's (no branch per row)
+            const float p0 = size * (float)u, p1 = size * (float)v, pl = (float)L * layer;   // rounded products:
+            s0 += p0;                                                                          // separate statements
+            s1 += p1;                                                                          // (no contraction
+            sl += pl;                                                                          // into FMAs)
             ++jl;
             if (++u == b2) { u = 0; if (++v == a) v = 0; }
         }
+        sc_by_formation(f, s0, s1, sl, mean);
     }
     for (int k = 0; k < 3; ++k) mean[k] /= (float)n;
     for (int k = 0; k < 3; ++k) gi[k] = gi[k] - mean[k] + c[k];
