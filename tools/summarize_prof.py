@@ -68,8 +68,12 @@ def main():
 
     import subprocess
     try:   # the tree the profiles were taken on (gpurun snapshots the working tree: dirty = uncommitted edits)
-        head = subprocess.run(["git", "-C", ROOT, "describe", "--always", "--dirty"], capture_output=True,
+        head = subprocess.run(["git", "-C", ROOT, "rev-parse", "--short", "HEAD"], capture_output=True,
                               text=True).stdout.strip()
+        # dirty = uncommitted edits to tracked files outside profiles/ (the summaries this script writes there)
+        dirty = subprocess.run(["git", "-C", ROOT, "status", "--porcelain", "--untracked-files=no", "--", ".",
+                                ":(exclude)profiles"], capture_output=True, text=True).stdout.strip()
+        head += "-dirty" if dirty else ""
     except OSError:
         head = None
     res = {"kernel": stats.get("name"), "config": args.config, "tree": head, "kernel_trace": stats,
