@@ -162,9 +162,13 @@ def test_one_step_from_identical_state(name):
         np.testing.assert_allclose(np_(f["pos"]), ostate(oenv, "pos"), atol=3e-5, err_msg=f"pos step {t}")
         np.testing.assert_allclose(np_(f["vel"]), ostate(oenv, "vel"), atol=5e-4, rtol=1e-3, err_msg=f"vel step {t}")
         # the PID's derivative terms divide step-to-step error changes by the tick (x100); the downwash case
-        # re-stacks its pairs every step, i.e. makes those changes large
-        # (and the 128-drone formations: 16 drones per goal column, 40 960 PID words a step)
-        pid_tol = 5e-3 if cfg.use_downwash or cfg.num_agents > 64 else 2e-3
+        # re-stacks its pairs every step, i.e. makes those changes large, and the goal scenarios move the goals
+        # through the hardware sin / cos (the oracle: libm).  Measured max |pid - oracle| (round 5, printed below):
+        # 1.4e-5 for the plain cases (n128 included), 2.2e-3 / 2.5e-3 mix128 / mix8, 2.4e-3 / 7.8e-4 dw8 / dw128,
+        # 2.3e-4 svs8 -- the bounds sit above those by 1.2-1.6x
+        moving = cfg.quads_mode in ("mix", "ep_lissajous3D", "ep_rand_bezier", "dynamic_same_goal", "dynamic_diff_goal",
+                                    "dynamic_formations", "swap_goals", "swarm_vs_swarm", "run_away")
+        pid_tol = 4e-3 if cfg.use_downwash else (3e-3 if moving else 2e-3)
         pid_worst = max(pid_worst, float(np.abs(np_(f["pid"]) - ostate(oenv, "pid")).max()))
         np.testing.assert_allclose(np_(f["pid"]), ostate(oenv, "pid"), atol=pid_tol, rtol=2e-3, err_msg=f"pid step {t}")
         tgt = np_(env.env_f[:2]).T
