@@ -659,19 +659,34 @@ template <int CTRL>
 __device__ __forceinline__ float dpp_f(float x) { return __int_as_float(dpp_i<CTRL>(__float_as_int(x))); }
 constexpr int quad_perm(int a, int b, int c, int d) { return a | (b << 2) | (c << 4) | (d << 6); }
 
+// Q = 8 (single-drone envs): the drone's 8 lanes are two quads of a 16-lane DPP row; the other quad's lane
+// (lane ^ 4) comes by row_shl:4 (lower quad) or row_shr:4 (upper quad)
+constexpr int DPP_ROW_SHL4 = 0x104, DPP_ROW_SHR4 = 0x114;
+__device__ __forceinline__ int xquad_i(int x) {
+    const int up = dpp_i<DPP_ROW_SHL4>(x), dn = dpp_i<DPP_ROW_SHR4>(x);
+    return (__lane_id() & 4) ? dn : up;
+}
+__device__ __forceinline__ float xquad_f(float x) { return __int_as_float(xquad_i(__float_as_int(x))); }
 // value of sub-lane K of this lane's drone
 template <int Q, int K>
 __device__ __forceinline__ float qbc(float x) {
     static_assert(K < Q, "sub-lane");
+    static_assert(Q == 1 || Q == 2 || Q == 4 || Q == 8, "sub-lanes per drone");
     if constexpr (Q == 1) return x;
     else if constexpr (Q == 2) return dpp_f<quad_perm(K, K, 2 + K, 2 + K)>(x);
-    else return dpp_f<quad_perm(K, K, K, K)>(x);
+    else if constexpr (Q == 4) return dpp_f<quad_perm(K, K, K, K)>(x);
+    else {   // lane K % 4 of each quad, then the quad that holds sub-lane K
+        const float v = dpp_f<quad_perm(K % 4, K % 4, K % 4, K % 4)>(x);
+        const float o = xquad_f(v);
+        return ((__lane_id() & 4) != 0) == (K >= 4) ? v : o;
+    }
 }
 // sum over the drone's sub-lanes: every lane gets the same bits ((a+b)+(c+d) == (c+d)+(a+b))
 template <int Q>
 __device__ __forceinline__ float qsum(float x) {
     if constexpr (Q >= 2) x += dpp_f<quad_perm(1, 0, 3, 2)>(x);
     if constexpr (Q >= 4) x += dpp_f<quad_perm(2, 3, 0, 1)>(x);
+    if constexpr (Q >= 8) x += xquad_f(x);
     return x;
 }
 // compile-time walk over the blocks of qdraws: block K lives on sub-lane K % Q, slot K / Q
@@ -693,6 +708,7 @@ __device__ __forceinline__ uint64_t qor(uint64_t m) {
     int lo = (int)(uint32_t)m, hi = (int)(uint32_t)(m >> 32);
     if constexpr (Q >= 2) { lo |= dpp_i<quad_perm(1, 0, 3, 2)>(lo); hi |= dpp_i<quad_perm(1, 0, 3, 2)>(hi); }
     if constexpr (Q >= 4) { lo |= dpp_i<quad_perm(2, 3, 0, 1)>(lo); hi |= dpp_i<quad_perm(2, 3, 0, 1)>(hi); }
+    if constexpr (Q >= 8) { lo |= xquad_i(lo); hi |= xquad_i(hi); }
     return (uint64_t)(uint32_t)lo | ((uint64_t)(uint32_t)hi << 32);
 }
 

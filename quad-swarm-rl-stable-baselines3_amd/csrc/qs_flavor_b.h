@@ -919,11 +919,13 @@ __global__ __launch_bounds__(StepGeo<NPAD>::WGS) void step_kernel(const KP* __re
     // are still in flight (the unpack below is the first wait on them).
     float zou[4], zs[12];
     {
-        float zr[4 / Q][4];
+        constexpr int ZT = (4 + Q - 1) / Q;   // blocks per sub-lane (Q = 8: sub-lanes 4-7 draw nothing)
+        float zr[ZT][4] = {};
 #pragma unroll
-        for (int t = 0; t < 4 / Q; ++t) {
+        for (int t = 0; t < ZT; ++t) {
             const int k = q + Q * t;
-            if (k == 0 || kp.sense) normals4(rng, gid, k == 0 ? S_OU : S_SENSOR, k == 0 ? 0u : (uint32_t)(k - 1), zr[t]);
+            if (k < 4 && (k == 0 || kp.sense))
+                normals4(rng, gid, k == 0 ? S_OU : S_SENSOR, k == 0 ? 0u : (uint32_t)(k - 1), zr[t]);
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {

@@ -1453,7 +1453,7 @@ static void jit_lanes(int* qb, int* qa) {
     for (auto kv : {std::make_pair("QS_QB", qb), std::make_pair("QS_QA", qa)})
         if (const char* v = getenv(kv.first)) {
             const int x = atoi(v);
-            if (x == 1 || x == 2 || x == 4) *kv.second = x;
+            if (x == 1 || x == 2 || x == 4 || (x == 8 && kv.second == qb)) *kv.second = x;   // 8: single-drone envs
         }
 }
 

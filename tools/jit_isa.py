@@ -37,7 +37,7 @@ def main():
     flavor_a = cfg.flavor == "A"
     kern = f"qs::step_kernel_a<{npad}>" if flavor_a else f"qs::step_kernel<{npad}, {'true' if cfg.use_obstacles else 'false'}>"
     sig = "(const qs::KP*, qs::Bufs)" if flavor_a else "(const qs::KP*, qs::Bufs, const qs::RArgs*)"
-    src = ("#define QS_JIT 1\n#define QS_QB 4\n#define QS_QA 2\n#define QS_KP_WORDS " +
+    src = (f"#define QS_JIT 1\n#define QS_QB {os.environ.get('QS_QB', 4)}\n#define QS_QA {os.environ.get('QS_QA', 2)}\n#define QS_KP_WORDS " +
            ",".join(f"0x{w:08x}u" for w in words) + "\n" +
            f'#include "{"qs_flavor_a.h" if flavor_a else "qs_flavor_b.h"}"\n' +
            f"template __global__ void {kern}{sig};\n")
