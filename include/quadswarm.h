@@ -522,16 +522,17 @@ int qs_attn_dw_x3(const float* G, const float* A, const float* col_scale, int64_
 /* Column reductions of a gradient G [R, H] in one pass over its rows (ABI 13; the update's bias gradients, the dW
  * column scales and layer 0's weight gradient, in place of torch's abs / amax / sum / skinny-GEMM passes), split
  * over n_parts row ranges, per part p and column n:
- *   part_max[p, n] = max |G[r, n]| (NaN / inf propagate), part_sum[p, n] = sum G[r, n],
+ *   part_max[p, n] = max |G[r, n]| (NaN / inf propagate), part_sum[p, n] = sum w[r] G[r, n] (row_w = w, or
+ *   NULL for w = 1: with row_w the dscore of the attention rows and G = a2 it is the score layer's weight gradient),
  *   part_x[p, c, n] = sum G[r, n] X(r, c) for c < nx (nx <= QS_COLSTATS_MAX_X; part_x may be NULL when nx = 0) with
  *   the layer-0 input of row r = k B + b of the attention encoder's repeat tiling (quad_multi_model.py:44-101):
  *   X(r, c) = obs[(r / K) * obs_stride + nbr_off + (r % K) * nd + c] for c < nd (neighbour k of row r / K, the
  *   reshape of the neighbour block), obs[(r % B) * obs_stride + c - nd] for nd <= c < nx (self.repeat(K, 1)).
  * H is 128 or 256. */
 #define QS_COLSTATS_MAX_X 32
-int qs_colstats(const float* G, int64_t R, int32_t H, const float* d_obs, int32_t obs_stride, int32_t nbr_off,
-                int32_t B, int32_t K, int32_t nd, int32_t nx, float* part_max, float* part_sum, float* part_x,
-                int32_t n_parts, void* stream);
+int qs_colstats(const float* G, int64_t R, int32_t H, const float* row_w, const float* d_obs, int32_t obs_stride,
+                int32_t nbr_off, int32_t B, int32_t K, int32_t nd, int32_t nx, float* part_max, float* part_sum,
+                float* part_x, int32_t n_parts, void* stream);
 
 /* sb_train's capture-radius curriculum on the device (ABI 11; replaces CurriculumCallback._on_step,
  * swarm_rl/custom_callbacks.py:441-468, which SB3 runs after every VecEnv step).  Flavor A.  The callback's state

@@ -595,40 +595,59 @@ __global__ __launch_bounds__(NTHR, 1) void dw_x3_kernel(const float* __restrict_
 
 // ------------------------------------------------------------------------------------------------------------------
 // column reductions of a gradient G [R, H] (qs_colstats): block p walks rows [p rows_per, (p+1) rows_per), thread n
-// owns column n (blockDim = H): a coalesced row of H floats per step, max |g|, sum g and, with NX > 0, sum g X(r, c)
-// with the layer-0 input X of row r = q K + m (neighbour m of agent q; self row r % B) -- wave-uniform addresses,
-// scalar loads.  The bias gradients, the dW column scales and the layer-0 weight gradient in one pass; an empty
-// trailing part writes the identities.
+// owns column n (blockDim = H): a coalesced row of H floats per step, max |g|, sum w_r g (w: optional row weights)
+// and, with NX > 0, sum g X(r, c) with the layer-0 input X of row r = q K + m (neighbour m of agent q; self row
+// r % B).  X is gathered a chunk of CH rows at a time into LDS by the whole block (each value once), then read as
+// LDS broadcasts by every column's thread.  The bias gradients, the dW column scales, the layer-0 weight gradient
+// and the score layer's weight gradient (w = dscore) in one pass each; an empty trailing part writes identities.
 // ------------------------------------------------------------------------------------------------------------------
 template <int NX>
 __global__ __launch_bounds__(256) void colstats_kernel(const float* __restrict__ G, long R, int H, long rows_per,
-                                                       const float* __restrict__ obs, int stride, int nbr_off, int B,
-                                                       int K, int nd, int nx, float* __restrict__ pmx,
-                                                       float* __restrict__ psm, float* __restrict__ px) {
+                                                       const float* __restrict__ rw, const float* __restrict__ obs,
+                                                       int stride, int nbr_off, int B, int K, int nd, int nx,
+                                                       float* __restrict__ pmx, float* __restrict__ psm,
+                                                       float* __restrict__ px) {
+    constexpr int CH = 64;   // rows per staged chunk of X
+    __shared__ float xs_lds[NX > 0 ? CH * NX : 1];
     const int n = threadIdx.x;
     const long r0 = (long)blockIdx.x * rows_per, r1 = r0 + rows_per < R ? r0 + rows_per : R;
     float mx = 0.f, sm = 0.f, xs[NX > 0 ? NX : 1];
 #pragma unroll
     for (int c = 0; c < (NX > 0 ? NX : 1); ++c) xs[c] = 0.f;
     bool bad = false;
-    long q = r0 / K, rb = r0 % B;
-    int m = (int)(r0 - q * K);
+    if constexpr (NX == 0) {
 #pragma unroll 8
-    for (long r = r0; r < r1; ++r) {
-        const float g = G[r * H + n];
-        const float a = fabsf(g);
-        mx = fmaxf(mx, a);
-        bad |= !(a <= 3.4028235e38f);
-        sm += g;
-        if constexpr (NX > 0) {
-            const float* xn = obs + q * stride + nbr_off + (long)m * nd;
-            const float* xf = obs + rb * stride - nd;
-#pragma unroll
-            for (int c = 0; c < NX; ++c)
-                if (c < nx) xs[c] = fmaf(g, c < nd ? xn[c] : xf[c], xs[c]);
+        for (long r = r0; r < r1; ++r) {
+            const float g = G[r * H + n];
+            const float a = fabsf(g);
+            mx = fmaxf(mx, a);
+            bad |= !(a <= 3.4028235e38f);
+            sm += rw ? rw[r] * g : g;
         }
-        if (++m == K) { m = 0; ++q; }
-        if (++rb == B) rb = 0;
+    } else {
+        for (long c0 = r0; c0 < r1; c0 += CH) {
+            const int rows = (int)(r1 - c0 < CH ? r1 - c0 : CH);
+            __syncthreads();   // the previous chunk's X has been read
+            for (int e = n; e < rows * nx; e += H) {   // 32-bit index arithmetic (the launcher checks R < 2^31)
+                const int i = e / nx, c = e - i * nx;
+                const int r = (int)c0 + i, q = r / K;
+                xs_lds[i * NX + c] = c < nd ? obs[(long)q * stride + nbr_off + (r - q * K) * nd + c]
+                                            : obs[(long)(r % B) * stride + (c - nd)];
+            }
+            __syncthreads();
+#pragma unroll 4
+            for (int i = 0; i < rows; ++i) {
+                const float g = G[(c0 + i) * H + n];
+                const float a = fabsf(g);
+                mx = fmaxf(mx, a);
+                bad |= !(a <= 3.4028235e38f);
+                sm += rw ? rw[c0 + i] * g : g;
+                const float* xr = xs_lds + i * NX;
+#pragma unroll
+                for (int c = 0; c < NX; ++c)
+                    if (c < nx) xs[c] = fmaf(g, xr[c], xs[c]);
+            }
+        }
     }
     pmx[(long)blockIdx.x * H + n] = bad ? __builtin_inff() : mx;
     psm[(long)blockIdx.x * H + n] = sm;

@@ -1259,26 +1259,30 @@ extern "C" int qs_attn_dw_x3(const float* G, const float* A, const float* col_sc
     hipStream_t st = (hipStream_t)stream;
     return H == 256 ? dw_launch<256>(G, A, col_scale, R, part, n_parts, st) : dw_launch<128>(G, A, col_scale, R, part, n_parts, st);
 }
-extern "C" int qs_colstats(const float* G, int64_t R, int32_t H, const float* obs, int32_t stride, int32_t nbr_off,
-                           int32_t B, int32_t K, int32_t nd, int32_t nx, float* pmx, float* psm, float* px,
-                           int32_t n_parts, void* stream) {
+extern "C" int qs_colstats(const float* G, int64_t R, int32_t H, const float* row_w, const float* obs, int32_t stride,
+                           int32_t nbr_off, int32_t B, int32_t K, int32_t nd, int32_t nx, float* pmx, float* psm,
+                           float* px, int32_t n_parts, void* stream) {
     namespace P = qs::pol;
     if (!G || !pmx || !psm) return fail(QS_E_INVALID, "NULL argument");
     if (H != 128 && H != 256) return fail(QS_E_INVALID, "hidden size must be 128 or 256");
     if (R < 1 || n_parts < 1 || n_parts > (1 << 24) || R * (int64_t)H >= (1ll << 40))
         return fail(QS_E_INVALID, "R >= 1, 1 <= n_parts <= 2^24");
     if (nx < 0 || nx > QS_COLSTATS_MAX_X) return fail(QS_E_INVALID, "nx out of range");
-    if (nx > 0 && (!obs || !px || B < 1 || K < 1 || nd < 0 || nd > nx || (int64_t)B * K != R || stride < nx ||
+    if (nx > 0 && (!obs || !px || B < 1 || K < 1 || nd < 0 || nd > nx || (int64_t)B * K != R || R >= (1ll << 31) ||
+                   stride < nx ||
                    nbr_off < 0 || nbr_off + (int64_t)K * nd > stride))
         return fail(QS_E_INVALID, "layer-0 input: obs, part_x, B K = R, nd <= nx, the neighbour block inside a row");
     hipStream_t st = (hipStream_t)stream;
     const long rows_per = (long)((R + n_parts - 1) / n_parts);
-    if (nx > 0)
+    if (nx > 8)
         hipLaunchKernelGGL(P::colstats_kernel<QS_COLSTATS_MAX_X>, dim3((unsigned)n_parts), dim3(H), 0, st, G, (long)R, H,
-                           rows_per, obs, stride, nbr_off, B, K, nd, nx, pmx, psm, px);
+                           rows_per, row_w, obs, stride, nbr_off, B, K, nd, nx, pmx, psm, px);
+    else if (nx > 0)   // the neighbour features alone (nd <= 8)
+        hipLaunchKernelGGL(P::colstats_kernel<8>, dim3((unsigned)n_parts), dim3(H), 0, st, G, (long)R, H, rows_per, row_w,
+                           obs, stride, nbr_off, B, K, nd, nx, pmx, psm, px);
     else
         hipLaunchKernelGGL(P::colstats_kernel<0>, dim3((unsigned)n_parts), dim3(H), 0, st, G, (long)R, H, rows_per,
-                           obs, stride, nbr_off, B > 0 ? B : 1, K > 0 ? K : 1, nd, 0, pmx, psm, px);
+                           row_w, obs, stride, nbr_off, B > 0 ? B : 1, K > 0 ? K : 1, nd, 0, pmx, psm, px);
     QS_HIP(hipGetLastError());
     return QS_OK;
 }

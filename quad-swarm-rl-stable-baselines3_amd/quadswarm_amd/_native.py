@@ -224,7 +224,7 @@ def lib():
         "qs_attn_bwd1_x3": ([I32, I32, I32, P(QsAttnTower), P(QsAttnTrain), I32, V], I32),
         "qs_attn_bwd2_x3": ([I32, I32, I32, P(QsAttnTower), P(QsAttnTrain), I32, V], I32),
         "qs_attn_dw_x3": ([V, V, V, ctypes.c_int64, I32, V, I32, V], I32),
-        "qs_colstats": ([V, ctypes.c_int64, I32, V, I32, I32, I32, I32, I32, I32, V, V, V, I32, V], I32),
+        "qs_colstats": ([V, ctypes.c_int64, I32, V, V, I32, I32, I32, I32, I32, I32, V, V, V, I32, V], I32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -54,10 +54,10 @@ def col_scales(G):
     return _pow2_scales(G.abs().amax(0))
 
 
-def col_stats(G, obs=None, B=0, K=0, nbr_off=0, nd=0, nx=0, parts=None):
-    """One pass over G [R, H] (qs_colstats): (the dW column scales, the column sums, and with obs the layer-0 weight
-    gradient sum_r G[r, :]^T X(r, :) as [nx, H] -- X the encoder's layer-0 input of row r, neighbour features first,
-    then the self features -- or None)."""
+def col_stats(G, obs=None, B=0, K=0, nbr_off=0, nd=0, nx=0, parts=None, row_w=None):
+    """One pass over G [R, H] (qs_colstats): (the dW column scales, the column sums sum_r w_r G[r, :] (row_w = w [R],
+    default 1), and with obs the layer-0 weight gradient sum_r G[r, :]^T X(r, :) as [nx, H] -- X the encoder's layer-0
+    input of row r, neighbour features first, then the self features -- or None)."""
     R, H = G.shape
     parts = parts or max(1, min(2048, (R + 255) // 256))
     z = lambda *sh: torch.empty(*sh, dtype=torch.float32, device=G.device)  # noqa: E731
@@ -65,6 +65,7 @@ def col_stats(G, obs=None, B=0, K=0, nbr_off=0, nd=0, nx=0, parts=None):
     px = z(parts, nx, H) if nx else None
     st = ctypes.c_void_p(torch.cuda.current_stream(G.device).cuda_stream)
     NAT.check(NAT.lib().qs_colstats(ctypes.c_void_p(G.data_ptr()), R, H,
+                                    ctypes.c_void_p(row_w.data_ptr() if row_w is not None else 0),
                                     ctypes.c_void_p(obs.data_ptr() if obs is not None else 0),
                                     obs.shape[1] if obs is not None else 0, nbr_off, B, K, nd, nx,
                                     ctypes.c_void_p(pmx.data_ptr()), ctypes.c_void_p(psm.data_ptr()),
@@ -194,11 +195,15 @@ class _Runner:
             gi["v2_w"], gi["v2_b"] = self.dw(b["dh_pre"], b["v1"])
             gi["v1_w"], gi["v1_b"] = self.dw(b["dv1_pre"], b["e2"])
             gi["a2_w"], gi["a2_b"] = self.dw(b["da2_pre"], b["a1"])
-            gi["a3_w"], gi["a3_b"] = b["dscore"].view(1, -1).mm(b["a2"]), b["dscore"].sum().view(1)
+            if self.dw_x3:   # sum_j dscore_j a2_j: a weighted column sum of a2 (one pass)
+                gi["a3_w"] = col_stats(b["a2"], row_w=b["dscore"])[1].view(1, -1)
+            else:
+                gi["a3_w"] = b["dscore"].view(1, -1).mm(b["a2"])
+            gi["a3_b"] = b["dscore"].sum().view(1)
             dP = b["da1_pre"].view(K, B, H).sum(0)                     # rows j with j % B == b (the repeat tiling)
             a1_w = params[w0 + 8]
             dA_e, gi["a1_b"] = self.dw(b["da1_pre"], b["e2"])          # a1_b = sum_j da1_pre_j = sum_b dP_b
-            gi["a1_w"] = torch.cat((dA_e, dP.t().mm(b["e_mean"])), dim=1)
+            gi["a1_w"] = torch.cat((dA_e, self.dw(dP, b["e_mean"])[0]), dim=1)   # |e_mean| <= 1 (a mean of tanh)
             torch.mm(dP, a1_w[:, H:], out=b["dem"])                    # dL/d e_mean
             for n in gi:
                 grads[w0 + _PARAMS.index(n)] = gi[n]
@@ -209,10 +214,12 @@ class _Runner:
             b, w0 = self.buf[i], 14 * i
             de2_pre, de1_pre = b["de2p"], b["dh_pre"]
             grads[w0 + 2], grads[w0 + 3] = self.dw(de2_pre, b["e1"])
-            # embedding_mlp[0] on cat(self_{j % B}, nbr_j): sum_j de1_pre_j^T [nbr_j | self_{j % B}] in one pass
+            # embedding_mlp[0] on cat(self_{j % B}, nbr_j): the neighbour half sum_j de1_pre_j^T nbr_j with the bias
+            # gradient in one pass; the self half over the K tiles summed first (B rows instead of B K)
             if self.dw_x3:
-                _, grads[w0 + 1], gx = col_stats(de1_pre, obs, B, K, so, nd, nd + so)
-                grads[w0] = torch.cat((gx[nd:].t(), gx[:nd].t()), dim=1)
+                _, grads[w0 + 1], gx = col_stats(de1_pre, obs, B, K, so, nd, nd)
+                g_self = de1_pre.view(K, B, H).sum(0).t().mm(self_obs)
+                grads[w0] = torch.cat((g_self, gx.t()), dim=1)
             else:
                 g_self = de1_pre.view(K, B, H).sum(0).t().mm(self_obs)
                 grads[w0] = torch.cat((g_self, de1_pre.t().mm(nbr_rows)), dim=1)

@@ -191,6 +191,11 @@ def test_colstats_matches_torch(H, B, K, parts):
     want_x = X.t().mm(G64)                      # [nd + so, H]
     scale = (X.abs().t().mm(G64.abs())).clamp_min(1e-300)
     assert ((gx.double() - want_x).abs() / scale).max().item() < 1e-6
+    # row weights: sum_r w_r G[r, :] (the score layer's weight gradient form)
+    w = torch.randn(R, device="cuda", generator=g)
+    _, wsum, _ = col_stats(G, row_w=w, parts=parts)
+    want_w = (w.double()[:, None] * G64).sum(0)
+    assert ((wsum.double() - want_w).abs() / (w.double().abs()[:, None] * G64.abs()).sum(0)).max().item() < 1e-6
     # a non-finite column gets scale 1 (and the sums carry the NaN)
     G[5, 3] = float("nan")
     gs2, sums2, _ = col_stats(G)
