@@ -237,6 +237,25 @@ __device__ uint64_t qs_dbg_stamps[65536 * QS_NSTAMP];
 #else
 #define QS_PRIO(k) do {} while (0)
 #endif
+// The younger wave drops the priority again at mark QS_PRIO_END (-1: keeps it to the end); marks 21 (after the
+// physics), 22 (after the collisions), 23 (after the impulses / scenario / state store) of the flavor-B step.
+// Round 5 (profiles/ab/r05_prio_end_ab.txt): 23 in the goal-scenario kernels only (c3mix 9.38 -> 9.30 us; C3 and
+// the earlier marks lose)
+#ifndef QS_PRIO_END
+#define QS_PRIO_END 23
+#endif
+#if QS_PRIO_AT >= 0 && QS_PRIO_END >= 0
+#define QS_PRIO_DROP(k)                                                                               \
+    do {                                                                                              \
+        if ((k) == QS_PRIO_END) {                                                                     \
+            uint32_t hw_;                                                                             \
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_));                        \
+            if (hw_ & 0xFu) __builtin_amdgcn_s_setprio(0);                                            \
+        }                                                                                             \
+    } while (0)
+#else
+#define QS_PRIO_DROP(k) do {} while (0)
+#endif
 
 struct Drone {
     float pos[3], vel[3], rot[9], om[3], rd[4], cd[4], ou[4], goal[3];

@@ -1014,6 +1014,7 @@ __global__ __launch_bounds__(StepGeo<NPAD>::WGS) void step_kernel(const KP* __re
     }
 
     QS_STAMP(2);
+    QS_PRIO_DROP(21);
     // ---- swarm phase: collisions + proximity (quadrotor_multi.py:537-568, 608-622) ----
     Row cur{};
     float pen = 0.f;
@@ -1124,6 +1125,7 @@ __global__ __launch_bounds__(StepGeo<NPAD>::WGS) void step_kernel(const KP* __re
     }
 
     QS_STAMP(3);
+    QS_PRIO_DROP(22);
     // ---- random forces (:659-698), replicated on the sub-lanes ----
     bool vchanged = false;
     if (kp.downwash && kp.N > 1)   // perform_downwash (aerodynamics/downwash.py:4-51)
@@ -1366,6 +1368,7 @@ __global__ __launch_bounds__(StepGeo<NPAD>::WGS) void step_kernel(const KP* __re
         }
     }
     QS_STAMP(4);
+    if (SCEN_STEP) QS_PRIO_DROP(23);   // goal-scenario kernels: c3mix 9.38 -> 9.30 us (C3 neutral-to-worse: kept)
     // ---- observations (post-impulse state; quadrotor_multi.py:704-720) ----
     const bool nbr = kp.neighbor == QS_NEIGHBOR_POS_VEL && kp.K > 0;
     if (nbr && ec.wany(vchanged)) {  // impulses changed velocities: refresh the tile
