@@ -203,7 +203,8 @@ def pmc_traffic(config):
         d = json.load(open(p))
         src = {"file": os.path.relpath(p, ROOT), "tree": d.get("tree"),
                "read_bytes": d.get("hbm_read_bytes_per_launch"), "write_bytes": d.get("hbm_write_bytes_per_launch"),
-               "passes": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate runs, FETCH x2 (gfx950)"}
+               "passes": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate runs, FETCH x2 (gfx950)",
+               "correction": d.get("correction")}
         return d.get("hbm_bytes_per_launch"), src
     except Exception:
         return None, None
@@ -746,6 +747,13 @@ def main(argv=None):
                          "bytes_per_agent_step": round(bpa, 1),
                          "bytes_per_agent_step_state_complete": (round(state_bytes_per_agent_step(cfg)[0], 1)
                                                                  if cfg.flavor == "B" else None),
+                         # the PMC reads against the reads the step needs once its istate, stats ring and env
+                         # words are counted (the FETCH x2 factor calibrated on the step's own load shape,
+                         # tools/calib/fetch_calib read_sub64)
+                         "read_ratio_state_complete": (round(traffic_src["read_bytes"] /
+                                                             (state_bytes_per_agent_step(cfg)[1] * I), 3)
+                                                       if cfg.flavor == "B" and traffic_src and
+                                                       traffic_src.get("read_bytes") else None),
                          "bytes_per_launch": round(bpa * I / S),
                          "valu": valu_roofline(args.config, I, k_ms) if cfg.flavor == "A" else None},
             "nonfinite_guard": guard,

@@ -72,9 +72,11 @@ def main():
     tot = d.sum(1)
     sub = None
     if cfg.flavor == "B" and (st[:, 18] != 0).any():   # the scenario sub-phases (slots 18-21)
-        seq = np.stack([st[:, 3], st[:, 18], st[:, 19], st[:, 21], st[:, 4]], axis=1)
+        # slots 19 / 20 are stamped only inside the scenario step: a kernel without one leaves them 0
+        s19 = np.where(st[:, 19] != 0, st[:, 19], st[:, 18])
+        seq = np.stack([st[:, 3], st[:, 18], s19, st[:, 21], st[:, 4]], axis=1)
         sub = np.diff(seq, axis=1)
-        s20 = np.where(st[:, 20] != 0, st[:, 20] - st[:, 19], 0)
+        s20 = np.where(st[:, 20] != 0, st[:, 20] - s19, 0)
         sub = np.concatenate([sub, s20[:, None]], axis=1)
         sub_names = ["  forces/impulses", "  scen: tables + sync", "  scen: step (+ via)", "  state store",
                      "  (of which scen step proper)"]

@@ -44,6 +44,7 @@ def main():
     ap.add_argument("--config", default="c3")
     ap.add_argument("--kernel", default="step_kernel")
     ap.add_argument("--prefix", default="prof", help="gpurun_out/<prefix>_{kt,fetch,write,sq} (profa for flavor A)")
+    ap.add_argument("--read-shape", default=None, help="calibration kernel for the FETCH_SIZE divisor (default by flavor)")
     args = ap.parse_args()
     tag = f"r{args.round:02d}_{args.config}"
     os.makedirs(PROF, exist_ok=True)
@@ -87,9 +88,12 @@ def main():
             res.setdefault("launches_sampled", {})[cname] = len(v)
     c = res.get("counters_per_launch", {})
     if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
-        # gfx950: FETCH_SIZE counts 64 B per 128-B request (MI355X_MICROARCH.md §HBM) -> use the
-        # ratio measured on our own 4-byte-per-lane load shape when the calibration ran, else x2.
-        fr = calib.get("read_b32:FETCH_SIZE")
+        # gfx950: FETCH_SIZE counts 64 B per 128-B request (MI355X_MICROARCH.md §HBM) -> use the ratio
+        # measured on the kernel's own state-word load shape when the calibration ran, else x2: flavor B's
+        # 4 sub-lanes per drone read four 64-B row segments per instruction (read_sub64, XCD-mapped like the
+        # step), flavor A's 2 sub-lanes 128-B segments (read_b32's shape)
+        shape = args.read_shape or ("read_b32" if args.kernel.endswith("_a") else "read_sub64<true>")
+        fr = calib.get(f"{shape}:FETCH_SIZE")
         wr = calib.get("write_b32:WRITE_SIZE")
         fetch = c["FETCH_SIZE"] * 1024.0 / (fr if fr else 0.5)
         write = c["WRITE_SIZE"] * 1024.0 / (wr if wr else 1.0)
@@ -97,7 +101,7 @@ def main():
         res["hbm_write_bytes_per_launch"] = write
         res["hbm_bytes_per_launch"] = fetch + write
         res["correction"] = {"fetch_divisor": fr or 0.5, "write_divisor": wr or 1.0,
-                             "source": "tools/calib/fetch_calib" if fr else "guide x2 (uncalibrated)"}
+                             "source": f"tools/calib/fetch_calib {shape}" if fr else "guide x2 (uncalibrated)"}
     if "SQ_WAVES" in c:
         w = c["SQ_WAVES"]
         res["per_wave"] = {k: c[k] / w for k in c if k.startswith("SQ_") and k != "SQ_WAVES"}
