@@ -112,6 +112,18 @@ def test_state_complete_bytes():
         assert got[0] > base
 
 
+def test_committed_pmc_reads_against_state_complete():
+    """The committed round-5 PMC summaries (FETCH x2 calibrated on the step's own load shape,
+    tools/calib/fetch_calib read_sub64) hold C2 / C3 reads within 10 % of the state-complete read count, as
+    DESIGN.md states, and the pmc_traffic hand-off carries the correction's source."""
+    for c in ("c2", "c3"):
+        traffic, src = bench.pmc_traffic(c)
+        assert traffic and src and src["correction"]["source"].endswith("read_sub64<true>"), (c, src)
+        cfg = bench.make_cfg(bench.CONFIGS[c])
+        ratio = src["read_bytes"] / (bench.state_bytes_per_agent_step(cfg)[1] * cfg.num_envs * cfg.num_agents)
+        assert 1.0 <= ratio < 1.1, (c, ratio)
+
+
 def test_every_bench_config_is_valid():
     """Every --config builds a configuration the C ABI accepts (layout query, no device): the sweep's configs,
     including the 128-drone flavor-A env (k = 7 <= QS_A_KMAX) and the obstacle / replay / mix variants."""
