@@ -885,6 +885,56 @@ __device__ __forceinline__ int tile_store(const float* lds, float* dst, int nflo
     return bad;
 }
 
+// float4 per lane of a block's obs tile (`slots` rows of obs_dim floats over `nthr` lanes): a compile-time bound in
+// the specialised kernels (obs_dim is a constant there), 0 in the generic ones (tile_store's loop)
+template <int SLOTS, int NTHR>
+__device__ constexpr int tile_vecs() {
+#ifdef QS_JIT
+    return (SLOTS * kKP.obs_dim / 4 + NTHR - 1) / NTHR;
+#else
+    return 0;
+#endif
+}
+
+// tile_store with every float4 read of the lane issued back to back before the stores: one LDS wait for the tile
+// instead of one per vector (the loop above waits on each read before its store).  Reads past the tile are
+// clamped to its last vector (stored by its own lane only); the non-finite count is the loop's, taken exactly in
+// the rare branch.  V = tile_vecs<>() bounds the vectors per lane; a larger tile falls back to the loop.
+#ifndef QS_TILE_BATCH
+#define QS_TILE_BATCH 1
+#endif
+template <int V>
+__device__ __forceinline__ int tile_store_v(const float* lds, float* dst, int nfloat, int lane, int nthr) {
+    const int nvec = nfloat >> 2;
+    if (!QS_TILE_BATCH || V <= 0 || V > 8 || (((uintptr_t)dst) & 15) != 0 || nvec < 1 || nvec > V * nthr)
+        return tile_store(lds, dst, nfloat, lane, nthr);
+    const float4* lv = reinterpret_cast<const float4*>(lds);
+    const __amdgpu_buffer_rsrc_t r = qs_rsrc(dst);
+    float4 x[V > 0 ? V : 1];
+#pragma unroll
+    for (int i = 0; i < V; ++i) x[i] = lv[min(lane + i * nthr, nvec - 1)];
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        const int v = lane + i * nthr;
+        if (v < nvec) st_wt4(r, (uint32_t)v * 16u, x[i]);
+        acc = fin_acc(fin_acc(fin_acc(fin_acc(acc, x[i].x), x[i].y), x[i].z), x[i].w);
+    }
+    int bad = 0;
+    if (!(acc == 0.f)) {   // some value is inf / NaN (a clamped copy included): count the tile's own exactly
+#pragma unroll
+        for (int i = 0; i < V; ++i)
+            if (lane + i * nthr < nvec)
+                bad += !(x[i].x * 0.f == 0.f) + !(x[i].y * 0.f == 0.f) + !(x[i].z * 0.f == 0.f) + !(x[i].w * 0.f == 0.f);
+    }
+    const int t = (nvec << 2) + lane;
+    if (t < nfloat) {
+        dst[t] = lds[t];
+        bad += !(lds[t] * 0.f == 0.f);
+    }
+    return bad;
+}
+
 // ---------------------------------------------------------------------------------------------
 // the fused step kernel
 // ---------------------------------------------------------------------------------------------

@@ -1077,7 +1077,8 @@ __global__ __launch_bounds__(StepGeoA<NPAD>::WGS) void step_kernel_a(const KP* _
     }
     lds_sync();
     QS_STAMP_ACC(8);
-    const int obs_bad = tile_store(lds, b.obs + (size_t)env0 * kp.N * kp.obs_dim, rows * kp.obs_dim, lane, WGS);
+    const int obs_bad = tile_store_v<tile_vecs<SLOTS, WGS>()>(lds, b.obs + (size_t)env0 * kp.N * kp.obs_dim, rows * kp.obs_dim,
+                                                              lane, WGS);
     guard_count(b, obs_bad, rew_bad, state_bad);
 
     if (lead) {

@@ -1514,7 +1514,8 @@ __global__ __launch_bounds__(StepGeo<NPAD>::WGS) void step_kernel(const KP* __re
     }
     lds_sync();
     QS_STAMP(8);
-    const int obs_bad = tile_store(lds, b.obs + (size_t)env0 * kp.N * kp.obs_dim, rows * kp.obs_dim, lane, WGS);
+    const int obs_bad = tile_store_v<tile_vecs<SLOTS, WGS>()>(lds, b.obs + (size_t)env0 * kp.N * kp.obs_dim, rows * kp.obs_dim,
+                                                              lane, WGS);
     QS_STAMP(9);
 
     if (lead) {
