@@ -66,6 +66,9 @@ __device__ __forceinline__ float sin_small(float x) {
 #ifndef QS_A_DEAL_SENSE
 #define QS_A_DEAL_SENSE 1
 #endif
+#ifndef QS_COL_FOLD
+#define QS_COL_FOLD 1
+#endif
 
 // (x + pi) % (2 pi) - pi with Python's modulo sign convention.  For r = x + pi in [-2 pi, 4 pi) -- every
 // angle the step wraps -- fmodf(r, 2 pi) is r itself below 2 pi and r - 2 pi above (exact by Sterbenz), so
@@ -695,7 +698,11 @@ __device__ __forceinline__ void col_row16_q2(const KP& kp, const Drone& d, int d
         const float dx = d.pos[0] - dpp_f<C>(d.pos[0]), dy = d.pos[1] - dpp_f<C>(d.pos[1]);
         const float dz = d.pos[2] - dpp_f<C>(d.pos[2]);
         const int j = dpp_i<C>(di);
-        const bool hit = (j != di) & (j < kp.N) & (dx * dx + dy * dy + dz * dz <= thr2);   // a select, not a branch
+        // only the K = 0 rotation can bring the drone itself (its own other sub-lane); with 8 drones every slot of the
+        // row is a drone (constants in the specialised kernels: the two tests fold away)
+        const bool self_ok = (QS_COL_FOLD && K != 0) || j != di;
+        const bool in_env = (QS_COL_FOLD && kp.N == 8) || j < kp.N;
+        const bool hit = self_ok & in_env & (dx * dx + dy * dy + dz * dz <= thr2);   // a select, not a branch
         cur |= hit ? (1u << j) : 0u;   // j < 8: the row's low word
         col_row16_q2<K + 1>(kp, d, di, thr2, cur);
     }
