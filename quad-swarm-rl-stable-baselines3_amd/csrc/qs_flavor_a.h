@@ -69,6 +69,9 @@ __device__ __forceinline__ float sin_small(float x) {
 #ifndef QS_COL_FOLD
 #define QS_COL_FOLD 1
 #endif
+#ifndef QS_ACT_FOLD
+#define QS_ACT_FOLD 1
+#endif
 
 // (x + pi) % (2 pi) - pi with Python's modulo sign convention.  For r = x + pi in [-2 pi, 4 pi) -- every
 // angle the step wraps -- fmodf(r, 2 pi) is r itself below 2 pi and r - 2 pi above (exact by Sterbenz), so
@@ -837,8 +840,13 @@ __global__ __launch_bounds__(StepGeoA<NPAD>::WGS) void step_kernel_a(const KP* _
     float gdist = 0.f;   // infos[i]["goal_dist"] of the last executed tick (per-step infos, kp.rcomp)
     bool dn = false;
     float zn[Q > 1 ? Q - 1 : 1][4] = {};   // OU normals of the next Q - 1 ticks, drawn by sub-lanes 1 .. Q-1
+    // Inside the tick loop `active` only masks the env-level collectives (each reads its own env's lanes) and the
+    // env's LDS rows -- no global access: an env past E (a partial last block) computes values it never stores, so
+    // the loop needs only the drone test, and none when the env's drones fill its lanes (a constant when specialised)
+    const bool active_tick = QS_ACT_FOLD ? (kp.N == NPAD || di < kp.N) : active;
 #pragma unroll 1   // 8 controller ticks: one copy of the body (I-cache), also when kp.ticks is a constant
     for (int sub = 0; sub < kp.ticks; ++sub) {
+        const bool active = active_tick;
         if (fin) continue;   // the reference breaks out of its tick loop (:988); segment-uniform
         const Rng rng = env_rng(seed, tick, episode);
         float u[4];
