@@ -497,11 +497,11 @@ __device__ __forceinline__ RodCoef rod_coef(const KP& kp, const float* R, const 
     r.w[2] = R[6] * om[0] + R[7] * om[1] + R[8] * om[2];
     const float w2 = r.w[0] * r.w[0] + r.w[1] * r.w[1] + r.w[2] * r.w[2];
     const float x = w2 * (dt * dt);
-    float sf, cf;
-    if (x < 0.36f) {  // a < 0.6: Taylor to a^8, truncation < 2e-10 (|omega| <= 40 per axis gives a <= 0.35)
-        sf = dt * (1.f + x * (-1.f / 6.f + x * (1.f / 120.f + x * (-1.f / 5040.f + x * (1.f / 362880.f)))));
-        cf = dt * dt * (0.5f + x * (-1.f / 24.f + x * (1.f / 720.f + x * (-1.f / 40320.f + x * (1.f / 3628800.f)))));
-    } else {          // after collision kicks (|omega| up to ~100 rad/s before the clip)
+    // a < 0.6: Taylor to a^8, truncation < 2e-10 (|omega| <= 40 per axis gives a <= 0.35); computed on every lane, the
+    // rare lanes past it overwrite it (one masked block instead of an if / else)
+    float sf = dt * (1.f + x * (-1.f / 6.f + x * (1.f / 120.f + x * (-1.f / 5040.f + x * (1.f / 362880.f)))));
+    float cf = dt * dt * (0.5f + x * (-1.f / 24.f + x * (1.f / 720.f + x * (-1.f / 40320.f + x * (1.f / 3628800.f)))));
+    if (!(x < 0.36f)) {   // after collision kicks (|omega| up to ~100 rad/s before the clip)
         const float wn = fsqrt(w2), a = wn * dt;
         float sa, ca;
         sincos_hw(0.5f * a, &sa, &ca);
@@ -589,8 +589,11 @@ __device__ __forceinline__ void substep_tail(const KP& kp, Drone& d, const Torqu
     if (before[2] > d.pos[2]) fl |= QS_FL_CRASH_CEIL;
     // floor (floor_interaction_numba :576-646, threshold = arm)
     float fx = R[2] * tsum, fy = R[5] * tsum, fz = R[8] * tsum;
-    float ax, ay, az;
-    if (d.pos[2] <= kp.arm) {
+    float az;
+    const float azf = -kp.grav + kp.inv_mass * fz;
+    const bool low = d.pos[2] <= kp.arm;
+    fl = low ? fl : (fl & ~(uint32_t)QS_FL_ON_FLOOR);
+    if (low) {
         d.pos[2] = kp.arm;
         if (fl & QS_FL_ON_FLOOR) {   // resting on the floor: the common case of an untrained swarm
             // rot = yaw_rot(arctan2(R10, R00 + EPS)) and the friction directions cos / sin of arctan2 as
@@ -635,15 +638,11 @@ __device__ __forceinline__ void substep_tail(const KP& kp, Drone& d, const Torqu
 #pragma unroll
             for (int k = 0; k < 4; ++k) { d.cd[k] = 0.f; d.rd[k] = 0.f; }
         }
-        ax = kp.inv_mass * fx;
-        ay = kp.inv_mass * fy;
-        az = fmaxf(-kp.grav + kp.inv_mass * fz, 0.f);
+        az = fmaxf(azf, 0.f);
     } else {
-        fl &= ~(uint32_t)QS_FL_ON_FLOOR;
-        ax = kp.inv_mass * fx;
-        ay = kp.inv_mass * fy;
-        az = -kp.grav + kp.inv_mass * fz;
+        az = azf;
     }
+    const float ax = kp.inv_mass * fx, ay = kp.inv_mass * fy;
     d.flags = fl;
     d.vel[0] = (1.f - kp.vel_damp) * d.vel[0] + dt * ax;  // (:652)
     d.vel[1] = (1.f - kp.vel_damp) * d.vel[1] + dt * ay;
