@@ -975,7 +975,9 @@ __global__ __launch_bounds__(StepGeoA<NPAD>::WGS) void step_kernel_a(const KP* _
             if (active && q == 0)
                 for (int k = 0; k < 3; ++k) stab[4 * di + k] = d.goal[k];
             lds_sync();
-            if (active && di == 0 && q == 0) {
+            // envok: `sc` is loaded only for envs < E (scen_load above); an env past E in a partial last block
+            // runs the tick loop (QS_ACT_FOLD) but must not step a scenario from uninitialised registers
+            if (active && envok && di == 0 && q == 0) {
                 SDraw sd = sdraw(rng, gid, S_SCN);
                 scen_step(kp, sc, tick, sd, stab, stab + 4 * (NPAD + 4));
             }

@@ -1395,6 +1395,22 @@ static int jit_compile(const qs_config* c, const qs::KP& kp, int npad, int qb, i
             fclose(f);
             dir_src.push_back(txt);
         }
+        // The host launches the directory's kernels with THIS library's argument list and workspace layout.  A
+        // source tree of another ABI (e.g. round 4's step kernel, which still took the replay wrapper's pointers
+        // as kernel arguments, under the ABI-13 host that passes them in the RArgs device block) reads its
+        // pointers from the wrong kernarg offsets and faults (round 5, hipErrorIllegalAddress):
+        // the directory's quadswarm.h must carry this library's QS_ABI_VERSION.
+        int dir_abi = -1;
+        for (int i = 0; i < kJitNumHeaders; ++i) {
+            if (std::string(kJitHeaderNames[i]) != "quadswarm.h") continue;
+            const std::string& t = dir_src[i];
+            const size_t p = t.find("#define QS_ABI_VERSION");
+            if (p != std::string::npos) dir_abi = atoi(t.c_str() + p + sizeof("#define QS_ABI_VERSION") - 1);
+        }
+        if (dir_abi != QS_ABI_VERSION)
+            return fail(QS_E_INVALID, "QS_JIT_SRC_DIR: " + std::string(dir) + "/quadswarm.h has QS_ABI_VERSION " +
+                                          std::to_string(dir_abi) + ", this library is ABI " +
+                                          std::to_string(QS_ABI_VERSION) + " (kernel arguments would not match)");
         for (int i = 0; i < kJitNumHeaders; ++i) hsrc[i] = dir_src[i].c_str();
     }
     hiprtcProgram prog;

@@ -164,11 +164,39 @@ class DeviceCurriculum(TrainerCallback):
         self.records = {}              # the logger values the reference records (curriculum/*)
         self.saved = []                # checkpoint paths written
         self.eval_env = eval_env
+        self.eval_freq, self.n_eval_episodes = int(eval_freq), int(n_eval_episodes)
         self.evaluator = None
         if eval_env is not None and eval_freq > 0:
             # CurriculumCallback(..., eval_env=eval_env, eval_freq=1000, n_eval_episodes=10) without save paths
-            self.evaluator = EvalCallback(eval_env, n_eval_episodes=n_eval_episodes, eval_freq=eval_freq,
-                                          verbose=verbose)
+            self.evaluator = self._make_evaluator(eval_env, self.eval_freq, self.n_eval_episodes)
+
+    def _make_evaluator(self, eval_env, eval_freq, n_eval_episodes):
+        return EvalCallback(eval_env, n_eval_episodes=n_eval_episodes, eval_freq=eval_freq, verbose=self.verbose)
+
+    def _agree_on_evaluator(self, trainer):
+        """Data parallel: evaluation is collective (rank 0 evaluates, every rank joins the broadcast of its mean
+        reward and a new best's save), so every rank needs an evaluator exactly when rank 0 has one.  EvalCallback
+        lets ranks other than 0 pass eval_env=None; here they may also omit it altogether: they get rank 0's
+        eval_freq / n_eval_episodes with no env.  A rank with an evaluator when rank 0 has none is refused on every
+        rank (all ranks reach the same decision from one all_gather)."""
+        if not getattr(trainer, "distributed", False):
+            return
+        dist = _dist()
+        mine = torch.tensor([self.evaluator is not None, self.eval_freq, self.n_eval_episodes], dtype=torch.int64)
+        cdev = trainer.device if dist.get_backend(trainer.group) == "nccl" else torch.device("cpu")
+        allv = torch.empty(trainer.world_size * 3, dtype=torch.int64, device=cdev)
+        dist.all_gather_into_tensor(allv, mine.to(cdev), group=trainer.group)
+        allv = allv.cpu().view(trainer.world_size, 3)
+        has0, freq0, n0 = (int(v) for v in allv[0])
+        if not has0:
+            if bool(allv[:, 0].any()):
+                raise NAT.QuadSwarmError("DeviceCurriculum: ranks other than 0 have an eval env but rank 0 has "
+                                         "none (rank 0 evaluates)")
+            return
+        if self.evaluator is None:
+            self.evaluator = self._make_evaluator(None, freq0, n0)
+        elif (self.evaluator.eval_freq, self.evaluator.n_eval_episodes) != (freq0, n0):
+            raise NAT.QuadSwarmError("DeviceCurriculum: eval_freq / n_eval_episodes differ from rank 0's")
 
     @classmethod
     def from_reference_cfg(cls, cfg, save_path=None, **kw):
@@ -200,7 +228,11 @@ class DeviceCurriculum(TrainerCallback):
             trainer.env.set_capture_radius(self.r0)
             if self.eval_env is not None:
                 self.eval_env.set_capture_radius(self.r0)
+        self._agree_on_evaluator(trainer)
         if self.evaluator is not None:
+            if getattr(self, "_pending_eval", None) is not None:
+                self.evaluator.load_state_dict(self._pending_eval)
+                self._pending_eval = None
             self.evaluator.on_training_start(trainer)
 
     def on_step(self, ctx):
@@ -249,6 +281,10 @@ class DeviceCurriculum(TrainerCallback):
     def on_rollout_end(self, trainer):
         self._report(trainer)
 
+    def on_iteration_end(self, trainer):
+        if self.evaluator is not None:
+            self.evaluator.on_iteration_end(trainer)
+
     def on_training_end(self, trainer):
         # reductions of a rollout that a callback stopped (no on_rollout_end) are still logged and checkpointed
         if self.dev_state is not None:
@@ -267,8 +303,10 @@ class DeviceCurriculum(TrainerCallback):
         """Takes effect at the next on_training_start (learn())."""
         self._pending = sd
         self.dev_state = None
-        if self.evaluator is not None and "eval" in sd:
-            self.evaluator.load_state_dict(sd["eval"])
+        self._pending_eval = sd.get("eval")
+        if self.evaluator is not None and self._pending_eval is not None:
+            self.evaluator.load_state_dict(self._pending_eval)
+            self._pending_eval = None
 
 
 class CheckpointCallback(TrainerCallback):
@@ -367,7 +405,12 @@ class EvalCallback(TrainerCallback):
     eval_freq=cfg.eval_freq // cfg.num_envs, n_eval_episodes=cfg.eval_episodes, deterministic=True) (sb_train.py:76-84).
 
     eval_env: a device env (QuadSwarmEnv; the reference's eval env is one env of N agents).  Data parallel: only rank 0
-    needs one (pass None elsewhere); rank 0's mean reward is broadcast."""
+    needs one (pass None elsewhere); rank 0's mean reward is broadcast.
+
+    The best model is saved at the end of the iteration in which the new best was found (or at the end of training,
+    if learn() stopped first), not mid-rollout: PPOTrainer.save checkpoints are resumable only at the iteration
+    boundary (a mid-rollout save would hold num_timesteps / env_steps of a partial rollout without its storage).  The
+    weights are the same either way -- the policy changes only in the update."""
 
     def __init__(self, eval_env, n_eval_episodes=5, eval_freq=10000, log_path=None, best_model_save_path=None,
                  deterministic=True, verbose=1, callback_on_new_best=None):
@@ -384,6 +427,7 @@ class EvalCallback(TrainerCallback):
         self.last_episodes = None      # (rewards, lengths, successes) of the last evaluation (rank 0)
         self.records = {}
         self.best_saved = []
+        self._best_due = False
 
     def on_training_start(self, trainer):
         if _is_main(trainer):
@@ -435,13 +479,24 @@ class EvalCallback(TrainerCallback):
             if self.verbose >= 1 and main:
                 print("New best mean reward!")
             if self.best_model_save_path is not None:
-                p = os.path.join(self.best_model_save_path, "best_model.pt")
-                trainer.save(p)
-                self.best_saved.append(p)
+                self._best_due = True          # written at the iteration boundary (on_iteration_end)
             self.best_mean_reward = mean
             if self.callback_on_new_best is not None:
                 go = self.callback_on_new_best.on_new_best(self) is not False
         return go
+
+    def _save_best(self, trainer):
+        if self._best_due:
+            self._best_due = False
+            p = os.path.join(self.best_model_save_path, "best_model.pt")
+            trainer.save(p)
+            self.best_saved.append(p)
+
+    def on_iteration_end(self, trainer):
+        self._save_best(trainer)
+
+    def on_training_end(self, trainer):
+        self._save_best(trainer)
 
     def state_dict(self):
         return {"n_calls": self.n_calls, "best_mean_reward": float(self.best_mean_reward),

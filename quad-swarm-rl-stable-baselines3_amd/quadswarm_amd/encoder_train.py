@@ -25,7 +25,7 @@ import ctypes
 import torch
 
 from . import _native as NAT
-from .policy_fused import pack_mfma_weight_x3, supports
+from .policy_fused import F16_MAX, X3_SIN, pack_mfma_weight_x3, supports
 
 _PARAMS = ("e1_w", "e1_b", "e2_w", "e2_b", "v1_w", "v1_b", "v2_w", "v2_b", "a1_w", "a1_b", "a2_w", "a2_b", "a3_w", "a3_b")
 
@@ -254,6 +254,28 @@ class FusedAttentionTrain:
     def params(self):
         return [p for enc in self.runner.encs for p in tower_params(enc)]
 
+    def obs_in_range(self, obs):
+        """True when every value of `obs` (e.g. the whole rollout storage, once per update) is inside the split-f16
+        range of layer 0 (|obs| < 4094: s = 16, f16 max 65504).  Beyond it the x3 split packs +-inf and the
+        gradients become NaN; PPOTrainer then runs that update's encoders on the torch autograd path.  Non-finite
+        values are left to the env's non-finite guard.  One host sync."""
+        v = float(obs.abs().amax())
+        ok = not (v == v and v != float("inf") and v * X3_SIN >= F16_MAX)
+        if not ok:
+            self._warn(f"an observation reached |obs| = {v:.4g} >= {F16_MAX / X3_SIN:.4g}")
+        return ok
+
+    def _warn(self, why):
+        import warnings
+        warnings.warn(f"fused x3 update: {why}, beyond the split-f16 range; this update's encoders run in torch fp32")
+
     def encodings(self, obs):
+        """Both towers' encoder outputs, or None (the caller's torch autograd path) when a weight left the split-f16
+        range (|w| >= 255.9: pack_mfma_weight_x3 refuses it before any kernel runs), as FusedRolloutPolicy.refresh
+        falls back to fp32 for the rollout."""
         assert obs.is_cuda and obs.dtype == torch.float32 and obs.dim() == 2
-        return list(_AttnTrainFn.apply(self.runner, obs.contiguous(), *self.params()))
+        try:
+            return list(_AttnTrainFn.apply(self.runner, obs.contiguous(), *self.params()))
+        except ValueError as e:
+            self._warn(str(e))
+            return None

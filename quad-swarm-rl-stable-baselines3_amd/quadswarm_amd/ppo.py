@@ -554,12 +554,15 @@ class PPOTrainer:
         adv_all, ret_all, old_v = st.flat("advantages"), st.flat("returns"), st.flat("values")
         acc = torch.zeros(6, dtype=torch.float64, device=self.device)
         n_mb = 0
+        # the fused x3 encoders only where the rollout's observations are inside their split-f16 range (one check per
+        # update, whatever the rollout's precision); a weight out of range falls back per minibatch (encodings -> None)
+        fused = self.fused_update if self.fused_update is not None and self.fused_update.obs_in_range(obs) else None
         for _ in range(c.n_epochs):
             perm = torch.randperm(n, device=self.device, generator=self.gen)
             for s in range(0, n, c.batch_size):
                 idx = perm[s:s + c.batch_size]
                 ob = obs[idx]
-                nbr = self.fused_update.encodings(ob) if self.fused_update is not None else None
+                nbr = fused.encodings(ob) if fused is not None else None
                 values, logp, entropy = pol.evaluate_actions(ob, act[idx], nbr=nbr)
                 values = values.flatten()
                 adv = adv_all[idx]
@@ -649,8 +652,9 @@ class PPOTrainer:
         return sh
 
     def _gather_shards(self, shard):
-        """Every rank's shard on rank 0 (None elsewhere): each serialised with torch.save, the byte strings padded to
-        the longest and all-gathered (one length exchange + one all_gather), read back with weights_only=True."""
+        """Every rank's shard on rank 0 (None elsewhere): each serialised with torch.save, the lengths all-gathered (8
+        bytes per rank), the byte strings padded to the longest and gathered to rank 0 only (the other ranks hold just
+        their own padded string), read back with weights_only=True."""
         if not self.distributed:
             return [shard]
         import io
@@ -665,13 +669,14 @@ class PPOTrainer:
         ns = ns.cpu().tolist()
         pad = torch.zeros(max(ns), dtype=torch.uint8)
         pad[:raw.numel()] = raw
-        allb = torch.empty(self.world_size * max(ns), dtype=torch.uint8, device=cdev)
-        dist.all_gather_into_tensor(allb, pad.to(cdev), group=self.group)
+        pad = pad.to(cdev)
+        dst = dist.get_global_rank(self.group, 0) if self.group is not None else 0
+        parts = [torch.empty_like(pad) for _ in range(self.world_size)] if self.rank == 0 else None
+        dist.gather(pad, gather_list=parts, dst=dst, group=self.group)
         if self.rank != 0:
             return None
-        allb = allb.cpu().view(self.world_size, max(ns))
-        return [torch.load(io.BytesIO(allb[r, :ns[r]].numpy().tobytes()), map_location="cpu", weights_only=True)
-                for r in range(self.world_size)]
+        return [torch.load(io.BytesIO(parts[r][:ns[r]].cpu().numpy().tobytes()), map_location="cpu",
+                           weights_only=True) for r in range(self.world_size)]
 
     def save(self, path, callbacks=None):
         """Everything the next iteration depends on: policy and Adam state, counters, the callbacks' state, and every

@@ -354,6 +354,29 @@ def test_jit_opts_may_not_change_launch_geometry(monkeypatch):
         assert opt[2:7] in L.qs_last_error().decode()
 
 
+def test_jit_src_dir_of_another_abi_is_refused(monkeypatch, tmp_path):
+    """QS_JIT_SRC_DIR (kernel-variant A/B) compiles the directory's headers but launches them with this library's
+    kernel arguments: a tree whose quadswarm.h carries another QS_ABI_VERSION is refused before hipRTC runs
+    (round 5's illegal address: round-4 sources under the ABI-13 host).  The current sources pass."""
+    import shutil
+    L = N.lib()
+    qc = QuadSwarmConfig(num_envs=64, num_agents=8, neighbor_visible_num=6).to_qs_config()
+    csrc = os.path.join(os.path.dirname(__file__), "..", "quad-swarm-rl-stable-baselines3_amd", "csrc")
+    inc = os.path.join(os.path.dirname(__file__), "..", "include")
+    for name in ("qs_rng.h", "qs_common.h", "qs_flavor_b.h", "qs_flavor_a.h", "qs_replay.h", "qs_scen.h"):
+        shutil.copy(os.path.join(csrc, name), tmp_path / name)
+    hdr = open(os.path.join(inc, "quadswarm.h")).read()
+    abi = N.ABI_VERSION
+    assert f"#define QS_ABI_VERSION {abi}\n" in hdr
+    monkeypatch.setenv("QS_JIT_SRC_DIR", str(tmp_path))
+    (tmp_path / "quadswarm.h").write_text(hdr)
+    assert L.qs_specialize_compile(qc) > 10000, L.qs_last_error()
+    (tmp_path / "quadswarm.h").write_text(hdr.replace(f"#define QS_ABI_VERSION {abi}\n",
+                                                      f"#define QS_ABI_VERSION {abi - 2}\n"))
+    assert L.qs_specialize_compile(qc) == -1          # QS_E_INVALID
+    assert f"QS_ABI_VERSION {abi - 2}" in L.qs_last_error().decode()
+
+
 def test_curriculum_init_fills_the_struct_mirror():
     """qs_curriculum_init (host only) writes exactly the mirrored struct: the reference's starting state of
     CurriculumCallback (custom_callbacks.py:442-451), a cleared window."""

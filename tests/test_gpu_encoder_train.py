@@ -200,3 +200,26 @@ def test_colstats_matches_torch(H, B, K, parts):
     G[5, 3] = float("nan")
     gs2, sums2, _ = col_stats(G)
     assert gs2[3].item() == 1.0 and torch.isnan(sums2[3]) and torch.equal(gs2[4:], gs[4:])
+
+
+def test_fused_update_falls_back_when_a_weight_leaves_the_x3_range():
+    """a weight beyond the split-f16 packing range (|w| >= 255.9) makes encodings() return None (the
+    caller's torch autograd path) instead of raising mid-training; back in range, the fused path returns."""
+    import warnings
+    pol = random_policy(6, H=128, seed=5)
+    f = FusedAttentionTrain(pol)
+    obs = obs_for(pol.cfg, 200)
+    assert f.encodings(obs) is not None
+    ne = pol.actor_encoder.neighbor_encoder
+    with torch.no_grad():
+        old = ne.embedding_mlp[2].weight[1, 2].item()
+        ne.embedding_mlp[2].weight[1, 2] = 400.0
+    with warnings.catch_warnings(record=True) as rec:
+        warnings.simplefilter("always")
+        assert f.encodings(obs) is None
+    assert any("torch fp32" in str(r.message) for r in rec)
+    with torch.no_grad():
+        ne.embedding_mlp[2].weight[1, 2] = old
+    out = f.encodings(obs)
+    ref = torch_encodings(pol, obs)
+    assert out is not None and max(rel_err(o, r) for o, r in zip(out, ref)) < 5e-5

@@ -56,3 +56,20 @@ def test_check_inputs_raises_on_out_of_range_observations():
     with pytest.raises(ValueError, match="rollout_precision='fp32'"):
         f.check_inputs()
     assert f._obs_absmax is None                        # reset after every check
+
+
+def test_fused_update_observation_range_guard():
+    """the fused x3 update checks the rollout's observations once per update (PPOTrainer.train) and
+    runs that update's encoders on the torch path when one is beyond layer 0's split-f16 range."""
+    from quadswarm_amd.encoder_train import FusedAttentionTrain
+    pol = SwarmActorCritic(sb_cfg()[1])
+    f = FusedAttentionTrain(pol)
+    obs = torch.randn(64, 28)
+    assert f.obs_in_range(obs)
+    obs[5, 3] = -F16_MAX / X3_SIN
+    with warnings.catch_warnings(record=True) as rec:
+        warnings.simplefilter("always")
+        assert not f.obs_in_range(obs)
+    assert any("torch fp32" in str(r.message) for r in rec)
+    obs[5, 3] = float("nan")                           # non-finite: the env's guard reports those
+    assert f.obs_in_range(obs)

@@ -290,3 +290,53 @@ def test_two_rank_checkpoint_resume_is_bitwise(tmp_path):
         assert "2 ranks" in str(e)
     else:
         raise AssertionError("a 2-rank checkpoint loaded into a 1-rank trainer")
+
+
+def _eval_worker(rank, world, port, path, q):
+    """only rank 0 has an eval env (EvalCallback's documented data-parallel use); DeviceCurriculum must
+    still give every rank an evaluator, or rank 0's evaluation broadcast / best-model save would wait forever."""
+    from quadswarm_amd.callbacks import EvalCallback
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n_steps = 8
+    env, tr = _trainer(rank, seed=3, n_steps=n_steps)
+    eenv = ToyEnvA(E=2, N=4, rank=0, seed=77) if rank == 0 else None
+    cur = DeviceCurriculum(0.6, 0.9, 2.0, window_size=10, verbose=0, step_fn=host_curriculum_step,
+                           eval_env=eenv, eval_freq=4, n_eval_episodes=4)
+    ev = EvalCallback(eenv, n_eval_episodes=4, eval_freq=n_steps, best_model_save_path=os.path.join(path, "best"),
+                      verbose=0)
+    seen = []
+
+    class Watch(TrainerCallback):
+        def on_iteration_end(self, trainer):
+            seen.append((trainer.num_timesteps, len(ev.best_saved), os.path.exists(os.path.join(path, "best",
+                                                                                               "best_model.pt"))))
+    tr.learn(3 * n_steps * world * env.I, callback=[cur, ev, Watch()])
+    sd = cur.state_dict()
+    q.put((rank, cur.evaluator is not None, sorted(sd), sd.get("eval"), ev.state_dict(), seen))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _guarded_eval(*a):
+    _guarded(_eval_worker)(*a)
+
+
+def test_two_rank_evaluation_with_an_eval_env_on_rank_0_only(tmp_path):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_guarded_eval, args=(r, 2, port, str(tmp_path), q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = _get(q, 2)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, has0, keys0, cev0, ev0, seen0), (_, has1, keys1, cev1, ev1, seen1) = res
+    assert has0 and has1                         # rank 1 got an evaluator without an eval env
+    assert keys0 == keys1 == ["eval", "qs_curriculum", "seen"]
+    assert cev0 == cev1 and cev0["n_calls"] == 3 * 8    # same evaluation count and broadcast rewards
+    assert ev0 == ev1 and np.isfinite(ev0["best_mean_reward"])
+    # the best model is written at an iteration boundary (collective), visible to both ranks there
+    assert seen0 == seen1 and seen0[0][1] == 1 and seen0[0][2]

@@ -8,7 +8,7 @@ run() {  # tag env... -- bench args
   timeout -k 10 200 env "$@" > gpurun_out/ab_q/$tag.log 2>&1
   local rc=$?
   echo "$tag rc=$rc $(tail -1 gpurun_out/ab_q/$tag.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["roofline"]["kernel_us"], d["value"])' 2>/dev/null)"
-  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+  if [ $rc -ne 0 ]; then exit $rc; fi
 }
 B="python bench.py --steps 2000 --no-cpu-baseline --e2e-iters 0"
 for cfg in c3 c4 c2 c5 c3mix; do
