@@ -1324,11 +1324,23 @@ __global__ __launch_bounds__(StepGeo<NPAD>::WGS) void step_kernel(const KP* __re
         const bool sact = active && scen_acts(kp, (int)srec[0], (int)srec[2], tick);
         if (ec.wany(sact)) {
             bool via = false;
+            int bz0 = 0;   // ep_rand_bezier: the first accepted try of its rejection loop, searched by the env's lanes
+            if constexpr (!WIDE)
+                if (kp.scen_b == SC_MIX || kp.scen_b == SC_EP_RAND_BEZIER) {
+                    const int steps = (int)(5.f * (1.f / kp.cdt));   // scen_step_lane's period
+                    // the env's active lanes (li < N Q) search; the padding lanes of an env with N < NPAD hold env
+                    // 0's tick / Philox counter and idle
+                    const bool bneed = active && sc_mode(kp, (int)srec[0]) == SC_EP_RAND_BEZIER &&
+                                       (tick % steps == 0 || tick == 1);
+                    if (ec.wany(bneed))
+                        bz0 = bz_first_parallel<LPE>(kp, srec, bneed, li, lbase, kp.N * Q, rng,
+                                                     kp.id0 + (uint32_t)(env * kp.N), stab);
+                }
             if (sact) {
                 Scen sc;
                 scen_from_words(srec, sc);
                 SDraw sd = sdraw(rng, kp.id0 + (uint32_t)(env * kp.N), S_SCN);
-                const int ch = scen_step_lane(kp, sc, tick, sd, di, stab, stab + 4 * (NPAD + 4), d.goal, via);
+                const int ch = scen_step_lane(kp, sc, tick, sd, di, stab, stab + 4 * (NPAD + 4), d.goal, via, bz0);
                 if (di == 0 && q == 0) {
                     if (ch == 2) scen_store(kp, b, env, sc);
                     else if (ch == 1) scen_store_size(kp, b, env, sc);

@@ -83,6 +83,33 @@ __device__ __forceinline__ uint32_t sd_word(SDraw& s) {
 }
 __device__ __forceinline__ float sd_uniform(SDraw& s, float lo, float hi) { return lo + (hi - lo) * u01(sd_word(s)); }
 __device__ __forceinline__ int sd_int(SDraw& s, int lo, int hi) { return lo + ufloor(sd_word(s), hi - lo); }
+// One try of ep_rand_bezier's rejection loop (ep_rand_bezier.py:20-33): 6 uniforms + 1 integer = 7 words from sd's
+// position, so try i reads words 7 i .. 7 i + 6 of the step's scenario stream (the loop draws nothing else first).
+// np_: the candidate's two control points [c][j]; returns whether both lie inside the shrunk bounds.
+constexpr int BZ_WORDS = 7, BZ_MAX_TRIES = 1024;
+__device__ __forceinline__ bool bz_try(SDraw& sd, const float* hi, const float* lo, float mx, const float* g,
+                                       float (&np_)[3][2]) {
+    float u[6];   // uniform(size=(2, 3)).reshape(3, 2): [c][j] = flat 2c + j
+    for (int k = 0; k < 6; ++k) u[k] = sd_uniform(sd, -hi[k % 3], hi[k % 3]);
+    const float mag = (float)sd_int(sd, (int)ceilf(mx * 0.5f), (int)floorf(mx) + 1);
+    bool ok = true;
+    for (int j = 0; j < 2; ++j) {
+        const float v0 = u[j], v1 = u[2 + j], v2 = u[4 + j];
+        const float sc = mag / fsqrt(v0 * v0 + v1 * v1 + v2 * v2);
+        np_[0][j] = v0 * sc + g[0]; np_[1][j] = v1 * sc + g[1]; np_[2][j] = v2 * sc + g[2];
+        for (int k = 0; k < 3; ++k) ok = ok && np_[k][j] > lo[k] + 0.5f && np_[k][j] < hi[k] - 0.5f;
+    }
+    return ok;
+}
+// the bounds of the tries for a formation of size `size` (ep_rand_bezier.py:13-19)
+__device__ __forceinline__ float bz_bounds(const KP& kp, float size, float* hi, float* lo) {
+    float rd[3];
+    for (int k = 0; k < 3; ++k) rd[k] = kp.room_hi[k] - kp.room_lo[k] - size;
+    const float mx = fminf(fmaxf(fmaxf(rd[0], rd[1]), rd[2]), 30.f);
+    hi[0] = rd[0] * 0.5f; hi[1] = rd[1] * 0.5f; hi[2] = rd[2];
+    lo[0] = -hi[0]; lo[1] = -hi[1]; lo[2] = 0.f;
+    return mx;
+}
 // Generator.shuffle as Fisher-Yates from the top over LDS rows g[4 i ..]
 __device__ __forceinline__ void sd_shuffle(SDraw& s, float* g, int n) {
     for (int i = n - 1; i >= 1; --i) {
@@ -341,26 +368,12 @@ __device__ void scen_step(const KP& kp, Scen& s, int tick, SDraw& sd, float* g, 
     } else if (s.mode == SC_EP_RAND_BEZIER) {   // ep_rand_bezier.py:6-47
         const int steps = (int)(5.f * cf);
         const int t = tick % steps;
-        float rd[3], hi[3], lo[3];
-        for (int k = 0; k < 3; ++k) rd[k] = kp.room_hi[k] - kp.room_lo[k] - s.size;
-        const float mx = fminf(fmaxf(fmaxf(rd[0], rd[1]), rd[2]), 30.f);
-        hi[0] = rd[0] * 0.5f; hi[1] = rd[1] * 0.5f; hi[2] = rd[2];
-        lo[0] = -hi[0]; lo[1] = -hi[1]; lo[2] = 0.f;
+        float hi[3], lo[3];
+        const float mx = bz_bounds(kp, s.size, hi, lo);
         if (t == 0 || tick == 1) {
             float np_[3][2];
-            for (int tries = 0;; ++tries) {   // uniform(size=(2, 3)).reshape(3, 2): [c][j] = flat 2c + j
-                float u[6];
-                for (int k = 0; k < 6; ++k) u[k] = sd_uniform(sd, -hi[k % 3], hi[k % 3]);
-                const float mag = (float)sd_int(sd, (int)ceilf(mx * 0.5f), (int)floorf(mx) + 1);
-                bool ok = true;
-                for (int j = 0; j < 2; ++j) {
-                    const float v0 = u[j], v1 = u[2 + j], v2 = u[4 + j];
-                    const float sc = mag / fsqrt(v0 * v0 + v1 * v1 + v2 * v2);
-                    np_[0][j] = v0 * sc + g[0]; np_[1][j] = v1 * sc + g[1]; np_[2][j] = v2 * sc + g[2];
-                    for (int k = 0; k < 3; ++k) ok = ok && np_[k][j] > lo[k] + 0.5f && np_[k][j] < hi[k] - 0.5f;
-                }
-                if (ok || tries >= 1023) break;   // the reference loops without a bound
-            }
+            for (int tries = 0;; ++tries)   // the reference loops without a bound
+                if (bz_try(sd, hi, lo, mx, g, np_) || tries >= BZ_MAX_TRIES - 1) break;
             for (int k = 0; k < 3; ++k) {
                 s.bz[k] = g[k];
                 s.bz[3 + k] = np_[k][0];
@@ -554,7 +567,7 @@ __device__ __forceinline__ void scen_from_words(const uint32_t* r, Scen& s) {
 // set via_tab: the new goal is tb's row di after a barrier).  goal: in, the drone's goal; out, its new goal.
 // Returns what of the scenario record changed: 0 nothing, 1 size / inc / speed, 2 more (the whole record).
 __device__ __forceinline__ int scen_step_lane(const KP& kp, Scen& s, int tick, SDraw& sd, int di, const float* ta,
-                                              float* tb, float* goal, bool& via_tab) {
+                                              float* tb, float* goal, bool& via_tab, int bz_first = 0) {
     const int N = kp.N;   // index arithmetic (a constant of the specialised kernel); float geometry: sc_row / sc_num
     const float box = kp.spawn_box, cf = 1.f / kp.cdt;
     const int pl = sc_per_layer(s.form);
@@ -614,27 +627,16 @@ __device__ __forceinline__ int scen_step_lane(const KP& kp, Scen& s, int tick, S
     } else if (mode == SC_EP_RAND_BEZIER) {   // ep_rand_bezier.py:6-47
         const int steps = (int)(5.f * cf);
         const int t = tick % steps;
-        float rd[3], hi[3], lo[3];
-        for (int k = 0; k < 3; ++k) rd[k] = kp.room_hi[k] - kp.room_lo[k] - s.size;
-        const float mx = fminf(fmaxf(fmaxf(rd[0], rd[1]), rd[2]), 30.f);
-        hi[0] = rd[0] * 0.5f; hi[1] = rd[1] * 0.5f; hi[2] = rd[2];
-        lo[0] = -hi[0]; lo[1] = -hi[1]; lo[2] = 0.f;
+        float hi[3], lo[3];
+        const float mx = bz_bounds(kp, s.size, hi, lo);
         int ch = 0;
         if (t == 0 || tick == 1) {
+            // the rejection loop from try bz_first on (the first try any lane of the env found accepted, or 0): the
+            // tries before it are rejected, so the loop ends on the same try as one from 0 would
             float np_[3][2];
-            for (int tries = 0;; ++tries) {   // uniform(size=(2, 3)).reshape(3, 2): [c][j] = flat 2c + j
-                float u[6];
-                for (int k = 0; k < 6; ++k) u[k] = sd_uniform(sd, -hi[k % 3], hi[k % 3]);
-                const float mag = (float)sd_int(sd, (int)ceilf(mx * 0.5f), (int)floorf(mx) + 1);
-                bool ok = true;
-                for (int j = 0; j < 2; ++j) {
-                    const float v0 = u[j], v1 = u[2 + j], v2 = u[4 + j];
-                    const float sc = mag / fsqrt(v0 * v0 + v1 * v1 + v2 * v2);
-                    np_[0][j] = v0 * sc + ta[0]; np_[1][j] = v1 * sc + ta[1]; np_[2][j] = v2 * sc + ta[2];
-                    for (int k = 0; k < 3; ++k) ok = ok && np_[k][j] > lo[k] + 0.5f && np_[k][j] < hi[k] - 0.5f;
-                }
-                if (ok || tries >= 1023) break;   // the reference loops without a bound
-            }
+            sd.k += (uint32_t)(BZ_WORDS * bz_first);
+            for (int tries = bz_first;; ++tries)   // the reference loops without a bound
+                if (bz_try(sd, hi, lo, mx, ta, np_) || tries >= BZ_MAX_TRIES - 1) break;
             for (int k = 0; k < 3; ++k) {
                 s.bz[k] = ta[k];
                 s.bz[3 + k] = np_[k][0];
@@ -683,6 +685,37 @@ __device__ __forceinline__ int scen_step_lane(const KP& kp, Scen& s, int tick, S
     }
     return 0;
 }
+// ep_rand_bezier's rejection loop over the env's lanes: the env's LA active lanes (li < LA) evaluate tries li,
+// li + LA, ... (each try's 7 words sit at a fixed offset of the stream), a ballot of their lane segment finds the
+// first accepted try; returns it (the same on the env's lanes), or BZ_MAX_TRIES - 1 when none of the first
+// BZ_MAX_TRIES - 1 tries is accepted, i.e. where the serial loop stops.  `need`: this lane's env resamples at this
+// tick (false on other lanes: they idle through the rounds).  An env that needed ~300 tries held its wave (and the
+// launch) for ~340 us serially (c3mix, ticks 1 / 500 / 1000).
+template <int LPE>
+__device__ __forceinline__ int bz_first_parallel(const KP& kp, const uint32_t* srec, bool need, int li, int lbase,
+                                                 int LA, const Rng& r, uint32_t key, const float* ta) {
+    static_assert(LPE <= 64, "the env's lanes inside one wave");
+    const uint64_t seg = LA >= 64 ? ~0ull : ((1ull << LA) - 1ull);
+    float hi[3], lo[3];
+    const float mx = bz_bounds(kp, __uint_as_float(srec[4]), hi, lo);
+    int found = need ? -1 : 0;
+    for (int rd = 0;; ++rd) {
+        const int tr = rd * LA + li;
+        bool ok = false;
+        if (found < 0 && tr < BZ_MAX_TRIES) {
+            SDraw t = sdraw(r, key, S_SCN);
+            t.k = (uint32_t)(BZ_WORDS * tr);
+            float np_[3][2];
+            ok = bz_try(t, hi, lo, mx, ta, np_);
+        }
+        const uint64_t m = (__ballot(ok) >> lbase) & seg;
+        if (found < 0 && m) found = min(rd * LA + (int)__ffsll((long long)m) - 1, BZ_MAX_TRIES - 1);
+        if (found < 0 && (rd + 1) * LA >= BZ_MAX_TRIES - 1) found = BZ_MAX_TRIES - 1;
+        if (__ballot(found < 0) == 0ull) break;
+    }
+    return found;
+}
+
 __device__ __forceinline__ void scen_store_size(const KP& kp, const Bufs& b, int env, const Scen& s) {
     b.env[QS_E_SC_INC * kp.E + env] = s.inc;
     *scf(b.envf, kp.E, env, QS_ENVF_SC_SIZE) = s.size;

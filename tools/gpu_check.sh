@@ -20,6 +20,7 @@ for s in "$@"; do
   case $s in
     smoke) step smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) step gpu_tests 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
+    testsel) step gpu_tests_sel 900 python -u -m pytest ${TESTS:?TESTS=<test files>} -x -v --timeout 200 --timeout-method thread ;;
     testsall) step gpu_tests 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread ;;
     testsnew) step gpu_tests_new 600 python -u -m pytest tests/test_gpu_stats.py tests/test_gpu_guard_params.py tests/test_gpu_c5.py -v --timeout 200 --timeout-method thread ;;
     testspar) step gpu_tests_par 900 python -u -m pytest tests/test_gpu_stats.py tests/test_gpu_parity.py tests/test_gpu_parity_a.py -v --timeout 300 --timeout-method thread ;;
@@ -183,7 +184,7 @@ for s in "$@"; do
       done
       ;;
     scenbit)   # scenario kernels bitwise against a base source tree (BASE, same ABI), then the scenario parity tests
-      step scen_bitwise 300 python tools/scen_bitwise.py ${BASE:-tools/jit/base} 1600
+      step scen_bitwise 400 python tools/scen_bitwise.py ${BASE:-tools/jit/base_r06} 1600
       step scen_tests 400 python -u -m pytest tests/test_gpu_parity_scen.py -q --timeout 200 --timeout-method thread
       ;;
     e2eprof)   # kernel trace of one C3 end-to-end PPO iteration (where update_s goes)
@@ -207,6 +208,9 @@ for s in "$@"; do
       step window_kt 300 rocprofv3 --kernel-trace --stats -d gpurun_out/window_kt -o kt --output-format csv -- python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --e2e-iters 0
       python3 tools/dispatch_summary.py gpurun_out/window_kt --all > gpurun_out/window_dispatch.txt 2>&1
       find gpurun_out/window_kt -name "*kernel_trace.csv" -delete
+      ;;
+    launch)    # launch-path A/B of the driver's 20-step window (tools/launch_probe.py)
+      step launch_probe 300 python tools/launch_probe.py --reps 10
       ;;
     mixtrace)  # per-dispatch trace of c3mix (the slow-launch outlier)
       export TMPDIR=/tmp

@@ -1,9 +1,10 @@
 #!/usr/bin/env python
 """Bitwise A/B of the flavor-B goal-scenario kernels: for each (quads_mode, drones) case, K steps of a specialised
-env compiled from the current sources and from a base source directory (QS_JIT_SRC_DIR, e.g. tools/jit/base_r04 =
-the previous round's kernels), digests of obs / rewards / dones every step plus the final env state.  Diagnostic.
+env compiled from the current sources and from a base source directory (QS_JIT_SRC_DIR, e.g. tools/jit/base_r06 =
+the kernels of an earlier commit with this library's ABI: `git show <rev>:<file>` of the six kernel headers and
+include/quadswarm.h), digests of obs / rewards / dones every step plus the final env state.  Diagnostic.
 
-    python tools/scen_bitwise.py tools/jit/base_r04 [steps] [mode:N ...]"""
+    python tools/scen_bitwise.py tools/jit/base_r06 [steps] [mode:N ...]"""
 import hashlib
 import os
 import sys
@@ -40,13 +41,11 @@ def digest(mode, n, steps, src):
         obs, rew, done, _ = env.step(acts)
         for t in (obs, rew, done):
             h.update(t.detach().cpu().numpy().tobytes())
-    # the final state: drone state, env ints and env floats with the scenario block as [row][E] rows (the current
-    # kernels store it env-major, ABI 13; the round-4 base as rows)
-    from quadswarm_amd import _native as NAT
-    ef = env.env_f.cpu().numpy()
+    # the final state: drone state, env ints and env floats (the base tree has this library's ABI -- the library
+    # refuses another -- so the same layout)
     h.update(env.state.cpu().numpy().tobytes())
     h.update(env.env_state.cpu().numpy().tobytes())
-    h.update((ef if src else NAT.env_f_rows(ef)).tobytes())
+    h.update(env.env_f.cpu().numpy().tobytes())
     env.close()
     return h.hexdigest()
 
