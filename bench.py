@@ -213,11 +213,19 @@ def pmc_traffic(config):
 VALU_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md chip table: FP32 vector (v_pk_fma_f32, 64 FLOP/clk/SIMD)
 
 
+SIMDS = 1024                  # 256 CUs x 4 SIMDs
+
+
 def valu_roofline(config, agents_per_launch, kernel_ms):
-    """The VALU side of a flavor-A step (flavor A is near the fp32-vector ridge), from the committed PMC
-    summary profiles/pmc_<config>.json (tools/summarize_prof.py):
+    """The VALU side of the step (flavor A is near the fp32-vector ridge; flavor B's waves are issue /
+    latency-bound below the HBM roofline), from the committed PMC summary profiles/pmc_<config>.json
+    (tools/summarize_prof.py):
       issue_frac   VALU instructions issued per wave / the wave's lifetime in quad-cycles (SQ_INSTS_VALU /
-                   SQ_WAVE_CYCLES per wave; one wave per SIMD, so the SIMD's VALU issue share)
+                   SQ_WAVE_CYCLES per wave; a wave64 VALU instruction occupies its SIMD for one quad-cycle)
+      waves_per_simd, simd_issue_frac   SQ_WAVES / 1024 SIMDs, and that many waves' VALU issue against one wave's
+                   lifetime: the share of the SIMD's VALU issue slots the launch uses (C3: 2 waves per SIMD)
+      issue_floor_us   simd_issue_frac x this line's kernel time: the launch if every SIMD issued VALU back to back
+                   (no memory / LDS / dependency wait); kernel_us / issue_floor_us is the latency factor
       flop         executed fp32 FLOP per launch = 64 lanes x (2 FMA + ADD + MUL + TRANS) instructions
                    (SQ_INSTS_VALU_{FMA,ADD,MUL,TRANS}_F32, the derived-counter formula of rocprofiler's
                    TOTAL_32_OPS without the integer and MFMA terms), per agent-step, and the rate at this
@@ -234,6 +242,13 @@ def valu_roofline(config, agents_per_launch, kernel_ms):
             out.update(valu_insts_per_wave=round(pw["SQ_INSTS_VALU"], 1),
                        wave_quad_cycles=round(pw["SQ_WAVE_CYCLES"], 1),
                        issue_frac=round(pw["SQ_INSTS_VALU"] / pw["SQ_WAVE_CYCLES"], 4))
+            if "SQ_WAVES" in c:
+                wps = c["SQ_WAVES"] / SIMDS
+                sif = wps * pw["SQ_INSTS_VALU"] / pw["SQ_WAVE_CYCLES"]
+                out.update(waves_per_simd=round(wps, 3), simd_issue_frac=round(sif, 4),
+                           issue_floor_us=round(sif * kernel_ms * 1e3, 3))
+            if "SQ_WAIT_ANY" in pw:
+                out["wait_frac"] = round(pw["SQ_WAIT_ANY"] / pw["SQ_WAVE_CYCLES"], 4)
         keys = ("SQ_INSTS_VALU_FMA_F32", "SQ_INSTS_VALU_ADD_F32", "SQ_INSTS_VALU_MUL_F32", "SQ_INSTS_VALU_TRANS_F32")
         if all(k in c for k in keys):
             flop = 64.0 * (2 * c[keys[0]] + c[keys[1]] + c[keys[2]] + c[keys[3]])
@@ -670,6 +685,25 @@ def main(argv=None):
         dist.barrier()
     total_agent_steps, el, per_rank = aggregate_ranks(I * args.steps, el, world, dev)
 
+    # the timed region's fixed cost, measured after it (untimed): the same event records and synchronize with no
+    # step between them (median of 5) -- the wall the region pays whatever the kernel time
+    empties = []
+    for _ in range(5):
+        e0_, e1_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize(dev)
+        t0_ = time.perf_counter()
+        e0_.record(stream)
+        e1_.record(stream)
+        torch.cuda.synchronize(dev)
+        empties.append(((time.perf_counter() - t0_) * 1e6, e0_.elapsed_time(e1_) * 1e3))
+    empty_wall, empty_ev = sorted(empties)[2]
+    window = {"region_wall_us": round(el * 1e6, 2), "region_events_us": round(k_ms * args.steps * 1e3, 2),
+              "host_side_us": round(el * 1e6 - k_ms * args.steps * 1e3, 2),
+              "empty_region_wall_us": round(empty_wall, 2), "empty_region_events_us": round(empty_ev, 2),
+              "note": "region wall = region events (graph launch latency + the step kernels) + host side (event "
+                      "records, synchronize wake-up); tools/window_probe.py and profiles/r06/window_* split it "
+                      "per launch"}
+
     # secondary: one eager launch of the one handle bracketed by its own events (includes the host launch gap)
     nk = min(200, max(20, args.steps // 10))
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(nk)]
@@ -755,7 +789,8 @@ def main(argv=None):
                                                        if cfg.flavor == "B" and traffic_src and
                                                        traffic_src.get("read_bytes") else None),
                          "bytes_per_launch": round(bpa * I / S),
-                         "valu": valu_roofline(args.config, I, k_ms) if cfg.flavor == "A" else None},
+                         "valu": valu_roofline(args.config, I, k_ms)},
+            "window": window,
             "nonfinite_guard": guard,
             "cpu_baseline": None,
             "end_to_end": e2e,

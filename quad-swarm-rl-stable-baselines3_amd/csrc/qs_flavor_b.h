@@ -656,8 +656,9 @@ __device__ __forceinline__ void load_words_q(const KP& kp, const Bufs& b, int g,
     }
 }
 // the drone on every sub-lane; stw (if given) gets the STAT_WORDS words as floats
-template <int Q, int NW, int NIW = 4>
-__device__ __forceinline__ void unpack_words_q(const DroneWords<Q, NW>& dw, Drone& d, float* stw = nullptr) {
+// DEAL (Q = 4, QS_DEAL_MOTORS): the motor words 18..29 are the sub-lane's own motor's (no broadcast; see motors_dealt4)
+template <int Q, int NW, int NIW = 4, bool DEAL = false>
+__device__ __forceinline__ void unpack_words_q(const DroneWords<Q, NW>& dw, Drone& d, float* stw = nullptr, int q = 0) {
     constexpr int T = DroneWords<Q, NW>::T, DW = WordsOf<NIW>::DW;
     const uint32_t (&r)[T] = dw.r;
     uint32_t wv[T * Q > DW ? T * Q : DW];
@@ -675,11 +676,23 @@ __device__ __forceinline__ void unpack_words_q(const DroneWords<Q, NW>& dw, Dron
     }
 #pragma unroll
     for (int i = 0; i < 9; ++i) d.rot[i] = __int_as_float((int)wv[QS_F_ROT + i]);
+    if constexpr (DEAL) {
+        static_assert(Q == 4, "dealt motors: one motor per sub-lane");
+        // the sub-lane's word of field F: F + ((q - F) & 3), in register slot (that word) / 4 -- F / 4 or F / 4 + 1
+        auto own = [&](int F) {
+            const int t = (F + ((q - F) & 3)) >> 2;
+            return __int_as_float((int)(t == F / 4 ? r[F / 4] : r[F / 4 + 1]));
+        };
+        const float rd = own(QS_F_ROT_DAMP), cd = own(QS_F_CMD_DAMP), ou = own(QS_F_OU);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { d.rd[i] = rd; d.cd[i] = cd; d.ou[i] = ou; }
+    } else {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         d.rd[i] = __int_as_float((int)wv[QS_F_ROT_DAMP + i]);
         d.cd[i] = __int_as_float((int)wv[QS_F_CMD_DAMP + i]);
         d.ou[i] = __int_as_float((int)wv[QS_F_OU + i]);
+    }
     }
     constexpr int IW = QS_F_GOAL + 3;
     d.svd = (int32_t)wv[IW + QS_I_SVD];
@@ -742,6 +755,70 @@ __device__ __forceinline__ void store_drone_q(const KP& kp, const Bufs& b, int g
         const bool wr = w < DW || (w < NW && ((stmask >> (w - DW)) & 1u));
         if (active && wr) st_wt1(rs, drone_word_off<NIW>(kp, b, w, go), 0u, v);
     }
+}
+
+// Dealt motors (QS_DEAL_MOTORS, Q = 4): sub-lane q runs motor m = (q + 2) & 3 of its drone -- the motor whose
+// rot_damp / cmd_damp / OU words (fields 18 + m, 22 + m, 26 + m: word w sits on sub-lane w % 4) that sub-lane already
+// loads and stores, so they need no broadcast.  The drone's Drone::rd / cd / ou hold that motor's value in all four
+// entries on the sub-lane (unpack_words_q<.., DEAL>, reset and the floor branch write every entry; the store takes word
+// F + m from sub-lane q, i.e. the owner's copy).  The motor filter, its noise and its thrust run once per motor
+// instead of four times per lane; thrust and the three torques are summed over the quad by qsum (DPP butterfly: every
+// sub-lane gets the same bits, so the replicated rest of the substep stays bit-identical on the quad).  The sums are
+// (m0 + m1) + (m2 + m3) instead of a running sum over the motors: fp32 reassociation, inside the parity tolerances
+// (the oracle is float64).  Measured slower on C3 / C2 / C4 (7.20 -> 7.28, 5.04 -> 5.08, 9.72 -> 9.82 us,
+// profiles/ab/r06_deal_motors_ab.txt; parity green either way): the quad sums lengthen the wave's dependency chain
+// more than the replicated motor arithmetic costs in issue slots.  Off by default; -DQS_DEAL_MOTORS=1 for A/Bs.
+#ifndef QS_DEAL_MOTORS
+#define QS_DEAL_MOTORS 0
+#endif
+struct MotorK {   // the sub-lane's motor: thrust_max, the three torque-arm coefficients, torque_max * ccw
+    float tmax, p0, p1, p2, tq;
+};
+__device__ __forceinline__ float sel4(int m, float a, float b, float c, float d) {
+    return m == 0 ? a : (m == 1 ? b : (m == 2 ? c : d));
+}
+__device__ __forceinline__ MotorK motor_k(const KP& kp, int m) {
+    MotorK k;
+    k.tmax = sel4(m, kp.thrust_max[0], kp.thrust_max[1], kp.thrust_max[2], kp.thrust_max[3]);
+    k.p0 = sel4(m, kp.pc0[0], kp.pc0[1], kp.pc0[2], kp.pc0[3]);
+    k.p1 = sel4(m, kp.pc1[0], kp.pc1[1], kp.pc1[2], kp.pc1[3]);
+    k.p2 = sel4(m, kp.pc2[0], kp.pc2[1], kp.pc2[2], kp.pc2[3]);
+    k.tq = sel4(m, kp.torque_max[0] * kp.ccw[0], kp.torque_max[1] * kp.ccw[1], kp.torque_max[2] * kp.ccw[2],
+                kp.torque_max[3] * kp.ccw[3]);
+    return k;
+}
+// motors() for the sub-lane's motor (quadrotor_dynamics.py:511-533), the sums over the quad
+__device__ __forceinline__ Torque motors_dealt4(const KP& kp, Drone& d, float cmd, float noise, const MotorK& mk) {
+    float tau = cmd < d.cd[0] ? kp.tau_down : kp.tau_up;
+    tau = fminf(tau, 1.0f);
+    const float r = tau * (fsqrt(cmd) - d.rd[0]) + d.rd[0];
+    const float c = clampf(r * r + cmd * noise, 0.f, 1.f);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { d.rd[k] = r; d.cd[k] = c; }
+    const float th = mk.tmax * (kp.lin == 1.f ? c : (1.f - kp.lin) * c * c + kp.lin * c);
+    Torque t;
+    t.t0 = qsum<4>(mk.p0 * th);
+    t.t1 = qsum<4>(mk.p1 * th);
+    t.t2 = qsum<4>(mk.p2 * th + mk.tq * c);
+    t.sum = qsum<4>(th);
+    return t;
+}
+__device__ __forceinline__ void substep_dealt4(const KP& kp, Drone& d, float cmd, float noise, const MotorK& mk,
+                                               const Rng& rng, uint32_t gid, int s) {
+    const Torque tq = motors_dealt4(kp, d, cmd, noise, mk);
+    {
+        const RodCoef rc = rod_coef(kp, d.rot, d.om);
+        float Rn[9];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            float dr[3];
+            rod_row(rc, i, dr);
+            rod_apply_row(dr, d.rot, Rn + 3 * i);
+        }
+#pragma unroll
+        for (int i = 0; i < 9; ++i) d.rot[i] = Rn[i];
+    }
+    substep_tail(kp, d, tq, rng, gid, s);
 }
 
 // Sub-lanes per drone of the flavor-B step kernel (QS_QB; 64 / NPAD when an env would not fit a wave).
@@ -939,7 +1016,8 @@ __global__ __launch_bounds__(StepGeo<NPAD>::WGS) void step_kernel(const KP* __re
     QS_PRIO(11);
     __builtin_amdgcn_sched_barrier(0);
     float stw[STAT_WORDS];
-    unpack_words_q<Q, LW, NIW>(dw, d, stw);
+    constexpr bool DEALM = QS_DEAL_MOTORS && Q == 4;
+    unpack_words_q<Q, LW, NIW, DEALM>(dw, d, stw, q);
     float a[4] = {av.x, av.y, av.z, av.w};
     const int tick = tick0 + 1;
     const bool done = tick > kpm.ep_len;
@@ -969,12 +1047,23 @@ __global__ __launch_bounds__(StepGeo<NPAD>::WGS) void step_kernel(const KP* __re
     bool floor_now = false;   // drone 0's on the env's flags: its rew_crash feeds the replay wrapper
     float rc_dist, rc_effort, rc_orient, rc_spin;   // compute_reward_weighted's raw terms (per-step infos)
     {
+        if constexpr (DEALM) {   // the sub-lane's motor m (motors_dealt4)
+            const int m = (q + 2) & 3;
+            const float zm = sel4(m, zou[0], zou[1], zou[2], zou[3]), am = sel4(m, a[0], a[1], a[2], a[3]);
+            const float ou = d.ou[0] + (kp.ou_theta * (kp.ou_mu - d.ou[0]) + kp.ou_sigma * zm);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) d.ou[k] = ou;
+            const float cmd = 0.5f * (clampf(am, -1.f, 1.f) + 1.f);
+            const MotorK mk = motor_k(kp, m);
+            for (int s = 0; s < kp.sim_steps; ++s) substep_dealt4(kp, d, cmd, ou, mk, rng, gid, s);
+        } else {
 #pragma unroll
         for (int k = 0; k < 4; ++k) d.ou[k] = d.ou[k] + (kp.ou_theta * (kp.ou_mu - d.ou[k]) + kp.ou_sigma * zou[k]);
         float cmds[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) cmds[k] = 0.5f * (clampf(a[k], -1.f, 1.f) + 1.f);
         for (int s = 0; s < kp.sim_steps; ++s) substep(kp, d, cmds, d.ou, rng, gid, s);
+        }
         // compute_reward_weighted (quadrotor_single.py:34-66)
         const float gx = d.goal[0] - d.pos[0], gy = d.goal[1] - d.pos[1], gz = d.goal[2] - d.pos[2];
         const bool on_floor = d.flags & QS_FL_ON_FLOOR;

@@ -209,6 +209,11 @@ for s in "$@"; do
       python3 tools/dispatch_summary.py gpurun_out/window_kt --all > gpurun_out/window_dispatch.txt 2>&1
       find gpurun_out/window_kt -name "*kernel_trace.csv" -delete
       ;;
+    abjit)     # interleaved A/B of a kernel macro: CONFIGS, AB="tag:-DX=0 tag2:" (twice each, in order)
+      for c in ${CONFIGS:-c3}; do
+        CONFIG=$c STEPS=${STEPS:-2000} step abjit_$c 900 bash tools/ab_jit.sh ${AB:?AB=tag:defs ...} ${AB}
+      done
+      ;;
     launch)    # launch-path A/B of the driver's 20-step window (tools/launch_probe.py)
       step launch_probe 300 python tools/launch_probe.py --reps 10
       ;;
