@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define QS_ABI_VERSION 13
+#define QS_ABI_VERSION 14
 #define QS_MAX_AGENTS 128           /* drones per env: up to 64 inside one 64-lane wavefront, 128 = a two-wave
                                        workgroup per env (flavor B without obstacles; paper/fps_compare.py:7) */
 #define QS_MAX_DR_CHOICES 8         /* entries per obstacle domain-randomisation list */
@@ -99,6 +99,11 @@ enum qs_scenario {
     QS_SCEN_SWAP_GOALS = 12,           /* swap_goals.py                                                */
     QS_SCEN_SWARM_VS_SWARM = 13,       /* swarm_vs_swarm.py                                            */
     QS_SCEN_RUN_AWAY = 14,             /* run_away.py                                                  */
+    /* flavor B with obstacles: the maps' dynamic scenarios (QUADS_MODE_LIST_OBSTACLES_TEST, scenarios/utils.py:18-20;
+     * the reference reaches them through create_scenario, scenarios/mix.py:24-36) -- ABI 14 */
+    QS_SCEN_O_SWAP_GOALS = 15,         /* scenarios/obstacles/o_swap_goals.py                          */
+    QS_SCEN_O_EP_RAND_BEZIER = 16,     /* scenarios/obstacles/o_ep_rand_bezier.py                      */
+    QS_SCEN_O_DYNAMIC_SAME_GOAL = 17,  /* scenarios/obstacles/o_dynamic_same_goal.py                   */
 };
 
 /* Environment + physical configuration.  Physical constants are derived on the host exactly like

@@ -71,6 +71,8 @@ class OrSDraw(ctypes.Structure):  # or_sdraw: scenario draw source (tape or Phil
 SC_MODES = ["static_same_goal", "static_diff_goal", "ep_lissajous3D", "ep_rand_bezier", "dynamic_same_goal",
             "dynamic_diff_goal", "dynamic_formations", "swap_goals", "swarm_vs_swarm", "run_away"]
 SC_NONE, SC_MIX = -1, 10
+SC_O_SWAP_GOALS, SC_O_EP_RAND_BEZIER, SC_O_DYNAMIC_SAME_GOAL = 11, 12, 13   # the obstacle maps' dynamic scenarios
+OSCEN_MODES = ["o_swap_goals", "o_ep_rand_bezier", "o_dynamic_same_goal"]  # obstacle modes 2, 3, 4
 S_SCN, S_SCN_RESET = 23, 24
 S_DR = 26
 
@@ -184,6 +186,8 @@ def lib():
         L.or_cell_xy.argtypes = [I, I, I, P(D)]
         L.or_scen_reset.argtypes = [P(OrParams), P(OrScen), P(OrSDraw), P(D)]
         L.or_scen_step.argtypes = [P(OrParams), P(OrScen), I, P(OrSDraw), P(D)]
+        L.or_oscen_reset.argtypes = [P(OrParams), I, P(OrScen), P(OrSDraw), P(ctypes.c_ubyte), I, P(I), P(D), P(D)]
+        L.or_oscen_step.argtypes = [P(OrParams), P(OrScen), I, P(OrSDraw), P(ctypes.c_ubyte), I, P(D)]
         L.or_generate_goals.argtypes = [I, I, I, D, D, P(D), P(D)]
         L.or_generate_goals.restype = I
         L.or_philox4x32_10.argtypes = [P(ctypes.c_uint32), P(ctypes.c_uint32), P(ctypes.c_uint32)]

@@ -792,6 +792,18 @@ static void obstacle_reset(const or_params* p, or_env* ev, uint32_t gbase, or_rn
             or_cell_xy(a / n, a % n, n, spawn[i]); spawn[i][2] = sz[i];
             or_cell_xy(b / n, b % n, n, goal[i]); goal[i][2] = gz[i];
         }
+    } else if (mode >= 2) {   /* the dynamic modes (Philox: the GPU's obstacle_reset_env order) */
+        choose_k(r, gbase, OR_S_OSCEN, 1, F, N, sp);
+        for (int i = 0; i < N; ++i)
+            sz[i] = 1.0 + 2.0 * or_philox_uniform(r->seed, gbase + (uint32_t)i, OR_S_RESET | OR_UNIF_BIT, r->step, 3);
+        or_sdraw sd;
+        memset(&sd, 0, sizeof sd);
+        sd.mode = OR_RNG_PHILOX; sd.seed = r->seed; sd.key = gbase; sd.stream = OR_S_SCN_RESET; sd.step = r->step;
+        or_oscen_reset(p, mode, &ev->scen, &sd, map, n, NULL, NULL, goal);
+        for (int i = 0; i < N; ++i) {
+            int a = fr[sp[i]];
+            or_cell_xy(a / n, a % n, n, spawn[i]); spawn[i][2] = sz[i];
+        }
     } else {           /* o_static_same_goal */
         if (tape) {
             (void)tape_next(r);   /* duration_time */
@@ -901,7 +913,9 @@ void or_episode_stats_done(const or_params* p, or_env* ev, or_drone* dr, int N) 
     s[OR_ES_COLRATE] = 1.0 - (double)n_ok / N;
     s[OR_ES_NCOLRATE] = 1.0 - (double)n_ha / N;
     s[OR_ES_OCOLRATE] = 1.0 - (double)n_ho / N;
-    s[OR_ES_SCEN] = p->use_obstacles ? 16 + ev->obst_mode : (p->scenario_b == OR_SC_NONE ? 0 : ev->scen.mode);
+    /* scenario ids of quadswarm_amd.stats: 16 + mode for o_random / o_static_same_goal, 17 + mode for the dynamic ones */
+    s[OR_ES_SCEN] = p->use_obstacles ? (ev->obst_mode < 2 ? 16 : 17) + ev->obst_mode
+                                     : (p->scenario_b == OR_SC_NONE ? 0 : ev->scen.mode);
     const int win[3] = {(int)(1.0 * freq), (int)(3.0 * freq), (int)(5.0 * freq)};
     for (int i = 0; i < N; ++i)
         for (int k = 0; k < 3; ++k) dr[i].ep_dist[k] = dr[i].dsum[k] / (double)(win[k] < T ? win[k] : T) / p->dt;
@@ -1099,13 +1113,25 @@ void or_env_step(const or_params* p, or_drone* drones, or_env* envs, int e, cons
     for (int i = 0; i < N; ++i) dr[i].prev_obst = ocol[i] >= 0;
     /* 4. scenario.step() (:700-701): new goals; the observations above keep the old ones unless the
      * state-update flag makes the reference recompute them below */
-    if (p->scenario_b != OR_SC_NONE && !p->use_obstacles) {
+    if ((p->scenario_b != OR_SC_NONE && !p->use_obstacles) || (p->use_obstacles && ev->obst_mode >= 2)) {
         or_sdraw sd;
         memset(&sd, 0, sizeof sd);
         sd.mode = OR_RNG_PHILOX; sd.seed = r->seed; sd.key = gbase; sd.stream = OR_S_SCN; sd.step = r->step;
         double g[OR_MAXN][3];
         for (int i = 0; i < N; ++i) memcpy(g[i], dr[i].goal, sizeof g[i]);
-        or_scen_step(p, &ev->scen, ev->tick, &sd, g);
+        if (p->use_obstacles) {   /* the map back from the pillar centres (or_cell_xy's inverse) */
+            const int n = p->obst_area;
+            const double h = (double)(n / 2);
+            unsigned char map[64 * 64];
+            memset(map, 0, sizeof map);
+            for (int o = 0; o < ev->n_obst; ++o) {
+                const int col = (int)lround(ev->obst[o][0] - 0.5 + h), row = n - 1 - (int)lround(ev->obst[o][1] - 0.5 + h);
+                map[row * n + col] = 1;
+            }
+            or_oscen_step(p, &ev->scen, ev->tick, &sd, map, n, g);
+        } else {
+            or_scen_step(p, &ev->scen, ev->tick, &sd, g);
+        }
         for (int i = 0; i < N; ++i) memcpy(dr[i].goal, g[i], sizeof g[i]);
     }
     /* 5. refresh and observations (:704-716) */

@@ -143,7 +143,8 @@ typedef struct {
     int use_obstacles;
     int num_obstacles;         /* int(density * area_l * area_w)                          */
     int obst_area;             /* spawn area side (8), 1 m grid cells                     */
-    int obst_scenario;         /* 0 = mix (o_random / o_static_same_goal), 1 = o_random, 2 = o_static_same_goal */
+    int obst_scenario;         /* 0 = mix (o_random / o_static_same_goal), 1 = o_random, 2 = o_static_same_goal,
+                                  3 = o_swap_goals, 4 = o_ep_rand_bezier, 5 = o_dynamic_same_goal (obstacle mode + 1) */
     double obst_size;          /* diameter (0.6); radius = size / 2                        */
     double obst_z;             /* pillar centre z = room height / 2 (only the 3-D inside test) */
     double sdf_resolution;     /* 0.1                                                      */
@@ -164,7 +165,9 @@ typedef struct {
  * reset (scenarios/mix.py) */
 enum { OR_SC_NONE = -1, OR_SC_STATIC_SAME_GOAL = 0, OR_SC_STATIC_DIFF_GOAL, OR_SC_EP_LISSAJOUS3D,
        OR_SC_EP_RAND_BEZIER, OR_SC_DYNAMIC_SAME_GOAL, OR_SC_DYNAMIC_DIFF_GOAL, OR_SC_DYNAMIC_FORMATIONS,
-       OR_SC_SWAP_GOALS, OR_SC_SWARM_VS_SWARM, OR_SC_RUN_AWAY, OR_SC_MIX };
+       OR_SC_SWAP_GOALS, OR_SC_SWARM_VS_SWARM, OR_SC_RUN_AWAY, OR_SC_MIX,
+       /* the obstacle maps' dynamic scenarios (scenarios/obstacles/, QUADS_MODE_LIST_OBSTACLES_TEST) */
+       OR_SC_O_SWAP_GOALS, OR_SC_O_EP_RAND_BEZIER, OR_SC_O_DYNAMIC_SAME_GOAL };
 
 /* per-env scenario state (the attributes of the reference's Scenario_* object) */
 typedef struct {
@@ -233,7 +236,8 @@ typedef struct {
     /* obstacles */
     int n_obst;
     double obst[64][2];                      /* MultiObstacles.pos_arr xy, in generation order   */
-    int obst_mode;                           /* 0 o_random, 1 o_static_same_goal                 */
+    int obst_mode;                           /* 0 o_random, 1 o_static_same_goal, 2 o_swap_goals, 3 o_ep_rand_bezier,
+                                                4 o_dynamic_same_goal (2..4 keep their state in scen) */
     or_scen scen;                            /* flavor-B goal scenario (p->scenario_b != OR_SC_NONE) */
     /* what the experience-replay wrapper reads of the last step (quad_experience_replay.py:161-163,
      * quadrotor_multi.py:725): a new drone collision (.any() of the ids) or obstacle hit; drone 0 on the floor */
@@ -308,6 +312,14 @@ int or_generate_goals(int formation, int n, int per_layer, double size, double l
                       double (*g)[3]);
 void or_scen_reset(const or_params* p, or_scen* sc, or_sdraw* s, double (*goals)[3]);
 void or_scen_step(const or_params* p, or_scen* sc, int tick, or_sdraw* s, double (*goals)[3]);
+/* the obstacle maps' dynamic scenarios (quadswarm_oracle_scen.c): omode 2 o_swap_goals, 3 o_ep_rand_bezier,
+ * 4 o_dynamic_same_goal; map = the n x n occupancy (row-major).  Tape mode reads the reference's whole reset draw
+ * sequence (spawn cells and heights included: sp_cells / sp_z out); Philox mode draws only the scenario's words
+ * (S_SCN_RESET order of csrc/qs_flavor_b.h obstacle_reset_env) and leaves the spawns to the caller. */
+void or_oscen_reset(const or_params* p, int omode, or_scen* sc, or_sdraw* s, const unsigned char* map, int n,
+                    int* sp_cells, double* sp_z, double (*goals)[3]);
+void or_oscen_step(const or_params* p, or_scen* sc, int tick, or_sdraw* s, const unsigned char* map, int n,
+                   double (*goals)[3]);
 
 /* ---- flavor A (quadrotor_multi_rewards.QuadrotorEnvMulti) ---- */
 void or_params_default_a(or_params* p);     /* Controller/ModelParams constants, camera, rewards */

@@ -77,6 +77,8 @@ static void mode_params(int mode, int* nform, double* low, double* high) {
         case OR_SC_STATIC_DIFF_GOAL: case OR_SC_DYNAMIC_DIFF_GOAL: case OR_SC_SWARM_VS_SWARM: case OR_SC_RUN_AWAY:
             *nform = 8; *low = 5 * arm; *high = 10 * arm; return;
         case OR_SC_SWAP_GOALS: *nform = 8; *low = 8 * arm; *high = 16 * arm; return;
+        /* QUADS_FORMATION_LIST_OBSTACLES (7 entries) indexes QUADS_FORMATION_LIST (update_formation_and_max_agent_per_layer) */
+        case OR_SC_O_SWAP_GOALS: *nform = 7; *low = 8 * arm; *high = 16 * arm; return;
         case OR_SC_DYNAMIC_FORMATIONS: *nform = 8; *low = 0.0; *high = 20 * arm; return;
         default: *nform = 1; *low = 0.0; *high = 0.0; return;   /* ['circle_horizontal'], [0, 0] */
     }
@@ -352,7 +354,8 @@ void or_scen_step(const or_params* p, or_scen* sc, int tick, or_sdraw* s, double
                      * drawn with the bounds of column (2c + j) % 3; node j = column j */
                     double u[6];
                     for (int k = 0; k < 6; ++k) u[k] = or_sd_uniform(s, -hi[k % 3], hi[k % 3]);
-                    const double mag = (double)or_sd_int(s, (int)ceil(min_dist), (int)floor(max_dist) + 1);
+                    /* np.random.randint(min_dist, max_dist + 1): numpy truncates float bounds */
+                    const double mag = (double)or_sd_int(s, (int)min_dist, (int)floor(max_dist) + 1);
                     int ok = 1;
                     for (int j = 0; j < 2; ++j) {
                         const double v[3] = {u[j], u[2 + j], u[4 + j]};
@@ -399,5 +402,165 @@ void or_scen_step(const or_params* p, or_scen* sc, int tick, or_sdraw* s, double
             return;
         default:
             return;   /* static_same_goal, static_diff_goal */
+    }
+}
+
+/* ---------------------------------------------------------------------------------------------- */
+/* the obstacle maps' dynamic scenarios (scenarios/obstacles/o_swap_goals.py, o_ep_rand_bezier.py,   */
+/* o_dynamic_same_goal.py; o_base.py).  free_space = np.where(map == 0): cells in row-major order;  */
+/* cell (x, y) of free_space -> cell_centers[x + n y] (or_cell_xy(x, y)).                          */
+/* ---------------------------------------------------------------------------------------------- */
+static int free_cells(const unsigned char* map, int n, int* fr) {
+    int F = 0;
+    for (int c = 0; c < n * n; ++c) if (!map[c]) fr[F++] = c;
+    return F;
+}
+/* Scenario_o_base.max_square_area_center's cell centre (o_base.py:125-153), z drawn by the caller */
+static void max_square_xy(const unsigned char* map, int n, double xy[2]) { or_max_square_center(map, n, xy); }
+
+/* generate_pos_obst_map_2 (o_base.py:74-88): np.random.choice(range(F), N, replace=False), then one
+ * np.random.uniform(1, 3) per drone (tape mode only) */
+static void tape_spawns(or_sdraw* s, int N, int* sp_cells, double* sp_z, const int* fr) {
+    for (int i = 0; i < N; ++i) sp_cells[i] = fr[(int)or_sd_uniform(s, 0, 0)];
+    for (int i = 0; i < N; ++i) sp_z[i] = or_sd_uniform(s, 1.0, 3.0);
+}
+
+void or_oscen_reset(const or_params* p, int omode, or_scen* sc, or_sdraw* s, const unsigned char* map, int n,
+                    int* sp_cells, double* sp_z, double (*g)[3]) {
+    const int N = p->num_agents, tape = s->mode == OR_RNG_TAPE;
+    const double cf = 1.0 / p->control_dt;
+    int fr[64 * 64];
+    const int F = free_cells(map, n, fr);
+    memset(sc, 0, sizeof *sc);
+    sc->mode = omode == 2 ? OR_SC_O_SWAP_GOALS : (omode == 3 ? OR_SC_O_EP_RAND_BEZIER : OR_SC_O_DYNAMIC_SAME_GOAL);
+    double xy[2];
+    if (omode == 3) {                                      /* o_ep_rand_bezier.py:55-103 */
+        sc->period = (int)(0.01 * cf);
+        if (tape) tape_spawns(s, N, sp_cells, sp_z, fr);
+        /* end_point = generate_pos_obst_map() (o_base.py:58-72) */
+        const int c = fr[tape ? (int)or_sd_uniform(s, 0, 0) : or_sd_int(s, 0, F)];
+        or_cell_xy(c / n, c % n, n, xy);
+        sc->center[0] = xy[0]; sc->center[1] = xy[1]; sc->center[2] = or_sd_uniform(s, 0.75, 3.0);
+        if (tape) {   /* the 10 trajectory points it samples and never uses (:79-96): replay their draws */
+            int pts[10], np_ = 0, Fc = F;
+            double cc[64][2];
+            for (int i = 0; i < n * n; ++i) or_cell_xy(i % n, i / n, n, cc[i]);   /* cell_centers[i] */
+            while (np_ < 10 && !s->overrun) {
+                const int idx = (int)or_sd_uniform(s, 0, 0);   /* np.random.choice(len(free_space)) */
+                int far = 0;
+                for (int k = 0; k < np_; ++k) {
+                    const double dx = cc[pts[k]][0] - cc[idx][0], dy = cc[pts[k]][1] - cc[idx][1];
+                    if (sqrt(dx * dx + dy * dy) > 4.0) far = 1;
+                }
+                if (far) continue;
+                pts[np_++] = idx;
+                --Fc;
+            }
+            (void)Fc;
+            update_formation(p, sc, s);                    /* circle_horizontal, size 0 */
+        }
+        for (int i = 0; i < N; ++i) memcpy(g[i], sc->center, sizeof sc->center);
+        return;
+    }
+    sc->period = (int)(or_sd_uniform(s, 4.0, 6.0) * cf);  /* duration_time ~ U(4, 6) */
+    if (omode == 2) {                                      /* o_swap_goals.py:27-52 */
+        update_formation(p, sc, s);
+        if (tape) tape_spawns(s, N, sp_cells, sp_z, fr);
+        max_square_xy(map, n, xy);
+        sc->center[0] = xy[0]; sc->center[1] = xy[1]; sc->center[2] = or_sd_uniform(s, 1.5, 3.0);
+        double tmp[OR_MAXN][3];
+        const int m = or_generate_goals(sc->formation, N, sc->per_layer, sc->size, sc->layer, sc->center, tmp);
+        or_sd_shuffle(s, tmp, m);                          /* np.random.shuffle(self.goals) */
+        memcpy(g, tmp, sizeof(double) * 3 * (size_t)N);
+        /* a sphere of N < 3 drones has 3 goals: the scenario keeps the rows no drone takes (they are shuffled
+         * back in at the next swap) -- in c1 / c2 */
+        if (m > N) memcpy(sc->c1, tmp[N], sizeof sc->c1);
+        if (m > N + 1) memcpy(sc->c2, tmp[N + 1], sizeof sc->c2);
+        return;
+    }
+    /* o_dynamic_same_goal.py:31-51 */
+    if (tape) tape_spawns(s, N, sp_cells, sp_z, fr);
+    max_square_xy(map, n, xy);
+    sc->center[0] = xy[0]; sc->center[1] = xy[1]; sc->center[2] = or_sd_uniform(s, 1.5, 3.0);
+    if (tape) update_formation(p, sc, s);                  /* circle_horizontal, size 0 */
+    for (int i = 0; i < N; ++i) memcpy(g[i], sc->center, sizeof sc->center);
+}
+
+void or_oscen_step(const or_params* p, or_scen* sc, int tick, or_sdraw* s, const unsigned char* map, int n,
+                   double (*g)[3]) {
+    const int N = p->num_agents, tape = s->mode == OR_RNG_TAPE;
+    const double cf = 1.0 / p->control_dt;
+    int fr[64 * 64];
+    const int F = free_cells(map, n, fr);
+    switch (sc->mode) {
+        case OR_SC_O_SWAP_GOALS:                           /* o_swap_goals.py:14-24 */
+            if (tick % sc->period == 0 && tick > 0) {      /* np.random.shuffle(self.goals): all of its rows */
+                const int m = (sc->formation == 3 && N < 3) ? 3 : N;   /* F_SPHERE: generate_points makes >= 3 */
+                double t[OR_MAXN + 2][3];
+                memcpy(t, g, sizeof(double) * 3 * (size_t)N);
+                if (m > N) memcpy(t[N], sc->c1, sizeof sc->c1);
+                if (m > N + 1) memcpy(t[N + 1], sc->c2, sizeof sc->c2);
+                or_sd_shuffle(s, t, m);
+                memcpy(g, t, sizeof(double) * 3 * (size_t)N);
+                if (m > N) memcpy(sc->c1, t[N], sizeof sc->c1);
+                if (m > N + 1) memcpy(sc->c2, t[N + 1], sizeof sc->c2);
+            }
+            return;
+        case OR_SC_O_DYNAMIC_SAME_GOAL:                    /* o_dynamic_same_goal.py:17-29 */
+            if (tick % sc->period == 0 || tick == 1) {
+                double ng[3];
+                for (int tries = 0;; ++tries) {            /* generate_pos_obst_map() until within max_dist = 4 */
+                    const int c = fr[tape ? (int)or_sd_uniform(s, 0, 0) : or_sd_int(s, 0, F)];
+                    double xy[2];
+                    or_cell_xy(c / n, c % n, n, xy);
+                    ng[0] = xy[0]; ng[1] = xy[1]; ng[2] = or_sd_uniform(s, 0.75, 3.0);
+                    const double d[3] = {sc->center[0] - ng[0], sc->center[1] - ng[1], sc->center[2] - ng[2]};
+                    if (!(sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]) > 4.0) || tries >= 4095 || s->overrun) break;
+                }
+                memcpy(sc->center, ng, sizeof ng);
+                for (int i = 0; i < N; ++i) memcpy(g[i], ng, sizeof ng);
+            }
+            return;
+        case OR_SC_O_EP_RAND_BEZIER: {                     /* o_ep_rand_bezier.py:14-53 */
+            const int steps = (int)(6 * cf);
+            const int t = tick % steps;
+            const double rd[3] = {p->room_hi[0] - p->room_lo[0] - sc->size, p->room_hi[1] - p->room_lo[1] - sc->size,
+                                  p->room_hi[2] - p->room_lo[2] - sc->size};
+            double mx = rd[0] > rd[1] ? rd[0] : rd[1];
+            mx = mx > rd[2] ? mx : rd[2];
+            const double max_dist = mx < 5 ? mx : 5, min_dist = max_dist / 2;
+            if (t == 0 || tick == 1) {
+                const double lo[3] = {-rd[0] / 2, -rd[1] / 2, 1.5}, hi[3] = {rd[0] / 2, rd[1] / 2, 3.0};
+                double np_[3][2];
+                for (int tries = 0;; ++tries) {
+                    double u[6];
+                    for (int k = 0; k < 6; ++k) u[k] = or_sd_uniform(s, -hi[k % 3], hi[k % 3]);
+                    const double mag = (double)or_sd_int(s, (int)min_dist, (int)floor(max_dist) + 1);
+                    int ok = 1;
+                    for (int j = 0; j < 2; ++j) {
+                        const double v[3] = {u[j], u[2 + j], u[4 + j]};
+                        const double nrm = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+                        for (int q = 0; q < 3; ++q) {
+                            np_[q][j] = v[q] * mag / nrm + g[0][q];
+                            if (!(np_[q][j] > lo[q] + 0.5 && np_[q][j] < hi[q] - 0.5)) ok = 0;
+                        }
+                    }
+                    if (ok || tries >= 8191 || s->overrun) break;   /* the reference loops without a bound */
+                }
+                for (int q = 0; q < 3; ++q) {
+                    sc->bz[0][q] = g[0][q];
+                    sc->bz[1][q] = np_[q][0];
+                    sc->bz[2][q] = np_[q][1];
+                }
+            }
+            if (t != 0 && tick > 1) {
+                double pt[3];
+                bezier2((const double(*)[3])sc->bz, t == steps - 1 ? 1.0 : t * (1.0 / (steps - 1)), pt);
+                for (int i = 0; i < N; ++i) memcpy(g[i], pt, sizeof pt);
+            }
+            return;
+        }
+        default:
+            return;
     }
 }

@@ -387,12 +387,7 @@ __device__ __forceinline__ void reset_drone(const KP& kp, Drone& d, const Rng& r
 // ---------------------------------------------------------------------------------------------
 // obstacles: pillars on an n x n grid of 1 m cells, xy only
 // ---------------------------------------------------------------------------------------------
-// grid cell (row, col) -> cell_centers[row + n*col] (obstacles/utils.py:46-58, quadrotor_multi.py:422)
-__device__ __forceinline__ float2 cell_xy(int cell, int n) {
-    const int row = cell / n, col = cell % n;
-    const float h = (float)(n / 2);
-    return make_float2((float)col + 0.5f - h, (float)(n - 1 - row) + 0.5f - h);
-}
+// (cell_xy: grid cell -> cell centre, qs_scen.h)
 
 
 // partial Fisher-Yates (the first k of a random permutation of 0..n-1): the Philox stand-in for
@@ -414,9 +409,12 @@ constexpr int QS_OBST_SCRATCH = 400;
 struct ObstScratch {
     uint8_t perm[64], map[64], fr[64], dp[64], sp[32], gl[32], ids[64];
     float ez;
-    int mode;
+    int mode;     // 0 o_random, 1 o_static_same_goal, 2 o_swap_goals, 3 o_ep_rand_bezier, 4 o_dynamic_same_goal
     int mi, si;   // domain randomisation: the env's pillar count / size table indices (in: current, out: new)
 };
+// the episode_extra_stats scenario id of an obstacle mode (quadswarm_amd.stats: 16 o_random, 17 o_static_same_goal,
+// 19 o_swap_goals, 20 o_ep_rand_bezier, 21 o_dynamic_same_goal; 18 is flavor A's dynamic_repulsive)
+__device__ __forceinline__ int obst_stats_id(int mode) { return mode < 2 ? 16 + mode : 17 + mode; }
 
 // The env's pillar geometry: count, radius, collision threshold (arm + radius).  Without domain
 // randomisation these are the (specialised) constants; with it, the env's table entries.
@@ -430,10 +428,36 @@ __device__ __forceinline__ OGeo ogeo(const KP& kp, int mi, int si) {
 }
 static_assert(sizeof(ObstScratch) <= QS_OBST_SCRATCH, "obstacle scratch");
 
+// the max_square_area_center cell of the env's map (Scenario_o_base, o_base.py:125-153): dp's first row and column
+// start as the map itself, the centre is (i - (s-1)//2, j - (s-1)//2)
+__device__ __forceinline__ int obst_max_square_cell(ObstScratch* sc, int n) {
+    const int nn = n * n;
+    for (int c = 0; c < nn; ++c) sc->dp[c] = 0;
+    for (int j = 0; j < n; ++j) sc->dp[j] = sc->map[j];
+    for (int i = 0; i < n; ++i) sc->dp[i * n] = sc->map[i * n];
+    int ms = 0, cx = 0, cy = 0;
+    for (int i = 1; i < n; ++i)
+        for (int j = 1; j < n; ++j)
+            if (sc->map[i * n + j] == 0) {
+                const int v = min(min(sc->dp[(i - 1) * n + j], sc->dp[i * n + j - 1]), sc->dp[(i - 1) * n + j - 1]) + 1;
+                sc->dp[i * n + j] = (uint8_t)v;
+                if (v > ms) { ms = v; cx = i - (ms - 1) / 2; cy = j - (ms - 1) / 2; }
+            }
+    return cx * n + cy;
+}
+
 // Obstacle map + scenario of one env (quadrotor_multi.py:405-426, 449-452; scenarios/mix.py:78-99;
-// o_random.py:26-51; o_static_same_goal.py:28-48; o_base.py:58-153).  One lane per env runs it;
-// the other lanes of the env read sp/gl/mode/ez after a barrier.  Writes the env's obstacle list.
-__device__ __forceinline__ void obstacle_reset_env(const KP& kp, const Rng& r, uint32_t genv, ObstScratch* sc, float2* ob) {
+// o_random.py:26-51; o_static_same_goal.py:28-48; o_base.py:58-153; the dynamic modes o_swap_goals.py:27-52,
+// o_ep_rand_bezier.py:55-103, o_dynamic_same_goal.py:31-51).  One lane per env runs it; the other lanes of the env
+// read sp/gl/mode/ez (and, dynamic modes, their goal rows in gtab) after a barrier.  Writes the env's obstacle list;
+// for the dynamic modes also `so`, the scenario record (stored by the caller) -- the draws of their scenario
+// parameters are one Philox word each on stream S_SCN_RESET (key: the env's drone 0), in this order:
+//   o_swap_goals          duration U(4, 6), formation, size, layer dist, end z U(1.5, 3), the goals' shuffle
+//   o_ep_rand_bezier      end cell (choice of the free cells), end z U(0.75, 3)
+//   o_dynamic_same_goal   duration U(4, 6), end z U(1.5, 3)
+// (the reference's o_ep_rand_bezier also samples 10 trajectory points it never uses: not drawn here).
+__device__ __forceinline__ void obstacle_reset_env(const KP& kp, const Rng& r, uint32_t genv, ObstScratch* sc, float2* ob,
+                                                   Scen* so = nullptr, float* gtab = nullptr) {
     if (kp.dr) {   // the replay wrapper's reset: np.random.choice of density, then of size (quad_experience_replay.py:106-118)
         if (kp.dr_nm > 0) {
             const int c = ufloor(ubits(r, genv, S_DR, 0), kp.dr_nm);
@@ -460,31 +484,61 @@ __device__ __forceinline__ void obstacle_reset_env(const KP& kp, const Rng& r, u
     if (mode == 0) {   // o_random: own goal cell per drone
         choose_k(r, genv, S_OSCEN, 1 + (uint32_t)N, F, N, sc->perm, sc->gl);
         for (int i = 0; i < N; ++i) sc->gl[i] = sc->fr[sc->gl[i]];
-    } else {           // o_static_same_goal: Scenario_o_base.max_square_area_center (o_base.py:125-153)
-        for (int c = 0; c < nn; ++c) sc->dp[c] = 0;
-        for (int j = 0; j < n; ++j) sc->dp[j] = sc->map[j];
-        for (int i = 0; i < n; ++i) sc->dp[i * n] = sc->map[i * n];
-        int ms = 0, cx = 0, cy = 0;
-        for (int i = 1; i < n; ++i)
-            for (int j = 1; j < n; ++j)
-                if (sc->map[i * n + j] == 0) {
-                    const int v = min(min(sc->dp[(i - 1) * n + j], sc->dp[i * n + j - 1]), sc->dp[(i - 1) * n + j - 1]) + 1;
-                    sc->dp[i * n + j] = (uint8_t)v;
-                    if (v > ms) { ms = v; cx = i - (ms - 1) / 2; cy = j - (ms - 1) / 2; }
-                }
-        for (int i = 0; i < N; ++i) sc->gl[i] = (uint8_t)(cx * n + cy);
+    } else if (mode == 1) {   // o_static_same_goal: Scenario_o_base.max_square_area_center (o_base.py:125-153)
+        const int cell = obst_max_square_cell(sc, n);
+        for (int i = 0; i < N; ++i) sc->gl[i] = (uint8_t)cell;
         sc->ez = 1.5f + 1.5f * uniform1(r, genv, S_OSCEN, 2 * (uint32_t)N + 1);
+    } else if (so != nullptr && gtab != nullptr) {   // the dynamic modes: goals into gtab rows, the record into so
+        Scen& s = *so;
+        s = Scen{};
+        s.mode = obst_stats_id(mode);
+        SDraw sd = sdraw(r, genv, S_SCN_RESET);
+        const float cf = 1.f / kp.cdt;
+        if (mode == 3) {   // o_ep_rand_bezier: end point = generate_pos_obst_map(); the curve is sampled at tick 1
+            const float2 xy = cell_xy(sc->fr[sd_int(sd, 0, F)], n);
+            s.c[0] = xy.x; s.c[1] = xy.y; s.c[2] = sd_uniform(sd, 0.75f, 3.f);
+            s.period = (int)(0.01f * cf);
+            for (int i = 0; i < N; ++i)
+                for (int k = 0; k < 3; ++k) gtab[4 * i + k] = s.c[k];
+        } else {
+            s.period = (int)(sd_uniform(sd, 4.f, 6.f) * cf);   // duration_time ~ U(4, 6)
+            if (mode == 2) {   // o_swap_goals: a formation (update_formation_and_relate_param) around the centre
+                Scen f{};
+                f.mode = SC_O_SWAP_GOALS;
+                sc_update_formation(kp, f, sd);
+                s.form = f.form; s.lo = f.lo; s.hi = f.hi; s.size = f.size; s.layer = f.layer;
+            }
+            const float2 xy = cell_xy(obst_max_square_cell(sc, n), n);   // max_square_area_center()
+            s.c[0] = xy.x; s.c[1] = xy.y; s.c[2] = sd_uniform(sd, 1.5f, 3.f);
+            if (mode == 2) {   // generate_goals(num_agents, formation_center, layer_dist), np.random.shuffle(goals)
+                const int m = sc_generate(s.form, sc_num(kp), sc_per_layer(s.form), s.size, s.layer, s.c, gtab);
+                sd_shuffle(sd, gtab, m);
+                // a sphere of N < 3 drones has 3 goal rows: the scenario keeps the ones no drone takes in c1 / c2
+                for (int k = 0; k < 3; ++k) {
+                    if (m > N) s.c1[k] = gtab[4 * N + k];
+                    if (m > N + 1) s.c2[k] = gtab[4 * (N + 1) + k];
+                }
+            } else {           // o_dynamic_same_goal: every drone's goal is the end point
+                for (int i = 0; i < N; ++i)
+                    for (int k = 0; k < 3; ++k) gtab[4 * i + k] = s.c[k];
+            }
+        }
     }
     sc->mode = mode;
 }
 
-// spawn point and goal of drone `di` after obstacle_reset_env (o_base.py:81-92: z ~ U(1, 3))
+// spawn point and goal of drone `di` after obstacle_reset_env (o_base.py:81-92: z ~ U(1, 3)); the dynamic modes'
+// goals are gtab's rows
 __device__ __forceinline__ void obstacle_spawn_goal(const KP& kp, const ObstScratch* sc, int di, const Rng& r,
-                                                    uint32_t gid, float* spawn, float* goal) {
+                                                    uint32_t gid, float* spawn, float* goal, const float* gtab = nullptr) {
     float u[4];
     uniforms4(r, gid, S_RESET, 0, u);   // u[3] = start z, block 1 word 0 = goal z
     const float2 s = cell_xy(sc->sp[di], kp.obst_n), g = cell_xy(sc->gl[di], kp.obst_n);
     spawn[0] = s.x; spawn[1] = s.y; spawn[2] = 1.f + 2.f * u[3];
+    if (sc->mode >= 2 && gtab != nullptr) {
+        for (int k = 0; k < 3; ++k) goal[k] = gtab[4 * di + k];
+        return;
+    }
     goal[0] = g.x; goal[1] = g.y;
     goal[2] = sc->mode == 0 ? 1.f + 2.f * uniform1(r, gid, S_RESET, 4) : sc->ez;
 }
@@ -598,6 +652,11 @@ __device__ __forceinline__ void collide_obstacle(const KP& kp, const OGeo& og, D
 // (qs_lds_bytes() in qs_step.hip sizes it)
 __device__ __forceinline__ float2* obst_tile(float* lds, const KP& kp, int slots) {
     return reinterpret_cast<float2*>(lds + slots * kp.obs_dim + slots * 8 + 64);
+}
+// the goal-scenario tables (qs_scen.h scen_tab): after the obstacle tiles and reset scratch in obstacle kernels
+template <bool OBST>
+__device__ __forceinline__ float* scen_tab_b(float* lds, const KP& kp, int slots, int epb) {
+    return scen_tab(lds, kp, slots) + (OBST ? epb * (2 * kp.M + QS_OBST_SCRATCH / 4) : 0);
 }
 
 // Geometry of the flavor-B step kernel: Q lanes per drone (Q * NPAD <= 64), EPB envs per wave.
@@ -968,7 +1027,10 @@ __global__ __launch_bounds__(StepGeo<NPAD>::WGS) void step_kernel(const KP* __re
     // goal scenario: the env's scenario record (SC_WORDS words) dealt over its lanes -- word li + LPE t on lane li
     // -- loaded with the step's other loads and staged in LDS for scenario.step() after the forces
     const bool SCEN = !OBST && kp.scen_b >= 0;
-    const bool SCEN_STEP = SCEN && kp.scen_b != SC_STATIC_DIFF_GOAL;   // static_diff_goal's step() does nothing
+    // the obstacle maps' dynamic scenarios (o_swap_goals, o_ep_rand_bezier, o_dynamic_same_goal): reset with the map
+    // (obstacle_reset_env), stepped like the goal scenarios
+    const bool OSCEN = OBST && kp.scen_b >= SC_O_SWAP_GOALS;
+    const bool SCEN_STEP = (SCEN && kp.scen_b != SC_STATIC_DIFF_GOAL) || OSCEN;   // static_diff_goal's step() does nothing
     constexpr int SRW = (SC_WORDS + LPE - 1) / LPE;
     uint32_t scw[SRW];
     auto load_scw = [&]() {
@@ -1398,7 +1460,7 @@ __global__ __launch_bounds__(StepGeo<NPAD>::WGS) void step_kernel(const KP* __re
     // every lane, the drone's own goal row); envs whose scenario does nothing at this tick skip it, and the
     // scenario record is stored only where it changed.
     float obs_goal[3] = {d.goal[0], d.goal[1], d.goal[2]};
-    float* stab = scen_tab(lds, kp, SLOTS) + el * scen_stride<NPAD>();
+    float* stab = scen_tab_b<OBST>(lds, kp, SLOTS, EPB) + el * scen_stride<NPAD>();
     QS_STAMP(18);   // sub-phases of "impulses+scenario+state store" (slots 18-21)
     if (SCEN_STEP) {
         uint32_t* srec = reinterpret_cast<uint32_t*>(stab + 2 * (NPAD + 4) * 4);
@@ -1415,11 +1477,13 @@ __global__ __launch_bounds__(StepGeo<NPAD>::WGS) void step_kernel(const KP* __re
             bool via = false;
             int bz0 = 0;   // ep_rand_bezier: the first accepted try of its rejection loop, searched by the env's lanes
             if constexpr (!WIDE)
-                if (kp.scen_b == SC_MIX || kp.scen_b == SC_EP_RAND_BEZIER) {
-                    const int steps = (int)(5.f * (1.f / kp.cdt));   // scen_step_lane's period
+                if (kp.scen_b == SC_MIX || kp.scen_b == SC_EP_RAND_BEZIER || kp.scen_b == SC_O_EP_RAND_BEZIER) {
+                    // scen_step_lane's period
+                    const int steps = (int)((kp.scen_b == SC_O_EP_RAND_BEZIER ? 6.f : 5.f) * (1.f / kp.cdt));
                     // the env's active lanes (li < N Q) search; the padding lanes of an env with N < NPAD hold env
                     // 0's tick / Philox counter and idle
-                    const bool bneed = active && sc_mode(kp, (int)srec[0]) == SC_EP_RAND_BEZIER &&
+                    const int bm = sc_mode(kp, (int)srec[0]);
+                    const bool bneed = active && (bm == SC_EP_RAND_BEZIER || bm == SC_O_EP_RAND_BEZIER) &&
                                        (tick % steps == 0 || tick == 1);
                     if (ec.wany(bneed))
                         bz0 = bz_first_parallel<LPE>(kp, srec, bneed, li, lbase, kp.N * Q, rng,
@@ -1429,7 +1493,9 @@ __global__ __launch_bounds__(StepGeo<NPAD>::WGS) void step_kernel(const KP* __re
                 Scen sc;
                 scen_from_words(srec, sc);
                 SDraw sd = sdraw(rng, kp.id0 + (uint32_t)(env * kp.N), S_SCN);
-                const int ch = scen_step_lane(kp, sc, tick, sd, di, stab, stab + 4 * (NPAD + 4), d.goal, via, bz0);
+                const OCtx oc{myob, og.m, kp.obst_n};
+                const int ch = scen_step_lane(kp, sc, tick, sd, di, stab, stab + 4 * (NPAD + 4), d.goal, via, bz0,
+                                              OBST ? &oc : nullptr);
                 if (di == 0 && q == 0) {
                     if (ch == 2) scen_store(kp, b, env, sc);
                     else if (ch == 1) scen_store_size(kp, b, env, sc);
@@ -1557,12 +1623,15 @@ __global__ __launch_bounds__(StepGeo<NPAD>::WGS) void step_kernel(const KP* __re
             if (active && done && di == 0 && q == 0) {
                 oscr[el].mi = omi;
                 oscr[el].si = osi;
-                obstacle_reset_env(kp, rng, kp.id0 + (uint32_t)(env * kp.N), oscr + el, otile + el * kp.M);
+                Scen so;
+                obstacle_reset_env(kp, rng, kp.id0 + (uint32_t)(env * kp.N), oscr + el, otile + el * kp.M,
+                                   OSCEN ? &so : nullptr, OSCEN ? stab : nullptr);
                 if (kp.dr) {
                     b.env[QS_E_OBST_M * kp.E + env] = oscr[el].mi;
                     b.env[QS_E_OBST_SZ * kp.E + env] = oscr[el].si;
                 }
-                if (kp.stats) b.env[QS_E_SC_MODE * kp.E + env] = 16 + oscr[el].mode;   // the stats' scenario name
+                if (OSCEN) scen_store(kp, b, env, so);   // its mode word is the stats' scenario id
+                else if (kp.stats) b.env[QS_E_SC_MODE * kp.E + env] = obst_stats_id(oscr[el].mode);   // the stats' name
             }
             lds_sync();
             if (active && done && kp.dr) og = ogeo(kp, oscr[el].mi, oscr[el].si);
@@ -1583,7 +1652,7 @@ __global__ __launch_bounds__(StepGeo<NPAD>::WGS) void step_kernel(const KP* __re
                 b.stale[2 * kp.I + g] = sv[2];
             }
             float spawn[3] = {kp.goal[0], kp.goal[1], kp.goal[2]}, goal[3] = {kp.goal[0], kp.goal[1], kp.goal[2]};
-            if (OBST) obstacle_spawn_goal(kp, oscr + el, di, rng, gid, spawn, goal);
+            if (OBST) obstacle_spawn_goal(kp, oscr + el, di, rng, gid, spawn, goal, OSCEN ? stab : nullptr);
             if (SCEN)   // spawn point = goal (quadrotor_multi.py:469-470)
                 for (int k = 0; k < 3; ++k) spawn[k] = goal[k] = stab[4 * di + k];
             reset_drone(kp, d, rng, gid, spawn, goal);
@@ -1689,20 +1758,24 @@ __global__ __launch_bounds__(NPAD > 64 ? NPAD : 64) void reset_kernel(const KP* 
     for (int c = 0; c < 3; ++c) sv[c] = stale_valid ? b.stale[c * kp.I + g] : d.vel[c];
     float2* otile = obst_tile(lds, kp, SLOTS);
     ObstScratch* oscr = reinterpret_cast<ObstScratch*>(otile + EPB * kp.M);
+    float* stab = scen_tab_b<OBST>(lds, kp, SLOTS, EPB) + el * scen_stride<NPAD>();
+    const bool OSCEN = OBST && kp.scen_b >= SC_O_SWAP_GOALS;
     if (OBST) {
         if (sel && di == 0) {
             oscr[el].mi = kp.dr ? b.env[QS_E_OBST_M * kp.E + env] : 0;
             oscr[el].si = kp.dr ? b.env[QS_E_OBST_SZ * kp.E + env] : 0;
-            obstacle_reset_env(kp, rng, kp.id0 + (uint32_t)(env * kp.N), oscr + el, otile + el * kp.M);
+            Scen so;
+            obstacle_reset_env(kp, rng, kp.id0 + (uint32_t)(env * kp.N), oscr + el, otile + el * kp.M,
+                               OSCEN ? &so : nullptr, OSCEN ? stab : nullptr);
             if (kp.dr) {
                 b.env[QS_E_OBST_M * kp.E + env] = oscr[el].mi;
                 b.env[QS_E_OBST_SZ * kp.E + env] = oscr[el].si;
             }
-            if (kp.stats) b.env[QS_E_SC_MODE * kp.E + env] = 16 + oscr[el].mode;
+            if (OSCEN) scen_store(kp, b, env, so);
+            else if (kp.stats) b.env[QS_E_SC_MODE * kp.E + env] = obst_stats_id(oscr[el].mode);
         }
         lds_sync();
     }
-    float* stab = scen_tab(lds, kp, SLOTS) + el * scen_stride<NPAD>();
     const bool SCEN = !OBST && kp.scen_b >= 0;
     if (SCEN) {   // scenario.reset() (quadrotor_multi.py:449-459) by each selected env's lead lane
         if (sel && di == 0) {
@@ -1715,7 +1788,7 @@ __global__ __launch_bounds__(NPAD > 64 ? NPAD : 64) void reset_kernel(const KP* 
     }
     if (sel) {
         float spawn[3] = {kp.goal[0], kp.goal[1], kp.goal[2]}, goal[3] = {kp.goal[0], kp.goal[1], kp.goal[2]};
-        if (OBST) obstacle_spawn_goal(kp, oscr + el, di, rng, kp.id0 + (uint32_t)g, spawn, goal);
+        if (OBST) obstacle_spawn_goal(kp, oscr + el, di, rng, kp.id0 + (uint32_t)g, spawn, goal, OSCEN ? stab : nullptr);
         if (SCEN)   // spawn point = goal (quadrotor_multi.py:469-470)
             for (int k = 0; k < 3; ++k) spawn[k] = goal[k] = stab[4 * di + k];
         reset_drone(kp, d, rng, kp.id0 + (uint32_t)g, spawn, goal);

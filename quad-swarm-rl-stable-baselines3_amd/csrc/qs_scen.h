@@ -22,7 +22,10 @@ __device__ __forceinline__ int ufloor(uint32_t w, int m) {
 // (step) / S_SCN_RESET (reset), one 32-bit word per draw in call order.
 // ---------------------------------------------------------------------------------------------
 enum { SC_STATIC_SAME_GOAL = 0, SC_STATIC_DIFF_GOAL, SC_EP_LISSAJOUS3D, SC_EP_RAND_BEZIER, SC_DYNAMIC_SAME_GOAL,
-       SC_DYNAMIC_DIFF_GOAL, SC_DYNAMIC_FORMATIONS, SC_SWAP_GOALS, SC_SWARM_VS_SWARM, SC_RUN_AWAY, SC_MIX };
+       SC_DYNAMIC_DIFF_GOAL, SC_DYNAMIC_FORMATIONS, SC_SWAP_GOALS, SC_SWARM_VS_SWARM, SC_RUN_AWAY, SC_MIX,
+       // the obstacle maps' dynamic scenarios (scenarios/obstacles/, QUADS_MODE_LIST_OBSTACLES_TEST utils.py:18-20):
+       // reset with the env's map by obstacle_reset_env (qs_flavor_b.h), stepped by scen_step_lane
+       SC_O_SWAP_GOALS, SC_O_EP_RAND_BEZIER, SC_O_DYNAMIC_SAME_GOAL };
 enum { F_CIRCLE_H = 0, F_CIRCLE_XZ, F_CIRCLE_YZ, F_SPHERE, F_GRID_H, F_GRID_XZ, F_GRID_YZ, F_CUBE };
 
 struct Scen {
@@ -87,11 +90,17 @@ __device__ __forceinline__ int sd_int(SDraw& s, int lo, int hi) { return lo + uf
 // position, so try i reads words 7 i .. 7 i + 6 of the step's scenario stream (the loop draws nothing else first).
 // np_: the candidate's two control points [c][j]; returns whether both lie inside the shrunk bounds.
 constexpr int BZ_WORDS = 7, BZ_MAX_TRIES = 1024;
+// o_ep_rand_bezier accepts ~0.6 % of its tries (its z band is 0.5 m wide): ~160 on average, beyond 1024 for ~0.2 % of
+// the resamples -- its bound is 8192 ((0.994)^8192 ~ 4e-22), searched by the env's lanes in parallel
+constexpr int BZ_MAX_TRIES_O = 8192;
+// o_dynamic_same_goal's rejection loop (a free cell within 4 m of the end point): bounded here
+constexpr int ODS_MAX_TRIES = 4096;
 __device__ __forceinline__ bool bz_try(SDraw& sd, const float* hi, const float* lo, float mx, const float* g,
                                        float (&np_)[3][2]) {
     float u[6];   // uniform(size=(2, 3)).reshape(3, 2): [c][j] = flat 2c + j
     for (int k = 0; k < 6; ++k) u[k] = sd_uniform(sd, -hi[k % 3], hi[k % 3]);
-    const float mag = (float)sd_int(sd, (int)ceilf(mx * 0.5f), (int)floorf(mx) + 1);
+    // np.random.randint(min_dist, max_dist + 1) with float bounds: numpy truncates both (randint(2.5, 6) draws 2..5)
+    const float mag = (float)sd_int(sd, (int)(mx * 0.5f), (int)floorf(mx) + 1);
     bool ok = true;
     for (int j = 0; j < 2; ++j) {
         const float v0 = u[j], v1 = u[2 + j], v2 = u[4 + j];
@@ -101,14 +110,46 @@ __device__ __forceinline__ bool bz_try(SDraw& sd, const float* hi, const float* 
     }
     return ok;
 }
-// the bounds of the tries for a formation of size `size` (ep_rand_bezier.py:13-19)
-__device__ __forceinline__ float bz_bounds(const KP& kp, float size, float* hi, float* lo) {
+// the bounds of the tries for a formation of size `size`: ep_rand_bezier.py:13-19, or (obst) o_ep_rand_bezier.py:19-28
+// (max_dist min(5, .), z in [1.5, 3.0])
+__device__ __forceinline__ float bz_bounds(const KP& kp, float size, float* hi, float* lo, bool obst = false) {
     float rd[3];
     for (int k = 0; k < 3; ++k) rd[k] = kp.room_hi[k] - kp.room_lo[k] - size;
-    const float mx = fminf(fmaxf(fmaxf(rd[0], rd[1]), rd[2]), 30.f);
-    hi[0] = rd[0] * 0.5f; hi[1] = rd[1] * 0.5f; hi[2] = rd[2];
-    lo[0] = -hi[0]; lo[1] = -hi[1]; lo[2] = 0.f;
+    const float mx = fminf(fmaxf(fmaxf(rd[0], rd[1]), rd[2]), obst ? 5.f : 30.f);
+    hi[0] = rd[0] * 0.5f; hi[1] = rd[1] * 0.5f; hi[2] = obst ? 3.f : rd[2];
+    lo[0] = -hi[0]; lo[1] = -hi[1]; lo[2] = obst ? 1.5f : 0.f;
     return mx;
+}
+
+// ---------------------------------------------------------------------------------------------
+// obstacle maps: pillars on an n x n grid of 1 m cells (quadrotor_multi.py:405-426, obstacles/utils.py:46-58)
+// ---------------------------------------------------------------------------------------------
+// grid cell (row, col) -> cell_centers[row + n*col]
+__device__ __forceinline__ float2 cell_xy(int cell, int n) {
+    const int row = cell / n, col = cell % n;
+    const float h = (float)(n / 2);
+    return make_float2((float)col + 0.5f - h, (float)(n - 1 - row) + 0.5f - h);
+}
+// the env's map as its pillar list (the block's LDS copy): m pillars on the n x n grid
+struct OCtx {
+    const float2* ob;
+    int m, n;
+};
+// Scenario_o_base.generate_pos_obst_map's cell (o_base.py:58-72): free_space[k] of np.where(obstacle_map == 0), i.e.
+// the k-th free cell in row-major order, as its centre; the occupied cells come back from the pillar centres
+// (cell_xy's inverse: small half-integers, exact)
+__device__ __forceinline__ float2 o_free_cell(const OCtx& oc, int k) {
+    const int n = oc.n;
+    const float h = (float)(n / 2);
+    uint64_t occ = 0ull;
+    for (int o = 0; o < oc.m; ++o) {
+        const int col = (int)(oc.ob[o].x - 0.5f + h), row = n - 1 - (int)(oc.ob[o].y - 0.5f + h);
+        occ |= 1ull << (row * n + col);
+    }
+    int c = 0;
+    for (; c < n * n; ++c)
+        if (!((occ >> c) & 1ull) && k-- == 0) break;
+    return cell_xy(min(c, n * n - 1), n);
 }
 // Generator.shuffle as Fisher-Yates from the top over LDS rows g[4 i ..]
 __device__ __forceinline__ void sd_shuffle(SDraw& s, float* g, int n) {
@@ -147,6 +188,8 @@ __device__ __forceinline__ void sc_mode_params(int mode, int& nform, float& low,
         nform = 8; low = 0.25f; high = 0.5f;
     } else if (mode == SC_SWAP_GOALS) {
         nform = 8; low = 0.4f; high = 0.8f;
+    } else if (mode == SC_O_SWAP_GOALS) {   // QUADS_FORMATION_LIST_OBSTACLES has 7 entries: index into QUADS_FORMATION_LIST
+        nform = 7; low = 0.4f; high = 0.8f;
     } else if (mode == SC_DYNAMIC_FORMATIONS) {
         nform = 8; low = 0.f; high = 1.0f;
     } else {
@@ -539,6 +582,9 @@ __device__ __forceinline__ bool scen_acts(const KP& kp, int mode, int period, in
         case SC_DYNAMIC_SAME_GOAL: case SC_DYNAMIC_DIFF_GOAL: case SC_SWAP_GOALS: case SC_SWARM_VS_SWARM: return ev;
         case SC_RUN_AWAY: return tick % (int)(1.f * (1.f / kp.cdt)) == 0 && tick > 0 && kp.N >= 2;
         case SC_EP_LISSAJOUS3D: case SC_EP_RAND_BEZIER: case SC_DYNAMIC_FORMATIONS: return true;
+        case SC_O_SWAP_GOALS: return ev;
+        case SC_O_EP_RAND_BEZIER: return true;
+        case SC_O_DYNAMIC_SAME_GOAL: return (period > 0 && tick % period == 0) || tick == 1;
         default: return false;
     }
 }
@@ -566,8 +612,10 @@ __device__ __forceinline__ void scen_from_words(const uint32_t* r, Scen& s) {
 // that use other drones' goals); tb: the shuffled goals (the shuffling modes write their drones' rows there and
 // set via_tab: the new goal is tb's row di after a barrier).  goal: in, the drone's goal; out, its new goal.
 // Returns what of the scenario record changed: 0 nothing, 1 size / inc / speed, 2 more (the whole record).
+// oc: the env's obstacle map (the obstacle scenarios only).
 __device__ __forceinline__ int scen_step_lane(const KP& kp, Scen& s, int tick, SDraw& sd, int di, const float* ta,
-                                              float* tb, float* goal, bool& via_tab, int bz_first = 0) {
+                                              float* tb, float* goal, bool& via_tab, int bz_first = 0,
+                                              const OCtx* oc = nullptr) {
     const int N = kp.N;   // index arithmetic (a constant of the specialised kernel); float geometry: sc_row / sc_num
     const float box = kp.spawn_box, cf = 1.f / kp.cdt;
     const int pl = sc_per_layer(s.form);
@@ -624,19 +672,22 @@ __device__ __forceinline__ int scen_step_lane(const KP& kp, Scen& s, int tick, S
                     nz = 0.01f * cos_any(2.f * t + 90.f) + ta[2];
         goal[0] = nx; goal[1] = ny; goal[2] = nz;
         return 0;
-    } else if (mode == SC_EP_RAND_BEZIER) {   // ep_rand_bezier.py:6-47
-        const int steps = (int)(5.f * cf);
+    } else if (mode == SC_EP_RAND_BEZIER || mode == SC_O_EP_RAND_BEZIER) {
+        // ep_rand_bezier.py:6-47; o_ep_rand_bezier.py:14-53 (6 s curves, max_dist min(5, .), z in [1.5, 3])
+        const bool ob = mode == SC_O_EP_RAND_BEZIER;
+        const int steps = (int)((ob ? 6.f : 5.f) * cf);
         const int t = tick % steps;
         float hi[3], lo[3];
-        const float mx = bz_bounds(kp, s.size, hi, lo);
+        const float mx = bz_bounds(kp, s.size, hi, lo, ob);
         int ch = 0;
         if (t == 0 || tick == 1) {
             // the rejection loop from try bz_first on (the first try any lane of the env found accepted, or 0): the
             // tries before it are rejected, so the loop ends on the same try as one from 0 would
             float np_[3][2];
+            const int cap = ob ? BZ_MAX_TRIES_O : BZ_MAX_TRIES;
             sd.k += (uint32_t)(BZ_WORDS * bz_first);
             for (int tries = bz_first;; ++tries)   // the reference loops without a bound
-                if (bz_try(sd, hi, lo, mx, ta, np_) || tries >= BZ_MAX_TRIES - 1) break;
+                if (bz_try(sd, hi, lo, mx, ta, np_) || tries >= cap - 1) break;
             for (int k = 0; k < 3; ++k) {
                 s.bz[k] = ta[k];
                 s.bz[3 + k] = np_[k][0];
@@ -675,6 +726,44 @@ __device__ __forceinline__ int scen_step_lane(const KP& kp, Scen& s, int tick, S
         }
         via_tab = true;
         return 2;
+    } else if (mode == SC_O_SWAP_GOALS) {   // o_swap_goals.py:14-24: np.random.shuffle(self.goals) every 4-6 s
+        if (!ev) return 0;
+        if (s.form == F_SPHERE && N < 3) {   // 3 goal rows (generate_points): the 1-2 no drone holds are c1 / c2
+            int idx[3] = {0, 1, 2};
+            for (int i = 2; i >= 1; --i) {
+                const int j = sd_int(sd, 0, i + 1);
+                const int t = idx[i];
+                idx[i] = idx[j];
+                idx[j] = t;
+            }
+            float old[3][3];
+            for (int r = 0; r < 3; ++r)
+                for (int k = 0; k < 3; ++k) old[r][k] = r < N ? ta[4 * r + k] : (r == N ? s.c1[k] : s.c2[k]);
+            for (int k = 0; k < 3; ++k) {
+                goal[k] = old[idx[di]][k];
+                s.c1[k] = old[idx[N]][k];
+                if (N + 1 < 3) s.c2[k] = old[idx[N + 1]][k];
+            }
+            return 2;
+        }
+        const int p = sd_track(sd, di, N);
+        tb[4 * p] = goal[0]; tb[4 * p + 1] = goal[1]; tb[4 * p + 2] = goal[2];
+        via_tab = true;
+        return 0;
+    } else if (mode == SC_O_DYNAMIC_SAME_GOAL) {   // o_dynamic_same_goal.py:17-29
+        if (!((s.period > 0 && tick % s.period == 0) || tick == 1)) return 0;
+        // generate_pos_obst_map() until the new goal is within max_dist = 4 of the end point: one free cell (choice of
+        // len(free_space)) and z ~ U(0.75, 3) per try, 2 words
+        const int F = oc->n * oc->n - oc->m;
+        float ng[3];
+        for (int tries = 0;; ++tries) {   // the reference loops without a bound
+            const float2 xy = o_free_cell(*oc, sd_int(sd, 0, F));
+            ng[0] = xy.x; ng[1] = xy.y; ng[2] = sd_uniform(sd, 0.75f, 3.f);
+            const float dx = s.c[0] - ng[0], dy = s.c[1] - ng[1], dz = s.c[2] - ng[2];
+            if (!(fsqrt(dx * dx + dy * dy + dz * dz) > 4.f) || tries >= ODS_MAX_TRIES - 1) break;
+        }
+        for (int k = 0; k < 3; ++k) s.c[k] = goal[k] = ng[k];
+        return 2;
     } else if (mode == SC_RUN_AWAY) {   // run_away.py:16-27
         if (tick % (int)(1.f * cf) == 0 && tick > 0 && N >= 2) {
             const int a = sd_int(sd, 1, N), b2 = sd_int(sd, 1, N);
@@ -697,20 +786,22 @@ __device__ __forceinline__ int bz_first_parallel(const KP& kp, const uint32_t* s
     static_assert(LPE <= 64, "the env's lanes inside one wave");
     const uint64_t seg = LA >= 64 ? ~0ull : ((1ull << LA) - 1ull);
     float hi[3], lo[3];
-    const float mx = bz_bounds(kp, __uint_as_float(srec[4]), hi, lo);
+    const bool ob = kp.scen_b == SC_O_EP_RAND_BEZIER;
+    const int cap = ob ? BZ_MAX_TRIES_O : BZ_MAX_TRIES;
+    const float mx = bz_bounds(kp, __uint_as_float(srec[4]), hi, lo, ob);
     int found = need ? -1 : 0;
     for (int rd = 0;; ++rd) {
         const int tr = rd * LA + li;
         bool ok = false;
-        if (found < 0 && tr < BZ_MAX_TRIES) {
+        if (found < 0 && tr < cap) {
             SDraw t = sdraw(r, key, S_SCN);
             t.k = (uint32_t)(BZ_WORDS * tr);
             float np_[3][2];
             ok = bz_try(t, hi, lo, mx, ta, np_);
         }
         const uint64_t m = (__ballot(ok) >> lbase) & seg;
-        if (found < 0 && m) found = min(rd * LA + (int)__ffsll((long long)m) - 1, BZ_MAX_TRIES - 1);
-        if (found < 0 && (rd + 1) * LA >= BZ_MAX_TRIES - 1) found = BZ_MAX_TRIES - 1;
+        if (found < 0 && m) found = min(rd * LA + (int)__ffsll((long long)m) - 1, cap - 1);
+        if (found < 0 && (rd + 1) * LA >= cap - 1) found = cap - 1;
         if (__ballot(found < 0) == 0ull) break;
     }
     return found;

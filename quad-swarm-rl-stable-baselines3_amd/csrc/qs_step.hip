@@ -140,8 +140,10 @@ static int validate(const qs_config* c) {
         if (c->neighbor_obs != QS_NEIGHBOR_NONE && c->neighbor_obs != QS_NEIGHBOR_POS_VEL)
             return fail(QS_E_UNSUPPORTED, "flavor B implements neighbor_obs none / pos_vel");
         if (c->use_obstacles) {
-            if (c->scenario < QS_SCEN_OBST_MIX || c->scenario > QS_SCEN_O_STATIC_SAME_GOAL)
-                return fail(QS_E_UNSUPPORTED, "obstacles need scenario obst_mix / o_random / o_static_same_goal");
+            if ((c->scenario < QS_SCEN_OBST_MIX || c->scenario > QS_SCEN_O_STATIC_SAME_GOAL) &&
+                (c->scenario < QS_SCEN_O_SWAP_GOALS || c->scenario > QS_SCEN_O_DYNAMIC_SAME_GOAL))
+                return fail(QS_E_UNSUPPORTED, "obstacles need scenario obst_mix / o_random / o_static_same_goal / "
+                                              "o_swap_goals / o_ep_rand_bezier / o_dynamic_same_goal");
             if (c->obst_area < 1 || c->obst_area > 8) return fail(QS_E_UNSUPPORTED, "obst_area must be in [1, 8]");
             if (c->num_obstacles < 1 || c->num_obstacles + c->num_agents > c->obst_area * c->obst_area)
                 return fail(QS_E_INVALID, "num_obstacles must leave a free cell per drone");
@@ -381,7 +383,11 @@ static qs::KP make_kp(const qs_config* c, const qs_layout& L) {
     }
     if (c->use_obstacles) {
         k.obst = 1; k.M = obst_slots(c); k.obst_n = c->obst_area;
-        k.obst_scen = c->scenario == QS_SCEN_OBST_MIX ? 0 : (c->scenario == QS_SCEN_O_RANDOM ? 1 : 2);
+        // 0 mix (o_random / o_static_same_goal), then the obstacle mode + 1: o_random, o_static_same_goal,
+        // o_swap_goals, o_ep_rand_bezier, o_dynamic_same_goal; the dynamic ones also step as goal scenarios (scen_b)
+        k.obst_scen = c->scenario == QS_SCEN_OBST_MIX ? 0 : (c->scenario == QS_SCEN_O_RANDOM ? 1 :
+                      c->scenario == QS_SCEN_O_STATIC_SAME_GOAL ? 2 : 3 + (c->scenario - QS_SCEN_O_SWAP_GOALS));
+        if (c->scenario >= QS_SCEN_O_SWAP_GOALS) k.scen_b = qs::SC_O_SWAP_GOALS + (c->scenario - QS_SCEN_O_SWAP_GOALS);
         k.obst_r = 0.5f * c->obst_size;
         k.obst_thr = (float)((double)c->arm + 0.5 * (double)c->obst_size);   // quad arm + pillar radius
         // domain randomisation tables: index 0 = the configured pillars, choice c = index c + 1
@@ -524,8 +530,9 @@ static size_t shm_bytes(const qs_config& c, int obs_dim, int npad, bool step, in
     const size_t epb = (size_t)envs_per_block(c, npad, step, qb, qa), slots = epb * (size_t)npad;
     size_t b = sizeof(float) * slots * (size_t)obs_dim + sizeof(float) * slots * 8 + sizeof(float) * 64;
     if (c.use_obstacles) b += epb * (sizeof(float) * 2 * (size_t)obst_slots(&c) + (size_t)qs::QS_OBST_SCRATCH);
-    else if (c.scenario >= QS_SCEN_MIX && c.scenario <= QS_SCEN_RUN_AWAY)   // goal tables (qs::scen_stride)
-        b += epb * sizeof(float) * (2 * ((size_t)npad + 4) * 4 + 32);
+    const bool tables = c.use_obstacles ? c.scenario >= QS_SCEN_O_SWAP_GOALS
+                                        : (c.scenario >= QS_SCEN_MIX && c.scenario <= QS_SCEN_RUN_AWAY);
+    if (tables) b += epb * sizeof(float) * (2 * ((size_t)npad + 4) * 4 + 32);   // goal tables (qs::scen_stride)
     return b;
 }
 

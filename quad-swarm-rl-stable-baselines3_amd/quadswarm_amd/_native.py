@@ -9,7 +9,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("QUADSWARM_LIB", os.path.join(HERE, "lib", "libquadswarm.so"))
 
-ABI_VERSION = 13
+ABI_VERSION = 14
 MAX_AGENTS = 128
 A_KMAX = 16   # flavor A, more than 64 drones: visible neighbours (qs_flavor_a.h QS_A_KMAX)
 MAX_DR_CHOICES = 8
@@ -27,7 +27,11 @@ NEIGHBOR_NONE, NEIGHBOR_POS_VEL = 0, 1
 NEIGHBOR = {"none": 0, "pos_vel": 1, "dist_angle": 2, "dist_sangle": 3, "ndist_nsangle": 4, "dist_angle_heading": 5,
             "dist_sangle_sheading": 6, "pos": 7, "npos": 8}
 NEIGHBOR_DIM = {0: 0, 1: 6, 2: 2, 3: 3, 4: 3, 5: 3, 6: 5, 7: 3, 8: 3}
-SCENARIO = {"static_same_goal": 0, "dynamic_repulsive": 1, "obst_mix": 2, "o_random": 3, "o_static_same_goal": 4}
+SCENARIO = {"static_same_goal": 0, "dynamic_repulsive": 1, "obst_mix": 2, "o_random": 3, "o_static_same_goal": 4,
+            "o_swap_goals": 15, "o_ep_rand_bezier": 16, "o_dynamic_same_goal": 17}
+# flavor B with obstacles: quads_mode -> qs_scenario (scenarios/obstacles/; the dynamic three: ABI 14)
+SCENARIO_OBST = {"mix": 2, "o_random": 3, "o_static_same_goal": 4, "o_swap_goals": 15, "o_ep_rand_bezier": 16,
+                 "o_dynamic_same_goal": 17}
 # flavor B without obstacles: quads_mode -> qs_scenario (the goal scenarios of gym_art/quadrotor_multi/scenarios/)
 SCENARIO_B = {"static_same_goal": 0, "mix": 5, "static_diff_goal": 6, "ep_lissajous3D": 7, "ep_rand_bezier": 8,
               "dynamic_same_goal": 9, "dynamic_diff_goal": 10, "dynamic_formations": 11, "swap_goals": 12,

@@ -217,8 +217,7 @@ class QuadSwarmConfig:
     @property
     def scenario_id(self):
         if self.use_obstacles:
-            return {"mix": N.SCENARIO["obst_mix"], "o_random": N.SCENARIO["o_random"],
-                    "o_static_same_goal": N.SCENARIO["o_static_same_goal"]}[self.quads_mode]
+            return N.SCENARIO_OBST[self.quads_mode]
         if self.flavor == "B" or self.quads_mode not in N.SCENARIO:
             return N.SCENARIO_B[self.quads_mode]   # goal scenarios (create_scenario) of either flavor
         return N.SCENARIO[self.quads_mode]
@@ -247,9 +246,8 @@ class QuadSwarmConfig:
         if self.use_obstacles:
             if self.flavor != "B":
                 raise NotImplementedError("obstacles are implemented for flavor B")
-            if self.quads_mode not in ("mix", "o_random", "o_static_same_goal"):
-                raise NotImplementedError(f"quads_mode {self.quads_mode!r} with obstacles (mix, o_random, "
-                                          "o_static_same_goal)")
+            if self.quads_mode not in N.SCENARIO_OBST:
+                raise NotImplementedError(f"quads_mode {self.quads_mode!r} with obstacles ({', '.join(N.SCENARIO_OBST)})")
             a = self.obst_spawn_area
             if a[0] != a[1] or int(a[0]) != a[0] or not 1 <= a[0] <= 8:
                 raise NotImplementedError("obst_spawn_area must be a square of 1..8 cells")

@@ -14,11 +14,13 @@ ES_SUCCESS, ES_DEADLOCK, ES_COLRATE, ES_NCOLRATE, ES_OCOLRATE, ES_SCEN, ES_D1, E
 NES = 24
 
 # scenario id of a row -> the reference's scenario class name minus "Scenario_": QUADS_MODE_LIST order
-# (scenarios/utils.py:7-10) + run_away for the goal scenarios, 16 + mode for the obstacle ones
+# (scenarios/utils.py:7-10) + run_away for the goal scenarios, 16 + mode for the obstacle ones (19-21: the maps'
+# dynamic scenarios, qs_flavor_b.h obst_stats_id)
 SCENARIO_NAMES = {0: "static_same_goal", 1: "static_diff_goal", 2: "ep_lissajous3D", 3: "ep_rand_bezier",
                   4: "dynamic_same_goal", 5: "dynamic_diff_goal", 6: "dynamic_formations", 7: "swap_goals",
                   8: "swarm_vs_swarm", 9: "run_away", 16: "o_random", 17: "o_static_same_goal",
-                  18: "dynamic_repulsive"}   # flavor A's target-chasing scenario
+                  18: "dynamic_repulsive",   # flavor A's target-chasing scenario
+                  19: "o_swap_goals", 20: "o_ep_rand_bezier", 21: "o_dynamic_same_goal"}
 
 
 def episode_extra_stats(row, use_obstacles=False):

@@ -49,7 +49,8 @@ def oracle_params(cfg: QuadSwarmConfig):
         p.use_obstacles = 1
         p.num_obstacles = cfg.num_obstacles
         p.obst_area = int(cfg.obst_spawn_area[0])
-        p.obst_scenario = {"mix": 0, "o_random": 1, "o_static_same_goal": 2}[cfg.quads_mode]
+        p.obst_scenario = {"mix": 0, "o_random": 1, "o_static_same_goal": 2, "o_swap_goals": 3,
+                           "o_ep_rand_bezier": 4, "o_dynamic_same_goal": 5}[cfg.quads_mode]
         p.obst_size = cfg.obst_size
         p.obst_z = rd[2] / 2.0
         p.sdf_resolution = 0.1
@@ -69,6 +70,10 @@ def oracle_params(cfg: QuadSwarmConfig):
 
 SC_I = ("mode", "formation", "period", "increase")
 SC_F = ("size", "lo", "hi", "layer", "speed")
+# the obstacle maps' dynamic scenarios: the GPU record's mode word is the stats' scenario id (19..21,
+# qs_flavor_b.h obst_stats_id), the oracle's or_scen.mode its OR_SC_O_* code (11..13)
+GPU_TO_OR_MODE = {19: O.SC_O_SWAP_GOALS, 20: O.SC_O_EP_RAND_BEZIER, 21: O.SC_O_DYNAMIC_SAME_GOAL}
+OR_TO_GPU_MODE = {v: k for k, v in GPU_TO_OR_MODE.items()}
 
 
 def scen_gpu_to_oracle(env, oenv):
@@ -79,6 +84,7 @@ def scen_gpu_to_oracle(env, oenv):
         sc = oenv.envs[e].scen
         for k, n in enumerate(SC_I):
             setattr(sc, n, int(es[NAT.E_SC_MODE + k, e]))
+        sc.mode = GPU_TO_OR_MODE.get(sc.mode, sc.mode)
         sc.per_layer = 50 if sc.formation in (4, 5, 6) else 8
         for k, n in enumerate(SC_F):
             setattr(sc, n, float(ef[NAT.ENVF_SC_SIZE + k, e]))
@@ -98,6 +104,7 @@ def scen_oracle_to_gpu(oenv, env):
         sc = oenv.envs[e].scen
         for k, n in enumerate(SC_I):
             es[NAT.E_SC_MODE + k, e] = getattr(sc, n)
+        es[NAT.E_SC_MODE, e] = OR_TO_GPU_MODE.get(sc.mode, sc.mode)
         for k, n in enumerate(SC_F):
             ef[NAT.ENVF_SC_SIZE + k, e] = getattr(sc, n)
         for c in range(3):

@@ -390,3 +390,18 @@ def test_curriculum_init_fills_the_struct_mirror():
     assert c.window_i == 0 and c.n_shrinks == 0 and c.success_rate == 0.0 and not any(c.past)
     assert L.qs_curriculum_init(raw, 0.5, 0.8, 0.9, 65) == -1
     assert L.qs_curriculum_init(raw, 0.0, 0.8, 0.9, 40) == -1
+
+
+@pytest.mark.parametrize("mode", ["o_swap_goals", "o_ep_rand_bezier", "o_dynamic_same_goal"])
+def test_obstacle_dynamic_scenarios_accepted(mode):
+    """The obstacle maps' dynamic scenarios (ABI 14): accepted with obstacles, their qs_scenario values, a layout with
+    the goal tables in the LDS budget, and specialised kernels that compile; refused without obstacles."""
+    L = N.lib()
+    c = QuadSwarmConfig.c4(num_envs=64, quads_mode=mode)
+    qc = c.to_qs_config()
+    assert qc.scenario == N.SCENARIO[mode] == {"o_swap_goals": 15, "o_ep_rand_bezier": 16, "o_dynamic_same_goal": 17}[mode]
+    lay = N.QsLayout()
+    assert L.qs_layout_query(qc, lay) == 0, L.qs_last_error()
+    assert L.qs_specialize_compile(qc) > 10000, L.qs_last_error()
+    with pytest.raises(NotImplementedError):
+        QuadSwarmConfig(num_envs=4, num_agents=8, quads_mode=mode).to_qs_config()

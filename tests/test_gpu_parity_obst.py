@@ -216,3 +216,111 @@ def test_domain_random_steps_from_identical_state():
         stats["obst"] += int((w_rew < -2.0).sum())
         gpu_to_oracle(env, oenv)
     assert stats["done"] > 0 and stats["obst"] > 0
+
+
+# ---------------------------------------------------------------- the obstacle maps' dynamic scenarios
+# o_swap_goals / o_ep_rand_bezier / o_dynamic_same_goal (scenarios/obstacles/, QUADS_MODE_LIST_OBSTACLES_TEST): the
+# oracle's restatement is pinned to the reference's own classes by tests/test_oracle_golden_oscen.py; here the GPU
+# matches it draw for draw (Philox) at reset and across the scenario's events.
+OSCEN = ["o_swap_goals", "o_ep_rand_bezier", "o_dynamic_same_goal"]
+
+
+def _scen_rows(env):
+    es = env.env_state.cpu().numpy()
+    ef = NAT.env_f_rows(env.env_f.double().cpu().numpy())
+    return es, ef
+
+
+def assert_scen_match(env, oenv, atol=2e-5):
+    from parity_utils import OR_TO_GPU_MODE
+    es, ef = _scen_rows(env)
+    for e in range(oenv.E):
+        sc = oenv.envs[e].scen
+        assert int(es[NAT.E_SC_MODE, e]) == OR_TO_GPU_MODE[sc.mode], e
+        assert int(es[NAT.E_SC_PERIOD, e]) == sc.period, e
+        assert int(es[NAT.E_SC_FORM, e]) == sc.formation, e
+        np.testing.assert_allclose(ef[NAT.ENVF_SC_CENTER:NAT.ENVF_SC_CENTER + 3, e], sc.center[:], atol=atol)
+        np.testing.assert_allclose([ef[NAT.ENVF_SC_SIZE, e], ef[NAT.ENVF_SC_LAYER, e]], [sc.size, sc.layer], atol=1e-6)
+
+
+def goals_of(oenv):
+    return np.array([oenv.drones[g].goal[:] for g in range(oenv.E * oenv.N)])
+
+
+@pytest.mark.parametrize("N", [8, 2])
+@pytest.mark.parametrize("mode", OSCEN)
+def test_dynamic_scenario_reset_matches_oracle(mode, N):
+    cfg, env, oenv = make_pair(E=512, N=N, quads_mode=mode, neighbor_visible_num=min(2, N - 1))
+    obs = np_(env.reset())
+    want = oenv.reset()
+    np.testing.assert_array_equal(np_(env.obstacles), obstacles_of(oenv))
+    np.testing.assert_allclose(obs, want, atol=2e-5, rtol=1e-5)
+    pos = np.array([oenv.drones[g].pos[:] for g in range(env.I)])
+    np.testing.assert_allclose(np_(env.drone_fields()["pos"]), pos, atol=2e-6)
+    np.testing.assert_allclose(np_(env.drone_fields()["goal"]), goals_of(oenv), atol=2e-5)
+    assert_scen_match(env, oenv)
+    periods = {oenv.envs[e].scen.period for e in range(oenv.E)}
+    assert len(periods) > 10 if mode != "o_ep_rand_bezier" else periods == {1}
+    if mode == "o_swap_goals":   # the formation draws cover several formations
+        assert len({oenv.envs[e].scen.formation for e in range(oenv.E)}) >= 5
+
+
+@pytest.mark.parametrize("mode", OSCEN)
+def test_dynamic_scenario_steps_from_identical_state(mode):
+    """Steps across the scenario's events from identical states: every env's tick is set a few ticks before its next
+    event (the swap / resample period, the bezier curve's 6 s boundary, tick 1), goals, rewards, obs and the scenario
+    record compared after every step."""
+    from parity_utils import scen_gpu_to_oracle, scen_oracle_to_gpu
+    N = 8
+    cfg, env, oenv = make_pair(E=256, N=N, quads_mode=mode, episode_duration=15.0)
+    env.reset()
+    oenv.reset()
+    rng = np.random.default_rng(11)
+    for e in range(oenv.E):   # the next event within 0..5 steps (tick 0 -> the tick-1 event)
+        ev = oenv.envs[e]
+        per = 600 if mode == "o_ep_rand_bezier" else ev.scen.period
+        ev.tick = 0 if e % 4 == 0 else max(per * (1 + e % 2) - int(rng.integers(1, 6)), 0)
+    K = cfg.k_neighbors
+    so = NAT.SELF_OBS_DIM[NAT.OBS_REPR[cfg.obs_repr]]
+    moved = 0
+    for t in range(10):
+        oracle_to_gpu(oenv, env)
+        scen_oracle_to_gpu(oenv, env)
+        g0 = goals_of(oenv)
+        a = (rng.uniform(-1, 1, (env.I, 4)) * 0.2 + 0.05).astype(np.float32)
+        obs, rew, done, term = env.step(torch.from_numpy(a).cuda())
+        w_obs, w_rew, w_done, w_term = oenv.step(a.astype(np.float64))
+        np.testing.assert_array_equal(done.cpu().numpy().astype(bool), w_done)
+        np.testing.assert_allclose(np_(env.drone_fields()["goal"]), goals_of(oenv), atol=2e-5, err_msg=f"step {t}")
+        np.testing.assert_allclose(np_(rew), w_rew, atol=2e-4, rtol=1e-4)
+        g_obs = np_(obs)
+        np.testing.assert_allclose(g_obs[:, -9:], w_obs[:, -9:], atol=2e-4, rtol=1e-4)
+        assert_obs_match(g_obs[:, :-9], w_obs[:, :-9], oenv, so, K)
+        assert_scen_match(env, oenv)
+        moved += int((np.abs(goals_of(oenv) - g0).max(axis=1) > 1e-6).sum())
+        gpu_to_oracle(env, oenv)
+        scen_gpu_to_oracle(env, oenv)
+    assert moved > env.I // 4, moved   # the events happened in the window
+
+
+@pytest.mark.parametrize("mode", OSCEN)
+def test_full_size_dynamic_scenarios(mode):
+    """4096 x 8 under each mode: finite obs, goals inside the room (the bezier goal inside its shrunk box), goals that
+    move, the episode stats' scenario name of the reference's class."""
+    from quadswarm_amd.stats import SCENARIO_NAMES
+    cfg = QuadSwarmConfig.c4(num_envs=4096, num_agents=8, seed=9, quads_mode=mode, episode_duration=7.0)
+    env = QuadSwarmEnv(cfg)
+    env.reset()
+    g0 = env.drone_fields()["goal"].clone()
+    rng = torch.Generator(device="cuda").manual_seed(3)
+    for t in range(700):
+        a = torch.rand(env.I, 4, device="cuda", generator=rng) * 2 - 1
+        obs, rew, done, term = env.step(a)
+    assert torch.isfinite(obs).all()
+    g = env.drone_fields()["goal"]
+    assert torch.isfinite(g).all() and (g[:, :2].abs() <= 5.0).all() and (g[:, 2] >= 0.0).all()
+    frac_moved = float(((g - g0).abs().max(dim=1).values > 1e-6).float().mean())
+    assert frac_moved > 0.5, frac_moved
+    es = env.env_state.cpu().numpy()
+    ids = set(es[NAT.E_SC_MODE].tolist())
+    assert ids == {19 + OSCEN.index(mode)} and SCENARIO_NAMES[ids.pop()] == mode

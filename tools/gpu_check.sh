@@ -214,6 +214,11 @@ for s in "$@"; do
         CONFIG=$c STEPS=${STEPS:-2000} step abjit_$c 900 bash tools/ab_jit.sh ${AB:?AB=tag:defs ...} ${AB}
       done
       ;;
+    absrc)     # bitwise digest + timing A/B against a base kernel tree: CONFIGS, BASE (default tools/jit/base_r06)
+      for c in ${CONFIGS:-c3}; do
+        CONFIG=$c STEPS=${STEPS:-2000} ROUNDS=${ROUNDS:-1} step absrc_$c 900 bash tools/ab_src.sh base:${BASE:-tools/jit/base_r06} new:
+      done
+      ;;
     launch)    # launch-path A/B of the driver's 20-step window (tools/launch_probe.py)
       step launch_probe 300 python tools/launch_probe.py --reps 10
       ;;
