@@ -277,9 +277,10 @@ def e2e_settings(cfg):
     return pc, PPOConfig(n_steps=128, n_epochs=1, gae_lambda=1.0, max_grad_norm=5.0), 16
 
 
-def update_flops_per_sample(pol, obs_dim, act_dim, dev, rows=256):
+def update_flops_per_sample(pol, obs_dim, act_dim, dev, rows=256, split=False):
     """FLOPs of one sample's PPO update (evaluate_actions forward + backward), counted by torch's
-    FlopCounterMode (GEMM / addmm / bmm flops) on a small batch of the same policy."""
+    FlopCounterMode (GEMM / addmm / bmm flops) on a small batch of the same policy.  split: also the share of the
+    two towers' neighbour encoders (the modules the fused x3 update runs on the f16 matrix cores)."""
     import torch
     from torch.utils.flop_counter import FlopCounterMode
     obs = torch.randn(rows, obs_dim, device=dev)
@@ -288,7 +289,15 @@ def update_flops_per_sample(pol, obs_dim, act_dim, dev, rows=256):
         v, lp, _ = pol.evaluate_actions(obs, act)
         (v.sum() + lp.sum()).backward()
     pol.zero_grad(set_to_none=False)
-    return fc.get_total_flops() / rows
+    total = fc.get_total_flops() / rows
+    if not split:
+        return total
+    enc = sum(sum(ops.values()) for name, ops in fc.get_flop_counts().items()
+              if name.endswith(".neighbor_encoder")) / rows
+    return total, enc
+
+
+F16_DENSE_TFLOPS = 2500.0     # MI355X_MICROARCH.md: BF16 / F16 MFMA ~2.5 PF dense
 
 
 def end_to_end(env, cfg, dev, world, iters, n_steps=None, log=None, fused=True, precision="fp32",
@@ -344,8 +353,13 @@ def end_to_end(env, cfg, dev, world, iters, n_steps=None, log=None, fused=True, 
         el, t_roll, t_train = (float(x) for x in t.tolist())
     nparam = sum(p.numel() for p in pol.parameters())
     # the update's GEMM work against the fp32 matrix-core peak (MI355X_MICROARCH: 157.3 TF dense f32)
-    fps = update_flops_per_sample(pol, env.obs_dim, env.act_dim, dev)
+    fps, enc_fps = update_flops_per_sample(pol, env.obs_dim, env.act_dim, dev, split=True)
     upd_tf = fps * samples * pcfg.n_epochs / (t_train / iters) / 1e12
+    # the ceiling of the update as it runs: with the fused x3 encoders their fp32-equivalent work is 3 f16 products per
+    # fp32 product on the f16 matrix cores (2.5 PF / 3), the rest fp32 on hipBLASLt (157.3 TF); without, all fp32
+    x3 = update_precision == "x3" and getattr(tr, "fused_update", None) is not None
+    enc_peak = (F16_DENSE_TFLOPS / 3.0) if x3 else 157.3
+    floor_s = samples * pcfg.n_epochs * (enc_fps / (enc_peak * 1e12) + (fps - enc_fps) / 157.3e12)
     tr.bucket.zero()
     return {
         "metric": "end-to-end PPO agent-steps/s (rollout + GAE + update; weak scaling, one gradient "
@@ -365,6 +379,11 @@ def end_to_end(env, cfg, dev, world, iters, n_steps=None, log=None, fused=True, 
         "gemm_table": tuned,
         "update_flop_per_sample": round(fps), "update_tflops": round(upd_tf, 2),
         "update_frac_fp32_mfma_peak": round(upd_tf / 157.3, 3),
+        "update_encoder_flop_share": round(enc_fps / fps, 3),
+        "update_ceiling": {"encoders_tflops": round(enc_peak, 1), "rest_tflops": 157.3, "floor_s": round(floor_s, 4),
+                           "frac": round(floor_s / (t_train / iters), 3),
+                           "note": "x3 encoders: 3 f16 MFMA products per fp32 product at the 2.5 PF dense f16 peak"
+                                   if x3 else "all fp32 matrix cores"},
         "last_update": {k: (round(v, 6) if isinstance(v, float) else v) for k, v in stats.items()},
     }
 
