@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define QS_ABI_VERSION 14
+#define QS_ABI_VERSION 15
 #define QS_MAX_AGENTS 128           /* drones per env: up to 64 inside one 64-lane wavefront, 128 = a two-wave
                                        workgroup per env (flavor B without obstacles; paper/fps_compare.py:7) */
 #define QS_MAX_DR_CHOICES 8         /* entries per obstacle domain-randomisation list */
@@ -509,7 +509,18 @@ typedef struct qs_attn_train {
     float* dscore;         /* backward 1: [B*K] dL/d score */
     float* de2p;           /* backward 1: dL/d e2 without the e_mean term */
     float* de2_pre; float* de1_pre;                                  /* backward 2 outputs */
+    /* ABI 15 (both may be NULL: not written): the gradients' column statistics, formed where the gradients are, per
+     * row block of the kernels (n_blocks = ceil(B K / (floor(64 / K) K)), block b = rows [b m, (b + 1) m), m =
+     * floor(64 / K) K):
+     * colmax: [QS_ATTN_NCOLMAX][n_blocks][H] max |g| over the block's rows per column (+inf when a g is not finite)
+     *   of dh_pre, dv1_pre, da2_pre, da1_pre (backward 1), de2_pre and de1_pre (backward 2) -- their max over the
+     *   blocks gives dW's column scales (qs_attn_dw_x3 / qs_attn_dw0_x3 col_scale);
+     * a3w_part: [n_blocks][H] the block's sum of dscore_j a2_j (the score layer's weight gradient is the sum over
+     *   the blocks). */
+    float* colmax;
+    float* a3w_part;
 } qs_attn_train;
+#define QS_ATTN_NCOLMAX 6   /* colmax rows: 0 dh_pre, 1 dv1_pre, 2 da2_pre, 3 da1_pre, 4 de2_pre, 5 de1_pre */
 int qs_attn_embed_train_x3(const float* d_obs, int32_t obs_stride, int32_t self_dim, int32_t nbr_off, int32_t B, int32_t K,
                            int32_t nd, int32_t H, const qs_attn_tower* towers, const qs_attn_train* trains,
                            int32_t n_towers, void* stream);
@@ -521,9 +532,20 @@ int qs_attn_bwd2_x3(int32_t B, int32_t K, int32_t H, const qs_attn_tower* towers
                     int32_t n_towers, void* stream);
 /* A weight gradient G^T A over R rows on the split-f16 matrix cores, split over n_parts row ranges:
  * part[p] = G[rows of p]^T A[rows of p] ([n_parts, H, H] fp32; dW = the sum over p).  G [R, H] (pre-activation
- * gradients) with a power-of-two scale per column, col_scale[n] |G[:, n]| < 2^14; A [R, H] with |A| <= 1 (tanh). */
+ * gradients) with a power-of-two scale per column, col_scale[n] |G[:, n]| < 2^14; A [R, H] with |A| <= 1 (tanh).
+ * part_sum (ABI 15; NULL: not written): [n_parts, H] the column sums of G over each part's rows (the bias gradient
+ * is their sum over p) from the same pass. */
 int qs_attn_dw_x3(const float* G, const float* A, const float* col_scale, int64_t R, int32_t H, float* part,
-                  int32_t n_parts, void* stream);
+                  float* part_sum, int32_t n_parts, void* stream);
+/* Layer 0's weight gradient (ABI 15): part[p] = G[rows of p]^T X[rows of p] ([n_parts, H, 32] fp32; the sum over p
+ * is the gradient of embedding layer 0's weight in the kernels' column order [neighbour (nd) | self (self_dim) | 0])
+ * with X the layer-0 input rows the forward gathers (row r = agent r / K, neighbour r % K of that agent's block at
+ * nbr_off, self features of agent r % B -- the reference's repeat pairing, quad_multi_model.py:44-101), G = de1_pre
+ * [B K, H] with col_scale as qs_attn_dw_x3, |obs| < 4094 (the forward's split-f16 range); part_sum (NULL: not
+ * written): [n_parts, H] G's column sums (the bias gradient's parts).  nd + self_dim <= 32. */
+int qs_attn_dw0_x3(const float* G, const float* col_scale, const float* d_obs, int32_t obs_stride, int32_t self_dim,
+                   int32_t nbr_off, int32_t B, int32_t K, int32_t nd, int32_t H, float* part, float* part_sum,
+                   int32_t n_parts, void* stream);
 /* Column reductions of a gradient G [R, H] in one pass over its rows (ABI 13; the update's bias gradients, the dW
  * column scales and layer 0's weight gradient, in place of torch's abs / amax / sum / skinny-GEMM passes), split
  * over n_parts row ranges, per part p and column n:

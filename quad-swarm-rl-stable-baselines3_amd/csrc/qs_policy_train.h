@@ -30,6 +30,10 @@
 namespace qs {
 namespace pol {
 
+#ifndef QS_BWD1_BR2
+#define QS_BWD1_BR2 8   // rows per batch of bwd1's second staging (de2p's value part is live: 64 VGPRs)
+#endif
+
 struct Trains {
     qs_attn_train t[QS_ATTN_MAX_TOWERS];
 };
@@ -39,15 +43,28 @@ __device__ __forceinline__ float row_scale(float mx) {
     if (!(mx > 0.f) || !(mx <= 3.0e38f)) return 1.f;
     return __builtin_amdgcn_ldexpf(1.f, 14 - __builtin_amdgcn_frexp_expf(mx));
 }
+// wave reductions (every lane active): DPP inside each 16-lane row (quad swaps, then row rotations by 4 and 8), then
+// the four rows' lane-0 values through readlane -- no LDS round trips (a __shfl_xor butterfly is six ds_bpermute)
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float rdl(float v, int l) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
-    return v;
+    v += dppf<0xB1>(v);    // quad_perm [1, 0, 3, 2]
+    v += dppf<0x4E>(v);    // quad_perm [2, 3, 0, 1]
+    v += dppf<0x124>(v);   // row_ror 4
+    v += dppf<0x128>(v);   // row_ror 8
+    return (rdl(v, 0) + rdl(v, 16)) + (rdl(v, 32) + rdl(v, 48));
 }
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) v = fmaxf(v, __shfl_xor(v, m));
-    return v;
+    v = fmaxf(v, dppf<0xB1>(v));
+    v = fmaxf(v, dppf<0x4E>(v));
+    v = fmaxf(v, dppf<0x124>(v));
+    v = fmaxf(v, dppf<0x128>(v));
+    return fmaxf(fmaxf(rdl(v, 0), rdl(v, 16)), fmaxf(rdl(v, 32), rdl(v, 48)));
 }
 __device__ __forceinline__ float4 ld4g(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ void st4g(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
@@ -57,32 +74,119 @@ __device__ __forceinline__ float4 f4_dtanh(float4 g, float4 t) {   // g (1 - t^2
     return make_float4(g.x * (1.f - t.x * t.x), g.y * (1.f - t.y * t.y), g.z * (1.f - t.z * t.z), g.w * (1.f - t.w * t.w));
 }
 
-// Rows staged from HBM: wave w takes rows w, w + 4, ...; lane l < H/4 the row's columns 4l .. 4l+3.
-// val(r, c4, on) -> the row's float4 (0 for unused rows), called by every lane of the wave (it may reduce over the
-// wave) with on = the lane holds columns (c4 is clamped for the others, whose value is dropped); sink(r, c4, v) sees
-// the lane's value (e.g. stores it); the tile gets s_r v and RS[r] = 1 / s_r.
-template <int H, typename Val, typename Sink>
-__device__ __forceinline__ void stage_rows_scaled(const TileX3& X, float* RS, int wave, int lane, Val val, Sink sink) {
+// column maxima of the gradients (qs_attn_train.colmax, dW's column scales): running max |x| (+inf once an x is not
+// finite); every block writes its own row of maxima (plain stores: atomics from every block to the same H addresses
+// serialise -- measured 2.6x slower backward kernels), the host takes the max over the blocks
+__device__ __forceinline__ float absmax_acc(float m, float x) {
+    const float a = fabsf(x);
+    return a <= 3.4028235e38f ? fmaxf(m, a) : __builtin_inff();
+}
+__device__ __forceinline__ float4 absmax_acc4(float4 m, float4 v) {
+    return make_float4(absmax_acc(m.x, v.x), absmax_acc(m.y, v.y), absmax_acc(m.z, v.z), absmax_acc(m.w, v.w));
+}
+__device__ __forceinline__ float4 max4(float4 a, float4 b) {
+    return make_float4(fmaxf(a.x, b.x), fmaxf(a.y, b.y), fmaxf(a.z, b.z), fmaxf(a.w, b.w));
+}
+// accumulator-layout maxima m[c][g] (column acc_n0(wave, c, g, lane) + j over the lane's rows) -> the block's maxima of
+// the wave's columns in dst[n]: over the 16 lanes of each lane row by DPP, then rows 0 + 1 and 2 + 3 (row_bcast 15:
+// lanes 16 and 48 hold the 32 rows of their column sets), stored by those two lanes
+template <int H>
+__device__ __forceinline__ void colmax_store_acc(float* dst, float4 (&m)[Geo<H>::CT][4], int wave, int lane) {
+#pragma unroll
+    for (int c = 0; c < Geo<H>::CT; ++c)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            float v[4] = {m[c][g].x, m[c][g].y, m[c][g].z, m[c][g].w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                v[j] = fmaxf(v[j], dppf<0xB1>(v[j]));
+                v[j] = fmaxf(v[j], dppf<0x4E>(v[j]));
+                v[j] = fmaxf(v[j], dppf<0x124>(v[j]));
+                v[j] = fmaxf(v[j], dppf<0x128>(v[j]));
+                const int b = __builtin_bit_cast(int, v[j]);
+                v[j] = fmaxf(v[j], __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(b, b, 0x142, 0xA, 0xF, false)));
+            }
+            if (lane == 16 || lane == 48) {
+                const int n0 = acc_n0<H>(wave, c, g, lane);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) dst[n0 + j] = v[j];
+            }
+        }
+}
+struct NoStat {
+    template <typename A>
+    __device__ void operator()(int, float4, const A&) const {}
+};
+
+// Rows staged from HBM: wave w takes rows w, w + 4, ...; lane l < H/4 the row's columns 4l .. 4l+3, BR rows at a time:
+// ld(r, c4) -> the row's HBM operands (unconditional loads: an unused row reads the block's first row), issued for
+// all BR rows before any is used, so a batch waits out one memory latency, not BR (a load behind a per-row branch, or
+// behind the previous row's stores, waits for everything in flight); val(r, c4, on, aux) -> the row's float4 (0 for
+// unused rows), called by every lane of the wave (it may reduce over the wave) with on = the lane holds columns (c4 is
+// clamped for the others, whose value is dropped); sink(r, c4, v) sees the lane's value (e.g. stores it); the tile
+// gets s_r v and RS[r] = 1 / s_r; stat(r, v, aux) sees every row's value (e.g. accumulates column statistics).
+template <int H, int BR, typename Ld, typename Val, typename Sink, typename Stat = NoStat>
+__device__ __forceinline__ void stage_rows_scaled(const TileX3& X, float* RS, int wave, int lane, Ld ld, Val val, Sink sink,
+                                                  Stat stat = NoStat()) {
     constexpr int L4 = H / 4;
+    static_assert((MROWS / NWAVE) % BR == 0, "whole batches of rows per wave");
     const bool on = lane < L4;
     const int c4 = on ? lane : 0;
-    for (int r = wave; r < MROWS; r += NWAVE) {
-        float4 v = val(r, c4, on);
-        if (!on) v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (on) sink(r, lane, v);
-        const float s = row_scale(wave_max(absmax4(v)));
-        if (on) X.put4(r, 4 * lane, f4_scale(v, s));
-        if (lane == 0) RS[r] = 1.f / s;
+    for (int r0 = wave; r0 < MROWS; r0 += NWAVE * BR) {
+        decltype(ld(0, 0)) aux[BR];
+#pragma unroll
+        for (int u = 0; u < BR; ++u) aux[u] = ld(r0 + u * NWAVE, c4);
+        float4 v[BR];
+        float m[BR];
+#pragma unroll
+        for (int u = 0; u < BR; ++u) {
+            v[u] = val(r0 + u * NWAVE, c4, on, aux[u]);
+            if (!on) v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            stat(r0 + u * NWAVE, v[u], aux[u]);
+            m[u] = absmax4(v[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < BR; ++u) m[u] = wave_max(m[u]);
+#pragma unroll
+        for (int u = 0; u < BR; ++u) {
+            const int r = r0 + u * NWAVE;
+            if (on) sink(r, lane, v[u]);
+            const float s = row_scale(m[u]);
+            if (on) X.put4(r, 4 * lane, f4_scale(v[u], s));
+            if (lane == 0) RS[r] = 1.f / s;
+        }
     }
 }
 
-// Rows staged from a layer's accumulators (acc -> y in place by f(i, n0, acc4) -> float4): per-row max over the
-// four waves through RMX, then the scaled tile.  Contains the barrier between the layer's last tile read and the
-// tile's overwrite.  RS[i] (read by f) is replaced by the new row's 1 / s.
+// the HBM values [RT][CT][4] of a row-major [R, H] array at the lane's accumulator positions (rows of unused tile
+// slots read the block's first row), all loads issued back to back
+template <int H, typename Ok>
+__device__ __forceinline__ void load_acc_rows(const float* __restrict__ src, long row0, Ok okrow, int wave, int lane,
+                                             float4 (&v)[RT][Geo<H>::CT][4]) {
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+        const int i = acc_i(rt, lane);
+        const float* p = src + (row0 + (okrow(i) ? i : 0)) * H;
+#pragma unroll
+        for (int c = 0; c < Geo<H>::CT; ++c)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) v[rt][c][g] = ld4g(p + acc_n0<H>(wave, c, g, lane));
+    }
+}
+
+// Rows staged from a layer's accumulators (acc -> y in place by f(i, n0, acc4, aux4) -> float4, aux: the HBM operand
+// at the same positions, loaded by the caller with load_acc_rows): per-row max over the four waves through RMX, then
+// the scaled tile.  Contains the barrier between the layer's last tile read and the tile's overwrite.  RS[i] (read by
+// f) is replaced by the new row's 1 / s.
 template <int H, typename F>
 __device__ __forceinline__ void stage_acc_scaled(const TileX3& X, f32x16 (&acc)[RT][Geo<H>::CT], float* RS, float* RMX,
-                                                 int wave, int lane, F f) {
+                                                 int wave, int lane, const float4 (&aux)[RT][Geo<H>::CT][4], F f,
+                                                 float4 (&cm)[Geo<H>::CT][4]) {
     constexpr int CT = Geo<H>::CT;
+#pragma unroll
+    for (int c = 0; c < CT; ++c)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) cm[c][g] = make_float4(0.f, 0.f, 0.f, 0.f);
     float mx[RT];
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
@@ -92,7 +196,8 @@ __device__ __forceinline__ void stage_acc_scaled(const TileX3& X, f32x16 (&acc)[
         for (int c = 0; c < CT; ++c)
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-                const float4 y = f(i, acc_n0<H>(wave, c, g, lane), acc4(acc[rt][c], g));
+                const float4 y = f(i, acc_n0<H>(wave, c, g, lane), acc4(acc[rt][c], g), aux[rt][c][g]);
+                cm[c][g] = absmax_acc4(cm[c][g], y);
                 acc[rt][c][4 * g] = y.x; acc[rt][c][4 * g + 1] = y.y;
                 acc[rt][c][4 * g + 2] = y.z; acc[rt][c][4 * g + 3] = y.w;
                 m = fmaxf(m, absmax4(y));
@@ -149,7 +254,7 @@ __global__ __launch_bounds__(NTHR, 2) __attribute__((amdgpu_waves_per_eu(2, 2)))
                          if (i < MU && row0 + i < R) st4g(tr.e1 + (row0 + i) * H + n0, y);
                      });
     __syncthreads();
-    mfma_layer_x3<H, H, true, false>(X, reinterpret_cast<const uint4*>(t.w_e2p), acc, wave, lane);
+    mfma_layer_x3<H, H, true, QS_EMBED_PIN != 0>(X, reinterpret_cast<const uint4*>(t.w_e2p), acc, wave, lane);
     __syncthreads();
     store_tanh_x3<H>(X, acc, 1.f / (X3_SX * X3_SW), wave, lane, [&](int, int n0) { return lds4(BI + H + n0); },
                      [&](int i, int n0, float4 y) {
@@ -301,7 +406,14 @@ constexpr size_t bwd_fixed_lds_bytes() {   // split tile + WT, DW, SC, RS (MROWS
 }
 
 // kernel 1: value chain (dh_pre -> dv1_pre -> de2 part) and attention chain (dscore -> da2_pre -> da1_pre -> de2 part);
-// dynamic LDS: bwd_fixed_lds_bytes<H>() + (MROWS / K) H floats for the block's dout rows
+// dynamic LDS: bwd_fixed_lds_bytes<H>() + max(MROWS / K, 2 NWAVE) H floats (the block's dout rows, then the column
+// statistics' scratch); kernel 2: bwd_fixed_lds_bytes<H>() + NWAVE H floats
+template <int H>
+constexpr size_t bwd1_lds_bytes(int K) {
+    return bwd_fixed_lds_bytes<H>() + (size_t)(MROWS / K > 2 * NWAVE ? MROWS / K : 2 * NWAVE) * H * 4;
+}
+template <int H>
+constexpr size_t bwd2_lds_bytes() { return bwd_fixed_lds_bytes<H>() + (size_t)NWAVE * H * 4; }
 template <int H>
 __global__ __launch_bounds__(NTHR, 2) void attn_bwd1_x3_kernel(int B, int K, Towers tw, Trains trs) {
     constexpr int LDH = GeoX3<H>::LDH, CT = Geo<H>::CT, L4 = H / 4;
@@ -314,7 +426,7 @@ __global__ __launch_bounds__(NTHR, 2) void attn_bwd1_x3_kernel(int B, int K, Tow
     float* RS = SC + MROWS;
     float* RMX = RS + MROWS;
     float* W3 = RMX + NWAVE * MROWS;
-    float* DO = W3 + H;
+    float* DO = W3 + H;   // [max(AB, 8) H]: the block's dout rows (stage 1), then the column statistics' scratch
     const qs_attn_tower& t = tw.t[blockIdx.y];
     const qs_attn_train& tr = trs.t[blockIdx.y];
     const int AB = MROWS / K, MU = AB * K;
@@ -329,11 +441,12 @@ __global__ __launch_bounds__(NTHR, 2) void attn_bwd1_x3_kernel(int B, int K, Tow
     for (int n = tid; n < H; n += NTHR) W3[n] = t.w_a3[n];
     if (tid < MROWS) WT[tid] = okrow(tid) ? tr.w[row0 + tid] : 0.f;
     __syncthreads();
+    float4 cmr = z4, aw = z4;   // column maxima / sum dscore a2 of the lane's columns over the wave's rows
     // dw_j = h_j . dout[a] and dh_pre = w_j dout[a] (1 - h^2): wave-owned rows
-    stage_rows_scaled<H>(X, RS, wave, lane,
-                         [&](int r, int c4, bool on) {
+    auto rowp = [&](const float* a, int r, int c4) { return a + (row0 + (okrow(r) ? r : 0)) * H + 4 * c4; };
+    stage_rows_scaled<H, MROWS / NWAVE>(X, RS, wave, lane, [&](int r, int c4) { return ld4g(rowp(tr.h, r, c4)); },
+                         [&](int r, int c4, bool on, float4 h) {
                              if (!okrow(r)) return z4;
-                             const float4 h = ld4g(tr.h + (row0 + r) * H + 4 * c4);
                              const float4 d = lds4(DO + (r / K) * H + 4 * c4);
                              const float dw = wave_sum(on ? h.x * d.x + h.y * d.y + h.z * d.z + h.w * d.w : 0.f);
                              if (lane == 0) DW[r] = dw;
@@ -341,18 +454,31 @@ __global__ __launch_bounds__(NTHR, 2) void attn_bwd1_x3_kernel(int B, int K, Tow
                          },
                          [&](int r, int c4, float4 v) {
                              if (okrow(r)) st4g(tr.dh_pre + (row0 + r) * H + 4 * c4, v);
-                         });
+                         },
+                         [&](int, float4 v, const float4&) { cmr = absmax_acc4(cmr, v); });
     __syncthreads();
+    // the waves' column maxima of dh_pre into the scratch (dout is no longer read); merged after the next barrier
+    if (lane < L4) *reinterpret_cast<float4*>(DO + wave * H + 4 * lane) = cmr;
+    const size_t nblk = gridDim.x;
+    auto cm_row = [&](int k) { return tr.colmax + ((size_t)k * nblk + blockIdx.x) * H; };
     f32x16 acc[RT][CT];
     constexpr float iSW = 1.f / X3_SW;
     // dv1_pre = (dh_pre W_v2) (1 - v1^2)
+    float4 aux[RT][CT][4];
+    load_acc_rows<H>(tr.v1, row0, okrow, wave, lane, aux);   // in flight during the layer's MFMAs
     mfma_layer_x3<H>(X, reinterpret_cast<const uint4*>(tr.w_v2tp), acc, wave, lane);
-    stage_acc_scaled<H>(X, acc, RS, RMX, wave, lane, [&](int i, int n0, float4 a) {
+    float4 cma[CT][4];
+    stage_acc_scaled<H>(X, acc, RS, RMX, wave, lane, aux, [&](int i, int n0, float4 a, float4 v1) {
         if (!okrow(i)) return z4;
-        const float4 y = f4_dtanh(f4_scale(a, RS[i] * iSW), ld4g(tr.v1 + (row0 + i) * H + n0));
+        const float4 y = f4_dtanh(f4_scale(a, RS[i] * iSW), v1);
         st4g(tr.dv1_pre + (row0 + i) * H + n0, y);
         return y;
-    });
+    }, cma);
+    if (tr.colmax) {
+        colmax_store_acc<H>(cm_row(1), cma, wave, lane);
+        for (int n = tid; n < H; n += NTHR)
+            cm_row(0)[n] = fmaxf(fmaxf(DO[n], DO[H + n]), fmaxf(DO[2 * H + n], DO[3 * H + n]));
+    }
     __syncthreads();
     // de2p = dv1_pre W_v1 + (the attention chain's part, below): the value part stays in registers until then, so
     // de2p is written once (a store, reload and store of 1.6 GB per tower before)
@@ -378,25 +504,43 @@ __global__ __launch_bounds__(NTHR, 2) void attn_bwd1_x3_kernel(int B, int K, Tow
         if (okrow(tid)) tr.dscore[row0 + tid] = ds;
     }
     __syncthreads();   // SC complete; every wave has read the tile and RS
+    cmr = z4;
     // da2_pre = dscore_j w3 (1 - a2^2)
-    stage_rows_scaled<H>(X, RS, wave, lane,
-                         [&](int r, int c4, bool) {
+    stage_rows_scaled<H, QS_BWD1_BR2>(X, RS, wave, lane, [&](int r, int c4) { return ld4g(rowp(tr.a2, r, c4)); },
+                         [&](int r, int c4, bool, float4 a2) {
                              if (!okrow(r)) return z4;
-                             const float4 a2 = ld4g(tr.a2 + (row0 + r) * H + 4 * c4);
                              return f4_dtanh(f4_scale(lds4(W3 + 4 * c4), SC[r]), a2);
                          },
                          [&](int r, int c4, float4 v) {
                              if (okrow(r)) st4g(tr.da2_pre + (row0 + r) * H + 4 * c4, v);
+                         },
+                         [&](int r, float4 v, const float4& a2) {
+                             cmr = absmax_acc4(cmr, v);
+                             aw = f4_add(aw, f4_scale(a2, SC[r]));   // SC = 0 on unused rows
                          });
+    if (lane < L4) {   // the scratch was last read before the dscore barrier
+        *reinterpret_cast<float4*>(DO + wave * H + 4 * lane) = cmr;
+        *reinterpret_cast<float4*>(DO + (NWAVE + wave) * H + 4 * lane) = aw;
+    }
     __syncthreads();
     // da1_pre = (da2_pre W_a2) (1 - a1^2)
     mfma_layer_x3<H>(X, reinterpret_cast<const uint4*>(tr.w_a2tp), acc, wave, lane);
-    stage_acc_scaled<H>(X, acc, RS, RMX, wave, lane, [&](int i, int n0, float4 a) {
+    load_acc_rows<H>(tr.a1, row0, okrow, wave, lane, aux);   // after the layer (de2p's value part holds 64 VGPRs)
+    stage_acc_scaled<H>(X, acc, RS, RMX, wave, lane, aux, [&](int i, int n0, float4 a, float4 a1) {
         if (!okrow(i)) return z4;
-        const float4 y = f4_dtanh(f4_scale(a, RS[i] * iSW), ld4g(tr.a1 + (row0 + i) * H + n0));
+        const float4 y = f4_dtanh(f4_scale(a, RS[i] * iSW), a1);
         st4g(tr.da1_pre + (row0 + i) * H + n0, y);
         return y;
-    });
+    }, cma);
+    if (tr.colmax) {
+        colmax_store_acc<H>(cm_row(3), cma, wave, lane);
+        for (int n = tid; n < H; n += NTHR)
+            cm_row(2)[n] = fmaxf(fmaxf(DO[n], DO[H + n]), fmaxf(DO[2 * H + n], DO[3 * H + n]));
+    }
+    if (tr.a3w_part)
+        for (int n = tid; n < H; n += NTHR)
+            tr.a3w_part[(size_t)blockIdx.x * H + n] =
+                (DO[NWAVE * H + n] + DO[(NWAVE + 1) * H + n]) + (DO[(NWAVE + 2) * H + n] + DO[(NWAVE + 3) * H + n]);
     __syncthreads();
     // de2p += da1_pre A_e
     mfma_layer_x3<H>(X, reinterpret_cast<const uint4*>(tr.w_a1etp), acc, wave, lane);
@@ -423,6 +567,7 @@ __global__ __launch_bounds__(NTHR, 2) void attn_bwd2_x3_kernel(int B, int K, Tow
     const TileX3 X{xh, xh + MROWS * LDH, LDH};
     float* RS = reinterpret_cast<float*>(xh + 2 * MROWS * LDH);
     float* RMX = RS + MROWS;
+    float* SCR = RMX + NWAVE * MROWS;   // [NWAVE][H] the waves' column maxima of de2_pre
     const qs_attn_tower& t = tw.t[blockIdx.y];
     const qs_attn_train& tr = trs.t[blockIdx.y];
     const int AB = MROWS / K, MU = AB * K;
@@ -431,21 +576,40 @@ __global__ __launch_bounds__(NTHR, 2) void attn_bwd2_x3_kernel(int B, int K, Tow
     auto okrow = [&](int i) { return i < MU && row0 + i < R; };
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
     const float invK = 1.f / (float)K;
-    stage_rows_scaled<H>(X, RS, wave, lane,
-                         [&](int r, int c4, bool) {
-                             if (!okrow(r)) return z4;
-                             const long j = row0 + r;
-                             const float4 g = f4_add(ld4g(tr.de2p + j * H + 4 * c4),
-                                                     f4_scale(ld4g(tr.dem + (j / K) * H + 4 * c4), invK));
-                             return f4_dtanh(g, ld4g(t.e2 + j * H + 4 * c4));
-                         },
-                         [&](int r, int c4, float4 v) {
-                             if (okrow(r)) st4g(tr.de2_pre + (row0 + r) * H + 4 * c4, v);
-                         });
+    float4 cmr = z4;   // column maxima of de2_pre over the wave's rows
+    struct Ops {
+        float4 g, m, e;
+    };
+    stage_rows_scaled<H, 8>(X, RS, wave, lane,
+                            [&](int r, int c4) {
+                                const long j = row0 + (okrow(r) ? r : 0);
+                                return Ops{ld4g(tr.de2p + j * H + 4 * c4), ld4g(tr.dem + (j / K) * H + 4 * c4),
+                                           ld4g(t.e2 + j * H + 4 * c4)};
+                            },
+                            [&](int r, int, bool, const Ops& o) {
+                                if (!okrow(r)) return z4;
+                                return f4_dtanh(f4_add(o.g, f4_scale(o.m, invK)), o.e);
+                            },
+                            [&](int r, int c4, float4 v) {
+                                if (okrow(r)) st4g(tr.de2_pre + (row0 + r) * H + 4 * c4, v);
+                            },
+                            [&](int, float4 v, const Ops&) { cmr = absmax_acc4(cmr, v); });
+    if (lane < H / 4) *reinterpret_cast<float4*>(SCR + wave * H + 4 * lane) = cmr;
     __syncthreads();
+    if (tr.colmax)
+        for (int n = tid; n < H; n += NTHR)
+            tr.colmax[((size_t)4 * gridDim.x + blockIdx.x) * H + n] =
+                fmaxf(fmaxf(SCR[n], SCR[H + n]), fmaxf(SCR[2 * H + n], SCR[3 * H + n]));
     f32x16 acc[RT][CT];
     constexpr float iSW = 1.f / X3_SW;
+    float4 e1[RT][CT][4];
+    load_acc_rows<H>(tr.e1, row0, okrow, wave, lane, e1);   // in flight during the layer's MFMAs
     mfma_layer_x3<H>(X, reinterpret_cast<const uint4*>(tr.w_e2tp), acc, wave, lane);
+    float4 cma[CT][4];
+#pragma unroll
+    for (int c = 0; c < CT; ++c)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) cma[c][g] = z4;
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
         const int i = acc_i(rt, lane);
@@ -455,11 +619,12 @@ __global__ __launch_bounds__(NTHR, 2) void attn_bwd2_x3_kernel(int B, int K, Tow
         for (int c = 0; c < CT; ++c)
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-                const int n0 = acc_n0<H>(wave, c, g, lane);
-                st4g(tr.de1_pre + (row0 + i) * H + n0,
-                     f4_dtanh(f4_scale(acc4(acc[rt][c], g), sc), ld4g(tr.e1 + (row0 + i) * H + n0)));
+                const float4 y = f4_dtanh(f4_scale(acc4(acc[rt][c], g), sc), e1[rt][c][g]);
+                st4g(tr.de1_pre + (row0 + i) * H + acc_n0<H>(wave, c, g, lane), y);
+                cma[c][g] = absmax_acc4(cma[c][g], y);
             }
     }
+    if (tr.colmax) colmax_store_acc<H>(tr.colmax + ((size_t)5 * gridDim.x + blockIdx.x) * H, cma, wave, lane);
     (void)RMX;
 }
 
@@ -489,7 +654,7 @@ constexpr size_t dw_lds_bytes() { return (size_t)2 * 4 * H * DW_LDR * 2; }   // 
 template <int H>
 __global__ __launch_bounds__(NTHR, 1) void dw_x3_kernel(const float* __restrict__ G, const float* __restrict__ A,
                                                         const float* __restrict__ gs, long R, int steps_per_block,
-                                                        float* __restrict__ part) {
+                                                        float* __restrict__ part, float* __restrict__ part_sum) {
     constexpr int NT = H / 128, KT = H / 32, TPC = NTHR / H, RPT = DW_STEP / TPC;   // threads per column, rows each
     static_assert(RPT % 8 == 0, "a thread's rows leave as whole 8-row (16-byte) groups");
     extern __shared__ float4 smem4[];
@@ -500,6 +665,7 @@ __global__ __launch_bounds__(NTHR, 1) void dw_x3_kernel(const float* __restrict_
     auto buf = [&](int b, int which) { return lds + ((size_t)b * 4 + which) * H * DW_LDR; };   // 0 Gh 1 Gl 2 Ah 3 Al
     const float sg = gs[sc];
     float gv[RPT], av[RPT];
+    float csum = 0.f;   // the column's sum over the part's rows (the bias gradient's part; rows in order)
     auto load = [&](int s) {
 #pragma unroll
         for (int u = 0; u < RPT; ++u) {
@@ -517,6 +683,7 @@ __global__ __launch_bounds__(NTHR, 1) void dw_x3_kernel(const float* __restrict_
             f16x8 gh, gl, ah, al;
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
+                csum += gv[o + u];
                 const float g = sg * gv[o + u], a = X3_SX * av[o + u];
                 gh[u] = (_Float16)g;
                 gl[u] = (_Float16)(g - (float)gh[u]);
@@ -573,6 +740,17 @@ __global__ __launch_bounds__(NTHR, 1) void dw_x3_kernel(const float* __restrict_
         if (s + 1 < steps_per_block) stage(b ^ 1);   // the other buffer: last read two steps ago (barrier below)
         __syncthreads();
     }
+    if (part_sum) {   // the TPC threads of a column through LDS (the staging buffers are free after the loop's barrier)
+        float* cs = reinterpret_cast<float*>(smem4);
+        cs[tid] = csum;
+        __syncthreads();
+        if (tid < H) {
+            float v = cs[tid];
+#pragma unroll
+            for (int q = 1; q < TPC; ++q) v += cs[q * H + tid];
+            part_sum[(size_t)blockIdx.x * H + tid] = v;
+        }
+    }
     // acc[t][k] register 4g + j: output row n = (wave NT + t) 32 + (lane & 31), column k 32 + 8 g + 4 (lane >> 5) + j
     float* out = part + (size_t)blockIdx.x * H * H;
 #pragma unroll
@@ -588,6 +766,136 @@ __global__ __launch_bounds__(NTHR, 1) void dw_x3_kernel(const float* __restrict_
                     make_float4(acc[t][k][4 * g] * inv, acc[t][k][4 * g + 1] * inv, acc[t][k][4 * g + 2] * inv,
                                 acc[t][k][4 * g + 3] * inv);
             }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------------------------
+// layer 0's weight gradient (qs_attn_dw0_x3): part[b] = G[rows of b]^T X[rows of b], X the layer-0 input rows
+// gathered from the observations (row r = agent r / K, slot r % K: [nbr (nd) | self of agent r % B (so) | 0], KD0 = 32
+// columns -- the forward's gather_rows0), G = de1_pre [R, H] with its column scales gs (|G[:, n]| gs[n] < 2^14), X at
+// the forward's layer-0 scale X3_SIN; the column sums of G (the bias gradient's parts) from the same pass.  The
+// structure of dw_x3_kernel with A = the gathered X: 16-row steps, G's tile and X's 32 columns staged transposed as
+// f16 hi / lo, double-buffered; per wave NT 32 x 32 output tiles (rows n of the wave's range, the 32 X columns).
+// ------------------------------------------------------------------------------------------------------------------
+template <int H>
+constexpr size_t dw0_lds_bytes() { return (size_t)2 * (2 * H + 2 * KD0) * DW_LDR * 2; }
+
+template <int H>
+__global__ __launch_bounds__(NTHR, 2) void dw0_x3_kernel(const float* __restrict__ G, const float* __restrict__ gs,
+                                                         const float* __restrict__ obs, int stride, int so, int off,
+                                                         int B, int K, int nd, long R, int steps_per_block,
+                                                         float* __restrict__ part, float* __restrict__ part_sum) {
+    constexpr int NT = H / 128, TPC = NTHR / H, RPT = DW_STEP / TPC;
+    constexpr int XR = DW_STEP * KD0 / NTHR;   // X values per thread and step (2): column tid % KD0, consecutive rows
+    static_assert(RPT % 8 == 0 && XR == 2, "staging shapes");
+    extern __shared__ float4 smem4[];
+    _Float16* lds = reinterpret_cast<_Float16*>(smem4);
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int sc = tid % H, sr = (tid / H) * RPT;
+    const int xc = tid % KD0, xr = (tid / KD0) * XR;
+    const long r_begin = (long)blockIdx.x * steps_per_block * DW_STEP;
+    constexpr size_t BUF = (size_t)(2 * H + 2 * KD0) * DW_LDR;   // halves per buffer: Gh, Gl [H][24], Xh, Xl [32][24]
+    auto gbuf = [&](int b, int which) { return lds + b * BUF + (size_t)which * H * DW_LDR; };
+    auto xbuf = [&](int b, int which) { return lds + b * BUF + (size_t)2 * H * DW_LDR + (size_t)which * KD0 * DW_LDR; };
+    const float sg = gs[sc];
+    float gv[RPT], xv[XR];
+    float csum = 0.f;
+    auto load = [&](int s) {
+#pragma unroll
+        for (int u = 0; u < RPT; ++u) {
+            const long r = r_begin + (long)s * DW_STEP + sr + u;
+            const bool ok = r < R && s < steps_per_block;
+            gv[u] = G[(ok ? r : 0) * H + sc] * (ok ? 1.f : 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < XR; ++u) {   // gather_rows0's indexing (unconditional loads, zeroed by a product)
+            const long r = r_begin + (long)s * DW_STEP + xr + u;
+            const bool ok = r < R && s < steps_per_block && xc < nd + so;
+            const long j = ok ? r : 0;
+            const long a = j / K;
+            const long idx = xc < nd ? a * stride + off + (j - a * K) * nd + xc : (j % B) * stride + (xc < nd + so ? xc - nd : 0);
+            xv[u] = obs[idx] * (ok ? 1.f : 0.f);
+        }
+    };
+    auto stage = [&](int b) {
+#pragma unroll
+        for (int o = 0; o < RPT; o += 8) {
+            f16x8 gh, gl;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                csum += gv[o + u];
+                const float g = sg * gv[o + u];
+                gh[u] = (_Float16)g;
+                gl[u] = (_Float16)(g - (float)gh[u]);
+            }
+            const int off8 = sc * DW_LDR + sr + o;
+            *reinterpret_cast<f16x8*>(gbuf(b, 0) + off8) = gh;
+            *reinterpret_cast<f16x8*>(gbuf(b, 1) + off8) = gl;
+        }
+        typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+        f16x2 h2, l2;
+#pragma unroll
+        for (int u = 0; u < XR; ++u) {
+            const float x = X3_SIN * xv[u];
+            h2[u] = (_Float16)x;
+            l2[u] = (_Float16)(x - (float)h2[u]);
+        }
+        *reinterpret_cast<f16x2*>(xbuf(b, 0) + xc * DW_LDR + xr) = h2;
+        *reinterpret_cast<f16x2*>(xbuf(b, 1) + xc * DW_LDR + xr) = l2;
+    };
+    f32x16 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+    const int aoff = (lane & 31) * DW_LDR + (lane >> 5) * 8;
+    load(0);
+    stage(0);
+    __syncthreads();
+    for (int s = 0; s < steps_per_block; ++s) {
+        const int b = s & 1;
+        if (s + 1 < steps_per_block) load(s + 1);
+        f16x8 gh[NT], gl[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const int n0 = (wave * NT + t) * 32;
+            gh[t] = *reinterpret_cast<const f16x8*>(gbuf(b, 0) + n0 * DW_LDR + aoff);
+            gl[t] = *reinterpret_cast<const f16x8*>(gbuf(b, 1) + n0 * DW_LDR + aoff);
+        }
+        const f16x8 xh = *reinterpret_cast<const f16x8*>(xbuf(b, 0) + aoff);
+        const f16x8 xl = *reinterpret_cast<const f16x8*>(xbuf(b, 1) + aoff);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, gh[t], acc[t], 0, 0, 0);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, gl[t], acc[t], 0, 0, 0);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xl, gh[t], acc[t], 0, 0, 0);
+        if (s + 1 < steps_per_block) stage(b ^ 1);
+        __syncthreads();
+    }
+    if (part_sum) {
+        float* cs = reinterpret_cast<float*>(smem4);
+        cs[tid] = csum;
+        __syncthreads();
+        if (tid < H) {
+            float v = cs[tid];
+#pragma unroll
+            for (int q = 1; q < TPC; ++q) v += cs[q * H + tid];
+            part_sum[(size_t)blockIdx.x * H + tid] = v;
+        }
+    }
+    // acc[t] register 4g + j: output row n = (wave NT + t) 32 + (lane & 31), X column 8 g + 4 (lane >> 5) + j
+    float* out = part + (size_t)blockIdx.x * H * KD0;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const int n = (wave * NT + t) * 32 + (lane & 31);
+        const float inv = 1.f / (gs[n] * X3_SIN);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int col = 8 * g + 4 * (lane >> 5);
+            *reinterpret_cast<float4*>(out + (size_t)n * KD0 + col) =
+                make_float4(acc[t][4 * g] * inv, acc[t][4 * g + 1] * inv, acc[t][4 * g + 2] * inv, acc[t][4 * g + 3] * inv);
+        }
     }
 }
 

@@ -26,6 +26,10 @@ namespace pol {
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
+#ifndef QS_EMBED_PIN
+#define QS_EMBED_PIN 1   // the embed kernels' H x H layer with the scheduling fences of mfma_layer_x3 (PIN)
+#endif
+
 constexpr float X3_SX = 256.f;        // activation scale (tanh outputs, e2 rows)
 constexpr float X3_SIN = 16.f;        // raw observation scale (layer 0 inputs)
 constexpr float X3_SW = 256.f;        // weight scale (policy_fused.pack_mfma_weight_x3)
@@ -201,7 +205,7 @@ __global__ __launch_bounds__(NTHR, 2) __attribute__((amdgpu_waves_per_eu(2, 2)))
         return (i < MU && row0 + i < R) ? lds4(BI + n0) : make_float4(0.f, 0.f, 0.f, 0.f);
     });
     __syncthreads();
-    mfma_layer_x3<H, H, true, false>(X, reinterpret_cast<const uint4*>(t.w_e2p), acc, wave, lane);
+    mfma_layer_x3<H, H, true, QS_EMBED_PIN != 0>(X, reinterpret_cast<const uint4*>(t.w_e2p), acc, wave, lane);
     __syncthreads();   // every wave has read the tile
     // e2 to HBM straight from the epilogue (fp32 tanh values; the pool's split of them is the tile's hi / lo, so
     // its products are the same) -- no read-back of the split tile

@@ -38,10 +38,8 @@
 #include "qs_flavor_a.h"
 #include "qs_gae.h"
 #include "qs_curriculum.h"
-#include "qs_policy_train.h"
-#include "qs_policy.h"
-#include "qs_policy_x3.h"
 #include "qs_replay.h"
+#include "qs_error.h"
 
 // =============================================================================================
 // C ABI
@@ -74,10 +72,11 @@ static hipError_t use_device(const qs_handle* h) {
     return hipSetDevice(h->device);
 }
 
-static int fail(int code, const std::string& msg) {
+int qs_fail(int code, const std::string& msg) {
     g_err = msg;
     return code;
 }
+static int fail(int code, const std::string& msg) { return qs_fail(code, msg); }
 
 #define QS_HIP(call)                                                                              \
     do {                                                                                          \
@@ -1063,239 +1062,6 @@ extern "C" int qs_curriculum_step_all(qs_handle* h, const uint8_t* d_reset_all, 
                        cap, (int)n_all, (int)h->cfg.num_envs, d_cur);
     QS_HIP(hipGetLastError());
     return QS_OK;
-}
-
-// fused attention-encoder forward (qs_policy.h)
-static int attn_check(int32_t B, int32_t K, int32_t H, const qs_attn_tower* towers, int32_t n_towers) {
-    if (!towers) return fail(QS_E_INVALID, "NULL towers");
-    if (n_towers < 1 || n_towers > QS_ATTN_MAX_TOWERS) return fail(QS_E_INVALID, "n_towers must be 1 or 2");
-    if (H != 128 && H != 256) return fail(QS_E_INVALID, "attention hidden size must be 128 or 256");
-    if (K < 1 || K > qs::pol::MROWS) return fail(QS_E_INVALID, "neighbours per agent must be 1..64");
-    if (B < 1) return fail(QS_E_INVALID, "B must be >= 1");
-    if ((long long)B * K * H >= (1ll << 31)) return fail(QS_E_INVALID, "B * K * H must stay below 2^31");
-    return QS_OK;
-}
-template <int H>
-static int attn_launch(bool embed, const float* obs, int32_t stride, int32_t so, int32_t off, int32_t B, int32_t K,
-                       int32_t nd, const qs::pol::Towers& tw, int32_t n_towers, hipStream_t st, bool x3 = false) {
-    const int mu = (qs::pol::MROWS / K) * K;
-    const dim3 grid((unsigned)(((long long)B * K + mu - 1) / mu), (unsigned)n_towers), block(qs::pol::NTHR);
-    if (x3) {   // the split-f16 contraction (qs_policy_x3.h)
-        if (embed) {
-            const size_t lds = qs::pol::embed_x3_lds_bytes<H>();
-            QS_HIP(hipFuncSetAttribute((const void*)qs::pol::attn_embed_x3_kernel<H>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-            hipLaunchKernelGGL(qs::pol::attn_embed_x3_kernel<H>, grid, block, lds, st, obs, stride, so, off, B, K, nd, tw);
-        } else {
-            const size_t lds = qs::pol::pool_x3_lds_bytes<H>();
-            QS_HIP(hipFuncSetAttribute((const void*)qs::pol::attn_pool_x3_kernel<H>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-            hipLaunchKernelGGL(qs::pol::attn_pool_x3_kernel<H>, grid, block, lds, st, B, K, tw);
-        }
-        QS_HIP(hipGetLastError());
-        return QS_OK;
-    }
-    if (embed) {
-        const size_t lds = qs::pol::embed_lds_bytes<H>();
-        QS_HIP(hipFuncSetAttribute((const void*)qs::pol::attn_embed_kernel<H>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL(qs::pol::attn_embed_kernel<H>, grid, block, lds, st, obs, stride, so, off, B, K, nd, tw);
-    } else {
-        const size_t lds = qs::pol::pool_lds_bytes<H>();
-        QS_HIP(hipFuncSetAttribute((const void*)qs::pol::attn_pool_kernel<H>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL(qs::pol::attn_pool_kernel<H>, grid, block, lds, st, B, K, tw);
-    }
-    QS_HIP(hipGetLastError());
-    return QS_OK;
-}
-static int attn_embed_impl(const float* obs, int32_t obs_stride, int32_t self_dim, int32_t nbr_off, int32_t B,
-                           int32_t K, int32_t nd, int32_t H, const qs_attn_tower* towers, int32_t n_towers,
-                           void* stream, bool x3) {
-    int rc = attn_check(B, K, H, towers, n_towers);
-    if (rc) return rc;
-    if (!obs) return fail(QS_E_INVALID, "NULL obs");
-    if (nd < 1 || nd > qs::pol::MAX_ND) return fail(QS_E_INVALID, "features per neighbour must be 1..16");
-    if (self_dim < 1 || self_dim > obs_stride) return fail(QS_E_INVALID, "self features must lie inside the obs row");
-    if (nd + self_dim > qs::pol::KD0) return fail(QS_E_INVALID, "self + neighbour features must be <= 32");
-    if (nbr_off < 0 || nbr_off + K * nd > obs_stride) return fail(QS_E_INVALID, "neighbour block outside the obs row");
-    qs::pol::Towers tw{};
-    for (int i = 0; i < n_towers; ++i) {
-        const qs_attn_tower& t = towers[i];
-        if (!t.w_e1p || !t.b_e1 || !t.w_e2p || !t.b_e2 || !t.e2 || !t.e_mean)
-            return fail(QS_E_INVALID, "NULL stage-1 tower pointer");
-        tw.t[i] = t;
-    }
-    hipStream_t st = (hipStream_t)stream;
-    return H == 256 ? attn_launch<256>(true, obs, obs_stride, self_dim, nbr_off, B, K, nd, tw, n_towers, st, x3)
-                    : attn_launch<128>(true, obs, obs_stride, self_dim, nbr_off, B, K, nd, tw, n_towers, st, x3);
-}
-extern "C" int qs_attn_embed(const float* obs, int32_t obs_stride, int32_t self_dim, int32_t nbr_off, int32_t B,
-                             int32_t K, int32_t nd, int32_t H, const qs_attn_tower* towers, int32_t n_towers,
-                             void* stream) {
-    return attn_embed_impl(obs, obs_stride, self_dim, nbr_off, B, K, nd, H, towers, n_towers, stream, false);
-}
-extern "C" int qs_attn_embed_x3(const float* obs, int32_t obs_stride, int32_t self_dim, int32_t nbr_off, int32_t B,
-                                int32_t K, int32_t nd, int32_t H, const qs_attn_tower* towers, int32_t n_towers,
-                                void* stream) {
-    return attn_embed_impl(obs, obs_stride, self_dim, nbr_off, B, K, nd, H, towers, n_towers, stream, true);
-}
-static int attn_pool_impl(int32_t B, int32_t K, int32_t H, const qs_attn_tower* towers, int32_t n_towers,
-                          void* stream, bool x3) {
-    int rc = attn_check(B, K, H, towers, n_towers);
-    if (rc) return rc;
-    qs::pol::Towers tw{};
-    for (int i = 0; i < n_towers; ++i) {
-        const qs_attn_tower& t = towers[i];
-        if (!t.e2 || !t.P || !t.w_v1p || !t.b_v1 || !t.w_v2p || !t.b_v2 || !t.w_a1ep || !t.w_a2p || !t.b_a2 ||
-            !t.w_a3 || !t.out)
-            return fail(QS_E_INVALID, "NULL stage-2 tower pointer");
-        tw.t[i] = t;
-    }
-    return H == 256 ? attn_launch<256>(false, nullptr, 0, 0, 0, B, K, 0, tw, n_towers, (hipStream_t)stream, x3)
-                    : attn_launch<128>(false, nullptr, 0, 0, 0, B, K, 0, tw, n_towers, (hipStream_t)stream, x3);
-}
-extern "C" int qs_attn_pool(int32_t B, int32_t K, int32_t H, const qs_attn_tower* towers, int32_t n_towers,
-                            void* stream) {
-    return attn_pool_impl(B, K, H, towers, n_towers, stream, false);
-}
-extern "C" int qs_attn_pool_x3(int32_t B, int32_t K, int32_t H, const qs_attn_tower* towers, int32_t n_towers,
-                               void* stream) {
-    return attn_pool_impl(B, K, H, towers, n_towers, stream, true);
-}
-
-// the PPO update's attention encoder (qs_policy_train.h)
-enum { TR_EMBED, TR_POOL, TR_BWD1, TR_BWD2 };
-template <int H>
-static int attn_train_launch(int what, const float* obs, int32_t stride, int32_t so, int32_t off, int32_t B, int32_t K,
-                             int32_t nd, const qs::pol::Towers& tw, const qs::pol::Trains& trs, int32_t n_towers,
-                             hipStream_t st) {
-    namespace P = qs::pol;
-    const int mu = (P::MROWS / K) * K;
-    const dim3 grid((unsigned)(((long long)B * K + mu - 1) / mu), (unsigned)n_towers), block(P::NTHR);
-    size_t lds = 0;
-    const void* fn = nullptr;
-    switch (what) {
-        case TR_EMBED: lds = P::embed_x3_lds_bytes<H>(); fn = (const void*)P::attn_embed_train_x3_kernel<H>; break;
-        case TR_POOL: lds = P::pool_x3_lds_bytes<H>(); fn = (const void*)P::attn_pool_train_x3_kernel<H>; break;
-        case TR_BWD1: lds = P::bwd_fixed_lds_bytes<H>() + (size_t)(P::MROWS / K) * H * 4; fn = (const void*)P::attn_bwd1_x3_kernel<H>; break;
-        default: lds = P::bwd_fixed_lds_bytes<H>(); fn = (const void*)P::attn_bwd2_x3_kernel<H>; break;
-    }
-    QS_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    switch (what) {
-        case TR_EMBED:
-            hipLaunchKernelGGL(P::attn_embed_train_x3_kernel<H>, grid, block, lds, st, obs, stride, so, off, B, K, nd, tw, trs);
-            break;
-        case TR_POOL: hipLaunchKernelGGL(P::attn_pool_train_x3_kernel<H>, grid, block, lds, st, B, K, tw, trs); break;
-        case TR_BWD1: hipLaunchKernelGGL(P::attn_bwd1_x3_kernel<H>, grid, block, lds, st, B, K, tw, trs); break;
-        default: hipLaunchKernelGGL(P::attn_bwd2_x3_kernel<H>, grid, block, lds, st, B, K, tw, trs); break;
-    }
-    QS_HIP(hipGetLastError());
-    return QS_OK;
-}
-static int attn_train_impl(int what, const float* obs, int32_t stride, int32_t so, int32_t off, int32_t B, int32_t K,
-                           int32_t nd, int32_t H, const qs_attn_tower* towers, const qs_attn_train* trains,
-                           int32_t n_towers, void* stream) {
-    int rc = attn_check(B, K, H, towers, n_towers);
-    if (rc) return rc;
-    if (!trains) return fail(QS_E_INVALID, "NULL trains");
-    if (what == TR_EMBED) {
-        if (!obs) return fail(QS_E_INVALID, "NULL obs");
-        if (nd < 1 || nd > qs::pol::MAX_ND) return fail(QS_E_INVALID, "features per neighbour must be 1..16");
-        if (so < 1 || so > stride) return fail(QS_E_INVALID, "self features must lie inside the obs row");
-        if (nd + so > qs::pol::KD0) return fail(QS_E_INVALID, "self + neighbour features must be <= 32");
-        if (off < 0 || off + K * nd > stride) return fail(QS_E_INVALID, "neighbour block outside the obs row");
-    }
-    qs::pol::Towers tw{};
-    qs::pol::Trains trs{};
-    for (int i = 0; i < n_towers; ++i) {
-        const qs_attn_tower& t = towers[i];
-        const qs_attn_train& r = trains[i];
-        bool ok = true;
-        switch (what) {
-            case TR_EMBED: ok = t.w_e1p && t.b_e1 && t.w_e2p && t.b_e2 && t.e2 && t.e_mean && r.e1; break;
-            case TR_POOL:
-                ok = t.e2 && t.P && t.w_v1p && t.b_v1 && t.w_v2p && t.b_v2 && t.w_a1ep && t.w_a2p && t.b_a2 && t.w_a3 &&
-                     t.out && r.a1 && r.a2 && r.v1 && r.h && r.w;
-                break;
-            case TR_BWD1:
-                ok = t.w_a3 && r.w && r.h && r.v1 && r.a1 && r.a2 && r.dout && r.w_v2tp && r.w_v1tp && r.w_a2tp &&
-                     r.w_a1etp && r.dh_pre && r.dv1_pre && r.da2_pre && r.da1_pre && r.dscore && r.de2p;
-                break;
-            default: ok = t.e2 && r.e1 && r.de2p && r.dem && r.w_e2tp && r.de2_pre && r.de1_pre; break;
-        }
-        if (!ok) return fail(QS_E_INVALID, "NULL tower / train pointer for this stage");
-        tw.t[i] = t;
-        trs.t[i] = r;
-    }
-    hipStream_t st = (hipStream_t)stream;
-    return H == 256 ? attn_train_launch<256>(what, obs, stride, so, off, B, K, nd, tw, trs, n_towers, st)
-                    : attn_train_launch<128>(what, obs, stride, so, off, B, K, nd, tw, trs, n_towers, st);
-}
-extern "C" int qs_attn_embed_train_x3(const float* obs, int32_t obs_stride, int32_t self_dim, int32_t nbr_off, int32_t B,
-                                      int32_t K, int32_t nd, int32_t H, const qs_attn_tower* towers,
-                                      const qs_attn_train* trains, int32_t n_towers, void* stream) {
-    return attn_train_impl(TR_EMBED, obs, obs_stride, self_dim, nbr_off, B, K, nd, H, towers, trains, n_towers, stream);
-}
-extern "C" int qs_attn_pool_train_x3(int32_t B, int32_t K, int32_t H, const qs_attn_tower* towers,
-                                     const qs_attn_train* trains, int32_t n_towers, void* stream) {
-    return attn_train_impl(TR_POOL, nullptr, 0, 0, 0, B, K, 0, H, towers, trains, n_towers, stream);
-}
-extern "C" int qs_attn_bwd1_x3(int32_t B, int32_t K, int32_t H, const qs_attn_tower* towers,
-                               const qs_attn_train* trains, int32_t n_towers, void* stream) {
-    return attn_train_impl(TR_BWD1, nullptr, 0, 0, 0, B, K, 0, H, towers, trains, n_towers, stream);
-}
-template <int H>
-static int dw_launch(const float* G, const float* A, const float* gs, int64_t R, float* part, int32_t n_parts,
-                     hipStream_t st) {
-    namespace P = qs::pol;
-    const long long rows_per = (R + n_parts - 1) / n_parts;
-    const int steps = (int)((rows_per + P::DW_STEP - 1) / P::DW_STEP);
-    const size_t lds = P::dw_lds_bytes<H>();
-    QS_HIP(hipFuncSetAttribute((const void*)P::dw_x3_kernel<H>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(P::dw_x3_kernel<H>, dim3((unsigned)n_parts), dim3(P::NTHR), lds, st, G, A, gs, (long)R, steps, part);
-    QS_HIP(hipGetLastError());
-    return QS_OK;
-}
-extern "C" int qs_attn_dw_x3(const float* G, const float* A, const float* col_scale, int64_t R, int32_t H, float* part,
-                             int32_t n_parts, void* stream) {
-    if (!G || !A || !col_scale || !part) return fail(QS_E_INVALID, "NULL argument");
-    if (H != 128 && H != 256) return fail(QS_E_INVALID, "hidden size must be 128 or 256");
-    if (R < 1 || n_parts < 1 || n_parts > 65535 || R * (int64_t)H >= (1ll << 40))
-        return fail(QS_E_INVALID, "R >= 1, 1 <= n_parts <= 65535");
-    hipStream_t st = (hipStream_t)stream;
-    return H == 256 ? dw_launch<256>(G, A, col_scale, R, part, n_parts, st) : dw_launch<128>(G, A, col_scale, R, part, n_parts, st);
-}
-extern "C" int qs_colstats(const float* G, int64_t R, int32_t H, const float* row_w, const float* obs, int32_t stride,
-                           int32_t nbr_off, int32_t B, int32_t K, int32_t nd, int32_t nx, float* pmx, float* psm,
-                           float* px, int32_t n_parts, void* stream) {
-    namespace P = qs::pol;
-    if (!G || !pmx || !psm) return fail(QS_E_INVALID, "NULL argument");
-    if (H != 128 && H != 256) return fail(QS_E_INVALID, "hidden size must be 128 or 256");
-    if (R < 1 || n_parts < 1 || n_parts > (1 << 24) || R * (int64_t)H >= (1ll << 40))
-        return fail(QS_E_INVALID, "R >= 1, 1 <= n_parts <= 2^24");
-    if (nx < 0 || nx > QS_COLSTATS_MAX_X) return fail(QS_E_INVALID, "nx out of range");
-    if (nx > 0 && (!obs || !px || B < 1 || K < 1 || nd < 0 || nd > nx || (int64_t)B * K != R || R >= (1ll << 31) ||
-                   stride < nx ||
-                   nbr_off < 0 || nbr_off + (int64_t)K * nd > stride))
-        return fail(QS_E_INVALID, "layer-0 input: obs, part_x, B K = R, nd <= nx, the neighbour block inside a row");
-    hipStream_t st = (hipStream_t)stream;
-    const long rows_per = (long)((R + n_parts - 1) / n_parts);
-    if (nx > 8)
-        hipLaunchKernelGGL(P::colstats_kernel<QS_COLSTATS_MAX_X>, dim3((unsigned)n_parts), dim3(H), 0, st, G, (long)R, H,
-                           rows_per, row_w, obs, stride, nbr_off, B, K, nd, nx, pmx, psm, px);
-    else if (nx > 0)   // the neighbour features alone (nd <= 8)
-        hipLaunchKernelGGL(P::colstats_kernel<8>, dim3((unsigned)n_parts), dim3(H), 0, st, G, (long)R, H, rows_per, row_w,
-                           obs, stride, nbr_off, B, K, nd, nx, pmx, psm, px);
-    else
-        hipLaunchKernelGGL(P::colstats_kernel<0>, dim3((unsigned)n_parts), dim3(H), 0, st, G, (long)R, H, rows_per,
-                           row_w, obs, stride, nbr_off, B > 0 ? B : 1, K > 0 ? K : 1, nd, 0, pmx, psm, px);
-    QS_HIP(hipGetLastError());
-    return QS_OK;
-}
-extern "C" int qs_attn_bwd2_x3(int32_t B, int32_t K, int32_t H, const qs_attn_tower* towers,
-                               const qs_attn_train* trains, int32_t n_towers, void* stream) {
-    return attn_train_impl(TR_BWD2, nullptr, 0, 0, 0, B, K, 0, H, towers, trains, n_towers, stream);
 }
 
 // the kernel parameter block a config produces (host only; runtime specialisation / diagnostics)

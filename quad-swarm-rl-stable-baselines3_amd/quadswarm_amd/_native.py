@@ -9,7 +9,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("QUADSWARM_LIB", os.path.join(HERE, "lib", "libquadswarm.so"))
 
-ABI_VERSION = 14
+ABI_VERSION = 15
 MAX_AGENTS = 128
 A_KMAX = 16   # flavor A, more than 64 drones: visible neighbours (qs_flavor_a.h QS_A_KMAX)
 MAX_DR_CHOICES = 8
@@ -141,6 +141,7 @@ R_HIST_N, R_HIST_HEAD, R_RESTORED, R_PUSHED, NR = 10, 11, 12, 13, 14
 
 
 ATTN_MAX_TOWERS = 2
+ATTN_NCOLMAX = 6          # qs_attn_train.colmax rows (QS_ATTN_NCOLMAX)
 
 
 class QsAttnTower(ctypes.Structure):
@@ -154,7 +155,7 @@ class QsAttnTrain(ctypes.Structure):
     """qs_attn_train (the PPO update's saved activations and gradients of one tower, quadswarm.h)."""
     _fields_ = [(n, ctypes.c_void_p) for n in ("e1", "a1", "a2", "v1", "h", "w", "dout", "dem", "w_v2tp", "w_v1tp",
                                                 "w_a2tp", "w_a1etp", "w_e2tp", "dh_pre", "dv1_pre", "da2_pre", "da1_pre",
-                                                "dscore", "de2p", "de2_pre", "de1_pre")]
+                                                "dscore", "de2p", "de2_pre", "de1_pre", "colmax", "a3w_part")]
 
 
 CUR_MAX_WINDOW = CUR_MAX_HIST = 64
@@ -181,7 +182,7 @@ EXPORTS = ["qs_abi_version", "qs_last_error", "qs_struct_sizes", "qs_config_defa
            "qs_replay_config_default", "qs_replay_workspace_bytes", "qs_replay_enable", "qs_replay_disable", "qs_replay_buffers_get",
            "qs_attn_embed", "qs_attn_pool", "qs_attn_embed_x3", "qs_attn_pool_x3", "qs_curriculum_init",
            "qs_curriculum_step", "qs_curriculum_step_all", "qs_attn_embed_train_x3", "qs_attn_pool_train_x3",
-           "qs_attn_bwd1_x3", "qs_attn_bwd2_x3", "qs_attn_dw_x3", "qs_colstats"]
+           "qs_attn_bwd1_x3", "qs_attn_bwd2_x3", "qs_attn_dw_x3", "qs_attn_dw0_x3", "qs_colstats"]
 
 _lib = None
 
@@ -227,8 +228,9 @@ def lib():
         "qs_attn_pool_train_x3": ([I32, I32, I32, P(QsAttnTower), P(QsAttnTrain), I32, V], I32),
         "qs_attn_bwd1_x3": ([I32, I32, I32, P(QsAttnTower), P(QsAttnTrain), I32, V], I32),
         "qs_attn_bwd2_x3": ([I32, I32, I32, P(QsAttnTower), P(QsAttnTrain), I32, V], I32),
-        "qs_attn_dw_x3": ([V, V, V, ctypes.c_int64, I32, V, I32, V], I32),
+        "qs_attn_dw_x3": ([V, V, V, ctypes.c_int64, I32, V, V, I32, V], I32),
         "qs_colstats": ([V, ctypes.c_int64, I32, V, V, I32, I32, I32, I32, I32, I32, V, V, V, I32, V], I32),
+        "qs_attn_dw0_x3": ([V, V, V, I32, I32, I32, I32, I32, I32, I32, V, V, I32, V], I32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

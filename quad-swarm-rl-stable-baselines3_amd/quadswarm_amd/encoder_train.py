@@ -74,19 +74,42 @@ def col_stats(G, obs=None, B=0, K=0, nbr_off=0, nd=0, nx=0, parts=None, row_w=No
     return _pow2_scales(pmx.amax(0)), psm.sum(0), (px.sum(0) if px is not None else None)
 
 
-def dw_x3(G, A, parts=256, out=None, gs=None):
+def dw_x3(G, A, parts=256, out=None, gs=None, sums=False):
     """G^T A ([H, H]) over the rows of G, A [R, H] (|A| <= 1) on the split-f16 matrix cores (qs_attn_dw_x3), the row
-    range split over `parts` blocks and the parts summed here.  gs: G's column scales (col_scales / col_stats)."""
+    range split over `parts` blocks and the parts summed here.  gs: G's column scales (col_scales / col_stats).
+    sums: also G's column sums from the same pass (returns (dW, sums))."""
     R, H = G.shape
     parts = max(1, min(parts, (R + 15) // 16))
     buf = torch.empty(parts, H, H, dtype=torch.float32, device=G.device)
+    psum = torch.empty(parts, H, dtype=torch.float32, device=G.device) if sums else None
     if gs is None:
         gs = col_scales(G)
     st = ctypes.c_void_p(torch.cuda.current_stream(G.device).cuda_stream)
     NAT.check(NAT.lib().qs_attn_dw_x3(ctypes.c_void_p(G.data_ptr()), ctypes.c_void_p(A.data_ptr()),
-                                      ctypes.c_void_p(gs.data_ptr()), R, H, ctypes.c_void_p(buf.data_ptr()), parts, st),
+                                      ctypes.c_void_p(gs.data_ptr()), R, H, ctypes.c_void_p(buf.data_ptr()),
+                                      ctypes.c_void_p(psum.data_ptr() if sums else 0), parts, st),
               "qs_attn_dw_x3")
-    return torch.sum(buf, dim=0, out=out)
+    dW = torch.sum(buf, dim=0, out=out)
+    return (dW, psum.sum(0)) if sums else dW
+
+
+def dw0_x3(G, obs, B, K, so, nd, gs=None, parts=512):
+    """Layer 0's weight gradient sum_j G_j^T x0_j ([H, nd + so], in the reference's column order [self | neighbour])
+    and the bias gradient sum_j G_j, x0_j = [nbr_j | self_{j % B}] gathered from `obs` (the forward's pairing), on the
+    split-f16 matrix cores (qs_attn_dw0_x3; gs: G's column scales, col_scales by default)."""
+    R, H = G.shape
+    parts = max(1, min(parts, (R + 15) // 16))
+    buf = torch.empty(parts, H, 32, dtype=torch.float32, device=G.device)
+    psum = torch.empty(parts, H, dtype=torch.float32, device=G.device)
+    if gs is None:
+        gs = col_scales(G)
+    st = ctypes.c_void_p(torch.cuda.current_stream(G.device).cuda_stream)
+    NAT.check(NAT.lib().qs_attn_dw0_x3(ctypes.c_void_p(G.data_ptr()), ctypes.c_void_p(gs.data_ptr()),
+                                       ctypes.c_void_p(obs.data_ptr()), obs.shape[1], so, so, B, K, nd, H,
+                                       ctypes.c_void_p(buf.data_ptr()), ctypes.c_void_p(psum.data_ptr()), parts, st),
+              "qs_attn_dw0_x3")
+    dW = buf.sum(0)
+    return torch.cat((dW[:, nd:nd + so], dW[:, :nd]), dim=1), psum.sum(0)
 
 
 class _Runner:
@@ -104,10 +127,14 @@ class _Runner:
         self.pending = False
         self.dw_x3 = True   # the weight gradients on the split-f16 matrix cores (else torch fp32 GEMMs)
 
-    def dw(self, G, A):
-        """(dW = G^T A over the B K rows (A: tanh outputs), the bias gradient sum_r G[r, :])."""
+    def dw(self, G, A, cm=None):
+        """(dW = G^T A over the B K rows (A: tanh outputs), the bias gradient sum_r G[r, :]).  cm: G's per-block column
+        maxima from the kernel that wrote G (qs_attn_train.colmax, [n_blocks, H]): then one pass over G and A (the
+        sums from the dW pass), else a column-statistics pass first."""
         if not self.dw_x3:
             return G.t().mm(A), G.sum(0)
+        if cm is not None:
+            return dw_x3(G, A, gs=_pow2_scales(cm.amax(0)), sums=True)
         gs, sums, _ = col_stats(G)
         return dw_x3(G, A, gs=gs), sums
 
@@ -115,9 +142,12 @@ class _Runner:
         H, T, R = self.H, self.T, B * self.K
         z = lambda *s: torch.empty(*s, dtype=torch.float32, device=dev)  # noqa: E731
         self.B = B
+        mu = (64 // self.K) * self.K                 # the kernels' row blocks (qs_policy.h MROWS = 64)
+        nblk = (R + mu - 1) // mu
         self.buf = [dict(e1=z(R, H), e2=z(R, H), a1=z(R, H), a2=z(R, H), v1=z(R, H), h=z(R, H), w=z(R),
                          e_mean=z(B, H), P=z(B, H), out=z(B, H), dh_pre=z(R, H), dv1_pre=z(R, H), da2_pre=z(R, H),
-                         da1_pre=z(R, H), de2p=z(R, H), dscore=z(R), dem=z(B, H)) for _ in range(T)]
+                         da1_pre=z(R, H), de2p=z(R, H), dscore=z(R), dem=z(B, H),
+                         colmax=z(NAT.ATTN_NCOLMAX, nblk, H), a3w_part=z(nblk, H)) for _ in range(T)]
 
     def _pack(self, params):
         """x3-pack the towers' weights (forward operands and the backward's transposes), bind every pointer."""
@@ -147,7 +177,8 @@ class _Runner:
             t.w_a1ep, t.w_a2p, t.b_a2, t.w_a3 = p(k["w_a1ep"]), p(k["w_a2p"]), p(k["b_a2"]), p(k["w_a3"])
             t.b_a3 = float(w["a3_b"].detach().item())
             r = self.trains[i]
-            for n in ("e1", "a1", "a2", "v1", "h", "w", "dh_pre", "dv1_pre", "da2_pre", "da1_pre", "dscore", "de2p", "dem"):
+            for n in ("e1", "a1", "a2", "v1", "h", "w", "dh_pre", "dv1_pre", "da2_pre", "da1_pre", "dscore", "de2p", "dem",
+                      "colmax", "a3w_part"):
                 setattr(r, n, p(b[n]))
             r.de2_pre = p(b["de2p"])      # in place: bwd2 reads de2p[j] and writes de2_pre[j] on the same lane
             r.de1_pre = p(b["dh_pre"])    # dh_pre's last reader (dW_v2) runs before bwd2
@@ -191,18 +222,17 @@ class _Runner:
         grads = [None] * (14 * self.T)
         for i in range(self.T):
             b, w0 = self.buf[i], 14 * i
+            cm = b["colmax"]   # the gradients' per-block column maxima, from the kernels that wrote them
             gi = {}
-            gi["v2_w"], gi["v2_b"] = self.dw(b["dh_pre"], b["v1"])
-            gi["v1_w"], gi["v1_b"] = self.dw(b["dv1_pre"], b["e2"])
-            gi["a2_w"], gi["a2_b"] = self.dw(b["da2_pre"], b["a1"])
-            if self.dw_x3:   # sum_j dscore_j a2_j: a weighted column sum of a2 (one pass)
-                gi["a3_w"] = col_stats(b["a2"], row_w=b["dscore"])[1].view(1, -1)
-            else:
-                gi["a3_w"] = b["dscore"].view(1, -1).mm(b["a2"])
+            gi["v2_w"], gi["v2_b"] = self.dw(b["dh_pre"], b["v1"], cm[0])
+            gi["v1_w"], gi["v1_b"] = self.dw(b["dv1_pre"], b["e2"], cm[1])
+            gi["a2_w"], gi["a2_b"] = self.dw(b["da2_pre"], b["a1"], cm[2])
+            # sum_j dscore_j a2_j: backward 1's per-block partial sums
+            gi["a3_w"] = b["a3w_part"].sum(0).view(1, -1) if self.dw_x3 else b["dscore"].view(1, -1).mm(b["a2"])
             gi["a3_b"] = b["dscore"].sum().view(1)
             dP = b["da1_pre"].view(K, B, H).sum(0)                     # rows j with j % B == b (the repeat tiling)
             a1_w = params[w0 + 8]
-            dA_e, gi["a1_b"] = self.dw(b["da1_pre"], b["e2"])          # a1_b = sum_j da1_pre_j = sum_b dP_b
+            dA_e, gi["a1_b"] = self.dw(b["da1_pre"], b["e2"], cm[3])   # a1_b = sum_j da1_pre_j = sum_b dP_b
             gi["a1_w"] = torch.cat((dA_e, self.dw(dP, b["e_mean"])[0]), dim=1)   # |e_mean| <= 1 (a mean of tanh)
             torch.mm(dP, a1_w[:, H:], out=b["dem"])                    # dL/d e_mean
             for n in gi:
@@ -213,13 +243,11 @@ class _Runner:
         for i in range(self.T):
             b, w0 = self.buf[i], 14 * i
             de2_pre, de1_pre = b["de2p"], b["dh_pre"]
-            grads[w0 + 2], grads[w0 + 3] = self.dw(de2_pre, b["e1"])
-            # embedding_mlp[0] on cat(self_{j % B}, nbr_j): the neighbour half sum_j de1_pre_j^T nbr_j with the bias
-            # gradient in one pass; the self half over the K tiles summed first (B rows instead of B K)
+            grads[w0 + 2], grads[w0 + 3] = self.dw(de2_pre, b["e1"], b["colmax"][4])
+            # embedding_mlp[0] on cat(self_{j % B}, nbr_j): both halves and the bias gradient in one pass over
+            # de1_pre with the layer-0 rows gathered as the forward gathers them
             if self.dw_x3:
-                _, grads[w0 + 1], gx = col_stats(de1_pre, obs, B, K, so, nd, nd)
-                g_self = de1_pre.view(K, B, H).sum(0).t().mm(self_obs)
-                grads[w0] = torch.cat((g_self, gx.t()), dim=1)
+                grads[w0], grads[w0 + 1] = dw0_x3(de1_pre, obs, B, K, so, nd, gs=_pow2_scales(b["colmax"][5].amax(0)))
             else:
                 g_self = de1_pre.view(K, B, H).sum(0).t().mm(self_obs)
                 grads[w0] = torch.cat((g_self, de1_pre.t().mm(nbr_rows)), dim=1)

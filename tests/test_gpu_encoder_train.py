@@ -17,7 +17,8 @@ torch = pytest.importorskip("torch")
 if not torch.cuda.is_available():  # pragma: no cover
     pytest.skip("no HIP device", allow_module_level=True)
 
-from quadswarm_amd.encoder_train import FusedAttentionTrain, col_scales, col_stats, dw_x3, tower_params  # noqa: E402
+from quadswarm_amd.encoder_train import (FusedAttentionTrain, col_scales, col_stats, dw0_x3, dw_x3,  # noqa: E402
+                                         tower_params)
 from quadswarm_amd.ppo import PolicyConfig, SwarmActorCritic  # noqa: E402
 
 
@@ -161,7 +162,11 @@ def test_dw_x3_matches_fp64(H, R):
     G = torch.randn(R, H, device="cuda", generator=g) * torch.exp2(torch.linspace(-20, 4, H, device="cuda"))
     A = torch.tanh(torch.randn(R, H, device="cuda", generator=g) * 2)
     want = G.double().t().mm(A.double())
-    got = dw_x3(G, A)
+    got, sums = dw_x3(G, A, sums=True)
+    assert torch.equal(got, dw_x3(G, A))
+    # the column sums from the same pass (the bias gradients; ABI 15)
+    G64 = G.double()
+    assert ((sums.double() - G64.sum(0)).abs() / G64.abs().sum(0)).max().item() < 1e-6
     t32 = G.t().mm(A)
     # per output row n (column n of G has its own scale): relative to the row's magnitude
     scale = want.abs().amax(1, keepdim=True).clamp_min(1e-300)
@@ -223,3 +228,55 @@ def test_fused_update_falls_back_when_a_weight_leaves_the_x3_range():
     out = f.encodings(obs)
     ref = torch_encodings(pol, obs)
     assert out is not None and max(rel_err(o, r) for o, r in zip(out, ref)) < 5e-5
+
+
+@pytest.mark.parametrize("case,B", [("c3", 3000), ("k1", 777)])
+def test_backward_column_statistics(case, B):
+    """The column statistics the backward kernels form where the gradients are (ABI 15): over the blocks, colmax rows
+    1..4 equal torch's max |g| of dv1_pre, da2_pre, da1_pre, de2_pre bitwise (a max is exact), row 0 (dh_pre,
+    overwritten by de1_pre later) that of w_j dout[a] (1 - h^2) from the saved tensors; the per-block partials of
+    sum_j dscore_j a2_j sum to torch's product."""
+    pol = fixture_policy(case) if case == "c3" else random_policy(1, H=128)
+    obs = obs_for(pol.cfg, B, seed=4)
+    H, K = pol.cfg.neighbor_hidden_size, pol.cfg.num_use_neighbor_obs
+    g = torch.Generator(device="cuda").manual_seed(11)
+    G = [torch.randn(B, H, device="cuda", generator=g) * 1e-3 for _ in range(2)]
+    fused = FusedAttentionTrain(pol)
+    outs = fused.encodings(obs)
+    params = fused.params()
+    torch.autograd.grad(sum((o * gi).sum() for o, gi in zip(outs, G)), params)
+    torch.cuda.synchronize()
+    for i, b in enumerate(fused.runner.buf):
+        cm = b["colmax"].amax(1)   # [5, n_blocks, H] -> the maxima over the blocks
+        for row, name in ((1, "dv1_pre"), (2, "da2_pre"), (3, "da1_pre"), (4, "de2p")):
+            assert torch.equal(cm[row], b[name].abs().amax(0)), (case, i, name)
+        w, h = b["w"], b["h"]
+        dh = (G[i].repeat_interleave(K, 0) * w[:, None]) * (1 - h * h)
+        assert ((cm[0] - dh.abs().amax(0)).abs() <= 1e-6 * dh.abs().amax(0)).all(), (case, i, "dh_pre")
+        want = b["dscore"].double()[None, :].mm(b["a2"].double())[0]
+        got = b["a3w_part"].sum(0).double()
+        scale = b["dscore"].double().abs()[None, :].mm(b["a2"].double().abs())[0].clamp_min(1e-300)
+        assert ((got - want).abs() / scale).max().item() < 1e-6, (case, i, "a3w")
+
+
+@pytest.mark.parametrize("H,B,K,parts", [(256, 4099, 6, 512), (128, 777, 1, 5), (256, 300, 7, 4096)])
+def test_dw0_x3_matches_fp64(H, B, K, parts):
+    """qs_attn_dw0_x3: layer 0's weight gradient sum_j G_j^T [self_{j % B} | nbr_j] (the reference's column order)
+    and the bias gradient against fp64, on ragged part splits (empty trailing parts) and column scales spanning
+    2^-20 .. 2^4."""
+    g = torch.Generator(device="cuda").manual_seed(B + K)
+    so, nd = 18, 6
+    R = B * K
+    G = torch.randn(R, H, device="cuda", generator=g) * torch.exp2(torch.linspace(-20, 4, H, device="cuda"))
+    obs = torch.randn(B, so + K * nd + 3, device="cuda", generator=g) * 3
+    got, sums = dw0_x3(G, obs, B, K, so, nd, parts=parts)
+    nbr = obs[:, so:so + K * nd].reshape(R, nd).double()
+    slf = obs[:, :so].double().repeat(K, 1)
+    X = torch.cat((slf, nbr), dim=1)
+    G64 = G.double()
+    want = G64.t().mm(X)                          # [H, so + nd]
+    scale = G64.abs().t().mm(X.abs()).clamp_min(1e-300)
+    err = ((got.double() - want).abs() / scale).max().item()
+    print(f"H={H} B={B} K={K}: layer-0 dW relative error {err:.2e}")
+    assert err < 2e-6
+    assert ((sums.double() - G64.sum(0)).abs() / G64.abs().sum(0)).max().item() < 1e-6

@@ -187,6 +187,18 @@ for s in "$@"; do
       step scen_bitwise 400 python tools/scen_bitwise.py ${BASE:-tools/jit/base_r06} 1600
       step scen_tests 400 python -u -m pytest tests/test_gpu_parity_scen.py -q --timeout 200 --timeout-method thread
       ;;
+    polab)     # policy-kernel A/B: one C3 end-to-end iteration under a kernel trace per library (LIBS="name ...",
+               # quadswarm_amd/lib/ab/libquadswarm_<name>.so from tools/build_pol_variant.sh; "base" = the in-tree library)
+      export TMPDIR=/tmp
+      for v in ${LIBS:?LIBS=<variant names>}; do
+        if [ "$v" = base ]; then unset QUADSWARM_LIB; else
+          export QUADSWARM_LIB=$PWD/quad-swarm-rl-stable-baselines3_amd/quadswarm_amd/lib/ab/libquadswarm_$v.so; fi
+        step polab_$v 500 rocprofv3 --kernel-trace --stats -d gpurun_out/polab_$v -o e2e --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline --e2e-iters 1
+        python3 tools/kstats.py gpurun_out/polab_$v 24 > gpurun_out/polab_${v}_summary.txt 2>&1
+        find gpurun_out/polab_$v -name "*kernel_trace.csv" -delete
+      done
+      unset QUADSWARM_LIB
+      ;;
     e2eprof)   # kernel trace of one C3 end-to-end PPO iteration (where update_s goes)
       export TMPDIR=/tmp
       step e2eprof_kt 500 rocprofv3 --kernel-trace --stats -d gpurun_out/e2eprof -o e2e --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline --e2e-iters 1
