@@ -17,6 +17,13 @@
 static int fail(int code, const std::string& msg) { return qs_fail(code, msg); }
 #define QS_HIP(call) QS_HIP_CHECK(call)
 
+#ifdef QS_STAMPS
+// the policy kernels' phase stamps (this translation unit's copy of qs_dbg_stamps; tools/policy_stamps.py)
+extern "C" int qs_debug_stamps_policy(uint64_t* host, size_t n) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(qs::qs_dbg_stamps), n * sizeof(uint64_t)) == hipSuccess ? 0 : -3;
+}
+#endif
+
 // fused attention-encoder forward (qs_policy.h)
 static int attn_check(int32_t B, int32_t K, int32_t H, const qs_attn_tower* towers, int32_t n_towers) {
     if (!towers) return fail(QS_E_INVALID, "NULL towers");
@@ -205,7 +212,7 @@ static int dw_launch(const float* G, const float* A, const float* gs, int64_t R,
     const int steps = (int)((rows_per + P::DW_STEP - 1) / P::DW_STEP);
     const size_t lds = P::dw_lds_bytes<H>();
     QS_HIP(hipFuncSetAttribute((const void*)P::dw_x3_kernel<H>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(P::dw_x3_kernel<H>, dim3((unsigned)n_parts), dim3(P::NTHR), lds, st, G, A, gs, (long)R, steps, part,
+    hipLaunchKernelGGL(P::dw_x3_kernel<H>, dim3((unsigned)n_parts), dim3(P::dw_threads<H>()), lds, st, G, A, gs, (long)R, steps, part,
                        part_sum);
     QS_HIP(hipGetLastError());
     return QS_OK;

@@ -25,6 +25,8 @@
 // is checked by the packer (policy_fused.pack_mfma_weight_x3).  Block geometry, row pairing and packing as in
 // qs_policy.h / qs_policy_x3.h; the W^T operands of the backward GEMMs are packed like any weight (of W^T).
 #pragma once
+#include <type_traits>
+
 #include "qs_policy_x3.h"
 
 namespace qs {
@@ -238,14 +240,20 @@ __global__ __launch_bounds__(NTHR, 2) __attribute__((amdgpu_waves_per_eu(2, 2)))
     const int AB = MROWS / K, MU = AB * K;
     const long R = (long)B * K, row0 = (long)blockIdx.x * MU;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    QS_STAMP_DECL
+    QS_RTSTAMP(12);
+    QS_STAMP(0);
     for (int n = tid; n < H; n += NTHR) {
         BI[n] = t.b_e1[n];
         BI[H + n] = t.b_e2[n];
     }
     gather_rows0(obs, stride, so, off, B, K, nd, row0, MU, R, tid, [&](int r, int c, float v) { X0.put(r, c, X3_SIN * v); });
     __syncthreads();
+    QS_STAMP(1);
     f32x16 acc[RT][CT];
     mfma_layer_x3<H, KD0, true, false>(X0, reinterpret_cast<const uint4*>(t.w_e1p), acc, wave, lane);
+    QS_STAMP(2);
+    const auto qe2 = mfma_prefetch_x3<H>(reinterpret_cast<const uint4*>(t.w_e2p), wave, lane);   // ahead of e1's stores
     store_tanh_x3<H>(X, acc, 1.f / (X3_SIN * X3_SW), wave, lane,
                      [&](int i, int n0) {
                          return (i < MU && row0 + i < R) ? lds4(BI + n0) : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -254,25 +262,17 @@ __global__ __launch_bounds__(NTHR, 2) __attribute__((amdgpu_waves_per_eu(2, 2)))
                          if (i < MU && row0 + i < R) st4g(tr.e1 + (row0 + i) * H + n0, y);
                      });
     __syncthreads();
-    mfma_layer_x3<H, H, true, QS_EMBED_PIN != 0>(X, reinterpret_cast<const uint4*>(t.w_e2p), acc, wave, lane);
+    QS_STAMP(3);
+    mfma_layer_x3<H, H, true, QS_EMBED_PIN != 0>(X, reinterpret_cast<const uint4*>(t.w_e2p), acc, wave, lane, qe2);
     __syncthreads();
-    store_tanh_x3<H>(X, acc, 1.f / (X3_SX * X3_SW), wave, lane, [&](int, int n0) { return lds4(BI + H + n0); },
-                     [&](int i, int n0, float4 y) {
-                         if (i < MU && row0 + i < R) st4g(t.e2 + (row0 + i) * H + n0, y);
-                     });
-    __syncthreads();
-    constexpr float isx = 1.f / X3_SX;
-    const float inv = 1.f / (float)K;
-    for (int e = tid; e < AB * H; e += NTHR) {
-        const int a = e / H, n = e - a * H;
-        const long agent = row0 / K + a;
-        if (agent < B) {
-            float s = 0.f;
-            for (int k = 0; k < K; ++k) s += X.get(a * K + k, n) * isx;
-            t.e_mean[agent * H + n] = s * inv;
-        }
-    }
+    QS_STAMP(4);
+    embed_e2_epilogue<H>(acc, BI + H, t.e2, t.e_mean, smem4, row0, MU, R, B, K, AB, wave, lane, tid);
+    QS_STAMP(5);
+    QS_STAMP(6);
+    QS_RTSTAMP(13);
+    if (blockIdx.y == 0) QS_STAMP_FLUSH();
 }
+
 
 template <int H>
 __global__ __launch_bounds__(NTHR, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void attn_pool_train_x3_kernel(
@@ -290,6 +290,9 @@ __global__ __launch_bounds__(NTHR, 2) __attribute__((amdgpu_waves_per_eu(2, 2)))
     const long R = (long)B * K, row0 = (long)blockIdx.x * MU;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     constexpr float SS = X3_SX * X3_SW, iSS = 1.f / SS;
+    QS_STAMP_DECL
+    QS_RTSTAMP(12);
+    QS_STAMP(0);
     for (int n = tid; n < H; n += NTHR) {
         A3[n] = t.w_a3[n];
         A3[H + n] = t.b_a2[n];
@@ -316,13 +319,17 @@ __global__ __launch_bounds__(NTHR, 2) __attribute__((amdgpu_waves_per_eu(2, 2)))
     }
     load_rows_x3<H>(X, t.e2, row0, MU, R, tid);
     __syncthreads();
+    QS_STAMP(1);
     mfma_layer_x3<H, H, false>(X, reinterpret_cast<const uint4*>(t.w_a1ep), acc, wave, lane);
     __syncthreads();
+    QS_STAMP(2);
     store_tanh_x3<H>(X, acc, iSS, wave, lane, ZeroInit(), [&](int i, int n0, float4 y) {
         if (okrow(i)) st4g(tr.a1 + (row0 + i) * H + n0, y);
     });
     __syncthreads();
+    QS_STAMP(3);
     mfma_layer_x3<H>(X, reinterpret_cast<const uint4*>(t.w_a2p), acc, wave, lane);
+    QS_STAMP(4);
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {   // a2 (the rollout kernel keeps it in the score's registers only)
         const int i = acc_i(rt, lane);
@@ -341,6 +348,7 @@ __global__ __launch_bounds__(NTHR, 2) __attribute__((amdgpu_waves_per_eu(2, 2)))
     float* SCP = A3 + 4 * H;
     score_partials<H>(acc, iSS, A3, A3 + H, SCP, wave, lane);
     __syncthreads();
+    QS_STAMP(5);
     if (tid < MROWS) SC[tid] = ((SCP[tid] + SCP[MROWS + tid]) + (SCP[2 * MROWS + tid] + SCP[3 * MROWS + tid])) + t.b_a3;
     __syncthreads();
     if (tid < AB) {
@@ -358,15 +366,19 @@ __global__ __launch_bounds__(NTHR, 2) __attribute__((amdgpu_waves_per_eu(2, 2)))
     load_rows_x3<H>(X, t.e2, row0, MU, R, tid);
     __syncthreads();
     if (tid < MU && row0 + tid < R) tr.w[row0 + tid] = WT[tid];
+    QS_STAMP(6);
     mfma_layer_x3<H>(X, reinterpret_cast<const uint4*>(t.w_v1p), acc, wave, lane);
     __syncthreads();
+    QS_STAMP(7);
     store_tanh_x3<H>(X, acc, iSS, wave, lane, [&](int, int n0) { return lds4(A3 + 2 * H + n0); },
                      [&](int i, int n0, float4 y) {
                          if (okrow(i)) st4g(tr.v1 + (row0 + i) * H + n0, y);
                      });
     __syncthreads();
+    QS_STAMP(8);
     mfma_layer_x3<H>(X, reinterpret_cast<const uint4*>(t.w_v2p), acc, wave, lane);
     __syncthreads();
+    QS_STAMP(9);
     float* Y = reinterpret_cast<float*>(smem4);
     constexpr int LDY = H + 4;
 #pragma unroll
@@ -386,7 +398,8 @@ __global__ __launch_bounds__(NTHR, 2) __attribute__((amdgpu_waves_per_eu(2, 2)))
             }
     }
     __syncthreads();
-    for (int e = tid; e < AB * H; e += NTHR) {
+    QS_STAMP(10);
+    for (int e = tid; e < AB * H; e += NTHR) {   // (float4-wide as the rollout kernel: 4 spilled registers here)
         const int a = e / H, n = e - a * H;
         const long agent = row0 / K + a;
         if (agent < B) {
@@ -395,7 +408,11 @@ __global__ __launch_bounds__(NTHR, 2) __attribute__((amdgpu_waves_per_eu(2, 2)))
             t.out[agent * H + n] = s;
         }
     }
+    QS_STAMP(11);
+    QS_RTSTAMP(13);
+    if (blockIdx.y == 0) QS_STAMP_FLUSH();
 }
+
 
 // ------------------------------------------------------------------------------------------------------------------
 // backward
@@ -434,6 +451,9 @@ __global__ __launch_bounds__(NTHR, 2) void attn_bwd1_x3_kernel(int B, int K, Tow
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     auto okrow = [&](int i) { return i < MU && row0 + i < R; };
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    QS_STAMP_DECL
+    QS_RTSTAMP(12);
+    QS_STAMP(0);
     for (int e = tid; e < AB * L4; e += NTHR) {
         const int a = e / L4, c4 = e - a * L4;
         reinterpret_cast<float4*>(DO)[e] = (a0 + a < B) ? ld4g(tr.dout + (a0 + a) * H + 4 * c4) : z4;
@@ -441,6 +461,7 @@ __global__ __launch_bounds__(NTHR, 2) void attn_bwd1_x3_kernel(int B, int K, Tow
     for (int n = tid; n < H; n += NTHR) W3[n] = t.w_a3[n];
     if (tid < MROWS) WT[tid] = okrow(tid) ? tr.w[row0 + tid] : 0.f;
     __syncthreads();
+    QS_STAMP(1);
     float4 cmr = z4, aw = z4;   // column maxima / sum dscore a2 of the lane's columns over the wave's rows
     // dw_j = h_j . dout[a] and dh_pre = w_j dout[a] (1 - h^2): wave-owned rows
     auto rowp = [&](const float* a, int r, int c4) { return a + (row0 + (okrow(r) ? r : 0)) * H + 4 * c4; };
@@ -459,6 +480,7 @@ __global__ __launch_bounds__(NTHR, 2) void attn_bwd1_x3_kernel(int B, int K, Tow
     __syncthreads();
     // the waves' column maxima of dh_pre into the scratch (dout is no longer read); merged after the next barrier
     if (lane < L4) *reinterpret_cast<float4*>(DO + wave * H + 4 * lane) = cmr;
+    QS_STAMP(2);
     const size_t nblk = gridDim.x;
     auto cm_row = [&](int k) { return tr.colmax + ((size_t)k * nblk + blockIdx.x) * H; };
     f32x16 acc[RT][CT];
@@ -467,6 +489,7 @@ __global__ __launch_bounds__(NTHR, 2) void attn_bwd1_x3_kernel(int B, int K, Tow
     float4 aux[RT][CT][4];
     load_acc_rows<H>(tr.v1, row0, okrow, wave, lane, aux);   // in flight during the layer's MFMAs
     mfma_layer_x3<H>(X, reinterpret_cast<const uint4*>(tr.w_v2tp), acc, wave, lane);
+    QS_STAMP(3);
     float4 cma[CT][4];
     stage_acc_scaled<H>(X, acc, RS, RMX, wave, lane, aux, [&](int i, int n0, float4 a, float4 v1) {
         if (!okrow(i)) return z4;
@@ -482,6 +505,7 @@ __global__ __launch_bounds__(NTHR, 2) void attn_bwd1_x3_kernel(int B, int K, Tow
     __syncthreads();
     // de2p = dv1_pre W_v1 + (the attention chain's part, below): the value part stays in registers until then, so
     // de2p is written once (a store, reload and store of 1.6 GB per tower before)
+    QS_STAMP(4);
     mfma_layer_x3<H>(X, reinterpret_cast<const uint4*>(tr.w_v1tp), acc, wave, lane);
     f32x16 dev[RT][CT];
 #pragma unroll
@@ -503,7 +527,9 @@ __global__ __launch_bounds__(NTHR, 2) void attn_bwd1_x3_kernel(int B, int K, Tow
         SC[tid] = ds;
         if (okrow(tid)) tr.dscore[row0 + tid] = ds;
     }
+    QS_STAMP(5);
     __syncthreads();   // SC complete; every wave has read the tile and RS
+    QS_STAMP(6);
     cmr = z4;
     // da2_pre = dscore_j w3 (1 - a2^2)
     stage_rows_scaled<H, QS_BWD1_BR2>(X, RS, wave, lane, [&](int r, int c4) { return ld4g(rowp(tr.a2, r, c4)); },
@@ -524,7 +550,9 @@ __global__ __launch_bounds__(NTHR, 2) void attn_bwd1_x3_kernel(int B, int K, Tow
     }
     __syncthreads();
     // da1_pre = (da2_pre W_a2) (1 - a1^2)
+    QS_STAMP(7);
     mfma_layer_x3<H>(X, reinterpret_cast<const uint4*>(tr.w_a2tp), acc, wave, lane);
+    QS_STAMP(8);
     load_acc_rows<H>(tr.a1, row0, okrow, wave, lane, aux);   // after the layer (de2p's value part holds 64 VGPRs)
     stage_acc_scaled<H>(X, acc, RS, RMX, wave, lane, aux, [&](int i, int n0, float4 a, float4 a1) {
         if (!okrow(i)) return z4;
@@ -543,7 +571,9 @@ __global__ __launch_bounds__(NTHR, 2) void attn_bwd1_x3_kernel(int B, int K, Tow
                 (DO[NWAVE * H + n] + DO[(NWAVE + 1) * H + n]) + (DO[(NWAVE + 2) * H + n] + DO[(NWAVE + 3) * H + n]);
     __syncthreads();
     // de2p += da1_pre A_e
+    QS_STAMP(9);
     mfma_layer_x3<H>(X, reinterpret_cast<const uint4*>(tr.w_a1etp), acc, wave, lane);
+    QS_STAMP(10);
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
         const int i = acc_i(rt, lane);
@@ -556,7 +586,11 @@ __global__ __launch_bounds__(NTHR, 2) void attn_bwd1_x3_kernel(int B, int K, Tow
                 st4g(tr.de2p + (row0 + i) * H + acc_n0<H>(wave, c, g, lane),
                      f4_add(acc4(dev[rt][c], g), f4_scale(acc4(acc[rt][c], g), sc)));
     }
+    QS_STAMP(11);
+    QS_RTSTAMP(13);
+    if (blockIdx.y == 0) QS_STAMP_FLUSH();
 }
+
 
 // kernel 2: de2_pre = (de2p + dem[j / K] / K) (1 - e2^2) -> de1_pre = (de2_pre W_e2) (1 - e1^2)
 template <int H>
@@ -651,12 +685,24 @@ constexpr int DW_STEP = 16, DW_LDR = DW_STEP + 8;   // rows per step; LDS row st
 template <int H>
 constexpr size_t dw_lds_bytes() { return (size_t)2 * 4 * H * DW_LDR * 2; }   // 2 buffers x {Gh, Gl, Ah, Al}
 
+#ifndef QS_DW_RING
+#define QS_DW_RING 2   // steps of rows in flight in registers ahead of the MFMAs (1: the next step only)
+#endif
+
+// threads of a dW block: one wave per 32 output rows n (H = 256: 8 waves, 128 accumulator registers each -- room for
+// the two-step register ring; H = 128: 4 waves)
 template <int H>
-__global__ __launch_bounds__(NTHR, 1) void dw_x3_kernel(const float* __restrict__ G, const float* __restrict__ A,
+constexpr int dw_threads() { return 64 * (H / 32); }
+
+template <int H>
+__global__ __launch_bounds__(dw_threads<H>(), 1) void dw_x3_kernel(const float* __restrict__ G, const float* __restrict__ A,
                                                         const float* __restrict__ gs, long R, int steps_per_block,
                                                         float* __restrict__ part, float* __restrict__ part_sum) {
-    constexpr int NT = H / 128, KT = H / 32, TPC = NTHR / H, RPT = DW_STEP / TPC;   // threads per column, rows each
+    constexpr int DWT = dw_threads<H>();
+    constexpr int NT = 1, KT = H / 32, TPC = DWT / H, RPT = DW_STEP / TPC;   // threads per column, rows each
+    constexpr int RING = QS_DW_RING;
     static_assert(RPT % 8 == 0, "a thread's rows leave as whole 8-row (16-byte) groups");
+    static_assert(RING == 1 || RING == 2, "one or two steps in flight");
     extern __shared__ float4 smem4[];
     _Float16* lds = reinterpret_cast<_Float16*>(smem4);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -664,27 +710,35 @@ __global__ __launch_bounds__(NTHR, 1) void dw_x3_kernel(const float* __restrict_
     const long r_begin = (long)blockIdx.x * steps_per_block * DW_STEP;
     auto buf = [&](int b, int which) { return lds + ((size_t)b * 4 + which) * H * DW_LDR; };   // 0 Gh 1 Gl 2 Ah 3 Al
     const float sg = gs[sc];
-    float gv[RPT], av[RPT];
+    // register ring: slot k % RING holds step k's rows from its load until it is staged (statically indexed: the
+    // main loop is unrolled by RING)
+    float gv[RING][RPT], av[RING][RPT];
     float csum = 0.f;   // the column's sum over the part's rows (the bias gradient's part; rows in order)
-    auto load = [&](int s) {
+    // the block's rows through buffer descriptors (base = its first row, records = its rows that exist): a 32-bit
+    // offset per load and the range check's zeros past R, no 64-bit address or select per row
+    const long r_end = r_begin + (long)steps_per_block * DW_STEP < R ? r_begin + (long)steps_per_block * DW_STEP : R;
+    const int nbytes = r_end > r_begin ? (int)((r_end - r_begin) * H * 4) : 0;
+    const auto rg = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(G + r_begin * H), (short)0, nbytes, 0x00020000);
+    const auto ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(A + r_begin * H), (short)0, nbytes, 0x00020000);
+    const int voff = (sr * H + sc) * 4;
+    auto load = [&](auto SL, int s) {
+        constexpr int sl = decltype(SL)::value;
+        const int soff = s * DW_STEP * H * 4;   // (a step past the block's rows reads zeros)
 #pragma unroll
         for (int u = 0; u < RPT; ++u) {
-            const long r = r_begin + (long)s * DW_STEP + sr + u;
-            const bool ok = r < R && s < steps_per_block;
-            const long rr = ok ? r : 0;
-            const float okf = ok ? 1.f : 0.f;
-            gv[u] = G[rr * H + sc] * okf;
-            av[u] = A[rr * H + sc] * okf;
+            gv[sl][u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, voff + u * H * 4, soff, 0));
+            av[sl][u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ra, voff + u * H * 4, soff, 0));
         }
     };
-    auto stage = [&](int b) {
+    auto stage = [&](auto SL, int b) {
+        constexpr int sl = decltype(SL)::value;
 #pragma unroll
         for (int o = 0; o < RPT; o += 8) {
             f16x8 gh, gl, ah, al;
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
-                csum += gv[o + u];
-                const float g = sg * gv[o + u], a = X3_SX * av[o + u];
+                csum += gv[sl][o + u];
+                const float g = sg * gv[sl][o + u], a = X3_SX * av[sl][o + u];
                 gh[u] = (_Float16)g;
                 gl[u] = (_Float16)(g - (float)gh[u]);
                 ah[u] = (_Float16)a;
@@ -705,40 +759,67 @@ __global__ __launch_bounds__(NTHR, 1) void dw_x3_kernel(const float* __restrict_
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[t][k][r] = 0.f;
     const int aoff = (lane & 31) * DW_LDR + (lane >> 5) * 8;
-    load(0);
-    stage(0);
-    __syncthreads();
-    for (int s = 0; s < steps_per_block; ++s) {
-        const int b = s & 1;
-        if (s + 1 < steps_per_block) load(s + 1);   // next rows in flight during this step's MFMAs
-        f16x8 gh[NT], gl[NT], ah[KT], al[KT];
+    auto mfmas = [&](int b) {
+        f16x8 gh[NT], gl[NT];
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
             const int n0 = (wave * NT + t) * 32;
             gh[t] = *reinterpret_cast<const f16x8*>(buf(b, 0) + n0 * DW_LDR + aoff);
             gl[t] = *reinterpret_cast<const f16x8*>(buf(b, 1) + n0 * DW_LDR + aoff);
         }
+        // A's columns as the first operand, G's as the second: the result tile is [k][n], i.e. a lane holds output
+        // row n = lane & 31 (the layout of the store below; qs_policy.h acc_i / acc_n0).  A's fragments stream one
+        // column tile ahead (a 32x32x16 MFMA chain on one accumulator issues at the full rate: no operand hoard)
+        f16x8 ahn = *reinterpret_cast<const f16x8*>(buf(b, 2) + aoff);
+        f16x8 aln = *reinterpret_cast<const f16x8*>(buf(b, 3) + aoff);
 #pragma unroll
         for (int k = 0; k < KT; ++k) {
-            ah[k] = *reinterpret_cast<const f16x8*>(buf(b, 2) + k * 32 * DW_LDR + aoff);
-            al[k] = *reinterpret_cast<const f16x8*>(buf(b, 3) + k * 32 * DW_LDR + aoff);
+            const f16x8 ah = ahn, al = aln;
+            if (k + 1 < KT) {
+                ahn = *reinterpret_cast<const f16x8*>(buf(b, 2) + (k + 1) * 32 * DW_LDR + aoff);
+                aln = *reinterpret_cast<const f16x8*>(buf(b, 3) + (k + 1) * 32 * DW_LDR + aoff);
+            }
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                acc[t][k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, gh[t], acc[t][k], 0, 0, 0);
+                acc[t][k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, gl[t], acc[t][k], 0, 0, 0);
+                acc[t][k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, gh[t], acc[t][k], 0, 0, 0);
+            }
         }
-        // A's columns as the first operand, G's as the second: the result tile is [k][n], i.e. a lane holds output
-        // row n = lane & 31 (the layout of the store below; qs_policy.h acc_i / acc_n0)
-#pragma unroll
-        for (int k = 0; k < KT; ++k)
-#pragma unroll
-            for (int t = 0; t < NT; ++t) acc[t][k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[k], gh[t], acc[t][k], 0, 0, 0);
-#pragma unroll
-        for (int k = 0; k < KT; ++k)
-#pragma unroll
-            for (int t = 0; t < NT; ++t) acc[t][k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[k], gl[t], acc[t][k], 0, 0, 0);
-#pragma unroll
-        for (int k = 0; k < KT; ++k)
-#pragma unroll
-            for (int t = 0; t < NT; ++t) acc[t][k] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[k], gh[t], acc[t][k], 0, 0, 0);
-        if (s + 1 < steps_per_block) stage(b ^ 1);   // the other buffer: last read two steps ago (barrier below)
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, RING - 1>;
+    if constexpr (RING == 1) {
+        load(I0{}, 0);
+        stage(I0{}, 0);
         __syncthreads();
+        for (int s = 0; s < steps_per_block; ++s) {
+            const int b = s & 1;
+            if (s + 1 < steps_per_block) load(I0{}, s + 1);   // next rows in flight during this step's MFMAs
+            mfmas(b);
+            if (s + 1 < steps_per_block) stage(I0{}, b ^ 1);   // the other buffer: last read two steps ago
+            __syncthreads();
+        }
+    } else {
+        // step k's rows: loaded at iteration k - 2 into slot k % 2, staged at iteration k - 1 into LDS buffer k % 2,
+        // multiplied at iteration k
+        load(I0{}, 0);
+        load(I1{}, 1);
+        stage(I0{}, 0);
+        __syncthreads();
+        auto iter = [&](auto SL, int s) {   // SL = s % 2
+            constexpr int sl = decltype(SL)::value;
+            using Cur = std::integral_constant<int, sl>;
+            using Nxt = std::integral_constant<int, sl ^ 1>;
+            if (s + 2 < steps_per_block) load(Cur{}, s + 2);   // slot s % 2 was staged last iteration
+            mfmas(sl);
+            if (s + 1 < steps_per_block) stage(Nxt{}, sl ^ 1);
+            __syncthreads();
+        };
+        for (int s = 0; s < steps_per_block; s += 2) {
+            iter(I0{}, s);
+            if (s + 1 < steps_per_block) iter(I1{}, s + 1);
+        }
     }
     if (part_sum) {   // the TPC threads of a column through LDS (the staging buffers are free after the loop's barrier)
         float* cs = reinterpret_cast<float*>(smem4);
@@ -798,15 +879,20 @@ __global__ __launch_bounds__(NTHR, 2) void dw0_x3_kernel(const float* __restrict
     auto gbuf = [&](int b, int which) { return lds + b * BUF + (size_t)which * H * DW_LDR; };
     auto xbuf = [&](int b, int which) { return lds + b * BUF + (size_t)2 * H * DW_LDR + (size_t)which * KD0 * DW_LDR; };
     const float sg = gs[sc];
-    float gv[RPT], xv[XR];
+    // two steps in flight in a register ring (slot k % 2; the loop is unrolled by 2), G through a buffer descriptor
+    // over the block's rows (as dw_x3_kernel)
+    float gv[2][RPT], xv[2][XR];
     float csum = 0.f;
-    auto load = [&](int s) {
+    const long r_end = r_begin + (long)steps_per_block * DW_STEP < R ? r_begin + (long)steps_per_block * DW_STEP : R;
+    const int nbytes = r_end > r_begin ? (int)((r_end - r_begin) * H * 4) : 0;
+    const auto rg = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(G + r_begin * H), (short)0, nbytes, 0x00020000);
+    const int voff = (sr * H + sc) * 4;
+    auto load = [&](auto SL, int s) {
+        constexpr int sl = decltype(SL)::value;
+        const int soff = s * DW_STEP * H * 4;
 #pragma unroll
-        for (int u = 0; u < RPT; ++u) {
-            const long r = r_begin + (long)s * DW_STEP + sr + u;
-            const bool ok = r < R && s < steps_per_block;
-            gv[u] = G[(ok ? r : 0) * H + sc] * (ok ? 1.f : 0.f);
-        }
+        for (int u = 0; u < RPT; ++u)
+            gv[sl][u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, voff + u * H * 4, soff, 0));
 #pragma unroll
         for (int u = 0; u < XR; ++u) {   // gather_rows0's indexing (unconditional loads, zeroed by a product)
             const long r = r_begin + (long)s * DW_STEP + xr + u;
@@ -814,17 +900,18 @@ __global__ __launch_bounds__(NTHR, 2) void dw0_x3_kernel(const float* __restrict
             const long j = ok ? r : 0;
             const long a = j / K;
             const long idx = xc < nd ? a * stride + off + (j - a * K) * nd + xc : (j % B) * stride + (xc < nd + so ? xc - nd : 0);
-            xv[u] = obs[idx] * (ok ? 1.f : 0.f);
+            xv[sl][u] = obs[idx] * (ok ? 1.f : 0.f);
         }
     };
-    auto stage = [&](int b) {
+    auto stage = [&](auto SL, int b) {
+        constexpr int sl = decltype(SL)::value;
 #pragma unroll
         for (int o = 0; o < RPT; o += 8) {
             f16x8 gh, gl;
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
-                csum += gv[o + u];
-                const float g = sg * gv[o + u];
+                csum += gv[sl][o + u];
+                const float g = sg * gv[sl][o + u];
                 gh[u] = (_Float16)g;
                 gl[u] = (_Float16)(g - (float)gh[u]);
             }
@@ -836,7 +923,7 @@ __global__ __launch_bounds__(NTHR, 2) void dw0_x3_kernel(const float* __restrict
         f16x2 h2, l2;
 #pragma unroll
         for (int u = 0; u < XR; ++u) {
-            const float x = X3_SIN * xv[u];
+            const float x = X3_SIN * xv[sl][u];
             h2[u] = (_Float16)x;
             l2[u] = (_Float16)(x - (float)h2[u]);
         }
@@ -849,12 +936,7 @@ __global__ __launch_bounds__(NTHR, 2) void dw0_x3_kernel(const float* __restrict
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
     const int aoff = (lane & 31) * DW_LDR + (lane >> 5) * 8;
-    load(0);
-    stage(0);
-    __syncthreads();
-    for (int s = 0; s < steps_per_block; ++s) {
-        const int b = s & 1;
-        if (s + 1 < steps_per_block) load(s + 1);
+    auto mfmas = [&](int b) {
         f16x8 gh[NT], gl[NT];
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
@@ -865,13 +947,28 @@ __global__ __launch_bounds__(NTHR, 2) void dw0_x3_kernel(const float* __restrict
         const f16x8 xh = *reinterpret_cast<const f16x8*>(xbuf(b, 0) + aoff);
         const f16x8 xl = *reinterpret_cast<const f16x8*>(xbuf(b, 1) + aoff);
 #pragma unroll
-        for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, gh[t], acc[t], 0, 0, 0);
-#pragma unroll
-        for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, gl[t], acc[t], 0, 0, 0);
-#pragma unroll
-        for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xl, gh[t], acc[t], 0, 0, 0);
-        if (s + 1 < steps_per_block) stage(b ^ 1);
+        for (int t = 0; t < NT; ++t) {
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, gh[t], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, gl[t], acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xl, gh[t], acc[t], 0, 0, 0);
+        }
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    load(I0{}, 0);
+    load(I1{}, 1);
+    stage(I0{}, 0);
+    __syncthreads();
+    auto iter = [&](auto SL, int s) {   // SL = s % 2: step s in LDS buffer s % 2, step s + 1 in slot (s + 1) % 2
+        constexpr int sl = decltype(SL)::value;
+        if (s + 2 < steps_per_block) load(std::integral_constant<int, sl>{}, s + 2);
+        mfmas(sl);
+        if (s + 1 < steps_per_block) stage(std::integral_constant<int, sl ^ 1>{}, sl ^ 1);
         __syncthreads();
+    };
+    for (int s = 0; s < steps_per_block; s += 2) {
+        iter(I0{}, s);
+        if (s + 1 < steps_per_block) iter(I1{}, s + 1);
     }
     if (part_sum) {
         float* cs = reinterpret_cast<float*>(smem4);

@@ -67,11 +67,41 @@ struct TileX3 {
     }
 };
 
-// acc = (Xh + Xl)(Wh + Wl)^T for the block's 64 rows (dropping Xl Wl), scaled by s_x s_w
+// A layer's first two 16-deep weight steps (the queue mfma_layer_x3 starts from).  Issued by the caller ahead of an
+// epilogue's HBM stores (mfma_prefetch_x3, then the stores, then the layer), the layer's first MFMAs wait for these
+// loads alone: the memory counter retires in order, so weight loads issued after a burst of stores wait for every
+// store's completion (one full HBM write latency per layer, measured on the update's kernels).
+template <int H, int KD = H>
+struct WQueue {
+    uint4 bh0[Geo<H>::CT], bl0[Geo<H>::CT], bh1[Geo<H>::CT], bl1[Geo<H>::CT];
+};
+template <int H, int KD = H>
+__device__ __forceinline__ const uint4* wlane_base(const uint4* __restrict__ Wp, int wave, int lane) {
+    // lane's 32 B of (ct, s): uint4 index ((ct S + s) 64 + lane) 2 + {0: hi, 1: lo}
+    return Wp + ((size_t)(wave * Geo<H>::CT) * GeoX3<KD>::S * 64 + lane) * 2;
+}
+template <int H, int KD = H>
+__device__ __forceinline__ WQueue<H, KD> mfma_prefetch_x3(const uint4* __restrict__ Wp, int wave, int lane) {
+    constexpr int CT = Geo<H>::CT, S = GeoX3<KD>::S;
+    const uint4* wb = wlane_base<H, KD>(Wp, wave, lane);
+    auto wld = [&](int c, int s, int part) { return wb[((size_t)(c * S + s) * 64) * 2 + part]; };
+    WQueue<H, KD> q;
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+        q.bh0[c] = wld(c, 0, 0);
+        q.bl0[c] = wld(c, 0, 1);
+        q.bh1[c] = S > 1 ? wld(c, 1, 0) : q.bh0[c];
+        q.bl1[c] = S > 1 ? wld(c, 1, 1) : q.bl0[c];
+    }
+    return q;
+}
+
+// acc = (Xh + Xl)(Wh + Wl)^T for the block's 64 rows (dropping Xl Wl), scaled by s_x s_w; starting from the weight
+// queue q (mfma_prefetch_x3 of the same Wp)
 // PIN: fence the MFMA block of each step with scheduling barriers (below); measured per kernel
 template <int H, int KD = H, bool ZERO = true, bool PIN = true>
 __device__ __forceinline__ void mfma_layer_x3(const TileX3& X, const uint4* __restrict__ Wp, f32x16 (&acc)[RT][Geo<H>::CT],
-                                              int wave, int lane) {
+                                              int wave, int lane, const WQueue<H, KD>& q) {
     constexpr int CT = Geo<H>::CT, S = GeoX3<KD>::S;
     if constexpr (ZERO) {
 #pragma unroll
@@ -82,8 +112,7 @@ __device__ __forceinline__ void mfma_layer_x3(const TileX3& X, const uint4* __re
                 for (int r = 0; r < 16; ++r) acc[rt][c][r] = 0.f;
     }
     const int aoff = (lane & 31) * X.ld + (lane >> 5) * 8;
-    // lane's 32 B of (ct, s): uint4 index ((ct S + s) 64 + lane) 2 + {0: hi, 1: lo}
-    const uint4* wb = Wp + ((size_t)(wave * CT) * S * 64 + lane) * 2;
+    const uint4* wb = wlane_base<H, KD>(Wp, wave, lane);
     auto wld = [&](int c, int s, int part) { return wb[((size_t)(c * S + s) * 64) * 2 + part]; };
     auto ald = [&](const _Float16* t, int rt, int s) {
         return *reinterpret_cast<const f16x8*>(t + aoff + rt * 32 * X.ld + 16 * s);
@@ -91,10 +120,10 @@ __device__ __forceinline__ void mfma_layer_x3(const TileX3& X, const uint4* __re
     uint4 bh0[CT], bl0[CT], bh1[CT], bl1[CT];
 #pragma unroll
     for (int c = 0; c < CT; ++c) {
-        bh0[c] = wld(c, 0, 0);
-        bl0[c] = wld(c, 0, 1);
-        bh1[c] = S > 1 ? wld(c, 1, 0) : bh0[c];
-        bl1[c] = S > 1 ? wld(c, 1, 1) : bl0[c];
+        bh0[c] = q.bh0[c];
+        bl0[c] = q.bl0[c];
+        bh1[c] = q.bh1[c];
+        bl1[c] = q.bl1[c];
     }
     f16x8 ahn[RT], aln[RT];
 #pragma unroll
@@ -140,6 +169,12 @@ __device__ __forceinline__ void mfma_layer_x3(const TileX3& X, const uint4* __re
     }
 }
 
+template <int H, int KD = H, bool ZERO = true, bool PIN = true>
+__device__ __forceinline__ void mfma_layer_x3(const TileX3& X, const uint4* __restrict__ Wp, f32x16 (&acc)[RT][Geo<H>::CT],
+                                              int wave, int lane) {
+    mfma_layer_x3<H, KD, ZERO, PIN>(X, Wp, acc, wave, lane, mfma_prefetch_x3<H, KD>(Wp, wave, lane));
+}
+
 // Y = tanh(acc / (s_x s_w) + bias4(i, n0)), stored scaled by X3_SX as hi / lo; out(i, n0, y4) also receives the
 // fp32 values (four consecutive columns of row i)
 struct NoOut {
@@ -165,6 +200,51 @@ __device__ __forceinline__ void store_tanh_x3(const TileX3& Y, const f32x16 (&ac
                 out(i, n0, y);
                 Y.put4(i, n0, make_float4(X3_SX * y.x, X3_SX * y.y, X3_SX * y.z, X3_SX * y.w));   // (exact: 2^8)
             }
+    }
+}
+
+// The embedding's last epilogue: e2 = tanh(acc / (s_x s_w) + b_e2) to HBM (rows < MU of the data) and as fp32 into
+// LDS (over the split tile: call after the barrier that follows the layer's last tile read), then e_mean[agent] = (sum_k
+// e2 rows of the agent) / K (torch's mean: the sum in k order, times 1 / K) as float4 per thread.
+template <int H>
+__device__ __forceinline__ void embed_e2_epilogue(const f32x16 (&acc)[RT][Geo<H>::CT], const float* bias, float* e2,
+                                                  float* e_mean, float4* smem4, long row0, int MU, long R, int B, int K,
+                                                  int AB, int wave, int lane, int tid) {
+    constexpr int CT = Geo<H>::CT, LDY = H + 4;
+    static_assert(MROWS * (H + 4) * 4 <= 2 * MROWS * GeoX3<H>::LDH * 2, "fp32 tile fits the split tile's bytes");
+    float* Y = reinterpret_cast<float*>(smem4);
+    constexpr float inv_s = 1.f / (X3_SX * X3_SW);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+        const int i = acc_i(rt, lane);
+#pragma unroll
+        for (int c = 0; c < CT; ++c)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int n0 = acc_n0<H>(wave, c, g, lane);
+                const float4 b = lds4(bias + n0);
+                const float4 y = make_float4(tanh_fast(fmaf(acc[rt][c][4 * g], inv_s, b.x)),
+                                             tanh_fast(fmaf(acc[rt][c][4 * g + 1], inv_s, b.y)),
+                                             tanh_fast(fmaf(acc[rt][c][4 * g + 2], inv_s, b.z)),
+                                             tanh_fast(fmaf(acc[rt][c][4 * g + 3], inv_s, b.w)));
+                if (i < MU && row0 + i < R) *reinterpret_cast<float4*>(e2 + (row0 + i) * H + n0) = y;
+                *reinterpret_cast<float4*>(Y + i * LDY + n0) = y;
+            }
+    }
+    __syncthreads();
+    const float inv = 1.f / (float)K;
+    constexpr int H4 = H / 4;
+    for (int e = tid; e < AB * H4; e += NTHR) {
+        const int a = e / H4, c4 = e - a * H4;
+        const long agent = row0 / K + a;
+        if (agent < B) {
+            float4 s = lds4(Y + (a * K) * LDY + 4 * c4);
+            for (int k = 1; k < K; ++k) {
+                const float4 v = lds4(Y + (a * K + k) * LDY + 4 * c4);
+                s = make_float4(s.x + v.x, s.y + v.y, s.z + v.z, s.w + v.w);
+            }
+            *reinterpret_cast<float4*>(e_mean + agent * H + 4 * c4) = make_float4(s.x * inv, s.y * inv, s.z * inv, s.w * inv);
+        }
     }
 }
 
@@ -207,24 +287,9 @@ __global__ __launch_bounds__(NTHR, 2) __attribute__((amdgpu_waves_per_eu(2, 2)))
     __syncthreads();
     mfma_layer_x3<H, H, true, QS_EMBED_PIN != 0>(X, reinterpret_cast<const uint4*>(t.w_e2p), acc, wave, lane);
     __syncthreads();   // every wave has read the tile
-    // e2 to HBM straight from the epilogue (fp32 tanh values; the pool's split of them is the tile's hi / lo, so
-    // its products are the same) -- no read-back of the split tile
-    store_tanh_x3<H>(X, acc, 1.f / (X3_SX * X3_SW), wave, lane, [&](int, int n0) { return lds4(BI + H + n0); },
-                     [&](int i, int n0, float4 y) {
-                         if (i < MU && row0 + i < R) *reinterpret_cast<float4*>(t.e2 + (row0 + i) * H + n0) = y;
-                     });
-    __syncthreads();
-    constexpr float isx = 1.f / X3_SX;
-    const float inv = 1.f / (float)K;   // torch's mean: the sum times 1 / K
-    for (int e = tid; e < AB * H; e += NTHR) {
-        const int a = e / H, n = e - a * H;
-        const long agent = row0 / K + a;
-        if (agent < B) {
-            float s = 0.f;
-            for (int k = 0; k < K; ++k) s += X.get(a * K + k, n) * isx;
-            t.e_mean[agent * H + n] = s * inv;
-        }
-    }
+    // e2 to HBM straight from the epilogue (fp32 tanh values) and into an fp32 tile over the split tile's bytes
+    // (the last layer: the split tile is not read again), whose rows the per-agent means then read as float4
+    embed_e2_epilogue<H>(acc, BI + H, t.e2, t.e_mean, smem4, row0, MU, R, B, K, AB, wave, lane, tid);
 }
 
 // the block's e2 rows (fp32, HBM) into the split tile (zero rows past the data)
@@ -348,13 +413,13 @@ __global__ __launch_bounds__(NTHR, 2) __attribute__((amdgpu_waves_per_eu(2, 2)))
             }
     }
     __syncthreads();
-    for (int e = tid; e < AB * H; e += NTHR) {
-        const int a = e / H, n = e - a * H;
+    for (int e = tid; e < AB * (H / 4); e += NTHR) {   // the agent's weighted rows summed in k order, float4 wide
+        const int a = e / (H / 4), c4 = e - a * (H / 4);
         const long agent = row0 / K + a;
         if (agent < B) {
-            float s = 0.f;
-            for (int k = 0; k < K; ++k) s += Y[(a * K + k) * LDY + n];
-            t.out[agent * H + n] = s;
+            float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int k = 0; k < K; ++k) s = f4_add(s, lds4(Y + (a * K + k) * LDY + 4 * c4));
+            *reinterpret_cast<float4*>(t.out + agent * H + 4 * c4) = s;
         }
     }
 }

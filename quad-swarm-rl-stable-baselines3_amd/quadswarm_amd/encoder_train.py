@@ -168,7 +168,8 @@ class _Runner:
                      w_e2tp=pack_mfma_weight_x3(w["e2_w"].t()),
                      b_e1=w["e1_b"].detach().contiguous(), b_e2=w["e2_b"].detach().contiguous(),
                      b_v1=w["v1_b"].detach().contiguous(), b_v2=w["v2_b"].detach().contiguous(),
-                     b_a2=w["a2_b"].detach().contiguous(), w_a3=w["a3_w"].detach().reshape(-1).contiguous())
+                     b_a2=w["a2_b"].detach().contiguous(), w_a3=w["a3_w"].detach().reshape(-1).contiguous(),
+                     a_m=w["a1_w"][:, H:].detach().contiguous())
             self.keep.append(k)
             t = self.towers[i]
             t.w_e1p, t.b_e1, t.w_e2p, t.b_e2 = p(k["w_e1p"]), p(k["b_e1"]), p(k["w_e2p"]), p(k["b_e2"])
@@ -199,9 +200,8 @@ class _Runner:
         H, K, so, st = self.H, self.K, self.so, self.stream(obs.device)
         NAT.check(self.L.qs_attn_embed_train_x3(ctypes.c_void_p(obs.data_ptr()), obs.shape[1], so, so, B, K, self.nd, H,
                                                 self.towers, self.trains, self.T, st), "qs_attn_embed_train_x3")
-        for i in range(self.T):
-            a1_w, a1_b = params[14 * i + 8], params[14 * i + 9]
-            torch.addmm(a1_b, self.buf[i]["e_mean"], a1_w[:, H:].t(), out=self.buf[i]["P"])
+        for i in range(self.T):   # P = e_mean A_m^T + b_a1 (A_m contiguous: the strided slice picks a 4x slower GEMM)
+            torch.addmm(params[14 * i + 9], self.buf[i]["e_mean"], self.keep[i]["a_m"].t(), out=self.buf[i]["P"])
         NAT.check(self.L.qs_attn_pool_train_x3(B, K, H, self.towers, self.trains, self.T, st), "qs_attn_pool_train_x3")
         self.pending = True
         return [self.buf[i]["out"].clone() for i in range(self.T)]
@@ -231,10 +231,9 @@ class _Runner:
             gi["a3_w"] = b["a3w_part"].sum(0).view(1, -1) if self.dw_x3 else b["dscore"].view(1, -1).mm(b["a2"])
             gi["a3_b"] = b["dscore"].sum().view(1)
             dP = b["da1_pre"].view(K, B, H).sum(0)                     # rows j with j % B == b (the repeat tiling)
-            a1_w = params[w0 + 8]
             dA_e, gi["a1_b"] = self.dw(b["da1_pre"], b["e2"], cm[3])   # a1_b = sum_j da1_pre_j = sum_b dP_b
             gi["a1_w"] = torch.cat((dA_e, self.dw(dP, b["e_mean"])[0]), dim=1)   # |e_mean| <= 1 (a mean of tanh)
-            torch.mm(dP, a1_w[:, H:], out=b["dem"])                    # dL/d e_mean
+            torch.mm(dP, self.keep[i]["a_m"], out=b["dem"])            # dL/d e_mean
             for n in gi:
                 grads[w0 + _PARAMS.index(n)] = gi[n]
         NAT.check(self.L.qs_attn_bwd2_x3(B, K, H, self.towers, self.trains, self.T, st), "qs_attn_bwd2_x3")

@@ -194,7 +194,8 @@ for s in "$@"; do
         if [ "$v" = base ]; then unset QUADSWARM_LIB; else
           export QUADSWARM_LIB=$PWD/quad-swarm-rl-stable-baselines3_amd/quadswarm_amd/lib/ab/libquadswarm_$v.so; fi
         step polab_$v 500 rocprofv3 --kernel-trace --stats -d gpurun_out/polab_$v -o e2e --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline --e2e-iters 1
-        python3 tools/kstats.py gpurun_out/polab_$v 24 > gpurun_out/polab_${v}_summary.txt 2>&1
+        python3 tools/kstats.py gpurun_out/polab_$v 40 > gpurun_out/polab_${v}_summary.txt 2>&1
+        python3 tools/e2e_split.py gpurun_out/polab_$v --top 40 > gpurun_out/polab_${v}_split.txt 2>&1
         find gpurun_out/polab_$v -name "*kernel_trace.csv" -delete
       done
       unset QUADSWARM_LIB

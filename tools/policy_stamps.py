@@ -20,7 +20,7 @@ POOL = ["load e2", "P + mfma a1", "sync + tanh store", "mfma a2", "sync + tanh s
 
 def report(L, name, names, nb):
     buf = np.zeros(65536 * 32, np.uint64)
-    assert L.qs_debug_stamps(buf.ctypes.data, buf.size) == 0
+    assert L.qs_debug_stamps_policy(buf.ctypes.data, buf.size) == 0
     st = buf.reshape(65536, 32)[:nb].astype(np.int64)
     rt = st[:, 12:14]
     t0 = rt[:, 0].min()
@@ -44,7 +44,7 @@ def main():
     fp = FusedRolloutPolicy(pol)
     obs = torch.randn(B, 54, device="cuda")
     L = N.lib()
-    L.qs_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    L.qs_debug_stamps_policy.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
     nb = -(-B * 6 // 60)
     with torch.no_grad():
         for _ in range(3):
