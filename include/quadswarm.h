@@ -537,12 +537,16 @@ int qs_attn_bwd2_x3(int32_t B, int32_t K, int32_t H, const qs_attn_tower* towers
  * is their sum over p) from the same pass. */
 int qs_attn_dw_x3(const float* G, const float* A, const float* col_scale, int64_t R, int32_t H, float* part,
                   float* part_sum, int32_t n_parts, void* stream);
+/* The maxima over the blocks of per-block column maxima (ABI 15; qs_attn_train.colmax rows): out[s][n] =
+ * max_b part_max[s][b][n] for s < n_stats (entries >= 0, +inf propagates), part_max [n_stats][n_blocks][H]. */
+int qs_colmax_reduce(const float* part_max, int32_t n_stats, int32_t n_blocks, int32_t H, float* out, void* stream);
 /* Layer 0's weight gradient (ABI 15): part[p] = G[rows of p]^T X[rows of p] ([n_parts, H, 32] fp32; the sum over p
  * is the gradient of embedding layer 0's weight in the kernels' column order [neighbour (nd) | self (self_dim) | 0])
  * with X the layer-0 input rows the forward gathers (row r = agent r / K, neighbour r % K of that agent's block at
  * nbr_off, self features of agent r % B -- the reference's repeat pairing, quad_multi_model.py:44-101), G = de1_pre
  * [B K, H] with col_scale as qs_attn_dw_x3, |obs| < 4094 (the forward's split-f16 range); part_sum (NULL: not
- * written): [n_parts, H] G's column sums (the bias gradient's parts).  nd + self_dim <= 32. */
+ * written): [n_parts, H] G's column sums (the bias gradient's parts).  nd + self_dim <= 32; nd = 0 with K = 1: the self
+ * features alone (the self encoder's first layer, rows = agents). */
 int qs_attn_dw0_x3(const float* G, const float* col_scale, const float* d_obs, int32_t obs_stride, int32_t self_dim,
                    int32_t nbr_off, int32_t B, int32_t K, int32_t nd, int32_t H, float* part, float* part_sum,
                    int32_t n_parts, void* stream);

@@ -249,12 +249,25 @@ extern "C" int qs_attn_dw0_x3(const float* G, const float* col_scale, const floa
     if (H != 128 && H != 256) return fail(QS_E_INVALID, "hidden size must be 128 or 256");
     if (B < 1 || K < 1 || (int64_t)B * K >= (1ll << 31) || n_parts < 1 || n_parts > 65535)
         return fail(QS_E_INVALID, "B, K >= 1, B K < 2^31, 1 <= n_parts <= 65535");
-    if (nd < 1 || so < 1 || nd + so > P::KD0) return fail(QS_E_INVALID, "nd, self_dim >= 1, nd + self_dim <= 32");
+    if (nd < 0 || so < 1 || nd + so > P::KD0) return fail(QS_E_INVALID, "nd >= 0, self_dim >= 1, nd + self_dim <= 32");
     if (so > stride || off < 0 || off + (int64_t)K * nd > stride)
         return fail(QS_E_INVALID, "self features and the neighbour block must lie inside the obs row");
     hipStream_t st = (hipStream_t)stream;
     return H == 256 ? dw0_launch<256>(G, col_scale, obs, stride, so, off, B, K, nd, part, part_sum, n_parts, st)
                     : dw0_launch<128>(G, col_scale, obs, stride, so, off, B, K, nd, part, part_sum, n_parts, st);
+}
+extern "C" int qs_colmax_reduce(const float* part_max, int32_t n_stats, int32_t n_blocks, int32_t H, float* out,
+                                void* stream) {
+    namespace P = qs::pol;
+    if (!part_max || !out) return fail(QS_E_INVALID, "NULL argument");
+    if (n_stats < 1 || n_stats > QS_ATTN_NCOLMAX || n_blocks < 1 || H < 1 || H > 4096)
+        return fail(QS_E_INVALID, "1 <= n_stats <= QS_ATTN_NCOLMAX, n_blocks >= 1, 1 <= H <= 4096");
+    hipStream_t st = (hipStream_t)stream;
+    QS_HIP(hipMemsetAsync(out, 0, (size_t)n_stats * H * sizeof(float), st));
+    hipLaunchKernelGGL(P::colmax_reduce_kernel, dim3(P::CM_CHUNKS, (unsigned)((H + 63) / 64), (unsigned)n_stats),
+                       dim3(256), 0, st, part_max, n_blocks, H, out);
+    QS_HIP(hipGetLastError());
+    return QS_OK;
 }
 extern "C" int qs_colstats(const float* G, int64_t R, int32_t H, const float* row_w, const float* obs, int32_t stride,
                            int32_t nbr_off, int32_t B, int32_t K, int32_t nd, int32_t nx, float* pmx, float* psm,

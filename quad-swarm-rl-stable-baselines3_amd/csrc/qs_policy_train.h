@@ -997,6 +997,34 @@ __global__ __launch_bounds__(NTHR, 2) void dw0_x3_kernel(const float* __restrict
 }
 
 // ------------------------------------------------------------------------------------------------------------------
+// the maxima over the blocks of the backward's per-block column maxima (qs_colmax_reduce): block (s, c, q) takes
+// stat s, 64 columns c, every CM_CHUNKS-th row chunk q; thread (r, n): column 64 c + n, rows r, r + 4, ... of the
+// chunk (a row's 64 columns are one 256-byte read per wave); the four row lanes through LDS, then one unsigned-bits
+// atomic max per column and block into out (zeroed by the launcher; maxima of non-negative floats, order-free)
+// ------------------------------------------------------------------------------------------------------------------
+constexpr int CM_CHUNKS = 16;
+__global__ __launch_bounds__(256) void colmax_reduce_kernel(const float* __restrict__ part, int nblk, int H,
+                                                            float* __restrict__ out) {
+    __shared__ float red[256];
+    const int s = blockIdx.z, c = blockIdx.y, q = blockIdx.x;
+    const int n = threadIdx.x & 63, r = threadIdx.x >> 6, col = 64 * c + n;
+    const long rows_per = (nblk + CM_CHUNKS - 1) / CM_CHUNKS;
+    const long r0 = q * rows_per, r1 = r0 + rows_per < nblk ? r0 + rows_per : nblk;
+    float m = 0.f;
+    if (col < H) {
+        const float* p = part + (size_t)s * nblk * H + col;
+#pragma unroll 4
+        for (long b = r0 + r; b < r1; b += 4) m = fmaxf(m, p[b * H]);   // inf stays inf; the entries are >= 0
+    }
+    red[threadIdx.x] = m;
+    __syncthreads();
+    if (r == 0 && col < H) {
+        m = fmaxf(fmaxf(red[n], red[64 + n]), fmaxf(red[128 + n], red[192 + n]));
+        atomicMax(reinterpret_cast<unsigned int*>(out) + (size_t)s * H + col, __float_as_uint(m));
+    }
+}
+
+// ------------------------------------------------------------------------------------------------------------------
 // column reductions of a gradient G [R, H] (qs_colstats): block p walks rows [p rows_per, (p+1) rows_per), thread n
 // owns column n (blockDim = H): a coalesced row of H floats per step, max |g|, sum w_r g (w: optional row weights)
 // and, with NX > 0, sum g X(r, c) with the layer-0 input X of row r = q K + m (neighbour m of agent q; self row

@@ -25,7 +25,7 @@ import ctypes
 import torch
 
 from . import _native as NAT
-from .policy_fused import F16_MAX, X3_SIN, pack_mfma_weight_x3, supports
+from .policy_fused import F16_MAX, X3_SIN, pack_mfma_weight_x3, pack_mfma_weights_x3, supports  # noqa: F401
 
 _PARAMS = ("e1_w", "e1_b", "e2_w", "e2_b", "v1_w", "v1_b", "v2_w", "v2_b", "a1_w", "a1_b", "a2_w", "a2_b", "a3_w", "a3_b")
 
@@ -72,6 +72,17 @@ def col_stats(G, obs=None, B=0, K=0, nbr_off=0, nd=0, nx=0, parts=None, row_w=No
                                     ctypes.c_void_p(px.data_ptr() if px is not None else 0), parts, st),
               "qs_colstats")
     return _pow2_scales(pmx.amax(0)), psm.sum(0), (px.sum(0) if px is not None else None)
+
+
+def colmax_scales(part_max):
+    """dW column scales from per-block column maxima [n_stats, n_blocks, H] (qs_attn_train.colmax rows): the max over
+    the blocks (qs_colmax_reduce), then the power-of-two scales -> [n_stats, H]."""
+    ns, nb, H = part_max.shape
+    out = torch.empty(ns, H, dtype=torch.float32, device=part_max.device)
+    st = ctypes.c_void_p(torch.cuda.current_stream(part_max.device).cuda_stream)
+    NAT.check(NAT.lib().qs_colmax_reduce(ctypes.c_void_p(part_max.data_ptr()), ns, nb, H, ctypes.c_void_p(out.data_ptr()),
+                                         st), "qs_colmax_reduce")
+    return _pow2_scales(out)
 
 
 def dw_x3(G, A, parts=256, out=None, gs=None, sums=False):
@@ -127,14 +138,14 @@ class _Runner:
         self.pending = False
         self.dw_x3 = True   # the weight gradients on the split-f16 matrix cores (else torch fp32 GEMMs)
 
-    def dw(self, G, A, cm=None):
-        """(dW = G^T A over the B K rows (A: tanh outputs), the bias gradient sum_r G[r, :]).  cm: G's per-block column
-        maxima from the kernel that wrote G (qs_attn_train.colmax, [n_blocks, H]): then one pass over G and A (the
-        sums from the dW pass), else a column-statistics pass first."""
+    def dw(self, G, A, gs=None):
+        """(dW = G^T A over the B K rows (A: tanh outputs), the bias gradient sum_r G[r, :]).  gs: G's column scales
+        from the maxima the kernels that wrote G formed (colmax_scales): then one pass over G and A (the sums from the
+        dW pass), else a column-statistics pass first."""
         if not self.dw_x3:
             return G.t().mm(A), G.sum(0)
-        if cm is not None:
-            return dw_x3(G, A, gs=_pow2_scales(cm.amax(0)), sums=True)
+        if gs is not None:
+            return dw_x3(G, A, gs=gs, sums=True)
         gs, sums, _ = col_stats(G)
         return dw_x3(G, A, gs=gs), sums
 
@@ -150,23 +161,27 @@ class _Runner:
                          colmax=z(NAT.ATTN_NCOLMAX, nblk, H), a3w_part=z(nblk, H)) for _ in range(T)]
 
     def _pack(self, params):
-        """x3-pack the towers' weights (forward operands and the backward's transposes), bind every pointer."""
+        """x3-pack the towers' weights (forward operands and the backward's transposes; both towers' 22 matrices as
+        one batched pack with one range check), bind every pointer."""
         H, so, nd = self.H, self.so, self.nd
         p = lambda t: t.data_ptr()  # noqa: E731
         self.keep = []
+        names = ("w_e1p", "w_e2p", "w_v1p", "w_v2p", "w_a1ep", "w_a2p", "w_v2tp", "w_v1tp", "w_a2tp", "w_a1etp",
+                 "w_e2tp")
+        ws, mats = [], []
         for i in range(self.T):
             w = dict(zip(_PARAMS, params[14 * i:14 * i + 14]))
-            b = self.buf[i]
             w_e1 = torch.zeros(H, 32, dtype=torch.float32, device=w["e1_w"].device)   # [neighbour | self | 0]
             w_e1[:, :nd] = w["e1_w"][:, so:]
             w_e1[:, nd:nd + so] = w["e1_w"][:, :so]
-            k = dict(w_e1p=pack_mfma_weight_x3(w_e1), w_e2p=pack_mfma_weight_x3(w["e2_w"]),
-                     w_v1p=pack_mfma_weight_x3(w["v1_w"]), w_v2p=pack_mfma_weight_x3(w["v2_w"]),
-                     w_a1ep=pack_mfma_weight_x3(w["a1_w"][:, :H]), w_a2p=pack_mfma_weight_x3(w["a2_w"]),
-                     w_v2tp=pack_mfma_weight_x3(w["v2_w"].t()), w_v1tp=pack_mfma_weight_x3(w["v1_w"].t()),
-                     w_a2tp=pack_mfma_weight_x3(w["a2_w"].t()), w_a1etp=pack_mfma_weight_x3(w["a1_w"][:, :H].t()),
-                     w_e2tp=pack_mfma_weight_x3(w["e2_w"].t()),
-                     b_e1=w["e1_b"].detach().contiguous(), b_e2=w["e2_b"].detach().contiguous(),
+            ws.append(w)
+            mats += [w_e1, w["e2_w"], w["v1_w"], w["v2_w"], w["a1_w"][:, :H], w["a2_w"], w["v2_w"].t(), w["v1_w"].t(),
+                     w["a2_w"].t(), w["a1_w"][:, :H].t(), w["e2_w"].t()]
+        packed = pack_mfma_weights_x3(mats)
+        for i in range(self.T):
+            w, b = ws[i], self.buf[i]
+            k = dict(zip(names, packed[len(names) * i:len(names) * (i + 1)]))
+            k.update(b_e1=w["e1_b"].detach().contiguous(), b_e2=w["e2_b"].detach().contiguous(),
                      b_v1=w["v1_b"].detach().contiguous(), b_v2=w["v2_b"].detach().contiguous(),
                      b_a2=w["a2_b"].detach().contiguous(), w_a3=w["a3_w"].detach().reshape(-1).contiguous(),
                      a_m=w["a1_w"][:, H:].detach().contiguous())
@@ -222,16 +237,16 @@ class _Runner:
         grads = [None] * (14 * self.T)
         for i in range(self.T):
             b, w0 = self.buf[i], 14 * i
-            cm = b["colmax"]   # the gradients' per-block column maxima, from the kernels that wrote them
+            gsc = colmax_scales(b["colmax"][:4])   # the gradients' column scales (per-block maxima from backward 1)
             gi = {}
-            gi["v2_w"], gi["v2_b"] = self.dw(b["dh_pre"], b["v1"], cm[0])
-            gi["v1_w"], gi["v1_b"] = self.dw(b["dv1_pre"], b["e2"], cm[1])
-            gi["a2_w"], gi["a2_b"] = self.dw(b["da2_pre"], b["a1"], cm[2])
+            gi["v2_w"], gi["v2_b"] = self.dw(b["dh_pre"], b["v1"], gsc[0])
+            gi["v1_w"], gi["v1_b"] = self.dw(b["dv1_pre"], b["e2"], gsc[1])
+            gi["a2_w"], gi["a2_b"] = self.dw(b["da2_pre"], b["a1"], gsc[2])
             # sum_j dscore_j a2_j: backward 1's per-block partial sums
             gi["a3_w"] = b["a3w_part"].sum(0).view(1, -1) if self.dw_x3 else b["dscore"].view(1, -1).mm(b["a2"])
             gi["a3_b"] = b["dscore"].sum().view(1)
             dP = b["da1_pre"].view(K, B, H).sum(0)                     # rows j with j % B == b (the repeat tiling)
-            dA_e, gi["a1_b"] = self.dw(b["da1_pre"], b["e2"], cm[3])   # a1_b = sum_j da1_pre_j = sum_b dP_b
+            dA_e, gi["a1_b"] = self.dw(b["da1_pre"], b["e2"], gsc[3])   # a1_b = sum_j da1_pre_j = sum_b dP_b
             gi["a1_w"] = torch.cat((dA_e, self.dw(dP, b["e_mean"])[0]), dim=1)   # |e_mean| <= 1 (a mean of tanh)
             torch.mm(dP, self.keep[i]["a_m"], out=b["dem"])            # dL/d e_mean
             for n in gi:
@@ -242,11 +257,12 @@ class _Runner:
         for i in range(self.T):
             b, w0 = self.buf[i], 14 * i
             de2_pre, de1_pre = b["de2p"], b["dh_pre"]
-            grads[w0 + 2], grads[w0 + 3] = self.dw(de2_pre, b["e1"], b["colmax"][4])
+            gsc2 = colmax_scales(b["colmax"][4:])   # de2_pre's and de1_pre's (backward 2)
+            grads[w0 + 2], grads[w0 + 3] = self.dw(de2_pre, b["e1"], gsc2[0])
             # embedding_mlp[0] on cat(self_{j % B}, nbr_j): both halves and the bias gradient in one pass over
             # de1_pre with the layer-0 rows gathered as the forward gathers them
             if self.dw_x3:
-                grads[w0], grads[w0 + 1] = dw0_x3(de1_pre, obs, B, K, so, nd, gs=_pow2_scales(b["colmax"][5].amax(0)))
+                grads[w0], grads[w0 + 1] = dw0_x3(de1_pre, obs, B, K, so, nd, gs=gsc2[1])
             else:
                 g_self = de1_pre.view(K, B, H).sum(0).t().mm(self_obs)
                 grads[w0] = torch.cat((g_self, de1_pre.t().mm(nbr_rows)), dim=1)
@@ -267,6 +283,27 @@ class _AttnTrainFn(torch.autograd.Function):
         return (None, None) + tuple(ctx.runner.backward(douts))
 
 
+class _SelfLayer0Fn(torch.autograd.Function):
+    """The self encoder's first Linear (self_obs [B, so] -> [B, R]) with its weight gradient on the split-f16 matrix
+    cores: forward F.linear; backward dW = G^T self_obs by qs_attn_dw0_x3 (rows = agents: K 1, no neighbour
+    features; G's column scales and the bias gradient from one column-statistics pass) in place of the skinny
+    [R x B] x [B x so] GEMM.  No input gradient (observations)."""
+
+    @staticmethod
+    def forward(ctx, obs, weight, bias, so):
+        ctx.save_for_backward(obs)
+        ctx.so = so
+        return torch.nn.functional.linear(obs[:, :so], weight, bias)
+
+    @staticmethod
+    def backward(ctx, g):
+        (obs,) = ctx.saved_tensors
+        g = g.contiguous()
+        gs, sums, _ = col_stats(g)
+        dW, db = dw0_x3(g, obs, obs.shape[0], 1, ctx.so, 0, gs=gs)
+        return None, dW, sums, None
+
+
 class FusedAttentionTrain:
     """Both towers' neighbour-encoder outputs for the PPO update as one autograd node on the HIP kernels:
     encodings(obs) -> [actor [B, H], critic [B, H]] (SwarmActorCritic.evaluate_actions(obs, actions, nbr=...)).  One
@@ -280,6 +317,15 @@ class FusedAttentionTrain:
 
     def params(self):
         return [p for enc in self.runner.encs for p in tower_params(enc)]
+
+    def self_layer0(self, lin, obs):
+        """The self encoder's first Linear of one tower on the full observation rows (QuadMultiEncoder.forward's l0
+        hook), its weight gradient on the matrix cores (_SelfLayer0Fn).  obs: the minibatch [B, obs_dim] (inside the
+        split-f16 range: obs_in_range)."""
+        so = self.runner.so
+        if lin.out_features not in (128, 256) or so > 32:   # the kernel's shapes; else torch
+            return lin(obs[:, :so])
+        return _SelfLayer0Fn.apply(obs.contiguous(), lin.weight, lin.bias, so)
 
     def obs_in_range(self, obs):
         """True when every value of `obs` (e.g. the whole rollout storage, once per update) is inside the split-f16

@@ -52,6 +52,39 @@ def pack_mfma_weight_x3(w):
     return torch.stack((lay(hi), lay(lo)), dim=3).contiguous().view(torch.int16)
 
 
+def pack_mfma_weights_x3(ws):
+    """pack_mfma_weight_x3 of several weights at once: those of one shape packed as one batch, the range of all of
+    them checked with one host read (the update packs 22 matrices per minibatch).  Same layout, same ValueError."""
+    groups = {}
+    for i, w in enumerate(ws):
+        groups.setdefault(tuple(w.shape), []).append(i)
+    out = [None] * len(ws)
+    scaled = {}
+    peak = []
+    for shape, idx in groups.items():
+        n, kd = shape
+        assert n % 32 == 0 and kd % 16 == 0, shape
+        x = torch.stack([ws[i].detach().float() for i in idx]) * X3_SW
+        scaled[shape] = x
+        peak.append(x.abs().amax())
+    if not bool(torch.stack(peak).amax() < F16_MAX):   # NaN fails too
+        m = max(float(w.detach().abs().amax()) for w in ws)
+        raise ValueError(f"x3 packing: max |w| = {m:.4g} is outside the split-f16 range (< {F16_MAX / X3_SW:.4g})")
+    for shape, idx in groups.items():
+        n, kd = shape
+        x = scaled[shape]
+        hi = x.half()
+        lo = (x - hi.float()).half()
+        g = len(idx)
+
+        def lay(t):   # [g, n, kd] -> [g, ct, s, h, r, j] -> [g, ct, s, l = 32 h + r, j]
+            return t.view(g, n // 32, 32, kd // 16, 2, 8).permute(0, 1, 3, 4, 2, 5).reshape(g, n // 32, kd // 16, 64, 8)
+        packed = torch.stack((lay(hi), lay(lo)), dim=4).contiguous().view(torch.int16)
+        for j, i in enumerate(idx):
+            out[i] = packed[j]
+    return out
+
+
 def supports(policy):
     """Can the fused kernels evaluate this policy's encoders?"""
     c = policy.cfg

@@ -193,11 +193,15 @@ class QuadMultiEncoder(nn.Module):
         self.feed_forward = nn.Sequential(nn.Linear(out, 2 * R), nn.Tanh())
         self.out_size = 2 * R
 
-    def forward(self, obs, nbr_out=None):
-        """nbr_out: the neighbour encoder's output computed elsewhere (the fused update, encoder_train.py)."""
+    def forward(self, obs, nbr_out=None, l0=None):
+        """nbr_out: the neighbour encoder's output computed elsewhere (the fused update, encoder_train.py); l0(lin,
+        obs): the self encoder's first Linear evaluated elsewhere (FusedAttentionTrain.self_layer0)."""
         so, na = self.cfg.self_obs_dim, self.all_neighbor_obs_size
         self_obs = obs[:, :so]
-        parts = [self.self_encoder(self_obs)]
+        if l0 is not None and len(self.self_encoder) > 1:
+            parts = [self.self_encoder[1:](l0(self.self_encoder[0], obs))]
+        else:
+            parts = [self.self_encoder(self_obs)]
         if nbr_out is not None:
             parts.append(nbr_out)
         elif self.neighbor_encoder is not None:
@@ -255,14 +259,15 @@ class SwarmActorCritic(nn.Module):
             actions = torch.tanh(mean + torch.randn_like(mean) * self.log_std.exp())
         return actions, values, squashed_log_prob(mean, self.log_std, actions)
 
-    def evaluate_actions(self, obs, actions, nbr=None):
+    def evaluate_actions(self, obs, actions, nbr=None, l0=None):
         """(values, log_prob, entropy=None) -- ActorCriticPolicyCustom.py:538-566.  nbr: (actor, critic) neighbour
-        encoder outputs from the fused update (encoder_train.FusedAttentionTrain), else the torch encoders run."""
+        encoder outputs from the fused update (encoder_train.FusedAttentionTrain), else the torch encoders run;
+        l0: the fused update's self-encoder first layer (FusedAttentionTrain.self_layer0), with nbr only."""
         if nbr is None:
             mean = self.action_net(self.actor_latent(obs))
             return self.predict_values(obs), squashed_log_prob(mean, self.log_std, actions), None
-        mean = self.action_net(self.actor_decoder(self.actor_core(self.actor_encoder(obs, nbr[0]))))
-        values = self.value_net(self.critic_decoder(self.critic_core(self.critic_encoder(obs, nbr[1]))))
+        mean = self.action_net(self.actor_decoder(self.actor_core(self.actor_encoder(obs, nbr[0], l0))))
+        values = self.value_net(self.critic_decoder(self.critic_core(self.critic_encoder(obs, nbr[1], l0))))
         return values, squashed_log_prob(mean, self.log_std, actions), None
 
     def predict(self, obs, deterministic=True):
@@ -563,7 +568,8 @@ class PPOTrainer:
                 idx = perm[s:s + c.batch_size]
                 ob = obs[idx]
                 nbr = fused.encodings(ob) if fused is not None else None
-                values, logp, entropy = pol.evaluate_actions(ob, act[idx], nbr=nbr)
+                values, logp, entropy = pol.evaluate_actions(ob, act[idx], nbr=nbr,
+                                                             l0=fused.self_layer0 if nbr is not None else None)
                 values = values.flatten()
                 adv = adv_all[idx]
                 if c.normalize_advantage and idx.numel() > 1:

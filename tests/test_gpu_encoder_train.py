@@ -17,8 +17,8 @@ torch = pytest.importorskip("torch")
 if not torch.cuda.is_available():  # pragma: no cover
     pytest.skip("no HIP device", allow_module_level=True)
 
-from quadswarm_amd.encoder_train import (FusedAttentionTrain, col_scales, col_stats, dw0_x3, dw_x3,  # noqa: E402
-                                         tower_params)
+from quadswarm_amd.encoder_train import (FusedAttentionTrain, _pow2_scales, col_scales, col_stats,  # noqa: E402
+                                         colmax_scales, dw0_x3, dw_x3, tower_params)
 from quadswarm_amd.ppo import PolicyConfig, SwarmActorCritic  # noqa: E402
 
 
@@ -102,7 +102,8 @@ def test_encoder_gradients_match_torch(case, B):
 @pytest.mark.parametrize("case", ["c3", "a8"])
 def test_ppo_loss_gradient_bucket_matches_torch(case):
     """The whole PPO minibatch step as PPOTrainer.train runs it: evaluate_actions with the fused encoders (nbr=...)
-    vs the torch module -- values, log-probs and every parameter's gradient."""
+    and the self encoder's first layer on the matrix cores (l0=...) vs the torch module -- values, log-probs and every
+    parameter's gradient."""
     pol = fixture_policy(case)
     B = 2048
     obs = obs_for(pol.cfg, B, seed=5)
@@ -114,7 +115,7 @@ def test_ppo_loss_gradient_bucket_matches_torch(case):
         return -(adv * torch.exp(lp - lp.detach())).mean() + 0.5 * (v.view(-1) ** 2).mean()
 
     fused = FusedAttentionTrain(pol)
-    v_f, lp_f, _ = pol.evaluate_actions(obs, act, nbr=fused.encodings(obs))
+    v_f, lp_f, _ = pol.evaluate_actions(obs, act, nbr=fused.encodings(obs), l0=fused.self_layer0)
     gf = torch.autograd.grad(loss_of(v_f, lp_f), list(pol.parameters()), allow_unused=True)
     v_t, lp_t, _ = pol.evaluate_actions(obs, act)
     gt = torch.autograd.grad(loss_of(v_t, lp_t), list(pol.parameters()), allow_unused=True)
@@ -247,7 +248,8 @@ def test_backward_column_statistics(case, B):
     torch.autograd.grad(sum((o * gi).sum() for o, gi in zip(outs, G)), params)
     torch.cuda.synchronize()
     for i, b in enumerate(fused.runner.buf):
-        cm = b["colmax"].amax(1)   # [5, n_blocks, H] -> the maxima over the blocks
+        cm = b["colmax"].amax(1)   # [6, n_blocks, H] -> the maxima over the blocks
+        assert torch.equal(colmax_scales(b["colmax"]), _pow2_scales(cm))   # qs_colmax_reduce
         for row, name in ((1, "dv1_pre"), (2, "da2_pre"), (3, "da1_pre"), (4, "de2p")):
             assert torch.equal(cm[row], b[name].abs().amax(0)), (case, i, name)
         w, h = b["w"], b["h"]
@@ -259,13 +261,14 @@ def test_backward_column_statistics(case, B):
         assert ((got - want).abs() / scale).max().item() < 1e-6, (case, i, "a3w")
 
 
-@pytest.mark.parametrize("H,B,K,parts", [(256, 4099, 6, 512), (128, 777, 1, 5), (256, 300, 7, 4096)])
-def test_dw0_x3_matches_fp64(H, B, K, parts):
+@pytest.mark.parametrize("H,B,K,parts,nd", [(256, 4099, 6, 512, 6), (128, 777, 1, 5, 6), (256, 300, 7, 4096, 6),
+                                             (256, 5000, 1, 512, 0)])
+def test_dw0_x3_matches_fp64(H, B, K, parts, nd):
     """qs_attn_dw0_x3: layer 0's weight gradient sum_j G_j^T [self_{j % B} | nbr_j] (the reference's column order)
     and the bias gradient against fp64, on ragged part splits (empty trailing parts) and column scales spanning
-    2^-20 .. 2^4."""
+    2^-20 .. 2^4; nd = 0, K = 1: the self encoder's first layer."""
     g = torch.Generator(device="cuda").manual_seed(B + K)
-    so, nd = 18, 6
+    so = 18
     R = B * K
     G = torch.randn(R, H, device="cuda", generator=g) * torch.exp2(torch.linspace(-20, 4, H, device="cuda"))
     obs = torch.randn(B, so + K * nd + 3, device="cuda", generator=g) * 3

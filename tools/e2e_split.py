@@ -1,7 +1,8 @@
 #!/usr/bin/env python
 """Split a rocprofv3 kernel trace of one end-to-end PPO iteration (bench.py --e2e-iters 1) into its rollout and its
-update: the update starts at the first attn_embed_train launch; per phase the kernels by total time, with calls and
-time per minibatch for the update (the minibatches are counted by the attn_bwd1 launches).  Diagnostic.
+update: the timed update starts after the last rollout encoder launch, the rollout after the warm-up update; per phase
+the kernels by total time, with calls and time per minibatch for the update (the minibatches are counted by the
+attn_bwd1 launches).  Diagnostic.
 
     python tools/e2e_split.py <trace dir or csv> [--top 30]
 """
@@ -32,9 +33,14 @@ def main():
         g = r.get("Grid_Size") or r.get("Grid_Size_X") or ""
         grids[short(r["Kernel_Name"])].add(f"{g}/{r.get('Workgroup_Size') or r.get('Workgroup_Size_X') or ''}")
     rows.sort()
-    t_up = next(s for s, _, n in rows if "attn_embed_train" in n)
+    # the timed update: everything after the last rollout encoder launch (bench.py's e2e runs a warm-up update,
+    # then the timed rollout and update); the rollout: from the first rollout encoder launch after the warm-up
+    t_up = max(s for s, _, n in rows if "attn_pool_x3" in n or "attn_pool_kernel" in n)
+    t_up = next(s for s, _, n in rows if s > t_up)
+    t_wu = max(s for s, _, n in rows if "attn_bwd2" in n and s < t_up) if any(
+        "attn_bwd2" in n and s < t_up for s, _, n in rows) else 0
     nmb = sum(1 for s, _, n in rows if "attn_bwd1" in n and s >= t_up)
-    for phase, sel in (("rollout (before the update)", lambda s: s < t_up), ("update", lambda s: s >= t_up)):
+    for phase, sel in (("rollout (after the warm-up update)", lambda s: t_wu < s < t_up), ("update", lambda s: s >= t_up)):
         agg = defaultdict(lambda: [0, 0.0])
         span = [None, None]
         for s, e, n in rows:
