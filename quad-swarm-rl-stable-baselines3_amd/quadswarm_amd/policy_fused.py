@@ -169,7 +169,7 @@ class FusedRolloutPolicy:
                 w_e2p=pack(emb[2].weight), b_e2=emb[2].bias.detach(),
                 w_v1p=pack(val[0].weight), b_v1=val[0].bias.detach(),
                 w_v2p=pack(val[2].weight), b_v2=val[2].bias.detach(),
-                w_a1ep=pack(att[0].weight[:, :H]), w_a1m=att[0].weight[:, H:].detach(),
+                w_a1ep=pack(att[0].weight[:, :H]), w_a1m=att[0].weight[:, H:].detach().contiguous(),
                 b_a1=att[0].bias.detach(),
                 w_a2p=pack(att[2].weight), b_a2=att[2].bias.detach(),
                 w_a3=att[4].weight.detach().reshape(-1).contiguous(), b_a3=float(att[4].bias.detach().item())))
