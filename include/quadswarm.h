@@ -537,6 +537,13 @@ int qs_attn_bwd2_x3(int32_t B, int32_t K, int32_t H, const qs_attn_tower* towers
  * is their sum over p) from the same pass. */
 int qs_attn_dw_x3(const float* G, const float* A, const float* col_scale, int64_t R, int32_t H, float* part,
                   float* part_sum, int32_t n_parts, void* stream);
+/* The encoder's feed_forward on the split-f16 matrix cores (ABI 15; quad_multi_model.py QuadMultiEncoder
+ * feed_forward = Linear + Tanh): Y [M, N] = tanh(X W^T + bias) for X [M, K] fp32 with |x| <= 1 (tanh outputs), K 256
+ * or 512, N a multiple of 256 (<= 1024); w_packed: for each 256-row block z of W and 256-column slice p (z-major), the
+ * pack of W[256 z .., 256 p ..] as the attention weights are packed (qs_attn_tower); w_bytes its size (checked:
+ * (N / 256) (K / 256) 262 144 bytes). */
+int qs_linear_tanh_x3(const float* X, int64_t M, int32_t K, const void* w_packed, int64_t w_bytes, const float* bias,
+                      float* Y, int32_t N, void* stream);
 /* The maxima over the blocks of per-block column maxima (ABI 15; qs_attn_train.colmax rows): out[s][n] =
  * max_b part_max[s][b][n] for s < n_stats (entries >= 0, +inf propagates), part_max [n_stats][n_blocks][H]. */
 int qs_colmax_reduce(const float* part_max, int32_t n_stats, int32_t n_blocks, int32_t H, float* out, void* stream);

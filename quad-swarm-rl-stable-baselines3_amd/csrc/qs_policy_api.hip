@@ -256,6 +256,29 @@ extern "C" int qs_attn_dw0_x3(const float* G, const float* col_scale, const floa
     return H == 256 ? dw0_launch<256>(G, col_scale, obs, stride, so, off, B, K, nd, part, part_sum, n_parts, st)
                     : dw0_launch<128>(G, col_scale, obs, stride, so, off, B, K, nd, part, part_sum, n_parts, st);
 }
+extern "C" int qs_linear_tanh_x3(const float* X, int64_t M, int32_t K, const void* w_packed, int64_t w_bytes,
+                                 const float* bias, float* Y, int32_t N, void* stream) {
+    namespace P = qs::pol;
+    if (!X || !w_packed || !bias || !Y) return fail(QS_E_INVALID, "NULL argument");
+    if (M < 1 || M >= (1ll << 31) / 512 || (K != 256 && K != 512) || N < 256 || N > 1024 || N % 256)
+        return fail(QS_E_INVALID, "M >= 1, K 256 or 512, N a multiple of 256 up to 1024");
+    // the packed operand: (N / 256) (K / 256) blocks of 256 x 256 weights as f16 hi + lo halves
+    if (w_bytes != (int64_t)(N / 256) * (K / 256) * 256 * 256 * 2 * 2)
+        return fail(QS_E_INVALID, "w_bytes: the packed weight must hold (N / 256) (K / 256) packed 256 x 256 blocks");
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 grid((unsigned)((M + P::MROWS - 1) / P::MROWS), (unsigned)(N / 256));
+    const size_t lds = P::linear_x3_lds_bytes();
+    const uint4* wp = reinterpret_cast<const uint4*>(w_packed);
+    if (K == 256) {
+        QS_HIP(hipFuncSetAttribute((const void*)P::linear_tanh_x3_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL(P::linear_tanh_x3_kernel<1>, grid, dim3(P::NTHR), lds, st, X, (long)M, wp, bias, Y, N);
+    } else {
+        QS_HIP(hipFuncSetAttribute((const void*)P::linear_tanh_x3_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL(P::linear_tanh_x3_kernel<2>, grid, dim3(P::NTHR), lds, st, X, (long)M, wp, bias, Y, N);
+    }
+    QS_HIP(hipGetLastError());
+    return QS_OK;
+}
 extern "C" int qs_colmax_reduce(const float* part_max, int32_t n_stats, int32_t n_blocks, int32_t H, float* out,
                                 void* stream) {
     namespace P = qs::pol;

@@ -426,3 +426,82 @@ __global__ __launch_bounds__(NTHR, 2) __attribute__((amdgpu_waves_per_eu(2, 2)))
 
 }  // namespace pol
 }  // namespace qs
+
+namespace qs {
+namespace pol {
+
+// ------------------------------------------------------------------------------------------------------------------
+// The encoder's feed_forward (quad_multi_model.py:250-353 QuadMultiEncoder: Linear(2R -> 2R) + Tanh on the
+// concatenated [self | neighbour] encodings) on the split-f16 matrix cores: Y[:, 256 z + n] = tanh(X W^T + b) for
+// X [M, 256 P] with |x| <= 1 (tanh outputs and the attention's softmax-weighted tanh rows), one 64-row block per
+// (row tile, output half z): the input's P 256-column slices pass through one split tile in turn, accumulating in
+// the same registers; weights packed per (z, p) as pack_mfma_weight_x3 of W[256 z .., 256 p ..].
+// ------------------------------------------------------------------------------------------------------------------
+template <int P>
+__global__ __launch_bounds__(NTHR, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void linear_tanh_x3_kernel(
+    const float* __restrict__ X, long M, const uint4* __restrict__ Wp, const float* __restrict__ bias,
+    float* __restrict__ Y, int N) {
+    constexpr int H = 256, LDH = GeoX3<H>::LDH, CT = Geo<H>::CT, KD = 256 * P, NV = MROWS * (H / 4) / NTHR;
+    constexpr size_t WBLK = (size_t)H * H * 2 * 2 / 16;   // uint4 per packed 256 x 256 block: hi + lo f16 halves
+    extern __shared__ float4 smem4[];
+    _Float16* xh = reinterpret_cast<_Float16*>(smem4);
+    const TileX3 T{xh, xh + MROWS * LDH, LDH};
+    float* BI = reinterpret_cast<float*>(xh + 2 * MROWS * LDH);
+    const long row0 = (long)blockIdx.x * MROWS;
+    const int z = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    for (int n = tid; n < H; n += NTHR) BI[n] = bias[256 * z + n];
+    f32x16 acc[RT][CT];
+    float4 v[NV];
+    auto load = [&](int p) {   // unconditional loads (row 0 stands in past M), zeroed when put
+#pragma unroll
+        for (int u = 0; u < NV; ++u) {
+            const int e = tid + u * NTHR, r = e / (H / 4), c4 = e - r * (H / 4);
+            v[u] = *reinterpret_cast<const float4*>(X + (row0 + r < M ? row0 + r : 0) * KD + 256 * p + 4 * c4);
+        }
+    };
+    auto put = [&]() {
+#pragma unroll
+        for (int u = 0; u < NV; ++u) {
+            const int e = tid + u * NTHR, r = e / (H / 4), c4 = e - r * (H / 4);
+            const float sx = row0 + r < M ? X3_SX : 0.f;
+            T.put4(r, 4 * c4, make_float4(sx * v[u].x, sx * v[u].y, sx * v[u].z, sx * v[u].w));
+        }
+    };
+    load(0);
+    put();
+    __syncthreads();
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+        if (p + 1 < P) load(p + 1);   // the next slice in flight during this one's MFMAs
+        const uint4* wp = Wp + ((size_t)z * P + p) * WBLK;
+        if (p == 0)
+            mfma_layer_x3<H, H, true>(T, wp, acc, wave, lane);
+        else
+            mfma_layer_x3<H, H, false>(T, wp, acc, wave, lane);
+        if (p + 1 < P) {
+            __syncthreads();   // every wave has read the tile
+            put();
+            __syncthreads();
+        }
+    }
+    constexpr float iSS = 1.f / (X3_SX * X3_SW);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+        const int i = acc_i(rt, lane);
+        if (row0 + i >= M) continue;
+#pragma unroll
+        for (int c = 0; c < CT; ++c)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int n0 = acc_n0<H>(wave, c, g, lane);
+                const float4 b = lds4(BI + n0);
+                *reinterpret_cast<float4*>(Y + (row0 + i) * N + 256 * z + n0) =
+                    make_float4(tanh_fast(fmaf(acc[rt][c][4 * g], iSS, b.x)), tanh_fast(fmaf(acc[rt][c][4 * g + 1], iSS, b.y)),
+                                tanh_fast(fmaf(acc[rt][c][4 * g + 2], iSS, b.z)), tanh_fast(fmaf(acc[rt][c][4 * g + 3], iSS, b.w)));
+            }
+    }
+}
+constexpr size_t linear_x3_lds_bytes() { return (size_t)(2 * MROWS * GeoX3<256>::LDH) * 2 + (size_t)256 * 4; }
+
+}  // namespace pol
+}  // namespace qs

@@ -25,7 +25,8 @@ import ctypes
 import torch
 
 from . import _native as NAT
-from .policy_fused import F16_MAX, X3_SIN, pack_mfma_weight_x3, pack_mfma_weights_x3, supports  # noqa: F401
+from .policy_fused import (F16_MAX, X3_SIN, X3_SW, ff_supported, linear_tanh_x3, pack_mfma_weight_x3,  # noqa: F401
+                           pack_mfma_weights_x3, supports)
 
 _PARAMS = ("e1_w", "e1_b", "e2_w", "e2_b", "v1_w", "v1_b", "v2_w", "v2_b", "a1_w", "a1_b", "a2_w", "a2_b", "a3_w", "a3_b")
 
@@ -136,6 +137,7 @@ class _Runner:
         self.towers = (NAT.QsAttnTower * NAT.ATTN_MAX_TOWERS)()
         self.trains = (NAT.QsAttnTrain * NAT.ATTN_MAX_TOWERS)()
         self.pending = False
+        self.ff_packed = None
         self.dw_x3 = True   # the weight gradients on the split-f16 matrix cores (else torch fp32 GEMMs)
 
     def dw(self, G, A, gs=None):
@@ -177,7 +179,21 @@ class _Runner:
             ws.append(w)
             mats += [w_e1, w["e2_w"], w["v1_w"], w["v2_w"], w["a1_w"][:, :H], w["a2_w"], w["v2_w"].t(), w["v1_w"].t(),
                      w["a2_w"].t(), w["a1_w"][:, :H].t(), w["e2_w"].t()]
+        # the feed_forward Linears' 256 x 256 blocks ride along (FusedAttentionTrain.feed_forward)
+        ffs = [enc.feed_forward[0] for enc in self.encs]
+        ff_on = all(ff_supported(f) for f in ffs)
+        nff = 0
+        if ff_on:
+            for f in ffs:
+                w = f.weight
+                blocks = [w[256 * z:256 * (z + 1), 256 * q:256 * (q + 1)] for z in range(w.shape[0] // 256)
+                          for q in range(w.shape[1] // 256)]
+                nff = len(blocks)
+                mats += blocks
         packed = pack_mfma_weights_x3(mats)
+        n_att = len(names) * self.T
+        self.ff_packed = ([torch.stack(packed[n_att + nff * i:n_att + nff * (i + 1)]).contiguous() for i in range(self.T)]
+                          if ff_on else None)
         for i in range(self.T):
             w, b = ws[i], self.buf[i]
             k = dict(zip(names, packed[len(names) * i:len(names) * (i + 1)]))
@@ -304,6 +320,23 @@ class _SelfLayer0Fn(torch.autograd.Function):
         return None, dW, sums, None
 
 
+class _FeedForwardFn(torch.autograd.Function):
+    """QuadMultiEncoder.feed_forward (Linear + Tanh) with its forward on the split-f16 matrix cores
+    (qs_linear_tanh_x3; |x| <= 1: tanh outputs); the backward is the torch one (g (1 - y^2), then the two GEMMs)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, packed):
+        y = linear_tanh_x3(x, packed, bias.detach())
+        ctx.save_for_backward(x, weight, y)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x, weight, y = ctx.saved_tensors
+        gp = torch.ops.aten.tanh_backward(g, y)
+        return gp.mm(weight), gp.t().mm(x), gp.sum(0), None
+
+
 class FusedAttentionTrain:
     """Both towers' neighbour-encoder outputs for the PPO update as one autograd node on the HIP kernels:
     encodings(obs) -> [actor [B, H], critic [B, H]] (SwarmActorCritic.evaluate_actions(obs, actions, nbr=...)).  One
@@ -317,6 +350,15 @@ class FusedAttentionTrain:
 
     def params(self):
         return [p for enc in self.runner.encs for p in tower_params(enc)]
+
+    def feed_forward(self, lin, x):
+        """One tower's feed_forward Linear + Tanh on the concatenated encodings x (QuadMultiEncoder.forward's ff
+        hook): the x3 kernel when this minibatch's encodings packed it (_FeedForwardFn), else torch."""
+        r = self.runner
+        for i, enc in enumerate(r.encs):
+            if enc.feed_forward[0] is lin and r.ff_packed is not None and x.is_contiguous():
+                return _FeedForwardFn.apply(x, lin.weight, lin.bias, r.ff_packed[i])
+        return torch.tanh(lin(x))
 
     def self_layer0(self, lin, obs):
         """The self encoder's first Linear of one tower on the full observation rows (QuadMultiEncoder.forward's l0

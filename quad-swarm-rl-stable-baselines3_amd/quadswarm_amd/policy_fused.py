@@ -85,6 +85,34 @@ def pack_mfma_weights_x3(ws):
     return out
 
 
+def pack_linear_x3(w):
+    """[N, K] fp32 weight (N a multiple of 256, K 256 or 512) -> the operand of qs_linear_tanh_x3: the packs of its
+    256 x 256 blocks W[256 z .., 256 p ..] in (z, p) order, one contiguous int16 tensor.  ValueError out of range."""
+    n, k = w.shape
+    assert n % 256 == 0 and k in (256, 512), (n, k)
+    blocks = [w[256 * z:256 * (z + 1), 256 * p:256 * (p + 1)] for z in range(n // 256) for p in range(k // 256)]
+    return torch.stack(pack_mfma_weights_x3(blocks)).contiguous()
+
+
+def ff_supported(lin):
+    """Can qs_linear_tanh_x3 evaluate this feed_forward Linear?"""
+    return lin.in_features in (256, 512) and lin.out_features % 256 == 0 and 256 <= lin.out_features <= 1024
+
+
+def linear_tanh_x3(x, packed, bias, out=None):
+    """tanh(x W^T + b) for x [M, K] (|x| <= 1: tanh outputs) on the split-f16 matrix cores (qs_linear_tanh_x3)."""
+    M, K = x.shape
+    N = bias.shape[0]
+    y = out if out is not None else torch.empty(M, N, dtype=torch.float32, device=x.device)
+    st = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
+    assert x.is_contiguous() and packed.is_contiguous() and bias.is_contiguous() and y.is_contiguous()
+    NAT.check(NAT.lib().qs_linear_tanh_x3(ctypes.c_void_p(x.data_ptr()), M, K, ctypes.c_void_p(packed.data_ptr()),
+                                          packed.numel() * packed.element_size(), ctypes.c_void_p(bias.data_ptr()),
+                                          ctypes.c_void_p(y.data_ptr()), N, st),
+              "qs_linear_tanh_x3")
+    return y
+
+
 def supports(policy):
     """Can the fused kernels evaluate this policy's encoders?"""
     c = policy.cfg
@@ -173,6 +201,9 @@ class FusedRolloutPolicy:
                 b_a1=att[0].bias.detach(),
                 w_a2p=pack(att[2].weight), b_a2=att[2].bias.detach(),
                 w_a3=att[4].weight.detach().reshape(-1).contiguous(), b_a3=float(att[4].bias.detach().item())))
+            ff = enc.feed_forward[0]
+            if prec == "x3" and ff_supported(ff) and float(ff.weight.detach().abs().amax()) < F16_MAX / X3_SW:
+                packed[-1].update(w_ffp=pack_linear_x3(ff.weight.detach()), b_ff=ff.bias.detach().contiguous())
         self.packed = packed
         self._bind()
 
@@ -222,12 +253,15 @@ class FusedRolloutPolicy:
         NAT.check(pool(B, K, H, self.towers, len(self.encs), st), "qs_attn_pool")
         return self.out
 
-    def _encode(self, enc, obs, nbr_out):
+    def _encode(self, enc, obs, nbr_out, w=None):
         so, na = self.so, enc.all_neighbor_obs_size
         parts = [enc.self_encoder(obs[:, :so]), nbr_out]
         if enc.obstacle_encoder is not None:
             parts.append(enc.obstacle_encoder(obs[:, so + na:]))
-        return enc.feed_forward(torch.cat(parts, dim=1))
+        x = torch.cat(parts, dim=1)
+        if w is not None and "w_ffp" in w:   # x3: the feed_forward's Linear + Tanh as one kernel (|x| <= 1: tanh rows)
+            return linear_tanh_x3(x, w["w_ffp"], w["b_ff"])
+        return enc.feed_forward(x)
 
     @torch.no_grad()
     def forward(self, obs, deterministic=False):
@@ -235,9 +269,10 @@ class FusedRolloutPolicy:
         from .ppo import squashed_log_prob
         pol = self.policy
         nbr = self.neighbor_encodings(obs)
-        a_lat = pol.actor_decoder(pol.actor_core(self._encode(pol.actor_encoder, obs, nbr[0])))
+        a_lat = pol.actor_decoder(pol.actor_core(self._encode(pol.actor_encoder, obs, nbr[0], self.packed[0])))
         mean = pol.action_net(a_lat)
-        values = pol.value_net(pol.critic_decoder(pol.critic_core(self._encode(pol.critic_encoder, obs, nbr[1]))))
+        values = pol.value_net(pol.critic_decoder(pol.critic_core(self._encode(pol.critic_encoder, obs, nbr[1],
+                                                                               self.packed[1]))))
         if deterministic:
             actions = torch.tanh(mean)
         else:
@@ -250,4 +285,5 @@ class FusedRolloutPolicy:
     def predict_values(self, obs):
         pol = self.policy
         nbr = self.neighbor_encodings(obs)
-        return pol.value_net(pol.critic_decoder(pol.critic_core(self._encode(pol.critic_encoder, obs, nbr[1]))))
+        return pol.value_net(pol.critic_decoder(pol.critic_core(self._encode(pol.critic_encoder, obs, nbr[1],
+                                                                             self.packed[1]))))

@@ -193,9 +193,10 @@ class QuadMultiEncoder(nn.Module):
         self.feed_forward = nn.Sequential(nn.Linear(out, 2 * R), nn.Tanh())
         self.out_size = 2 * R
 
-    def forward(self, obs, nbr_out=None, l0=None):
+    def forward(self, obs, nbr_out=None, l0=None, ff=None):
         """nbr_out: the neighbour encoder's output computed elsewhere (the fused update, encoder_train.py); l0(lin,
-        obs): the self encoder's first Linear evaluated elsewhere (FusedAttentionTrain.self_layer0)."""
+        obs): the self encoder's first Linear evaluated elsewhere (FusedAttentionTrain.self_layer0); ff(lin, x): the
+        feed_forward's Linear + Tanh evaluated elsewhere (FusedAttentionTrain.feed_forward)."""
         so, na = self.cfg.self_obs_dim, self.all_neighbor_obs_size
         self_obs = obs[:, :so]
         if l0 is not None and len(self.self_encoder) > 1:
@@ -209,7 +210,10 @@ class QuadMultiEncoder(nn.Module):
             parts.append(self.neighbor_encoder(self_obs, nbr))
         if self.obstacle_encoder is not None:
             parts.append(self.obstacle_encoder(obs[:, so + na:]))
-        return self.feed_forward(torch.cat(parts, dim=1) if len(parts) > 1 else parts[0])
+        x = torch.cat(parts, dim=1) if len(parts) > 1 else parts[0]
+        if ff is not None and isinstance(self.feed_forward[0], nn.Linear):
+            return ff(self.feed_forward[0], x)
+        return self.feed_forward(x)
 
 
 class SwarmActorCritic(nn.Module):
@@ -259,15 +263,18 @@ class SwarmActorCritic(nn.Module):
             actions = torch.tanh(mean + torch.randn_like(mean) * self.log_std.exp())
         return actions, values, squashed_log_prob(mean, self.log_std, actions)
 
-    def evaluate_actions(self, obs, actions, nbr=None, l0=None):
+    def evaluate_actions(self, obs, actions, nbr=None, l0=None, ff=None):
         """(values, log_prob, entropy=None) -- ActorCriticPolicyCustom.py:538-566.  nbr: (actor, critic) neighbour
         encoder outputs from the fused update (encoder_train.FusedAttentionTrain), else the torch encoders run;
-        l0: the fused update's self-encoder first layer (FusedAttentionTrain.self_layer0), with nbr only."""
+        l0 / ff: the fused update's self-encoder first layer and feed_forward (FusedAttentionTrain.self_layer0 /
+        .feed_forward), with nbr only."""
         if nbr is None:
             mean = self.action_net(self.actor_latent(obs))
             return self.predict_values(obs), squashed_log_prob(mean, self.log_std, actions), None
-        mean = head_linear(self.action_net, self.actor_decoder(self.actor_core(self.actor_encoder(obs, nbr[0], l0))))
-        values = head_linear(self.value_net, self.critic_decoder(self.critic_core(self.critic_encoder(obs, nbr[1], l0))))
+        mean = head_linear(self.action_net,
+                           self.actor_decoder(self.actor_core(self.actor_encoder(obs, nbr[0], l0, ff))))
+        values = head_linear(self.value_net,
+                             self.critic_decoder(self.critic_core(self.critic_encoder(obs, nbr[1], l0, ff))))
         return values, squashed_log_prob(mean, self.log_std, actions), None
 
     def predict(self, obs, deterministic=True):
@@ -601,7 +608,8 @@ class PPOTrainer:
                 ob = obs[idx]
                 nbr = fused.encodings(ob) if fused is not None else None
                 values, logp, entropy = pol.evaluate_actions(ob, act[idx], nbr=nbr,
-                                                             l0=fused.self_layer0 if nbr is not None else None)
+                                                             l0=fused.self_layer0 if nbr is not None else None,
+                                                             ff=fused.feed_forward if nbr is not None else None)
                 values = values.flatten()
                 adv = adv_all[idx]
                 if c.normalize_advantage and idx.numel() > 1:

@@ -102,8 +102,8 @@ def test_encoder_gradients_match_torch(case, B):
 @pytest.mark.parametrize("case", ["c3", "a8"])
 def test_ppo_loss_gradient_bucket_matches_torch(case):
     """The whole PPO minibatch step as PPOTrainer.train runs it: evaluate_actions with the fused encoders (nbr=...)
-    and the self encoder's first layer on the matrix cores (l0=...) vs the torch module -- values, log-probs and every
-    parameter's gradient."""
+    and the self encoder's first layer and the feed_forward on the matrix cores (l0=..., ff=...) vs the torch module --
+    values, log-probs and every parameter's gradient."""
     pol = fixture_policy(case)
     B = 2048
     obs = obs_for(pol.cfg, B, seed=5)
@@ -115,7 +115,8 @@ def test_ppo_loss_gradient_bucket_matches_torch(case):
         return -(adv * torch.exp(lp - lp.detach())).mean() + 0.5 * (v.view(-1) ** 2).mean()
 
     fused = FusedAttentionTrain(pol)
-    v_f, lp_f, _ = pol.evaluate_actions(obs, act, nbr=fused.encodings(obs), l0=fused.self_layer0)
+    v_f, lp_f, _ = pol.evaluate_actions(obs, act, nbr=fused.encodings(obs), l0=fused.self_layer0,
+                                        ff=fused.feed_forward)
     gf = torch.autograd.grad(loss_of(v_f, lp_f), list(pol.parameters()), allow_unused=True)
     v_t, lp_t, _ = pol.evaluate_actions(obs, act)
     gt = torch.autograd.grad(loss_of(v_t, lp_t), list(pol.parameters()), allow_unused=True)
@@ -283,3 +284,21 @@ def test_dw0_x3_matches_fp64(H, B, K, parts, nd):
     print(f"H={H} B={B} K={K}: layer-0 dW relative error {err:.2e}")
     assert err < 2e-6
     assert ((sums.double() - G64.sum(0)).abs() / G64.abs().sum(0)).max().item() < 1e-6
+
+
+@pytest.mark.parametrize("M,K,N", [(1000, 512, 512), (4097, 256, 256), (64, 512, 1024)])
+def test_linear_tanh_x3_matches_fp64(M, K, N):
+    """qs_linear_tanh_x3 (the feed_forward's Linear + Tanh on the split-f16 matrix cores) against fp64 on tanh-range
+    inputs, ragged row counts."""
+    from quadswarm_amd.policy_fused import linear_tanh_x3, pack_linear_x3
+    g = torch.Generator(device="cuda").manual_seed(M + K + N)
+    x = torch.tanh(torch.randn(M, K, device="cuda", generator=g) * 2)
+    w = torch.randn(N, K, device="cuda", generator=g) / K ** 0.5
+    b = torch.randn(N, device="cuda", generator=g) * 0.1
+    got = linear_tanh_x3(x, pack_linear_x3(w), b)
+    want = torch.tanh(x.double().mm(w.double().t()) + b.double())
+    t32 = torch.tanh(torch.nn.functional.linear(x, w, b))
+    e_x3 = (got.double() - want).abs().max().item()
+    e_32 = (t32.double() - want).abs().max().item()
+    print(f"M={M} K={K} N={N}: max |err| x3 {e_x3:.2e}, torch fp32 {e_32:.2e}")
+    assert e_x3 < 2e-6 and e_x3 < 8 * e_32 + 1e-6
