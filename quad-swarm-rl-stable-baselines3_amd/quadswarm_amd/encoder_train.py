@@ -26,7 +26,7 @@ import torch
 
 from . import _native as NAT
 from .policy_fused import (F16_MAX, X3_SIN, X3_SW, ff_supported, linear_tanh_x3, pack_mfma_weight_x3,  # noqa: F401
-                           pack_mfma_weights_x3, supports)
+                           pack_mfma_weights_x3, self_l2_supported, supports)
 
 _PARAMS = ("e1_w", "e1_b", "e2_w", "e2_b", "v1_w", "v1_b", "v2_w", "v2_b", "a1_w", "a1_b", "a2_w", "a2_b", "a3_w", "a3_b")
 
@@ -137,7 +137,7 @@ class _Runner:
         self.towers = (NAT.QsAttnTower * NAT.ATTN_MAX_TOWERS)()
         self.trains = (NAT.QsAttnTrain * NAT.ATTN_MAX_TOWERS)()
         self.pending = False
-        self.ff_packed = None
+        self.lin_packed = {}   # id(Linear) -> its qs_linear_tanh_x3 operand, packed with this minibatch's weights
         self.dw_x3 = True   # the weight gradients on the split-f16 matrix cores (else torch fp32 GEMMs)
 
     def dw(self, G, A, gs=None):
@@ -179,21 +179,19 @@ class _Runner:
             ws.append(w)
             mats += [w_e1, w["e2_w"], w["v1_w"], w["v2_w"], w["a1_w"][:, :H], w["a2_w"], w["v2_w"].t(), w["v1_w"].t(),
                      w["a2_w"].t(), w["a1_w"][:, :H].t(), w["e2_w"].t()]
-        # the feed_forward Linears' 256 x 256 blocks ride along (FusedAttentionTrain.feed_forward)
-        ffs = [enc.feed_forward[0] for enc in self.encs]
-        ff_on = all(ff_supported(f) for f in ffs)
-        nff = 0
-        if ff_on:
-            for f in ffs:
-                w = f.weight
-                blocks = [w[256 * z:256 * (z + 1), 256 * q:256 * (q + 1)] for z in range(w.shape[0] // 256)
-                          for q in range(w.shape[1] // 256)]
-                nff = len(blocks)
-                mats += blocks
+        # the feed_forward Linears' and the self encoders' second Linears' 256 x 256 blocks ride along
+        # (FusedAttentionTrain.feed_forward: Linear + Tanh of tanh inputs on qs_linear_tanh_x3)
+        lins = [enc.feed_forward[0] for enc in self.encs if ff_supported(enc.feed_forward[0])]
+        lins += [enc.self_encoder[2] for enc in self.encs if self_l2_supported(enc.self_encoder)]
+        spans = []
+        for f in lins:
+            w = f.weight
+            blocks = [w[256 * z:256 * (z + 1), 256 * q:256 * (q + 1)] for z in range(w.shape[0] // 256)
+                      for q in range(w.shape[1] // 256)]
+            spans.append((len(mats), len(blocks)))
+            mats += blocks
         packed = pack_mfma_weights_x3(mats)
-        n_att = len(names) * self.T
-        self.ff_packed = ([torch.stack(packed[n_att + nff * i:n_att + nff * (i + 1)]).contiguous() for i in range(self.T)]
-                          if ff_on else None)
+        self.lin_packed = {id(f): torch.stack(packed[a:a + n]).contiguous() for f, (a, n) in zip(lins, spans)}
         for i in range(self.T):
             w, b = ws[i], self.buf[i]
             k = dict(zip(names, packed[len(names) * i:len(names) * (i + 1)]))
@@ -352,12 +350,12 @@ class FusedAttentionTrain:
         return [p for enc in self.runner.encs for p in tower_params(enc)]
 
     def feed_forward(self, lin, x):
-        """One tower's feed_forward Linear + Tanh on the concatenated encodings x (QuadMultiEncoder.forward's ff
-        hook): the x3 kernel when this minibatch's encodings packed it (_FeedForwardFn), else torch."""
-        r = self.runner
-        for i, enc in enumerate(r.encs):
-            if enc.feed_forward[0] is lin and r.ff_packed is not None and x.is_contiguous():
-                return _FeedForwardFn.apply(x, lin.weight, lin.bias, r.ff_packed[i])
+        """tanh(lin(x)) for a tower's feed_forward Linear or its self encoder's second Linear, x a tanh-range input
+        (QuadMultiEncoder.forward's ff hook): the x3 kernel when this minibatch's encodings packed it
+        (_FeedForwardFn), else torch."""
+        packed = self.runner.lin_packed.get(id(lin))
+        if packed is not None and x.is_contiguous():
+            return _FeedForwardFn.apply(x, lin.weight, lin.bias, packed)
         return torch.tanh(lin(x))
 
     def self_layer0(self, lin, obs):

@@ -99,6 +99,13 @@ def ff_supported(lin):
     return lin.in_features in (256, 512) and lin.out_features % 256 == 0 and 256 <= lin.out_features <= 1024
 
 
+def self_l2_supported(se):
+    """The self encoder's second Linear + Tanh (Sequential(Linear, Tanh, Linear, Tanh), tanh inputs) on
+    qs_linear_tanh_x3?"""
+    return (len(se) == 4 and isinstance(se[1], torch.nn.Tanh) and isinstance(se[3], torch.nn.Tanh)
+            and isinstance(se[2], torch.nn.Linear) and ff_supported(se[2]))
+
+
 def linear_tanh_x3(x, packed, bias, out=None):
     """tanh(x W^T + b) for x [M, K] (|x| <= 1: tanh outputs) on the split-f16 matrix cores (qs_linear_tanh_x3)."""
     M, K = x.shape
@@ -204,6 +211,10 @@ class FusedRolloutPolicy:
             ff = enc.feed_forward[0]
             if prec == "x3" and ff_supported(ff) and float(ff.weight.detach().abs().amax()) < F16_MAX / X3_SW:
                 packed[-1].update(w_ffp=pack_linear_x3(ff.weight.detach()), b_ff=ff.bias.detach().contiguous())
+            se = enc.self_encoder
+            if (prec == "x3" and self_l2_supported(se)
+                    and float(se[2].weight.detach().abs().amax()) < F16_MAX / X3_SW):
+                packed[-1].update(w_s2p=pack_linear_x3(se[2].weight.detach()), b_s2=se[2].bias.detach().contiguous())
         self.packed = packed
         self._bind()
 
@@ -255,7 +266,11 @@ class FusedRolloutPolicy:
 
     def _encode(self, enc, obs, nbr_out, w=None):
         so, na = self.so, enc.all_neighbor_obs_size
-        parts = [enc.self_encoder(obs[:, :so]), nbr_out]
+        se = enc.self_encoder
+        if w is not None and "w_s2p" in w:   # x3: the second Linear + Tanh (tanh inputs) as one kernel
+            parts = [linear_tanh_x3(se[1](se[0](obs[:, :so])), w["w_s2p"], w["b_s2"]), nbr_out]
+        else:
+            parts = [se(obs[:, :so]), nbr_out]
         if enc.obstacle_encoder is not None:
             parts.append(enc.obstacle_encoder(obs[:, so + na:]))
         x = torch.cat(parts, dim=1)

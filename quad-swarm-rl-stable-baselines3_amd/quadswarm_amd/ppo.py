@@ -199,10 +199,15 @@ class QuadMultiEncoder(nn.Module):
         feed_forward's Linear + Tanh evaluated elsewhere (FusedAttentionTrain.feed_forward)."""
         so, na = self.cfg.self_obs_dim, self.all_neighbor_obs_size
         self_obs = obs[:, :so]
-        if l0 is not None and len(self.self_encoder) > 1:
-            parts = [self.self_encoder[1:](l0(self.self_encoder[0], obs))]
+        se = self.self_encoder
+        if l0 is not None and len(se) > 1:
+            s1 = se[1](l0(se[0], obs))
+            if ff is not None and len(se) == 4 and isinstance(se[2], nn.Linear) and isinstance(se[3], nn.Tanh):
+                parts = [ff(se[2], s1)]   # the second Linear + Tanh (tanh inputs) evaluated elsewhere
+            else:
+                parts = [se[2:](s1)]
         else:
-            parts = [self.self_encoder(self_obs)]
+            parts = [se(self_obs)]
         if nbr_out is not None:
             parts.append(nbr_out)
         elif self.neighbor_encoder is not None:
