@@ -537,6 +537,10 @@ int qs_attn_bwd2_x3(int32_t B, int32_t K, int32_t H, const qs_attn_tower* towers
  * is their sum over p) from the same pass. */
 int qs_attn_dw_x3(const float* G, const float* A, const float* col_scale, int64_t R, int32_t H, float* part,
                   float* part_sum, int32_t n_parts, void* stream);
+/* qs_attn_dw_x3 on column slices of wider rows (ABI 15): row strides ldg / lda (floats, H .. 4096) -- e.g. the 256 x
+ * 256 blocks of the feed_forward's [512, 512] weight gradient. */
+int qs_dw_x3_ld(const float* G, int32_t ldg, const float* A, int32_t lda, const float* col_scale, int64_t R, int32_t H,
+                float* part, float* part_sum, int32_t n_parts, void* stream);
 /* The encoder's feed_forward on the split-f16 matrix cores (ABI 15; quad_multi_model.py QuadMultiEncoder
  * feed_forward = Linear + Tanh): Y [M, N] = tanh(X W^T + bias) for X [M, K] fp32 with |x| <= 1 (tanh outputs), K 256
  * or 512, N a multiple of 256 (<= 1024); w_packed: for each 256-row block z of W and 256-column slice p (z-major), the

@@ -205,27 +205,34 @@ extern "C" int qs_attn_bwd1_x3(int32_t B, int32_t K, int32_t H, const qs_attn_to
     return attn_train_impl(TR_BWD1, nullptr, 0, 0, 0, B, K, 0, H, towers, trains, n_towers, stream);
 }
 template <int H>
-static int dw_launch(const float* G, const float* A, const float* gs, int64_t R, float* part, float* part_sum,
-                     int32_t n_parts, hipStream_t st) {
+static int dw_launch(const float* G, int32_t ldg, const float* A, int32_t lda, const float* gs, int64_t R, float* part,
+                     float* part_sum, int32_t n_parts, hipStream_t st) {
     namespace P = qs::pol;
     const long long rows_per = (R + n_parts - 1) / n_parts;
     const int steps = (int)((rows_per + P::DW_STEP - 1) / P::DW_STEP);
     const size_t lds = P::dw_lds_bytes<H>();
     QS_HIP(hipFuncSetAttribute((const void*)P::dw_x3_kernel<H>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    if ((long long)steps * P::DW_STEP * (ldg > lda ? ldg : lda) * 4 >= (1ll << 31))
+        return fail(QS_E_INVALID, "rows per part x row stride too large (use more parts)");
     hipLaunchKernelGGL(P::dw_x3_kernel<H>, dim3((unsigned)n_parts), dim3(P::dw_threads<H>()), lds, st, G, A, gs, (long)R, steps, part,
-                       part_sum);
+                       part_sum, (int)ldg, (int)lda);
     QS_HIP(hipGetLastError());
     return QS_OK;
 }
-extern "C" int qs_attn_dw_x3(const float* G, const float* A, const float* col_scale, int64_t R, int32_t H, float* part,
-                             float* part_sum, int32_t n_parts, void* stream) {
+extern "C" int qs_dw_x3_ld(const float* G, int32_t ldg, const float* A, int32_t lda, const float* col_scale, int64_t R,
+                           int32_t H, float* part, float* part_sum, int32_t n_parts, void* stream) {
     if (!G || !A || !col_scale || !part) return fail(QS_E_INVALID, "NULL argument");
     if (H != 128 && H != 256) return fail(QS_E_INVALID, "hidden size must be 128 or 256");
-    if (R < 1 || n_parts < 1 || n_parts > 65535 || R * (int64_t)H >= (1ll << 40))
+    if (ldg < H || lda < H || ldg > 4096 || lda > 4096) return fail(QS_E_INVALID, "row strides H .. 4096 floats");
+    if (R < 1 || n_parts < 1 || n_parts > 65535 || R * (int64_t)(ldg > lda ? ldg : lda) >= (1ll << 40))
         return fail(QS_E_INVALID, "R >= 1, 1 <= n_parts <= 65535");
     hipStream_t st = (hipStream_t)stream;
-    return H == 256 ? dw_launch<256>(G, A, col_scale, R, part, part_sum, n_parts, st)
-                    : dw_launch<128>(G, A, col_scale, R, part, part_sum, n_parts, st);
+    return H == 256 ? dw_launch<256>(G, ldg, A, lda, col_scale, R, part, part_sum, n_parts, st)
+                    : dw_launch<128>(G, ldg, A, lda, col_scale, R, part, part_sum, n_parts, st);
+}
+extern "C" int qs_attn_dw_x3(const float* G, const float* A, const float* col_scale, int64_t R, int32_t H, float* part,
+                             float* part_sum, int32_t n_parts, void* stream) {
+    return qs_dw_x3_ld(G, H, A, H, col_scale, R, H, part, part_sum, n_parts, stream);
 }
 template <int H>
 static int dw0_launch(const float* G, const float* gs, const float* obs, int32_t stride, int32_t so, int32_t off,

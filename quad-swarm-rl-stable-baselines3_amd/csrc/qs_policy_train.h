@@ -697,7 +697,8 @@ constexpr int dw_threads() { return 64 * (H / 32); }
 template <int H>
 __global__ __launch_bounds__(dw_threads<H>(), 1) void dw_x3_kernel(const float* __restrict__ G, const float* __restrict__ A,
                                                         const float* __restrict__ gs, long R, int steps_per_block,
-                                                        float* __restrict__ part, float* __restrict__ part_sum) {
+                                                        float* __restrict__ part, float* __restrict__ part_sum,
+                                                        int ldg, int lda) {
     constexpr int DWT = dw_threads<H>();
     constexpr int NT = 1, KT = H / 32, TPC = DWT / H, RPT = DW_STEP / TPC;   // threads per column, rows each
     constexpr int RING = QS_DW_RING;
@@ -716,18 +717,21 @@ __global__ __launch_bounds__(dw_threads<H>(), 1) void dw_x3_kernel(const float* 
     float csum = 0.f;   // the column's sum over the part's rows (the bias gradient's part; rows in order)
     // the block's rows through buffer descriptors (base = its first row, records = its rows that exist): a 32-bit
     // offset per load and the range check's zeros past R, no 64-bit address or select per row
+    // (row strides ldg / lda in floats: G and A may be column slices of wider rows)
     const long r_end = r_begin + (long)steps_per_block * DW_STEP < R ? r_begin + (long)steps_per_block * DW_STEP : R;
-    const int nbytes = r_end > r_begin ? (int)((r_end - r_begin) * H * 4) : 0;
-    const auto rg = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(G + r_begin * H), (short)0, nbytes, 0x00020000);
-    const auto ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(A + r_begin * H), (short)0, nbytes, 0x00020000);
-    const int voff = (sr * H + sc) * 4;
+    const long nrow = r_end > r_begin ? r_end - r_begin : 0;
+    const auto rg = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(G + r_begin * ldg), (short)0,
+                                                      (int)(nrow * ldg * 4), 0x00020000);
+    const auto ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(A + r_begin * lda), (short)0,
+                                                      (int)(nrow * lda * 4), 0x00020000);
+    const int voffg = (sr * ldg + sc) * 4, voffa = (sr * lda + sc) * 4;
     auto load = [&](auto SL, int s) {
         constexpr int sl = decltype(SL)::value;
-        const int soff = s * DW_STEP * H * 4;   // (a step past the block's rows reads zeros)
+        const int sog = s * DW_STEP * ldg * 4, soa = s * DW_STEP * lda * 4;   // (a step past the rows reads zeros)
 #pragma unroll
         for (int u = 0; u < RPT; ++u) {
-            gv[sl][u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, voff + u * H * 4, soff, 0));
-            av[sl][u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ra, voff + u * H * 4, soff, 0));
+            gv[sl][u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, voffg + u * ldg * 4, sog, 0));
+            av[sl][u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ra, voffa + u * lda * 4, soa, 0));
         }
     };
     auto stage = [&](auto SL, int b) {

@@ -91,16 +91,18 @@ def dw_x3(G, A, parts=256, out=None, gs=None, sums=False):
     range split over `parts` blocks and the parts summed here.  gs: G's column scales (col_scales / col_stats).
     sums: also G's column sums from the same pass (returns (dW, sums))."""
     R, H = G.shape
+    assert G.stride(1) == 1 and A.stride(1) == 1 and A.shape == G.shape   # rows may be slices of wider ones
     parts = max(1, min(parts, (R + 15) // 16))
     buf = torch.empty(parts, H, H, dtype=torch.float32, device=G.device)
     psum = torch.empty(parts, H, dtype=torch.float32, device=G.device) if sums else None
     if gs is None:
         gs = col_scales(G)
+    gs = gs.contiguous()
     st = ctypes.c_void_p(torch.cuda.current_stream(G.device).cuda_stream)
-    NAT.check(NAT.lib().qs_attn_dw_x3(ctypes.c_void_p(G.data_ptr()), ctypes.c_void_p(A.data_ptr()),
-                                      ctypes.c_void_p(gs.data_ptr()), R, H, ctypes.c_void_p(buf.data_ptr()),
-                                      ctypes.c_void_p(psum.data_ptr() if sums else 0), parts, st),
-              "qs_attn_dw_x3")
+    NAT.check(NAT.lib().qs_dw_x3_ld(ctypes.c_void_p(G.data_ptr()), G.stride(0), ctypes.c_void_p(A.data_ptr()),
+                                    A.stride(0), ctypes.c_void_p(gs.data_ptr()), R, H, ctypes.c_void_p(buf.data_ptr()),
+                                    ctypes.c_void_p(psum.data_ptr() if sums else 0), parts, st),
+              "qs_dw_x3_ld")
     dW = torch.sum(buf, dim=0, out=out)
     return (dW, psum.sum(0)) if sums else dW
 
@@ -332,7 +334,20 @@ class _FeedForwardFn(torch.autograd.Function):
     def backward(ctx, g):
         x, weight, y = ctx.saved_tensors
         gp = torch.ops.aten.tanh_backward(g, y)
-        return gp.mm(weight), gp.t().mm(x), gp.sum(0), None
+        N, K = weight.shape
+        # the weight gradient gp^T x on the split-f16 matrix cores by 256 x 256 blocks (x: tanh range; gp's column
+        # scales from one max pass), the bias gradient from the same passes; dX in torch
+        gs = _pow2_scales(torch.linalg.vector_norm(gp, ord=float("inf"), dim=0))
+        dW = torch.empty(N, K, dtype=torch.float32, device=g.device)
+        db = torch.empty(N, dtype=torch.float32, device=g.device)
+        for zn in range(N // 256):
+            for zk in range(K // 256):
+                r = dw_x3(gp[:, 256 * zn:256 * (zn + 1)], x[:, 256 * zk:256 * (zk + 1)], gs=gs[256 * zn:256 * (zn + 1)],
+                          sums=True)
+                dW[256 * zn:256 * (zn + 1), 256 * zk:256 * (zk + 1)] = r[0]
+                if zk == 0:
+                    db[256 * zn:256 * (zn + 1)] = r[1]
+        return gp.mm(weight), dW, db, None
 
 
 class FusedAttentionTrain:

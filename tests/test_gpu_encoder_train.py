@@ -302,3 +302,21 @@ def test_linear_tanh_x3_matches_fp64(M, K, N):
     e_32 = (t32.double() - want).abs().max().item()
     print(f"M={M} K={K} N={N}: max |err| x3 {e_x3:.2e}, torch fp32 {e_32:.2e}")
     assert e_x3 < 2e-6 and e_x3 < 8 * e_32 + 1e-6
+
+
+def test_dw_x3_on_column_slices():
+    """qs_dw_x3_ld: the 256 x 256 blocks of a [512, 512] weight gradient from column slices of [R, 512] rows (the
+    feed_forward's backward), against fp64."""
+    g = torch.Generator(device="cuda").manual_seed(5)
+    R = 20011
+    G = torch.randn(R, 512, device="cuda", generator=g) * torch.exp2(torch.linspace(-10, 3, 512, device="cuda"))
+    A = torch.tanh(torch.randn(R, 512, device="cuda", generator=g) * 2)
+    want = G.double().t().mm(A.double())
+    for zn in range(2):
+        for zk in range(2):
+            got, sums = dw_x3(G[:, 256 * zn:256 * (zn + 1)], A[:, 256 * zk:256 * (zk + 1)], sums=True)
+            w = want[256 * zn:256 * (zn + 1), 256 * zk:256 * (zk + 1)]
+            scale = w.abs().amax(1, keepdim=True).clamp_min(1e-300)
+            assert ((got.double() - w).abs() / scale).max().item() < 1e-5, (zn, zk)
+            G64 = G[:, 256 * zn:256 * (zn + 1)].double()
+            assert ((sums.double() - G64.sum(0)).abs() / G64.abs().sum(0)).max().item() < 1e-6
