@@ -548,6 +548,12 @@ int qs_dw_x3_ld(const float* G, int32_t ldg, const float* A, int32_t lda, const 
  * (N / 256) (K / 256) 262 144 bytes). */
 int qs_linear_tanh_x3(const float* X, int64_t M, int32_t K, const void* w_packed, int64_t w_bytes, const float* bias,
                       float* Y, int32_t N, void* stream);
+/* Y [M, N] = X W^T for rows X [M, K] of any magnitude (ABI 15; the feed_forward's backward dX = G W with the packed
+ * W^T): row r staged at its power-of-two scale row_scale[r] (max |X[r, :]| row_scale[r] < 2^14 -- the
+ * qs_attn_dw_x3 column-scale rule applied to rows), no bias, no activation; K, N, w_packed / w_bytes as
+ * qs_linear_tanh_x3. */
+int qs_linear_rows_x3(const float* X, const float* row_scale, int64_t M, int32_t K, const void* w_packed, int64_t w_bytes,
+                      float* Y, int32_t N, void* stream);
 /* The maxima over the blocks of per-block column maxima (ABI 15; qs_attn_train.colmax rows): out[s][n] =
  * max_b part_max[s][b][n] for s < n_stats (entries >= 0, +inf propagates), part_max [n_stats][n_blocks][H]. */
 int qs_colmax_reduce(const float* part_max, int32_t n_stats, int32_t n_blocks, int32_t H, float* out, void* stream);

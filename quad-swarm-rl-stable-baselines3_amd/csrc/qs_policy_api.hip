@@ -277,11 +277,37 @@ extern "C" int qs_linear_tanh_x3(const float* X, int64_t M, int32_t K, const voi
     const size_t lds = P::linear_x3_lds_bytes();
     const uint4* wp = reinterpret_cast<const uint4*>(w_packed);
     if (K == 256) {
-        QS_HIP(hipFuncSetAttribute((const void*)P::linear_tanh_x3_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL(P::linear_tanh_x3_kernel<1>, grid, dim3(P::NTHR), lds, st, X, (long)M, wp, bias, Y, N);
+        QS_HIP(hipFuncSetAttribute((const void*)P::linear_tanh_x3_kernel<1, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL((P::linear_tanh_x3_kernel<1, false>), grid, dim3(P::NTHR), lds, st, X, (long)M, wp, bias, Y, N,
+                           nullptr);
     } else {
-        QS_HIP(hipFuncSetAttribute((const void*)P::linear_tanh_x3_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL(P::linear_tanh_x3_kernel<2>, grid, dim3(P::NTHR), lds, st, X, (long)M, wp, bias, Y, N);
+        QS_HIP(hipFuncSetAttribute((const void*)P::linear_tanh_x3_kernel<2, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL((P::linear_tanh_x3_kernel<2, false>), grid, dim3(P::NTHR), lds, st, X, (long)M, wp, bias, Y, N,
+                           nullptr);
+    }
+    QS_HIP(hipGetLastError());
+    return QS_OK;
+}
+extern "C" int qs_linear_rows_x3(const float* X, const float* row_scale, int64_t M, int32_t K, const void* w_packed,
+                                 int64_t w_bytes, float* Y, int32_t N, void* stream) {
+    namespace P = qs::pol;
+    if (!X || !row_scale || !w_packed || !Y) return fail(QS_E_INVALID, "NULL argument");
+    if (M < 1 || M >= (1ll << 31) / 512 || (K != 256 && K != 512) || N < 256 || N > 1024 || N % 256)
+        return fail(QS_E_INVALID, "M >= 1, K 256 or 512, N a multiple of 256 up to 1024");
+    if (w_bytes != (int64_t)(N / 256) * (K / 256) * 256 * 256 * 2 * 2)
+        return fail(QS_E_INVALID, "w_bytes: the packed weight must hold (N / 256) (K / 256) packed 256 x 256 blocks");
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 grid((unsigned)((M + P::MROWS - 1) / P::MROWS), (unsigned)(N / 256));
+    const size_t lds = P::linear_x3_lds_bytes();
+    const uint4* wp = reinterpret_cast<const uint4*>(w_packed);
+    if (K == 256) {
+        QS_HIP(hipFuncSetAttribute((const void*)P::linear_tanh_x3_kernel<1, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL((P::linear_tanh_x3_kernel<1, true>), grid, dim3(P::NTHR), lds, st, X, (long)M, wp, nullptr, Y, N,
+                           row_scale);
+    } else {
+        QS_HIP(hipFuncSetAttribute((const void*)P::linear_tanh_x3_kernel<2, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL((P::linear_tanh_x3_kernel<2, true>), grid, dim3(P::NTHR), lds, st, X, (long)M, wp, nullptr, Y, N,
+                           row_scale);
     }
     QS_HIP(hipGetLastError());
     return QS_OK;

@@ -437,10 +437,13 @@ namespace pol {
 // (row tile, output half z): the input's P 256-column slices pass through one split tile in turn, accumulating in
 // the same registers; weights packed per (z, p) as pack_mfma_weight_x3 of W[256 z .., 256 p ..].
 // ------------------------------------------------------------------------------------------------------------------
-template <int P>
+// ROWS (the backward's dX = G W for gradient rows G of any magnitude): no bias and no activation, row r of X staged
+// at its power-of-two scale rs[r] (max |x_r| rs[r] in [2^13, 2^14): exact, it factors out of the row's products),
+// Y = acc / (rs[r] s_w).
+template <int P, bool ROWS = false>
 __global__ __launch_bounds__(NTHR, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void linear_tanh_x3_kernel(
     const float* __restrict__ X, long M, const uint4* __restrict__ Wp, const float* __restrict__ bias,
-    float* __restrict__ Y, int N) {
+    float* __restrict__ Y, int N, const float* __restrict__ rs = nullptr) {
     constexpr int H = 256, LDH = GeoX3<H>::LDH, CT = Geo<H>::CT, KD = 256 * P, NV = MROWS * (H / 4) / NTHR;
     constexpr size_t WBLK = (size_t)H * H * 2 * 2 / 16;   // uint4 per packed 256 x 256 block: hi + lo f16 halves
     extern __shared__ float4 smem4[];
@@ -449,7 +452,18 @@ __global__ __launch_bounds__(NTHR, 2) __attribute__((amdgpu_waves_per_eu(2, 2)))
     float* BI = reinterpret_cast<float*>(xh + 2 * MROWS * LDH);
     const long row0 = (long)blockIdx.x * MROWS;
     const int z = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    for (int n = tid; n < H; n += NTHR) BI[n] = bias[256 * z + n];
+    float* RSI = BI + H;        // ROWS: 1 / (rs[r] s_w) of the block's rows
+    float* RSX = RSI + MROWS;   // ROWS: rs[r] (0 past M)
+    if constexpr (ROWS) {
+        if (tid < MROWS) {
+            const float r = row0 + tid < M ? rs[row0 + tid] : 0.f;
+            RSX[tid] = r;
+            RSI[tid] = r > 0.f ? 1.f / (r * X3_SW) : 0.f;
+        }
+        __syncthreads();
+    } else {
+        for (int n = tid; n < H; n += NTHR) BI[n] = bias[256 * z + n];
+    }
     f32x16 acc[RT][CT];
     float4 v[NV];
     auto load = [&](int p) {   // unconditional loads (row 0 stands in past M), zeroed when put
@@ -463,7 +477,7 @@ __global__ __launch_bounds__(NTHR, 2) __attribute__((amdgpu_waves_per_eu(2, 2)))
 #pragma unroll
         for (int u = 0; u < NV; ++u) {
             const int e = tid + u * NTHR, r = e / (H / 4), c4 = e - r * (H / 4);
-            const float sx = row0 + r < M ? X3_SX : 0.f;
+            const float sx = ROWS ? RSX[r] : (row0 + r < M ? X3_SX : 0.f);
             T.put4(r, 4 * c4, make_float4(sx * v[u].x, sx * v[u].y, sx * v[u].z, sx * v[u].w));
         }
     };
@@ -489,19 +503,26 @@ __global__ __launch_bounds__(NTHR, 2) __attribute__((amdgpu_waves_per_eu(2, 2)))
     for (int rt = 0; rt < RT; ++rt) {
         const int i = acc_i(rt, lane);
         if (row0 + i >= M) continue;
+        const float si = ROWS ? RSI[i] : 0.f;
 #pragma unroll
         for (int c = 0; c < CT; ++c)
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 const int n0 = acc_n0<H>(wave, c, g, lane);
-                const float4 b = lds4(BI + n0);
-                *reinterpret_cast<float4*>(Y + (row0 + i) * N + 256 * z + n0) =
-                    make_float4(tanh_fast(fmaf(acc[rt][c][4 * g], iSS, b.x)), tanh_fast(fmaf(acc[rt][c][4 * g + 1], iSS, b.y)),
-                                tanh_fast(fmaf(acc[rt][c][4 * g + 2], iSS, b.z)), tanh_fast(fmaf(acc[rt][c][4 * g + 3], iSS, b.w)));
+                float4 y;
+                if constexpr (ROWS) {
+                    y = make_float4(acc[rt][c][4 * g] * si, acc[rt][c][4 * g + 1] * si, acc[rt][c][4 * g + 2] * si,
+                                    acc[rt][c][4 * g + 3] * si);
+                } else {
+                    const float4 b = lds4(BI + n0);
+                    y = make_float4(tanh_fast(fmaf(acc[rt][c][4 * g], iSS, b.x)), tanh_fast(fmaf(acc[rt][c][4 * g + 1], iSS, b.y)),
+                                    tanh_fast(fmaf(acc[rt][c][4 * g + 2], iSS, b.z)), tanh_fast(fmaf(acc[rt][c][4 * g + 3], iSS, b.w)));
+                }
+                *reinterpret_cast<float4*>(Y + (row0 + i) * N + 256 * z + n0) = y;
             }
     }
 }
-constexpr size_t linear_x3_lds_bytes() { return (size_t)(2 * MROWS * GeoX3<256>::LDH) * 2 + (size_t)256 * 4; }
+constexpr size_t linear_x3_lds_bytes() { return (size_t)(2 * MROWS * GeoX3<256>::LDH) * 2 + (size_t)(256 + 2 * MROWS) * 4; }
 
 }  // namespace pol
 }  // namespace qs

@@ -25,8 +25,8 @@ import ctypes
 import torch
 
 from . import _native as NAT
-from .policy_fused import (F16_MAX, X3_SIN, X3_SW, ff_supported, linear_tanh_x3, pack_mfma_weight_x3,  # noqa: F401
-                           pack_mfma_weights_x3, self_l2_supported, supports)
+from .policy_fused import (F16_MAX, X3_SIN, X3_SW, ff_supported, linear_rows_x3, linear_tanh_x3,  # noqa: F401
+                           pack_mfma_weight_x3, pack_mfma_weights_x3, self_l2_supported, supports)
 
 _PARAMS = ("e1_w", "e1_b", "e2_w", "e2_b", "v1_w", "v1_b", "v2_w", "v2_b", "a1_w", "a1_b", "a2_w", "a2_b", "a3_w", "a3_b")
 
@@ -187,13 +187,14 @@ class _Runner:
         lins += [enc.self_encoder[2] for enc in self.encs if self_l2_supported(enc.self_encoder)]
         spans = []
         for f in lins:
-            w = f.weight
-            blocks = [w[256 * z:256 * (z + 1), 256 * q:256 * (q + 1)] for z in range(w.shape[0] // 256)
-                      for q in range(w.shape[1] // 256)]
-            spans.append((len(mats), len(blocks)))
-            mats += blocks
+            for w in (f.weight, f.weight.t()):   # the forward's W and the backward's dX operand W^T
+                blocks = [w[256 * z:256 * (z + 1), 256 * q:256 * (q + 1)] for z in range(w.shape[0] // 256)
+                          for q in range(w.shape[1] // 256)]
+                spans.append((len(mats), len(blocks)))
+                mats += blocks
         packed = pack_mfma_weights_x3(mats)
-        self.lin_packed = {id(f): torch.stack(packed[a:a + n]).contiguous() for f, (a, n) in zip(lins, spans)}
+        self.lin_packed = {id(f): tuple(torch.stack(packed[a:a + n]).contiguous() for a, n in spans[2 * i:2 * i + 2])
+                           for i, f in enumerate(lins)}
         for i in range(self.T):
             w, b = ws[i], self.buf[i]
             k = dict(zip(names, packed[len(names) * i:len(names) * (i + 1)]))
@@ -321,13 +322,15 @@ class _SelfLayer0Fn(torch.autograd.Function):
 
 
 class _FeedForwardFn(torch.autograd.Function):
-    """QuadMultiEncoder.feed_forward (Linear + Tanh) with its forward on the split-f16 matrix cores
-    (qs_linear_tanh_x3; |x| <= 1: tanh outputs); the backward is the torch one (g (1 - y^2), then the two GEMMs)."""
+    """QuadMultiEncoder.feed_forward (Linear + Tanh; also the self encoder's second layer) on the split-f16 matrix
+    cores: forward qs_linear_tanh_x3 (|x| <= 1: tanh outputs); backward gp = g (1 - y^2) in torch, then dW = gp^T x
+    by 256 x 256 blocks (qs_dw_x3_ld, column scales) and dX = gp W (qs_linear_rows_x3, row scales)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, packed):
+    def forward(ctx, x, weight, bias, packed, packed_t):
         y = linear_tanh_x3(x, packed, bias.detach())
         ctx.save_for_backward(x, weight, y)
+        ctx.packed_t = packed_t
         return y
 
     @staticmethod
@@ -347,7 +350,10 @@ class _FeedForwardFn(torch.autograd.Function):
                 dW[256 * zn:256 * (zn + 1), 256 * zk:256 * (zk + 1)] = r[0]
                 if zk == 0:
                     db[256 * zn:256 * (zn + 1)] = r[1]
-        return gp.mm(weight), dW, db, None
+        # dX = gp W with each row at its power-of-two scale (one max pass over the rows)
+        rs = _pow2_scales(torch.linalg.vector_norm(gp, ord=float("inf"), dim=1))
+        dx = linear_rows_x3(gp.contiguous(), rs, ctx.packed_t, K)
+        return dx, dW, db, None, None
 
 
 class FusedAttentionTrain:
@@ -370,7 +376,7 @@ class FusedAttentionTrain:
         (_FeedForwardFn), else torch."""
         packed = self.runner.lin_packed.get(id(lin))
         if packed is not None and x.is_contiguous():
-            return _FeedForwardFn.apply(x, lin.weight, lin.bias, packed)
+            return _FeedForwardFn.apply(x, lin.weight, lin.bias, packed[0], packed[1])
         return torch.tanh(lin(x))
 
     def self_layer0(self, lin, obs):

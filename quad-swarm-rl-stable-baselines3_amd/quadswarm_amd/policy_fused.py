@@ -120,6 +120,20 @@ def linear_tanh_x3(x, packed, bias, out=None):
     return y
 
 
+def linear_rows_x3(x, row_scale, packed, n_out, out=None):
+    """x W^T for rows x [M, K] of any magnitude (their power-of-two scales row_scale [M]: _pow2_scales of the row
+    maxima) on the split-f16 matrix cores (qs_linear_rows_x3); packed = pack_linear_x3(W) for W [n_out, K]."""
+    M, K = x.shape
+    y = out if out is not None else torch.empty(M, n_out, dtype=torch.float32, device=x.device)
+    assert x.is_contiguous() and row_scale.is_contiguous() and packed.is_contiguous() and y.is_contiguous()
+    st = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
+    NAT.check(NAT.lib().qs_linear_rows_x3(ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(row_scale.data_ptr()), M, K,
+                                          ctypes.c_void_p(packed.data_ptr()), packed.numel() * packed.element_size(),
+                                          ctypes.c_void_p(y.data_ptr()), n_out, st),
+              "qs_linear_rows_x3")
+    return y
+
+
 def supports(policy):
     """Can the fused kernels evaluate this policy's encoders?"""
     c = policy.cfg

@@ -320,3 +320,21 @@ def test_dw_x3_on_column_slices():
             assert ((got.double() - w).abs() / scale).max().item() < 1e-5, (zn, zk)
             G64 = G[:, 256 * zn:256 * (zn + 1)].double()
             assert ((sums.double() - G64.sum(0)).abs() / G64.abs().sum(0)).max().item() < 1e-6
+
+
+@pytest.mark.parametrize("M,K,N", [(3001, 512, 512), (700, 256, 256)])
+def test_linear_rows_x3_matches_fp64(M, K, N):
+    """qs_linear_rows_x3 (the backward's dX = G W): gradient rows spanning 2^-20 .. 2^6 in magnitude, each at its
+    power-of-two scale, against fp64 (relative to each row's magnitude)."""
+    from quadswarm_amd.encoder_train import _pow2_scales
+    from quadswarm_amd.policy_fused import linear_rows_x3, pack_linear_x3
+    g = torch.Generator(device="cuda").manual_seed(M + K)
+    x = torch.randn(M, K, device="cuda", generator=g) * torch.exp2(torch.linspace(-20, 6, M, device="cuda"))[:, None]
+    w = torch.randn(N, K, device="cuda", generator=g) / K ** 0.5
+    rs = _pow2_scales(x.abs().amax(1))
+    got = linear_rows_x3(x, rs, pack_linear_x3(w), N)
+    want = x.double().mm(w.double().t())
+    scale = (x.double().abs().mm(w.double().abs().t())).clamp_min(1e-300)
+    err = ((got.double() - want).abs() / scale).max().item()
+    print(f"M={M} K={K} N={N}: dX relative error {err:.2e}")
+    assert err < 2e-6
