@@ -554,6 +554,11 @@ int qs_linear_tanh_x3(const float* X, int64_t M, int32_t K, const void* w_packed
  * qs_linear_tanh_x3. */
 int qs_linear_rows_x3(const float* X, const float* row_scale, int64_t M, int32_t K, const void* w_packed, int64_t w_bytes,
                       float* Y, int32_t N, void* stream);
+/* tanh backward with its x3 statistics (ABI 15): gp = g (1 - y^2) for [M, N] rows (N 256 or 512), row_scale [M] the
+ * power-of-two scale of each gp row (qs_linear_rows_x3's), col_part [ceil(M / 64)][N] per 64-row block column maxima
+ * of |gp| (qs_colmax_reduce -> qs_dw_x3_ld's column scales); +inf marks a non-finite value. */
+int qs_tanh_grad_stats(const float* g, const float* y, float* gp, float* row_scale, float* col_part, int64_t M, int32_t N,
+                       void* stream);
 /* The maxima over the blocks of per-block column maxima (ABI 15; qs_attn_train.colmax rows): out[s][n] =
  * max_b part_max[s][b][n] for s < n_stats (entries >= 0, +inf propagates), part_max [n_stats][n_blocks][H]. */
 int qs_colmax_reduce(const float* part_max, int32_t n_stats, int32_t n_blocks, int32_t H, float* out, void* stream);

@@ -312,6 +312,20 @@ extern "C" int qs_linear_rows_x3(const float* X, const float* row_scale, int64_t
     QS_HIP(hipGetLastError());
     return QS_OK;
 }
+extern "C" int qs_tanh_grad_stats(const float* g, const float* y, float* gp, float* row_scale, float* col_part, int64_t M,
+                                  int32_t N, void* stream) {
+    namespace P = qs::pol;
+    if (!g || !y || !gp || !row_scale || !col_part) return fail(QS_E_INVALID, "NULL argument");
+    if (M < 1 || M >= (1ll << 31) / 512 || (N != 256 && N != 512)) return fail(QS_E_INVALID, "M >= 1, N 256 or 512");
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 grid((unsigned)((M + P::MROWS - 1) / P::MROWS));
+    if (N == 256)
+        hipLaunchKernelGGL(P::tanh_grad_stats_kernel<1>, grid, dim3(P::NTHR), 0, st, g, y, gp, row_scale, col_part, (long)M);
+    else
+        hipLaunchKernelGGL(P::tanh_grad_stats_kernel<2>, grid, dim3(P::NTHR), 0, st, g, y, gp, row_scale, col_part, (long)M);
+    QS_HIP(hipGetLastError());
+    return QS_OK;
+}
 extern "C" int qs_colmax_reduce(const float* part_max, int32_t n_stats, int32_t n_blocks, int32_t H, float* out,
                                 void* stream) {
     namespace P = qs::pol;

@@ -1029,6 +1029,68 @@ __global__ __launch_bounds__(256) void colmax_reduce_kernel(const float* __restr
 }
 
 // ------------------------------------------------------------------------------------------------------------------
+// tanh backward with the statistics the x3 backward needs (qs_tanh_grad_stats): gp = g (1 - y^2) for [M, N] rows,
+// each row's power-of-two scale (row_scale: max |gp_r| s in [2^13, 2^14), 1 for a zero or non-finite row) and the
+// block's column maxima (col_part [n_blocks][N]: +inf where a value is not finite) -- one pass instead of torch's
+// tanh_backward and two max-abs reductions.  Block = 64 rows, wave w its rows w, w + 4, ...; lane l the columns
+// 4 (l + 64 f) .. + 3, f < N / 256, TG_BR rows' loads in flight at a time.
+// ------------------------------------------------------------------------------------------------------------------
+constexpr int TG_BR = 4;
+template <int NF>
+__global__ __launch_bounds__(NTHR) void tanh_grad_stats_kernel(const float* __restrict__ g, const float* __restrict__ y,
+                                                               float* __restrict__ gp, float* __restrict__ row_scale,
+                                                               float* __restrict__ col_part, long M) {
+    constexpr int N = 256 * NF;
+    __shared__ float4 cm_lds[NWAVE][64 * NF];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const long row0 = (long)blockIdx.x * MROWS;
+    float4 cm[NF];
+#pragma unroll
+    for (int f = 0; f < NF; ++f) cm[f] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int r0 = wave; r0 < MROWS; r0 += NWAVE * TG_BR) {
+        float4 gv[TG_BR][NF], yv[TG_BR][NF];
+#pragma unroll
+        for (int u = 0; u < TG_BR; ++u) {
+            const long r = row0 + r0 + u * NWAVE;
+            const long rr = r < M ? r : 0;   // unconditional loads (row 0 stands in past M)
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+                gv[u][f] = ld4g(g + rr * N + 4 * (lane + 64 * f));
+                yv[u][f] = ld4g(y + rr * N + 4 * (lane + 64 * f));
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < TG_BR; ++u) {
+            const long r = row0 + r0 + u * NWAVE;
+            float m = 0.f;
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+                const float4 v = f4_dtanh(gv[u][f], yv[u][f]);
+                if (r < M) {
+                    st4g(gp + r * N + 4 * (lane + 64 * f), v);
+                    cm[f] = absmax_acc4(cm[f], v);
+                    m = absmax_acc(m, v.x);
+                    m = absmax_acc(m, v.y);
+                    m = absmax_acc(m, v.z);
+                    m = absmax_acc(m, v.w);
+                }
+            }
+            m = wave_max(m);   // (inf stays inf: row_scale -> 1)
+            if (lane == 0 && r < M) row_scale[r] = qs::pol::row_scale(m);
+        }
+    }
+#pragma unroll
+    for (int f = 0; f < NF; ++f) cm_lds[wave][lane + 64 * f] = cm[f];
+    __syncthreads();
+    for (int c4 = tid; c4 < N / 4; c4 += NTHR) {
+        float4 m = cm_lds[0][c4];
+#pragma unroll
+        for (int w = 1; w < NWAVE; ++w) m = max4(m, cm_lds[w][c4]);
+        *reinterpret_cast<float4*>(col_part + (size_t)blockIdx.x * N + 4 * c4) = m;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------------------------
 // column reductions of a gradient G [R, H] (qs_colstats): block p walks rows [p rows_per, (p+1) rows_per), thread n
 // owns column n (blockDim = H): a coalesced row of H floats per step, max |g|, sum w_r g (w: optional row weights)
 // and, with NX > 0, sum g X(r, c) with the layer-0 input X of row r = q K + m (neighbour m of agent q; self row

@@ -323,8 +323,9 @@ class _SelfLayer0Fn(torch.autograd.Function):
 
 class _FeedForwardFn(torch.autograd.Function):
     """QuadMultiEncoder.feed_forward (Linear + Tanh; also the self encoder's second layer) on the split-f16 matrix
-    cores: forward qs_linear_tanh_x3 (|x| <= 1: tanh outputs); backward gp = g (1 - y^2) in torch, then dW = gp^T x
-    by 256 x 256 blocks (qs_dw_x3_ld, column scales) and dX = gp W (qs_linear_rows_x3, row scales)."""
+    cores: forward qs_linear_tanh_x3 (|x| <= 1: tanh outputs); backward gp = g (1 - y^2) with its row scales and
+    column maxima (qs_tanh_grad_stats), then dW = gp^T x by 256 x 256 blocks (qs_dw_x3_ld) and dX = gp W
+    (qs_linear_rows_x3)."""
 
     @staticmethod
     def forward(ctx, x, weight, bias, packed, packed_t):
@@ -336,11 +337,21 @@ class _FeedForwardFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         x, weight, y = ctx.saved_tensors
-        gp = torch.ops.aten.tanh_backward(g, y)
         N, K = weight.shape
-        # the weight gradient gp^T x on the split-f16 matrix cores by 256 x 256 blocks (x: tanh range; gp's column
-        # scales from one max pass), the bias gradient from the same passes; dX in torch
-        gs = _pow2_scales(torch.linalg.vector_norm(gp, ord=float("inf"), dim=0))
+        M = g.shape[0]
+        # gp = g (1 - y^2) with its row scales and per-block column maxima in one pass (qs_tanh_grad_stats)
+        g = g.contiguous()
+        gp = torch.empty(M, N, dtype=torch.float32, device=g.device)
+        rs = torch.empty(M, dtype=torch.float32, device=g.device)
+        nblk = (M + 63) // 64
+        cpart = torch.empty(1, nblk, N, dtype=torch.float32, device=g.device)
+        st = ctypes.c_void_p(torch.cuda.current_stream(g.device).cuda_stream)
+        NAT.check(NAT.lib().qs_tanh_grad_stats(ctypes.c_void_p(g.data_ptr()), ctypes.c_void_p(y.data_ptr()),
+                                               ctypes.c_void_p(gp.data_ptr()), ctypes.c_void_p(rs.data_ptr()),
+                                               ctypes.c_void_p(cpart.data_ptr()), M, N, st), "qs_tanh_grad_stats")
+        # the weight gradient gp^T x on the split-f16 matrix cores by 256 x 256 blocks (x: tanh range), the bias
+        # gradient from the same passes
+        gs = colmax_scales(cpart)[0]
         dW = torch.empty(N, K, dtype=torch.float32, device=g.device)
         db = torch.empty(N, dtype=torch.float32, device=g.device)
         for zn in range(N // 256):
@@ -350,9 +361,8 @@ class _FeedForwardFn(torch.autograd.Function):
                 dW[256 * zn:256 * (zn + 1), 256 * zk:256 * (zk + 1)] = r[0]
                 if zk == 0:
                     db[256 * zn:256 * (zn + 1)] = r[1]
-        # dX = gp W with each row at its power-of-two scale (one max pass over the rows)
-        rs = _pow2_scales(torch.linalg.vector_norm(gp, ord=float("inf"), dim=1))
-        dx = linear_rows_x3(gp.contiguous(), rs, ctx.packed_t, K)
+        # dX = gp W with each row at its power-of-two scale
+        dx = linear_rows_x3(gp, rs, ctx.packed_t, K)
         return dx, dW, db, None, None
 
 

@@ -338,3 +338,30 @@ def test_linear_rows_x3_matches_fp64(M, K, N):
     err = ((got.double() - want).abs() / scale).max().item()
     print(f"M={M} K={K} N={N}: dX relative error {err:.2e}")
     assert err < 2e-6
+
+
+@pytest.mark.parametrize("M,N", [(4099, 512), (777, 256)])
+def test_tanh_grad_stats(M, N):
+    """qs_tanh_grad_stats: gp = g (1 - y^2) (to an fma's rounding), the row scales bitwise those of _pow2_scales over
+    gp's rows, the per-block column maxima's max bitwise torch's, a non-finite value -> +inf / scale 1."""
+    import ctypes
+    from quadswarm_amd import _native as NAT
+    from quadswarm_amd.encoder_train import _pow2_scales
+    g0 = torch.Generator(device="cuda").manual_seed(M)
+    g = torch.randn(M, N, device="cuda", generator=g0) * torch.exp2(torch.linspace(-12, 3, M, device="cuda"))[:, None]
+    y = torch.tanh(torch.randn(M, N, device="cuda", generator=g0))
+    g[7, 5] = float("inf")
+    gp = torch.empty_like(g)
+    rs = torch.empty(M, device="cuda")
+    nb = (M + 63) // 64
+    cp = torch.empty(nb, N, device="cuda")
+    NAT.check(NAT.lib().qs_tanh_grad_stats(ctypes.c_void_p(g.data_ptr()), ctypes.c_void_p(y.data_ptr()),
+                                           ctypes.c_void_p(gp.data_ptr()), ctypes.c_void_p(rs.data_ptr()),
+                                           ctypes.c_void_p(cp.data_ptr()), M, N, None), "qs_tanh_grad_stats")
+    want = g * (1 - y * y)
+    fin = torch.isfinite(want)
+    assert ((gp - want).abs() <= 2e-7 * g.abs())[fin].all()   # (1 - y^2) may be one fma apart
+    m = gp.abs()
+    m[~torch.isfinite(gp)] = float("inf")
+    assert torch.equal(rs, _pow2_scales(m.amax(1)))
+    assert torch.equal(cp.amax(0), m.amax(0))

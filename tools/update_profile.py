@@ -36,7 +36,7 @@ def main():
 
     def step():
         nbr = fused.encodings(obs)
-        values, logp, _ = pol.evaluate_actions(obs, act, nbr=nbr, l0=fused.self_layer0)
+        values, logp, _ = pol.evaluate_actions(obs, act, nbr=nbr, l0=fused.self_layer0, ff=fused.feed_forward)
         ad = (adv - adv.mean()) / (adv.std() + 1e-8)
         ratio = torch.exp(logp - old_lp)
         loss = -torch.min(ad * ratio, ad * torch.clamp(ratio, 0.8, 1.2)).mean() + 0.5 * F.mse_loss(ret, values.flatten())
@@ -57,7 +57,13 @@ def main():
     ev.sort(key=lambda e: -dev(e))
     tot = sum(dev(e) for e in prof.key_averages() if not e.key.startswith(("aten::", "autograd", "_Attn", "Optimizer",
                                                                          "cudaLaunch", "hipLaunch")))
-    print(f"device time of the step's kernels: {tot / 1e3:.2f} ms; aten ops by device time (incl. their kernels):")
+    print(f"device time of the step's kernels: {tot / 1e3:.2f} ms; kernels by device time:")
+    kern = [e for e in prof.key_averages() if not e.key.startswith(("aten::", "autograd", "_Attn", "Optimizer", "cudaLaunch",
+                                                                     "hipLaunch", "_Feed", "_Self", "_Head"))]
+    kern.sort(key=lambda e: -dev(e))
+    for e in kern[:a.rows]:
+        print(f"  {e.key[:70]:70s} x{e.count:3d} {dev(e) / 1e3:8.3f} ms")
+    print("aten ops by device time (incl. their kernels):")
     for e in ev[:a.rows]:
         print(f"  {e.key:22s} x{e.count:3d} {dev(e) / 1e3:8.3f} ms  {str(e.input_shapes)[:150]}")
 
