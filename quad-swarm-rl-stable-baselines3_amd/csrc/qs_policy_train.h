@@ -321,6 +321,10 @@ __global__ __launch_bounds__(NTHR, 2) __attribute__((amdgpu_waves_per_eu(2, 2)))
     __syncthreads();
     QS_STAMP(1);
     mfma_layer_x3<H, H, false>(X, reinterpret_cast<const uint4*>(t.w_a1ep), acc, wave, lane);
+#if QS_POOL_V1_EARLY
+    f32x16 accv[RT][CT];   // neighbor_value_mlp's first layer on the same e2 tile (attn_pool_x3_kernel)
+    mfma_layer_x3<H>(X, reinterpret_cast<const uint4*>(t.w_v1p), accv, wave, lane);
+#endif
     __syncthreads();
     QS_STAMP(2);
     store_tanh_x3<H>(X, acc, iSS, wave, lane, ZeroInit(), [&](int i, int n0, float4 y) {
@@ -363,6 +367,17 @@ __global__ __launch_bounds__(NTHR, 2) __attribute__((amdgpu_waves_per_eu(2, 2)))
         }
         for (int k = 0; k < K; ++k) WT[base + k] = WT[base + k] / s;
     }
+#if QS_POOL_V1_EARLY
+    __syncthreads();   // WT complete (the tile is free since the score barrier)
+    if (tid < MU && row0 + tid < R) tr.w[row0 + tid] = WT[tid];
+    QS_STAMP(6);
+    QS_STAMP(7);
+    store_tanh_x3<H>(X, accv, iSS, wave, lane, [&](int, int n0) { return lds4(A3 + 2 * H + n0); },
+                     [&](int i, int n0, float4 y) {
+                         if (okrow(i)) st4g(tr.v1 + (row0 + i) * H + n0, y);
+                     });
+    __syncthreads();
+#else
     load_rows_x3<H>(X, t.e2, row0, MU, R, tid);
     __syncthreads();
     if (tid < MU && row0 + tid < R) tr.w[row0 + tid] = WT[tid];
@@ -375,6 +390,7 @@ __global__ __launch_bounds__(NTHR, 2) __attribute__((amdgpu_waves_per_eu(2, 2)))
                          if (okrow(i)) st4g(tr.v1 + (row0 + i) * H + n0, y);
                      });
     __syncthreads();
+#endif
     QS_STAMP(8);
     mfma_layer_x3<H>(X, reinterpret_cast<const uint4*>(t.w_v2p), acc, wave, lane);
     __syncthreads();

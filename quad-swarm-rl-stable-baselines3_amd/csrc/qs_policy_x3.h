@@ -30,6 +30,10 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 #define QS_EMBED_PIN 1   // the embed kernels' H x H layer with the scheduling fences of mfma_layer_x3 (PIN)
 #endif
 
+#ifndef QS_POOL_V1_EARLY
+#define QS_POOL_V1_EARLY 1   // pool kernels: value layer 1 on the first e2 tile (no second e2 load; 64 more live registers)
+#endif
+
 constexpr float X3_SX = 256.f;        // activation scale (tanh outputs, e2 rows)
 constexpr float X3_SIN = 16.f;        // raw observation scale (layer 0 inputs)
 constexpr float X3_SW = 256.f;        // weight scale (policy_fused.pack_mfma_weight_x3)
@@ -360,6 +364,11 @@ __global__ __launch_bounds__(NTHR, 2) __attribute__((amdgpu_waves_per_eu(2, 2)))
     load_rows_x3<H>(X, t.e2, row0, MU, R, tid);
     __syncthreads();
     mfma_layer_x3<H, H, false>(X, reinterpret_cast<const uint4*>(t.w_a1ep), acc, wave, lane);
+#if QS_POOL_V1_EARLY
+    // neighbor_value_mlp's first layer on the same e2 tile (its pre-activations held until the tile is free again)
+    f32x16 accv[RT][CT];
+    mfma_layer_x3<H>(X, reinterpret_cast<const uint4*>(t.w_v1p), accv, wave, lane);
+#endif
     __syncthreads();
     store_tanh_x3<H>(X, acc, iSS, wave, lane, ZeroInit());
     __syncthreads();
@@ -382,6 +391,10 @@ __global__ __launch_bounds__(NTHR, 2) __attribute__((amdgpu_waves_per_eu(2, 2)))
         }
         for (int k = 0; k < K; ++k) WT[base + k] = WT[base + k] / s;
     }
+#if QS_POOL_V1_EARLY
+    store_tanh_x3<H>(X, accv, iSS, wave, lane, [&](int, int n0) { return lds4(A3 + 2 * H + n0); });
+    __syncthreads();
+#else
     // neighbor_value_mlp on the e2 rows again (L2 / Infinity Cache)
     load_rows_x3<H>(X, t.e2, row0, MU, R, tid);
     __syncthreads();
@@ -389,6 +402,7 @@ __global__ __launch_bounds__(NTHR, 2) __attribute__((amdgpu_waves_per_eu(2, 2)))
     __syncthreads();
     store_tanh_x3<H>(X, acc, iSS, wave, lane, [&](int, int n0) { return lds4(A3 + 2 * H + n0); });
     __syncthreads();
+#endif
     mfma_layer_x3<H>(X, reinterpret_cast<const uint4*>(t.w_v2p), acc, wave, lane);
     __syncthreads();
     // the weighted h rows into a plain fp32 tile over the same LDS (the split tile is no longer read)

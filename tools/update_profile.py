@@ -19,6 +19,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--B", type=int, default=262144)
     ap.add_argument("--rows", type=int, default=40)
+    ap.add_argument("--rollout", action="store_true", help="one rollout policy forward (FusedRolloutPolicy x3, 32768 "
+                    "agents) instead of the update's minibatch step")
     a = ap.parse_args()
     from quadswarm_amd.encoder_train import FusedAttentionTrain
     from quadswarm_amd.ppo import PolicyConfig, SwarmActorCritic
@@ -34,7 +36,18 @@ def main():
     ret = torch.randn(B, device="cuda")
     old_lp = torch.randn(B, device="cuda")
 
-    def step():
+    if a.rollout:
+        from quadswarm_amd.policy_fused import FusedRolloutPolicy
+        fp = FusedRolloutPolicy(pol, precision="x3")
+        ob = obs[:32768].contiguous()
+
+        def step():
+            fp(ob)
+    else:
+        def step():
+            _minibatch()
+
+    def _minibatch():
         nbr = fused.encodings(obs)
         values, logp, _ = pol.evaluate_actions(obs, act, nbr=nbr, l0=fused.self_layer0, ff=fused.feed_forward)
         ad = (adv - adv.mean()) / (adv.std() + 1e-8)
