@@ -280,7 +280,8 @@ def e2e_settings(cfg):
 def update_flops_per_sample(pol, obs_dim, act_dim, dev, rows=256, split=False):
     """FLOPs of one sample's PPO update (evaluate_actions forward + backward), counted by torch's
     FlopCounterMode (GEMM / addmm / bmm flops) on a small batch of the same policy.  split: also the share of the
-    two towers' neighbour encoders (the modules the fused x3 update runs on the f16 matrix cores)."""
+    modules the fused x3 update runs on the f16 matrix cores: both towers' neighbour encoders, feed_forward and
+    self encoder (all but its first layer's forward, 18 inputs, which stays in hipBLASLt like the heads)."""
     import torch
     from torch.utils.flop_counter import FlopCounterMode
     obs = torch.randn(rows, obs_dim, device=dev)
@@ -292,9 +293,12 @@ def update_flops_per_sample(pol, obs_dim, act_dim, dev, rows=256, split=False):
     total = fc.get_total_flops() / rows
     if not split:
         return total
-    enc = sum(sum(ops.values()) for name, ops in fc.get_flop_counts().items()
-              if name.endswith(".neighbor_encoder")) / rows
-    return total, enc
+    # the x3 share = everything but the heads (forward, dX, dW: 6 d_in d_out each) and the self encoders' first
+    # layer forward (2 so R per tower; its dW is x3) -- FlopCounterMode's per-module keys nest and collide
+    heads = sum(6 * m.in_features * m.out_features for m in (pol.action_net, pol.value_net))
+    l0 = sum(2 * e.self_encoder[0].in_features * e.self_encoder[0].out_features
+             for e in (pol.actor_encoder, pol.critic_encoder))
+    return total, total - heads - l0
 
 
 F16_DENSE_TFLOPS = 2500.0     # MI355X_MICROARCH.md: BF16 / F16 MFMA ~2.5 PF dense
@@ -371,10 +375,12 @@ def end_to_end(env, cfg, dev, world, iters, n_steps=None, log=None, fused=True, 
         "minibatches_per_epoch": n_mb, "policy_params": nparam,
         "policy": f"ActorCriticPolicyCustomSeparateWeights: {pc.neighbor_encoder_type} k={pc.num_use_neighbor_obs}, "
                   f"rnn {pc.rnn_size}, core {pc.rnn_type or 'identity'} x{pc.rnn_num_layers if pc.rnn_type else 0}, "
-                  f"fp32 (torch/hipBLASLt GEMMs" + (f", rollout neighbour encoders: fused HIP MFMA kernels, {precision})"
+                  f"fp32 (torch/hipBLASLt GEMMs" + (f", rollout neighbour encoders + feed_forward / self-encoder layers: "
+                                                    f"fused HIP MFMA kernels, {precision})"
                                                     if tr.fused is not None else ")"),
         "rollout_precision": precision if tr.fused is not None else "torch fp32",
-        "update_precision": ("x3: fused HIP attention-encoder forward + backward (encoder_train.py), dW on split-f16 MFMA (qs_attn_dw_x3)"
+        "update_precision": ("x3: fused HIP attention-encoder forward + backward (encoder_train.py), the encoders' "
+                             "feed_forward / self-encoder layers and every dW on split-f16 MFMA; heads in torch fp32"
                              if upd == "x3" else "torch fp32 autograd (hipBLASLt)"),
         "gemm_table": tuned,
         "update_flop_per_sample": round(fps), "update_tflops": round(upd_tf, 2),
@@ -382,8 +388,8 @@ def end_to_end(env, cfg, dev, world, iters, n_steps=None, log=None, fused=True, 
         "update_encoder_flop_share": round(enc_fps / fps, 3),
         "update_ceiling": {"encoders_tflops": round(enc_peak, 1), "rest_tflops": 157.3, "floor_s": round(floor_s, 4),
                            "frac": round(floor_s / (t_train / iters), 3),
-                           "note": "x3 encoders: 3 f16 MFMA products per fp32 product at the 2.5 PF dense f16 peak"
-                                   if x3 else "all fp32 matrix cores"},
+                           "note": "x3 encoders + MLP layers: 3 f16 MFMA products per fp32 product at the 2.5 PF "
+                                   "dense f16 peak; the rest (heads) fp32" if x3 else "all fp32 matrix cores"},
         "last_update": {k: (round(v, 6) if isinstance(v, float) else v) for k, v in stats.items()},
     }
 
