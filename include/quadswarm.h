@@ -554,6 +554,16 @@ int qs_linear_tanh_x3(const float* X, int64_t M, int32_t K, const void* w_packed
  * qs_linear_tanh_x3. */
 int qs_linear_rows_x3(const float* X, const float* row_scale, int64_t M, int32_t K, const void* w_packed, int64_t w_bytes,
                       float* Y, int32_t N, void* stream);
+/* Y [M, N] = X W^T + bias for X [M, K] fp32 with |x| <= 1 on the split-f16 matrix cores (ABI 15; the attention
+ * score layer's mean half P = e_mean A_m^T + b_a1, quad_multi_model.py:90-93 -- attention_mlp[0] on the repeated
+ * neighbour-embedding mean): qs_linear_tanh_x3 without the tanh; K, N, w_packed / w_bytes as qs_linear_tanh_x3. */
+int qs_linear_bias_x3(const float* X, int64_t M, int32_t K, const void* w_packed, int64_t w_bytes, const float* bias,
+                      float* Y, int32_t N, void* stream);
+/* out [M, N] = sum_{s < n_slabs} G[s M + m, :] for G [n_slabs M, N] (ABI 15; the backward's dP[b] = sum_k
+ * da1_pre[k B + b] of the repeat tiling, quad_multi_model.py:90-92), with out's row scales (row_scale [M]) and per
+ * 64-row block column maxima (col_part [ceil(M / 64)][N]) as qs_tanh_grad_stats; N 256 or 512. */
+int qs_slab_sum_stats(const float* G, int32_t n_slabs, int64_t M, int32_t N, float* out, float* row_scale,
+                      float* col_part, void* stream);
 /* tanh backward with its x3 statistics (ABI 15): gp = g (1 - y^2) for [M, N] rows (N 256 or 512), row_scale [M] the
  * power-of-two scale of each gp row (qs_linear_rows_x3's), col_part [ceil(M / 64)][N] per 64-row block column maxima
  * of |gp| (qs_colmax_reduce -> qs_dw_x3_ld's column scales); +inf marks a non-finite value. */

@@ -277,12 +277,12 @@ extern "C" int qs_linear_tanh_x3(const float* X, int64_t M, int32_t K, const voi
     const size_t lds = P::linear_x3_lds_bytes();
     const uint4* wp = reinterpret_cast<const uint4*>(w_packed);
     if (K == 256) {
-        QS_HIP(hipFuncSetAttribute((const void*)P::linear_tanh_x3_kernel<1, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL((P::linear_tanh_x3_kernel<1, false>), grid, dim3(P::NTHR), lds, st, X, (long)M, wp, bias, Y, N,
+        QS_HIP(hipFuncSetAttribute((const void*)P::linear_tanh_x3_kernel<1, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL((P::linear_tanh_x3_kernel<1, false, true>), grid, dim3(P::NTHR), lds, st, X, (long)M, wp, bias, Y, N,
                            nullptr);
     } else {
-        QS_HIP(hipFuncSetAttribute((const void*)P::linear_tanh_x3_kernel<2, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL((P::linear_tanh_x3_kernel<2, false>), grid, dim3(P::NTHR), lds, st, X, (long)M, wp, bias, Y, N,
+        QS_HIP(hipFuncSetAttribute((const void*)P::linear_tanh_x3_kernel<2, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL((P::linear_tanh_x3_kernel<2, false, true>), grid, dim3(P::NTHR), lds, st, X, (long)M, wp, bias, Y, N,
                            nullptr);
     }
     QS_HIP(hipGetLastError());
@@ -301,12 +301,12 @@ extern "C" int qs_linear_rows_x3(const float* X, const float* row_scale, int64_t
     const size_t lds = P::linear_x3_lds_bytes();
     const uint4* wp = reinterpret_cast<const uint4*>(w_packed);
     if (K == 256) {
-        QS_HIP(hipFuncSetAttribute((const void*)P::linear_tanh_x3_kernel<1, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL((P::linear_tanh_x3_kernel<1, true>), grid, dim3(P::NTHR), lds, st, X, (long)M, wp, nullptr, Y, N,
+        QS_HIP(hipFuncSetAttribute((const void*)P::linear_tanh_x3_kernel<1, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL((P::linear_tanh_x3_kernel<1, true, true>), grid, dim3(P::NTHR), lds, st, X, (long)M, wp, nullptr, Y, N,
                            row_scale);
     } else {
-        QS_HIP(hipFuncSetAttribute((const void*)P::linear_tanh_x3_kernel<2, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL((P::linear_tanh_x3_kernel<2, true>), grid, dim3(P::NTHR), lds, st, X, (long)M, wp, nullptr, Y, N,
+        QS_HIP(hipFuncSetAttribute((const void*)P::linear_tanh_x3_kernel<2, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL((P::linear_tanh_x3_kernel<2, true, true>), grid, dim3(P::NTHR), lds, st, X, (long)M, wp, nullptr, Y, N,
                            row_scale);
     }
     QS_HIP(hipGetLastError());
@@ -323,6 +323,47 @@ extern "C" int qs_tanh_grad_stats(const float* g, const float* y, float* gp, flo
         hipLaunchKernelGGL(P::tanh_grad_stats_kernel<1>, grid, dim3(P::NTHR), 0, st, g, y, gp, row_scale, col_part, (long)M);
     else
         hipLaunchKernelGGL(P::tanh_grad_stats_kernel<2>, grid, dim3(P::NTHR), 0, st, g, y, gp, row_scale, col_part, (long)M);
+    QS_HIP(hipGetLastError());
+    return QS_OK;
+}
+extern "C" int qs_linear_bias_x3(const float* X, int64_t M, int32_t K, const void* w_packed, int64_t w_bytes,
+                                 const float* bias, float* Y, int32_t N, void* stream) {
+    namespace P = qs::pol;
+    if (!X || !w_packed || !bias || !Y) return fail(QS_E_INVALID, "NULL argument");
+    if (M < 1 || M >= (1ll << 31) / 512 || (K != 256 && K != 512) || N < 256 || N > 1024 || N % 256)
+        return fail(QS_E_INVALID, "M >= 1, K 256 or 512, N a multiple of 256 up to 1024");
+    if (w_bytes != (int64_t)(N / 256) * (K / 256) * 256 * 256 * 2 * 2)
+        return fail(QS_E_INVALID, "w_bytes: the packed weight must hold (N / 256) (K / 256) packed 256 x 256 blocks");
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 grid((unsigned)((M + P::MROWS - 1) / P::MROWS), (unsigned)(N / 256));
+    const size_t lds = P::linear_x3_lds_bytes();
+    const uint4* wp = reinterpret_cast<const uint4*>(w_packed);
+    if (K == 256) {
+        QS_HIP(hipFuncSetAttribute((const void*)P::linear_tanh_x3_kernel<1, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL((P::linear_tanh_x3_kernel<1, false, false>), grid, dim3(P::NTHR), lds, st, X, (long)M, wp, bias, Y,
+                           N, nullptr);
+    } else {
+        QS_HIP(hipFuncSetAttribute((const void*)P::linear_tanh_x3_kernel<2, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL((P::linear_tanh_x3_kernel<2, false, false>), grid, dim3(P::NTHR), lds, st, X, (long)M, wp, bias, Y,
+                           N, nullptr);
+    }
+    QS_HIP(hipGetLastError());
+    return QS_OK;
+}
+extern "C" int qs_slab_sum_stats(const float* G, int32_t n_slabs, int64_t M, int32_t N, float* out, float* row_scale,
+                                 float* col_part, void* stream) {
+    namespace P = qs::pol;
+    if (!G || !out || !row_scale || !col_part) return fail(QS_E_INVALID, "NULL argument");
+    if (n_slabs < 1 || M < 1 || (int64_t)n_slabs * M >= (1ll << 31) / 512 || (N != 256 && N != 512))
+        return fail(QS_E_INVALID, "n_slabs >= 1, M >= 1, n_slabs M < 2^22, N 256 or 512");
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 grid((unsigned)((M + P::MROWS - 1) / P::MROWS));
+    if (N == 256)
+        hipLaunchKernelGGL(P::slab_sum_stats_kernel<1>, grid, dim3(P::NTHR), 0, st, G, (int)n_slabs, out, row_scale, col_part,
+                           (long)M);
+    else
+        hipLaunchKernelGGL(P::slab_sum_stats_kernel<2>, grid, dim3(P::NTHR), 0, st, G, (int)n_slabs, out, row_scale, col_part,
+                           (long)M);
     QS_HIP(hipGetLastError());
     return QS_OK;
 }

@@ -1107,6 +1107,84 @@ __global__ __launch_bounds__(NTHR) void tanh_grad_stats_kernel(const float* __re
 }
 
 // ------------------------------------------------------------------------------------------------------------------
+// A sum over slabs with the same statistics (qs_slab_sum_stats): out[m] = sum_{s < S} G[s M + m] for [M, N] rows -- the
+// score layer's mean-half gradient dP[b] = sum_k da1_pre[k B + b] (quad_multi_model.py:90-92 pairs attention row j
+// with agent j % B through the repeat tiling) -- with each out row's power-of-two scale and the block's column maxima
+// as qs_tanh_grad_stats (for qs_linear_rows_x3 and qs_dw_x3_ld).  The slabs SS_U at a time with unconditional loads
+// (the last slab stands in past S and is not added); SS_BR rows per wave in flight.
+// ------------------------------------------------------------------------------------------------------------------
+constexpr int SS_BR = 4, SS_U = 4;
+template <int NF>
+__global__ __launch_bounds__(NTHR) void slab_sum_stats_kernel(const float* __restrict__ G, int S, float* __restrict__ out,
+                                                              float* __restrict__ row_scale, float* __restrict__ col_part,
+                                                              long M) {
+    constexpr int N = 256 * NF;
+    __shared__ float4 cm_lds[NWAVE][64 * NF];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const long row0 = (long)blockIdx.x * MROWS;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 cm[NF];
+#pragma unroll
+    for (int f = 0; f < NF; ++f) cm[f] = z4;
+    for (int r0 = wave; r0 < MROWS; r0 += NWAVE * SS_BR) {
+        float4 sum[SS_BR][NF];
+#pragma unroll
+        for (int u = 0; u < SS_BR; ++u)
+#pragma unroll
+            for (int f = 0; f < NF; ++f) sum[u][f] = z4;
+        for (int s0 = 0; s0 < S; s0 += SS_U) {
+            float4 v[SS_U][SS_BR][NF];
+#pragma unroll
+            for (int q = 0; q < SS_U; ++q) {
+                const long s = s0 + q < S ? s0 + q : S - 1;
+#pragma unroll
+                for (int u = 0; u < SS_BR; ++u) {
+                    const long r = row0 + r0 + u * NWAVE;
+                    const long rr = r < M ? r : 0;   // unconditional loads (row 0 stands in past M)
+#pragma unroll
+                    for (int f = 0; f < NF; ++f) v[q][u][f] = ld4g(G + (s * M + rr) * N + 4 * (lane + 64 * f));
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < SS_U; ++q)
+                if (s0 + q < S)
+#pragma unroll
+                    for (int u = 0; u < SS_BR; ++u)
+#pragma unroll
+                        for (int f = 0; f < NF; ++f) sum[u][f] = f4_add(sum[u][f], v[q][u][f]);
+        }
+#pragma unroll
+        for (int u = 0; u < SS_BR; ++u) {
+            const long r = row0 + r0 + u * NWAVE;
+            float m = 0.f;
+#pragma unroll
+            for (int f = 0; f < NF; ++f) {
+                const float4 x = sum[u][f];
+                if (r < M) {
+                    st4g(out + r * N + 4 * (lane + 64 * f), x);
+                    cm[f] = absmax_acc4(cm[f], x);
+                    m = absmax_acc(m, x.x);
+                    m = absmax_acc(m, x.y);
+                    m = absmax_acc(m, x.z);
+                    m = absmax_acc(m, x.w);
+                }
+            }
+            m = wave_max(m);
+            if (lane == 0 && r < M) row_scale[r] = qs::pol::row_scale(m);
+        }
+    }
+#pragma unroll
+    for (int f = 0; f < NF; ++f) cm_lds[wave][lane + 64 * f] = cm[f];
+    __syncthreads();
+    for (int c4 = tid; c4 < N / 4; c4 += NTHR) {
+        float4 m = cm_lds[0][c4];
+#pragma unroll
+        for (int w = 1; w < NWAVE; ++w) m = max4(m, cm_lds[w][c4]);
+        *reinterpret_cast<float4*>(col_part + (size_t)blockIdx.x * N + 4 * c4) = m;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------------------------
 // column reductions of a gradient G [R, H] (qs_colstats): block p walks rows [p rows_per, (p+1) rows_per), thread n
 // owns column n (blockDim = H): a coalesced row of H floats per step, max |g|, sum w_r g (w: optional row weights)
 // and, with NX > 0, sum g X(r, c) with the layer-0 input X of row r = q K + m (neighbour m of agent q; self row

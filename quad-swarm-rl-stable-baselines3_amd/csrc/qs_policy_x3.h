@@ -453,8 +453,8 @@ namespace pol {
 // ------------------------------------------------------------------------------------------------------------------
 // ROWS (the backward's dX = G W for gradient rows G of any magnitude): no bias and no activation, row r of X staged
 // at its power-of-two scale rs[r] (max |x_r| rs[r] in [2^13, 2^14): exact, it factors out of the row's products),
-// Y = acc / (rs[r] s_w).
-template <int P, bool ROWS = false>
+// Y = acc / (rs[r] s_w).  ACT false (the attention score layer's mean half P = e_mean A_m^T + b_a1): bias, no tanh.
+template <int P, bool ROWS = false, bool ACT = true>
 __global__ __launch_bounds__(NTHR, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void linear_tanh_x3_kernel(
     const float* __restrict__ X, long M, const uint4* __restrict__ Wp, const float* __restrict__ bias,
     float* __restrict__ Y, int N, const float* __restrict__ rs = nullptr) {
@@ -529,8 +529,9 @@ __global__ __launch_bounds__(NTHR, 2) __attribute__((amdgpu_waves_per_eu(2, 2)))
                                     acc[rt][c][4 * g + 3] * si);
                 } else {
                     const float4 b = lds4(BI + n0);
-                    y = make_float4(tanh_fast(fmaf(acc[rt][c][4 * g], iSS, b.x)), tanh_fast(fmaf(acc[rt][c][4 * g + 1], iSS, b.y)),
-                                    tanh_fast(fmaf(acc[rt][c][4 * g + 2], iSS, b.z)), tanh_fast(fmaf(acc[rt][c][4 * g + 3], iSS, b.w)));
+                    y = make_float4(fmaf(acc[rt][c][4 * g], iSS, b.x), fmaf(acc[rt][c][4 * g + 1], iSS, b.y),
+                                    fmaf(acc[rt][c][4 * g + 2], iSS, b.z), fmaf(acc[rt][c][4 * g + 3], iSS, b.w));
+                    if constexpr (ACT) y = make_float4(tanh_fast(y.x), tanh_fast(y.y), tanh_fast(y.z), tanh_fast(y.w));
                 }
                 *reinterpret_cast<float4*>(Y + (row0 + i) * N + 256 * z + n0) = y;
             }

@@ -7,11 +7,11 @@ with tanh, forward and backward, ~20 hipBLASLt GEMMs and as many elementwise tan
 Here both towers' encoders are one autograd node (FusedAttentionTrain), whose forward and backward are the HIP
 kernels of csrc/qs_policy_train.h through the C ABI:
 
-  forward   qs_attn_embed_train_x3 (e1, e2, mean_K e2), torch P = mean A_m^T + b_a1, qs_attn_pool_train_x3 (a1, a2,
+  forward   qs_attn_embed_train_x3 (e1, e2, mean_K e2), P = mean A_m^T + b_a1 (qs_linear_bias_x3), qs_attn_pool_train_x3 (a1, a2,
             softmax, v1, h, pooled out) -- the rollout's x3 kernels plus the saved activations
   backward  qs_attn_bwd1_x3: the value chain (dh_pre -> dv1_pre -> dL/de2) and the attention chain (dscore ->
             da2_pre -> da1_pre -> dL/de2) of every 64-row block on the matrix cores, tanh derivatives in the epilogues;
-            torch: dP, dL/d e_mean (the grid-wide per-agent terms, [B, H]);
+            dP (qs_slab_sum_stats) and dL/d e_mean (qs_linear_rows_x3): the grid-wide per-agent terms, [B, H];
             qs_attn_bwd2_x3: dL/de2 -> de2_pre -> de1_pre;
             the weight gradients dW = grad^T act over the B K rows on the same split-f16 matrix cores (qs_attn_dw_x3:
             split over row ranges, per-column power-of-two scales of the gradient, the parts summed by torch), the
@@ -25,8 +25,8 @@ import ctypes
 import torch
 
 from . import _native as NAT
-from .policy_fused import (F16_MAX, X3_SIN, X3_SW, ff_supported, linear_rows_x3, linear_tanh_x3,  # noqa: F401
-                           pack_mfma_weight_x3, pack_mfma_weights_x3, self_l2_supported, supports)
+from .policy_fused import (F16_MAX, X3_SIN, X3_SW, ff_supported, linear_bias_x3, linear_rows_x3,  # noqa: F401
+                           linear_tanh_x3, pack_mfma_weight_x3, pack_mfma_weights_x3, self_l2_supported, supports)
 
 _PARAMS = ("e1_w", "e1_b", "e2_w", "e2_b", "v1_w", "v1_b", "v2_w", "v2_b", "a1_w", "a1_b", "a2_w", "a2_b", "a3_w", "a3_b")
 
@@ -126,6 +126,19 @@ def dw0_x3(G, obs, B, K, so, nd, gs=None, parts=512):
     return torch.cat((dW[:, nd:nd + so], dW[:, :nd]), dim=1), psum.sum(0)
 
 
+def slab_sum_stats(G, n_slabs, out, row_scale, col_part):
+    """out [M, N] = sum_s G[s M + m] for G [n_slabs M, N] (qs_slab_sum_stats: dP[b] = sum_k da1_pre[k B + b]), with
+    out's row scales [M] and per-64-row-block column maxima [1, ceil(M / 64), N] in the same pass."""
+    M, N = out.shape
+    assert G.is_contiguous() and G.shape == (n_slabs * M, N) and out.is_contiguous()
+    assert row_scale.shape == (M,) and col_part.shape == (1, (M + 63) // 64, N)
+    st = ctypes.c_void_p(torch.cuda.current_stream(G.device).cuda_stream)
+    NAT.check(NAT.lib().qs_slab_sum_stats(ctypes.c_void_p(G.data_ptr()), n_slabs, M, N, ctypes.c_void_p(out.data_ptr()),
+                                          ctypes.c_void_p(row_scale.data_ptr()), ctypes.c_void_p(col_part.data_ptr()),
+                                          st), "qs_slab_sum_stats")
+    return out
+
+
 class _Runner:
     """Buffers and launches for one policy's towers (reused across minibatches of the same size)."""
 
@@ -162,7 +175,8 @@ class _Runner:
         self.buf = [dict(e1=z(R, H), e2=z(R, H), a1=z(R, H), a2=z(R, H), v1=z(R, H), h=z(R, H), w=z(R),
                          e_mean=z(B, H), P=z(B, H), out=z(B, H), dh_pre=z(R, H), dv1_pre=z(R, H), da2_pre=z(R, H),
                          da1_pre=z(R, H), de2p=z(R, H), dscore=z(R), dem=z(B, H),
-                         colmax=z(NAT.ATTN_NCOLMAX, nblk, H), a3w_part=z(nblk, H)) for _ in range(T)]
+                         colmax=z(NAT.ATTN_NCOLMAX, nblk, H), a3w_part=z(nblk, H),
+                         dP=z(B, H), dP_rs=z(B), dP_cm=z(1, (B + 63) // 64, H)) for _ in range(T)]
 
     def _pack(self, params):
         """x3-pack the towers' weights (forward operands and the backward's transposes; both towers' 22 matrices as
@@ -181,6 +195,12 @@ class _Runner:
             ws.append(w)
             mats += [w_e1, w["e2_w"], w["v1_w"], w["v2_w"], w["a1_w"][:, :H], w["a2_w"], w["v2_w"].t(), w["v1_w"].t(),
                      w["a2_w"].t(), w["a1_w"][:, :H].t(), w["e2_w"].t()]
+        # the score layer's mean half A_m (P's forward) and A_m^T (dL/d e_mean) for the x3 linear kernels (H 256)
+        am_span = None
+        if H == 256 and self.dw_x3:
+            am_span = len(mats)
+            for w in ws:
+                mats += [w["a1_w"][:, H:], w["a1_w"][:, H:].t()]
         # the feed_forward Linears' and the self encoders' second Linears' 256 x 256 blocks ride along
         # (FusedAttentionTrain.feed_forward: Linear + Tanh of tanh inputs on qs_linear_tanh_x3)
         lins = [enc.feed_forward[0] for enc in self.encs if ff_supported(enc.feed_forward[0])]
@@ -195,13 +215,15 @@ class _Runner:
         packed = pack_mfma_weights_x3(mats)
         self.lin_packed = {id(f): tuple(torch.stack(packed[a:a + n]).contiguous() for a, n in spans[2 * i:2 * i + 2])
                            for i, f in enumerate(lins)}
+        self.am_packed = ([(packed[am_span + 2 * i][None].contiguous(), packed[am_span + 2 * i + 1][None].contiguous())
+                           for i in range(self.T)] if am_span is not None else None)
         for i in range(self.T):
             w, b = ws[i], self.buf[i]
             k = dict(zip(names, packed[len(names) * i:len(names) * (i + 1)]))
             k.update(b_e1=w["e1_b"].detach().contiguous(), b_e2=w["e2_b"].detach().contiguous(),
                      b_v1=w["v1_b"].detach().contiguous(), b_v2=w["v2_b"].detach().contiguous(),
                      b_a2=w["a2_b"].detach().contiguous(), w_a3=w["a3_w"].detach().reshape(-1).contiguous(),
-                     a_m=w["a1_w"][:, H:].detach().contiguous())
+                     a_m=w["a1_w"][:, H:].detach().contiguous(), b_a1=w["a1_b"].detach().contiguous())
             self.keep.append(k)
             t = self.towers[i]
             t.w_e1p, t.b_e1, t.w_e2p, t.b_e2 = p(k["w_e1p"]), p(k["b_e1"]), p(k["w_e2p"]), p(k["b_e2"])
@@ -232,8 +254,11 @@ class _Runner:
         H, K, so, st = self.H, self.K, self.so, self.stream(obs.device)
         NAT.check(self.L.qs_attn_embed_train_x3(ctypes.c_void_p(obs.data_ptr()), obs.shape[1], so, so, B, K, self.nd, H,
                                                 self.towers, self.trains, self.T, st), "qs_attn_embed_train_x3")
-        for i in range(self.T):   # P = e_mean A_m^T + b_a1 (A_m contiguous: the strided slice picks a 4x slower GEMM)
-            torch.addmm(params[14 * i + 9], self.buf[i]["e_mean"], self.keep[i]["a_m"].t(), out=self.buf[i]["P"])
+        for i in range(self.T):   # P = e_mean A_m^T + b_a1 (|e_mean| <= 1: a mean of tanh rows)
+            if self.am_packed is not None:
+                linear_bias_x3(self.buf[i]["e_mean"], self.am_packed[i][0], self.keep[i]["b_a1"], out=self.buf[i]["P"])
+            else:   # A_m contiguous: the strided slice picks a 4x slower GEMM
+                torch.addmm(params[14 * i + 9], self.buf[i]["e_mean"], self.keep[i]["a_m"].t(), out=self.buf[i]["P"])
         NAT.check(self.L.qs_attn_pool_train_x3(B, K, H, self.towers, self.trains, self.T, st), "qs_attn_pool_train_x3")
         self.pending = True
         return [self.buf[i]["out"].clone() for i in range(self.T)]
@@ -262,10 +287,18 @@ class _Runner:
             # sum_j dscore_j a2_j: backward 1's per-block partial sums
             gi["a3_w"] = b["a3w_part"].sum(0).view(1, -1) if self.dw_x3 else b["dscore"].view(1, -1).mm(b["a2"])
             gi["a3_b"] = b["dscore"].sum().view(1)
-            dP = b["da1_pre"].view(K, B, H).sum(0)                     # rows j with j % B == b (the repeat tiling)
             dA_e, gi["a1_b"] = self.dw(b["da1_pre"], b["e2"], gsc[3])   # a1_b = sum_j da1_pre_j = sum_b dP_b
-            gi["a1_w"] = torch.cat((dA_e, self.dw(dP, b["e_mean"])[0]), dim=1)   # |e_mean| <= 1 (a mean of tanh)
-            torch.mm(dP, self.keep[i]["a_m"], out=b["dem"])            # dL/d e_mean
+            if self.am_packed is not None:
+                # dP[b] = sum of the rows j with j % B == b (the repeat tiling) with its row scales and column maxima,
+                # dL/d e_mean = dP A_m on the x3 layer at those row scales, dA_m = dP^T e_mean (|e_mean| <= 1)
+                dP = slab_sum_stats(b["da1_pre"], K, b["dP"], b["dP_rs"], b["dP_cm"])
+                dA_m = self.dw(dP, b["e_mean"], colmax_scales(b["dP_cm"])[0])[0]
+                linear_rows_x3(dP, b["dP_rs"], self.am_packed[i][1], H, out=b["dem"])
+            else:
+                dP = b["da1_pre"].view(K, B, H).sum(0)                 # rows j with j % B == b (the repeat tiling)
+                dA_m = self.dw(dP, b["e_mean"])[0]
+                torch.mm(dP, self.keep[i]["a_m"], out=b["dem"])        # dL/d e_mean
+            gi["a1_w"] = torch.cat((dA_e, dA_m), dim=1)
             for n in gi:
                 grads[w0 + _PARAMS.index(n)] = gi[n]
         NAT.check(self.L.qs_attn_bwd2_x3(B, K, H, self.towers, self.trains, self.T, st), "qs_attn_bwd2_x3")

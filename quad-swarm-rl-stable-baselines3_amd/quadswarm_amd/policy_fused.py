@@ -6,7 +6,7 @@ swarm_rl/models/quad_multi_model.py:44-101) run by the HIP kernels of csrc/qs_po
 
 Per step, for the actor and the critic tower at once (one launch per stage):
   HIP     e1 (self and neighbour halves of layer 0), e2 rows, mean_K(e2)   (qs_attn_embed)
-  torch   P = mean_K(e2) W_a1[:, H:]^T + b_a1                      [B, H]
+  HIP     P = mean_K(e2) W_a1[:, H:]^T + b_a1 (x3, H 256; else torch)   [B, H]
   HIP     value path, attention path, softmax over K, pooled out    (qs_attn_pool)
   torch   self encoder, feed_forward, core, decoder, heads          (small per-agent GEMMs)
 The result is the same function as the torch module (fp32 throughout; only the summation order of the
@@ -120,6 +120,21 @@ def linear_tanh_x3(x, packed, bias, out=None):
     return y
 
 
+def linear_bias_x3(x, packed, bias, out=None):
+    """x W^T + b for x [M, K] (|x| <= 1) on the split-f16 matrix cores (qs_linear_bias_x3: qs_linear_tanh_x3 without
+    the tanh); the attention score layer's mean half P = e_mean A_m^T + b_a1."""
+    M, K = x.shape
+    N = bias.shape[0]
+    y = out if out is not None else torch.empty(M, N, dtype=torch.float32, device=x.device)
+    assert x.is_contiguous() and packed.is_contiguous() and bias.is_contiguous() and y.is_contiguous()
+    st = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
+    NAT.check(NAT.lib().qs_linear_bias_x3(ctypes.c_void_p(x.data_ptr()), M, K, ctypes.c_void_p(packed.data_ptr()),
+                                          packed.numel() * packed.element_size(), ctypes.c_void_p(bias.data_ptr()),
+                                          ctypes.c_void_p(y.data_ptr()), N, st),
+              "qs_linear_bias_x3")
+    return y
+
+
 def linear_rows_x3(x, row_scale, packed, n_out, out=None):
     """x W^T for rows x [M, K] of any magnitude (their power-of-two scales row_scale [M]: _pow2_scales of the row
     maxima) on the split-f16 matrix cores (qs_linear_rows_x3); packed = pack_linear_x3(W) for W [n_out, K]."""
@@ -219,9 +234,11 @@ class FusedRolloutPolicy:
                 w_v1p=pack(val[0].weight), b_v1=val[0].bias.detach(),
                 w_v2p=pack(val[2].weight), b_v2=val[2].bias.detach(),
                 w_a1ep=pack(att[0].weight[:, :H]), w_a1m=att[0].weight[:, H:].detach().contiguous(),
-                b_a1=att[0].bias.detach(),
+                b_a1=att[0].bias.detach().contiguous(),
                 w_a2p=pack(att[2].weight), b_a2=att[2].bias.detach(),
                 w_a3=att[4].weight.detach().reshape(-1).contiguous(), b_a3=float(att[4].bias.detach().item())))
+            if prec == "x3" and H == 256:   # P = e_mean A_m^T + b_a1 on qs_linear_bias_x3 (|e_mean| <= 1)
+                packed[-1].update(w_a1mp=pack_linear_x3(att[0].weight[:, H:].detach()))
             ff = enc.feed_forward[0]
             if prec == "x3" and ff_supported(ff) and float(ff.weight.detach().abs().amax()) < F16_MAX / X3_SW:
                 packed[-1].update(w_ffp=pack_linear_x3(ff.weight.detach()), b_ff=ff.bias.detach().contiguous())
@@ -274,7 +291,10 @@ class FusedRolloutPolicy:
         NAT.check(embed(ctypes.c_void_p(obs.data_ptr()), obs.shape[1], so, so, B, K, self.nd, H,
                         self.towers, len(self.encs), st), "qs_attn_embed")
         for i, w in enumerate(self.packed):
-            torch.addmm(w["b_a1"], self.e_mean[i], w["w_a1m"].t(), out=self.P[i])
+            if "w_a1mp" in w:
+                linear_bias_x3(self.e_mean[i], w["w_a1mp"], w["b_a1"], out=self.P[i])
+            else:
+                torch.addmm(w["b_a1"], self.e_mean[i], w["w_a1m"].t(), out=self.P[i])
         NAT.check(pool(B, K, H, self.towers, len(self.encs), st), "qs_attn_pool")
         return self.out
 

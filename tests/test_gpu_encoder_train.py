@@ -304,6 +304,48 @@ def test_linear_tanh_x3_matches_fp64(M, K, N):
     assert e_x3 < 2e-6 and e_x3 < 8 * e_32 + 1e-6
 
 
+@pytest.mark.parametrize("M,K,N", [(4097, 256, 256), (1000, 512, 512)])
+def test_linear_bias_x3_matches_fp64(M, K, N):
+    """qs_linear_bias_x3 (the score layer's mean half P = e_mean A_m^T + b_a1) against fp64 on tanh-range inputs,
+    ragged row counts, relative to the row's |x| |w| products."""
+    from quadswarm_amd.policy_fused import linear_bias_x3, pack_linear_x3
+    g = torch.Generator(device="cuda").manual_seed(M + K + N + 1)
+    x = torch.tanh(torch.randn(M, K, device="cuda", generator=g) * 2)
+    w = torch.randn(N, K, device="cuda", generator=g) / K ** 0.5
+    b = torch.randn(N, device="cuda", generator=g) * 0.1
+    got = linear_bias_x3(x, pack_linear_x3(w), b)
+    want = x.double().mm(w.double().t()) + b.double()
+    scale = x.double().abs().mm(w.double().abs().t()) + b.double().abs()
+    err = ((got.double() - want).abs() / scale).max().item()
+    e32 = ((torch.nn.functional.linear(x, w, b).double() - want).abs() / scale).max().item()
+    print(f"M={M} K={K} N={N}: relative error x3 {err:.2e}, torch fp32 {e32:.2e}")
+    assert err < 2e-6
+
+
+@pytest.mark.parametrize("S,M,N", [(6, 4099, 256), (7, 777, 512), (1, 64, 256), (5, 1, 256)])
+def test_slab_sum_stats(S, M, N):
+    """qs_slab_sum_stats (dP[b] = sum_k da1_pre[k B + b]): the sum against fp64, the row scales bitwise those of
+    _pow2_scales over the result's rows, the block maxima's max bitwise torch's, a non-finite value -> +inf / scale 1."""
+    from quadswarm_amd.encoder_train import _pow2_scales, slab_sum_stats
+    g0 = torch.Generator(device="cuda").manual_seed(S * M + N)
+    G = torch.randn(S * M, N, device="cuda", generator=g0) * torch.exp2(torch.linspace(-14, 4, S * M, device="cuda"))[:, None]
+    if M > 7:
+        G[(S - 1) * M + 7, 5] = float("nan")
+    out = torch.full((M, N), 7.0, device="cuda")
+    rs = torch.empty(M, device="cuda")
+    cp = torch.empty(1, (M + 63) // 64, N, device="cuda")
+    slab_sum_stats(G, S, out, rs, cp)
+    want = G.double().view(S, M, N).sum(0)
+    fin = torch.isfinite(want)
+    scale = G.double().abs().view(S, M, N).sum(0)
+    assert ((out.double() - want).abs() <= 8e-7 * scale)[fin].all()
+    assert (~torch.isfinite(out) == ~fin).all()
+    m = out.abs()
+    m[~torch.isfinite(out)] = float("inf")
+    assert torch.equal(rs, _pow2_scales(m.amax(1)))
+    assert torch.equal(cp[0].amax(0), m.amax(0))
+
+
 def test_dw_x3_on_column_slices():
     """qs_dw_x3_ld: the 256 x 256 blocks of a [512, 512] weight gradient from column slices of [R, 512] rows (the
     feed_forward's backward), against fp64."""
