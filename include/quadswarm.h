@@ -548,6 +548,11 @@ int qs_dw_x3_ld(const float* G, int32_t ldg, const float* A, int32_t lda, const 
  * (N / 256) (K / 256) 262 144 bytes). */
 int qs_linear_tanh_x3(const float* X, int64_t M, int32_t K, const void* w_packed, int64_t w_bytes, const float* bias,
                       float* Y, int32_t N, void* stream);
+/* qs_linear_tanh_x3 with K = 512 on the concatenation [X0 | X1] of two [M, 256] row-major tensors (ABI 15; the
+ * feed_forward's input torch.cat((embeddings, neighborhood_embedding), 1), quad_multi_model.py:342, without
+ * forming it); w_packed / w_bytes as qs_linear_tanh_x3 for W [N, 512]. */
+int qs_linear_tanh_cat_x3(const float* X0, const float* X1, int64_t M, const void* w_packed, int64_t w_bytes,
+                          const float* bias, float* Y, int32_t N, void* stream);
 /* Y [M, N] = X W^T for rows X [M, K] of any magnitude (ABI 15; the feed_forward's backward dX = G W with the packed
  * W^T): row r staged at its power-of-two scale row_scale[r] (max |X[r, :]| row_scale[r] < 2^14 -- the
  * qs_attn_dw_x3 column-scale rule applied to rows), no bias, no activation; K, N, w_packed / w_bytes as

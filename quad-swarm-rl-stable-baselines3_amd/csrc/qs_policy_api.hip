@@ -278,13 +278,30 @@ extern "C" int qs_linear_tanh_x3(const float* X, int64_t M, int32_t K, const voi
     const uint4* wp = reinterpret_cast<const uint4*>(w_packed);
     if (K == 256) {
         QS_HIP(hipFuncSetAttribute((const void*)P::linear_tanh_x3_kernel<1, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL((P::linear_tanh_x3_kernel<1, false, true>), grid, dim3(P::NTHR), lds, st, X, (long)M, wp, bias, Y, N,
+        hipLaunchKernelGGL((P::linear_tanh_x3_kernel<1, false, true>), grid, dim3(P::NTHR), lds, st, X, X + 256, (long)K, (long)M, wp, bias, Y, N,
                            nullptr);
     } else {
         QS_HIP(hipFuncSetAttribute((const void*)P::linear_tanh_x3_kernel<2, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL((P::linear_tanh_x3_kernel<2, false, true>), grid, dim3(P::NTHR), lds, st, X, (long)M, wp, bias, Y, N,
+        hipLaunchKernelGGL((P::linear_tanh_x3_kernel<2, false, true>), grid, dim3(P::NTHR), lds, st, X, X + 256, (long)K, (long)M, wp, bias, Y, N,
                            nullptr);
     }
+    QS_HIP(hipGetLastError());
+    return QS_OK;
+}
+extern "C" int qs_linear_tanh_cat_x3(const float* X0, const float* X1, int64_t M, const void* w_packed, int64_t w_bytes,
+                                     const float* bias, float* Y, int32_t N, void* stream) {
+    namespace P = qs::pol;
+    if (!X0 || !X1 || !w_packed || !bias || !Y) return fail(QS_E_INVALID, "NULL argument");
+    if (M < 1 || M >= (1ll << 31) / 512 || N < 256 || N > 1024 || N % 256)
+        return fail(QS_E_INVALID, "M >= 1, N a multiple of 256 up to 1024");
+    if (w_bytes != (int64_t)(N / 256) * 2 * 256 * 256 * 2 * 2)
+        return fail(QS_E_INVALID, "w_bytes: the packed weight must hold (N / 256) 2 packed 256 x 256 blocks");
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 grid((unsigned)((M + P::MROWS - 1) / P::MROWS), (unsigned)(N / 256));
+    const size_t lds = P::linear_x3_lds_bytes();
+    QS_HIP(hipFuncSetAttribute((const void*)P::linear_tanh_x3_kernel<2, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL((P::linear_tanh_x3_kernel<2, false, true>), grid, dim3(P::NTHR), lds, st, X0, X1, 256l, (long)M,
+                       reinterpret_cast<const uint4*>(w_packed), bias, Y, N, nullptr);
     QS_HIP(hipGetLastError());
     return QS_OK;
 }
@@ -302,11 +319,11 @@ extern "C" int qs_linear_rows_x3(const float* X, const float* row_scale, int64_t
     const uint4* wp = reinterpret_cast<const uint4*>(w_packed);
     if (K == 256) {
         QS_HIP(hipFuncSetAttribute((const void*)P::linear_tanh_x3_kernel<1, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL((P::linear_tanh_x3_kernel<1, true, true>), grid, dim3(P::NTHR), lds, st, X, (long)M, wp, nullptr, Y, N,
+        hipLaunchKernelGGL((P::linear_tanh_x3_kernel<1, true, true>), grid, dim3(P::NTHR), lds, st, X, X + 256, (long)K, (long)M, wp, nullptr, Y, N,
                            row_scale);
     } else {
         QS_HIP(hipFuncSetAttribute((const void*)P::linear_tanh_x3_kernel<2, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL((P::linear_tanh_x3_kernel<2, true, true>), grid, dim3(P::NTHR), lds, st, X, (long)M, wp, nullptr, Y, N,
+        hipLaunchKernelGGL((P::linear_tanh_x3_kernel<2, true, true>), grid, dim3(P::NTHR), lds, st, X, X + 256, (long)K, (long)M, wp, nullptr, Y, N,
                            row_scale);
     }
     QS_HIP(hipGetLastError());
@@ -340,11 +357,11 @@ extern "C" int qs_linear_bias_x3(const float* X, int64_t M, int32_t K, const voi
     const uint4* wp = reinterpret_cast<const uint4*>(w_packed);
     if (K == 256) {
         QS_HIP(hipFuncSetAttribute((const void*)P::linear_tanh_x3_kernel<1, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL((P::linear_tanh_x3_kernel<1, false, false>), grid, dim3(P::NTHR), lds, st, X, (long)M, wp, bias, Y,
+        hipLaunchKernelGGL((P::linear_tanh_x3_kernel<1, false, false>), grid, dim3(P::NTHR), lds, st, X, X + 256, (long)K, (long)M, wp, bias, Y,
                            N, nullptr);
     } else {
         QS_HIP(hipFuncSetAttribute((const void*)P::linear_tanh_x3_kernel<2, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL((P::linear_tanh_x3_kernel<2, false, false>), grid, dim3(P::NTHR), lds, st, X, (long)M, wp, bias, Y,
+        hipLaunchKernelGGL((P::linear_tanh_x3_kernel<2, false, false>), grid, dim3(P::NTHR), lds, st, X, X + 256, (long)K, (long)M, wp, bias, Y,
                            N, nullptr);
     }
     QS_HIP(hipGetLastError());

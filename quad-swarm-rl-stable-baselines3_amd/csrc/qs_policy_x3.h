@@ -454,11 +454,13 @@ namespace pol {
 // ROWS (the backward's dX = G W for gradient rows G of any magnitude): no bias and no activation, row r of X staged
 // at its power-of-two scale rs[r] (max |x_r| rs[r] in [2^13, 2^14): exact, it factors out of the row's products),
 // Y = acc / (rs[r] s_w).  ACT false (the attention score layer's mean half P = e_mean A_m^T + b_a1): bias, no tanh.
+// The input's column slice p is read from X (p = 0) or X1 (p = 1) with row stride ldx: one [M, 512] input is X, X + 256,
+// ldx 512; the feed_forward's [self | neighbour] encodings are two [M, 256] tensors (X, X1, ldx 256: no concatenation).
 template <int P, bool ROWS = false, bool ACT = true>
 __global__ __launch_bounds__(NTHR, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void linear_tanh_x3_kernel(
-    const float* __restrict__ X, long M, const uint4* __restrict__ Wp, const float* __restrict__ bias,
-    float* __restrict__ Y, int N, const float* __restrict__ rs = nullptr) {
-    constexpr int H = 256, LDH = GeoX3<H>::LDH, CT = Geo<H>::CT, KD = 256 * P, NV = MROWS * (H / 4) / NTHR;
+    const float* __restrict__ X, const float* __restrict__ X1, long ldx, long M, const uint4* __restrict__ Wp,
+    const float* __restrict__ bias, float* __restrict__ Y, int N, const float* __restrict__ rs = nullptr) {
+    constexpr int H = 256, LDH = GeoX3<H>::LDH, CT = Geo<H>::CT, NV = MROWS * (H / 4) / NTHR;
     constexpr size_t WBLK = (size_t)H * H * 2 * 2 / 16;   // uint4 per packed 256 x 256 block: hi + lo f16 halves
     extern __shared__ float4 smem4[];
     _Float16* xh = reinterpret_cast<_Float16*>(smem4);
@@ -484,7 +486,7 @@ __global__ __launch_bounds__(NTHR, 2) __attribute__((amdgpu_waves_per_eu(2, 2)))
 #pragma unroll
         for (int u = 0; u < NV; ++u) {
             const int e = tid + u * NTHR, r = e / (H / 4), c4 = e - r * (H / 4);
-            v[u] = *reinterpret_cast<const float4*>(X + (row0 + r < M ? row0 + r : 0) * KD + 256 * p + 4 * c4);
+            v[u] = *reinterpret_cast<const float4*>((p == 0 ? X : X1) + (row0 + r < M ? row0 + r : 0) * ldx + 4 * c4);
         }
     };
     auto put = [&]() {

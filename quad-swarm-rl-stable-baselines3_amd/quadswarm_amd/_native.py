@@ -184,7 +184,8 @@ EXPORTS = ["qs_abi_version", "qs_last_error", "qs_struct_sizes", "qs_config_defa
            "qs_curriculum_step", "qs_curriculum_step_all", "qs_attn_embed_train_x3", "qs_attn_pool_train_x3",
            "qs_attn_bwd1_x3", "qs_attn_bwd2_x3", "qs_attn_dw_x3", "qs_attn_dw0_x3", "qs_colmax_reduce", "qs_colstats",
            "qs_linear_tanh_x3", "qs_dw_x3_ld", "qs_linear_rows_x3",
-           "qs_tanh_grad_stats", "qs_linear_bias_x3", "qs_slab_sum_stats"]
+           "qs_tanh_grad_stats", "qs_linear_bias_x3", "qs_slab_sum_stats",
+           "qs_linear_tanh_cat_x3"]
 
 _lib = None
 
@@ -240,6 +241,7 @@ def lib():
         "qs_tanh_grad_stats": ([V, V, V, V, V, ctypes.c_int64, I32, V], I32),
         "qs_linear_bias_x3": ([V, ctypes.c_int64, I32, V, ctypes.c_int64, V, V, I32, V], I32),
         "qs_slab_sum_stats": ([V, I32, ctypes.c_int64, I32, V, V, V, V], I32),
+        "qs_linear_tanh_cat_x3": ([V, V, ctypes.c_int64, V, ctypes.c_int64, V, V, I32, V], I32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

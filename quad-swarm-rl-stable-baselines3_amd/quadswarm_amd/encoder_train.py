@@ -25,8 +25,9 @@ import ctypes
 import torch
 
 from . import _native as NAT
-from .policy_fused import (F16_MAX, X3_SIN, X3_SW, ff_supported, linear_bias_x3, linear_rows_x3,  # noqa: F401
-                           linear_tanh_x3, pack_mfma_weight_x3, pack_mfma_weights_x3, self_l2_supported, supports)
+from .policy_fused import (F16_MAX, X3_SIN, X3_SW, cat_free, ff_supported, linear_bias_x3,  # noqa: F401
+                           linear_rows_x3, linear_tanh_cat_x3, linear_tanh_x3, pack_mfma_weight_x3, pack_mfma_weights_x3,
+                           self_l2_supported, supports)
 
 _PARAMS = ("e1_w", "e1_b", "e2_w", "e2_b", "v1_w", "v1_b", "v2_w", "v2_b", "a1_w", "a1_b", "a2_w", "a2_b", "a3_w", "a3_b")
 
@@ -173,7 +174,7 @@ class _Runner:
         mu = (64 // self.K) * self.K                 # the kernels' row blocks (qs_policy.h MROWS = 64)
         nblk = (R + mu - 1) // mu
         self.buf = [dict(e1=z(R, H), e2=z(R, H), a1=z(R, H), a2=z(R, H), v1=z(R, H), h=z(R, H), w=z(R),
-                         e_mean=z(B, H), P=z(B, H), out=z(B, H), dh_pre=z(R, H), dv1_pre=z(R, H), da2_pre=z(R, H),
+                         e_mean=z(B, H), P=z(B, H), dh_pre=z(R, H), dv1_pre=z(R, H), da2_pre=z(R, H),
                          da1_pre=z(R, H), de2p=z(R, H), dscore=z(R), dem=z(B, H),
                          colmax=z(NAT.ATTN_NCOLMAX, nblk, H), a3w_part=z(nblk, H),
                          dP=z(B, H), dP_rs=z(B), dP_cm=z(1, (B + 63) // 64, H)) for _ in range(T)]
@@ -227,7 +228,7 @@ class _Runner:
             self.keep.append(k)
             t = self.towers[i]
             t.w_e1p, t.b_e1, t.w_e2p, t.b_e2 = p(k["w_e1p"]), p(k["b_e1"]), p(k["w_e2p"]), p(k["b_e2"])
-            t.e2, t.e_mean, t.P, t.out = p(b["e2"]), p(b["e_mean"]), p(b["P"]), p(b["out"])
+            t.e2, t.e_mean, t.P = p(b["e2"]), p(b["e_mean"]), p(b["P"])   # t.out: per forward
             t.w_v1p, t.b_v1, t.w_v2p, t.b_v2 = p(k["w_v1p"]), p(k["b_v1"]), p(k["w_v2p"]), p(k["b_v2"])
             t.w_a1ep, t.w_a2p, t.b_a2, t.w_a3 = p(k["w_a1ep"]), p(k["w_a2p"]), p(k["b_a2"]), p(k["w_a3"])
             t.b_a3 = float(w["a3_b"].detach().item())
@@ -259,9 +260,13 @@ class _Runner:
                 linear_bias_x3(self.buf[i]["e_mean"], self.am_packed[i][0], self.keep[i]["b_a1"], out=self.buf[i]["P"])
             else:   # A_m contiguous: the strided slice picks a 4x slower GEMM
                 torch.addmm(params[14 * i + 9], self.buf[i]["e_mean"], self.keep[i]["a_m"].t(), out=self.buf[i]["P"])
+        # the pooled outputs into fresh tensors (autograd owns them; no copy out of a reused buffer)
+        outs = [torch.empty(B, H, dtype=torch.float32, device=obs.device) for _ in range(self.T)]
+        for i in range(self.T):
+            self.towers[i].out = outs[i].data_ptr()
         NAT.check(self.L.qs_attn_pool_train_x3(B, K, H, self.towers, self.trains, self.T, st), "qs_attn_pool_train_x3")
         self.pending = True
-        return [self.buf[i]["out"].clone() for i in range(self.T)]
+        return outs
 
     @torch.no_grad()
     def backward(self, douts):
@@ -354,6 +359,20 @@ class _SelfLayer0Fn(torch.autograd.Function):
         return None, dW, sums, None
 
 
+def _tanh_grad_stats(g, y):
+    """gp = g (1 - y^2) with its row scales and its dW column scales (qs_tanh_grad_stats + qs_colmax_reduce)."""
+    M, N = y.shape
+    g = g.contiguous()
+    gp = torch.empty(M, N, dtype=torch.float32, device=g.device)
+    rs = torch.empty(M, dtype=torch.float32, device=g.device)
+    cpart = torch.empty(1, (M + 63) // 64, N, dtype=torch.float32, device=g.device)
+    st = ctypes.c_void_p(torch.cuda.current_stream(g.device).cuda_stream)
+    NAT.check(NAT.lib().qs_tanh_grad_stats(ctypes.c_void_p(g.data_ptr()), ctypes.c_void_p(y.data_ptr()),
+                                           ctypes.c_void_p(gp.data_ptr()), ctypes.c_void_p(rs.data_ptr()),
+                                           ctypes.c_void_p(cpart.data_ptr()), M, N, st), "qs_tanh_grad_stats")
+    return gp, rs, colmax_scales(cpart)[0]
+
+
 class _FeedForwardFn(torch.autograd.Function):
     """QuadMultiEncoder.feed_forward (Linear + Tanh; also the self encoder's second layer) on the split-f16 matrix
     cores: forward qs_linear_tanh_x3 (|x| <= 1: tanh outputs); backward gp = g (1 - y^2) with its row scales and
@@ -371,20 +390,9 @@ class _FeedForwardFn(torch.autograd.Function):
     def backward(ctx, g):
         x, weight, y = ctx.saved_tensors
         N, K = weight.shape
-        M = g.shape[0]
-        # gp = g (1 - y^2) with its row scales and per-block column maxima in one pass (qs_tanh_grad_stats)
-        g = g.contiguous()
-        gp = torch.empty(M, N, dtype=torch.float32, device=g.device)
-        rs = torch.empty(M, dtype=torch.float32, device=g.device)
-        nblk = (M + 63) // 64
-        cpart = torch.empty(1, nblk, N, dtype=torch.float32, device=g.device)
-        st = ctypes.c_void_p(torch.cuda.current_stream(g.device).cuda_stream)
-        NAT.check(NAT.lib().qs_tanh_grad_stats(ctypes.c_void_p(g.data_ptr()), ctypes.c_void_p(y.data_ptr()),
-                                               ctypes.c_void_p(gp.data_ptr()), ctypes.c_void_p(rs.data_ptr()),
-                                               ctypes.c_void_p(cpart.data_ptr()), M, N, st), "qs_tanh_grad_stats")
+        gp, rs, gs = _tanh_grad_stats(g, y)
         # the weight gradient gp^T x on the split-f16 matrix cores by 256 x 256 blocks (x: tanh range), the bias
         # gradient from the same passes
-        gs = colmax_scales(cpart)[0]
         dW = torch.empty(N, K, dtype=torch.float32, device=g.device)
         db = torch.empty(N, dtype=torch.float32, device=g.device)
         for zn in range(N // 256):
@@ -397,6 +405,39 @@ class _FeedForwardFn(torch.autograd.Function):
         # dX = gp W with each row at its power-of-two scale
         dx = linear_rows_x3(gp, rs, ctx.packed_t, K)
         return dx, dW, db, None, None
+
+
+class _FeedForwardCatFn(torch.autograd.Function):
+    """_FeedForwardFn on the concatenation [x0 | x1] of two [M, 256] encodings without forming it: the forward reads both
+    (qs_linear_tanh_cat_x3), the backward's dX halves are two N = 256 products on W^T's row blocks (each contiguous:
+    no split copies of a [M, 512] gradient) and dW's column blocks take x0 / x1 directly."""
+
+    @staticmethod
+    def forward(ctx, x0, x1, weight, bias, packed, packed_t):
+        y = linear_tanh_cat_x3(x0, x1, packed, bias.detach())
+        ctx.save_for_backward(x0, x1, weight, y)
+        ctx.packed_t = packed_t
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x0, x1, weight, y = ctx.saved_tensors
+        N = weight.shape[0]
+        gp, rs, gs = _tanh_grad_stats(g, y)
+        dW = torch.empty(N, 512, dtype=torch.float32, device=g.device)
+        db = torch.empty(N, dtype=torch.float32, device=g.device)
+        for zn in range(N // 256):
+            for zk, x in enumerate((x0, x1)):
+                r = dw_x3(gp[:, 256 * zn:256 * (zn + 1)], x, gs=gs[256 * zn:256 * (zn + 1)], sums=True)
+                dW[256 * zn:256 * (zn + 1), 256 * zk:256 * (zk + 1)] = r[0]
+                if zk == 0:
+                    db[256 * zn:256 * (zn + 1)] = r[1]
+        # dX = gp W: W^T's packed blocks are z-major over its 512 rows, (N / 256) blocks per 256 rows
+        nb = N // 256
+        pt = ctx.packed_t
+        dx0 = linear_rows_x3(gp, rs, pt[:nb], 256) if ctx.needs_input_grad[0] else None
+        dx1 = linear_rows_x3(gp, rs, pt[nb:2 * nb], 256) if ctx.needs_input_grad[1] else None
+        return dx0, dx1, dW, db, None, None
 
 
 class FusedAttentionTrain:
@@ -414,10 +455,14 @@ class FusedAttentionTrain:
         return [p for enc in self.runner.encs for p in tower_params(enc)]
 
     def feed_forward(self, lin, x):
-        """tanh(lin(x)) for a tower's feed_forward Linear or its self encoder's second Linear, x a tanh-range input
-        (QuadMultiEncoder.forward's ff hook): the x3 kernel when this minibatch's encodings packed it
-        (_FeedForwardFn), else torch."""
+        """tanh(lin(x)) for a tower's feed_forward Linear or its self encoder's second Linear, x a tanh-range input or
+        the list of the encoder's parts to concatenate (QuadMultiEncoder.forward's ff hook): the x3 kernel when this
+        minibatch's encodings packed it (_FeedForwardCatFn on two [B, 256] parts, else _FeedForwardFn), else torch."""
         packed = self.runner.lin_packed.get(id(lin))
+        if isinstance(x, (list, tuple)):   # the encoder's [self | neighbour (| obstacle)] parts
+            if packed is not None and lin.in_features == 512 and cat_free(x):
+                return _FeedForwardCatFn.apply(x[0], x[1], lin.weight, lin.bias, packed[0], packed[1])
+            x = torch.cat(x, dim=1) if len(x) > 1 else x[0]
         if packed is not None and x.is_contiguous():
             return _FeedForwardFn.apply(x, lin.weight, lin.bias, packed[0], packed[1])
         return torch.tanh(lin(x))

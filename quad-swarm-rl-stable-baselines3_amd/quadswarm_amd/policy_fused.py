@@ -120,6 +120,28 @@ def linear_tanh_x3(x, packed, bias, out=None):
     return y
 
 
+def linear_tanh_cat_x3(x0, x1, packed, bias, out=None):
+    """tanh([x0 | x1] W^T + b) for x0, x1 [M, 256] (|x| <= 1) without forming the concatenation (qs_linear_tanh_cat_x3);
+    packed = pack_linear_x3(W) for W [N, 512]."""
+    M = x0.shape[0]
+    N = bias.shape[0]
+    assert x0.shape == (M, 256) and x1.shape == (M, 256)
+    y = out if out is not None else torch.empty(M, N, dtype=torch.float32, device=x0.device)
+    assert x0.is_contiguous() and x1.is_contiguous() and packed.is_contiguous() and bias.is_contiguous() and y.is_contiguous()
+    st = ctypes.c_void_p(torch.cuda.current_stream(x0.device).cuda_stream)
+    NAT.check(NAT.lib().qs_linear_tanh_cat_x3(ctypes.c_void_p(x0.data_ptr()), ctypes.c_void_p(x1.data_ptr()), M,
+                                              ctypes.c_void_p(packed.data_ptr()), packed.numel() * packed.element_size(),
+                                              ctypes.c_void_p(bias.data_ptr()), ctypes.c_void_p(y.data_ptr()), N, st),
+              "qs_linear_tanh_cat_x3")
+    return y
+
+
+def cat_free(parts):
+    """Two contiguous [M, 256] parts: qs_linear_tanh_cat_x3 reads them in place of their concatenation."""
+    return (len(parts) == 2 and all(p.dim() == 2 and p.shape[1] == 256 and p.is_contiguous() for p in parts)
+            and parts[0].shape[0] == parts[1].shape[0])
+
+
 def linear_bias_x3(x, packed, bias, out=None):
     """x W^T + b for x [M, K] (|x| <= 1) on the split-f16 matrix cores (qs_linear_bias_x3: qs_linear_tanh_x3 without
     the tanh); the attention score layer's mean half P = e_mean A_m^T + b_a1."""
@@ -307,6 +329,8 @@ class FusedRolloutPolicy:
             parts = [se(obs[:, :so]), nbr_out]
         if enc.obstacle_encoder is not None:
             parts.append(enc.obstacle_encoder(obs[:, so + na:]))
+        if w is not None and "w_ffp" in w and cat_free(parts):   # x3, [self | neighbour] read in place
+            return linear_tanh_cat_x3(parts[0], parts[1], w["w_ffp"], w["b_ff"])
         x = torch.cat(parts, dim=1)
         if w is not None and "w_ffp" in w:   # x3: the feed_forward's Linear + Tanh as one kernel (|x| <= 1: tanh rows)
             return linear_tanh_x3(x, w["w_ffp"], w["b_ff"])

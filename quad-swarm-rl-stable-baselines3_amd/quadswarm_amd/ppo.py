@@ -196,7 +196,8 @@ class QuadMultiEncoder(nn.Module):
     def forward(self, obs, nbr_out=None, l0=None, ff=None):
         """nbr_out: the neighbour encoder's output computed elsewhere (the fused update, encoder_train.py); l0(lin,
         obs): the self encoder's first Linear evaluated elsewhere (FusedAttentionTrain.self_layer0); ff(lin, x): the
-        feed_forward's Linear + Tanh evaluated elsewhere (FusedAttentionTrain.feed_forward)."""
+        feed_forward's Linear + Tanh evaluated elsewhere (FusedAttentionTrain.feed_forward), x a tensor or, for the
+        feed_forward, the list of parts to concatenate."""
         so, na = self.cfg.self_obs_dim, self.all_neighbor_obs_size
         self_obs = obs[:, :so]
         se = self.self_encoder
@@ -215,9 +216,9 @@ class QuadMultiEncoder(nn.Module):
             parts.append(self.neighbor_encoder(self_obs, nbr))
         if self.obstacle_encoder is not None:
             parts.append(self.obstacle_encoder(obs[:, so + na:]))
-        x = torch.cat(parts, dim=1) if len(parts) > 1 else parts[0]
         if ff is not None and isinstance(self.feed_forward[0], nn.Linear):
-            return ff(self.feed_forward[0], x)
+            return ff(self.feed_forward[0], parts)   # the hook concatenates (or reads the parts in place)
+        x = torch.cat(parts, dim=1) if len(parts) > 1 else parts[0]
         return self.feed_forward(x)
 
 

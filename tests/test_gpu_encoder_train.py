@@ -304,6 +304,28 @@ def test_linear_tanh_x3_matches_fp64(M, K, N):
     assert e_x3 < 2e-6 and e_x3 < 8 * e_32 + 1e-6
 
 
+@pytest.mark.parametrize("M,N", [(4097, 512), (65, 256)])
+def test_linear_tanh_cat_x3_is_the_concatenated_layer(M, N):
+    """qs_linear_tanh_cat_x3 on two [M, 256] parts is bitwise qs_linear_tanh_x3 on their concatenation, and the
+    cat-free autograd node's gradients match the concatenated one's."""
+    from quadswarm_amd.encoder_train import _FeedForwardCatFn, _FeedForwardFn
+    from quadswarm_amd.policy_fused import linear_tanh_cat_x3, linear_tanh_x3, pack_linear_x3
+    g = torch.Generator(device="cuda").manual_seed(M + N)
+    x0 = torch.tanh(torch.randn(M, 256, device="cuda", generator=g) * 2)
+    x1 = torch.tanh(torch.randn(M, 256, device="cuda", generator=g) * 2)
+    w = torch.randn(N, 512, device="cuda", generator=g) / 512 ** 0.5
+    b = torch.randn(N, device="cuda", generator=g) * 0.1
+    pw, pwt = pack_linear_x3(w), pack_linear_x3(w.t())
+    assert torch.equal(linear_tanh_cat_x3(x0, x1, pw, b), linear_tanh_x3(torch.cat((x0, x1), 1), pw, b))
+    G = torch.randn(M, N, device="cuda", generator=g) * 1e-2
+    a0, a1, wa, ba = (t.clone().requires_grad_() for t in (x0, x1, w, b))
+    ga = torch.autograd.grad((_FeedForwardCatFn.apply(a0, a1, wa, ba, pw, pwt) * G).sum(), (a0, a1, wa, ba))
+    c0, c1, wc, bc = (t.clone().requires_grad_() for t in (x0, x1, w, b))
+    gc = torch.autograd.grad((_FeedForwardFn.apply(torch.cat((c0, c1), 1), wc, bc, pw, pwt) * G).sum(), (c0, c1, wc, bc))
+    for u, v in zip(ga, gc):
+        assert torch.equal(u, v)
+
+
 @pytest.mark.parametrize("M,K,N", [(4097, 256, 256), (1000, 512, 512)])
 def test_linear_bias_x3_matches_fp64(M, K, N):
     """qs_linear_bias_x3 (the score layer's mean half P = e_mean A_m^T + b_a1) against fp64 on tanh-range inputs,
