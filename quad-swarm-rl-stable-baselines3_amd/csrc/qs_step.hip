@@ -1203,6 +1203,10 @@ static int jit_compile(const qs_config* c, const qs::KP& kp, int npad, int qb, i
     opts.push_back("-mllvm");
     opts.push_back("-amdgpu-sched-strategy=max-ilp");
     opts.push_back("-fno-slp-vectorize");
+    // Flavor A: fp32 denormals flushed (no denormal scaling around the transcendentals of the controller and the
+    // camera model).  Bitwise identical digests on a8 and C3 / C2 (no denormal reaches a result), a8 21.31 -> 21.10
+    // us, C3 / C2 neutral (profiles/ab/r06_fp_opts_ab.txt): flavor A only.
+    if (c->flavor == QS_FLAVOR_A) opts.push_back("-fgpu-flush-denormals-to-zero");
     // (flavor A kept DPP permutes without bound_ctrl in round 3; on the round-4 kernel bound_ctrl is as good or
     // better there too, a8 23.54 -> 23.37, 23.48 -> 23.41 us, profiles/ab/r04_a8_dpp_bc_ab.txt: one form for both)
     // QS_JIT_OPTS: extra space-separated hipRTC options (kernel-variant experiments, e.g. -DQS_X=1).  The launch

@@ -44,8 +44,9 @@ def main():
     with tempfile.TemporaryDirectory() as d:
         f = os.path.join(d, "jit.hip")
         open(f, "w").write(src)
-        # the hipRTC options of qs_step.hip jit_compile (scheduler, no SLP packing)
-        jit = ["-mllvm", "-amdgpu-sched-strategy=max-ilp", "-fno-slp-vectorize"]
+        # the hipRTC options of qs_step.hip jit_compile (scheduler, no SLP packing, flavor A's denormal flush)
+        jit = ["-mllvm", "-amdgpu-sched-strategy=max-ilp", "-fno-slp-vectorize"] + \
+            (["-fgpu-flush-denormals-to-zero"] if flavor_a else [])
         subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=on",
                         "-munsafe-fp-atomics", "--cuda-device-only", "-S"] + jit + ["-I",
                         os.environ.get("QS_JIT_SRC_DIR", os.path.join(PKG, "csrc")), "-I",
