@@ -209,7 +209,7 @@ __device__ __forceinline__ float norm_rate(float p0, float p1, float v0, float v
     const float q0 = p0 + v0 * dt, q1 = p1 + v1 * dt;
     const float den = fsqrt(q0 * q0 + q1 * q1) + pn;
     const float num = 2.f * (p0 * v0 + p1 * v1) + dt * (v0 * v0 + v1 * v1);
-    return den > 0.f ? num / den : 0.f;
+    return den > 0.f ? num * frcp(den) : 0.f;   // a reciprocal product (~1 ulp), no IEEE division per neighbour
 }
 
 // simulate_camera_measurement_vect (get_state.py:128-176 == quadrotor_multi_rewards.py:275-324) for one
@@ -257,7 +257,8 @@ __device__ __forceinline__ void camera(const KP& kp, float rx, float ry, float g
     // 0 * rcp(0) = NaN)
     const float icn = frcp(cn);
     const float a = r2 * icn;
-    const float h = sqrtf(r2 - a * a);                   // NaN when the target is inside the marker
+    // v_sqrt_f32 (~1 ulp) instead of the correctly-rounded sqrtf expansion; NaN when the target is inside the marker
+    const float h = fsqrt(r2 - a * a);
     const float mf = 1.f - r2 * (icn * icn);
     const float mid0 = c0 * mf, mid1 = c1 * mf;
     const float pe0 = c1 * icn, pe1 = -c0 * icn;
